@@ -1,0 +1,78 @@
+// api.hip — C-ABI plumbing of libdppo_hip.so: errors, dimension checks, sizes, packing entry points.
+#include <stdarg.h>
+#include <stdio.h>
+#include "dppo_common.cuh"
+#include "dppo_internal.h"
+
+static thread_local char g_err[512] = "";
+
+int dppo_set_error(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int dppo_hip_fail(hipError_t e, const char* what) {
+    return dppo_set_error(DPPO_EHIP, "HIP error %d (%s) in %s", (int)e, hipGetErrorString(e), what);
+}
+
+int dppo_check_dims(const dppo_dims* d, Dims* o) {
+    DPPO_CHECK(d != nullptr, "dims is NULL");
+    o->Do = d->obs_dim; o->Da = d->action_dim; o->Ta = d->horizon_steps; o->To = d->cond_steps;
+    o->TD = d->time_dim; o->H = d->actor_hidden; o->HC = d->critic_hidden;
+    o->K = d->denoising_steps; o->KF = d->ft_denoising_steps;
+    DPPO_CHECK(o->Do > 0 && o->Da > 0 && o->Ta > 0 && o->To > 0, "obs/action/horizon/cond dims must be > 0");
+    DPPO_CHECK(o->TD >= 4 && o->TD % 2 == 0 && o->TD <= 64, "time_dim must be even, in [4, 64]");
+    DPPO_CHECK(o->H % 128 == 0 && o->H >= 128 && o->H <= 512, "actor_hidden must be 128/256/384/512");
+    DPPO_CHECK(o->HC % 128 == 0 && o->HC >= 128 && o->HC <= 512, "critic_hidden must be 128/256/384/512");
+    DPPO_CHECK(o->K >= 1 && o->K <= 1000, "denoising_steps out of range");
+    DPPO_CHECK(o->KF >= 1 && o->KF <= o->K, "ft_denoising_steps must be in [1, denoising_steps]");
+    o->XD = o->Ta * o->Da;
+    o->SD = o->To * o->Do;
+    o->IN = o->XD + o->TD + o->SD;
+    DPPO_CHECK(o->XD <= 32, "horizon_steps*action_dim must be <= 32");
+    DPPO_CHECK(o->SD <= 64, "cond_steps*obs_dim must be <= 64");
+    return DPPO_OK;
+}
+
+extern "C" int dppo_abi_version(void) { return DPPO_ABI_VERSION; }
+extern "C" const char* dppo_last_error(void) { return g_err; }
+
+extern "C" size_t dppo_actor_param_count(const dppo_dims* d) {
+    Dims D;
+    if (dppo_check_dims(d, &D)) return 0;
+    return make_flat_offsets(D.IN, D.H, D.XD, D.TD).count;
+}
+extern "C" size_t dppo_critic_param_count(const dppo_dims* d) {
+    Dims D;
+    if (dppo_check_dims(d, &D)) return 0;
+    return make_flat_offsets(D.SD, D.HC, 1, 0).count;
+}
+extern "C" size_t dppo_actor_packed_bytes(const dppo_dims* d, int precision) {
+    Dims D;
+    if (dppo_check_dims(d, &D)) return 0;
+    return make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision).total;
+}
+extern "C" size_t dppo_critic_packed_bytes(const dppo_dims* d, int precision) {
+    Dims D;
+    if (dppo_check_dims(d, &D)) return 0;
+    return make_mlp_layout(D.SD, D.HC, 1, 0, precision).total;
+}
+extern "C" int dppo_pack_actor(const dppo_dims* d, int precision, const float* params, void* packed, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(params && packed, "dppo_pack_actor: null pointer");
+    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    return dppo_pack_mlp(D.IN, D.H, D.XD, D.TD, precision, params, packed, (hipStream_t)stream);
+}
+extern "C" int dppo_pack_critic(const dppo_dims* d, int precision, const float* params, void* packed, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(params && packed, "dppo_pack_critic: null pointer");
+    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    return dppo_pack_mlp(D.SD, D.HC, 1, 0, precision, params, packed, (hipStream_t)stream);
+}

@@ -1,0 +1,230 @@
+// dppo_common.cuh — shared device code for the gfx950 DPPO kernels.
+//
+// Design: every MLP layer is an MFMA GEMM whose A operand (activations)
+// sits in LDS as a row-major tile and whose B operand (weights) is streamed from global memory
+// (L2/MALL resident) in a PRE-PACKED fragment order, so each wave-instruction of the weight
+// stream is one fully-coalesced 1 KiB `global_load_dwordx4`. Two precision policies share the
+// code: bf16 (v_mfma_f32_16x16x32_bf16) and fp32 (v_mfma_f32_16x16x4_f32, exact fp32 products,
+// used for parity). Both consume 16 bytes of A and 16 bytes of B per lane per "k-step".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "dppo_layout.h"
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+#define DPPO_WAVES 8
+#define DPPO_THREADS (DPPO_WAVES * 64)
+
+// ------------------------------------------------------------------------------------------------
+// precision policies
+// ------------------------------------------------------------------------------------------------
+struct PolicyBF16 {
+    using AT = __bf16;                 // activation element type in LDS
+    static constexpr int KG = 32;      // k covered by one 16-B fragment
+    static constexpr int EPL = 8;      // elements per lane per fragment
+    __device__ static inline AT cvt(float x) { return (__bf16)x; }
+    __device__ static inline float tof(AT x) { return (float)x; }
+    __device__ static inline f32x4 mma(u32x4 a, u32x4 b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                       __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+    }
+};
+
+struct PolicyF32 {
+    using AT = float;
+    static constexpr int KG = 16;
+    static constexpr int EPL = 4;
+    __device__ static inline AT cvt(float x) { return x; }
+    __device__ static inline float tof(AT x) { return x; }
+    // lane holds k = 4*(lane>>4) + q of the 16-k group for q = 0..3; MFMA q pairs A and B
+    // entries of the same k, so the four 16x16x4 products sum the whole group.
+    // NOTE: bit-cast the whole vector, then index. Per-component __builtin_bit_cast(float, a.y)
+    // is miscompiled by hipcc (ROCm 7.2): all four MFMAs received component x.
+    __device__ static inline f32x4 mma(u32x4 a, u32x4 b, f32x4 c) {
+        const f32x4 af = __builtin_bit_cast(f32x4, a);
+        const f32x4 bf = __builtin_bit_cast(f32x4, b);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(af[0], bf[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(af[1], bf[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(af[2], bf[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(af[3], bf[3], c, 0, 0, 0);
+        return c;
+    }
+};
+
+template <class P> __device__ __host__ constexpr int lds_pad_elems() { return 32 / (int)sizeof(typename P::AT); }
+
+// ------------------------------------------------------------------------------------------------
+// fragment access
+// ------------------------------------------------------------------------------------------------
+// A fragment: row (lane & 15) of row-tile mt, k-step ks; 16 contiguous bytes in LDS.
+template <class P>
+__device__ inline u32x4 lds_afrag(const typename P::AT* A, int lda, int mt, int ks, int lane) {
+    const typename P::AT* p = A + (mt * 16 + (lane & 15)) * lda + ks * P::KG + (lane >> 4) * P::EPL;
+    return *reinterpret_cast<const u32x4*>(p);
+}
+
+// B fragment from a packed matrix: [ntile][ks][lane] x 16 B.
+__device__ inline u32x4 load_bfrag(const u32x4* __restrict__ W, int KS, int ntile, int ks, int lane) {
+    return __builtin_nontemporal_load(&W[((size_t)ntile * KS + ks) * 64 + lane]) ;
+}
+__device__ inline u32x4 load_bfrag_c(const u32x4* __restrict__ W, int KS, int ntile, int ks, int lane) {
+    return W[((size_t)ntile * KS + ks) * 64 + lane];
+}
+
+__device__ inline void zero_acc(f32x4& a) { a = f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// Wide layer: this wave computes n-tiles [ntile0, ntile0+NT) for all MT row tiles over KS k-steps.
+// Weight fragments are prefetched DEPTH k-steps ahead in a compile-time-indexed register ring.
+template <class P, int MT, int NT, int DEPTH>
+__device__ inline void gemm_wide(const typename P::AT* A, int lda, int KS, const u32x4* __restrict__ W,
+                                 int ntile0, f32x4 (&acc)[MT][NT], int lane) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) zero_acc(acc[m][n]);
+    u32x4 ring[DEPTH][NT];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+        const int ks = d < KS ? d : KS - 1;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) ring[d][n] = load_bfrag_c(W, KS, ntile0 + n, ks, lane);
+    }
+    for (int ks0 = 0; ks0 < KS; ks0 += DEPTH) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const int ks = ks0 + d;
+            if (ks < KS) {
+                u32x4 b[NT];
+#pragma unroll
+                for (int n = 0; n < NT; ++n) b[n] = ring[d][n];
+                const int kn = (ks + DEPTH < KS) ? ks + DEPTH : KS - 1;
+#pragma unroll
+                for (int n = 0; n < NT; ++n) ring[d][n] = load_bfrag_c(W, KS, ntile0 + n, kn, lane);
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    const u32x4 a = lds_afrag<P>(A, lda, m, ks, lane);
+#pragma unroll
+                    for (int n = 0; n < NT; ++n) acc[m][n] = P::mma(a, b[n], acc[m][n]);
+                }
+            }
+        }
+    }
+}
+
+// Narrow layer (n-tiles < waves): k-steps are dealt round-robin to the 8 waves; each wave
+// returns a partial sum that the caller reduces through LDS.
+template <class P, int MT, int NTN>
+__device__ inline void gemm_narrow(const typename P::AT* A, int lda, int KS, const u32x4* __restrict__ W,
+                                   f32x4 (&acc)[MT][NTN], int wave, int lane) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NTN; ++n) zero_acc(acc[m][n]);
+    for (int ks = wave; ks < KS; ks += DPPO_WAVES) {
+        u32x4 b[NTN];
+#pragma unroll
+        for (int n = 0; n < NTN; ++n) b[n] = load_bfrag_c(W, KS, n, ks, lane);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            const u32x4 a = lds_afrag<P>(A, lda, m, ks, lane);
+#pragma unroll
+            for (int n = 0; n < NTN; ++n) acc[m][n] = P::mma(a, b[n], acc[m][n]);
+        }
+    }
+}
+
+// C/D fragment coordinates (dtype independent on gfx950): col = lane&15, row = 4*(lane>>4) + r
+__device__ inline int crow(int lane, int r) { return ((lane >> 4) << 2) + r; }
+__device__ inline int ccol(int lane) { return lane & 15; }
+
+// ------------------------------------------------------------------------------------------------
+// activations (Keras: relu, mish = x * tanh(softplus(x)))
+// ------------------------------------------------------------------------------------------------
+__device__ inline float softplusf(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+__device__ inline float mishf(float x) { return x * tanhf(softplusf(x)); }
+__device__ inline float mish_gradf(float x) {
+    const float sp = softplusf(x);
+    const float th = tanhf(sp);
+    const float sig = 1.f / (1.f + expf(-x));
+    return th + x * (1.f - th * th) * sig;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Philox4x32-10 + Box-Muller (restated bit-for-bit by oracle/philox.py)
+// ------------------------------------------------------------------------------------------------
+struct u32x4s { uint32_t x, y, z, w; };
+__device__ __host__ inline u32x4s philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                               uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return u32x4s{c0, c1, c2, c3};
+}
+__device__ inline float u32_unit(uint32_t w) { return ((float)(w >> 9) + 0.5f) * (1.0f / 8388608.0f); }
+
+// normal #q (0..3) of the Philox block (group, row, slot, call)
+__device__ inline float philox_normal(uint64_t seed, uint32_t group, uint32_t row, uint32_t slot,
+                                      uint32_t call, int q) {
+    const u32x4s w = philox4x32_10(group, row, slot, call, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float ua = u32_unit(q < 2 ? w.x : w.z);
+    const float ub = u32_unit(q < 2 ? w.y : w.w);
+    const float r = sqrtf(-2.0f * logf(ua));
+    const float ang = 6.283185307179586f * ub;
+    return (q & 1) ? r * sinf(ang) : r * cosf(ang);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Feistel minibatch permutation (restated by oracle/philox.py:feistel_permute)
+// ------------------------------------------------------------------------------------------------
+struct FeistelKey { uint32_t k[4]; int half_bits; uint64_t n; };
+__host__ __device__ inline FeistelKey feistel_key(uint64_t n, uint64_t seed, int epoch) {
+    FeistelKey f;
+    int hb = 1;
+    while ((1ull << (2 * hb)) < n) ++hb;
+    f.half_bits = hb;
+    f.n = n;
+    const u32x4s w = philox4x32_10((uint32_t)epoch, 0x5EEDu, 0u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
+    f.k[0] = w.x; f.k[1] = w.y; f.k[2] = w.z; f.k[3] = w.w;
+    return f;
+}
+__host__ __device__ inline uint64_t feistel_once(uint64_t x, const FeistelKey& f) {
+    const uint64_t mask = (1ull << f.half_bits) - 1;
+    uint64_t l = (x >> f.half_bits) & mask, r = x & mask;
+    for (int i = 0; i < 4; ++i) {
+        uint32_t h = (uint32_t)(r ^ f.k[i]);
+        h *= 0x9E3779B1u; h ^= h >> 15; h *= 0x85EBCA77u; h ^= h >> 13;
+        const uint64_t nr = (l ^ h) & mask;
+        l = r; r = nr;
+    }
+    return (l << f.half_bits) | r;
+}
+// cycle walking; bounded (P(>1024 walks) < 1e-128); returns n on give-up (caller treats as invalid)
+__host__ __device__ inline uint64_t feistel_permute(uint64_t i, const FeistelKey& f) {
+    uint64_t x = feistel_once(i, f);
+    for (int it = 0; it < 1024 && x >= f.n; ++it) x = feistel_once(x, f);
+    return x < f.n ? x : f.n;
+}
+
+// ------------------------------------------------------------------------------------------------
+// wave reductions
+// ------------------------------------------------------------------------------------------------
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ inline double wave_sumd(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}

@@ -1,0 +1,98 @@
+// dppo_layout.h — host+device description of the packed (MFMA fragment-ordered) weight images.
+//
+// A residual MLP (model/common/mlp.py:95-206: in-Dense, one pre-activation two-Dense block,
+// out-Dense) is stored as segments, each 256-B aligned:
+//   TIME   fp32 time MLP (actor only): w1[TD,2TD] b1[2TD] w2[2TD,TD] b2[TD]
+//   W_IN   packed fwd  [K=in_dim][N=H]      B_IN  fp32 [H]
+//   W_L1   packed fwd  [H][H]               B_L1  fp32 [H]
+//   W_L2   packed fwd  [H][H]               B_L2  fp32 [H]
+//   W_OUT  packed fwd  [H][out]             B_OUT fp32 [16*ceil(out/16)] (zero padded)
+//   T_OUT  packed bwd  W_out^T as [K=out][N=H]
+//   T_L2   packed bwd  W_l2^T  as [K=H][N=H]
+//   T_L1   packed bwd  W_l1^T  as [K=H][N=H]
+// A packed matrix [K][N] is ceil(N/16) n-tiles x KS k-steps x 64 lanes x 16 B, with
+// KS = ceil(K / KG), KG = 32 (bf16) or 16 (fp32). Lane l of (ntile, ks) holds, for e < EPL,
+//   W[ks*KG + (l>>4)*EPL + e][ntile*16 + (l&15)]   (zero outside [K][N]).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define DPPO_HD __host__ __device__
+#else
+#define DPPO_HD
+#endif
+
+enum MlpSeg { SEG_TIME = 0, SEG_W_IN, SEG_B_IN, SEG_W_L1, SEG_B_L1, SEG_W_L2, SEG_B_L2, SEG_W_OUT, SEG_B_OUT,
+              SEG_T_OUT, SEG_T_L2, SEG_T_L1, SEG_COUNT };
+
+struct MlpLayout {
+    int in_dim, hidden, out_dim, time_dim, precision;
+    int KG;                 // 32 bf16 / 16 fp32
+    int ks_in, ks_h, ks_out_t;   // k-steps: in layer, hidden layers, transposed out (K = out_dim)
+    int nt_h, nt_out;       // n-tiles: hidden, out
+    size_t off[SEG_COUNT];
+    size_t total;
+};
+
+DPPO_HD inline size_t dppo_align256(size_t x) { return (x + 255) & ~(size_t)255; }
+DPPO_HD inline size_t dppo_align16(size_t x) { return (x + 15) & ~(size_t)15; }
+DPPO_HD inline int dppo_cdiv(int a, int b) { return (a + b - 1) / b; }
+DPPO_HD inline size_t packed_matrix_bytes(int K, int N, int KG) {
+    return (size_t)dppo_cdiv(N, 16) * (size_t)dppo_cdiv(K, KG) * 64 * 16;
+}
+
+DPPO_HD inline MlpLayout make_mlp_layout(int in_dim, int hidden, int out_dim, int time_dim, int precision) {
+    MlpLayout L;
+    L.in_dim = in_dim; L.hidden = hidden; L.out_dim = out_dim; L.time_dim = time_dim; L.precision = precision;
+    L.KG = precision == 1 ? 32 : 16;
+    L.ks_in = dppo_cdiv(in_dim, L.KG);
+    L.ks_h = dppo_cdiv(hidden, L.KG);
+    L.ks_out_t = dppo_cdiv(out_dim, L.KG);
+    L.nt_h = dppo_cdiv(hidden, 16);
+    L.nt_out = dppo_cdiv(out_dim, 16);
+    size_t o = 0;
+    const size_t tsz = time_dim > 0 ? (size_t)4 * (time_dim * 2 * time_dim + 2 * time_dim + 2 * time_dim * time_dim + time_dim) : 0;
+    L.off[SEG_TIME] = o; o = dppo_align256(o + tsz);
+    L.off[SEG_W_IN] = o; o = dppo_align256(o + packed_matrix_bytes(in_dim, hidden, L.KG));
+    L.off[SEG_B_IN] = o; o = dppo_align256(o + (size_t)4 * hidden);
+    L.off[SEG_W_L1] = o; o = dppo_align256(o + packed_matrix_bytes(hidden, hidden, L.KG));
+    L.off[SEG_B_L1] = o; o = dppo_align256(o + (size_t)4 * hidden);
+    L.off[SEG_W_L2] = o; o = dppo_align256(o + packed_matrix_bytes(hidden, hidden, L.KG));
+    L.off[SEG_B_L2] = o; o = dppo_align256(o + (size_t)4 * hidden);
+    L.off[SEG_W_OUT] = o; o = dppo_align256(o + packed_matrix_bytes(hidden, out_dim, L.KG));
+    L.off[SEG_B_OUT] = o; o = dppo_align256(o + (size_t)4 * 16 * L.nt_out);
+    L.off[SEG_T_OUT] = o; o = dppo_align256(o + packed_matrix_bytes(out_dim, hidden, L.KG));
+    L.off[SEG_T_L2] = o; o = dppo_align256(o + packed_matrix_bytes(hidden, hidden, L.KG));
+    L.off[SEG_T_L1] = o; o = dppo_align256(o + packed_matrix_bytes(hidden, hidden, L.KG));
+    L.total = o;
+    return L;
+}
+
+// flat fp32 parameter offsets (include/dppo.h layout)
+struct FlatOffsets {
+    size_t time_w1, time_b1, time_w2, time_b2, in_w, in_b, l1_w, l1_b, l2_w, l2_b, out_w, out_b, count;
+};
+DPPO_HD inline FlatOffsets make_flat_offsets(int in_dim, int hidden, int out_dim, int time_dim) {
+    FlatOffsets f;
+    size_t o = 0;
+    f.time_w1 = o; o += (size_t)time_dim * 2 * time_dim;
+    f.time_b1 = o; o += (size_t)2 * time_dim;
+    f.time_w2 = o; o += (size_t)2 * time_dim * time_dim;
+    f.time_b2 = o; o += (size_t)time_dim;
+    f.in_w = o; o += (size_t)in_dim * hidden;
+    f.in_b = o; o += hidden;
+    f.l1_w = o; o += (size_t)hidden * hidden;
+    f.l1_b = o; o += hidden;
+    f.l2_w = o; o += (size_t)hidden * hidden;
+    f.l2_b = o; o += hidden;
+    f.out_w = o; o += (size_t)hidden * out_dim;
+    f.out_b = o; o += out_dim;
+    f.count = o;
+    return f;
+}
+
+// actor: in = XD + TD + SD, out = XD, time_dim = TD; critic: in = SD, out = 1, time_dim = 0
+struct ModelDims {
+    int XD, SD, TD, H, HC, K, KF, Ta, Da;
+};

@@ -1,0 +1,88 @@
+// dppo_ppo.h — argument blocks and workspace layout of the PPO-update kernels.
+#pragma once
+#include "dppo_common.cuh"
+#include "dppo_internal.h"
+
+// feature-major ("transposed") activation / gradient images written by the row-tile kernels and
+// consumed by the split-K weight-gradient kernel: X^T[f][ldm], ldm = rows rounded up to 64.
+struct PpoWorkspace {
+    size_t ldm;
+    // actor
+    void *a0T, *u1T, *u2T, *h3T, *dyT, *dh3T, *dh2T, *dh1T;
+    // critic
+    void *csT, *cu1T, *cu2T, *ch3T, *cdvT, *cdh3T, *cdh2T, *cdh1T;
+    int8_t* seg;      // [ldm] t of each row (bucket id for the one-hot bias/temb sums), -1 invalid
+    float* gseg;      // [16][H] per-t sums of dh1 (actor in-layer)
+    double* stats;    // [4] adv {count, sum, sumsq}
+    size_t total;
+};
+
+inline PpoWorkspace make_ppo_workspace(const Dims& D, int precision, int rows, uint8_t* base) {
+    PpoWorkspace w;
+    const size_t es = precision == DPPO_BF16 ? 2 : 4;
+    w.ldm = (size_t)dppo_cdiv(rows > 0 ? rows : 1, 64) * 64;
+    size_t o = 0;
+    auto take = [&](size_t feats) -> void* {
+        void* p = base ? (void*)(base + o) : nullptr;
+        o = dppo_align256(o + feats * w.ldm * es);
+        return p;
+    };
+    w.a0T = take(D.IN); w.u1T = take(D.H); w.u2T = take(D.H); w.h3T = take(D.H);
+    w.dyT = take(D.XD); w.dh3T = take(D.H); w.dh2T = take(D.H); w.dh1T = take(D.H);
+    w.csT = take(D.SD); w.cu1T = take(D.HC); w.cu2T = take(D.HC); w.ch3T = take(D.HC);
+    w.cdvT = take(1); w.cdh3T = take(D.HC); w.cdh2T = take(D.HC); w.cdh1T = take(D.HC);
+    w.seg = base ? (int8_t*)(base + o) : nullptr; o = dppo_align256(o + w.ldm);
+    w.gseg = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * 16 * (size_t)D.H);
+    w.stats = base ? (double*)(base + o) : nullptr; o = dppo_align256(o + 8 * 4);
+    w.total = o;
+    return w;
+}
+
+// per-row source of a row-tile launch
+enum { ROWS_LOGPROB = 0, ROWS_TRAIN = 1, ROWS_VALUE = 2 };
+
+struct LossHP {
+    float gamma_denoising, clip_coef, clip_coef_base, clip_coef_rate, min_lp_std, vf_coef;
+    int norm_adv, reward_horizon;
+    float grad_scale;     // loss_scale / global_rows
+};
+
+struct ActorArgs {
+    const uint8_t* packed;
+    MlpLayout L;
+    const float* sched;
+    const float* obs;      // [nsamp][SD]
+    const float* chains;   // [nsamp][KF+1][XD]
+    int XD, SD, TD, IN, H, KF, Da, mode;
+    int64_t nrows;         // logprob: nsamp*KF; train: rows
+    // logprob outputs
+    float* lp_elem;
+    float* lp_mean;
+    // train
+    FeistelKey fk;
+    int64_t start;
+    const float* lp_old;   // [nsamp][KF]
+    const float* adv;      // [nsamp]
+    const double* adv_stats;
+    LossHP hp;
+    PpoWorkspace ws;
+    double* metrics;
+};
+
+struct CriticArgs {
+    const uint8_t* packed;
+    MlpLayout L;
+    const float* obs;
+    int SD, HC, KF, mode;
+    int64_t nrows;
+    float* values;        // value mode
+    FeistelKey fk;
+    int64_t start;
+    const float* returns;
+    LossHP hp;
+    PpoWorkspace ws;
+    double* metrics;
+};
+
+int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s);
+int launch_critic_rowtile(const CriticArgs& a, int precision, hipStream_t s);

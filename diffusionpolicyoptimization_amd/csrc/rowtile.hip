@@ -1,0 +1,658 @@
+// rowtile.hip — row-tile fused MLP kernels for the update half of the hot path.
+//
+// One workgroup (8 waves) owns 16*MT rows and runs a whole residual MLP on them with the
+// activations in LDS and the weights streamed in fragment order (dppo_common.cuh):
+//   actor, mode LOGPROB : DiffusionMLP forward + p_mean_var + Normal.log_prob epilogue
+//                         (VPGDiffusion.get_logprobs, model/diffusion/diffusion_vpg.py:343-425)
+//   actor, mode TRAIN   : rows gathered through the minibatch permutation
+//                         (train_ppo_diffusion_agent.py:287-312) -> forward -> fused c_loss policy
+//                         term and its gradient (diffusion_ppo.py:45-106) -> backward dX chain,
+//                         writing feature-major activation/gradient images for the dW kernel
+//   critic, mode VALUE  : CriticObs forward (model/common/critic.py:40-54)
+//   critic, mode TRAIN  : forward -> v_loss gradient (diffusion_ppo.py:108-118) -> backward chain
+#include "dppo_ppo.h"
+
+#define LOG_2PI_HALF 0.91893853320467274178f
+
+// 4 consecutive rows of one column into a feature-major image XT[col][row..row+3]
+template <class P>
+__device__ inline void store4T(void* XTv, size_t ldm, int col, size_t row, float v0, float v1, float v2, float v3) {
+    using AT = typename P::AT;
+    AT* XT = (AT*)XTv + (size_t)col * ldm + row;
+    if constexpr (sizeof(AT) == 2) {
+        __bf16 e[4] = {(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)v3};
+        *reinterpret_cast<uint2*>(XT) = __builtin_bit_cast(uint2, e);
+    } else {
+        *reinterpret_cast<float4*>(XT) = make_float4(v0, v1, v2, v3);
+    }
+}
+
+template <class P, int MT, int NT>
+__device__ inline void store_accT(void* XT, size_t ldm, int ntile0, size_t grow0, int lane, const f32x4 (&v)[MT][NT]) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+            store4T<P>(XT, ldm, (ntile0 + n) * 16 + ccol(lane), grow0 + m * 16 + ((lane >> 4) << 2),
+                       v[m][n][0], v[m][n][1], v[m][n][2], v[m][n][3]);
+}
+
+template <class P, int MT, int NT>
+__device__ inline void store_acc_lds(typename P::AT* T, int ld, int ntile0, int lane, const f32x4 (&v)[MT][NT]) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int col = (ntile0 + n) * 16 + ccol(lane);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) T[(m * 16 + crow(lane, r)) * ld + col] = P::cvt(v[m][n][r]);
+        }
+}
+
+template <int MT, int NT>
+__device__ inline void add_bias(f32x4 (&v)[MT][NT], const float* __restrict__ b, int ntile0, int lane) {
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const float bv = b[(ntile0 + n) * 16 + ccol(lane)];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[m][n][r] += bv;
+    }
+}
+
+__device__ inline void atomic_add_metric(double* m, int i, double v) { atomicAdd(m + i, v); }
+
+// =============================================================================================
+// actor
+// =============================================================================================
+template <class P, int MT>
+struct ActorSmem {
+    static constexpr int ROWS = 16 * MT;
+    size_t tA, tB, a0, xp, xn, st, temb, ta1, sch, rn, rj, total;
+    __host__ __device__ ActorSmem(const ActorArgs& a) {
+        using AT = typename P::AT;
+        const int pad = lds_pad_elems<P>();
+        const int ldh = a.H + pad, lda0 = a.L.ks_in * P::KG + pad;
+        size_t o = 0;
+        tA = o; o += dppo_align16(sizeof(AT) * ROWS * ldh);
+        tB = o; o += dppo_align16(sizeof(AT) * ROWS * ldh);
+        a0 = o; o += dppo_align16(sizeof(AT) * ROWS * lda0);
+        xp = o; o += dppo_align16(4 * ROWS * a.XD);
+        xn = o; o += dppo_align16(4 * ROWS * a.XD);
+        st = o; o += dppo_align16(4 * ROWS * a.SD);
+        temb = o; o += dppo_align16(4 * a.KF * a.TD);
+        ta1 = o; o += dppo_align16(4 * a.KF * 2 * a.TD);
+        sch = o; o += dppo_align16(4 * a.KF * DPPO_SCHED_COLS);
+        rn = o; o += dppo_align16(4 * ROWS);
+        rj = o; o += dppo_align16(4 * ROWS);
+        total = o;
+    }
+};
+
+template <class P, int MT, int NT, int NO>
+__global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a) {
+    using AT = typename P::AT;
+    constexpr int ROWS = 16 * MT;
+    constexpr int DEP = MT >= 2 ? 2 : 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const MlpLayout& L = a.L;
+    const ActorSmem<P, MT> S(a);
+    const int pad = lds_pad_elems<P>();
+    const int ldh = a.H + pad;
+    const int k1w = L.ks_in * P::KG, lda0 = k1w + pad;
+    const int ktw = L.ks_out_t * P::KG;   // width of the dy tile (A operand of dh3 = dy W_out^T)
+    const int XD = a.XD, SD = a.SD, TD = a.TD, KF = a.KF, IN = a.IN;
+    const bool train = a.mode == ROWS_TRAIN;
+    AT* tA = (AT*)(smem + S.tA);
+    AT* tB = (AT*)(smem + S.tB);
+    AT* a0 = (AT*)(smem + S.a0);
+    float* xp = (float*)(smem + S.xp);
+    float* xn = (float*)(smem + S.xn);
+    float* st = (float*)(smem + S.st);
+    float* temb = (float*)(smem + S.temb);
+    float* ta1 = (float*)(smem + S.ta1);
+    float* sch = (float*)(smem + S.sch);
+    int* rn = (int*)(smem + S.rn);
+    int* rj = (int*)(smem + S.rj);
+    float* part = (float*)(smem + S.tB);   // out-layer partials alias tB (u2 is dead by then)
+    const size_t grow0 = (size_t)blockIdx.x * ROWS;
+
+    // ---- prologue: rows, schedule, time embedding for t < K' (actor_ft) ----
+    if (tid < ROWS) {
+        const int64_t gr = (int64_t)grow0 + tid;
+        int n = -1, j = 0;
+        if (gr < a.nrows) {
+            if (train) {
+                const uint64_t idx = feistel_permute((uint64_t)(a.start + gr), a.fk);
+                if (idx < a.fk.n) { n = (int)(idx / KF); j = (int)(idx % KF); }   // tf.unravel_index
+            } else {
+                n = (int)(gr / KF); j = (int)(gr % KF);
+            }
+        }
+        rn[tid] = n; rj[tid] = j;
+    }
+    for (int i = tid; i < KF * DPPO_SCHED_COLS; i += DPPO_THREADS) sch[i] = a.sched[i];
+    const int half = TD / 2;
+    const float lnf = logf(10000.f) / (float)(half - 1);
+    const float* tw = (const float*)(a.packed + L.off[SEG_TIME]);
+    for (int i = tid; i < KF * 2 * TD; i += DPPO_THREADS) {
+        const int t = i / (2 * TD), jj = i % (2 * TD);
+        float acc = tw[TD * 2 * TD + jj];
+        for (int k = 0; k < TD; ++k) {
+            const float f = expf(-(float)(k % half) * lnf) * (float)t;
+            acc += (k < half ? sinf(f) : cosf(f)) * tw[k * 2 * TD + jj];
+        }
+        ta1[i] = mishf(acc);
+    }
+    __syncthreads();
+    for (int i = tid; i < KF * TD; i += DPPO_THREADS) {
+        const int t = i / TD, jj = i % TD;
+        const float* w2 = tw + TD * 2 * TD + 2 * TD;
+        float acc = w2[2 * TD * TD + jj];
+        for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + jj];
+        temb[i] = acc;
+    }
+    for (int i = tid; i < ROWS * XD; i += DPPO_THREADS) {
+        const int r = i / XD, q = i % XD, n = rn[r];
+        float vp = 0.f, vn = 0.f;
+        if (n >= 0) {
+            const float* c = a.chains + ((size_t)n * (KF + 1) + rj[r]) * XD + q;
+            vp = c[0]; vn = c[XD];   // chains_prev = chains[:, j], chains_next = chains[:, j+1]
+        }
+        xp[i] = vp; xn[i] = vn;
+    }
+    for (int i = tid; i < ROWS * SD; i += DPPO_THREADS) {
+        const int r = i / SD, c = i % SD, n = rn[r];
+        st[i] = n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f;
+    }
+    __syncthreads();
+    // a0 = [x_prev, temb(t), state] (mlp_diffusion.py:86), t = K'-1-j (diffusion_vpg.py:456-458)
+    for (int i = tid; i < ROWS * k1w; i += DPPO_THREADS) {
+        const int r = i / k1w, c = i % k1w;
+        const int t = KF - 1 - rj[r];
+        float v = 0.f;
+        if (c < XD) v = xp[r * XD + c];
+        else if (c < XD + TD) v = temb[t * TD + c - XD];
+        else if (c < IN) v = st[r * SD + c - XD - TD];
+        a0[r * lda0 + c] = P::cvt(v);
+    }
+    if (train) {
+        AT* a0T = (AT*)a.ws.a0T;
+        for (int i = tid; i < ROWS * IN; i += DPPO_THREADS) {
+            const int c = i / ROWS, r = i % ROWS;
+            const int t = KF - 1 - rj[r];
+            float v;
+            if (c < XD) v = xp[r * XD + c];
+            else if (c < XD + TD) v = temb[t * TD + c - XD];
+            else v = st[r * SD + c - XD - TD];
+            a0T[(size_t)c * a.ws.ldm + grow0 + r] = P::cvt(v);
+        }
+        if (tid < ROWS) a.ws.seg[grow0 + tid] = rn[tid] >= 0 ? (int8_t)(KF - 1 - rj[tid]) : (int8_t)-1;
+    }
+    __syncthreads();
+
+    const int ntile0 = wave * NT;
+    f32x4 H1[MT][NT], acc[MT][NT];
+    uint64_t mask1 = 0, mask2 = 0;
+    // ---- L1: h1 = a0 W_in + b (no activation on the input layer) ----
+    gemm_wide<P, MT, NT, DEP>(a0, lda0, L.ks_in, (const u32x4*)(a.packed + L.off[SEG_W_IN]), ntile0, H1, lane);
+    add_bias(H1, (const float*)(a.packed + L.off[SEG_B_IN]), ntile0, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                acc[m][n][r] = fmaxf(H1[m][n][r], 0.f);
+                if (H1[m][n][r] > 0.f) mask1 |= 1ull << ((m * NT + n) * 4 + r);
+            }
+    store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
+    if (train) store_accT<P, MT, NT>(a.ws.u1T, a.ws.ldm, ntile0, grow0, lane, acc);
+    __syncthreads();
+    // ---- L2: h2 = relu(h1) W_l1 + b ----
+    gemm_wide<P, MT, NT, DEP>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_L1]), ntile0, acc, lane);
+    add_bias(acc, (const float*)(a.packed + L.off[SEG_B_L1]), ntile0, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (acc[m][n][r] > 0.f) mask2 |= 1ull << ((m * NT + n) * 4 + r);
+                acc[m][n][r] = fmaxf(acc[m][n][r], 0.f);
+            }
+    store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
+    if (train) store_accT<P, MT, NT>(a.ws.u2T, a.ws.ldm, ntile0, grow0, lane, acc);
+    __syncthreads();
+    // ---- L3: h3 = relu(h2) W_l2 + b + h1 ----
+    gemm_wide<P, MT, NT, DEP>(tB, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_L2]), ntile0, acc, lane);
+    add_bias(acc, (const float*)(a.packed + L.off[SEG_B_L2]), ntile0, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[m][n][r] += H1[m][n][r];
+    store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
+    if (train) store_accT<P, MT, NT>(a.ws.h3T, a.ws.ldm, ntile0, grow0, lane, acc);
+    __syncthreads();
+    // ---- L4: eps = h3 W_out + b (k split over the waves) ----
+    {
+        f32x4 po[MT][NO];
+        gemm_narrow<P, MT, NO>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_OUT]), po, wave, lane);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NO; ++n)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    part[(wave * ROWS + m * 16 + crow(lane, r)) * (16 * NO) + n * 16 + ccol(lane)] = po[m][n][r];
+    }
+    __syncthreads();
+
+    // ---- epilogue: p_mean_var + Normal.log_prob (+ c_loss policy term and its gradient) ----
+    if (wave == 0 && lane < ROWS) {
+        const int r = lane, n = rn[r], j = rj[r], t = KF - 1 - j;
+        const bool valid = n >= 0;
+        const float* bo = (const float*)(a.packed + L.off[SEG_B_OUT]);
+        const float* sc = sch + t * DPPO_SCHED_COLS;
+        const float sd = fminf(fmaxf(expf(0.5f * sc[4]), a.hp.min_lp_std), 1e6f);   // diffusion_vpg.py:473-474
+        const float inv_var = 1.f / (sd * sd);
+        const float logsd = logf(sd);
+        const int nh = min(a.hp.reward_horizon, XD / a.Da) * a.Da;                  // [:, :reward_horizon]
+        auto elem = [&](int q, float& eps, float& mu, float& lp, bool& unclipped) {
+            eps = bo[q];
+#pragma unroll
+            for (int w = 0; w < DPPO_WAVES; ++w) eps += part[(w * ROWS + r) * (16 * NO) + q];
+            const float x = xp[r * XD + q];
+            float xr = sc[0] * x - sc[1] * eps;
+            unclipped = fabsf(xr) <= 1.f;
+            xr = fminf(fmaxf(xr, -1.f), 1.f);
+            mu = sc[2] * xr + sc[3] * x;
+            const float z = (xn[r * XD + q] - mu) / sd;
+            lp = -0.5f * z * z - logsd - LOG_2PI_HALF;
+        };
+        float lpsum = 0.f;
+        for (int q = 0; q < XD; ++q) {
+            float eps, mu, lp; bool uc;
+            elem(q, eps, mu, lp, uc);
+            if (!train && valid && a.lp_elem) a.lp_elem[((size_t)n * KF + j) * XD + q] = lp;
+            if (q < nh) lpsum += fminf(fmaxf(lp, -5.f), 2.f);
+        }
+        const float newlp = lpsum / (float)nh;
+        if (!train) {
+            if (valid && a.lp_mean) a.lp_mean[(size_t)n * KF + j] = newlp;
+        } else {
+            float pg = 0.f, kl = 0.f, cf = 0.f, ra = 0.f, dnewlp = 0.f;
+            if (valid) {
+                const double* S3 = a.adv_stats;
+                float A = a.adv[n];
+                if (a.hp.norm_adv) {   // population std over the minibatch (diffusion_ppo.py:74-75)
+                    const double mean = S3[1] / S3[0];
+                    const double var = fmax(S3[2] / S3[0] - mean * mean, 0.0);
+                    A = (float)(((double)A - mean) / (sqrt(var) + 1e-8));
+                }
+                A *= powf(a.hp.gamma_denoising, (float)(KF - j - 1));                 // :83-86
+                const float oldlp = a.lp_old[(size_t)n * KF + j];
+                const float logratio = newlp - oldlp;
+                const float ratio = expf(logratio);
+                float cc;                                                              // :93-101
+                if (KF > 1) {
+                    const float tf = (float)j / (float)(KF - 1);
+                    cc = a.hp.clip_coef_base + (a.hp.clip_coef - a.hp.clip_coef_base) *
+                         (expf(a.hp.clip_coef_rate * tf) - 1.f) / (expf(a.hp.clip_coef_rate) - 1.f);
+                } else {
+                    cc = (float)j;
+                }
+                const float pg1 = -A * ratio;
+                const float rcl = fminf(fmaxf(ratio, 1.f - cc), 1.f + cc);
+                const float pg2 = -A * rcl;
+                pg = fmaxf(pg1, pg2);
+                kl = (ratio - 1.f) - logratio;
+                cf = fabsf(ratio - 1.f) > cc ? 1.f : 0.f;
+                ra = ratio;
+                const bool in_r = ratio >= 1.f - cc && ratio <= 1.f + cc;
+                const float dpg = (pg1 >= pg2) ? -A : (in_r ? -A : 0.f);   // tf.maximum ties -> first arg
+                dnewlp = dpg * ratio * a.hp.grad_scale;
+            }
+            // d loss / d eps (through clip(lp), Normal.log_prob, mu, clip(x_recon))
+            AT* dyt = a0;   // a0 tile is dead after L1; dy tile has row stride lda0
+            for (int q = 0; q < ktw; ++q) {
+                float d = 0.f;
+                if (q < XD && valid && q < nh) {
+                    float eps, mu, lp; bool uc;
+                    elem(q, eps, mu, lp, uc);
+                    const bool inc = lp >= -5.f && lp <= 2.f;
+                    const float dlp = inc ? dnewlp / (float)nh : 0.f;
+                    const float dmu = dlp * (xn[r * XD + q] - mu) * inv_var;
+                    d = uc ? -sc[1] * sc[2] * dmu : 0.f;
+                }
+                dyt[r * lda0 + q] = P::cvt(d);
+                if (q < XD) ((AT*)a.ws.dyT)[(size_t)q * a.ws.ldm + grow0 + r] = P::cvt(d);
+            }
+            pg = wave_sum(pg); kl = wave_sum(kl); cf = wave_sum(cf); ra = wave_sum(ra);
+            if (lane == 0) {
+                atomic_add_metric(a.metrics, 0, pg);
+                atomic_add_metric(a.metrics, 2, kl);
+                atomic_add_metric(a.metrics, 3, cf);
+                atomic_add_metric(a.metrics, 4, ra);
+            }
+        }
+    }
+    if (!train) return;
+    __syncthreads();
+
+    // ---- backward dX chain ----
+    // B4: dh3 = dy W_out^T
+    f32x4 DH3[MT][NT];
+    gemm_wide<P, MT, NT, DEP>(a0, lda0, L.ks_out_t, (const u32x4*)(a.packed + L.off[SEG_T_OUT]), ntile0, DH3, lane);
+    store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, DH3);
+    store_accT<P, MT, NT>(a.ws.dh3T, a.ws.ldm, ntile0, grow0, lane, DH3);
+    __syncthreads();
+    // B3: dh2 = (dh3 W_l2^T) * relu'(h2)
+    gemm_wide<P, MT, NT, DEP>(tB, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_T_L2]), ntile0, acc, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (!((mask2 >> ((m * NT + n) * 4 + r)) & 1ull)) acc[m][n][r] = 0.f;
+    store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
+    store_accT<P, MT, NT>(a.ws.dh2T, a.ws.ldm, ntile0, grow0, lane, acc);
+    __syncthreads();
+    // B2: dh1 = dh3 + (dh2 W_l1^T) * relu'(h1)
+    gemm_wide<P, MT, NT, DEP>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_T_L1]), ntile0, acc, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool on = (mask1 >> ((m * NT + n) * 4 + r)) & 1ull;
+                acc[m][n][r] = DH3[m][n][r] + (on ? acc[m][n][r] : 0.f);
+            }
+    store_accT<P, MT, NT>(a.ws.dh1T, a.ws.ldm, ntile0, grow0, lane, acc);
+}
+
+// =============================================================================================
+// critic
+// =============================================================================================
+template <class P, int MT>
+struct CriticSmem {
+    static constexpr int ROWS = 16 * MT;
+    size_t tA, tB, a0, rn, rv, total;
+    __host__ __device__ CriticSmem(const CriticArgs& a) {
+        using AT = typename P::AT;
+        const int pad = lds_pad_elems<P>();
+        const int ldh = a.HC + pad;
+        const int ka = (a.L.ks_in > a.L.ks_out_t ? a.L.ks_in : a.L.ks_out_t) * P::KG + pad;
+        size_t o = 0;
+        tA = o; o += dppo_align16(sizeof(AT) * ROWS * ldh);
+        tB = o; o += dppo_align16(sizeof(AT) * ROWS * ldh);
+        a0 = o; o += dppo_align16(sizeof(AT) * ROWS * ka);
+        rn = o; o += dppo_align16(4 * ROWS);
+        rv = o; o += dppo_align16(4 * ROWS);
+        total = o;
+    }
+};
+
+template <class P, int MT, int NT>
+__global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs a) {
+    using AT = typename P::AT;
+    constexpr int ROWS = 16 * MT;
+    constexpr int DEP = MT >= 2 ? 2 : 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const MlpLayout& L = a.L;
+    const CriticSmem<P, MT> S(a);
+    const int pad = lds_pad_elems<P>();
+    const int ldh = a.HC + pad;
+    const int lda0 = (L.ks_in > L.ks_out_t ? L.ks_in : L.ks_out_t) * P::KG + pad;
+    const int k1w = L.ks_in * P::KG, ktw = L.ks_out_t * P::KG;
+    const int SD = a.SD;
+    const bool train = a.mode == ROWS_TRAIN;
+    AT* tA = (AT*)(smem + S.tA);
+    AT* tB = (AT*)(smem + S.tB);
+    AT* a0 = (AT*)(smem + S.a0);
+    int* rn = (int*)(smem + S.rn);
+    float* part = (float*)(smem + S.tB);
+    const size_t grow0 = (size_t)blockIdx.x * ROWS;
+
+    if (tid < ROWS) {
+        const int64_t gr = (int64_t)grow0 + tid;
+        int n = -1;
+        if (gr < a.nrows) {
+            if (train) {
+                const uint64_t idx = feistel_permute((uint64_t)(a.start + gr), a.fk);
+                if (idx < a.fk.n) n = (int)(idx / a.KF);
+            } else {
+                n = (int)gr;
+            }
+        }
+        rn[tid] = n;
+    }
+    __syncthreads();
+    for (int i = tid; i < ROWS * k1w; i += DPPO_THREADS) {
+        const int r = i / k1w, c = i % k1w, n = rn[r];
+        a0[r * lda0 + c] = P::cvt((n >= 0 && c < SD) ? a.obs[(size_t)n * SD + c] : 0.f);
+    }
+    if (train) {
+        for (int i = tid; i < ROWS * SD; i += DPPO_THREADS) {
+            const int c = i / ROWS, r = i % ROWS, n = rn[r];
+            ((AT*)a.ws.csT)[(size_t)c * a.ws.ldm + grow0 + r] = P::cvt(n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f);
+        }
+    }
+    __syncthreads();
+
+    const int ntile0 = wave * NT;
+    f32x4 H1[MT][NT], H2[MT][NT], acc[MT][NT];
+    // L1: h1 = s W_in + b
+    gemm_wide<P, MT, NT, DEP>(a0, lda0, L.ks_in, (const u32x4*)(a.packed + L.off[SEG_W_IN]), ntile0, H1, lane);
+    add_bias(H1, (const float*)(a.packed + L.off[SEG_B_IN]), ntile0, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[m][n][r] = mishf(H1[m][n][r]);
+    store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
+    if (train) store_accT<P, MT, NT>(a.ws.cu1T, a.ws.ldm, ntile0, grow0, lane, acc);
+    __syncthreads();
+    // L2: h2 = mish(h1) W_l1 + b
+    gemm_wide<P, MT, NT, DEP>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_L1]), ntile0, H2, lane);
+    add_bias(H2, (const float*)(a.packed + L.off[SEG_B_L1]), ntile0, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[m][n][r] = mishf(H2[m][n][r]);
+    store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
+    if (train) store_accT<P, MT, NT>(a.ws.cu2T, a.ws.ldm, ntile0, grow0, lane, acc);
+    __syncthreads();
+    // L3: h3 = mish(h2) W_l2 + b + h1
+    gemm_wide<P, MT, NT, DEP>(tB, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_L2]), ntile0, acc, lane);
+    add_bias(acc, (const float*)(a.packed + L.off[SEG_B_L2]), ntile0, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[m][n][r] += H1[m][n][r];
+    store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
+    if (train) store_accT<P, MT, NT>(a.ws.ch3T, a.ws.ldm, ntile0, grow0, lane, acc);
+    __syncthreads();
+    // L4: V = h3 W_out + b
+    {
+        f32x4 po[MT][1];
+        gemm_narrow<P, MT, 1>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_OUT]), po, wave, lane);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[(wave * ROWS + m * 16 + crow(lane, r)) * 16 + ccol(lane)] = po[m][0][r];
+    }
+    __syncthreads();
+    if (wave == 0 && lane < ROWS) {
+        const int r = lane, n = rn[r];
+        float V = ((const float*)(a.packed + L.off[SEG_B_OUT]))[0];
+#pragma unroll
+        for (int w = 0; w < DPPO_WAVES; ++w) V += part[(w * ROWS + r) * 16];
+        if (!train) {
+            if (n >= 0) a.values[n] = V;
+        } else {
+            float vl = 0.f, dv = 0.f;
+            if (n >= 0) {
+                const float diff = V - a.returns[n];
+                vl = 0.5f * diff * diff;                         // v_loss = 0.5 mean((V-R)^2), diffusion_ppo.py:118
+                dv = a.hp.vf_coef * diff * a.hp.grad_scale;      // loss = pg + vf_coef * v_loss (agent :340)
+            }
+            for (int q = 0; q < ktw; ++q) a0[r * lda0 + q] = P::cvt(q == 0 ? dv : 0.f);
+            ((AT*)a.ws.cdvT)[grow0 + r] = P::cvt(dv);
+            vl = wave_sum(vl);
+            if (lane == 0) atomic_add_metric(a.metrics, 1, vl);
+        }
+    }
+    if (!train) return;
+    __syncthreads();
+    // B4: dh3 = dV W_out^T
+    f32x4 DH3[MT][NT];
+    gemm_wide<P, MT, NT, DEP>(a0, lda0, L.ks_out_t, (const u32x4*)(a.packed + L.off[SEG_T_OUT]), ntile0, DH3, lane);
+    store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, DH3);
+    store_accT<P, MT, NT>(a.ws.cdh3T, a.ws.ldm, ntile0, grow0, lane, DH3);
+    __syncthreads();
+    // B3: dh2 = (dh3 W_l2^T) * mish'(h2)
+    gemm_wide<P, MT, NT, DEP>(tB, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_T_L2]), ntile0, acc, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[m][n][r] *= mish_gradf(H2[m][n][r]);
+    store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
+    store_accT<P, MT, NT>(a.ws.cdh2T, a.ws.ldm, ntile0, grow0, lane, acc);
+    __syncthreads();
+    // B2: dh1 = dh3 + (dh2 W_l1^T) * mish'(h1)
+    gemm_wide<P, MT, NT, DEP>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_T_L1]), ntile0, acc, lane);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[m][n][r] = DH3[m][n][r] + acc[m][n][r] * mish_gradf(H1[m][n][r]);
+    store_accT<P, MT, NT>(a.ws.cdh1T, a.ws.ldm, ntile0, grow0, lane, acc);
+}
+
+// =============================================================================================
+// launchers
+// =============================================================================================
+template <class P, int MT, int NT, int NO>
+static int launch_actor_t(const ActorArgs& a, hipStream_t s) {
+    const ActorSmem<P, MT> S(a);
+    const int pad = lds_pad_elems<P>();
+    const size_t part_bytes = (size_t)4 * DPPO_WAVES * 16 * MT * 16 * NO;
+    const size_t tb_bytes = sizeof(typename P::AT) * 16 * MT * (a.H + pad);
+    if (part_bytes > tb_bytes) return dppo_set_error(DPPO_EUNSUPPORTED, "actor: partial buffer does not fit");
+    if (S.total > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "actor row tile needs %zu B LDS", S.total);
+    auto k = actor_rowtile_kernel<P, MT, NT, NO>;
+    DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S.total));
+    // TRAIN mode covers every row of the 64-padded feature-major images (padding rows get
+    // finite activations and zero gradients), so the dW kernel never reads unwritten memory
+    const int64_t rows = a.mode == ROWS_TRAIN ? (int64_t)a.ws.ldm : a.nrows;
+    const int64_t grid = (rows + 16 * MT - 1) / (16 * MT);
+    if (grid == 0) return DPPO_OK;
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(DPPO_THREADS), S.total, s, a);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+template <class P, int MT>
+static int dispatch_actor(const ActorArgs& a, hipStream_t s) {
+    const int NT = a.H / (16 * DPPO_WAVES), NO = dppo_cdiv(a.XD, 16);
+    if (NT == 4 && NO == 1) return launch_actor_t<P, MT, 4, 1>(a, s);
+    if (NT == 4 && NO == 2) return launch_actor_t<P, MT, 4, 2>(a, s);
+    if (NT == 2 && NO == 1) return launch_actor_t<P, MT, 2, 1>(a, s);
+    if (NT == 2 && NO == 2) return launch_actor_t<P, MT, 2, 2>(a, s);
+    return dppo_set_error(DPPO_EUNSUPPORTED, "actor: hidden %d / chunk %d not instantiated", a.H, a.XD);
+}
+
+// rows per workgroup of the update kernels: 64 (bf16) / 32 (fp32, LDS-limited)
+int actor_rows_per_tile(int precision) { (void)precision; return 32; }
+
+int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
+    return precision == DPPO_BF16 ? dispatch_actor<PolicyBF16, 2>(a, s) : dispatch_actor<PolicyF32, 2>(a, s);
+}
+
+template <class P, int MT, int NT>
+static int launch_critic_t(const CriticArgs& a, hipStream_t s) {
+    const CriticSmem<P, MT> S(a);
+    if (S.total > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "critic row tile needs %zu B LDS", S.total);
+    auto k = critic_rowtile_kernel<P, MT, NT>;
+    DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S.total));
+    // TRAIN mode covers every row of the 64-padded feature-major images (padding rows get
+    // finite activations and zero gradients), so the dW kernel never reads unwritten memory
+    const int64_t rows = a.mode == ROWS_TRAIN ? (int64_t)a.ws.ldm : a.nrows;
+    const int64_t grid = (rows + 16 * MT - 1) / (16 * MT);
+    if (grid == 0) return DPPO_OK;
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(DPPO_THREADS), S.total, s, a);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+template <class P, int MT>
+static int dispatch_critic(const CriticArgs& a, hipStream_t s) {
+    const int NT = a.HC / (16 * DPPO_WAVES);
+    if (NT == 2) return launch_critic_t<P, MT, 2>(a, s);
+    if (NT == 1) return launch_critic_t<P, MT, 1>(a, s);
+    return dppo_set_error(DPPO_EUNSUPPORTED, "critic: hidden %d not instantiated", a.HC);
+}
+
+int launch_critic_rowtile(const CriticArgs& a, int precision, hipStream_t s) {
+    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2>(a, s) : dispatch_critic<PolicyF32, 2>(a, s);
+}
+
+// =============================================================================================
+// C ABI: old-logprob pass and value pass
+// =============================================================================================
+extern "C" int dppo_logprob(const dppo_dims* d, int precision, const void* packed_ft, const float* sched,
+                            const float* cond, const float* chains, int n, float min_logprob_std, int reward_horizon,
+                            float* lp_elem, float* lp_mean, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    DPPO_CHECK(n >= 0, "dppo_logprob: n < 0");
+    if (n == 0) return DPPO_OK;
+    DPPO_CHECK(packed_ft && sched && cond && chains && (lp_elem || lp_mean), "dppo_logprob: null pointer");
+    DPPO_CHECK(reward_horizon >= 1, "dppo_logprob: reward_horizon < 1");
+    ActorArgs a = {};
+    a.packed = (const uint8_t*)packed_ft;
+    a.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision);
+    a.sched = sched; a.obs = cond; a.chains = chains;
+    a.XD = D.XD; a.SD = D.SD; a.TD = D.TD; a.IN = D.IN; a.H = D.H; a.KF = D.KF; a.Da = D.Da;
+    a.mode = ROWS_LOGPROB;
+    a.nrows = (int64_t)n * D.KF;
+    a.lp_elem = lp_elem; a.lp_mean = lp_mean;
+    a.hp.min_lp_std = min_logprob_std;
+    a.hp.reward_horizon = reward_horizon;
+    return launch_actor_rowtile(a, precision, (hipStream_t)stream);
+}
+
+extern "C" int dppo_critic_forward(const dppo_dims* d, int precision, const void* packed_critic, const float* cond,
+                                   int n, float* values, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    DPPO_CHECK(n >= 0, "dppo_critic_forward: n < 0");
+    if (n == 0) return DPPO_OK;
+    DPPO_CHECK(packed_critic && cond && values, "dppo_critic_forward: null pointer");
+    CriticArgs a = {};
+    a.packed = (const uint8_t*)packed_critic;
+    a.L = make_mlp_layout(D.SD, D.HC, 1, 0, precision);
+    a.obs = cond; a.SD = D.SD; a.HC = D.HC; a.KF = D.KF;
+    a.mode = ROWS_VALUE; a.nrows = n; a.values = values;
+    return launch_critic_rowtile(a, precision, (hipStream_t)stream);
+}

@@ -1,0 +1,262 @@
+// sampler.hip — a9: VPGDiffusion.call (model/diffusion/diffusion_vpg.py:250-339), DDPM branch.
+//
+// One workgroup (8 waves) owns 16 env rows for ALL K denoising steps: rows are independent, so
+// the K x 4 dependent GEMMs of a rollout step run without any inter-workgroup synchronisation.
+// Per step: a0 = [x, t_emb(t), state] (mlp_diffusion.py:72-86) -> in-Dense -> relu -> l1 -> relu
+// -> l2 + h1 (residual, mlp.py:186-206) -> out-Dense = eps; then the fused fp32 DDPM epilogue
+// (diffusion_vpg.py:198-243, 301-320). Activations never leave LDS; weights stream from L2.
+// The actor used at step t is actor_ft when t < K' else the frozen base actor (diffusion_vpg.py:161-180);
+// the reference's always-computed base forward (:161) does not change the result and is skipped.
+#include "dppo_common.cuh"
+#include "dppo_internal.h"
+
+struct SampleArgs {
+    const uint8_t* packed_base;
+    const uint8_t* packed_ft;
+    const float* sched;   // [K][8]
+    const float* cond;    // [E][SD]
+    const float* x_T;     // [E][XD] or null
+    const float* noise;   // [K][E][XD] or null
+    float* actions;       // [E][XD]
+    float* chains;        // [E][KF+1][XD] or null
+    uint64_t seed;
+    uint32_t call_id;
+    int E, env_offset, deterministic;
+    float min_std, randn_clip, final_clip;
+    int XD, SD, TD, H, K, KF, IN;
+    MlpLayout L;          // same layout for base and ft
+};
+
+template <class P, int NT, int NO>
+__global__ __launch_bounds__(DPPO_THREADS) void sample_kernel(SampleArgs a) {
+    using AT = typename P::AT;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int row0 = blockIdx.x * 16;
+    const MlpLayout& L = a.L;
+    const int pad = lds_pad_elems<P>();
+    const int ldh = a.H + pad;
+    const int k1w = L.ks_in * P::KG;
+    const int lda0 = k1w + pad;
+    const int XD = a.XD, SD = a.SD, TD = a.TD, K = a.K, KF = a.KF;
+    const int NOC = 16 * NO;
+
+    // ---- LDS carve (all offsets multiples of 16 B) ----
+    size_t o = 0;
+    AT* tA = (AT*)(smem + o); o += dppo_align16(sizeof(AT) * 16 * ldh);
+    AT* tB = (AT*)(smem + o); o += dppo_align16(sizeof(AT) * 16 * ldh);
+    AT* a0 = (AT*)(smem + o); o += dppo_align16(sizeof(AT) * 16 * lda0);
+    float* xs = (float*)(smem + o); o += dppo_align16(4 * 16 * XD);
+    float* st = (float*)(smem + o); o += dppo_align16(4 * 16 * SD);
+    float* temb = (float*)(smem + o); o += dppo_align16(4 * K * TD);
+    float* ta1 = (float*)(smem + o); o += dppo_align16(4 * K * 2 * TD);
+    float* part = (float*)(smem + o); o += dppo_align16(4 * DPPO_WAVES * 16 * NOC);
+    float* sch = (float*)(smem + o); o += dppo_align16(4 * K * DPPO_SCHED_COLS);
+
+    // ---- prologue: schedule, state, x_T, time-embedding table ----
+    for (int i = tid; i < K * DPPO_SCHED_COLS; i += DPPO_THREADS) sch[i] = a.sched[i];
+    for (int i = tid; i < 16 * SD; i += DPPO_THREADS) {
+        const int r = i / SD, c = i % SD, row = row0 + r;
+        st[i] = row < a.E ? a.cond[(size_t)row * SD + c] : 0.f;
+    }
+    for (int i = tid; i < 16 * XD; i += DPPO_THREADS) {
+        const int r = i / XD, q = i % XD, row = row0 + r;
+        float x;
+        if (a.x_T) x = row < a.E ? a.x_T[(size_t)row * XD + q] : 0.f;
+        else x = philox_normal(a.seed, (uint32_t)(q >> 2), (uint32_t)(a.env_offset + row), (uint32_t)K, a.call_id, q & 3);
+        xs[i] = x;
+        if (KF == K && a.chains && row < a.E) a.chains[((size_t)row * (KF + 1) + 0) * XD + q] = x;
+    }
+    // time MLP (mlp_diffusion.py:40-45): SinusoidalPosEmb -> Dense(TD->2TD, mish) -> Dense(2TD->TD)
+    const int half = TD / 2;
+    const float lnf = logf(10000.f) / (float)(half - 1);
+    for (int i = tid; i < K * 2 * TD; i += DPPO_THREADS) {
+        const int t = i / (2 * TD), j = i % (2 * TD);
+        const float* tw = (const float*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIME]);
+        const float* w1 = tw;                       // [TD][2TD]
+        const float* b1 = tw + TD * 2 * TD;         // [2TD]
+        float acc = b1[j];
+        for (int k = 0; k < TD; ++k) {
+            const float f = expf(-(float)(k % half) * lnf) * (float)t;
+            const float e = k < half ? sinf(f) : cosf(f);
+            acc += e * w1[k * 2 * TD + j];
+        }
+        ta1[i] = mishf(acc);
+    }
+    __syncthreads();
+    for (int i = tid; i < K * TD; i += DPPO_THREADS) {
+        const int t = i / TD, j = i % TD;
+        const float* tw = (const float*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIME]);
+        const float* w2 = tw + TD * 2 * TD + 2 * TD;  // [2TD][TD]
+        const float* b2 = w2 + 2 * TD * TD;           // [TD]
+        float acc = b2[j];
+        for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + j];
+        temb[i] = acc;
+    }
+    __syncthreads();
+
+    const int ntile0 = wave * NT;
+    for (int i = 0; i < K; ++i) {
+        const int t = K - 1 - i;
+        const uint8_t* PK = t < KF ? a.packed_ft : a.packed_base;
+        // a) a0 = [x, temb(t), state, 0-pad]
+        for (int idx = tid; idx < 16 * k1w; idx += DPPO_THREADS) {
+            const int r = idx / k1w, c = idx % k1w;
+            float v = 0.f;
+            if (c < XD) v = xs[r * XD + c];
+            else if (c < XD + TD) v = temb[t * TD + c - XD];
+            else if (c < a.IN) v = st[r * SD + c - XD - TD];
+            a0[r * lda0 + c] = P::cvt(v);
+        }
+        __syncthreads();
+        // b) in-Dense: h1 = a0 W_in + b_in  (no activation after the input layer, mlp.py:144)
+        f32x4 h1[1][NT], acc[1][NT];
+        gemm_wide<P, 1, NT, 3>(a0, lda0, L.ks_in, (const u32x4*)(PK + L.off[SEG_W_IN]), ntile0, h1, lane);
+        {
+            const float* bb = (const float*)(PK + L.off[SEG_B_IN]);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int col = (ntile0 + n) * 16 + ccol(lane);
+                const float bv = bb[col];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    h1[0][n][r] += bv;
+                    tA[crow(lane, r) * ldh + col] = P::cvt(fmaxf(h1[0][n][r], 0.f));
+                }
+            }
+        }
+        __syncthreads();
+        // c) l1: relu(h1) W_l1 + b -> relu -> tB   (pre-activation block, mlp.py:192-193,202-203)
+        gemm_wide<P, 1, NT, 3>(tA, ldh, L.ks_h, (const u32x4*)(PK + L.off[SEG_W_L1]), ntile0, acc, lane);
+        {
+            const float* bb = (const float*)(PK + L.off[SEG_B_L1]);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int col = (ntile0 + n) * 16 + ccol(lane);
+                const float bv = bb[col];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tB[crow(lane, r) * ldh + col] = P::cvt(fmaxf(acc[0][n][r] + bv, 0.f));
+            }
+        }
+        __syncthreads();
+        // d) l2: relu(h2) W_l2 + b + h1 (residual, mlp.py:206) -> tA (no activation before out-Dense)
+        gemm_wide<P, 1, NT, 3>(tB, ldh, L.ks_h, (const u32x4*)(PK + L.off[SEG_W_L2]), ntile0, acc, lane);
+        {
+            const float* bb = (const float*)(PK + L.off[SEG_B_L2]);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int col = (ntile0 + n) * 16 + ccol(lane);
+                const float bv = bb[col];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tA[crow(lane, r) * ldh + col] = P::cvt(acc[0][n][r] + bv + h1[0][n][r]);
+            }
+        }
+        __syncthreads();
+        // e) out-Dense (N = XD <= 16*NO): k split over the 8 waves, partials through LDS
+        {
+            f32x4 po[1][NO];
+            gemm_narrow<P, 1, NO>(tA, ldh, L.ks_h, (const u32x4*)(PK + L.off[SEG_W_OUT]), po, wave, lane);
+#pragma unroll
+            for (int n = 0; n < NO; ++n)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    part[(wave * 16 + crow(lane, r)) * NOC + n * 16 + ccol(lane)] = po[0][n][r];
+        }
+        __syncthreads();
+        // f) DDPM epilogue, fp32 (diffusion_vpg.py:198-243, 301-320)
+        if (tid < 16 * XD) {
+            const int r = tid / XD, q = tid % XD, row = row0 + r;
+            const float* bo = (const float*)(PK + L.off[SEG_B_OUT]);
+            float eps = bo[q];
+#pragma unroll
+            for (int w = 0; w < DPPO_WAVES; ++w) eps += part[(w * 16 + r) * NOC + q];
+            const float* sc = sch + t * DPPO_SCHED_COLS;
+            const float x = xs[tid];
+            float xr = sc[0] * x - sc[1] * eps;
+            xr = fminf(fmaxf(xr, -1.f), 1.f);                    // denoised_clip_value = 1 (diffusion.py:28)
+            const float mu = sc[2] * xr + sc[3] * x;
+            float sd = expf(0.5f * sc[4]);
+            if (a.deterministic && t == 0) sd = 0.f;
+            else if (a.deterministic) sd = fminf(fmaxf(sd, 1e-3f), 1e6f);
+            else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
+            float z;
+            if (a.noise) z = row < a.E ? a.noise[((size_t)i * a.E + row) * XD + q] : 0.f;
+            else z = philox_normal(a.seed, (uint32_t)(q >> 2), (uint32_t)(a.env_offset + row), (uint32_t)i, a.call_id, q & 3);
+            z = fminf(fmaxf(z, -a.randn_clip), a.randn_clip);
+            float xn = mu + sd * z;
+            if (a.final_clip > 0.f && i == K - 1) xn = fminf(fmaxf(xn, -a.final_clip), a.final_clip);
+            xs[tid] = xn;
+            if (row < a.E) {
+                if (a.chains && t <= KF) a.chains[((size_t)row * (KF + 1) + (KF - t)) * XD + q] = xn;
+                if (i == K - 1) a.actions[(size_t)row * XD + q] = xn;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <class P>
+static size_t sample_lds_bytes(const SampleArgs& a, int NO) {
+    using AT = typename P::AT;
+    const int pad = lds_pad_elems<P>();
+    const int ldh = a.H + pad;
+    const int lda0 = a.L.ks_in * P::KG + pad;
+    size_t o = 0;
+    o += dppo_align16(sizeof(AT) * 16 * ldh) * 2;
+    o += dppo_align16(sizeof(AT) * 16 * lda0);
+    o += dppo_align16(4 * 16 * a.XD);
+    o += dppo_align16(4 * 16 * a.SD);
+    o += dppo_align16(4 * a.K * a.TD);
+    o += dppo_align16(4 * a.K * 2 * a.TD);
+    o += dppo_align16(4 * DPPO_WAVES * 16 * 16 * NO);
+    o += dppo_align16(4 * a.K * DPPO_SCHED_COLS);
+    return o;
+}
+
+template <class P, int NT, int NO>
+static int launch_sample(const SampleArgs& a, hipStream_t s) {
+    const size_t lds = sample_lds_bytes<P>(a, NO);
+    if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "sampler needs %zu B of LDS", lds);
+    auto k = sample_kernel<P, NT, NO>;
+    DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k, dim3(dppo_cdiv(a.E, 16)), dim3(DPPO_THREADS), lds, s, a);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+template <class P>
+static int dispatch_sample(const SampleArgs& a, hipStream_t s) {
+    const int NT = a.H / (16 * DPPO_WAVES);
+    const int NO = dppo_cdiv(a.XD, 16);
+    if (NT == 4 && NO == 1) return launch_sample<P, 4, 1>(a, s);
+    if (NT == 4 && NO == 2) return launch_sample<P, 4, 2>(a, s);
+    if (NT == 2 && NO == 1) return launch_sample<P, 2, 1>(a, s);
+    if (NT == 2 && NO == 2) return launch_sample<P, 2, 2>(a, s);
+    if (NT == 1 && NO == 1) return launch_sample<P, 1, 1>(a, s);
+    if (NT == 1 && NO == 2) return launch_sample<P, 1, 2>(a, s);
+    return dppo_set_error(DPPO_EUNSUPPORTED, "sampler: hidden %d / action chunk %d not instantiated", a.H, a.XD);
+}
+
+extern "C" int dppo_sample(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
+                           const float* sched, const float* cond, int n_envs, const float* x_T, const float* noise,
+                           uint64_t seed, uint64_t call_id, int env_offset, int deterministic,
+                           float min_sampling_std, float randn_clip, float final_clip,
+                           float* actions, float* chains, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(n_envs >= 0, "dppo_sample: n_envs < 0");
+    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "dppo_sample: bad precision %d", precision);
+    if (n_envs == 0) return DPPO_OK;
+    DPPO_CHECK(packed_base && packed_ft && sched && cond && actions, "dppo_sample: null pointer argument");
+    SampleArgs a;
+    a.packed_base = (const uint8_t*)packed_base;
+    a.packed_ft = (const uint8_t*)packed_ft;
+    a.sched = sched; a.cond = cond; a.x_T = x_T; a.noise = noise; a.actions = actions; a.chains = chains;
+    a.seed = seed; a.call_id = (uint32_t)call_id; a.E = n_envs; a.env_offset = env_offset;
+    a.deterministic = deterministic; a.min_std = min_sampling_std; a.randn_clip = randn_clip; a.final_clip = final_clip;
+    a.XD = D.XD; a.SD = D.SD; a.TD = D.TD; a.H = D.H; a.K = D.K; a.KF = D.KF; a.IN = D.IN;
+    a.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision);
+    hipStream_t s = (hipStream_t)stream;
+    return precision == DPPO_BF16 ? dispatch_sample<PolicyBF16>(a, s) : dispatch_sample<PolicyF32>(a, s);
+}

@@ -1,0 +1,217 @@
+// scan.hip — a18 RunningRewardScaler (util/reward_scaling.py:13-87) and a19 GAE
+// (agent/finetune/train_ppo_diffusion_agent.py:239-263) as wave-level affine-map scans.
+//
+// Both recurrences are first-order affine: y_t = d_t + c_t * y_{t-/+1}. One wavefront owns one
+// env: each lane folds a contiguous chunk of time steps into a map (C, D), the 64 maps are
+// composed with a 6-step shuffle scan, and each lane replays its chunk from the scanned carry.
+// Arithmetic is fp64 like the reference's NumPy float64 path.
+#include "dppo_common.cuh"
+#include "dppo_internal.h"
+
+#define SCAN_WAVES 4
+
+// inclusive composition over lanes. forward=true: lane l gets M_l o ... o M_0 (prefix, carry in from
+// lower t); forward=false: lane l gets M_l o M_{l+1} o ... o M_63 (suffix, carry from higher t).
+__device__ inline void affine_scan(double& C, double& D, int lane, bool forward) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const double oc = forward ? __shfl_up(C, off, 64) : __shfl_down(C, off, 64);
+        const double od = forward ? __shfl_up(D, off, 64) : __shfl_down(D, off, 64);
+        const bool has = forward ? (lane >= off) : (lane + off < 64);
+        if (has) {  // (M_self o M_other)(y) = D + C*(od + oc*y)
+            D = D + C * od;
+            C = C * oc;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// GAE: A_t = delta_t + gamma*lam*nonterm_t * A_{t+1}; R = A + V
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64 * SCAN_WAVES) void gae_kernel(const double* __restrict__ rew, const float* __restrict__ val,
+                                                              const float* __restrict__ last_val, const uint8_t* __restrict__ term,
+                                                              int S, int E, double gamma, double lam, double rsc,
+                                                              float* __restrict__ adv, float* __restrict__ ret) {
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x * SCAN_WAVES + (threadIdx.x >> 6);
+    if (e >= E) return;
+    const int CH = (S + 63) / 64;
+    const int t0 = lane * CH, t1 = min(S, t0 + CH);
+    auto delta_c = [&](int t, double& dl, double& c) {
+        const double nonterm = 1.0 - (double)term[(size_t)t * E + e];
+        const double nextv = (t == S - 1) ? (double)last_val[e] : (double)val[(size_t)(t + 1) * E + e];
+        dl = rew[(size_t)t * E + e] * rsc + gamma * nextv * nonterm - (double)val[(size_t)t * E + e];
+        c = gamma * lam * nonterm;
+    };
+    // chunk map, processed from t1-1 down to t0: y(t0) = D + C * y(t1)
+    double C = 1.0, D = 0.0;
+    for (int t = t1 - 1; t >= t0; --t) {
+        double dl, c;
+        delta_c(t, dl, c);
+        D = dl + c * D;
+        C = c * C;
+    }
+    affine_scan(C, D, lane, false);
+    // carry into this chunk = y at t1 = scanned D of lane+1 (applied to y_S = 0)
+    double carry = __shfl_down(D, 1, 64);
+    if (lane == 63) carry = 0.0;
+    for (int t = t1 - 1; t >= t0; --t) {
+        double dl, c;
+        delta_c(t, dl, c);
+        carry = dl + c * carry;
+        adv[(size_t)t * E + e] = (float)carry;
+        ret[(size_t)t * E + e] = (float)(carry + (double)val[(size_t)t * E + e]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// reward scaler pass 1: rets_t = r_t + (1-first_t)*gamma*rets_{t-1}; per-env Chan moments
+// ---------------------------------------------------------------------------------------------
+__device__ inline void chan_merge(double& n, double& mean, double& m2, double nb, double meanb, double m2b) {
+    if (nb == 0.0) return;
+    if (n == 0.0) { n = nb; mean = meanb; m2 = m2b; return; }
+    const double tot = n + nb;
+    const double delta = meanb - mean;
+    mean = mean + delta * nb / tot;
+    m2 = m2 + m2b + delta * delta * n * nb / tot;
+    n = tot;
+}
+
+__global__ __launch_bounds__(64 * SCAN_WAVES) void rets_kernel(const double* __restrict__ rew, const uint8_t* __restrict__ first,
+                                                               double* __restrict__ ret_state, double* __restrict__ rets,
+                                                               double* __restrict__ env_mom, int S, int E, double gamma) {
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x * SCAN_WAVES + (threadIdx.x >> 6);
+    if (e >= E) return;
+    const int CH = (S + 63) / 64;
+    const int t0 = lane * CH, t1 = min(S, t0 + CH);
+    double C = 1.0, D = 0.0;  // y(t1-1) = D + C * y(t0-1)
+    for (int t = t0; t < t1; ++t) {
+        const double g = (1.0 - (double)first[(size_t)t * E + e]) * gamma;
+        D = rew[(size_t)t * E + e] + g * D;
+        C = g * C;
+    }
+    affine_scan(C, D, lane, true);
+    const double y0 = ret_state[e];
+    // scanned map of lane l-1 applied to y0 gives the carry into lane l
+    double pc = __shfl_up(C, 1, 64), pd = __shfl_up(D, 1, 64);
+    double carry = lane == 0 ? y0 : pd + pc * y0;
+    double n = 0.0, mean = 0.0, m2 = 0.0;
+    for (int t = t0; t < t1; ++t) {
+        const double g = (1.0 - (double)first[(size_t)t * E + e]) * gamma;
+        carry = rew[(size_t)t * E + e] + g * carry;
+        rets[(size_t)t * E + e] = carry;
+        n += 1.0;  // Welford
+        const double dlt = carry - mean;
+        mean += dlt / n;
+        m2 += dlt * (carry - mean);
+    }
+    // last step's ret becomes the carried state (reward_scaling.py:62)
+    if (t1 == S && t0 < t1) ret_state[e] = carry;
+    // merge moments across the wave
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double on = __shfl_xor(n, off, 64), om = __shfl_xor(mean, off, 64), o2 = __shfl_xor(m2, off, 64);
+        chan_merge(n, mean, m2, on, om, o2);
+    }
+    if (lane == 0) { env_mom[3 * e + 0] = n; env_mom[3 * e + 1] = mean; env_mom[3 * e + 2] = m2; }
+}
+
+// merge per-env moments -> moments[3] = {n, mean, M2}; if rms != null also apply the
+// RunningMeanStd.update_from_moments (reward_scaling.py:29-39) to rms = {mean, var, count}
+__global__ void moments_kernel(const double* __restrict__ env_mom, int E, double* __restrict__ moments, double* __restrict__ rms) {
+    __shared__ double sh[3 * 64];
+    const int tid = threadIdx.x;
+    double n = 0.0, mean = 0.0, m2 = 0.0;
+    for (int e = tid; e < E; e += 64) chan_merge(n, mean, m2, env_mom[3 * e], env_mom[3 * e + 1], env_mom[3 * e + 2]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double on = __shfl_xor(n, off, 64), om = __shfl_xor(mean, off, 64), o2 = __shfl_xor(m2, off, 64);
+        chan_merge(n, mean, m2, on, om, o2);
+    }
+    (void)sh;
+    if (tid == 0) {
+        moments[0] = n; moments[1] = mean; moments[2] = m2;
+        if (rms) {
+            const double bm = mean, bv = n > 0 ? m2 / n : 0.0, bc = n;
+            const double delta = bm - rms[0];
+            const double tot = rms[2] + bc;
+            const double new_mean = rms[0] + delta * bc / tot;
+            const double M2 = rms[1] * rms[2] + bv * bc + delta * delta * rms[2] * bc / tot;
+            rms[0] = new_mean;
+            rms[1] = M2 / (tot - 1.0);
+            rms[2] = tot;
+        }
+    }
+}
+
+__global__ void scale_apply_kernel(double* __restrict__ rew, const double* __restrict__ rms, int64_t n, double cliprew, double eps) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double s = sqrt(rms[1] + eps);
+    double r = rew[i] / s;
+    r = r < -cliprew ? -cliprew : (r > cliprew ? cliprew : r);
+    rew[i] = r;
+}
+
+extern "C" int dppo_gae(const double* reward, const float* values, const float* last_values, const uint8_t* terminated,
+                        int S, int E, double gamma, double lam, double reward_scale_const,
+                        float* advantages, float* returns, void* stream) {
+    DPPO_CHECK(S >= 0 && E >= 0, "dppo_gae: negative size");
+    if (S == 0 || E == 0) return DPPO_OK;
+    DPPO_CHECK(reward && values && last_values && terminated && advantages && returns, "dppo_gae: null pointer");
+    hipLaunchKernelGGL(gae_kernel, dim3(dppo_cdiv(E, SCAN_WAVES)), dim3(64 * SCAN_WAVES), 0, (hipStream_t)stream,
+                       reward, values, last_values, terminated, S, E, gamma, lam, reward_scale_const, advantages, returns);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+extern "C" int dppo_reward_scale_moments(const double* reward, const uint8_t* first, double* ret_state, double* workspace,
+                                         double* moments, int S, int E, double gamma, void* stream) {
+    DPPO_CHECK(S > 0 && E > 0, "dppo_reward_scale_moments: empty");
+    DPPO_CHECK(reward && first && ret_state && workspace && moments, "dppo_reward_scale_moments: null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    double* rets_ws = workspace;
+    double* env_mom = rets_ws + (size_t)S * E;
+    hipLaunchKernelGGL(rets_kernel, dim3(dppo_cdiv(E, SCAN_WAVES)), dim3(64 * SCAN_WAVES), 0, s,
+                       reward, first, ret_state, rets_ws, env_mom, S, E, gamma);
+    DPPO_HIP(hipGetLastError());
+    hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(64), 0, s, env_mom, E, moments, (double*)nullptr);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+extern "C" int dppo_reward_scale_apply(double* reward, const double* rms_state, int S, int E, double cliprew,
+                                       double epsilon, void* stream) {
+    DPPO_CHECK(reward && rms_state, "dppo_reward_scale_apply: null pointer");
+    const int64_t n = (int64_t)S * E;
+    if (n == 0) return DPPO_OK;
+    hipLaunchKernelGGL(scale_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       reward, rms_state, n, cliprew, epsilon);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+extern "C" size_t dppo_reward_scale_workspace_doubles(int S, int E) {
+    return (size_t)S * E + (size_t)3 * E + 3;
+}
+
+extern "C" int dppo_reward_scale(double* reward, const uint8_t* first, double* ret_state, double* rms_state,
+                                 double* workspace, int S, int E, double gamma, double cliprew, double epsilon,
+                                 void* stream) {
+    DPPO_CHECK(S > 0 && E > 0, "dppo_reward_scale: empty");
+    DPPO_CHECK(reward && first && ret_state && rms_state && workspace, "dppo_reward_scale: null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    double* rets = workspace;
+    double* env_mom = rets + (size_t)S * E;
+    double* moments = env_mom + (size_t)3 * E;
+    hipLaunchKernelGGL(rets_kernel, dim3(dppo_cdiv(E, SCAN_WAVES)), dim3(64 * SCAN_WAVES), 0, s,
+                       reward, first, ret_state, rets, env_mom, S, E, gamma);
+    DPPO_HIP(hipGetLastError());
+    hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(64), 0, s, env_mom, E, moments, rms_state);
+    DPPO_HIP(hipGetLastError());
+    hipLaunchKernelGGL(scale_apply_kernel, dim3(dppo_cdiv(S * E, 256)), dim3(256), 0, s, reward, rms_state,
+                       (int64_t)S * E, cliprew, epsilon);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}

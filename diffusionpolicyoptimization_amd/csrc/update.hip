@@ -1,0 +1,391 @@
+// update.hip — weight gradients, time-MLP backward, minibatch statistics, optimiser, and the
+// dppo_ppo_minibatch orchestration (agent/finetune/train_ppo_diffusion_agent.py:287-356).
+#include "dppo_ppo.h"
+
+// ---------------------------------------------------------------------------------------------
+// grouped split-K weight-gradient GEMM:  G[k][n] += sum_m XT[k][m] * DT[n][m]
+// (dW = X^T dH in Keras [in,out] layout). A workgroup owns a 64x64 output tile and one m-chunk;
+// 4 waves each hold a 32x32 sub-tile (2x2 MFMA tiles). Both operands are feature-major, so every
+// fragment is 16 contiguous bytes along m. The k-tile-0 workgroups also produce the "extra" rows:
+//   ONES   -> bias gradient  sum_m DT[n][m]
+//   ONEHOT -> per-bucket sums sum_{m: seg[m]=q} DT[n][m]  (actor in-layer: in_b and d t_emb)
+// Partial tiles are added with fp32 atomics (one add per element per m-chunk).
+// ---------------------------------------------------------------------------------------------
+enum { EXTRA_NONE = 0, EXTRA_ONES = 1, EXTRA_ONEHOT = 2 };
+#define DW_MAXP 8
+
+struct DWProb {
+    const void* XT; const void* DT; float* G; float* Gx;
+    int Kx, N, extra, ktiles, ntiles;
+};
+struct DWArgs {
+    DWProb p[DW_MAXP];
+    int tile_start[DW_MAXP + 1];
+    int nprob, nchunks, mchunk;
+    size_t ldm;
+    const int8_t* seg;
+};
+
+template <class P>
+__device__ inline u32x4 load_frag_rows(const typename P::AT* base, size_t ldm, int row, int nrows, size_t m) {
+    const int rr = row < nrows ? row : nrows - 1;
+    u32x4 v = *reinterpret_cast<const u32x4*>(base + (size_t)rr * ldm + m);
+    if (row >= nrows) v = u32x4{0u, 0u, 0u, 0u};
+    return v;
+}
+
+template <class P>
+__device__ inline u32x4 extra_frag(int extra, int q, const int8_t* seg, size_t m) {
+    using AT = typename P::AT;
+    AT e[P::EPL];
+#pragma unroll
+    for (int i = 0; i < P::EPL; ++i) {
+        float v = extra == EXTRA_ONES ? 1.f : ((int)seg[m + i] == q ? 1.f : 0.f);
+        e[i] = P::cvt(v);
+    }
+    return __builtin_bit_cast(u32x4, e);
+}
+
+template <class P>
+__global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
+    using AT = typename P::AT;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int chunk = blockIdx.x % a.nchunks;
+    const int tile = blockIdx.x / a.nchunks;
+    int pi = 0;
+    while (pi + 1 < a.nprob && tile >= a.tile_start[pi + 1]) ++pi;
+    const DWProb& pr = a.p[pi];
+    const int lt = tile - a.tile_start[pi];
+    const int kt = lt / pr.ntiles, nt = lt % pr.ntiles;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int k0 = kt * 64 + wr * 32, n0 = nt * 64 + wc * 32;
+    const size_t m_begin = (size_t)chunk * a.mchunk;
+    const size_t m_end = m_begin + a.mchunk < a.ldm ? m_begin + a.mchunk : a.ldm;
+    if (m_begin >= m_end) return;
+    const AT* XT = (const AT*)pr.XT;
+    const AT* DT = (const AT*)pr.DT;
+    const bool do_extra = pr.extra != EXTRA_NONE && kt == 0 && wr == 0;
+    f32x4 acc[2][2], acce[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        zero_acc(acce[i]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) zero_acc(acc[i][j]);
+    }
+    const int lr = lane & 15, lq = (lane >> 4) * P::EPL;
+    for (size_t m = m_begin; m < m_end; m += P::KG) {
+        const size_t mm = m + lq;
+        u32x4 A0 = load_frag_rows<P>(XT, a.ldm, k0 + lr, pr.Kx, mm);
+        u32x4 A1 = load_frag_rows<P>(XT, a.ldm, k0 + 16 + lr, pr.Kx, mm);
+        u32x4 B0 = load_frag_rows<P>(DT, a.ldm, n0 + lr, pr.N, mm);
+        u32x4 B1 = load_frag_rows<P>(DT, a.ldm, n0 + 16 + lr, pr.N, mm);
+        acc[0][0] = P::mma(A0, B0, acc[0][0]);
+        acc[0][1] = P::mma(A0, B1, acc[0][1]);
+        acc[1][0] = P::mma(A1, B0, acc[1][0]);
+        acc[1][1] = P::mma(A1, B1, acc[1][1]);
+        if (do_extra) {
+            const u32x4 AE = extra_frag<P>(pr.extra, lr, a.seg, mm);
+            acce[0] = P::mma(AE, B0, acce[0]);
+            acce[1] = P::mma(AE, B1, acce[1]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + j * 16 + ccol(lane);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = k0 + i * 16 + crow(lane, r);
+                if (k < pr.Kx && n < pr.N) atomicAdd(pr.G + (size_t)k * pr.N + n, acc[i][j][r]);
+            }
+        }
+    if (do_extra) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + j * 16 + ccol(lane);
+            if (n >= pr.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int q = crow(lane, r);
+                if (pr.extra == EXTRA_ONES) {
+                    if (q == 0) atomicAdd(pr.Gx + n, acce[j][r]);
+                } else {
+                    atomicAdd(pr.Gx + (size_t)q * pr.N + n, acce[j][r]);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// time-MLP backward (mlp_diffusion.py:40-45) from the per-t bucket sums of dh1:
+//   in_b' = sum_q G[q];  dtemb[q] = G[q] . W_in[XD:XD+TD]^T;  then Dense/mish/Dense backward.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void time_bwd_kernel(const float* __restrict__ gseg, const float* __restrict__ prm,
+                                                       float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* dtemb = sm;                  // [KF][TD]
+    float* e = dtemb + KF * TD;         // [KF][TD]
+    float* a1 = e + KF * TD;            // [KF][2TD]
+    float* da1 = a1 + KF * 2 * TD;      // [KF][2TD]
+    const int tid = threadIdx.x;
+    for (int n = tid; n < H; n += 256) {
+        float s = 0.f;
+        for (int q = 0; q < KF; ++q) s += gseg[q * H + n];
+        grad[F.in_b + n] = s;
+    }
+    const int half = TD / 2;
+    const float lnf = logf(10000.f) / (float)(half - 1);
+    for (int i = tid; i < KF * TD; i += 256) {
+        const int q = i / TD, j = i % TD;
+        float s = 0.f;
+        for (int n = 0; n < H; ++n) s += gseg[q * H + n] * prm[F.in_w + (size_t)(XD + j) * H + n];
+        dtemb[i] = s;
+        const float f = expf(-(float)(j % half) * lnf) * (float)q;
+        e[i] = j < half ? sinf(f) : cosf(f);
+    }
+    __syncthreads();
+    for (int i = tid; i < KF * 2 * TD; i += 256) {
+        const int q = i / (2 * TD), h = i % (2 * TD);
+        float s = prm[F.time_b1 + h];
+        for (int k = 0; k < TD; ++k) s += e[q * TD + k] * prm[F.time_w1 + k * 2 * TD + h];
+        a1[i] = s;
+    }
+    __syncthreads();
+    for (int i = tid; i < KF * 2 * TD; i += 256) {
+        const int q = i / (2 * TD), h = i % (2 * TD);
+        float dm = 0.f;
+        for (int j = 0; j < TD; ++j) dm += dtemb[q * TD + j] * prm[F.time_w2 + h * TD + j];
+        da1[i] = dm * mish_gradf(a1[i]);
+    }
+    __syncthreads();
+    for (int i = tid; i < 2 * TD * TD; i += 256) {            // time_w2 [2TD][TD]
+        const int h = i / TD, j = i % TD;
+        float s = 0.f;
+        for (int q = 0; q < KF; ++q) s += mishf(a1[q * 2 * TD + h]) * dtemb[q * TD + j];
+        grad[F.time_w2 + i] = s;
+    }
+    for (int j = tid; j < TD; j += 256) {
+        float s = 0.f;
+        for (int q = 0; q < KF; ++q) s += dtemb[q * TD + j];
+        grad[F.time_b2 + j] = s;
+    }
+    for (int i = tid; i < TD * 2 * TD; i += 256) {            // time_w1 [TD][2TD]
+        const int k = i / (2 * TD), h = i % (2 * TD);
+        float s = 0.f;
+        for (int q = 0; q < KF; ++q) s += e[q * TD + k] * da1[q * 2 * TD + h];
+        grad[F.time_w1 + i] = s;
+    }
+    for (int h = tid; h < 2 * TD; h += 256) {
+        float s = 0.f;
+        for (int q = 0; q < KF; ++q) s += da1[q * 2 * TD + h];
+        grad[F.time_b1 + h] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// minibatch advantage statistics {count, sum, sumsq} (for norm_adv, diffusion_ppo.py:74-75)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict__ adv, FeistelKey fk, int KF, int64_t start,
+                                                        int rows, double* __restrict__ stats) {
+    __shared__ double sh[3][4];
+    double c = 0.0, s = 0.0, s2 = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < rows; i += (int64_t)gridDim.x * 256) {
+        const uint64_t idx = feistel_permute((uint64_t)(start + i), fk);
+        if (idx >= fk.n) continue;
+        const double v = adv[idx / KF];
+        c += 1.0; s += v; s2 += v * v;
+    }
+    c = wave_sumd(c); s = wave_sumd(s); s2 = wave_sumd(s2);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[0][w] = c; sh[1][w] = s; sh[2][w] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(stats + 0, sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3]);
+        atomicAdd(stats + 1, sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3]);
+        atomicAdd(stats + 2, sh[2][0] + sh[2][1] + sh[2][2] + sh[2][3]);
+    }
+}
+
+__global__ void feistel_kernel(int64_t first, int64_t count, FeistelKey fk, int64_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) {
+        const uint64_t v = feistel_permute((uint64_t)(first + i), fk);
+        out[i] = v < fk.n ? (int64_t)v : -1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// AdamW over a flat fp32 buffer
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                                    float* __restrict__ v, int64_t n, float lr, float wd, float b1, float b2,
+                                                    float eps, float alpha, float bc1, float bc2, int mode) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        float pi = p[i], gi = g[i], mi = m[i], vi = v[i];
+        if (mode == DPPO_ADAMW_KERAS) {
+            // Keras 3: decoupled decay first (variable -= variable*wd*lr), then Adam with
+            // m += (g-m)(1-b1); v += (g^2-v)(1-b2); p -= m*alpha/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t)
+            pi -= pi * wd * lr;
+            mi += (gi - mi) * (1.f - b1);
+            vi += (gi * gi - vi) * (1.f - b2);
+            pi -= (mi * alpha) / (sqrtf(vi) + eps);
+        } else {
+            pi *= 1.f - lr * wd;
+            mi = b1 * mi + (1.f - b1) * gi;
+            vi = b2 * vi + (1.f - b2) * gi * gi;
+            pi -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+        }
+        p[i] = pi; m[i] = mi; v[i] = vi;
+    }
+}
+
+extern "C" int dppo_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
+                          float weight_decay, float beta1, float beta2, float eps, int mode, void* stream) {
+    DPPO_CHECK(n >= 0 && step >= 1, "dppo_adamw: n < 0 or step < 1");
+    if (n == 0) return DPPO_OK;
+    DPPO_CHECK(params && grads && m && v, "dppo_adamw: null pointer");
+    DPPO_CHECK(mode == DPPO_ADAMW_KERAS || mode == DPPO_ADAMW_TORCH, "dppo_adamw: bad mode");
+    const double bc1 = 1.0 - pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - pow((double)beta2, (double)step);
+    const float alpha = (float)((double)lr * sqrt(bc2) / bc1);
+    const int64_t blocks64 = (n + 255) / 256;
+    const unsigned blocks = (unsigned)(blocks64 < 4096 ? blocks64 : 4096);
+    hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads, m, v, n, lr,
+                       weight_decay, beta1, beta2, eps, alpha, (float)bc1, (float)bc2, mode);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+extern "C" int dppo_feistel_permute(int64_t first, int64_t count, int64_t n, uint64_t seed, int epoch, int64_t* out,
+                                    void* stream) {
+    DPPO_CHECK(n > 0 && count >= 0 && first >= 0, "dppo_feistel_permute: bad range");
+    if (count == 0) return DPPO_OK;
+    DPPO_CHECK(out, "dppo_feistel_permute: null out");
+    const FeistelKey fk = feistel_key((uint64_t)n, seed, epoch);
+    hipLaunchKernelGGL(feistel_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       first, count, fk, out);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+extern "C" int dppo_ppo_adv_stats(const float* advantages, int64_t total, int K_ft, uint64_t perm_seed, int epoch,
+                                  int64_t start, int rows, double* adv_stats, void* stream) {
+    DPPO_CHECK(advantages && adv_stats && total > 0 && K_ft > 0 && rows >= 0, "dppo_ppo_adv_stats: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    DPPO_HIP(hipMemsetAsync(adv_stats, 0, 3 * sizeof(double), s));
+    if (rows == 0) return DPPO_OK;
+    const FeistelKey fk = feistel_key((uint64_t)total, perm_seed, epoch);
+    const int blocks = dppo_cdiv(rows, 256) < 512 ? dppo_cdiv(rows, 256) : 512;
+    hipLaunchKernelGGL(adv_stats_kernel, dim3(blocks), dim3(256), 0, s, advantages, fk, K_ft, start, rows, adv_stats);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+extern "C" size_t dppo_ppo_workspace_bytes(const dppo_dims* d, int precision, int batch_rows) {
+    Dims D;
+    if (dppo_check_dims(d, &D) || batch_rows < 0) return 0;
+    return make_ppo_workspace(D, precision, batch_rows, nullptr).total;
+}
+
+template <class P>
+static int launch_dw(const DWArgs& a, hipStream_t s) {
+    const int tiles = a.tile_start[a.nprob];
+    const int64_t blocks = (int64_t)tiles * a.nchunks;
+    hipLaunchKernelGGL(dw_kernel<P>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
+                                  const void* packed_ft, const void* packed_critic, const float* actor_params,
+                                  const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
+                                  const float* advantages, const float* returns, int64_t total, uint64_t perm_seed,
+                                  int epoch, int64_t start, int rows, const double* adv_stats,
+                                  void* workspace, float* grads, double* metrics, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    DPPO_CHECK(hp && packed_ft && packed_critic && actor_params && sched && obs && chains && lp_old_mean && advantages &&
+               returns && workspace && grads && metrics, "dppo_ppo_minibatch: null pointer");
+    DPPO_CHECK(total > 0 && total % D.KF == 0, "dppo_ppo_minibatch: total must be a positive multiple of K'");
+    DPPO_CHECK(rows > 0 && start >= 0, "dppo_ppo_minibatch: bad rows/start");
+    DPPO_CHECK(hp->global_rows > 0, "dppo_ppo_minibatch: global_rows must be > 0");
+    DPPO_CHECK(D.KF <= 16, "dppo_ppo_minibatch: ft_denoising_steps > 16 unsupported (bucket sums)");
+    hipStream_t s = (hipStream_t)stream;
+    const PpoWorkspace ws = make_ppo_workspace(D, precision, rows, (uint8_t*)workspace);
+    const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
+    const FlatOffsets FC = make_flat_offsets(D.SD, D.HC, 1, 0);
+    float* ga = grads;
+    float* gc = grads + FA.count;
+    DPPO_HIP(hipMemsetAsync(grads, 0, sizeof(float) * (FA.count + FC.count), s));
+    DPPO_HIP(hipMemsetAsync(metrics, 0, sizeof(double) * 16, s));
+    DPPO_HIP(hipMemsetAsync(ws.gseg, 0, sizeof(float) * 16 * D.H, s));
+    const double* stats = adv_stats;
+    if (!stats) {
+        rc = dppo_ppo_adv_stats(advantages, total, D.KF, perm_seed, epoch, start, rows, ws.stats, stream);
+        if (rc) return rc;
+        stats = ws.stats;
+    }
+    const FeistelKey fk = feistel_key((uint64_t)total, perm_seed, epoch);
+    LossHP lh;
+    lh.gamma_denoising = hp->gamma_denoising; lh.clip_coef = hp->clip_ploss_coef;
+    lh.clip_coef_base = hp->clip_ploss_coef_base; lh.clip_coef_rate = hp->clip_ploss_coef_rate;
+    lh.min_lp_std = hp->min_logprob_std; lh.vf_coef = hp->vf_coef; lh.norm_adv = hp->norm_adv;
+    lh.reward_horizon = hp->reward_horizon;
+    lh.grad_scale = hp->loss_scale / (float)hp->global_rows;
+
+    ActorArgs aa = {};
+    aa.packed = (const uint8_t*)packed_ft;
+    aa.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision);
+    aa.sched = sched; aa.obs = obs; aa.chains = chains;
+    aa.XD = D.XD; aa.SD = D.SD; aa.TD = D.TD; aa.IN = D.IN; aa.H = D.H; aa.KF = D.KF; aa.Da = D.Da;
+    aa.mode = ROWS_TRAIN; aa.nrows = rows; aa.fk = fk; aa.start = start;
+    aa.lp_old = lp_old_mean; aa.adv = advantages; aa.adv_stats = stats; aa.hp = lh; aa.ws = ws; aa.metrics = metrics;
+    rc = launch_actor_rowtile(aa, precision, s);
+    if (rc) return rc;
+
+    CriticArgs ca = {};
+    ca.packed = (const uint8_t*)packed_critic;
+    ca.L = make_mlp_layout(D.SD, D.HC, 1, 0, precision);
+    ca.obs = obs; ca.SD = D.SD; ca.HC = D.HC; ca.KF = D.KF; ca.mode = ROWS_TRAIN; ca.nrows = rows;
+    ca.fk = fk; ca.start = start; ca.returns = returns; ca.hp = lh; ca.ws = ws; ca.metrics = metrics;
+    rc = launch_critic_rowtile(ca, precision, s);
+    if (rc) return rc;
+
+    DWArgs w = {};
+    auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
+        DWProb& p = w.p[w.nprob];
+        p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
+        p.ktiles = dppo_cdiv(Kx, 64); p.ntiles = dppo_cdiv(N, 64);
+        w.tile_start[w.nprob + 1] = w.tile_start[w.nprob] + p.ktiles * p.ntiles;
+        w.nprob++;
+    };
+    add(ws.a0T, D.IN, ws.dh1T, D.H, ga + FA.in_w, EXTRA_ONEHOT, ws.gseg);
+    add(ws.u1T, D.H, ws.dh2T, D.H, ga + FA.l1_w, EXTRA_ONES, ga + FA.l1_b);
+    add(ws.u2T, D.H, ws.dh3T, D.H, ga + FA.l2_w, EXTRA_ONES, ga + FA.l2_b);
+    add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
+    add(ws.csT, D.SD, ws.cdh1T, D.HC, gc + FC.in_w, EXTRA_ONES, gc + FC.in_b);
+    add(ws.cu1T, D.HC, ws.cdh2T, D.HC, gc + FC.l1_w, EXTRA_ONES, gc + FC.l1_b);
+    add(ws.cu2T, D.HC, ws.cdh3T, D.HC, gc + FC.l2_w, EXTRA_ONES, gc + FC.l2_b);
+    add(ws.ch3T, D.HC, ws.cdvT, 1, gc + FC.out_w, EXTRA_ONES, gc + FC.out_b);
+    w.ldm = ws.ldm;
+    w.seg = ws.seg;
+    // m-chunks: about 6 workgroups per CU over the whole grid, chunk a multiple of 64 rows
+    const int tiles = w.tile_start[w.nprob];
+    int nch = dppo_cdiv(256 * 6, tiles);
+    const int max_ch = (int)(ws.ldm / 64);
+    if (nch > max_ch) nch = max_ch;
+    if (nch < 1) nch = 1;
+    w.mchunk = (int)(dppo_cdiv((int)ws.ldm, nch * 64) * 64);
+    w.nchunks = dppo_cdiv((int)ws.ldm, w.mchunk);
+    rc = precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, s) : launch_dw<PolicyF32>(w, s);
+    if (rc) return rc;
+
+    const size_t tsm = sizeof(float) * (size_t)D.KF * (2 * D.TD + 2 * 2 * D.TD);
+    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(256), tsm, s, ws.gseg, actor_params, ga, FA, D.XD, D.TD, D.H, D.KF);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}

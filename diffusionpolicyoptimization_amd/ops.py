@@ -1,0 +1,308 @@
+"""Thin torch-tensor wrappers over the C ABI (include/dppo.h).
+
+Tensors are device tensors owned by the caller; every op is enqueued on the current torch
+stream of the tensor's device. Shapes/dtypes are checked here before any launch so that a bad
+call can never reach a kernel with mismatched extents.
+"""
+import ctypes
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import ptr, stream_handle
+
+
+@dataclass(frozen=True)
+class ModelDims:
+    obs_dim: int = 11
+    action_dim: int = 3
+    horizon_steps: int = 4
+    cond_steps: int = 1
+    time_dim: int = 16
+    actor_hidden: int = 512
+    critic_hidden: int = 256
+    denoising_steps: int = 20
+    ft_denoising_steps: int = 10
+
+    @property
+    def xd(self):
+        return self.horizon_steps * self.action_dim
+
+    @property
+    def sd(self):
+        return self.cond_steps * self.obs_dim
+
+    @property
+    def actor_in(self):
+        return self.xd + self.time_dim + self.sd
+
+    def c(self):
+        return _lib.DppoDims(self.obs_dim, self.action_dim, self.horizon_steps, self.cond_steps, self.time_dim,
+                             self.actor_hidden, self.critic_hidden, self.denoising_steps, self.ft_denoising_steps)
+
+
+def actor_param_spec(d: ModelDims):
+    """Flat fp32 layout of include/dppo.h (Keras kernels [in,out])."""
+    td, h, xd = d.time_dim, d.actor_hidden, d.xd
+    return [("time_w1", (td, 2 * td)), ("time_b1", (2 * td,)), ("time_w2", (2 * td, td)), ("time_b2", (td,)),
+            ("in_w", (d.actor_in, h)), ("in_b", (h,)), ("l1_w", (h, h)), ("l1_b", (h,)),
+            ("l2_w", (h, h)), ("l2_b", (h,)), ("out_w", (h, xd)), ("out_b", (xd,))]
+
+
+def critic_param_spec(d: ModelDims):
+    h = d.critic_hidden
+    return [("in_w", (d.sd, h)), ("in_b", (h,)), ("l1_w", (h, h)), ("l1_b", (h,)),
+            ("l2_w", (h, h)), ("l2_b", (h,)), ("out_w", (h, 1)), ("out_b", (1,))]
+
+
+def spec_count(spec):
+    return int(sum(int(np.prod(s)) for _, s in spec))
+
+
+def flatten_params(spec, params):
+    return np.concatenate([np.asarray(params[n], np.float32).reshape(-1) for n, _ in spec])
+
+
+def unflatten_params(spec, flat):
+    out, o = {}, 0
+    flat = np.asarray(flat)
+    for n, s in spec:
+        k = int(np.prod(s))
+        out[n] = flat[o:o + k].reshape(s)
+        o += k
+    return out
+
+
+def _check(t, shape, dtype, name):
+    if t is None:
+        return
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f"{name}: expected a device tensor")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+
+
+def _prec(precision):
+    return _lib.PRECISION[precision] if isinstance(precision, str) else int(precision)
+
+
+# ------------------------------------------------------------------------------------------------
+# packing
+# ------------------------------------------------------------------------------------------------
+def actor_packed_bytes(d: ModelDims, precision):
+    return int(_lib.query("dppo_actor_packed_bytes", ctypes.byref(d.c()), _prec(precision)))
+
+
+def critic_packed_bytes(d: ModelDims, precision):
+    return int(_lib.query("dppo_critic_packed_bytes", ctypes.byref(d.c()), _prec(precision)))
+
+
+def pack_actor(d: ModelDims, params_flat, precision, out=None):
+    _check(params_flat, (spec_count(actor_param_spec(d)),), torch.float32, "actor params")
+    if out is None:
+        out = torch.empty(actor_packed_bytes(d, precision), dtype=torch.uint8, device=params_flat.device)
+    _lib.call("dppo_pack_actor", ctypes.byref(d.c()), _prec(precision), ptr(params_flat), ptr(out),
+              stream_handle(params_flat.device))
+    return out
+
+
+def pack_critic(d: ModelDims, params_flat, precision, out=None):
+    _check(params_flat, (spec_count(critic_param_spec(d)),), torch.float32, "critic params")
+    if out is None:
+        out = torch.empty(critic_packed_bytes(d, precision), dtype=torch.uint8, device=params_flat.device)
+    _lib.call("dppo_pack_critic", ctypes.byref(d.c()), _prec(precision), ptr(params_flat), ptr(out),
+              stream_handle(params_flat.device))
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# sampler / logprob / critic
+# ------------------------------------------------------------------------------------------------
+def sample(d: ModelDims, precision, packed_base, packed_ft, sched, cond, x_T=None, noise=None, seed=0, call_id=0,
+           env_offset=0, deterministic=False, min_sampling_std=0.1, randn_clip=3.0, final_clip=None,
+           actions=None, chains=None, want_chains=True):
+    E = cond.shape[0]
+    dev = cond.device
+    _check(cond, (E, d.sd), torch.float32, "cond")
+    _check(sched, (d.denoising_steps, _lib.SCHED_COLS), torch.float32, "sched")
+    _check(x_T, (E, d.xd), torch.float32, "x_T")
+    _check(noise, (d.denoising_steps, E, d.xd), torch.float32, "noise")
+    _check(packed_base, (actor_packed_bytes(d, precision),), torch.uint8, "packed_base")
+    _check(packed_ft, (actor_packed_bytes(d, precision),), torch.uint8, "packed_ft")
+    if actions is None:
+        actions = torch.empty(E, d.xd, dtype=torch.float32, device=dev)
+    if chains is None and want_chains:
+        chains = torch.empty(E, d.ft_denoising_steps + 1, d.xd, dtype=torch.float32, device=dev)
+    _check(actions, (E, d.xd), torch.float32, "actions")
+    _check(chains, (E, d.ft_denoising_steps + 1, d.xd), torch.float32, "chains")
+    _lib.call("dppo_sample", ctypes.byref(d.c()), _prec(precision), ptr(packed_base), ptr(packed_ft), ptr(sched),
+              ptr(cond), E, ptr(x_T), ptr(noise), ctypes.c_uint64(seed & (2 ** 64 - 1)), ctypes.c_uint64(call_id),
+              int(env_offset), int(bool(deterministic)), float(min_sampling_std), float(randn_clip),
+              float(final_clip) if final_clip is not None else 0.0, ptr(actions), ptr(chains), stream_handle(dev))
+    return actions, chains
+
+
+def logprob(d: ModelDims, precision, packed_ft, sched, cond, chains, min_logprob_std=0.1, reward_horizon=None,
+            want_elem=True, want_mean=True, lp_elem=None, lp_mean=None):
+    n = cond.shape[0]
+    dev = cond.device
+    kf = d.ft_denoising_steps
+    _check(cond, (n, d.sd), torch.float32, "cond")
+    _check(chains, (n, kf + 1, d.xd), torch.float32, "chains")
+    _check(sched, (d.denoising_steps, _lib.SCHED_COLS), torch.float32, "sched")
+    _check(packed_ft, (actor_packed_bytes(d, precision),), torch.uint8, "packed_ft")
+    if want_elem and lp_elem is None:
+        lp_elem = torch.empty(n * kf, d.xd, dtype=torch.float32, device=dev)
+    if want_mean and lp_mean is None:
+        lp_mean = torch.empty(n, kf, dtype=torch.float32, device=dev)
+    _check(lp_elem, (n * kf, d.xd), torch.float32, "lp_elem")
+    _check(lp_mean, (n, kf), torch.float32, "lp_mean")
+    rh = d.horizon_steps if reward_horizon is None else int(reward_horizon)
+    _lib.call("dppo_logprob", ctypes.byref(d.c()), _prec(precision), ptr(packed_ft), ptr(sched), ptr(cond),
+              ptr(chains), n, float(min_logprob_std), rh, ptr(lp_elem), ptr(lp_mean), stream_handle(dev))
+    return lp_elem, lp_mean
+
+
+def critic_forward(d: ModelDims, precision, packed_critic, cond, values=None):
+    n = cond.shape[0]
+    _check(cond, (n, d.sd), torch.float32, "cond")
+    _check(packed_critic, (critic_packed_bytes(d, precision),), torch.uint8, "packed_critic")
+    if values is None:
+        values = torch.empty(n, dtype=torch.float32, device=cond.device)
+    _check(values, (n,), torch.float32, "values")
+    _lib.call("dppo_critic_forward", ctypes.byref(d.c()), _prec(precision), ptr(packed_critic), ptr(cond), n,
+              ptr(values), stream_handle(cond.device))
+    return values
+
+
+# ------------------------------------------------------------------------------------------------
+# scans
+# ------------------------------------------------------------------------------------------------
+def gae(reward, values, last_values, terminated, gamma=0.99, lam=0.95, reward_scale_const=1.0, adv=None, ret=None):
+    S, E = reward.shape
+    _check(reward, (S, E), torch.float64, "reward")
+    _check(values, (S, E), torch.float32, "values")
+    _check(last_values, (E,), torch.float32, "last_values")
+    _check(terminated, (S, E), torch.uint8, "terminated")
+    if adv is None:
+        adv = torch.empty(S, E, dtype=torch.float32, device=reward.device)
+    if ret is None:
+        ret = torch.empty(S, E, dtype=torch.float32, device=reward.device)
+    _lib.call("dppo_gae", ptr(reward), ptr(values), ptr(last_values), ptr(terminated), S, E, float(gamma), float(lam),
+              float(reward_scale_const), ptr(adv), ptr(ret), stream_handle(reward.device))
+    return adv, ret
+
+
+def reward_scale_workspace(S, E, device):
+    n = int(_lib.query("dppo_reward_scale_workspace_doubles", S, E))
+    return torch.empty(n, dtype=torch.float64, device=device)
+
+
+def reward_scale(reward, first, ret_state, rms_state, workspace=None, gamma=0.99, cliprew=10.0, epsilon=1e-8):
+    """In place: reward [S,E] fp64 is replaced by the scaled reward (RunningRewardScaler.__call__)."""
+    S, E = reward.shape
+    _check(reward, (S, E), torch.float64, "reward")
+    _check(first, (S, E), torch.uint8, "first")
+    _check(ret_state, (E,), torch.float64, "ret_state")
+    _check(rms_state, (3,), torch.float64, "rms_state")
+    if workspace is None:
+        workspace = reward_scale_workspace(S, E, reward.device)
+    _lib.call("dppo_reward_scale", ptr(reward), ptr(first), ptr(ret_state), ptr(rms_state), ptr(workspace), S, E,
+              float(gamma), float(cliprew), float(epsilon), stream_handle(reward.device))
+    return reward
+
+
+def reward_scale_moments(reward, first, ret_state, moments, workspace, gamma=0.99):
+    S, E = reward.shape
+    _lib.call("dppo_reward_scale_moments", ptr(reward), ptr(first), ptr(ret_state), ptr(workspace), ptr(moments), S, E,
+              float(gamma), stream_handle(reward.device))
+    return moments
+
+
+def reward_scale_apply(reward, rms_state, cliprew=10.0, epsilon=1e-8):
+    S, E = reward.shape
+    _lib.call("dppo_reward_scale_apply", ptr(reward), ptr(rms_state), S, E, float(cliprew), float(epsilon),
+              stream_handle(reward.device))
+    return reward
+
+
+# ------------------------------------------------------------------------------------------------
+# update
+# ------------------------------------------------------------------------------------------------
+def feistel_permute(first, count, n, seed, epoch, device):
+    out = torch.empty(count, dtype=torch.int64, device=device)
+    _lib.call("dppo_feistel_permute", int(first), int(count), int(n), ctypes.c_uint64(seed), int(epoch), ptr(out),
+              stream_handle(device))
+    return out
+
+
+def ppo_workspace(d: ModelDims, precision, rows, device):
+    nbytes = int(_lib.query("dppo_ppo_workspace_bytes", ctypes.byref(d.c()), _prec(precision), int(rows)))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+def ppo_adv_stats(advantages, total, kf, perm_seed, epoch, start, rows, out):
+    _lib.call("dppo_ppo_adv_stats", ptr(advantages), int(total), int(kf), ctypes.c_uint64(perm_seed), int(epoch),
+              int(start), int(rows), ptr(out), stream_handle(advantages.device))
+    return out
+
+
+def ppo_hparams(gamma_denoising=0.99, clip_ploss_coef=0.01, clip_ploss_coef_base=0.01, clip_ploss_coef_rate=3.0,
+                min_logprob_std=0.1, vf_coef=0.5, norm_adv=True, reward_horizon=4, loss_scale=1.0, global_rows=1):
+    return _lib.DppoPpoHparams(float(gamma_denoising), float(clip_ploss_coef), float(clip_ploss_coef_base),
+                               float(clip_ploss_coef_rate), float(min_logprob_std), float(vf_coef), int(bool(norm_adv)),
+                               int(reward_horizon), float(loss_scale), int(global_rows))
+
+
+def ppo_minibatch(d: ModelDims, precision, hp, packed_ft, packed_critic, actor_params, sched, obs, chains, lp_old_mean,
+                  advantages, returns, perm_seed, epoch, start, rows, workspace, grads, metrics, adv_stats=None):
+    n = obs.shape[0]
+    kf = d.ft_denoising_steps
+    _check(obs, (n, d.sd), torch.float32, "obs")
+    _check(chains, (n, kf + 1, d.xd), torch.float32, "chains")
+    _check(lp_old_mean, (n, kf), torch.float32, "lp_old_mean")
+    _check(advantages, (n,), torch.float32, "advantages")
+    _check(returns, (n,), torch.float32, "returns")
+    na, nc = spec_count(actor_param_spec(d)), spec_count(critic_param_spec(d))
+    _check(actor_params, (na,), torch.float32, "actor_params")
+    _check(grads, (na + nc,), torch.float32, "grads")
+    _check(metrics, (16,), torch.float64, "metrics")
+    need = int(_lib.query("dppo_ppo_workspace_bytes", ctypes.byref(d.c()), _prec(precision), int(rows)))
+    if workspace.numel() < need:
+        raise ValueError(f"workspace too small: {workspace.numel()} < {need}")
+    _lib.call("dppo_ppo_minibatch", ctypes.byref(d.c()), _prec(precision), ctypes.byref(hp), ptr(packed_ft),
+              ptr(packed_critic), ptr(actor_params), ptr(sched), ptr(obs), ptr(chains), ptr(lp_old_mean),
+              ptr(advantages), ptr(returns), int(n * kf), ctypes.c_uint64(perm_seed), int(epoch), int(start), int(rows),
+              ptr(adv_stats), ptr(workspace), ptr(grads), ptr(metrics), stream_handle(obs.device))
+
+
+def adamw(params, grads, m, v, step, lr, weight_decay=0.004, beta1=0.9, beta2=0.999, eps=1e-7, mode="keras"):
+    n = params.numel()
+    for t, nm in ((grads, "grads"), (m, "m"), (v, "v")):
+        _check(t, (n,), torch.float32, nm)
+    _lib.call("dppo_adamw", ptr(params), ptr(grads), ptr(m), ptr(v), int(n), int(step), float(lr), float(weight_decay),
+              float(beta1), float(beta2), float(eps),
+              _lib.DPPO_ADAMW_KERAS if mode == "keras" else _lib.DPPO_ADAMW_TORCH, stream_handle(params.device))
+
+
+def sched_table(schedule):
+    """[K][8] fp32 table from the fp32 DDPM buffers (see model/diffusion/sampling.py)."""
+    K = len(schedule["betas"])
+    tab = np.zeros((K, _lib.SCHED_COLS), np.float32)
+    tab[:, 0] = schedule["sqrt_recip_alphas_cumprod"]
+    tab[:, 1] = schedule["sqrt_recipm1_alphas_cumprod"]
+    tab[:, 2] = schedule["ddpm_mu_coef1"]
+    tab[:, 3] = schedule["ddpm_mu_coef2"]
+    tab[:, 4] = schedule["ddpm_logvar_clipped"]
+    return tab
+
+
+def adam_alpha(lr, beta1, beta2, step):
+    return lr * math.sqrt(1 - beta2 ** step) / (1 - beta1 ** step)

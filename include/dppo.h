@@ -1,0 +1,167 @@
+/*
+ * dppo.h — C ABI of libdppo_hip.so, the MI355X (gfx950) DPPO fine-tuning hot path.
+ *
+ * The TF reference has no native boundary: its hot path is TF/Keras/TFP ops called from Python.
+ * Each entry point below replaces one reference interface (cited file:line, relative to the
+ * reference repo root); the Python layer diffusionpolicyoptimization_amd/ (same class names and
+ * kwargs as the reference) is the drop-in, and it binds these symbols with ctypes
+ * (diffusionpolicyoptimization_amd/_lib.py). INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - every pointer argument is DEVICE memory owned by the caller unless it says "host";
+ *   - every call is asynchronous on `stream` (a hipStream_t; 0 = null stream) and allocates
+ *     nothing; scratch comes from a caller-owned workspace sized by the *_workspace_bytes query;
+ *   - return 0 on success, a DPPO_E* code otherwise; dppo_last_error() gives the message
+ *     (thread-local); no C++ exception crosses the ABI;
+ *   - precision: DPPO_F32 = f32-input MFMA (exact fp32 products, the parity mode) or
+ *     DPPO_BF16 = bf16 MFMA with fp32 accumulation and an fp32 DDPM/loss epilogue;
+ *   - flat parameter layout (fp32, Keras kernel [in,out] row-major, then bias [out]):
+ *       actor : time_w1[TD,2TD] time_b1[2TD] time_w2[2TD,TD] time_b2[TD]
+ *               in_w[XD+TD+SD, H] in_b[H] l1_w[H,H] l1_b[H] l2_w[H,H] l2_b[H] out_w[H,XD] out_b[XD]
+ *       critic: in_w[SD,HC] in_b[HC] l1_w[HC,HC] l1_b[HC] l2_w[HC,HC] l2_b[HC] out_w[HC,1] out_b[1]
+ *     with XD = horizon*action_dim, SD = cond_steps*obs_dim, TD = time_dim.
+ */
+#ifndef DPPO_H
+#define DPPO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPPO_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define DPPO_API __attribute__((visibility("default")))
+#else
+#define DPPO_API
+#endif
+
+enum { DPPO_OK = 0, DPPO_EINVAL = 1, DPPO_EHIP = 2, DPPO_EUNSUPPORTED = 3 };
+enum { DPPO_F32 = 0, DPPO_BF16 = 1 };
+enum { DPPO_ADAMW_KERAS = 0, DPPO_ADAMW_TORCH = 1 };
+
+/* Model / schedule dimensions (cfg keys of cfg/gym/finetune/hopper-v2/ft_ppo_diffusion_mlp.yaml:18-25,78-110). */
+typedef struct dppo_dims {
+    int32_t obs_dim;          /* Do */
+    int32_t action_dim;       /* Da */
+    int32_t horizon_steps;    /* Ta */
+    int32_t cond_steps;       /* To */
+    int32_t time_dim;         /* TD (16) */
+    int32_t actor_hidden;     /* H  (512), multiple of 128 */
+    int32_t critic_hidden;    /* HC (256), multiple of 128 */
+    int32_t denoising_steps;  /* K  (20) */
+    int32_t ft_denoising_steps; /* K' (10) */
+} dppo_dims;
+
+/* DDPM schedule table, one row per t: {sqrt_recip_ac, sqrt_recipm1_ac, mu_coef1, mu_coef2,
+ * logvar_clipped, 0, 0, 0} fp32 — the buffers of model/diffusion/diffusion.py:57-73. */
+#define DPPO_SCHED_COLS 8
+
+DPPO_API int         dppo_abi_version(void);
+DPPO_API const char* dppo_last_error(void);
+
+/* ---- parameter packing (replaces Keras variable storage; model/common/mlp.py:95-206) ---- */
+DPPO_API size_t dppo_actor_param_count(const dppo_dims* d);
+DPPO_API size_t dppo_critic_param_count(const dppo_dims* d);
+/* bytes of the packed (MFMA fragment-ordered) device image of one actor / critic */
+DPPO_API size_t dppo_actor_packed_bytes(const dppo_dims* d, int precision);
+DPPO_API size_t dppo_critic_packed_bytes(const dppo_dims* d, int precision);
+/* params: flat fp32 (layout above) -> packed image (forward + transposed fragments) */
+DPPO_API int dppo_pack_actor(const dppo_dims* d, int precision, const float* params, void* packed, void* stream);
+DPPO_API int dppo_pack_critic(const dppo_dims* d, int precision, const float* params, void* packed, void* stream);
+
+/* ---- a9: diffusion-policy action sampler, VPGDiffusion.call (model/diffusion/diffusion_vpg.py:250-339) ----
+ * All K DDPM steps for n_envs rows in ONE launch: DiffusionMLP forward on MFMA + fused DDPM
+ * reparameterisation epilogue (diffusion_vpg.py:152-245, 301-320).
+ *   cond     [n_envs, To*Do]
+ *   x_T      [n_envs, Ta*Da] or NULL -> in-kernel Philox (seed, call_id) stream
+ *   noise    [K, n_envs, Ta*Da] raw N(0,1) draws for loop index i (t = K-1-i), or NULL -> Philox
+ *   env_offset: global row index of row 0 (Philox counter; multi-GPU shards stay distinct)
+ *   final_clip <= 0 means None (cfg default)
+ *   actions  [n_envs, Ta*Da]                 (Sample.trajectories)
+ *   chains   [n_envs, K'+1, Ta*Da] or NULL   (Sample.chains)                                 */
+DPPO_API int dppo_sample(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
+                const float* sched, const float* cond, int n_envs, const float* x_T, const float* noise,
+                uint64_t seed, uint64_t call_id, int env_offset, int deterministic,
+                float min_sampling_std, float randn_clip, float final_clip,
+                float* actions, float* chains, void* stream);
+
+/* ---- a10: VPGDiffusion.get_logprobs (diffusion_vpg.py:343-425) + the clip/mean of c_loss
+ * (diffusion_ppo.py:50-59) for the old-logprob pass (agent/finetune/train_ppo_diffusion_agent.py:214-229).
+ *   cond [n, To*Do], chains [n, K'+1, Ta*Da]
+ *   lp_elem [n*K', Ta*Da] or NULL (row = sample*K' + j, t = K'-1-j)
+ *   lp_mean [n, K'] or NULL: mean over the first reward_horizon Ta rows of clip(lp, -5, 2)   */
+DPPO_API int dppo_logprob(const dppo_dims* d, int precision, const void* packed_ft, const float* sched,
+                 const float* cond, const float* chains, int n, float min_logprob_std, int reward_horizon,
+                 float* lp_elem, float* lp_mean, void* stream);
+
+/* ---- a6: CriticObs forward (model/common/critic.py:40-54): values [n] ---- */
+DPPO_API int dppo_critic_forward(const dppo_dims* d, int precision, const void* packed_critic, const float* cond,
+                        int n, float* values, void* stream);
+
+/* ---- a18: RunningRewardScaler.__call__ (util/reward_scaling.py:60-87), in place on device.
+ *   reward [S, E] (time-major, fp64), first [S, E] (u8); ret_state [E] fp64 carried across calls;
+ *   rms_state [3] fp64 {mean, var, count} (init {0, 1, 1e-4}); reward overwritten with the scaled value;
+ *   workspace: dppo_reward_scale_workspace_doubles(S, E) fp64 */
+DPPO_API size_t dppo_reward_scale_workspace_doubles(int S, int E);
+DPPO_API int dppo_reward_scale(double* reward, const uint8_t* first, double* ret_state, double* rms_state, double* workspace,
+                      int S, int E, double gamma, double cliprew, double epsilon, void* stream);
+/* same, split for multi-GPU: pass 1 (returns local moments {n, mean, M2} in moments[3]) ... */
+DPPO_API int dppo_reward_scale_moments(const double* reward, const uint8_t* first, double* ret_state, double* workspace,
+                              double* moments, int S, int E, double gamma, void* stream);
+/* ... caller all-reduces/merges moments into rms_state, then pass 2 */
+DPPO_API int dppo_reward_scale_apply(double* reward, const double* rms_state, int S, int E, double cliprew,
+                            double epsilon, void* stream);
+
+/* ---- a19: GAE (train_ppo_diffusion_agent.py:239-263). reward fp64 [S,E], values fp32 [S,E],
+ * last_values fp32 [E], terminated u8 [S,E] -> advantages, returns fp32 [S,E] */
+DPPO_API int dppo_gae(const double* reward, const float* values, const float* last_values, const uint8_t* terminated,
+             int S, int E, double gamma, double lam, double reward_scale_const,
+             float* advantages, float* returns, void* stream);
+
+/* ---- a12/a13/a20: one PPO minibatch: gather by permutation, PPODiffusion.c_loss forward + gradient
+ * of pg_loss + vf_coef*v_loss w.r.t. actor_ft and critic (diffusion_ppo.py:32-132,
+ * train_ppo_diffusion_agent.py:287-346).
+ * Rollout buffers (sample index n = step*E + env, total = S*E*K'):
+ *   obs [S*E, To*Do], chains [S*E, K'+1, Ta*Da], lp_old_mean [S*E, K'] (from dppo_logprob),
+ *   advantages / returns [S*E] fp32.
+ * Minibatch rows: perm(start .. start+rows-1) with perm = Feistel bijection of [0,total) keyed
+ * by (perm_seed, epoch), unravelled to (n, j) = (idx / K', idx % K') (tf.unravel_index).
+ * grads [actor_count + critic_count] fp32 are OVERWRITTEN (actor first). metrics (device, fp64[16]):
+ *   {pg_loss, v_loss, approx_kl, clipfrac, ratio_mean, loss, adv_mean, adv_std, ...}.
+ * adv_stats: fp64[3] {count, sum, sumsq} of the minibatch advantages, or NULL to compute locally;
+ *   a multi-GPU caller computes them with dppo_ppo_adv_stats + all-reduce first. */
+typedef struct dppo_ppo_hparams {
+    float gamma_denoising, clip_ploss_coef, clip_ploss_coef_base, clip_ploss_coef_rate;
+    float min_logprob_std, vf_coef;
+    int32_t norm_adv, reward_horizon;
+    float loss_scale;       /* multiplies 1/b (= 1/world_size for a DP all-reduce-sum) */
+    int32_t global_rows;    /* b used in the 1/b means (rows over all ranks) */
+} dppo_ppo_hparams;
+
+DPPO_API size_t dppo_ppo_workspace_bytes(const dppo_dims* d, int precision, int batch_rows);
+DPPO_API int dppo_ppo_adv_stats(const float* advantages, int64_t total, int K_ft, uint64_t perm_seed, int epoch,
+                       int64_t start, int rows, double* adv_stats, void* stream);
+DPPO_API int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
+                       const void* packed_ft, const void* packed_critic, const float* actor_params,
+                       const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
+                       const float* advantages, const float* returns, int64_t total, uint64_t perm_seed,
+                       int epoch, int64_t start, int rows, const double* adv_stats,
+                       void* workspace, float* grads, double* metrics, void* stream);
+
+/* Feistel permutation used above, exposed for tests: out[i] = perm(first + i), i < count. */
+DPPO_API int dppo_feistel_permute(int64_t first, int64_t count, int64_t n, uint64_t seed, int epoch, int64_t* out,
+                         void* stream);
+
+/* ---- a14: optimiser step over a flat fp32 buffer (Keras 3 AdamW semantics by default;
+ * train_ppo_agent.py:45-49). step is 1-based. ---- */
+DPPO_API int dppo_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
+               float weight_decay, float beta1, float beta2, float eps, int mode, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPPO_H */

@@ -1,0 +1,274 @@
+"""GPU parity: every HIP entry point vs the float64 oracle on the same seeded inputs.
+
+Tolerances: fp32 (f32-input MFMA) mode is checked tightly; bf16 mode (bf16 operands, fp32
+accumulate/epilogue) against a stated looser bound. Integer work (Feistel permutation) is bit-exact.
+"""
+import numpy as np
+import pytest
+
+from oracle import dppo_oracle as O
+from oracle import philox as PX
+from tests.helpers import HOPPER, WALKER, make_models, to_f64
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(dims, cuda, seed=0):
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.model.diffusion.sampling import ddpm_buffers
+    d = ops.ModelDims(**dims)
+    base, ft, critic = make_models(seed, dims)
+    sched = ddpm_buffers(d.denoising_steps)
+    tab = torch.tensor(ops.sched_table(sched), device=cuda)
+    fa = lambda p: torch.tensor(ops.flatten_params(ops.actor_param_spec(d), p), device=cuda)
+    fc = lambda p: torch.tensor(ops.flatten_params(ops.critic_param_spec(d), p), device=cuda)
+    return d, base, ft, critic, sched, tab, fa(base), fa(ft), fc(critic)
+
+
+def _rnd(precision):
+    return O.round_bf16 if precision == "bf16" else None
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-4), ("bf16", 2e-3)])
+@pytest.mark.parametrize("dims", [HOPPER, WALKER], ids=["hopper", "walker"])
+def test_sampler_injected_noise(cuda, precision, tol, dims):
+    """fp32: vs the exact f64 oracle. bf16: vs the oracle rounding operands to bf16 at the
+    kernel's rounding points (fp32 accumulation order and rare rounding-boundary flips remain)."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(dims, cuda)
+    E = 37  # ragged: not a multiple of the 16-row tile
+    rng = np.random.default_rng(1)
+    state = rng.uniform(-1, 1, (E, d.cond_steps, d.obs_dim)).astype(np.float32)
+    xT = rng.standard_normal((E, d.horizon_steps, d.action_dim)).astype(np.float32)
+    z = rng.standard_normal((d.denoising_steps, E, d.horizon_steps, d.action_dim)).astype(np.float32)
+    ref_a, ref_c = O.sample(to_f64(base), to_f64(ft), sched, state.astype(np.float64), xT, z, d.ft_denoising_steps,
+                            rnd=_rnd(precision))
+    packb, packf = ops.pack_actor(d, pb, precision), ops.pack_actor(d, pf, precision)
+    act, ch = ops.sample(d, precision, packb, packf, tab, torch.tensor(state.reshape(E, -1), device=cuda),
+                         x_T=torch.tensor(xT.reshape(E, -1), device=cuda),
+                         noise=torch.tensor(z.reshape(d.denoising_steps, E, -1), device=cuda))
+    torch.cuda.synchronize()
+    act = act.cpu().numpy().reshape(ref_a.shape)
+    ch = ch.cpu().numpy().reshape(ref_c.shape)
+    err_a = np.abs(act - ref_a).max()
+    err_c = np.abs(ch - ref_c).max()
+    if precision == "fp32":
+        assert err_a < tol and err_c < tol, (err_a, err_c)
+    else:
+        # the t=19 x0 reconstruction amplifies eps differences by 406 before its clip, so a rare
+        # bf16 rounding-boundary flip can move one element; bound the 99th percentile tightly
+        q99 = np.quantile(np.abs(act - ref_a), 0.99)
+        assert q99 < tol and np.abs(ch - ref_c).mean() < tol, (q99, err_a, err_c)
+
+
+def test_sampler_philox_stream(cuda):
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    E, seed, call = 19, 1234567890123, 7
+    rng = np.random.default_rng(2)
+    state = rng.uniform(-1, 1, (E, 1, d.obs_dim)).astype(np.float32)
+    xT = PX.sampler_normals(seed, call, 0, E, d.xd, d.denoising_steps).reshape(E, d.horizon_steps, d.action_dim)
+    z = np.stack([PX.sampler_normals(seed, call, 0, E, d.xd, i) for i in range(d.denoising_steps)])
+    z = z.reshape(d.denoising_steps, E, d.horizon_steps, d.action_dim)
+    ref_a, ref_c = O.sample(to_f64(base), to_f64(ft), sched, state.astype(np.float64), xT, z, d.ft_denoising_steps)
+    packb, packf = ops.pack_actor(d, pb, "fp32"), ops.pack_actor(d, pf, "fp32")
+    act, ch = ops.sample(d, "fp32", packb, packf, tab, torch.tensor(state.reshape(E, -1), device=cuda),
+                         seed=seed, call_id=call)
+    torch.cuda.synchronize()
+    assert np.abs(act.cpu().numpy().reshape(ref_a.shape) - ref_a).max() < 1e-3
+
+
+def test_sampler_deterministic_and_empty(cuda):
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    E = 16
+    rng = np.random.default_rng(3)
+    state = rng.uniform(-1, 1, (E, 1, d.obs_dim)).astype(np.float32)
+    xT = rng.standard_normal((E, 4, 3)).astype(np.float32)
+    z = rng.standard_normal((20, E, 4, 3)).astype(np.float32)
+    ref_a, _ = O.sample(to_f64(base), to_f64(ft), sched, state.astype(np.float64), xT, z, 10, deterministic=True)
+    packb, packf = ops.pack_actor(d, pb, "fp32"), ops.pack_actor(d, pf, "fp32")
+    act, _ = ops.sample(d, "fp32", packb, packf, tab, torch.tensor(state.reshape(E, -1), device=cuda),
+                        x_T=torch.tensor(xT.reshape(E, -1), device=cuda),
+                        noise=torch.tensor(z.reshape(20, E, -1), device=cuda), deterministic=True)
+    torch.cuda.synchronize()
+    assert np.abs(act.cpu().numpy().reshape(ref_a.shape) - ref_a).max() < 2e-4
+    # E = 0 is a no-op
+    ops.sample(d, "fp32", packb, packf, tab, torch.zeros(0, d.sd, device=cuda))
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 2e-3)])
+def test_logprob(cuda, precision, tol):
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    n = 45
+    rng = np.random.default_rng(4)
+    state = rng.uniform(-1, 1, (n, 1, d.obs_dim)).astype(np.float32)
+    chains = (rng.standard_normal((n, d.ft_denoising_steps + 1, 4, 3)) * 0.5).astype(np.float32)
+    ref = O.get_logprobs(to_f64(ft), sched, state.astype(np.float64), chains.astype(np.float64), d.ft_denoising_steps,
+                         rnd=_rnd(precision))
+    packf = ops.pack_actor(d, pf, precision)
+    lpe, lpm = ops.logprob(d, precision, packf, tab, torch.tensor(state.reshape(n, -1), device=cuda),
+                           torch.tensor(chains.reshape(n, d.ft_denoising_steps + 1, -1), device=cuda))
+    torch.cuda.synchronize()
+    lpe = lpe.cpu().numpy().reshape(ref.shape)
+    ref_mean = np.clip(ref, -5, 2).mean(axis=(1, 2)).reshape(n, d.ft_denoising_steps)
+    rel = np.abs(lpe - ref) / (1 + np.abs(ref))
+    assert np.quantile(rel, 0.99) < tol, np.quantile(rel, 0.99)
+    assert np.abs(lpm.cpu().numpy() - ref_mean).max() < tol * 10
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("bf16", 1e-3)])
+def test_critic_forward(cuda, precision, tol):
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    n = 77
+    state = np.random.default_rng(5).uniform(-1, 1, (n, 1, d.obs_dim)).astype(np.float32)
+    ref, _ = O.critic_forward(to_f64(critic), state.astype(np.float64), rnd=_rnd(precision))
+    v = ops.critic_forward(d, precision, ops.pack_critic(d, pc, precision),
+                           torch.tensor(state.reshape(n, -1), device=cuda))
+    torch.cuda.synchronize()
+    assert np.abs(v.cpu().numpy() - ref[:, 0]).max() < tol * (1 + np.abs(ref).max())
+
+
+@pytest.mark.parametrize("S,E", [(50, 4), (500, 64), (7, 3), (1, 5)])
+def test_gae(cuda, S, E):
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    rng = np.random.default_rng(S * 100 + E)
+    r = rng.normal(size=(S, E))
+    v = rng.normal(size=(S, E)).astype(np.float32)
+    lv = rng.normal(size=E).astype(np.float32)
+    term = (rng.uniform(size=(S, E)) < 0.05).astype(np.uint8)
+    ref_a, ref_r = O.gae(r, v.astype(np.float64), lv.astype(np.float64), term.astype(np.float64))
+    a, ret = ops.gae(torch.tensor(r, device=cuda), torch.tensor(v, device=cuda), torch.tensor(lv, device=cuda),
+                     torch.tensor(term, device=cuda))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(a.cpu().numpy(), ref_a, rtol=1e-6, atol=1e-5)
+    np.testing.assert_allclose(ret.cpu().numpy(), ref_r, rtol=1e-6, atol=1e-5)
+
+
+def test_reward_scale_multi_call(cuda):
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    S, E = 50, 6
+    rng = np.random.default_rng(9)
+    orc = O.RunningRewardScalerOracle(E)
+    ret_state = torch.zeros(E, dtype=torch.float64, device=cuda)
+    rms = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=cuda)
+    for it in range(3):
+        r = rng.normal(2.0, 3.0, size=(S, E))
+        first = (rng.uniform(size=(S, E)) < 0.04).astype(np.uint8)
+        ref = orc(r.T, first.T.astype(np.float64)).T
+        rt = torch.tensor(r, device=cuda)
+        ops.reward_scale(rt, torch.tensor(first, device=cuda), ret_state, rms)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(rt.cpu().numpy(), ref, rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(rms.cpu().numpy(), [orc.mean, orc.var, orc.count], rtol=1e-10)
+
+
+def test_feistel_bit_exact(cuda):
+    from diffusionpolicyoptimization_amd import ops
+    for n, seed, ep in [(320000, 42, 0), (1000, 7, 3), (13, 1, 1), (1, 5, 0)]:
+        got = ops.feistel_permute(0, n, n, seed, ep, cuda).cpu().numpy()
+        ref = PX.feistel_permute(np.arange(n), n, seed, ep)
+        assert np.array_equal(got, ref)
+        assert np.array_equal(np.sort(got), np.arange(n))
+
+
+@pytest.mark.parametrize("mode", ["keras", "torch"])
+def test_adamw(cuda, mode):
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    rng = np.random.default_rng(11)
+    n = 100003
+    p = rng.normal(size=n).astype(np.float32)
+    m = np.zeros(n); v = np.zeros(n)
+    P, M, V = (torch.tensor(x, dtype=torch.float32, device=cuda) for x in (p, m, v))
+    ref = p.astype(np.float64)
+    for step in range(1, 4):
+        g = rng.normal(size=n).astype(np.float32)
+        if mode == "keras":
+            ref, m, v = O.keras_adamw_step(ref, g, m, v, step, lr=1e-3, wd=0.004)
+            ops.adamw(P, torch.tensor(g, device=cuda), M, V, step, 1e-3, 0.004, 0.9, 0.999, 1e-7, "keras")
+        else:
+            ref, m, v = O.torch_adamw_step(ref, g, m, v, step, lr=1e-3, wd=0.01)
+            ops.adamw(P, torch.tensor(g, device=cuda), M, V, step, 1e-3, 0.01, 0.9, 0.999, 1e-8, "torch")
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(P.cpu().numpy(), ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("precision,case,rtol", [("fp32", "perturbed", 2e-3), ("fp32", "ratio1", 2e-3),
+                                                  ("bf16", "ratio1", 1e-2), ("bf16", "perturbed", 2e-2)])
+def test_ppo_minibatch_grads(cuda, precision, case, rtol):
+    """c_loss forward metrics and gradients of pg_loss + 0.5 v_loss vs the oracle.
+
+    'perturbed': old logprobs = current ones + noise, so ~60% of rows sit on a PPO clip branch;
+    exercised in fp32 only, since bf16 rounding flips those discrete branches (a bf16-rounded
+    oracle itself moves 10-29% from the f64 one there). 'ratio1': old logprobs are the policy's
+    own (the first-epoch situation: ratio == 1, no clip). bf16 is compared against the oracle that
+    rounds operands to bf16 at the kernels' rounding points (plain f64 differs by 10-29% here
+    because these minibatch sums cancel ~12x and clip branches flip under rounding)."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    dims = HOPPER
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(dims, cuda)
+    rng = np.random.default_rng(12)
+    N = 40                                  # samples (steps*envs)
+    kf = d.ft_denoising_steps
+    total = N * kf
+    obs = rng.uniform(-1, 1, (N, d.sd)).astype(np.float32)
+    chains = (rng.standard_normal((N, kf + 1, d.xd)) * 0.5).astype(np.float32)
+    adv = rng.normal(size=N).astype(np.float32)
+    ret = rng.normal(size=N).astype(np.float32)
+    T = lambda x: torch.tensor(x, device=cuda)
+    packf = ops.pack_actor(d, pf, precision)
+    lp_ref = O.get_logprobs(to_f64(ft), sched, obs.reshape(N, 1, -1).astype(np.float64),
+                            chains.reshape(N, kf + 1, 4, 3).astype(np.float64), kf, rnd=_rnd(precision))
+    lp_ref_mean = np.clip(lp_ref, -5, 2).mean(axis=(1, 2)).reshape(N, kf)
+    if case == "perturbed":
+        lp_old = (lp_ref_mean + rng.normal(0, 0.02, (N, kf))).astype(np.float32)
+        lp_old_gpu = lp_old
+        lp_old_ref = lp_old.astype(np.float64)
+    else:
+        _, lpm = ops.logprob(d, precision, packf, tab, T(obs), T(chains), want_elem=False)
+        lp_old_gpu = lpm.cpu().numpy()
+        lp_old_ref = lp_ref_mean
+    seed, epoch, start, rows = 99, 1, 37, 150
+    perm = PX.feistel_permute(np.arange(start, start + rows), total, seed, epoch)
+    bi, di = perm // kf, perm % kf
+    metrics_ref, ga_ref, gc_ref = O.c_loss(
+        to_f64(ft), to_f64(critic), sched, obs[bi].reshape(rows, 1, -1).astype(np.float64),
+        chains[bi, di].reshape(rows, 4, 3).astype(np.float64), chains[bi, di + 1].reshape(rows, 4, 3).astype(np.float64),
+        di, ret[bi].astype(np.float64), None, adv[bi].astype(np.float64), lp_old_ref[bi, di], kf,
+        rnd=_rnd(precision))
+    na = ops.spec_count(ops.actor_param_spec(d))
+    nc = ops.spec_count(ops.critic_param_spec(d))
+    grads = torch.zeros(na + nc, dtype=torch.float32, device=cuda)
+    metrics = torch.zeros(16, dtype=torch.float64, device=cuda)
+    ws = ops.ppo_workspace(d, precision, rows, cuda)
+    hp = ops.ppo_hparams(global_rows=rows)
+    ops.ppo_minibatch(d, precision, hp, packf, ops.pack_critic(d, pc, precision), pf, tab,
+                      T(obs), T(chains), T(lp_old_gpu), T(adv), T(ret), seed, epoch, start, rows, ws, grads, metrics)
+    torch.cuda.synchronize()
+    m = metrics.cpu().numpy() / rows
+    assert abs(m[0] - metrics_ref["pg_loss"]) < rtol * (abs(metrics_ref["pg_loss"]) + 1e-2)
+    assert abs(m[1] - metrics_ref["v_loss"]) < rtol * (abs(metrics_ref["v_loss"]) + 1e-2)
+    assert abs(m[2] - metrics_ref["approx_kl"]) < rtol * 10 * (abs(metrics_ref["approx_kl"]) + 1e-4)
+    assert abs(m[3] - metrics_ref["clipfrac"]) <= (0.0 if case == "ratio1" else 0.02)
+    g = grads.cpu().numpy()
+    ga = ops.unflatten_params(ops.actor_param_spec(d), g[:na])
+    gc = ops.unflatten_params(ops.critic_param_spec(d), g[na:])
+    errs = {}
+    for name, ref in list(ga_ref.items()):
+        errs[name] = np.abs(ga[name] - ref).max() / (np.abs(ref).max() + 1e-12)
+    for name, ref in gc_ref.items():
+        errs["critic." + name] = np.abs(gc[name] - ref).max() / (np.abs(ref).max() + 1e-12)
+    bad = {k: float(v) for k, v in errs.items() if not v < rtol}
+    assert not bad, (bad, {k: float(v) for k, v in errs.items()})
