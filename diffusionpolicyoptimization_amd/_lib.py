@@ -59,9 +59,9 @@ _SIGNATURES = {
     "dppo_reward_scale_apply": (_I, [_P, _P, _I, _I, _D, _D, _P]),
     "dppo_gae": (_I, [_P, _P, _P, _P, _I, _I, _D, _D, _D, _P, _P, _P]),
     "dppo_ppo_workspace_bytes": (_SZ, [_DIMS, _I, _I]),
-    "dppo_ppo_adv_stats": (_I, [_P, _I64, _I, _U64, _I, _I64, _I, _P, _P]),
+    "dppo_ppo_adv_stats": (_I, [_P, _I64, _I, _U64, _I, _I64, _I, _P, _P, _P]),
     "dppo_ppo_minibatch": (_I, [_DIMS, _I, ctypes.POINTER(DppoPpoHparams), _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                               _I64, _U64, _I, _I64, _I, _P, _P, _P, _P, _P]),
+                               _I64, _U64, _I, _I64, _I, _P, _P, _P, _P, _P, _P]),
     "dppo_feistel_permute": (_I, [_I64, _I64, _I64, _U64, _I, _P, _P]),
     "dppo_adamw": (_I, [_P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P]),
 }

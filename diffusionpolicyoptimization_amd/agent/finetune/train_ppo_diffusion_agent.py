@@ -1,0 +1,278 @@
+"""TrainPPODiffusionAgent (reference agent/finetune/train_ppo_diffusion_agent.py:22-468) on MI355X.
+
+One iteration = rollout + (train iterations only) value/log-prob pass, reward scaling, GAE and
+the PPO epochs. Differences from the reference are only where data lives and what runs it:
+  * rollout buffers (obs [S,E,SD], chains [S,E,K'+1,XD]) stay in HBM; per env step the host
+    moves only obs (H2D, pinned) and actions (D2H, pinned); chains never leave the device;
+  * sampler / critic / log-prob / reward scaler / GAE / PPO loss+grad / AdamW are HIP kernels;
+  * data parallel: each rank owns n_envs/world envs, draws its share of every minibatch from its
+    own rollout, and the gradient, the minibatch advantage moments, the reward-RMS moments and
+    the metrics are summed with torch.distributed (RCCL) so all replicas take identical steps.
+Semantics kept on purpose: eval at itr % val_freq == 0 with env reset only
+then (4), population-std advantage normalisation per minibatch (3), one optimiser (2)."""
+import logging
+import math
+import os
+import pickle
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ... import ops
+from ...util.timer import Timer
+from .train_ppo_agent import TrainPPOAgent
+
+log = logging.getLogger(__name__)
+
+
+class TrainPPODiffusionAgent(TrainPPOAgent):
+    def __init__(self, cfg):
+        super().__init__(cfg)
+        self.reward_horizon = cfg.get("reward_horizon", self.act_steps)
+        self.learn_eta = self.model.learn_eta
+        self.perm_seed = int(cfg.train.get("perm_seed", self.seed * 1_000_003 + 17)) + 7919 * self.rank
+        self.timing = {"rollout_s": 0.0, "update_s": 0.0, "n_updates": 0, "env_steps": 0, "iters": 0}
+        self.sampler_events = None    # optional list of (start, end) torch.cuda.Event pairs
+        self.update_events = None
+        self._alloc_buffers()
+        self.done_venv = np.zeros(self.n_envs, dtype=bool)
+        self.last_itr_eval = False
+        self.cnt_train_step = 0
+        self.run_results = []
+        self.prev_obs_venv = None
+        self.last_info = {}
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc_buffers(self):
+        S, E, d = self.n_steps, self.n_envs, self.model.dims
+        dev = self.device
+        self.obs_traj = torch.empty(S, E, d.sd, dtype=torch.float32, device=dev)
+        self.chains_traj = torch.empty(S, E, d.ft_denoising_steps + 1, d.xd, dtype=torch.float32, device=dev)
+        self.act_dev = torch.empty(E, d.xd, dtype=torch.float32, device=dev)
+        self.obs_pin = torch.empty(E, self.n_cond_step, self.obs_dim, dtype=torch.float32).pin_memory()
+        self.act_pin = torch.empty(E, d.xd, dtype=torch.float32).pin_memory()
+        self.reward_pin = torch.empty(S, E, dtype=torch.float64).pin_memory()
+        self.term_pin = torch.empty(S, E, dtype=torch.uint8).pin_memory()
+        self.firsts = np.zeros((S + 1, E))
+        self.reward_dev = torch.empty(S, E, dtype=torch.float64, device=dev)
+        self.first_dev = torch.empty(S, E, dtype=torch.uint8, device=dev)
+        self.term_dev = torch.empty(S, E, dtype=torch.uint8, device=dev)
+        self.values = torch.empty(S * E, dtype=torch.float32, device=dev)
+        self.last_values = torch.empty(E, dtype=torch.float32, device=dev)
+        self.lp_old = torch.empty(S * E, d.ft_denoising_steps, dtype=torch.float32, device=dev)
+        self.adv = torch.empty(S, E, dtype=torch.float32, device=dev)
+        self.ret = torch.empty(S, E, dtype=torch.float32, device=dev)
+        self.adv_stats = torch.zeros(3, dtype=torch.float64, device=dev)
+
+    def _allreduce(self, t):
+        if self.world_size > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
+
+    # ------------------------------------------------------------------ rollout (agent :58-141)
+    def rollout(self, eval_mode):
+        S, E = self.n_steps, self.n_envs
+        if self.reset_at_iteration or eval_mode or self.last_itr_eval or self.prev_obs_venv is None:
+            obs = self.reset_env_all()
+            self.obs_pin.numpy()[:] = obs["state"]
+            self.firsts[0] = 1
+        else:
+            self.firsts[0] = self.done_venv  # envs that finished were already reset in-wrapper
+        self.last_itr_eval = eval_mode
+        obs_np = self.obs_pin.numpy()
+        act_np = self.act_pin.numpy().reshape(E, self.horizon_steps, self.action_dim)
+        stream = torch.cuda.current_stream(self.device)
+        rew_np, term_np = self.reward_pin.numpy(), self.term_pin.numpy()
+        for step in range(S):
+            self.obs_traj[step].copy_(self.obs_pin.view(E, -1), non_blocking=True)          # H2D obs
+            if self.sampler_events is not None:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record(stream)
+            self.model(self.obs_traj[step], deterministic=eval_mode, return_chain=True,
+                       actions_out=self.act_dev, chains_out=self.chains_traj[step])
+            if self.sampler_events is not None:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record(stream)
+                self.sampler_events.append((ev0, ev1))
+            self.act_pin.copy_(self.act_dev, non_blocking=True)                                 # D2H actions
+            stream.synchronize()
+            _, reward, terminated, truncated, _ = self.venv.step(act_np[:, :self.act_steps], obs_out=obs_np)
+            done = terminated | truncated
+            rew_np[step] = reward
+            term_np[step] = terminated
+            self.firsts[step + 1] = done
+            self.done_venv = done
+            if not eval_mode:
+                self.cnt_train_step += self.n_envs_global * self.act_steps
+        self.prev_obs_venv = {"state": obs_np}
+        return self.episode_stats()
+
+    def episode_stats(self):
+        """agent :144-183; sums over ranks so every rank logs the global statistics."""
+        firsts, rew = self.firsts, self.reward_pin.numpy()
+        n_ep, tot, best, succ = 0, 0.0, 0.0, 0.0
+        for e in range(self.n_envs):
+            idx = np.nonzero(firsts[:, e] == 1)[0]
+            for i in range(len(idx) - 1):
+                s, en = idx[i], idx[i + 1]
+                if en - s > 1:
+                    r = rew[s:en, e]
+                    n_ep += 1
+                    tot += r.sum()
+                    b = r.max() / self.act_steps
+                    best += b
+                    succ += float(b >= self.best_reward_threshold_for_success)
+        if self.world_size > 1:
+            t = torch.tensor([n_ep, tot, best, succ], dtype=torch.float64, device=self.device)
+            self._allreduce(t)
+            n_ep, tot, best, succ = t.tolist()
+        if n_ep == 0:
+            return dict(num_episode_finished=0, avg_episode_reward=0.0, avg_best_reward=0.0, success_rate=0.0)
+        return dict(num_episode_finished=int(n_ep), avg_episode_reward=tot / n_ep, avg_best_reward=best / n_ep,
+                    success_rate=succ / n_ep)
+
+    # ------------------------------------------------------------------ update (agent :186-377)
+    def update(self):
+        S, E, m = self.n_steps, self.n_envs, self.model
+        kf = m.ft_denoising_steps
+        N = S * E
+        obs_flat = self.obs_traj.view(N, -1)
+        chains_flat = self.chains_traj.view(N, kf + 1, -1)
+        # values and old log-probs (:191-229) — one fused pass each, no num_split needed
+        ops.critic_forward(m.dims, m.precision, m.packed_critic, obs_flat, values=self.values)
+        ops.logprob(m.dims, m.precision, m.packed_ft, m.sched, obs_flat, chains_flat,
+                    min_logprob_std=m.min_logprob_denoising_std, reward_horizon=self.reward_horizon,
+                    want_elem=False, lp_mean=self.lp_old)
+        self.reward_dev.copy_(self.reward_pin, non_blocking=True)
+        self.term_dev.copy_(self.term_pin, non_blocking=True)
+        self.first_dev.copy_(torch.from_numpy(self.firsts[:-1].astype(np.uint8)), non_blocking=True)
+        if self.reward_scale_running:                                                  # :232-236
+            self.running_reward_scaler.scale_(self.reward_dev, self.first_dev,
+                                              group=dist.group.WORLD if self.world_size > 1 else None)
+        last_obs = self.obs_pin.view(E, -1).to(self.device, non_blocking=True)
+        ops.critic_forward(m.dims, m.precision, m.packed_critic, last_obs, values=self.last_values)
+        ops.gae(self.reward_dev, self.values.view(S, E), self.last_values, self.term_dev, self.gamma, self.gae_lambda,
+                self.reward_scale_const, adv=self.adv, ret=self.ret)                       # :239-263
+        adv_flat, ret_flat = self.adv.view(-1), self.ret.view(-1)
+
+        total_local = N * kf
+        total_global = total_local * self.world_size
+        num_batch = max(1, total_global // self.batch_size)                               # :288
+        rows_local_full = self.batch_size // self.world_size
+        clipfracs, info = [], {}
+        stream = torch.cuda.current_stream(self.device)
+        for update_epoch in range(self.update_epochs):
+            flag_break = False
+            for batch in range(num_batch):
+                start = batch * rows_local_full
+                rows = min(rows_local_full, total_local - start)
+                if rows <= 0:
+                    break
+                global_rows = rows * self.world_size
+                stats = None
+                if self.world_size > 1:
+                    ops.ppo_adv_stats(adv_flat, total_local, kf, self.perm_seed, update_epoch + 1000 * self.itr,
+                                      start, rows, self.adv_stats)
+                    self._allreduce(self.adv_stats)
+                    stats = self.adv_stats
+                if self.update_events is not None:
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev0.record(stream)
+                m.minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, self.perm_seed,
+                            update_epoch + 1000 * self.itr, start, rows, global_rows=global_rows,
+                            reward_horizon=self.reward_horizon, adv_stats=stats)
+                if self.world_size > 1:
+                    self._allreduce(m.grads)
+                    self._allreduce(m.metrics)
+                if self.itr >= self.n_critic_warmup_itr:
+                    if self.max_grad_norm is not None:
+                        self._clip_by_norm_per_tensor()
+                    lr = self.actor_optimizer.apply_gradients(m.grads)
+                    m.repack()
+                if self.update_events is not None:
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev1.record(stream)
+                    self.update_events.append((ev0, ev1))
+                met = (m.metrics[:5] / global_rows).cpu().numpy()                       # host sync (KL stop)
+                self.timing["n_updates"] += 1
+                info = dict(pg_loss=float(met[0]), v_loss=float(met[1]), approx_kl=float(met[2]),
+                            clipfrac=float(met[3]), ratio=float(met[4]), bc_loss=0.0, eta=1.0,
+                            entropy_loss=-1.0, loss=float(met[0] + self.vf_coef * met[1]))
+                clipfracs.append(info["clipfrac"])
+                if self.target_kl is not None and info["approx_kl"] > self.target_kl:       # :366-370
+                    flag_break = True
+                    break
+            if flag_break:
+                break
+        # explained variance (:373-377)
+        y_pred = self.values.double()
+        y_true = ret_flat.double()
+        mom = torch.stack([y_true.sum(), (y_true ** 2).sum(), (y_true - y_pred).sum(), ((y_true - y_pred) ** 2).sum(),
+                           torch.tensor(float(N), dtype=torch.float64, device=self.device)])
+        self._allreduce(mom)
+        n = mom[4]
+        var_y = mom[1] / n - (mom[0] / n) ** 2
+        var_d = mom[3] / n - (mom[2] / n) ** 2
+        info["explained_var"] = float("nan") if float(var_y) == 0 else float(1 - var_d / var_y)
+        info["clipfrac"] = float(np.mean(clipfracs)) if clipfracs else 0.0
+        return info
+
+    def _clip_by_norm_per_tensor(self):
+        """Else-branch of agent :349-353: tf.clip_by_norm(grad, 1.0) per variable."""
+        g = self.model.grads
+        o = 0
+        for spec in (self.model.actor_spec, self.model.critic_spec):
+            for _, shape in spec:
+                k = int(np.prod(shape))
+                seg = g[o:o + k]
+                nrm = torch.linalg.vector_norm(seg)
+                seg.mul_(torch.clamp(1.0 / torch.clamp(nrm, min=1e-30), max=1.0))
+                o += k
+
+    # ------------------------------------------------------------------ one iteration / the loop
+    def iteration(self, force_train=None):
+        timer = Timer()
+        ft = self.force_train if force_train is None else force_train
+        eval_mode = self.itr % self.val_freq == 0 and not ft
+        torch.cuda.synchronize(self.device)
+        t0 = Timer()
+        stats = self.rollout(eval_mode)
+        torch.cuda.synchronize(self.device)
+        t_roll = t0()
+        info = {}
+        if not eval_mode:
+            info = self.update()
+            torch.cuda.synchronize(self.device)
+        t_upd = t0()
+        self.timing["rollout_s"] += t_roll
+        self.timing["update_s"] += t_upd
+        self.timing["iters"] += 1
+        if not eval_mode:
+            self.timing["env_steps"] += self.n_envs_global * self.act_steps * self.n_steps
+        self.model.step()
+        if self.itr % self.save_model_freq == 0 or self.itr == self.n_train_itr - 1:
+            if self.cfg.train.get("save_checkpoints", True):
+                self.save_model()
+        res = {"itr": self.itr, "step": self.cnt_train_step, "time": timer(), "eval": eval_mode, **stats, **info}
+        self.run_results.append(res)
+        if self.rank == 0 and self.itr % self.log_freq == 0:
+            if eval_mode:
+                log.info("eval: success rate %8.4f | avg episode reward %8.4f | avg best reward %8.4f",
+                         stats["success_rate"], stats["avg_episode_reward"], stats["avg_best_reward"])
+            else:
+                log.info("%d: step %8d | loss %8.4f | pg loss %8.4f | value loss %8.4f | reward %8.4f | t:%8.4f",
+                         self.itr, self.cnt_train_step, info["loss"], info["pg_loss"], info["v_loss"],
+                         stats["avg_episode_reward"], res["time"])
+        self.last_info = res
+        self.itr += 1
+        return res
+
+    def run(self):
+        while self.itr < self.n_train_itr:
+            self.iteration()
+            if self.rank == 0 and self.cfg.train.get("save_results", True):
+                os.makedirs(os.path.dirname(self.result_path) or ".", exist_ok=True)
+                with open(self.result_path, "wb") as f:
+                    pickle.dump(self.run_results, f)
+        return self.run_results

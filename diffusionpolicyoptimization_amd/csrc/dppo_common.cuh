@@ -208,6 +208,15 @@ __host__ __device__ inline uint64_t feistel_once(uint64_t x, const FeistelKey& f
     }
     return (l << f.half_bits) | r;
 }
+// minibatch row -> flat sample index: explicit table or Feistel permutation (n = invalid)
+__host__ __device__ inline uint64_t feistel_permute(uint64_t i, const FeistelKey& f);
+__device__ inline uint64_t minibatch_row(const int64_t* row_index, uint64_t i, const FeistelKey& f) {
+    if (row_index) {
+        const int64_t v = row_index[i];
+        return (v >= 0 && (uint64_t)v < f.n) ? (uint64_t)v : f.n;
+    }
+    return feistel_permute(i, f);
+}
 // cycle walking; bounded (P(>1024 walks) < 1e-128); returns n on give-up (caller treats as invalid)
 __host__ __device__ inline uint64_t feistel_permute(uint64_t i, const FeistelKey& f) {
     uint64_t x = feistel_once(i, f);

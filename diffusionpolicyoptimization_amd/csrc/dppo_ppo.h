@@ -61,6 +61,7 @@ struct ActorArgs {
     // train
     FeistelKey fk;
     int64_t start;
+    const int64_t* row_index;
     const float* lp_old;   // [nsamp][KF]
     const float* adv;      // [nsamp]
     const double* adv_stats;
@@ -78,6 +79,7 @@ struct CriticArgs {
     float* values;        // value mode
     FeistelKey fk;
     int64_t start;
+    const int64_t* row_index;
     const float* returns;
     LossHP hp;
     PpoWorkspace ws;

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
         int n = -1, j = 0;
         if (gr < a.nrows) {
             if (train) {
-                const uint64_t idx = feistel_permute((uint64_t)(a.start + gr), a.fk);
+                const uint64_t idx = minibatch_row(a.row_index, (uint64_t)(a.start + gr), a.fk);
                 if (idx < a.fk.n) { n = (int)(idx / KF); j = (int)(idx % KF); }   // tf.unravel_index
             } else {
                 n = (int)(gr / KF); j = (int)(gr % KF);
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
         int n = -1;
         if (gr < a.nrows) {
             if (train) {
-                const uint64_t idx = feistel_permute((uint64_t)(a.start + gr), a.fk);
+                const uint64_t idx = minibatch_row(a.row_index, (uint64_t)(a.start + gr), a.fk);
                 if (idx < a.fk.n) n = (int)(idx / a.KF);
             } else {
                 n = (int)gr;

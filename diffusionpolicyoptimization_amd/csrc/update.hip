@@ -188,11 +188,12 @@ __global__ __launch_bounds__(256) void time_bwd_kernel(const float* __restrict__
 // minibatch advantage statistics {count, sum, sumsq} (for norm_adv, diffusion_ppo.py:74-75)
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict__ adv, FeistelKey fk, int KF, int64_t start,
-                                                        int rows, double* __restrict__ stats) {
+                                                        int rows, const int64_t* __restrict__ row_index,
+                                                        double* __restrict__ stats) {
     __shared__ double sh[3][4];
     double c = 0.0, s = 0.0, s2 = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < rows; i += (int64_t)gridDim.x * 256) {
-        const uint64_t idx = feistel_permute((uint64_t)(start + i), fk);
+        const uint64_t idx = minibatch_row(row_index, (uint64_t)(start + i), fk);
         if (idx >= fk.n) continue;
         const double v = adv[idx / KF];
         c += 1.0; s += v; s2 += v * v;
@@ -271,14 +272,15 @@ extern "C" int dppo_feistel_permute(int64_t first, int64_t count, int64_t n, uin
 }
 
 extern "C" int dppo_ppo_adv_stats(const float* advantages, int64_t total, int K_ft, uint64_t perm_seed, int epoch,
-                                  int64_t start, int rows, double* adv_stats, void* stream) {
+                                  int64_t start, int rows, const int64_t* row_index, double* adv_stats, void* stream) {
     DPPO_CHECK(advantages && adv_stats && total > 0 && K_ft > 0 && rows >= 0, "dppo_ppo_adv_stats: bad args");
     hipStream_t s = (hipStream_t)stream;
     DPPO_HIP(hipMemsetAsync(adv_stats, 0, 3 * sizeof(double), s));
     if (rows == 0) return DPPO_OK;
     const FeistelKey fk = feistel_key((uint64_t)total, perm_seed, epoch);
     const int blocks = dppo_cdiv(rows, 256) < 512 ? dppo_cdiv(rows, 256) : 512;
-    hipLaunchKernelGGL(adv_stats_kernel, dim3(blocks), dim3(256), 0, s, advantages, fk, K_ft, start, rows, adv_stats);
+    hipLaunchKernelGGL(adv_stats_kernel, dim3(blocks), dim3(256), 0, s, advantages, fk, K_ft, start, rows, row_index,
+                       adv_stats);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -302,7 +304,7 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
                                   const void* packed_ft, const void* packed_critic, const float* actor_params,
                                   const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
                                   const float* advantages, const float* returns, int64_t total, uint64_t perm_seed,
-                                  int epoch, int64_t start, int rows, const double* adv_stats,
+                                  int epoch, int64_t start, int rows, const int64_t* row_index, const double* adv_stats,
                                   void* workspace, float* grads, double* metrics, void* stream) {
     Dims D;
     int rc = dppo_check_dims(d, &D);
@@ -325,7 +327,7 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     DPPO_HIP(hipMemsetAsync(ws.gseg, 0, sizeof(float) * 16 * D.H, s));
     const double* stats = adv_stats;
     if (!stats) {
-        rc = dppo_ppo_adv_stats(advantages, total, D.KF, perm_seed, epoch, start, rows, ws.stats, stream);
+        rc = dppo_ppo_adv_stats(advantages, total, D.KF, perm_seed, epoch, start, rows, row_index, ws.stats, stream);
         if (rc) return rc;
         stats = ws.stats;
     }
@@ -342,7 +344,7 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     aa.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision);
     aa.sched = sched; aa.obs = obs; aa.chains = chains;
     aa.XD = D.XD; aa.SD = D.SD; aa.TD = D.TD; aa.IN = D.IN; aa.H = D.H; aa.KF = D.KF; aa.Da = D.Da;
-    aa.mode = ROWS_TRAIN; aa.nrows = rows; aa.fk = fk; aa.start = start;
+    aa.mode = ROWS_TRAIN; aa.nrows = rows; aa.fk = fk; aa.start = start; aa.row_index = row_index;
     aa.lp_old = lp_old_mean; aa.adv = advantages; aa.adv_stats = stats; aa.hp = lh; aa.ws = ws; aa.metrics = metrics;
     rc = launch_actor_rowtile(aa, precision, s);
     if (rc) return rc;
@@ -351,7 +353,7 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     ca.packed = (const uint8_t*)packed_critic;
     ca.L = make_mlp_layout(D.SD, D.HC, 1, 0, precision);
     ca.obs = obs; ca.SD = D.SD; ca.HC = D.HC; ca.KF = D.KF; ca.mode = ROWS_TRAIN; ca.nrows = rows;
-    ca.fk = fk; ca.start = start; ca.returns = returns; ca.hp = lh; ca.ws = ws; ca.metrics = metrics;
+    ca.fk = fk; ca.start = start; ca.row_index = row_index; ca.returns = returns; ca.hp = lh; ca.ws = ws; ca.metrics = metrics;
     rc = launch_critic_rowtile(ca, precision, s);
     if (rc) return rc;
 

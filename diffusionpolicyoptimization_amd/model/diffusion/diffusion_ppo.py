@@ -1,0 +1,82 @@
+"""PPODiffusion (reference model/diffusion/diffusion_ppo.py:7-132).
+
+c_loss keeps the reference signature and 8-tuple return; its forward AND the gradient of
+pg_loss + vf_coef * v_loss (train_ppo_diffusion_agent.py:340) w.r.t. [actor_ft | critic] are one
+fused HIP pass (dppo_ppo_minibatch), left in `self.grads` for the optimiser. The agent uses
+`minibatch()`, the same pass gathering rows straight from the HBM-resident rollout buffers."""
+import numpy as np
+import torch
+
+from ... import ops
+from .diffusion_vpg import VPGDiffusion, _as_state
+
+# metrics slots written by the kernels (sums over rows; see update.hip)
+M_PG, M_VLOSS, M_KL, M_CLIPFRAC, M_RATIO = 0, 1, 2, 3, 4
+
+
+class PPODiffusion(VPGDiffusion):
+    def __init__(self, gamma_denoising, clip_ploss_coef, clip_ploss_coef_base=1e-3, clip_ploss_coef_rate=3,
+                 clip_vloss_coef=None, clip_advantage_lower_quantile=0, clip_advantage_upper_quantile=1, norm_adv=True,
+                 vf_coef=0.5, **kwargs):
+        super().__init__(**kwargs)
+        if clip_vloss_coef is not None:
+            raise NotImplementedError("clip_vloss_coef (None in every cfg) is not implemented in the fused loss")
+        self.gamma_denoising = gamma_denoising
+        self.clip_ploss_coef = clip_ploss_coef
+        self.clip_ploss_coef_base = clip_ploss_coef_base
+        self.clip_ploss_coef_rate = clip_ploss_coef_rate
+        self.clip_vloss_coef = clip_vloss_coef
+        self.clip_advantage_lower_quantile = clip_advantage_lower_quantile  # unused, as in the reference (:77-80)
+        self.clip_advantage_upper_quantile = clip_advantage_upper_quantile
+        self.norm_adv = norm_adv
+        self.vf_coef = vf_coef
+        self.metrics = torch.zeros(16, dtype=torch.float64, device=self.device)
+        self._ws = {}
+
+    def hparams(self, global_rows, reward_horizon=4, loss_scale=1.0):
+        return ops.ppo_hparams(self.gamma_denoising, self.clip_ploss_coef, self.clip_ploss_coef_base,
+                               self.clip_ploss_coef_rate, self.min_logprob_denoising_std, self.vf_coef, self.norm_adv,
+                               reward_horizon, loss_scale, global_rows)
+
+    def workspace(self, rows):
+        ws = self._ws.get(rows)
+        if ws is None:
+            ws = self._ws[rows] = ops.ppo_workspace(self.dims, self.precision, rows, self.device)
+        return ws
+
+    def minibatch(self, obs, chains, lp_old_mean, advantages, returns, perm_seed, epoch, start, rows,
+                  global_rows=None, reward_horizon=4, loss_scale=1.0, adv_stats=None, row_index=None):
+        """One fused PPO minibatch over HBM rollout buffers (obs [N,SD], chains [N,K'+1,XD],
+        lp_old_mean [N,K'], advantages/returns [N]); writes self.grads and self.metrics (sums)."""
+        hp = self.hparams(global_rows or rows, reward_horizon, loss_scale)
+        ops.ppo_minibatch(self.dims, self.precision, hp, self.packed_ft, self.packed_critic, self.actor_ft_params,
+                          self.sched, obs, chains, lp_old_mean, advantages, returns, perm_seed, epoch, start, rows,
+                          self.workspace(rows), self.grads, self.metrics, adv_stats=adv_stats, row_index=row_index)
+
+    def c_loss(self, obs, chains_prev, chains_next, denoising_inds, returns, oldvalues, advantages, oldlogprobs,
+               use_bc_loss=False, reward_horizon=4):
+        """diffusion_ppo.py:32-132 on an explicit batch. Returns (pg_loss, entropy_loss, v_loss, clipfrac,
+        approx_kl, ratio, bc_loss, eta) as floats; gradients are left in self.grads."""
+        if use_bc_loss:
+            raise NotImplementedError("use_bc_loss (False in every cfg) is not implemented")
+        dev = self.device
+        state = _as_state(obs, dev, self.dims.sd)
+        b = state.shape[0]
+        kf, xd = self.ft_denoising_steps, self.dims.xd
+        j = torch.as_tensor(denoising_inds, device=dev).long().reshape(b)
+        r = torch.arange(b, device=dev)
+        ch = torch.zeros(b, kf + 1, xd, dtype=torch.float32, device=dev)
+        ch[r, j] = torch.as_tensor(chains_prev, device=dev, dtype=torch.float32).reshape(b, xd)
+        ch[r, j + 1] = torch.as_tensor(chains_next, device=dev, dtype=torch.float32).reshape(b, xd)
+        old = torch.as_tensor(oldlogprobs, device=dev, dtype=torch.float32)
+        if old.dim() == 3:  # per element [b, Ta, Da]: clip to [-5, 2] and mean over the horizon (:50-59)
+            old = old.clamp(-5, 2)[:, :reward_horizon].mean(dim=(1, 2))
+        lp_old = torch.zeros(b, kf, dtype=torch.float32, device=dev)
+        lp_old[r, j] = old.reshape(b)
+        adv = torch.as_tensor(advantages, device=dev, dtype=torch.float32).reshape(b).contiguous()
+        ret = torch.as_tensor(returns, device=dev, dtype=torch.float32).reshape(b).contiguous()
+        row_index = (r * kf + j).contiguous()
+        self.minibatch(state, ch, lp_old, adv, ret, 0, 0, 0, b, reward_horizon=reward_horizon, row_index=row_index)
+        m = (self.metrics[:5] / b).cpu().numpy()
+        return (float(m[M_PG]), -1.0, float(m[M_VLOSS]), float(m[M_CLIPFRAC]), float(m[M_KL]), float(m[M_RATIO]),
+                0.0, 1.0)

@@ -1,0 +1,214 @@
+"""VPGDiffusion (reference model/diffusion/diffusion_vpg.py:27-481) on MI355X.
+
+State lives in HBM as flat fp32 buffers in the Keras layout (include/dppo.h):
+  base_params   frozen pretrained actor                       (diffusion_vpg.py:100-102)
+  train_params  [actor_ft | critic], the variables the single AdamW updates (quirk 2)
+plus their packed MFMA fragment images (bf16 or fp32) that the kernels read. Every forward runs
+in a fused HIP kernel: the K-step sampler (dppo_sample), the chain log-prob pass (dppo_logprob),
+the critic value pass (dppo_critic_forward); the PPO loss/gradient is PPODiffusion.c_loss."""
+import copy
+import logging
+import os
+
+import numpy as np
+import torch
+
+from ... import ops
+from .diffusion import DiffusionModel, Sample
+
+log = logging.getLogger(__name__)
+
+
+def _as_state(cond, device, sd):
+    x = cond["state"] if isinstance(cond, dict) else cond
+    if not isinstance(x, torch.Tensor):
+        x = torch.as_tensor(np.asarray(x, np.float32))
+    x = x.to(device=device, dtype=torch.float32)
+    return x.reshape(x.shape[0], sd).contiguous()
+
+
+class VPGDiffusion(DiffusionModel):
+    def __init__(self, actor, critic, ft_denoising_steps, ft_denoising_steps_d=0, ft_denoising_steps_t=0,
+                 network_path=None, min_sampling_denoising_std=0.1, min_logprob_denoising_std=0.1, eta=None,
+                 learn_eta=False, **kwargs):
+        super().__init__(network=actor, network_path=network_path, **kwargs)
+        assert ft_denoising_steps <= self.denoising_steps
+        if learn_eta or eta is not None:
+            raise NotImplementedError("eta / learn_eta belong to DDIM (not implemented this round)")
+        self.ft_denoising_steps = int(ft_denoising_steps)
+        self.ft_denoising_steps_d = ft_denoising_steps_d
+        self.ft_denoising_steps_t = ft_denoising_steps_t
+        self.ft_denoising_steps_cnt = 0
+        self.min_sampling_denoising_std = min_sampling_denoising_std
+        self.min_logprob_denoising_std = min_logprob_denoising_std
+        self.learn_eta = False
+        self.actor = actor
+        self.critic = critic
+        critic._owner = self
+        cond_steps = actor.cond_dim // self.obs_dim
+        self.dims = ops.ModelDims(obs_dim=self.obs_dim, action_dim=self.action_dim,
+                                  horizon_steps=self.horizon_steps, cond_steps=cond_steps, time_dim=actor.time_dim,
+                                  actor_hidden=actor.hidden, critic_hidden=critic.hidden,
+                                  denoising_steps=self.denoising_steps, ft_denoising_steps=self.ft_denoising_steps)
+        self.actor_spec = ops.actor_param_spec(self.dims)
+        self.critic_spec = ops.critic_param_spec(self.dims)
+        self.n_actor = ops.spec_count(self.actor_spec)
+        self.n_critic = ops.spec_count(self.critic_spec)
+        rng = np.random.default_rng(self.seed)
+        base = self._load_actor(network_path, rng)
+        critic_p = critic.init_params(np.random.default_rng(self.seed + 1))  # fresh critic (:109-110)
+        dev = self.device
+        self.base_params = torch.tensor(ops.flatten_params(self.actor_spec, base), device=dev)
+        self.train_params = torch.empty(self.n_actor + self.n_critic, dtype=torch.float32, device=dev)
+        self.train_params[:self.n_actor].copy_(self.base_params)  # actor_ft = deepcopy(actor) (:95-97)
+        self.train_params[self.n_actor:].copy_(torch.tensor(ops.flatten_params(self.critic_spec, critic_p)))
+        self.grads = torch.zeros_like(self.train_params)
+        self.packed_base = ops.pack_actor(self.dims, self.base_params, self.precision)
+        self.packed_ft = torch.empty_like(self.packed_base)
+        self.packed_critic = torch.empty(ops.critic_packed_bytes(self.dims, self.precision), dtype=torch.uint8,
+                                         device=dev)
+        self.repack()
+        self._call_id = 0
+        self._env_offset = 0
+        log.info("Number of finetuned parameters: %d (actor_ft) + %d (critic)", self.n_actor, self.n_critic)
+
+    # ------------------------------------------------------------------ parameters
+    @property
+    def actor_ft_params(self):
+        return self.train_params[:self.n_actor]
+
+    @property
+    def critic_params(self):
+        return self.train_params[self.n_actor:]
+
+    @property
+    def trainable_variables(self):
+        return [self.train_params]
+
+    def repack(self):
+        """Re-derive the packed fragment images of actor_ft and critic after an optimiser step."""
+        ops.pack_actor(self.dims, self.actor_ft_params, self.precision, out=self.packed_ft)
+        ops.pack_critic(self.dims, self.critic_params, self.precision, out=self.packed_critic)
+
+    def _load_actor(self, path, rng):
+        if path is None or not os.path.exists(str(path)):
+            if path is not None:
+                log.warning("base policy %s not found: using a seeded glorot_uniform actor (synthetic weights)", path)
+            return self.network.init_params(rng)
+        path = str(path)
+        if path.endswith(".npz"):
+            with np.load(path, allow_pickle=False) as f:
+                keys = [k for k in f.files]
+                pref = "actor." if any(k.startswith("actor.") for k in keys) else ""
+                return {n: np.asarray(f[pref + n], np.float32).reshape(s) for n, s in self.actor_spec}
+        if path.endswith(".h5"):
+            try:
+                import h5py  # noqa: F401
+            except ImportError as e:
+                raise NotImplementedError(f"{path}: Keras .weights.h5 needs h5py, which is not installed; convert "
+                                          "the checkpoint to .npz (keys " + ", ".join(n for n, _ in self.actor_spec)
+                                          + ")") from e
+            raise NotImplementedError(".weights.h5 reader: SURVEY.md §8(f) rank 2")
+        raise ValueError(f"unsupported checkpoint format: {path}")
+
+    def save_weights(self, path):
+        d = {}
+        for prefix, flat, spec in (("actor.", self.base_params, self.actor_spec),
+                                   ("actor_ft.", self.actor_ft_params, self.actor_spec),
+                                   ("critic.", self.critic_params, self.critic_spec)):
+            for n, v in ops.unflatten_params(spec, flat.detach().cpu().numpy()).items():
+                d[prefix + n] = v
+        np.savez(path, **d)
+
+    def load_weights(self, path):
+        with np.load(path, allow_pickle=False) as f:
+            for prefix, flat, spec in (("actor.", self.base_params, self.actor_spec),
+                                       ("actor_ft.", self.actor_ft_params, self.actor_spec),
+                                       ("critic.", self.critic_params, self.critic_spec)):
+                if all(prefix + n in f.files for n, _ in spec):
+                    flat.copy_(torch.tensor(ops.flatten_params(spec, {n: f[prefix + n] for n, _ in spec})))
+        ops.pack_actor(self.dims, self.base_params, self.precision, out=self.packed_base)
+        self.repack()
+
+    # ------------------------------------------------------------------ annealing (diffusion_vpg.py:114-148)
+    def step(self):
+        if not isinstance(self.min_sampling_denoising_std, float):
+            self.min_sampling_denoising_std.step()
+        self.ft_denoising_steps_cnt += 1
+        if (self.ft_denoising_steps_d > 0 and self.ft_denoising_steps_t > 0
+                and self.ft_denoising_steps_cnt % self.ft_denoising_steps_t == 0):
+            self.ft_denoising_steps = max(0, self.ft_denoising_steps - self.ft_denoising_steps_d)
+            self.base_params.copy_(self.actor_ft_params)
+            self.dims = ops.ModelDims(**{**self.dims.__dict__, "ft_denoising_steps": self.ft_denoising_steps})
+            ops.pack_actor(self.dims, self.base_params, self.precision, out=self.packed_base)
+            log.info("Finished annealing fine-tuning denoising steps to %d", self.ft_denoising_steps)
+
+    def get_min_sampling_denoising_std(self):
+        if isinstance(self.min_sampling_denoising_std, float):
+            return self.min_sampling_denoising_std
+        return self.min_sampling_denoising_std()
+
+    # ------------------------------------------------------------------ sampler (diffusion_vpg.py:250-339)
+    def set_rng(self, seed, env_offset=0):
+        """Philox stream of the in-kernel noise: (seed, call counter, global env row)."""
+        self.seed = int(seed)
+        self._env_offset = int(env_offset)
+
+    def __call__(self, cond, deterministic=False, return_chain=True, use_base_policy=False, *, x_T=None, noise=None,
+                 actions_out=None, chains_out=None):
+        state = _as_state(cond, self.device, self.dims.sd)
+        E = state.shape[0]
+        packed_ft = self.packed_base if use_base_policy else self.packed_ft
+        acts, chains = ops.sample(
+            self.dims, self.precision, self.packed_base, packed_ft, self.sched, state, x_T=x_T, noise=noise,
+            seed=self.seed, call_id=self._call_id, env_offset=self._env_offset, deterministic=deterministic,
+            min_sampling_std=self.get_min_sampling_denoising_std(), randn_clip=self.randn_clip_value,
+            final_clip=self.final_action_clip_value, actions=actions_out, chains=chains_out,
+            want_chains=return_chain)
+        self._call_id += 1
+        traj = acts.view(E, self.horizon_steps, self.action_dim)
+        ch = chains.view(E, self.ft_denoising_steps + 1, self.horizon_steps, self.action_dim) if chains is not None else None
+        return Sample(traj, ch)
+
+    # ------------------------------------------------------------------ log-probs (diffusion_vpg.py:343-481)
+    def get_logprobs(self, cond, chains, get_ent=False, use_base_policy=False, reduced=False):
+        """-> [n*K', Ta, Da] (row = sample*K' + j, t = K'-1-j). reduced=True instead returns the
+        clipped mean c_loss uses, [n, K'] (diffusion_ppo.py:50-59)."""
+        state = _as_state(cond, self.device, self.dims.sd)
+        n = state.shape[0]
+        kf = self.ft_denoising_steps
+        ch = torch.as_tensor(chains, device=self.device, dtype=torch.float32).reshape(n, kf + 1, self.dims.xd)
+        packed = self.packed_base if use_base_policy else self.packed_ft
+        lpe, lpm = ops.logprob(self.dims, self.precision, packed, self.sched, state, ch.contiguous(),
+                               min_logprob_std=self.min_logprob_denoising_std, want_elem=not reduced,
+                               want_mean=reduced)
+        if reduced:
+            return lpm
+        lpe = lpe.view(n * kf, self.horizon_steps, self.action_dim)
+        if get_ent:
+            return lpe, torch.ones_like(lpe)
+        return lpe
+
+    def get_logprobs_subsample(self, cond, chains_prev, chains_next, denoising_inds, get_ent=False,
+                               use_base_policy=False):
+        """Per-row denoising index j (t = K'-1-j): evaluated by placing each (prev, next) pair at
+        chain slots (j, j+1) of a one-sample chain and reading row j of the chain log-probs."""
+        state = _as_state(cond, self.device, self.dims.sd)
+        b = state.shape[0]
+        kf, xd = self.ft_denoising_steps, self.dims.xd
+        j = torch.as_tensor(denoising_inds, device=self.device).long().reshape(b)
+        ch = torch.zeros(b, kf + 1, xd, dtype=torch.float32, device=self.device)
+        r = torch.arange(b, device=self.device)
+        ch[r, j] = torch.as_tensor(chains_prev, device=self.device, dtype=torch.float32).reshape(b, xd)
+        ch[r, j + 1] = torch.as_tensor(chains_next, device=self.device, dtype=torch.float32).reshape(b, xd)
+        lpe = self.get_logprobs(state, ch, use_base_policy=use_base_policy).view(b, kf, self.horizon_steps,
+                                                                                 self.action_dim)
+        out = lpe[r, j]
+        if get_ent:
+            return out, torch.ones_like(out)
+        return out
+
+    # ------------------------------------------------------------------ critic (critic.py:40-54)
+    def critic_values(self, cond):
+        state = _as_state(cond, self.device, self.dims.sd)
+        return ops.critic_forward(self.dims, self.precision, self.packed_critic, state)

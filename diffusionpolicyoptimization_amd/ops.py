@@ -248,9 +248,9 @@ def ppo_workspace(d: ModelDims, precision, rows, device):
     return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
-def ppo_adv_stats(advantages, total, kf, perm_seed, epoch, start, rows, out):
+def ppo_adv_stats(advantages, total, kf, perm_seed, epoch, start, rows, out, row_index=None):
     _lib.call("dppo_ppo_adv_stats", ptr(advantages), int(total), int(kf), ctypes.c_uint64(perm_seed), int(epoch),
-              int(start), int(rows), ptr(out), stream_handle(advantages.device))
+              int(start), int(rows), ptr(row_index), ptr(out), stream_handle(advantages.device))
     return out
 
 
@@ -262,7 +262,8 @@ def ppo_hparams(gamma_denoising=0.99, clip_ploss_coef=0.01, clip_ploss_coef_base
 
 
 def ppo_minibatch(d: ModelDims, precision, hp, packed_ft, packed_critic, actor_params, sched, obs, chains, lp_old_mean,
-                  advantages, returns, perm_seed, epoch, start, rows, workspace, grads, metrics, adv_stats=None):
+                  advantages, returns, perm_seed, epoch, start, rows, workspace, grads, metrics, adv_stats=None,
+                  row_index=None):
     n = obs.shape[0]
     kf = d.ft_denoising_steps
     _check(obs, (n, d.sd), torch.float32, "obs")
@@ -274,13 +275,17 @@ def ppo_minibatch(d: ModelDims, precision, hp, packed_ft, packed_critic, actor_p
     _check(actor_params, (na,), torch.float32, "actor_params")
     _check(grads, (na + nc,), torch.float32, "grads")
     _check(metrics, (16,), torch.float64, "metrics")
+    if row_index is not None:
+        _check(row_index, (row_index.numel(),), torch.int64, "row_index")
+        if row_index.numel() < start + rows:
+            raise ValueError("row_index shorter than start + rows")
     need = int(_lib.query("dppo_ppo_workspace_bytes", ctypes.byref(d.c()), _prec(precision), int(rows)))
     if workspace.numel() < need:
         raise ValueError(f"workspace too small: {workspace.numel()} < {need}")
     _lib.call("dppo_ppo_minibatch", ctypes.byref(d.c()), _prec(precision), ctypes.byref(hp), ptr(packed_ft),
               ptr(packed_critic), ptr(actor_params), ptr(sched), ptr(obs), ptr(chains), ptr(lp_old_mean),
               ptr(advantages), ptr(returns), int(n * kf), ctypes.c_uint64(perm_seed), int(epoch), int(start), int(rows),
-              ptr(adv_stats), ptr(workspace), ptr(grads), ptr(metrics), stream_handle(obs.device))
+              ptr(row_index), ptr(adv_stats), ptr(workspace), ptr(grads), ptr(metrics), stream_handle(obs.device))
 
 
 def adamw(params, grads, m, v, step, lr, weight_decay=0.004, beta1=0.9, beta2=0.999, eps=1e-7, mode="keras"):

@@ -1,0 +1,41 @@
+"""AdamW over the flat [actor_ft | critic] buffer on the device (dppo_adamw).
+
+Default semantics are Keras 3 AdamW as the reference constructs it (train_ppo_agent.py:45-49):
+`decay=` is not weight decay in Keras 3, so the default weight_decay = 0.004 applies to every
+variable, decoupled and before the Adam step, epsilon = 1e-7, and ONE optimiser trains actor_ft
+and critic at the actor LR (the critic optimiser is never applied, agent :360). mode="torch"
+gives PyTorch AdamW as a documented alternative."""
+from .. import ops
+
+
+class AdamW:
+    def __init__(self, params, learning_rate, weight_decay=0.004, beta_1=0.9, beta_2=0.999, epsilon=1e-7,
+                 mode="keras"):
+        import torch
+        self.params = params
+        self.m = torch.zeros_like(params)
+        self.v = torch.zeros_like(params)
+        self.learning_rate = learning_rate
+        self.weight_decay, self.beta_1, self.beta_2, self.epsilon = weight_decay, beta_1, beta_2, epsilon
+        self.mode = mode
+        self.iterations = 0
+
+    def current_lr(self):
+        lr = self.learning_rate
+        return float(lr(self.iterations)) if callable(lr) else float(lr)
+
+    def apply_gradients(self, grads):
+        lr = self.current_lr()
+        self.iterations += 1
+        ops.adamw(self.params, grads, self.m, self.v, self.iterations, lr, self.weight_decay, self.beta_1, self.beta_2,
+                  self.epsilon, self.mode)
+        return lr
+
+    def state_dict(self):
+        return {"m": self.m.detach().cpu().numpy(), "v": self.v.detach().cpu().numpy(), "iterations": self.iterations}
+
+    def load_state_dict(self, d):
+        import torch
+        self.m.copy_(torch.as_tensor(d["m"]))
+        self.v.copy_(torch.as_tensor(d["v"]))
+        self.iterations = int(d["iterations"])

@@ -129,7 +129,9 @@ DPPO_API int dppo_gae(const double* reward, const float* values, const float* la
  *   obs [S*E, To*Do], chains [S*E, K'+1, Ta*Da], lp_old_mean [S*E, K'] (from dppo_logprob),
  *   advantages / returns [S*E] fp32.
  * Minibatch rows: perm(start .. start+rows-1) with perm = Feistel bijection of [0,total) keyed
- * by (perm_seed, epoch), unravelled to (n, j) = (idx / K', idx % K') (tf.unravel_index).
+ * by (perm_seed, epoch), unravelled to (n, j) = (idx / K', idx % K') (tf.unravel_index);
+ * or, when row_index != NULL, idx = row_index[start + r] (host-chosen rows, e.g. c_loss on an
+ * explicit batch or a replayed tf.random.shuffle permutation).
  * grads [actor_count + critic_count] fp32 are OVERWRITTEN (actor first). metrics (device, fp64[16]):
  *   {pg_loss, v_loss, approx_kl, clipfrac, ratio_mean, loss, adv_mean, adv_std, ...}.
  * adv_stats: fp64[3] {count, sum, sumsq} of the minibatch advantages, or NULL to compute locally;
@@ -144,12 +146,12 @@ typedef struct dppo_ppo_hparams {
 
 DPPO_API size_t dppo_ppo_workspace_bytes(const dppo_dims* d, int precision, int batch_rows);
 DPPO_API int dppo_ppo_adv_stats(const float* advantages, int64_t total, int K_ft, uint64_t perm_seed, int epoch,
-                       int64_t start, int rows, double* adv_stats, void* stream);
+                       int64_t start, int rows, const int64_t* row_index, double* adv_stats, void* stream);
 DPPO_API int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
                        const void* packed_ft, const void* packed_critic, const float* actor_params,
                        const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
                        const float* advantages, const float* returns, int64_t total, uint64_t perm_seed,
-                       int epoch, int64_t start, int rows, const double* adv_stats,
+                       int epoch, int64_t start, int rows, const int64_t* row_index, const double* adv_stats,
                        void* workspace, float* grads, double* metrics, void* stream);
 
 /* Feistel permutation used above, exposed for tests: out[i] = perm(first + i), i < count. */
