@@ -76,64 +76,121 @@ __device__ inline u32x4 load_bfrag_c(const u32x4* __restrict__ W, int KS, int nt
 
 __device__ inline void zero_acc(f32x4& a) { a = f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// Wide layer: this wave computes n-tiles [ntile0, ntile0+NT) for all MT row tiles over KS k-steps.
-// Weight fragments are prefetched DEPTH k-steps ahead in a compile-time-indexed register ring.
-template <class P, int MT, int NT, int DEPTH>
-__device__ inline void gemm_wide(const typename P::AT* A, int lda, int KS, const u32x4* __restrict__ W,
-                                 int ntile0, f32x4 (&acc)[MT][NT], int lane) {
+// ------------------------------------------------------------------------------------------------
+// The weight stream. Each wave walks its fragments of every layer as one continuous stream: a
+// register ring holds the next TWO k-steps (NT fragments each), and the tail of a layer already
+// loads the first two k-steps of the NEXT layer, so the load queue never drains at a layer
+// boundary. Every packed matrix has an even k-step count (dppo_layout.h), so the loop body is
+// branch-free (the source switch is a scalar select) and hipcc emits counted vmcnt waits.
+// ------------------------------------------------------------------------------------------------
+template <int NT>
+struct WRing {
+    u32x4 b0[NT], b1[NT];
+};
+
+struct NextLayer {
+    const u32x4* W;   // packed matrix the stream continues into (may repeat the current one)
+    int KS, ntile0;
+};
+
+template <int NT>
+__device__ inline void ring_prime(WRing<NT>& R, const u32x4* __restrict__ W, int KS, int ntile0, int lane) {
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        R.b0[n] = load_bfrag_c(W, KS, ntile0 + n, 0, lane);
+        R.b1[n] = load_bfrag_c(W, KS, ntile0 + n, 1, lane);
+    }
+}
+
+// acc[MT][NT] = A[16*MT rows][KS*KG] x W[:, ntile0*16 .. (ntile0+NT)*16)   (W from the ring).
+// KS is a template parameter: the layer is straight-line code, so the waitcnt pass emits exact
+// counted vmcnt waits (a runtime trip count lets hipcc rotate the ring across the back-edge and
+// fall back to vmcnt(0) every k-step).
+template <class P, int MT, int NT, int KS>
+__device__ inline void gemm_stream(const typename P::AT* A, int lda, const u32x4* __restrict__ W, int ntile0,
+                                   f32x4 (&acc)[MT][NT], int lane, WRing<NT>& R, NextLayer nx) {
+    static_assert(KS % 2 == 0, "packed k-step counts are even");
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < NT; ++n) zero_acc(acc[m][n]);
-    u32x4 ring[DEPTH][NT];
 #pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-        const int ks = d < KS ? d : KS - 1;
+    for (int ks = 0; ks < KS; ks += 2) {
+        const bool in = ks + 2 < KS;
+        const u32x4* src = in ? W : nx.W;
+        const int kss = in ? KS : nx.KS;
+        const int nt0 = in ? ntile0 : nx.ntile0;
+        const int k0 = in ? ks + 2 : 0;
+        u32x4 c[NT];
 #pragma unroll
-        for (int n = 0; n < NT; ++n) ring[d][n] = load_bfrag_c(W, KS, ntile0 + n, ks, lane);
-    }
-    for (int ks0 = 0; ks0 < KS; ks0 += DEPTH) {
+        for (int n = 0; n < NT; ++n) c[n] = R.b0[n];
 #pragma unroll
-        for (int d = 0; d < DEPTH; ++d) {
-            const int ks = ks0 + d;
-            if (ks < KS) {
-                u32x4 b[NT];
-#pragma unroll
-                for (int n = 0; n < NT; ++n) b[n] = ring[d][n];
-                const int kn = (ks + DEPTH < KS) ? ks + DEPTH : KS - 1;
-#pragma unroll
-                for (int n = 0; n < NT; ++n) ring[d][n] = load_bfrag_c(W, KS, ntile0 + n, kn, lane);
-#pragma unroll
-                for (int m = 0; m < MT; ++m) {
-                    const u32x4 a = lds_afrag<P>(A, lda, m, ks, lane);
-#pragma unroll
-                    for (int n = 0; n < NT; ++n) acc[m][n] = P::mma(a, b[n], acc[m][n]);
-                }
-            }
-        }
-    }
-}
-
-// Narrow layer (n-tiles < waves): k-steps are dealt round-robin to the 8 waves; each wave
-// returns a partial sum that the caller reduces through LDS.
-template <class P, int MT, int NTN>
-__device__ inline void gemm_narrow(const typename P::AT* A, int lda, int KS, const u32x4* __restrict__ W,
-                                   f32x4 (&acc)[MT][NTN], int wave, int lane) {
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NTN; ++n) zero_acc(acc[m][n]);
-    for (int ks = wave; ks < KS; ks += DPPO_WAVES) {
-        u32x4 b[NTN];
-#pragma unroll
-        for (int n = 0; n < NTN; ++n) b[n] = load_bfrag_c(W, KS, n, ks, lane);
+        for (int n = 0; n < NT; ++n) R.b0[n] = load_bfrag_c(src, kss, nt0 + n, k0, lane);
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
             const u32x4 a = lds_afrag<P>(A, lda, m, ks, lane);
 #pragma unroll
-            for (int n = 0; n < NTN; ++n) acc[m][n] = P::mma(a, b[n], acc[m][n]);
+            for (int n = 0; n < NT; ++n) acc[m][n] = P::mma(a, c[n], acc[m][n]);
+        }
+#pragma unroll
+        for (int n = 0; n < NT; ++n) c[n] = R.b1[n];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) R.b1[n] = load_bfrag_c(src, kss, nt0 + n, k0 + 1, lane);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            const u32x4 a = lds_afrag<P>(A, lda, m, ks + 1, lane);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[m][n] = P::mma(a, c[n], acc[m][n]);
         }
     }
+}
+
+// hidden-layer k-steps for a precision and n-tiles-per-wave (H = 16*NT*WAVES)
+template <class P> __host__ __device__ constexpr int ksh_for(int NT, int WAVES = DPPO_WAVES) { return NT * 16 * WAVES / P::KG; }
+
+// Narrow layer (out-Dense, n-tiles < waves): k-steps dealt round-robin over the 8 waves, NOK per
+// wave (host guarantees KS == 8*NOK). The fragments are fetched early (out_prefetch, issued a
+// layer or more ahead) so the narrow layer itself waits on nothing; partials reduce through LDS.
+template <int NOK, int NO>
+struct ORing {
+    u32x4 b[NOK][NO];
+};
+
+template <int NOK, int NO, int WAVES = DPPO_WAVES>
+__device__ inline void out_prefetch(ORing<NOK, NO>& O, const u32x4* __restrict__ W, int KS, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < NOK; ++i)
+#pragma unroll
+        for (int n = 0; n < NO; ++n) O.b[i][n] = load_bfrag_c(W, KS, n, wave + WAVES * i, lane);
+}
+
+template <class P, int MT, int NOK, int NO, int WAVES = DPPO_WAVES>
+__device__ inline void gemm_narrow_pre(const typename P::AT* A, int lda, const ORing<NOK, NO>& O,
+                                       f32x4 (&acc)[MT][NO], int wave, int lane) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NO; ++n) zero_acc(acc[m][n]);
+#pragma unroll
+    for (int i = 0; i < NOK; ++i)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            const u32x4 a = lds_afrag<P>(A, lda, m, wave + WAVES * i, lane);
+#pragma unroll
+            for (int n = 0; n < NO; ++n) acc[m][n] = P::mma(a, O.b[i][n], acc[m][n]);
+        }
+}
+
+// out-layer k-steps per wave when H = 16*NT*WAVES (KS_h = H / KG dealt over WAVES waves)
+template <class P> __host__ __device__ constexpr int nok_for(int NT) { return NT * 16 / P::KG; }
+
+// Workgroup barrier for LDS hand-offs that leaves global loads in flight: waits for this wave's
+// LDS ops only (a __syncthreads() would also emit s_waitcnt vmcnt(0) and drain the weight stream).
+// The empty asm statements stop the compiler moving memory operations across the barrier.
+__device__ inline void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 }
 
 // C/D fragment coordinates (dtype independent on gfx950): col = lane&15, row = 4*(lane>>4) + r

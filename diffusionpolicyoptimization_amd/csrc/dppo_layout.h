@@ -11,7 +11,8 @@
 //   T_L2   packed bwd  W_l2^T  as [K=H][N=H]
 //   T_L1   packed bwd  W_l1^T  as [K=H][N=H]
 // A packed matrix [K][N] is ceil(N/16) n-tiles x KS k-steps x 64 lanes x 16 B, with
-// KS = ceil(K / KG), KG = 32 (bf16) or 16 (fp32). Lane l of (ntile, ks) holds, for e < EPL,
+// KS = ceil(K / KG) rounded up to EVEN (the weight stream runs in k-step pairs), KG = 32 (bf16)
+// or 16 (fp32). Lane l of (ntile, ks) holds, for e < EPL,
 //   W[ks*KG + (l>>4)*EPL + e][ntile*16 + (l&15)]   (zero outside [K][N]).
 #pragma once
 #include <stddef.h>
@@ -38,17 +39,18 @@ struct MlpLayout {
 DPPO_HD inline size_t dppo_align256(size_t x) { return (x + 255) & ~(size_t)255; }
 DPPO_HD inline size_t dppo_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 DPPO_HD inline int dppo_cdiv(int a, int b) { return (a + b - 1) / b; }
+DPPO_HD inline int packed_ksteps(int K, int KG) { return (dppo_cdiv(K, KG) + 1) & ~1; }
 DPPO_HD inline size_t packed_matrix_bytes(int K, int N, int KG) {
-    return (size_t)dppo_cdiv(N, 16) * (size_t)dppo_cdiv(K, KG) * 64 * 16;
+    return (size_t)dppo_cdiv(N, 16) * (size_t)packed_ksteps(K, KG) * 64 * 16;
 }
 
 DPPO_HD inline MlpLayout make_mlp_layout(int in_dim, int hidden, int out_dim, int time_dim, int precision) {
     MlpLayout L;
     L.in_dim = in_dim; L.hidden = hidden; L.out_dim = out_dim; L.time_dim = time_dim; L.precision = precision;
     L.KG = precision == 1 ? 32 : 16;
-    L.ks_in = dppo_cdiv(in_dim, L.KG);
-    L.ks_h = dppo_cdiv(hidden, L.KG);
-    L.ks_out_t = dppo_cdiv(out_dim, L.KG);
+    L.ks_in = packed_ksteps(in_dim, L.KG);
+    L.ks_h = packed_ksteps(hidden, L.KG);
+    L.ks_out_t = packed_ksteps(out_dim, L.KG);
     L.nt_h = dppo_cdiv(hidden, 16);
     L.nt_out = dppo_cdiv(out_dim, 16);
     size_t o = 0;

@@ -6,7 +6,7 @@
 // one thread per (ntile, ks, lane) fragment slot; writes 16 B
 template <int KG, int EPL>
 __global__ void pack_matrix_kernel(const float* __restrict__ W, int K, int N, int transposed, uint8_t* __restrict__ out) {
-    const int KS = (K + KG - 1) / KG;
+    const int KS = packed_ksteps(K, KG);
     const int NTL = (N + 15) / 16;
     const int total = NTL * KS * 64;
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -48,7 +48,7 @@ __global__ void copy_pad_kernel(const float* __restrict__ src, int n, int npad, 
 static hipError_t pack_matrix(const float* W, int K, int N, bool transposed, int precision, uint8_t* out,
                               hipStream_t s) {
     const int KG = precision == DPPO_BF16 ? 32 : 16;
-    const int total = dppo_cdiv(N, 16) * dppo_cdiv(K, KG) * 64;
+    const int total = dppo_cdiv(N, 16) * packed_ksteps(K, KG) * 64;
     const int blocks = dppo_cdiv(total, 256);
     if (precision == DPPO_BF16)
         hipLaunchKernelGGL((pack_matrix_kernel<32, 8>), dim3(blocks), dim3(256), 0, s, W, K, N, transposed ? 1 : 0, out);

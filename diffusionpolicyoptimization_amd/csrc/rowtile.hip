@@ -69,7 +69,7 @@ __device__ inline void atomic_add_metric(double* m, int i, double v) { atomicAdd
 template <class P, int MT>
 struct ActorSmem {
     static constexpr int ROWS = 16 * MT;
-    size_t tA, tB, a0, xp, xn, st, temb, ta1, sch, rn, rj, total;
+    size_t tA, tB, a0, xp, xn, st, temb, ta1, sch, rn, rj, bias, total;
     __host__ __device__ ActorSmem(const ActorArgs& a) {
         using AT = typename P::AT;
         const int pad = lds_pad_elems<P>();
@@ -86,15 +86,18 @@ struct ActorSmem {
         sch = o; o += dppo_align16(4 * a.KF * DPPO_SCHED_COLS);
         rn = o; o += dppo_align16(4 * ROWS);
         rj = o; o += dppo_align16(4 * ROWS);
+        bias = o; o += dppo_align16(4 * (3 * a.H + 16 * dppo_cdiv(a.XD, 16)));
         total = o;
     }
 };
 
-template <class P, int MT, int NT, int NO>
+template <class P, int MT, int NT, int NO, int KSI, bool TRAIN>
 __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a) {
     using AT = typename P::AT;
     constexpr int ROWS = 16 * MT;
-    constexpr int DEP = MT >= 2 ? 2 : 4;
+    constexpr int KSH = ksh_for<P>(NT);
+    constexpr int NOK = nok_for<P>(NT);
+    constexpr int KSO = 2;   // k-steps of the transposed out layer (out dim <= 2*KG, padded even)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const MlpLayout& L = a.L;
@@ -104,10 +107,12 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
     const int k1w = L.ks_in * P::KG, lda0 = k1w + pad;
     const int ktw = L.ks_out_t * P::KG;   // width of the dy tile (A operand of dh3 = dy W_out^T)
     const int XD = a.XD, SD = a.SD, TD = a.TD, KF = a.KF, IN = a.IN;
-    const bool train = a.mode == ROWS_TRAIN;
+    constexpr bool train = TRAIN;
+    const int H = a.H;
     AT* tA = (AT*)(smem + S.tA);
     AT* tB = (AT*)(smem + S.tB);
     AT* a0 = (AT*)(smem + S.a0);
+    float* bias = (float*)(smem + S.bias);   // [in, l1, l2][H], out[16*NO]
     float* xp = (float*)(smem + S.xp);
     float* xn = (float*)(smem + S.xn);
     float* st = (float*)(smem + S.st);
@@ -134,6 +139,11 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
         rn[tid] = n; rj[tid] = j;
     }
     for (int i = tid; i < KF * DPPO_SCHED_COLS; i += DPPO_THREADS) sch[i] = a.sched[i];
+    for (int i = tid; i < 3 * H + 16 * NO; i += DPPO_THREADS) {
+        const int seg = i < H ? SEG_B_IN : (i < 2 * H ? SEG_B_L1 : (i < 3 * H ? SEG_B_L2 : SEG_B_OUT));
+        const int j = i < 3 * H ? i % H : i - 3 * H;
+        bias[i] = ((const float*)(a.packed + L.off[seg]))[j];
+    }
     const int half = TD / 2;
     const float lnf = logf(10000.f) / (float)(half - 1);
     const float* tw = (const float*)(a.packed + L.off[SEG_TIME]);
@@ -194,11 +204,16 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
     __syncthreads();
 
     const int ntile0 = wave * NT;
+    auto W = [&](int seg) { return (const u32x4*)(a.packed + L.off[seg]); };
     f32x4 H1[MT][NT], acc[MT][NT];
     uint64_t mask1 = 0, mask2 = 0;
+    WRing<NT> R;
+    ring_prime(R, W(SEG_W_IN), KSI, ntile0, lane);
+    ORing<NOK, NO> ob;
+    out_prefetch(ob, W(SEG_W_OUT), KSH, wave, lane);
     // ---- L1: h1 = a0 W_in + b (no activation on the input layer) ----
-    gemm_wide<P, MT, NT, DEP>(a0, lda0, L.ks_in, (const u32x4*)(a.packed + L.off[SEG_W_IN]), ntile0, H1, lane);
-    add_bias(H1, (const float*)(a.packed + L.off[SEG_B_IN]), ntile0, lane);
+    gemm_stream<P, MT, NT, KSI>(a0, lda0, W(SEG_W_IN), ntile0, H1, lane, R, NextLayer{W(SEG_W_L1), KSH, ntile0});
+    add_bias(H1, bias, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -209,11 +224,11 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
                 if (H1[m][n][r] > 0.f) mask1 |= 1ull << ((m * NT + n) * 4 + r);
             }
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    if (train) store_accT<P, MT, NT>(a.ws.u1T, a.ws.ldm, ntile0, grow0, lane, acc);
-    __syncthreads();
+    if constexpr (train) store_accT<P, MT, NT>(a.ws.u1T, a.ws.ldm, ntile0, grow0, lane, acc);
+    lds_sync();
     // ---- L2: h2 = relu(h1) W_l1 + b ----
-    gemm_wide<P, MT, NT, DEP>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_L1]), ntile0, acc, lane);
-    add_bias(acc, (const float*)(a.packed + L.off[SEG_B_L1]), ntile0, lane);
+    gemm_stream<P, MT, NT, KSH>(tA, ldh, W(SEG_W_L1), ntile0, acc, lane, R, NextLayer{W(SEG_W_L2), KSH, ntile0});
+    add_bias(acc, bias + H, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -224,11 +239,12 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
                 acc[m][n][r] = fmaxf(acc[m][n][r], 0.f);
             }
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
-    if (train) store_accT<P, MT, NT>(a.ws.u2T, a.ws.ldm, ntile0, grow0, lane, acc);
-    __syncthreads();
-    // ---- L3: h3 = relu(h2) W_l2 + b + h1 ----
-    gemm_wide<P, MT, NT, DEP>(tB, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_L2]), ntile0, acc, lane);
-    add_bias(acc, (const float*)(a.packed + L.off[SEG_B_L2]), ntile0, lane);
+    if constexpr (train) store_accT<P, MT, NT>(a.ws.u2T, a.ws.ldm, ntile0, grow0, lane, acc);
+    lds_sync();
+    // ---- L3: h3 = relu(h2) W_l2 + b + h1; the stream continues into the backward's W_out^T ----
+    gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_W_L2), ntile0, acc, lane, R,
+                                train ? NextLayer{W(SEG_T_OUT), KSO, ntile0} : NextLayer{W(SEG_W_L2), KSH, ntile0});
+    add_bias(acc, bias + 2 * H, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -236,12 +252,12 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[m][n][r] += H1[m][n][r];
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    if (train) store_accT<P, MT, NT>(a.ws.h3T, a.ws.ldm, ntile0, grow0, lane, acc);
-    __syncthreads();
-    // ---- L4: eps = h3 W_out + b (k split over the waves) ----
+    if constexpr (train) store_accT<P, MT, NT>(a.ws.h3T, a.ws.ldm, ntile0, grow0, lane, acc);
+    lds_sync();
+    // ---- L4: eps = h3 W_out + b (k split over the waves, fragments prefetched before L1) ----
     {
         f32x4 po[MT][NO];
-        gemm_narrow<P, MT, NO>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_OUT]), po, wave, lane);
+        gemm_narrow_pre<P, MT, NOK, NO>(tA, ldh, ob, po, wave, lane);
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -250,13 +266,13 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
                 for (int r = 0; r < 4; ++r)
                     part[(wave * ROWS + m * 16 + crow(lane, r)) * (16 * NO) + n * 16 + ccol(lane)] = po[m][n][r];
     }
-    __syncthreads();
+    lds_sync();
 
     // ---- epilogue: p_mean_var + Normal.log_prob (+ c_loss policy term and its gradient) ----
     if (wave == 0 && lane < ROWS) {
         const int r = lane, n = rn[r], j = rj[r], t = KF - 1 - j;
         const bool valid = n >= 0;
-        const float* bo = (const float*)(a.packed + L.off[SEG_B_OUT]);
+        const float* bo = bias + 3 * H;
         const float* sc = sch + t * DPPO_SCHED_COLS;
         const float sd = fminf(fmaxf(expf(0.5f * sc[4]), a.hp.min_lp_std), 1e6f);   // diffusion_vpg.py:473-474
         const float inv_var = 1.f / (sd * sd);
@@ -341,18 +357,18 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
             }
         }
     }
-    if (!train) return;
-    __syncthreads();
+    if constexpr (!train) return;
+    lds_sync();
 
-    // ---- backward dX chain ----
+    // ---- backward dX chain (weights continue in the same stream) ----
     // B4: dh3 = dy W_out^T
     f32x4 DH3[MT][NT];
-    gemm_wide<P, MT, NT, DEP>(a0, lda0, L.ks_out_t, (const u32x4*)(a.packed + L.off[SEG_T_OUT]), ntile0, DH3, lane);
+    gemm_stream<P, MT, NT, KSO>(a0, lda0, W(SEG_T_OUT), ntile0, DH3, lane, R, NextLayer{W(SEG_T_L2), KSH, ntile0});
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, DH3);
     store_accT<P, MT, NT>(a.ws.dh3T, a.ws.ldm, ntile0, grow0, lane, DH3);
-    __syncthreads();
+    lds_sync();
     // B3: dh2 = (dh3 W_l2^T) * relu'(h2)
-    gemm_wide<P, MT, NT, DEP>(tB, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_T_L2]), ntile0, acc, lane);
+    gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_T_L2), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -362,9 +378,9 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
                 if (!((mask2 >> ((m * NT + n) * 4 + r)) & 1ull)) acc[m][n][r] = 0.f;
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
     store_accT<P, MT, NT>(a.ws.dh2T, a.ws.ldm, ntile0, grow0, lane, acc);
-    __syncthreads();
+    lds_sync();
     // B2: dh1 = dh3 + (dh2 W_l1^T) * relu'(h1)
-    gemm_wide<P, MT, NT, DEP>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_T_L1]), ntile0, acc, lane);
+    gemm_stream<P, MT, NT, KSH>(tA, ldh, W(SEG_T_L1), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -383,7 +399,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
 template <class P, int MT>
 struct CriticSmem {
     static constexpr int ROWS = 16 * MT;
-    size_t tA, tB, a0, rn, rv, total;
+    size_t tA, tB, a0, rn, rv, bias, total;
     __host__ __device__ CriticSmem(const CriticArgs& a) {
         using AT = typename P::AT;
         const int pad = lds_pad_elems<P>();
@@ -395,15 +411,18 @@ struct CriticSmem {
         a0 = o; o += dppo_align16(sizeof(AT) * ROWS * ka);
         rn = o; o += dppo_align16(4 * ROWS);
         rv = o; o += dppo_align16(4 * ROWS);
+        bias = o; o += dppo_align16(4 * (3 * a.HC + 16));
         total = o;
     }
 };
 
-template <class P, int MT, int NT>
+template <class P, int MT, int NT, bool TRAIN>
 __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs a) {
     using AT = typename P::AT;
     constexpr int ROWS = 16 * MT;
-    constexpr int DEP = MT >= 2 ? 2 : 4;
+    constexpr int KSH = ksh_for<P>(NT);
+    constexpr int NOK = nok_for<P>(NT);
+    constexpr int KSI = 2, KSO = 2;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const MlpLayout& L = a.L;
@@ -413,12 +432,19 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
     const int lda0 = (L.ks_in > L.ks_out_t ? L.ks_in : L.ks_out_t) * P::KG + pad;
     const int k1w = L.ks_in * P::KG, ktw = L.ks_out_t * P::KG;
     const int SD = a.SD;
-    const bool train = a.mode == ROWS_TRAIN;
+    constexpr bool train = TRAIN;
+    const int HC = a.HC;
     AT* tA = (AT*)(smem + S.tA);
     AT* tB = (AT*)(smem + S.tB);
     AT* a0 = (AT*)(smem + S.a0);
     int* rn = (int*)(smem + S.rn);
+    float* bias = (float*)(smem + S.bias);
     float* part = (float*)(smem + S.tB);
+    for (int i = tid; i < 3 * HC + 16; i += DPPO_THREADS) {
+        const int seg = i < HC ? SEG_B_IN : (i < 2 * HC ? SEG_B_L1 : (i < 3 * HC ? SEG_B_L2 : SEG_B_OUT));
+        const int j = i < 3 * HC ? i % HC : i - 3 * HC;
+        bias[i] = ((const float*)(a.packed + L.off[seg]))[j];
+    }
     const size_t grow0 = (size_t)blockIdx.x * ROWS;
 
     if (tid < ROWS) {
@@ -448,10 +474,15 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
     __syncthreads();
 
     const int ntile0 = wave * NT;
+    auto W = [&](int seg) { return (const u32x4*)(a.packed + L.off[seg]); };
     f32x4 H1[MT][NT], H2[MT][NT], acc[MT][NT];
+    WRing<NT> R;
+    ring_prime(R, W(SEG_W_IN), KSI, ntile0, lane);
+    ORing<NOK, 1> ob;
+    out_prefetch(ob, W(SEG_W_OUT), KSH, wave, lane);
     // L1: h1 = s W_in + b
-    gemm_wide<P, MT, NT, DEP>(a0, lda0, L.ks_in, (const u32x4*)(a.packed + L.off[SEG_W_IN]), ntile0, H1, lane);
-    add_bias(H1, (const float*)(a.packed + L.off[SEG_B_IN]), ntile0, lane);
+    gemm_stream<P, MT, NT, KSI>(a0, lda0, W(SEG_W_IN), ntile0, H1, lane, R, NextLayer{W(SEG_W_L1), KSH, ntile0});
+    add_bias(H1, bias, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -459,11 +490,11 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[m][n][r] = mishf(H1[m][n][r]);
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    if (train) store_accT<P, MT, NT>(a.ws.cu1T, a.ws.ldm, ntile0, grow0, lane, acc);
-    __syncthreads();
+    if constexpr (train) store_accT<P, MT, NT>(a.ws.cu1T, a.ws.ldm, ntile0, grow0, lane, acc);
+    lds_sync();
     // L2: h2 = mish(h1) W_l1 + b
-    gemm_wide<P, MT, NT, DEP>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_L1]), ntile0, H2, lane);
-    add_bias(H2, (const float*)(a.packed + L.off[SEG_B_L1]), ntile0, lane);
+    gemm_stream<P, MT, NT, KSH>(tA, ldh, W(SEG_W_L1), ntile0, H2, lane, R, NextLayer{W(SEG_W_L2), KSH, ntile0});
+    add_bias(H2, bias + HC, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -471,11 +502,12 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[m][n][r] = mishf(H2[m][n][r]);
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
-    if (train) store_accT<P, MT, NT>(a.ws.cu2T, a.ws.ldm, ntile0, grow0, lane, acc);
-    __syncthreads();
+    if constexpr (train) store_accT<P, MT, NT>(a.ws.cu2T, a.ws.ldm, ntile0, grow0, lane, acc);
+    lds_sync();
     // L3: h3 = mish(h2) W_l2 + b + h1
-    gemm_wide<P, MT, NT, DEP>(tB, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_L2]), ntile0, acc, lane);
-    add_bias(acc, (const float*)(a.packed + L.off[SEG_B_L2]), ntile0, lane);
+    gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_W_L2), ntile0, acc, lane, R,
+                                train ? NextLayer{W(SEG_T_OUT), KSO, ntile0} : NextLayer{W(SEG_W_L2), KSH, ntile0});
+    add_bias(acc, bias + 2 * HC, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -483,21 +515,21 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[m][n][r] += H1[m][n][r];
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    if (train) store_accT<P, MT, NT>(a.ws.ch3T, a.ws.ldm, ntile0, grow0, lane, acc);
-    __syncthreads();
+    if constexpr (train) store_accT<P, MT, NT>(a.ws.ch3T, a.ws.ldm, ntile0, grow0, lane, acc);
+    lds_sync();
     // L4: V = h3 W_out + b
     {
         f32x4 po[MT][1];
-        gemm_narrow<P, MT, 1>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_W_OUT]), po, wave, lane);
+        gemm_narrow_pre<P, MT, NOK, 1>(tA, ldh, ob, po, wave, lane);
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int r = 0; r < 4; ++r) part[(wave * ROWS + m * 16 + crow(lane, r)) * 16 + ccol(lane)] = po[m][0][r];
     }
-    __syncthreads();
+    lds_sync();
     if (wave == 0 && lane < ROWS) {
         const int r = lane, n = rn[r];
-        float V = ((const float*)(a.packed + L.off[SEG_B_OUT]))[0];
+        float V = bias[3 * HC];
 #pragma unroll
         for (int w = 0; w < DPPO_WAVES; ++w) V += part[(w * ROWS + r) * 16];
         if (!train) {
@@ -515,16 +547,16 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
             if (lane == 0) atomic_add_metric(a.metrics, 1, vl);
         }
     }
-    if (!train) return;
-    __syncthreads();
+    if constexpr (!train) return;
+    lds_sync();
     // B4: dh3 = dV W_out^T
     f32x4 DH3[MT][NT];
-    gemm_wide<P, MT, NT, DEP>(a0, lda0, L.ks_out_t, (const u32x4*)(a.packed + L.off[SEG_T_OUT]), ntile0, DH3, lane);
+    gemm_stream<P, MT, NT, KSO>(a0, lda0, W(SEG_T_OUT), ntile0, DH3, lane, R, NextLayer{W(SEG_T_L2), KSH, ntile0});
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, DH3);
     store_accT<P, MT, NT>(a.ws.cdh3T, a.ws.ldm, ntile0, grow0, lane, DH3);
-    __syncthreads();
+    lds_sync();
     // B3: dh2 = (dh3 W_l2^T) * mish'(h2)
-    gemm_wide<P, MT, NT, DEP>(tB, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_T_L2]), ntile0, acc, lane);
+    gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_T_L2), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -533,9 +565,9 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
             for (int r = 0; r < 4; ++r) acc[m][n][r] *= mish_gradf(H2[m][n][r]);
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
     store_accT<P, MT, NT>(a.ws.cdh2T, a.ws.ldm, ntile0, grow0, lane, acc);
-    __syncthreads();
+    lds_sync();
     // B2: dh1 = dh3 + (dh2 W_l1^T) * mish'(h1)
-    gemm_wide<P, MT, NT, DEP>(tA, ldh, L.ks_h, (const u32x4*)(a.packed + L.off[SEG_T_L1]), ntile0, acc, lane);
+    gemm_stream<P, MT, NT, KSH>(tA, ldh, W(SEG_T_L1), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -548,15 +580,17 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
 // =============================================================================================
 // launchers
 // =============================================================================================
-template <class P, int MT, int NT, int NO>
+template <class P, int MT, int NT, int NO, int KSI, bool TRAIN>
 static int launch_actor_t(const ActorArgs& a, hipStream_t s) {
+    if (a.L.ks_in != KSI || a.L.ks_h != ksh_for<P>(NT) || a.L.ks_out_t != 2 || a.L.ks_h != DPPO_WAVES * nok_for<P>(NT))
+        return dppo_set_error(DPPO_EUNSUPPORTED, "actor row tile: layout does not match the instantiation");
     const ActorSmem<P, MT> S(a);
     const int pad = lds_pad_elems<P>();
     const size_t part_bytes = (size_t)4 * DPPO_WAVES * 16 * MT * 16 * NO;
     const size_t tb_bytes = sizeof(typename P::AT) * 16 * MT * (a.H + pad);
     if (part_bytes > tb_bytes) return dppo_set_error(DPPO_EUNSUPPORTED, "actor: partial buffer does not fit");
     if (S.total > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "actor row tile needs %zu B LDS", S.total);
-    auto k = actor_rowtile_kernel<P, MT, NT, NO>;
+    auto k = actor_rowtile_kernel<P, MT, NT, NO, KSI, TRAIN>;
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S.total));
     // TRAIN mode covers every row of the 64-padded feature-major images (padding rows get
     // finite activations and zero gradients), so the dW kernel never reads unwritten memory
@@ -568,13 +602,24 @@ static int launch_actor_t(const ActorArgs& a, hipStream_t s) {
     return DPPO_OK;
 }
 
+template <class P, int MT, int NT, int NO, int KSI>
+static int launch_actor_m(const ActorArgs& a, hipStream_t s) {
+    return a.mode == ROWS_TRAIN ? launch_actor_t<P, MT, NT, NO, KSI, true>(a, s)
+                                : launch_actor_t<P, MT, NT, NO, KSI, false>(a, s);
+}
+
 template <class P, int MT>
 static int dispatch_actor(const ActorArgs& a, hipStream_t s) {
-    const int NT = a.H / (16 * DPPO_WAVES), NO = dppo_cdiv(a.XD, 16);
-    if (NT == 4 && NO == 1) return launch_actor_t<P, MT, 4, 1>(a, s);
-    if (NT == 4 && NO == 2) return launch_actor_t<P, MT, 4, 2>(a, s);
-    if (NT == 2 && NO == 1) return launch_actor_t<P, MT, 2, 1>(a, s);
-    if (NT == 2 && NO == 2) return launch_actor_t<P, MT, 2, 2>(a, s);
+    const int NT = a.H / (16 * DPPO_WAVES), NO = dppo_cdiv(a.XD, 16), KSI = a.L.ks_in;
+#define DPPO_ACTOR_CASE(nt, no, ksi) \
+    if (NT == nt && NO == no && KSI == ksi) return launch_actor_m<P, MT, nt, no, ksi>(a, s);
+    if constexpr (P::KG == 32) {   // bf16: the in-layer is 2 k-steps up to 64 inputs, 4 up to 128
+        DPPO_ACTOR_CASE(4, 1, 2) DPPO_ACTOR_CASE(4, 2, 2) DPPO_ACTOR_CASE(4, 1, 4) DPPO_ACTOR_CASE(4, 2, 4)
+        DPPO_ACTOR_CASE(2, 1, 2) DPPO_ACTOR_CASE(2, 2, 2) DPPO_ACTOR_CASE(2, 1, 4) DPPO_ACTOR_CASE(2, 2, 4)
+    } else {                       // fp32: 33..64 inputs -> 4 k-steps
+        DPPO_ACTOR_CASE(4, 1, 4) DPPO_ACTOR_CASE(4, 2, 4) DPPO_ACTOR_CASE(2, 1, 4) DPPO_ACTOR_CASE(2, 2, 4)
+    }
+#undef DPPO_ACTOR_CASE
     return dppo_set_error(DPPO_EUNSUPPORTED, "actor: hidden %d / chunk %d not instantiated", a.H, a.XD);
 }
 
@@ -585,11 +630,13 @@ int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
     return precision == DPPO_BF16 ? dispatch_actor<PolicyBF16, 2>(a, s) : dispatch_actor<PolicyF32, 2>(a, s);
 }
 
-template <class P, int MT, int NT>
+template <class P, int MT, int NT, bool TRAIN>
 static int launch_critic_t(const CriticArgs& a, hipStream_t s) {
+    if (a.L.ks_in != 2 || a.L.ks_h != ksh_for<P>(NT) || a.L.ks_out_t != 2 || a.L.ks_h != DPPO_WAVES * nok_for<P>(NT))
+        return dppo_set_error(DPPO_EUNSUPPORTED, "critic row tile: layout does not match the instantiation");
     const CriticSmem<P, MT> S(a);
     if (S.total > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "critic row tile needs %zu B LDS", S.total);
-    auto k = critic_rowtile_kernel<P, MT, NT>;
+    auto k = critic_rowtile_kernel<P, MT, NT, TRAIN>;
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S.total));
     // TRAIN mode covers every row of the 64-padded feature-major images (padding rows get
     // finite activations and zero gradients), so the dW kernel never reads unwritten memory
@@ -604,8 +651,8 @@ static int launch_critic_t(const CriticArgs& a, hipStream_t s) {
 template <class P, int MT>
 static int dispatch_critic(const CriticArgs& a, hipStream_t s) {
     const int NT = a.HC / (16 * DPPO_WAVES);
-    if (NT == 2) return launch_critic_t<P, MT, 2>(a, s);
-    if (NT == 1) return launch_critic_t<P, MT, 1>(a, s);
+    const bool tr = a.mode == ROWS_TRAIN;
+    if (NT == 2) return tr ? launch_critic_t<P, MT, 2, true>(a, s) : launch_critic_t<P, MT, 2, false>(a, s);
     return dppo_set_error(DPPO_EUNSUPPORTED, "critic: hidden %d not instantiated", a.HC);
 }
 

@@ -27,15 +27,23 @@ struct SampleArgs {
     MlpLayout L;          // same layout for base and ft
 };
 
-template <class P, int NT, int NO>
-__global__ __launch_bounds__(DPPO_THREADS) void sample_kernel(SampleArgs a) {
+// 16 waves per workgroup: each wave streams NT = H/256 n-tiles, so a CU keeps twice the weight
+// fragments in flight of an 8-wave layout at the same ring depth.
+#define SW 16
+#define ST (SW * 64)
+
+template <class P, int NT, int NO, int KSI, bool INJ>
+__global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
     using AT = typename P::AT;
+    constexpr int KSH = ksh_for<P>(NT, SW);
+    constexpr int NOK = KSH / SW;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int row0 = blockIdx.x * 16;
     const MlpLayout& L = a.L;
     const int pad = lds_pad_elems<P>();
-    const int ldh = a.H + pad;
+    const int H = a.H;
+    const int ldh = H + pad;
     const int k1w = L.ks_in * P::KG;
     const int lda0 = k1w + pad;
     const int XD = a.XD, SD = a.SD, TD = a.TD, K = a.K, KF = a.KF;
@@ -50,16 +58,37 @@ __global__ __launch_bounds__(DPPO_THREADS) void sample_kernel(SampleArgs a) {
     float* st = (float*)(smem + o); o += dppo_align16(4 * 16 * SD);
     float* temb = (float*)(smem + o); o += dppo_align16(4 * K * TD);
     float* ta1 = (float*)(smem + o); o += dppo_align16(4 * K * 2 * TD);
-    float* part = (float*)(smem + o); o += dppo_align16(4 * DPPO_WAVES * 16 * NOC);
+    float* part = (float*)(smem + o); o += dppo_align16(4 * SW * 16 * NOC);
     float* sch = (float*)(smem + o); o += dppo_align16(4 * K * DPPO_SCHED_COLS);
+    float* bias = (float*)(smem + o); o += dppo_align16(4 * 2 * (3 * H + NOC));  // [actor][in,l1,l2,out]
+    float* zt = (float*)(smem + o); o += dppo_align16(4 * K * 16 * XD);           // clipped noise [i][row][q]
 
-    // ---- prologue: schedule, state, x_T, time-embedding table ----
-    for (int i = tid; i < K * DPPO_SCHED_COLS; i += DPPO_THREADS) sch[i] = a.sched[i];
-    for (int i = tid; i < 16 * SD; i += DPPO_THREADS) {
+    // ---- prologue: schedule, biases, state, x_T, time-embedding table ----
+    for (int i = tid; i < K * DPPO_SCHED_COLS; i += ST) sch[i] = a.sched[i];
+    for (int i = tid; i < 2 * (3 * H + NOC); i += ST) {
+        const int w = i / (3 * H + NOC), j = i % (3 * H + NOC);
+        const uint8_t* PK = w ? a.packed_ft : a.packed_base;
+        float v;
+        if (j < H) v = ((const float*)(PK + L.off[SEG_B_IN]))[j];
+        else if (j < 2 * H) v = ((const float*)(PK + L.off[SEG_B_L1]))[j - H];
+        else if (j < 3 * H) v = ((const float*)(PK + L.off[SEG_B_L2]))[j - 2 * H];
+        else v = ((const float*)(PK + L.off[SEG_B_OUT]))[j - 3 * H];
+        bias[i] = v;
+    }
+    for (int i = tid; i < 16 * SD; i += ST) {
         const int r = i / SD, c = i % SD, row = row0 + r;
         st[i] = row < a.E ? a.cond[(size_t)row * SD + c] : 0.f;
     }
-    for (int i = tid; i < 16 * XD; i += DPPO_THREADS) {
+    // all K steps' noise up front (injected, or the Philox stream), clipped to +-randn_clip (:319),
+    // so the denoising loop carries no RNG state and issues no global loads outside the weight stream
+    for (int i = tid; i < K * 16 * XD; i += ST) {
+        const int step = i / (16 * XD), r = (i / XD) % 16, q = i % XD, row = row0 + r;
+        float z;
+        if constexpr (INJ) z = row < a.E ? a.noise[((size_t)step * a.E + row) * XD + q] : 0.f;
+        else z = philox_normal(a.seed, (uint32_t)(q >> 2), (uint32_t)(a.env_offset + row), (uint32_t)step, a.call_id, q & 3);
+        zt[i] = fminf(fmaxf(z, -a.randn_clip), a.randn_clip);
+    }
+    for (int i = tid; i < 16 * XD; i += ST) {
         const int r = i / XD, q = i % XD, row = row0 + r;
         float x;
         if (a.x_T) x = row < a.E ? a.x_T[(size_t)row * XD + q] : 0.f;
@@ -70,37 +99,42 @@ __global__ __launch_bounds__(DPPO_THREADS) void sample_kernel(SampleArgs a) {
     // time MLP (mlp_diffusion.py:40-45): SinusoidalPosEmb -> Dense(TD->2TD, mish) -> Dense(2TD->TD)
     const int half = TD / 2;
     const float lnf = logf(10000.f) / (float)(half - 1);
-    for (int i = tid; i < K * 2 * TD; i += DPPO_THREADS) {
+    for (int i = tid; i < K * 2 * TD; i += ST) {
         const int t = i / (2 * TD), j = i % (2 * TD);
         const float* tw = (const float*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIME]);
-        const float* w1 = tw;                       // [TD][2TD]
-        const float* b1 = tw + TD * 2 * TD;         // [2TD]
-        float acc = b1[j];
+        float acc = tw[TD * 2 * TD + j];
         for (int k = 0; k < TD; ++k) {
             const float f = expf(-(float)(k % half) * lnf) * (float)t;
-            const float e = k < half ? sinf(f) : cosf(f);
-            acc += e * w1[k * 2 * TD + j];
+            acc += (k < half ? sinf(f) : cosf(f)) * tw[k * 2 * TD + j];
         }
         ta1[i] = mishf(acc);
     }
     __syncthreads();
-    for (int i = tid; i < K * TD; i += DPPO_THREADS) {
+    for (int i = tid; i < K * TD; i += ST) {
         const int t = i / TD, j = i % TD;
         const float* tw = (const float*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIME]);
         const float* w2 = tw + TD * 2 * TD + 2 * TD;  // [2TD][TD]
-        const float* b2 = w2 + 2 * TD * TD;           // [TD]
-        float acc = b2[j];
+        float acc = w2[2 * TD * TD + j];
         for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + j];
         temb[i] = acc;
     }
     __syncthreads();
 
     const int ntile0 = wave * NT;
+    auto W = [&](const uint8_t* PK, int seg) { return (const u32x4*)(PK + L.off[seg]); };
+    // the stream starts with step 0's in-layer (t = K-1)
+    WRing<NT> R;
+    ring_prime(R, W(K - 1 < KF ? a.packed_ft : a.packed_base, SEG_W_IN), L.ks_in, ntile0, lane);
     for (int i = 0; i < K; ++i) {
         const int t = K - 1 - i;
-        const uint8_t* PK = t < KF ? a.packed_ft : a.packed_base;
+        const int is_ft = t < KF;
+        const uint8_t* PK = is_ft ? a.packed_ft : a.packed_base;
+        const uint8_t* PKn = (t - 1 >= 0 && t - 1 < KF) ? a.packed_ft : (t - 1 >= 0 ? a.packed_base : PK);
+        const float* bb = bias + is_ft * (3 * H + NOC);
+        ORing<NOK, NO> ob;                                 // out-layer fragments, consumed 3 layers later
+        out_prefetch<NOK, NO, SW>(ob, W(PK, SEG_W_OUT), L.ks_h, wave, lane);
         // a) a0 = [x, temb(t), state, 0-pad]
-        for (int idx = tid; idx < 16 * k1w; idx += DPPO_THREADS) {
+        for (int idx = tid; idx < 16 * k1w; idx += ST) {
             const int r = idx / k1w, c = idx % k1w;
             float v = 0.f;
             if (c < XD) v = xs[r * XD + c];
@@ -108,68 +142,62 @@ __global__ __launch_bounds__(DPPO_THREADS) void sample_kernel(SampleArgs a) {
             else if (c < a.IN) v = st[r * SD + c - XD - TD];
             a0[r * lda0 + c] = P::cvt(v);
         }
-        __syncthreads();
+        lds_sync();
         // b) in-Dense: h1 = a0 W_in + b_in  (no activation after the input layer, mlp.py:144)
         f32x4 h1[1][NT], acc[1][NT];
-        gemm_wide<P, 1, NT, 3>(a0, lda0, L.ks_in, (const u32x4*)(PK + L.off[SEG_W_IN]), ntile0, h1, lane);
-        {
-            const float* bb = (const float*)(PK + L.off[SEG_B_IN]);
+        gemm_stream<P, 1, NT, KSI>(a0, lda0, W(PK, SEG_W_IN), ntile0, h1, lane, R,
+                              NextLayer{W(PK, SEG_W_L1), L.ks_h, ntile0});
 #pragma unroll
-            for (int n = 0; n < NT; ++n) {
-                const int col = (ntile0 + n) * 16 + ccol(lane);
-                const float bv = bb[col];
+        for (int n = 0; n < NT; ++n) {
+            const int col = (ntile0 + n) * 16 + ccol(lane);
+            const float bv = bb[col];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    h1[0][n][r] += bv;
-                    tA[crow(lane, r) * ldh + col] = P::cvt(fmaxf(h1[0][n][r], 0.f));
-                }
+            for (int r = 0; r < 4; ++r) {
+                h1[0][n][r] += bv;
+                tA[crow(lane, r) * ldh + col] = P::cvt(fmaxf(h1[0][n][r], 0.f));
             }
         }
-        __syncthreads();
+        lds_sync();
         // c) l1: relu(h1) W_l1 + b -> relu -> tB   (pre-activation block, mlp.py:192-193,202-203)
-        gemm_wide<P, 1, NT, 3>(tA, ldh, L.ks_h, (const u32x4*)(PK + L.off[SEG_W_L1]), ntile0, acc, lane);
-        {
-            const float* bb = (const float*)(PK + L.off[SEG_B_L1]);
+        gemm_stream<P, 1, NT, KSH>(tA, ldh, W(PK, SEG_W_L1), ntile0, acc, lane, R,
+                              NextLayer{W(PK, SEG_W_L2), L.ks_h, ntile0});
 #pragma unroll
-            for (int n = 0; n < NT; ++n) {
-                const int col = (ntile0 + n) * 16 + ccol(lane);
-                const float bv = bb[col];
+        for (int n = 0; n < NT; ++n) {
+            const int col = (ntile0 + n) * 16 + ccol(lane);
+            const float bv = bb[H + col];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) tB[crow(lane, r) * ldh + col] = P::cvt(fmaxf(acc[0][n][r] + bv, 0.f));
-            }
+            for (int r = 0; r < 4; ++r) tB[crow(lane, r) * ldh + col] = P::cvt(fmaxf(acc[0][n][r] + bv, 0.f));
         }
-        __syncthreads();
-        // d) l2: relu(h2) W_l2 + b + h1 (residual, mlp.py:206) -> tA (no activation before out-Dense)
-        gemm_wide<P, 1, NT, 3>(tB, ldh, L.ks_h, (const u32x4*)(PK + L.off[SEG_W_L2]), ntile0, acc, lane);
-        {
-            const float* bb = (const float*)(PK + L.off[SEG_B_L2]);
+        lds_sync();
+        // d) l2: relu(h2) W_l2 + b + h1 (residual, mlp.py:206) -> tA; the stream moves on to the
+        //    next denoising step's in-layer (possibly the other actor)
+        gemm_stream<P, 1, NT, KSH>(tB, ldh, W(PK, SEG_W_L2), ntile0, acc, lane, R,
+                              NextLayer{W(PKn, SEG_W_IN), L.ks_in, ntile0});
 #pragma unroll
-            for (int n = 0; n < NT; ++n) {
-                const int col = (ntile0 + n) * 16 + ccol(lane);
-                const float bv = bb[col];
+        for (int n = 0; n < NT; ++n) {
+            const int col = (ntile0 + n) * 16 + ccol(lane);
+            const float bv = bb[2 * H + col];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) tA[crow(lane, r) * ldh + col] = P::cvt(acc[0][n][r] + bv + h1[0][n][r]);
-            }
+            for (int r = 0; r < 4; ++r) tA[crow(lane, r) * ldh + col] = P::cvt(acc[0][n][r] + bv + h1[0][n][r]);
         }
-        __syncthreads();
+        lds_sync();
         // e) out-Dense (N = XD <= 16*NO): k split over the 8 waves, partials through LDS
         {
             f32x4 po[1][NO];
-            gemm_narrow<P, 1, NO>(tA, ldh, L.ks_h, (const u32x4*)(PK + L.off[SEG_W_OUT]), po, wave, lane);
+            gemm_narrow_pre<P, 1, NOK, NO, SW>(tA, ldh, ob, po, wave, lane);
 #pragma unroll
             for (int n = 0; n < NO; ++n)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     part[(wave * 16 + crow(lane, r)) * NOC + n * 16 + ccol(lane)] = po[0][n][r];
         }
-        __syncthreads();
+        lds_sync();
         // f) DDPM epilogue, fp32 (diffusion_vpg.py:198-243, 301-320)
         if (tid < 16 * XD) {
             const int r = tid / XD, q = tid % XD, row = row0 + r;
-            const float* bo = (const float*)(PK + L.off[SEG_B_OUT]);
-            float eps = bo[q];
+            float eps = bb[3 * H + q];
 #pragma unroll
-            for (int w = 0; w < DPPO_WAVES; ++w) eps += part[(w * 16 + r) * NOC + q];
+            for (int w = 0; w < SW; ++w) eps += part[(w * 16 + r) * NOC + q];
             const float* sc = sch + t * DPPO_SCHED_COLS;
             const float x = xs[tid];
             float xr = sc[0] * x - sc[1] * eps;
@@ -179,11 +207,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void sample_kernel(SampleArgs a) {
             if (a.deterministic && t == 0) sd = 0.f;
             else if (a.deterministic) sd = fminf(fmaxf(sd, 1e-3f), 1e6f);
             else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
-            float z;
-            if (a.noise) z = row < a.E ? a.noise[((size_t)i * a.E + row) * XD + q] : 0.f;
-            else z = philox_normal(a.seed, (uint32_t)(q >> 2), (uint32_t)(a.env_offset + row), (uint32_t)i, a.call_id, q & 3);
-            z = fminf(fmaxf(z, -a.randn_clip), a.randn_clip);
-            float xn = mu + sd * z;
+            float xn = mu + sd * zt[i * 16 * XD + tid];
             if (a.final_clip > 0.f && i == K - 1) xn = fminf(fmaxf(xn, -a.final_clip), a.final_clip);
             xs[tid] = xn;
             if (row < a.E) {
@@ -191,7 +215,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void sample_kernel(SampleArgs a) {
                 if (i == K - 1) a.actions[(size_t)row * XD + q] = xn;
             }
         }
-        __syncthreads();
+        lds_sync();
     }
 }
 
@@ -208,33 +232,47 @@ static size_t sample_lds_bytes(const SampleArgs& a, int NO) {
     o += dppo_align16(4 * 16 * a.SD);
     o += dppo_align16(4 * a.K * a.TD);
     o += dppo_align16(4 * a.K * 2 * a.TD);
-    o += dppo_align16(4 * DPPO_WAVES * 16 * 16 * NO);
+    o += dppo_align16(4 * SW * 16 * 16 * NO);
     o += dppo_align16(4 * a.K * DPPO_SCHED_COLS);
+    o += dppo_align16(4 * 2 * (3 * a.H + 16 * NO));
+    o += dppo_align16(4 * a.K * 16 * a.XD);
     return o;
 }
 
-template <class P, int NT, int NO>
-static int launch_sample(const SampleArgs& a, hipStream_t s) {
+template <class P, int NT, int NO, int KSI, bool INJ>
+static int launch_sample_k(const SampleArgs& a, hipStream_t s) {
+    if (a.L.ks_h != ksh_for<P>(NT, SW) || a.L.ks_in != KSI || a.L.ks_h % SW != 0)
+        return dppo_set_error(DPPO_EUNSUPPORTED, "sampler: hidden %d not supported at this precision", a.H);
     const size_t lds = sample_lds_bytes<P>(a, NO);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "sampler needs %zu B of LDS", lds);
-    auto k = sample_kernel<P, NT, NO>;
+    auto k = sample_kernel<P, NT, NO, KSI, INJ>;
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k, dim3(dppo_cdiv(a.E, 16)), dim3(DPPO_THREADS), lds, s, a);
+    hipLaunchKernelGGL(k, dim3(dppo_cdiv(a.E, 16)), dim3(ST), lds, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
 
+template <class P, int NT, int NO, int KSI>
+static int launch_sample(const SampleArgs& a, hipStream_t s) {
+    if (a.noise) return launch_sample_k<P, NT, NO, KSI, true>(a, s);
+    return launch_sample_k<P, NT, NO, KSI, false>(a, s);
+}
+
 template <class P>
 static int dispatch_sample(const SampleArgs& a, hipStream_t s) {
-    const int NT = a.H / (16 * DPPO_WAVES);
+    const int NT = a.H / (16 * SW);
     const int NO = dppo_cdiv(a.XD, 16);
-    if (NT == 4 && NO == 1) return launch_sample<P, 4, 1>(a, s);
-    if (NT == 4 && NO == 2) return launch_sample<P, 4, 2>(a, s);
-    if (NT == 2 && NO == 1) return launch_sample<P, 2, 1>(a, s);
-    if (NT == 2 && NO == 2) return launch_sample<P, 2, 2>(a, s);
-    if (NT == 1 && NO == 1) return launch_sample<P, 1, 1>(a, s);
-    if (NT == 1 && NO == 2) return launch_sample<P, 1, 2>(a, s);
-    return dppo_set_error(DPPO_EUNSUPPORTED, "sampler: hidden %d / action chunk %d not instantiated", a.H, a.XD);
+    const int KSI = a.L.ks_in;
+#define DPPO_SAMPLE_CASE(nt, no, ksi) \
+    if (NT == nt && NO == no && KSI == ksi) return launch_sample<P, nt, no, ksi>(a, s);
+    if constexpr (P::KG == 32) {   // bf16: H = 512 (NT 2) or 256 (NT 1)
+        DPPO_SAMPLE_CASE(2, 1, 2) DPPO_SAMPLE_CASE(2, 2, 2) DPPO_SAMPLE_CASE(2, 1, 4) DPPO_SAMPLE_CASE(2, 2, 4)
+    } else {                       // fp32: H = 512 or 256
+        DPPO_SAMPLE_CASE(2, 1, 4) DPPO_SAMPLE_CASE(2, 2, 4) DPPO_SAMPLE_CASE(1, 1, 4) DPPO_SAMPLE_CASE(1, 2, 4)
+    }
+#undef DPPO_SAMPLE_CASE
+    return dppo_set_error(DPPO_EUNSUPPORTED, "sampler: hidden %d / action chunk %d / in-layer k-steps %d not instantiated",
+                          a.H, a.XD, KSI);
 }
 
 extern "C" int dppo_sample(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
