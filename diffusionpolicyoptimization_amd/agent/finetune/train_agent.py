@@ -11,6 +11,7 @@ import torch.distributed as dist
 
 from ...env.gym_utils import make_async
 from ...util.config import instantiate
+from ...util.dist import shard_envs
 
 log = logging.getLogger(__name__)
 
@@ -46,12 +47,8 @@ class TrainAgent:
 
         # env batch: cfg.env.n_envs is the GLOBAL count, sharded evenly over ranks
         self.env_name = cfg.env.name
-        n_global = int(cfg.env.n_envs)
-        if n_global % self.world_size:
-            raise ValueError(f"env.n_envs={n_global} must divide evenly over {self.world_size} ranks")
-        self.n_envs_global = n_global
-        self.n_envs = n_global // self.world_size
-        self.env_offset = self.rank * self.n_envs
+        self.n_envs_global = int(cfg.env.n_envs)
+        self.n_envs, self.env_offset = shard_envs(self.n_envs_global, self.world_size, self.rank)
         wrappers = cfg.env.get("wrappers", None)
         self.venv = make_async(cfg.env.name, env_type=cfg.env.get("env_type", None), num_envs=self.n_envs,
                                asynchronous=True, max_episode_steps=cfg.env.max_episode_steps, wrappers=wrappers,

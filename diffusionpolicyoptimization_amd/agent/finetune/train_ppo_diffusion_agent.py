@@ -11,7 +11,6 @@ the PPO epochs. Differences from the reference are only where data lives and wha
 Semantics kept on purpose: eval at itr % val_freq == 0 with env reset only
 then (4), population-std advantage normalisation per minibatch (3), one optimiser (2)."""
 import logging
-import math
 import os
 import pickle
 
@@ -20,10 +19,37 @@ import torch
 import torch.distributed as dist
 
 from ... import ops
+from ...util.dist import allreduce_sum_, explained_variance
 from ...util.timer import Timer
 from .train_ppo_agent import TrainPPOAgent
 
 log = logging.getLogger(__name__)
+
+
+def episode_sums(firsts, rew, act_steps, success_threshold):
+    """Per-rank episode sums (n_finished, sum of returns, sum of best rewards, n_success) over
+    the episodes that start and end inside the rollout (agent :144-167). firsts [S+1,E], rew [S,E]."""
+    n_ep, tot, best, succ = 0, 0.0, 0.0, 0.0
+    for e in range(firsts.shape[1]):
+        idx = np.nonzero(firsts[:, e] == 1)[0]
+        for i in range(len(idx) - 1):
+            s, en = idx[i], idx[i + 1]
+            if en - s > 1:
+                r = rew[s:en, e]
+                n_ep += 1
+                tot += float(r.sum())
+                b = float(r.max()) / act_steps
+                best += b
+                succ += float(b >= success_threshold)
+    return [float(n_ep), tot, best, succ]
+
+
+def episode_stats_from_sums(sums):
+    n_ep, tot, best, succ = sums
+    if n_ep == 0:
+        return dict(num_episode_finished=0, avg_episode_reward=0.0, avg_best_reward=0.0, success_rate=0.0)
+    return dict(num_episode_finished=int(n_ep), avg_episode_reward=tot / n_ep, avg_best_reward=best / n_ep,
+                success_rate=succ / n_ep)
 
 
 class TrainPPODiffusionAgent(TrainPPOAgent):
@@ -66,9 +92,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         self.adv_stats = torch.zeros(3, dtype=torch.float64, device=dev)
 
     def _allreduce(self, t):
-        if self.world_size > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return t
+        return allreduce_sum_(t)
 
     # ------------------------------------------------------------------ rollout (agent :58-141)
     def rollout(self, eval_mode):
@@ -110,27 +134,13 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
 
     def episode_stats(self):
         """agent :144-183; sums over ranks so every rank logs the global statistics."""
-        firsts, rew = self.firsts, self.reward_pin.numpy()
-        n_ep, tot, best, succ = 0, 0.0, 0.0, 0.0
-        for e in range(self.n_envs):
-            idx = np.nonzero(firsts[:, e] == 1)[0]
-            for i in range(len(idx) - 1):
-                s, en = idx[i], idx[i + 1]
-                if en - s > 1:
-                    r = rew[s:en, e]
-                    n_ep += 1
-                    tot += r.sum()
-                    b = r.max() / self.act_steps
-                    best += b
-                    succ += float(b >= self.best_reward_threshold_for_success)
+        sums = episode_sums(self.firsts, self.reward_pin.numpy(), self.act_steps,
+                            self.best_reward_threshold_for_success)
         if self.world_size > 1:
-            t = torch.tensor([n_ep, tot, best, succ], dtype=torch.float64, device=self.device)
+            t = torch.tensor(sums, dtype=torch.float64, device=self.device)
             self._allreduce(t)
-            n_ep, tot, best, succ = t.tolist()
-        if n_ep == 0:
-            return dict(num_episode_finished=0, avg_episode_reward=0.0, avg_best_reward=0.0, success_rate=0.0)
-        return dict(num_episode_finished=int(n_ep), avg_episode_reward=tot / n_ep, avg_best_reward=best / n_ep,
-                    success_rate=succ / n_ep)
+            sums = t.tolist()
+        return episode_stats_from_sums(sums)
 
     # ------------------------------------------------------------------ update (agent :186-377)
     def update(self):
@@ -206,15 +216,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             if flag_break:
                 break
         # explained variance (:373-377)
-        y_pred = self.values.double()
-        y_true = ret_flat.double()
-        mom = torch.stack([y_true.sum(), (y_true ** 2).sum(), (y_true - y_pred).sum(), ((y_true - y_pred) ** 2).sum(),
-                           torch.tensor(float(N), dtype=torch.float64, device=self.device)])
-        self._allreduce(mom)
-        n = mom[4]
-        var_y = mom[1] / n - (mom[0] / n) ** 2
-        var_d = mom[3] / n - (mom[2] / n) ** 2
-        info["explained_var"] = float("nan") if float(var_y) == 0 else float(1 - var_d / var_y)
+        info["explained_var"] = explained_variance(self.values, ret_flat)
         info["clipfrac"] = float(np.mean(clipfracs)) if clipfracs else 0.0
         return info
 

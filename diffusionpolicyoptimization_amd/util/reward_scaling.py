@@ -9,6 +9,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from . import dist as dist_util
 
 
 class RunningRewardScaler:
@@ -35,26 +36,8 @@ class RunningRewardScaler:
             return reward_se
         moments = torch.zeros(3, dtype=torch.float64, device=self.device)
         ops.reward_scale_moments(reward_se, first_se, self.ret, moments, ws, self.gamma)
-        world = torch.distributed.get_world_size(group)
-        gathered = [torch.zeros_like(moments) for _ in range(world)]
-        torch.distributed.all_gather(gathered, moments, group=group)
-        n, mean, m2 = 0.0, 0.0, 0.0
-        for g in gathered:  # Chan merge in fp64, identical order on every rank
-            gn, gm, g2 = (float(x) for x in g.cpu())
-            if gn == 0:
-                continue
-            tot = n + gn
-            delta = gm - mean
-            mean = mean + delta * gn / tot
-            m2 = m2 + g2 + delta * delta * n * gn / tot
-            n = tot
-        r = self.rms.cpu().numpy()
-        bv = m2 / n
-        delta = mean - r[0]
-        tot = r[2] + n
-        new_mean = r[0] + delta * n / tot
-        M2 = r[1] * r[2] + bv * n + delta * delta * r[2] * n / tot
-        self.rms.copy_(torch.tensor([new_mean, M2 / (tot - 1), tot], dtype=torch.float64))
+        n, mean, m2 = dist_util.gather_moments(moments, group)
+        self.rms.copy_(torch.tensor(dist_util.rms_update(self.rms.cpu().tolist(), n, mean, m2), dtype=torch.float64))
         ops.reward_scale_apply(reward_se, self.rms, self.cliprew, self.epsilon)
         return reward_se
 

@@ -284,8 +284,13 @@ def get_logprobs(p_ft, sched, state, chains, ft_steps, min_logprob_std=0.1, rnd=
 def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, returns, oldvalues,
            advantages, oldlogprobs, ft_steps, gamma_denoising=0.99, clip_ploss_coef=0.01,
            clip_ploss_coef_base=0.01, clip_ploss_coef_rate=3.0, clip_vloss_coef=None,
-           norm_adv=True, min_logprob_std=0.1, vf_coef=0.5, with_grad=True, reward_horizon=4, rnd=None):
+           norm_adv=True, min_logprob_std=0.1, vf_coef=0.5, with_grad=True, reward_horizon=4, rnd=None,
+           adv_mean_std=None, denom=None):
     """Returns (metrics dict, grads_actor dict, grads_critic dict).
+
+    Data-parallel restatement hooks: adv_mean_std overrides the minibatch
+    advantage mean/std (the global ones), denom overrides the row count the means divide by
+    (the global minibatch size) — summing such per-shard gradients gives the full-batch one.
 
     oldlogprobs may be per element [b,Ta,Da] (clipped & averaged here, :50-59) or already the
     clipped per-row mean [b]."""
@@ -306,7 +311,9 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
         oldlp = np.asarray(oldlogprobs, np.float64)
     adv = np.asarray(advantages, np.float64)
     if norm_adv:                                                  # :74-75 (population std)
-        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        am, asd = (adv.mean(), adv.std()) if adv_mean_std is None else adv_mean_std
+        adv = (adv - am) / (asd + 1e-8)
+    D = b if denom is None else denom
     disc = gamma_denoising ** (ft_steps - j.astype(np.float64) - 1)  # :83-86
     adv = adv * disc
     logratio = newlp - oldlp                                      # :89
@@ -320,7 +327,7 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
     pg1 = -adv * ratio
     rclip = np.clip(ratio, 1 - cc, 1 + cc)
     pg2 = -adv * rclip
-    pg_loss = np.maximum(pg1, pg2).mean()                         # :104-106
+    pg_loss = np.maximum(pg1, pg2).sum() / D                      # :104-106
     v, ccache = critic_forward(pc, obs, rnd=rnd)
     v = v[:, 0]                                                   # :109
     if clip_vloss_coef is not None:                               # :110-116
@@ -329,11 +336,11 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
         vl_cl = (v_cl - returns) ** 2
         v_loss = 0.5 * np.maximum(vl_un, vl_cl).mean()
     else:
-        v_loss = 0.5 * ((v - returns) ** 2).mean()                # :118
-    approx_kl = ((ratio - 1) - logratio).mean()                   # :121
-    clipfrac = (np.abs(ratio - 1.0) > cc).astype(np.float64).mean()
+        v_loss = 0.5 * ((v - returns) ** 2).sum() / D             # :118
+    approx_kl = ((ratio - 1) - logratio).sum() / D                # :121
+    clipfrac = (np.abs(ratio - 1.0) > cc).astype(np.float64).sum() / D
     metrics = dict(pg_loss=pg_loss, entropy_loss=-1.0, v_loss=v_loss, clipfrac=clipfrac,
-                   approx_kl=approx_kl, ratio=ratio.mean(), bc_loss=0.0, eta=1.0,
+                   approx_kl=approx_kl, ratio=ratio.sum() / D, bc_loss=0.0, eta=1.0,
                    loss=pg_loss + vf_coef * v_loss)
     if not with_grad:
         return metrics, None, None
@@ -341,7 +348,7 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
     # tf.maximum routes ties to the first argument; tf.clip_by_value passes grads inside [lo, hi].
     take1 = pg1 >= pg2
     ratio_in = (ratio >= 1 - cc) & (ratio <= 1 + cc)
-    dpg_dratio = np.where(take1, -adv, np.where(ratio_in, -adv, 0.0)) / b
+    dpg_dratio = np.where(take1, -adv, np.where(ratio_in, -adv, 0.0)) / D
     dnewlp = dpg_dratio * ratio
     dlp_el = np.zeros_like(lp_el)
     dlp_el[:, :H] = (dnewlp / (H * lp_el.shape[2]))[:, None, None]
@@ -353,7 +360,7 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
     ga = diffusion_mlp_backward(p_ft, acache, deps, xdim)
     if clip_vloss_coef is not None:
         raise NotImplementedError("clip_vloss_coef gradient (cfg default None)")
-    dv = vf_coef * (v - returns) / b
+    dv = vf_coef * (v - returns) / D
     gc, _ = residual_mlp_backward(pc, ccache, dv[:, None], "Mish", "")
     return metrics, ga, gc
 

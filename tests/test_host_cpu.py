@@ -1,0 +1,125 @@
+"""Host-side checks that need no GPU: the C-ABI library loads and exports exactly what
+include/dppo.h declares, its host-only queries and argument validation, the native env stepper
+against its NumPy specification, and the LR schedules."""
+import ctypes
+import math
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dppo.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from diffusionpolicyoptimization_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "diffusionpolicyoptimization_amd", "csrc"), "-j8"],
+                       check=True)
+    return _lib.load()
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"DPPO_API\s+[\w\s\*]+?\b(dppo_\w+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    from diffusionpolicyoptimization_amd import _lib
+    names = _declared()
+    assert len(names) >= 20
+    assert names == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    nm = subprocess.run(["nm", "-D", "--defined-only", lib._name], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (dppo_\w+)", nm))
+    assert set(_declared()) <= exported
+    assert exported <= set(_declared()), f"undeclared exports: {exported - set(_declared())}"
+    assert lib.dppo_abi_version() == 1
+
+
+def test_host_queries_match_python_layout(lib):
+    from diffusionpolicyoptimization_amd import ops
+    for d in (ops.ModelDims(), ops.ModelDims(obs_dim=17, action_dim=6), ops.ModelDims(actor_hidden=256)):
+        c = d.c()
+        assert lib.dppo_actor_param_count(ctypes.byref(c)) == ops.spec_count(ops.actor_param_spec(d))
+        assert lib.dppo_critic_param_count(ctypes.byref(c)) == ops.spec_count(ops.critic_param_spec(d))
+        for prec in (0, 1):
+            nb = lib.dppo_actor_packed_bytes(ctypes.byref(c), prec)
+            assert nb > 0 and nb % 256 == 0
+            # bf16 images hold half the bytes of fp32 in the weight segments
+        assert lib.dppo_actor_packed_bytes(ctypes.byref(c), 1) < lib.dppo_actor_packed_bytes(ctypes.byref(c), 0)
+    assert lib.dppo_reward_scale_workspace_doubles(500, 64) > 0
+
+
+@pytest.mark.parametrize("field,value,msg", [("actor_hidden", 100, "actor_hidden"), ("time_dim", 3, "time_dim"),
+                                             ("ft_denoising_steps", 30, "ft_denoising_steps"),
+                                             ("action_dim", 9, "horizon_steps*action_dim")])
+def test_invalid_dims_fail_loudly_before_any_device_work(lib, field, value, msg):
+    from diffusionpolicyoptimization_amd import ops
+    d = ops.ModelDims(**{field: value})
+    c = d.c()
+    assert lib.dppo_actor_param_count(ctypes.byref(c)) == 0
+    rc = lib.dppo_sample(ctypes.byref(c), 0, None, None, None, None, 4, None, None, 0, 0, 0, 0, 0.1, 3.0, 1.0,
+                         None, None, None)
+    assert rc == 1
+    assert msg in lib.dppo_last_error().decode()
+
+
+def test_missing_library_raises(tmp_path):
+    from diffusionpolicyoptimization_amd import _lib
+    saved = _lib._lib
+    _lib._lib = None
+    try:
+        with pytest.raises(_lib.DppoError, match="no CPU fallback"):
+            _lib.load(str(tmp_path / "libdppo_hip.so"))
+    finally:
+        _lib._lib = saved
+
+
+def test_native_env_matches_numpy_spec():
+    from diffusionpolicyoptimization_amd.env.synthetic import SyntheticLocomotionVecEnv, _native
+    if _native() is None:
+        subprocess.run(["make", "-C", os.path.join(ROOT, "diffusionpolicyoptimization_amd", "csrc"), "-j8"],
+                       check=True)
+    E, Do, Da = 7, 11, 3
+    envs = [SyntheticLocomotionVecEnv(E, Do, Da, act_steps=4, max_episode_steps=40, family_seed=2, native=nat)
+            for nat in (True, False)]
+    assert envs[0].native is not None and envs[1].native is None
+    for e in envs:
+        e.seed(range(100, 100 + E))
+    o0, o1 = envs[0].reset_arg(), envs[1].reset_arg()
+    np.testing.assert_allclose(o0["state"], o1["state"])
+    rng = np.random.default_rng(0)
+    n_trunc = 0
+    for _ in range(25):
+        a = rng.normal(0, 0.8, (E, 4, Da)).astype(np.float32)
+        r0 = envs[0].step(a)
+        r1 = envs[1].step(a)
+        np.testing.assert_allclose(r0[0]["state"], r1[0]["state"], atol=3e-6)
+        np.testing.assert_allclose(r0[1], r1[1], atol=3e-6)
+        np.testing.assert_array_equal(r0[2], r1[2])
+        np.testing.assert_array_equal(r0[3], r1[3])
+        n_trunc += int(r0[3].sum())
+    assert n_trunc == 2 * E  # 40 sub-steps = 10 chunks; 25 chunks cross two truncations
+
+
+def test_lr_schedules():
+    from diffusionpolicyoptimization_amd.util.scheduler import (CosineAnnealingWarmupRestarts,
+                                                                CosineAnnealingWarmupRestarts2)
+    # shipped cfg: initial = max lr -> constant
+    s = CosineAnnealingWarmupRestarts2(1e-4, first_cycle_steps=10, max_lr=1e-4, min_lr=1e-4, warmup_steps=1)
+    assert all(abs(s(i) - 1e-4) < 1e-15 for i in range(50))
+    s = CosineAnnealingWarmupRestarts2(1e-5, first_cycle_steps=10, max_lr=1e-3, min_lr=1e-5, warmup_steps=2)
+    assert s(0) == pytest.approx(1e-5)
+    assert s(1) == pytest.approx(1e-5 + (1e-3 - 1e-5) / 2)
+    assert s(2) == pytest.approx(1e-3)
+    assert s(6) == pytest.approx(1e-5 + (1e-3 - 1e-5) * (1 + math.cos(math.pi * 0.5)) / 2)
+    assert s(12) == pytest.approx(1e-3)  # restart: step 12 = step 2 of cycle 1
+    e = CosineAnnealingWarmupRestarts(first_cycle_steps=8, max_lr=1.0, min_lr=0.0, warmup_steps=0)
+    assert e(0) == pytest.approx(1.0) and e(4) == pytest.approx(0.5) and e(8) == pytest.approx(1.0)
