@@ -78,6 +78,27 @@ def cpu_baseline(cfg, n_envs, S, bs, seconds=12.0):
             "ppo_updates_per_sec": 1.0 / t_mb}
 
 
+def sampler_burst_ms(agent, n=30):
+    """Average sampler launch duration with HIP events on the launch stream, over n launches
+    enqueued back to back on the rollout's own buffers (same workload as the timed region). The
+    per-step events inside the rollout also contain the host's enqueue gap after the event record
+    (the stream is idle between env steps), so they overstate the kernel; this burst measures the
+    kernel itself and is what rocprofv3's per-kernel average reports."""
+    import torch
+    m = agent.model
+    stream = torch.cuda.current_stream(agent.device)
+    args = dict(deterministic=False, return_chain=True, actions_out=agent.act_dev, chains_out=agent.chains_traj[0])
+    m(agent.obs_traj[0], **args)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(agent.device)
+    ev0.record(stream)
+    for _ in range(n):
+        m(agent.obs_traj[0], **args)
+    ev1.record(stream)
+    ev1.synchronize()
+    return ev0.elapsed_time(ev1) / n, n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -131,7 +152,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, t_roll, t_upd = t.tolist()
 
-    samp_ms = sum(a.elapsed_time(b) for a, b in agent.sampler_events) / max(1, len(agent.sampler_events))
+    loop_samp_ms = sum(a.elapsed_time(b) for a, b in agent.sampler_events) / max(1, len(agent.sampler_events))
+    samp_ms, n_burst = sampler_burst_ms(agent)
     upd_ms = sum(a.elapsed_time(b) for a, b in agent.update_events) / max(1, len(agent.update_events))
     env_steps = agent.n_envs_global * cfg.act_steps * cfg.train.n_steps * args.steps
     n_updates = agent.timing["n_updates"]
@@ -161,7 +183,8 @@ def main():
         "roofline": {"bound": "mfma", "kernel": "sample_kernel (K-step DDPM sampler, all layers fused)",
                      "achieved": achieved, "peak": PEAK["bf16" if prec == "bf16" else "fp32"], "unit": "TFLOP/s",
                      "frac": achieved / PEAK["bf16" if prec == "bf16" else "fp32"], "traffic": traffic,
-                     "avg_launch_ms": samp_ms, "flops_per_launch": flops, "launches": len(agent.sampler_events),
+                     "avg_launch_ms": samp_ms, "flops_per_launch": flops, "burst_launches": n_burst,
+                     "in_loop_event_ms": loop_samp_ms, "in_loop_launches": len(agent.sampler_events),
                      "note": ("M = envs/GPU rows per GEMM: at 64 rows the dependent 80-GEMM chain is bound by "
                               "streaming ~1.1 MB of bf16 weights per denoising step from L2 into one CU per "
                               "16-row tile, not by MFMA issue; see DESIGN.md")},

@@ -53,7 +53,8 @@ class TrainAgent:
         self.venv = make_async(cfg.env.name, env_type=cfg.env.get("env_type", None), num_envs=self.n_envs,
                                asynchronous=True, max_episode_steps=cfg.env.max_episode_steps, wrappers=wrappers,
                                obs_dim=cfg.obs_dim, action_dim=cfg.action_dim, act_steps=cfg.act_steps,
-                               obs_steps=cfg.cond_steps, family_seed=cfg.env.get("family_seed", 0))
+                               obs_steps=cfg.cond_steps, family_seed=cfg.env.get("family_seed", 0),
+                               native=bool(cfg.env.get("native", True)))
         self.venv.seed([self.seed + self.env_offset + i for i in range(self.n_envs)])  # train_agent.py:53-56
         self.n_cond_step = cfg.cond_steps
         self.obs_dim = cfg.obs_dim

@@ -9,7 +9,7 @@ _LOCOMOTION = ("hopper", "walker2d", "halfcheetah", "ant", "synthetic")
 
 
 def make_async(id, num_envs=1, asynchronous=True, wrappers=None, render=False, obs_dim=23, action_dim=7,
-               env_type=None, max_episode_steps=None, act_steps=4, obs_steps=1, family_seed=0, **kwargs):
+               env_type=None, max_episode_steps=None, act_steps=4, obs_steps=1, family_seed=0, native=True, **kwargs):
     name = str(id).lower()
     if env_type not in (None, "gym") or not any(name.startswith(p) for p in _LOCOMOTION):
         raise NotImplementedError(f"env {id!r} (type {env_type}): only the gym locomotion tasks are in scope")
@@ -25,4 +25,4 @@ def make_async(id, num_envs=1, asynchronous=True, wrappers=None, render=False, o
                                      act_steps=ms.get("n_action_steps", act_steps),
                                      n_obs_steps=ms.get("n_obs_steps", obs_steps),
                                      max_episode_steps=ms.get("max_episode_steps", max_episode_steps or 1000),
-                                     family_seed=family_seed)
+                                     family_seed=family_seed, native=native)
