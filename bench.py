@@ -164,7 +164,7 @@ def main():
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("kernel", "").startswith("sample_kernel") and tj.get("precision") == prec \
+        if "sample_kernel" in tj.get("kernel", "") and tj.get("precision") == prec \
                 and tj.get("envs") == agent.n_envs:
             traffic = tj.get("hbm_bytes_per_launch")
     out = {

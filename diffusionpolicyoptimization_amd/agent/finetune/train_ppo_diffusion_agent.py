@@ -68,6 +68,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         self.run_results = []
         self.prev_obs_venv = None
         self.last_info = {}
+        self._stepper = None
 
     # ------------------------------------------------------------------ buffers
     def _alloc_buffers(self):
@@ -105,23 +106,24 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             self.firsts[0] = self.done_venv  # envs that finished were already reset in-wrapper
         self.last_itr_eval = eval_mode
         obs_np = self.obs_pin.numpy()
-        act_np = self.act_pin.numpy().reshape(E, self.horizon_steps, self.action_dim)
+        act_view = self.act_pin.numpy().reshape(E, self.horizon_steps, self.action_dim)[:, :self.act_steps]
         stream = torch.cuda.current_stream(self.device)
         rew_np, term_np = self.reward_pin.numpy(), self.term_pin.numpy()
+        if self._stepper is None:
+            self._stepper = self.model.bind_rollout(self.obs_pin, self.obs_traj, self.act_dev, self.act_pin,
+                                                    self.chains_traj)
+        sample_step = self._stepper
         for step in range(S):
-            self.obs_traj[step].copy_(self.obs_pin.view(E, -1), non_blocking=True)          # H2D obs
             if self.sampler_events is not None:
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev0.record(stream)
-            self.model(self.obs_traj[step], deterministic=eval_mode, return_chain=True,
-                       actions_out=self.act_dev, chains_out=self.chains_traj[step])
+            # H2D obs -> obs_traj[step], K-step sampler -> chains_traj[step], D2H actions, stream wait
+            sample_step(step, eval_mode)
             if self.sampler_events is not None:
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev1.record(stream)
                 self.sampler_events.append((ev0, ev1))
-            self.act_pin.copy_(self.act_dev, non_blocking=True)                                 # D2H actions
-            stream.synchronize()
-            _, reward, terminated, truncated, _ = self.venv.step(act_np[:, :self.act_steps], obs_out=obs_np)
+            _, reward, terminated, truncated, _ = self.venv.step(act_view, obs_out=obs_np)
             done = terminated | truncated
             rew_np[step] = reward
             term_np[step] = terminated

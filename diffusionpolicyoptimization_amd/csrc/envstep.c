@@ -2,59 +2,98 @@
  * One call advances all E envs by one action chunk (MultiStep semantics: act_steps sub-steps,
  * reward summed, stop at termination/truncation) and writes the float32 observation straight into
  * the caller's (pinned) staging buffer, so the next H2D copy needs no host-side repacking.
- * Resets of finished envs are applied by the Python wrapper (rare: once per 250 chunks). */
+ * Envs are processed in blocks of EB with the state transposed to [Do][EB] in registers/L1, so
+ * every inner loop runs over envs and vectorises (AVX2: 4 doubles). Resets of finished envs are
+ * applied by the Python wrapper (rare: once per 250 chunks). */
+#include <immintrin.h>
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
 
 #define DPPO_ENV_API __attribute__((visibility("default")))
+#define EB 16
+#define MAXD 64
 
-static inline double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+DPPO_ENV_API int dppo_env_abi(void) { return 2; }
 
-DPPO_ENV_API int dppo_env_abi(void) { return 1; }
+typedef double v4d __attribute__((vector_size(32)));
+#define NV (EB / 4)
 
-/* AT = A^T (row i holds column i of A) so the state update vectorises over the output coordinate */
-DPPO_ENV_API void dppo_env_step(int E, int Do, int Da, int act_steps, int Ta, int max_steps, int n_obs_steps,
+static inline v4d v4_splat(double x) { return (v4d){x, x, x, x}; }
+static inline v4d v4_clamp1(v4d x) {
+    return (v4d)_mm256_min_pd(_mm256_max_pd((__m256d)x, _mm256_set1_pd(-1.0)), _mm256_set1_pd(1.0));
+}
+
+/* AT = A^T (AT[i*Do + j] = A[j][i]); B [Da][Do]; state [E][Do] f64; actions [E][Ta][Da] f32 */
+/* returns the number of envs whose episode ended in this chunk */
+DPPO_ENV_API int dppo_env_step(int E, int Do, int Da, int act_steps, int Ta, int max_steps, int n_obs_steps,
                                 const double* __restrict__ AT, const double* __restrict__ B,
                                 const double* __restrict__ c, const double* __restrict__ goal,
                                 double* __restrict__ state, int64_t* __restrict__ cnt, const float* __restrict__ actions,
                                 double* __restrict__ reward, uint8_t* __restrict__ terminated,
                                 uint8_t* __restrict__ truncated, float* __restrict__ obs_out) {
-    double s2[64];
-    for (int e = 0; e < E; ++e) {
-        double* s = state + (size_t)e * Do;
-        double rsum = 0.0;
-        uint8_t trunc = 0;
-        for (int k = 0; k < act_steps && k < Ta; ++k) {
-            const float* a = actions + ((size_t)e * Ta + k) * Da;
-            cnt[e] += 1;
-            for (int j = 0; j < Do; ++j) s2[j] = c[j];
-            for (int i = 0; i < Do; ++i) {
-                const double si = s[i];
-                const double* ai_row = AT + (size_t)i * Do;
-                for (int j = 0; j < Do; ++j) s2[j] += ai_row[j] * si;
-            }
-            double asq = 0.0;
-            for (int i = 0; i < Da; ++i) {
-                const double ai = clampd((double)a[i], -1.0, 1.0);
-                asq += (double)a[i] * (double)a[i];
-                const double* b_row = B + (size_t)i * Do;
-                for (int j = 0; j < Do; ++j) s2[j] += ai * b_row[j];
-            }
-            double err = 0.0;
-            for (int j = 0; j < Do; ++j) {
-                const double v = clampd(s2[j], -1.0, 1.0);
-                s[j] = v;
-                const double d = v - goal[j];
-                err += d * d;
-            }
-            rsum += 1.0 - err / Do - 0.01 * asq / Da;
-            if (cnt[e] >= max_steps) { trunc = 1; break; }
+    v4d s[MAXD][NV], ac[MAXD][NV];
+    double rsum[EB], alive[EB];
+    int64_t ct[EB];
+    const int nsub = act_steps < Ta ? act_steps : Ta;
+    int n_done = 0;
+    for (int e0 = 0; e0 < E; e0 += EB) {
+        const int nb = E - e0 < EB ? E - e0 : EB;
+        for (int b = 0; b < EB; ++b) {
+            const int e = e0 + (b < nb ? b : 0);
+            for (int j = 0; j < Do; ++j) s[j][b >> 2][b & 3] = state[(size_t)e * Do + j];
+            ct[b] = cnt[e];
+            rsum[b] = 0.0;
+            alive[b] = b < nb ? 1.0 : 0.0;
         }
-        reward[e] = rsum;
-        terminated[e] = 0;
-        truncated[e] = trunc;
-        for (int o = 0; o < n_obs_steps; ++o)
-            for (int j = 0; j < Do; ++j) obs_out[((size_t)e * n_obs_steps + o) * Do + j] = (float)s[j];
+        for (int k = 0; k < nsub; ++k) {
+            for (int b = 0; b < EB; ++b) {
+                const float* a = actions + ((size_t)(e0 + (b < nb ? b : 0)) * Ta + k) * Da;
+                for (int i = 0; i < Da; ++i) ac[i][b >> 2][b & 3] = (double)a[i];
+            }
+            v4d asq[NV], err[NV], acl[MAXD][NV];
+            for (int v = 0; v < NV; ++v) { asq[v] = v4_splat(0.0); err[v] = v4_splat(0.0); }
+            for (int i = 0; i < Da; ++i)
+                for (int v = 0; v < NV; ++v) { asq[v] += ac[i][v] * ac[i][v]; acl[i][v] = v4_clamp1(ac[i][v]); }
+            v4d s2[MAXD][NV];
+            for (int j = 0; j < Do; ++j) {
+                v4d acc[NV];
+                for (int v = 0; v < NV; ++v) acc[v] = v4_splat(c[j]);
+                for (int i = 0; i < Do; ++i) {
+                    const v4d w = v4_splat(AT[(size_t)i * Do + j]);
+                    for (int v = 0; v < NV; ++v) acc[v] += w * s[i][v];
+                }
+                for (int i = 0; i < Da; ++i) {
+                    const v4d w = v4_splat(B[(size_t)i * Do + j]);
+                    for (int v = 0; v < NV; ++v) acc[v] += w * acl[i][v];
+                }
+                const v4d gj = v4_splat(goal[j]);
+                for (int v = 0; v < NV; ++v) {
+                    s2[j][v] = v4_clamp1(acc[v]);
+                    const v4d d = s2[j][v] - gj;
+                    err[v] += d * d;
+                }
+            }
+            for (int b = 0; b < EB; ++b) {
+                if (alive[b] != 0.0) {
+                    for (int j = 0; j < Do; ++j) s[j][b >> 2][b & 3] = s2[j][b >> 2][b & 3];
+                    ct[b] += 1;
+                    rsum[b] += 1.0 - err[b >> 2][b & 3] / Do - 0.01 * asq[b >> 2][b & 3] / Da;
+                    if (ct[b] >= max_steps) alive[b] = 0.0;
+                }
+            }
+        }
+        for (int b = 0; b < nb; ++b) {
+            const int e = e0 + b;
+            for (int j = 0; j < Do; ++j) state[(size_t)e * Do + j] = s[j][b >> 2][b & 3];
+            cnt[e] = ct[b];
+            reward[e] = rsum[b];
+            terminated[e] = 0;
+            truncated[e] = ct[b] >= max_steps;
+            n_done += truncated[e];
+            for (int o = 0; o < n_obs_steps; ++o)
+                for (int j = 0; j < Do; ++j) obs_out[((size_t)e * n_obs_steps + o) * Do + j] = (float)s[j][b >> 2][b & 3];
+        }
     }
+    return n_done;
 }

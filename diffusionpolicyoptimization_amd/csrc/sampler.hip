@@ -298,3 +298,26 @@ extern "C" int dppo_sample(const dppo_dims* d, int precision, const void* packed
     hipStream_t s = (hipStream_t)stream;
     return precision == DPPO_BF16 ? dispatch_sample<PolicyBF16>(a, s) : dispatch_sample<PolicyF32>(a, s);
 }
+
+// One rollout step's device work in one call (train_ppo_diffusion_agent.py:106-122): H2D of the
+// pinned observation into its rollout slot, the K-step sampler, D2H of the actions into pinned
+// memory and (optionally) the stream wait, so the host's per-step overhead is one FFI call.
+extern "C" int dppo_sample_step(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
+                                const float* sched, const float* cond_host, float* cond, int n_envs, uint64_t seed,
+                                uint64_t call_id, int env_offset, int deterministic, float min_sampling_std,
+                                float randn_clip, float final_clip, float* actions, float* actions_host,
+                                float* chains, int synchronize, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    if (n_envs == 0) return DPPO_OK;
+    DPPO_CHECK(cond_host && cond && actions && actions_host, "dppo_sample_step: null pointer argument");
+    hipStream_t s = (hipStream_t)stream;
+    DPPO_HIP(hipMemcpyAsync(cond, cond_host, sizeof(float) * (size_t)n_envs * D.SD, hipMemcpyHostToDevice, s));
+    rc = dppo_sample(d, precision, packed_base, packed_ft, sched, cond, n_envs, nullptr, nullptr, seed, call_id,
+                     env_offset, deterministic, min_sampling_std, randn_clip, final_clip, actions, chains, stream);
+    if (rc) return rc;
+    DPPO_HIP(hipMemcpyAsync(actions_host, actions, sizeof(float) * (size_t)n_envs * D.XD, hipMemcpyDeviceToHost, s));
+    if (synchronize) DPPO_HIP(hipStreamSynchronize(s));
+    return DPPO_OK;
+}

@@ -26,7 +26,7 @@ def _native():
         lib = ctypes.CDLL(_ENV_LIB)
         P = ctypes.c_void_p
         lib.dppo_env_step.argtypes = [ctypes.c_int] * 7 + [P] * 11
-        lib.dppo_env_step.restype = None
+        lib.dppo_env_step.restype = ctypes.c_int
         _lib = lib
     return _lib
 
@@ -51,6 +51,7 @@ class SyntheticLocomotionVecEnv:
         self._term = np.zeros(num_envs, dtype=np.uint8)
         self._trunc = np.zeros(num_envs, dtype=np.uint8)
         self._static_ptrs = None
+        self._last_a = self._last_o = None
         self.seeds = np.arange(num_envs)
         self.state = np.zeros((num_envs, obs_dim))
         self.cnt = np.zeros(num_envs, dtype=np.int64)
@@ -88,15 +89,23 @@ class SyntheticLocomotionVecEnv:
         """actions [E, Ta, Da]; obs_out: optional float32 [E, To, Do] buffer (e.g. pinned staging)."""
         E = self.num_envs
         if self.native is not None:
-            a = np.ascontiguousarray(actions, dtype=np.float32).reshape(E, -1, self.action_dim)
+            a = actions if (isinstance(actions, np.ndarray) and actions.dtype == np.float32
+                            and actions.flags.c_contiguous) else np.ascontiguousarray(actions, dtype=np.float32)
+            ta = a.size // (E * self.action_dim)
             out = obs_out if obs_out is not None else np.empty((E, self.n_obs_steps, self.obs_dim), np.float32)
             if self._static_ptrs is None:
                 self.state = np.ascontiguousarray(self.state)
                 self._AT = np.ascontiguousarray(self.A.T)
                 self._static_ptrs = [_p(x) for x in (self._AT, self.B, self.c, self.goal, self.state, self.cnt)]
-            self.native.dppo_env_step(E, self.obs_dim, self.action_dim, self.act_steps, a.shape[1],
-                                      self.max_episode_steps, self.n_obs_steps, *self._static_ptrs, _p(a),
-                                      _p(self._reward), _p(self._term), _p(self._trunc), _p(out))
+                self._tail_ptrs = [_p(x) for x in (self._reward, self._term, self._trunc)]
+            # pointer caches keyed by object identity (the reference held here keeps the id unique)
+            if a is not self._last_a:
+                self._last_a, self._last_pa = a, _p(a)
+            if out is not self._last_o:
+                self._last_o, self._last_po = out, _p(out)
+            n_done = self.native.dppo_env_step(E, self.obs_dim, self.action_dim, self.act_steps, ta,
+                                               self.max_episode_steps, self.n_obs_steps, *self._static_ptrs,
+                                               self._last_pa, *self._tail_ptrs, self._last_po)
             reward = self._reward.copy()
             terminated, truncated = self._term.astype(bool), self._trunc.astype(bool)
         else:
@@ -115,9 +124,9 @@ class SyntheticLocomotionVecEnv:
                 truncated |= alive & (self.cnt >= self.max_episode_steps)
                 alive &= ~truncated
             out = None
-        done = terminated | truncated
         infos = None
-        if np.any(done):                                              # reset_within_step (multi_step.py:177-187)
+        if (n_done if self.native is not None else (terminated | truncated).any()):  # reset_within_step
+            done = terminated | truncated                                            # (multi_step.py:177-187)
             idx = np.nonzero(done)[0]
             infos = {int(i): {"final_obs": self.state[i].copy()} for i in idx}
             self.episode[idx] += 1

@@ -170,6 +170,13 @@ class VPGDiffusion(DiffusionModel):
         ch = chains.view(E, self.ft_denoising_steps + 1, self.horizon_steps, self.action_dim) if chains is not None else None
         return Sample(traj, ch)
 
+    def bind_rollout(self, cond_host, obs_traj, actions, actions_host, chains_traj):
+        """A pre-bound rollout step: step(i, deterministic) copies the pinned observation
+        cond_host [E, SD] into obs_traj[i], samples into actions / chains_traj[i] and copies the
+        actions into pinned actions_host, then waits for the stream — one FFI call per env step
+        (dppo_sample_step). Same Philox stream and call counter as __call__."""
+        return ops.SampleStepper(self, cond_host, obs_traj, actions, actions_host, chains_traj)
+
     # ------------------------------------------------------------------ log-probs (diffusion_vpg.py:343-481)
     def get_logprobs(self, cond, chains, get_ent=False, use_base_policy=False, reduced=False):
         """-> [n*K', Ta, Da] (row = sample*K' + j, t = K'-1-j). reduced=True instead returns the

@@ -149,6 +149,46 @@ def sample(d: ModelDims, precision, packed_base, packed_ft, sched, cond, x_T=Non
     return actions, chains
 
 
+class SampleStepper:
+    """dppo_sample_step with every argument but the step index, call counter and mode bound once
+    (the rollout's buffers never move), so a rollout step costs one ctypes call."""
+
+    def __init__(self, model, cond_host, obs_traj, actions, actions_host, chains_traj):
+        d = model.dims
+        S, E = obs_traj.shape[0], obs_traj.shape[1]
+        _check(obs_traj, (S, E, d.sd), torch.float32, "obs_traj")
+        _check(chains_traj, (S, E, d.ft_denoising_steps + 1, d.xd), torch.float32, "chains_traj")
+        _check(actions, (E, d.xd), torch.float32, "actions")
+        if cond_host.is_cuda or actions_host.is_cuda or not (cond_host.is_pinned() and actions_host.is_pinned()):
+            raise ValueError("cond_host / actions_host must be pinned host tensors")
+        if cond_host.numel() != E * d.sd or actions_host.numel() != E * d.xd:
+            raise ValueError("cond_host / actions_host sizes do not match the rollout")
+        self.model, self.S, self.E = model, S, E
+        self._fn = _lib.load().dppo_sample_step
+        self._dims = d.c()
+        self._keep = (cond_host, obs_traj, actions, actions_host, chains_traj)
+        self._obs0, self._obs_step = obs_traj.data_ptr(), E * d.sd * 4
+        self._ch0, self._ch_step = chains_traj.data_ptr(), E * (d.ft_denoising_steps + 1) * d.xd * 4
+        self._fixed = (ptr(cond_host), ptr(actions), ptr(actions_host))
+        self._stream = stream_handle(obs_traj.device)
+
+    def __call__(self, i, deterministic=False):
+        if not 0 <= i < self.S:
+            raise IndexError(f"rollout step {i} outside [0, {self.S})")
+        m = self.model
+        fc = m.final_action_clip_value
+        cond_host, actions, actions_host = self._fixed
+        rc = self._fn(ctypes.byref(self._dims), _prec(m.precision), ptr(m.packed_base), ptr(m.packed_ft), ptr(m.sched),
+                      cond_host, ctypes.c_void_p(self._obs0 + i * self._obs_step), self.E,
+                      ctypes.c_uint64(m.seed & (2 ** 64 - 1)), ctypes.c_uint64(m._call_id), m._env_offset,
+                      int(bool(deterministic)), float(m.get_min_sampling_denoising_std()), float(m.randn_clip_value),
+                      float(fc) if fc is not None else 0.0, actions, actions_host,
+                      ctypes.c_void_p(self._ch0 + i * self._ch_step), 1, self._stream)
+        if rc:
+            raise _lib.DppoError(f"dppo_sample_step failed ({rc}): {_lib.load().dppo_last_error().decode()}")
+        m._call_id += 1
+
+
 def logprob(d: ModelDims, precision, packed_ft, sched, cond, chains, min_logprob_std=0.1, reward_horizon=None,
             want_elem=True, want_mean=True, lp_elem=None, lp_mean=None):
     n = cond.shape[0]

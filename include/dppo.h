@@ -89,6 +89,15 @@ DPPO_API int dppo_sample(const dppo_dims* d, int precision, const void* packed_b
                 float min_sampling_std, float randn_clip, float final_clip,
                 float* actions, float* chains, void* stream);
 
+/* One rollout step (agent/finetune/train_ppo_diffusion_agent.py:106-122) in one call:
+ * hipMemcpyAsync(cond <- cond_host [host, pinned]), dppo_sample with the Philox noise, hipMemcpyAsync
+ * (actions_host [host, pinned] <- actions), then hipStreamSynchronize when synchronize != 0. */
+DPPO_API int dppo_sample_step(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
+                const float* sched, const float* cond_host, float* cond, int n_envs, uint64_t seed,
+                uint64_t call_id, int env_offset, int deterministic, float min_sampling_std,
+                float randn_clip, float final_clip, float* actions, float* actions_host,
+                float* chains, int synchronize, void* stream);
+
 /* ---- a10: VPGDiffusion.get_logprobs (diffusion_vpg.py:343-425) + the clip/mean of c_loss
  * (diffusion_ppo.py:50-59) for the old-logprob pass (agent/finetune/train_ppo_diffusion_agent.py:214-229).
  *   cond [n, To*Do], chains [n, K'+1, Ta*Da]

@@ -25,3 +25,37 @@ def test_agent_iterations(cuda, precision, tmp_path):
     p = agent.model.train_params.cpu().numpy()
     assert np.isfinite(p).all()
     assert os.path.exists(os.path.join(tmp_path, "checkpoint", "state_0.npz"))
+
+
+def test_bound_rollout_step_matches_model_call(cuda):
+    """dppo_sample_step (H2D + sampler + D2H in one call) == model(...) on the same Philox draws."""
+    import torch
+
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
+                      ["model.precision=bf16"])
+    model = instantiate(cfg.model, device=cuda, seed=3)
+    d = model.dims
+    S, E = 3, 40
+    obs_pin = torch.empty(E, d.sd, dtype=torch.float32).pin_memory()
+    act_pin = torch.empty(E, d.xd, dtype=torch.float32).pin_memory()
+    obs_traj = torch.zeros(S, E, d.sd, device=cuda)
+    chains = torch.zeros(S, E, d.ft_denoising_steps + 1, d.xd, device=cuda)
+    act = torch.empty(E, d.xd, device=cuda)
+    step = model.bind_rollout(obs_pin, obs_traj, act, act_pin, chains)
+    rng = np.random.default_rng(0)
+    for i in range(S):
+        o = rng.uniform(-1, 1, (E, d.sd)).astype(np.float32)
+        obs_pin.numpy()[:] = o
+        cid = model._call_id
+        step(i, deterministic=(i == 2))
+        got_a = act_pin.numpy().copy()
+        model._call_id = cid
+        ref = model(torch.tensor(o, device=cuda), deterministic=(i == 2), return_chain=True)
+        torch.cuda.synchronize()
+        assert model._call_id == cid + 1
+        np.testing.assert_array_equal(obs_traj[i].cpu().numpy(), o)
+        np.testing.assert_array_equal(got_a, ref.trajectories.reshape(E, -1).cpu().numpy())
+        np.testing.assert_array_equal(chains[i].cpu().numpy(), ref.chains.reshape(E, -1, d.xd).cpu().numpy())
+    with pytest.raises(IndexError):
+        step(S)
