@@ -91,15 +91,17 @@ struct ActorSmem {
     }
 };
 
-template <class P, int MT, int NT, int NO, int KSI, bool TRAIN>
-__global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a) {
+template <class P, int MT, int NT, int NO, int KSI, bool TRAIN, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) {
     using AT = typename P::AT;
+    constexpr int THREADS = 64 * WAVES;
     constexpr int ROWS = 16 * MT;
-    constexpr int KSH = ksh_for<P>(NT);
+    static_assert(ROWS <= 64, "the epilogue maps one row per lane of wave 0");
+    constexpr int KSH = ksh_for<P>(NT, WAVES);
     constexpr int NOK = nok_for<P>(NT);
     constexpr int KSO = 2;   // k-steps of the transposed out layer (out dim <= 2*KG, padded even)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const MlpLayout& L = a.L;
     const ActorSmem<P, MT> S(a);
     const int pad = lds_pad_elems<P>();
@@ -138,8 +140,8 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
         }
         rn[tid] = n; rj[tid] = j;
     }
-    for (int i = tid; i < KF * DPPO_SCHED_COLS; i += DPPO_THREADS) sch[i] = a.sched[i];
-    for (int i = tid; i < 3 * H + 16 * NO; i += DPPO_THREADS) {
+    for (int i = tid; i < KF * DPPO_SCHED_COLS; i += THREADS) sch[i] = a.sched[i];
+    for (int i = tid; i < 3 * H + 16 * NO; i += THREADS) {
         const int seg = i < H ? SEG_B_IN : (i < 2 * H ? SEG_B_L1 : (i < 3 * H ? SEG_B_L2 : SEG_B_OUT));
         const int j = i < 3 * H ? i % H : i - 3 * H;
         bias[i] = ((const float*)(a.packed + L.off[seg]))[j];
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
     const int half = TD / 2;
     const float lnf = logf(10000.f) / (float)(half - 1);
     const float* tw = (const float*)(a.packed + L.off[SEG_TIME]);
-    for (int i = tid; i < KF * 2 * TD; i += DPPO_THREADS) {
+    for (int i = tid; i < KF * 2 * TD; i += THREADS) {
         const int t = i / (2 * TD), jj = i % (2 * TD);
         float acc = tw[TD * 2 * TD + jj];
         for (int k = 0; k < TD; ++k) {
@@ -157,14 +159,14 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
         ta1[i] = mishf(acc);
     }
     __syncthreads();
-    for (int i = tid; i < KF * TD; i += DPPO_THREADS) {
+    for (int i = tid; i < KF * TD; i += THREADS) {
         const int t = i / TD, jj = i % TD;
         const float* w2 = tw + TD * 2 * TD + 2 * TD;
         float acc = w2[2 * TD * TD + jj];
         for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + jj];
         temb[i] = acc;
     }
-    for (int i = tid; i < ROWS * XD; i += DPPO_THREADS) {
+    for (int i = tid; i < ROWS * XD; i += THREADS) {
         const int r = i / XD, q = i % XD, n = rn[r];
         float vp = 0.f, vn = 0.f;
         if (n >= 0) {
@@ -173,13 +175,13 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
         }
         xp[i] = vp; xn[i] = vn;
     }
-    for (int i = tid; i < ROWS * SD; i += DPPO_THREADS) {
+    for (int i = tid; i < ROWS * SD; i += THREADS) {
         const int r = i / SD, c = i % SD, n = rn[r];
         st[i] = n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f;
     }
     __syncthreads();
     // a0 = [x_prev, temb(t), state] (mlp_diffusion.py:86), t = K'-1-j (diffusion_vpg.py:456-458)
-    for (int i = tid; i < ROWS * k1w; i += DPPO_THREADS) {
+    for (int i = tid; i < ROWS * k1w; i += THREADS) {
         const int r = i / k1w, c = i % k1w;
         const int t = KF - 1 - rj[r];
         float v = 0.f;
@@ -190,7 +192,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
     }
     if (train) {
         AT* a0T = (AT*)a.ws.a0T;
-        for (int i = tid; i < ROWS * IN; i += DPPO_THREADS) {
+        for (int i = tid; i < ROWS * IN; i += THREADS) {
             const int c = i / ROWS, r = i % ROWS;
             const int t = KF - 1 - rj[r];
             float v;
@@ -204,13 +206,14 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
     __syncthreads();
 
     const int ntile0 = wave * NT;
-    auto W = [&](int seg) { return (const u32x4*)(a.packed + L.off[seg]); };
+    const __amdgpu_buffer_rsrc_t rs = packed_rsrc(a.packed);
+    auto W = [&](int seg) { return wsrc(rs, L.off[seg]); };
     f32x4 H1[MT][NT], acc[MT][NT];
     uint64_t mask1 = 0, mask2 = 0;
     WRing<NT> R;
     ring_prime(R, W(SEG_W_IN), KSI, ntile0, lane);
     ORing<NOK, NO> ob;
-    out_prefetch(ob, W(SEG_W_OUT), KSH, wave, lane);
+    out_prefetch<NOK, NO, WAVES>(ob, W(SEG_W_OUT), KSH, wave, lane);
     // ---- L1: h1 = a0 W_in + b (no activation on the input layer) ----
     gemm_stream<P, MT, NT, KSI>(a0, lda0, W(SEG_W_IN), ntile0, H1, lane, R, NextLayer{W(SEG_W_L1), KSH, ntile0});
     add_bias(H1, bias, ntile0, lane);
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
     // ---- L4: eps = h3 W_out + b (k split over the waves, fragments prefetched before L1) ----
     {
         f32x4 po[MT][NO];
-        gemm_narrow_pre<P, MT, NOK, NO>(tA, ldh, ob, po, wave, lane);
+        gemm_narrow_pre<P, MT, NOK, NO, WAVES>(tA, ldh, ob, po, wave, lane);
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void actor_rowtile_kernel(ActorArgs a
         auto elem = [&](int q, float& eps, float& mu, float& lp, bool& unclipped) {
             eps = bo[q];
 #pragma unroll
-            for (int w = 0; w < DPPO_WAVES; ++w) eps += part[(w * ROWS + r) * (16 * NO) + q];
+            for (int w = 0; w < WAVES; ++w) eps += part[(w * ROWS + r) * (16 * NO) + q];
             const float x = xp[r * XD + q];
             float xr = sc[0] * x - sc[1] * eps;
             unclipped = fabsf(xr) <= 1.f;
@@ -416,15 +419,17 @@ struct CriticSmem {
     }
 };
 
-template <class P, int MT, int NT, bool TRAIN>
-__global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs a) {
+template <class P, int MT, int NT, bool TRAIN, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void critic_rowtile_kernel(CriticArgs a) {
     using AT = typename P::AT;
+    constexpr int THREADS = 64 * WAVES;
     constexpr int ROWS = 16 * MT;
-    constexpr int KSH = ksh_for<P>(NT);
+    static_assert(ROWS <= 64, "the epilogue maps one row per lane of wave 0");
+    constexpr int KSH = ksh_for<P>(NT, WAVES);
     constexpr int NOK = nok_for<P>(NT);
     constexpr int KSI = 2, KSO = 2;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const MlpLayout& L = a.L;
     const CriticSmem<P, MT> S(a);
     const int pad = lds_pad_elems<P>();
@@ -440,7 +445,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
     int* rn = (int*)(smem + S.rn);
     float* bias = (float*)(smem + S.bias);
     float* part = (float*)(smem + S.tB);
-    for (int i = tid; i < 3 * HC + 16; i += DPPO_THREADS) {
+    for (int i = tid; i < 3 * HC + 16; i += THREADS) {
         const int seg = i < HC ? SEG_B_IN : (i < 2 * HC ? SEG_B_L1 : (i < 3 * HC ? SEG_B_L2 : SEG_B_OUT));
         const int j = i < 3 * HC ? i % HC : i - 3 * HC;
         bias[i] = ((const float*)(a.packed + L.off[seg]))[j];
@@ -461,12 +466,12 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
         rn[tid] = n;
     }
     __syncthreads();
-    for (int i = tid; i < ROWS * k1w; i += DPPO_THREADS) {
+    for (int i = tid; i < ROWS * k1w; i += THREADS) {
         const int r = i / k1w, c = i % k1w, n = rn[r];
         a0[r * lda0 + c] = P::cvt((n >= 0 && c < SD) ? a.obs[(size_t)n * SD + c] : 0.f);
     }
     if (train) {
-        for (int i = tid; i < ROWS * SD; i += DPPO_THREADS) {
+        for (int i = tid; i < ROWS * SD; i += THREADS) {
             const int c = i / ROWS, r = i % ROWS, n = rn[r];
             ((AT*)a.ws.csT)[(size_t)c * a.ws.ldm + grow0 + r] = P::cvt(n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f);
         }
@@ -474,12 +479,13 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
     __syncthreads();
 
     const int ntile0 = wave * NT;
-    auto W = [&](int seg) { return (const u32x4*)(a.packed + L.off[seg]); };
+    const __amdgpu_buffer_rsrc_t rs = packed_rsrc(a.packed);
+    auto W = [&](int seg) { return wsrc(rs, L.off[seg]); };
     f32x4 H1[MT][NT], H2[MT][NT], acc[MT][NT];
     WRing<NT> R;
     ring_prime(R, W(SEG_W_IN), KSI, ntile0, lane);
     ORing<NOK, 1> ob;
-    out_prefetch(ob, W(SEG_W_OUT), KSH, wave, lane);
+    out_prefetch<NOK, 1, WAVES>(ob, W(SEG_W_OUT), KSH, wave, lane);
     // L1: h1 = s W_in + b
     gemm_stream<P, MT, NT, KSI>(a0, lda0, W(SEG_W_IN), ntile0, H1, lane, R, NextLayer{W(SEG_W_L1), KSH, ntile0});
     add_bias(H1, bias, ntile0, lane);
@@ -520,7 +526,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
     // L4: V = h3 W_out + b
     {
         f32x4 po[MT][1];
-        gemm_narrow_pre<P, MT, NOK, 1>(tA, ldh, ob, po, wave, lane);
+        gemm_narrow_pre<P, MT, NOK, 1, WAVES>(tA, ldh, ob, po, wave, lane);
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -531,7 +537,7 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
         const int r = lane, n = rn[r];
         float V = bias[3 * HC];
 #pragma unroll
-        for (int w = 0; w < DPPO_WAVES; ++w) V += part[(w * ROWS + r) * 16];
+        for (int w = 0; w < WAVES; ++w) V += part[(w * ROWS + r) * 16];
         if (!train) {
             if (n >= 0) a.values[n] = V;
         } else {
@@ -580,39 +586,41 @@ __global__ __launch_bounds__(DPPO_THREADS) void critic_rowtile_kernel(CriticArgs
 // =============================================================================================
 // launchers
 // =============================================================================================
-template <class P, int MT, int NT, int NO, int KSI, bool TRAIN>
+template <class P, int MT, int NT, int NO, int KSI, bool TRAIN, int WAVES>
 static int launch_actor_t(const ActorArgs& a, hipStream_t s) {
-    if (a.L.ks_in != KSI || a.L.ks_h != ksh_for<P>(NT) || a.L.ks_out_t != 2 || a.L.ks_h != DPPO_WAVES * nok_for<P>(NT))
+    if (a.L.ks_in != KSI || a.L.ks_h != ksh_for<P>(NT, WAVES) || a.L.ks_out_t != 2 || a.L.ks_h != WAVES * nok_for<P>(NT))
         return dppo_set_error(DPPO_EUNSUPPORTED, "actor row tile: layout does not match the instantiation");
     const ActorSmem<P, MT> S(a);
     const int pad = lds_pad_elems<P>();
-    const size_t part_bytes = (size_t)4 * DPPO_WAVES * 16 * MT * 16 * NO;
+    const size_t part_bytes = (size_t)4 * WAVES * 16 * MT * 16 * NO;
     const size_t tb_bytes = sizeof(typename P::AT) * 16 * MT * (a.H + pad);
     if (part_bytes > tb_bytes) return dppo_set_error(DPPO_EUNSUPPORTED, "actor: partial buffer does not fit");
     if (S.total > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "actor row tile needs %zu B LDS", S.total);
-    auto k = actor_rowtile_kernel<P, MT, NT, NO, KSI, TRAIN>;
+    auto k = actor_rowtile_kernel<P, MT, NT, NO, KSI, TRAIN, WAVES>;
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S.total));
     // TRAIN mode covers every row of the 64-padded feature-major images (padding rows get
     // finite activations and zero gradients), so the dW kernel never reads unwritten memory
     const int64_t rows = a.mode == ROWS_TRAIN ? (int64_t)a.ws.ldm : a.nrows;
     const int64_t grid = (rows + 16 * MT - 1) / (16 * MT);
     if (grid == 0) return DPPO_OK;
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(DPPO_THREADS), S.total, s, a);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * WAVES), S.total, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
 
-template <class P, int MT, int NT, int NO, int KSI>
+template <class P, int MT, int NT, int NO, int KSI, int WAVES>
 static int launch_actor_m(const ActorArgs& a, hipStream_t s) {
-    return a.mode == ROWS_TRAIN ? launch_actor_t<P, MT, NT, NO, KSI, true>(a, s)
-                                : launch_actor_t<P, MT, NT, NO, KSI, false>(a, s);
+    return a.mode == ROWS_TRAIN ? launch_actor_t<P, MT, NT, NO, KSI, true, WAVES>(a, s)
+                                : launch_actor_t<P, MT, NT, NO, KSI, false, WAVES>(a, s);
 }
 
-template <class P, int MT>
+// bf16: 64-row tiles, 16 waves (half the weight stream per row of 32-row tiles; LDS-limited);
+// fp32: 32-row tiles, 8 waves
+template <class P, int MT, int WAVES>
 static int dispatch_actor(const ActorArgs& a, hipStream_t s) {
-    const int NT = a.H / (16 * DPPO_WAVES), NO = dppo_cdiv(a.XD, 16), KSI = a.L.ks_in;
+    const int NT = a.H / (16 * WAVES), NO = dppo_cdiv(a.XD, 16), KSI = a.L.ks_in;
 #define DPPO_ACTOR_CASE(nt, no, ksi) \
-    if (NT == nt && NO == no && KSI == ksi) return launch_actor_m<P, MT, nt, no, ksi>(a, s);
+    if (NT == nt && NO == no && KSI == ksi) return launch_actor_m<P, MT, nt, no, ksi, WAVES>(a, s);
     if constexpr (P::KG == 32) {   // bf16: the in-layer is 2 k-steps up to 64 inputs, 4 up to 128
         DPPO_ACTOR_CASE(4, 1, 2) DPPO_ACTOR_CASE(4, 2, 2) DPPO_ACTOR_CASE(4, 1, 4) DPPO_ACTOR_CASE(4, 2, 4)
         DPPO_ACTOR_CASE(2, 1, 2) DPPO_ACTOR_CASE(2, 2, 2) DPPO_ACTOR_CASE(2, 1, 4) DPPO_ACTOR_CASE(2, 2, 4)
@@ -623,41 +631,41 @@ static int dispatch_actor(const ActorArgs& a, hipStream_t s) {
     return dppo_set_error(DPPO_EUNSUPPORTED, "actor: hidden %d / chunk %d not instantiated", a.H, a.XD);
 }
 
-// rows per workgroup of the update kernels: 64 (bf16) / 32 (fp32, LDS-limited)
-int actor_rows_per_tile(int precision) { (void)precision; return 32; }
-
 int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
-    return precision == DPPO_BF16 ? dispatch_actor<PolicyBF16, 2>(a, s) : dispatch_actor<PolicyF32, 2>(a, s);
+    if (precision != DPPO_BF16) return dispatch_actor<PolicyF32, 2, 8>(a, s);
+    return dispatch_actor<PolicyBF16, 2, 8>(a, s);
 }
 
-template <class P, int MT, int NT, bool TRAIN>
+template <class P, int MT, int NT, bool TRAIN, int WAVES>
 static int launch_critic_t(const CriticArgs& a, hipStream_t s) {
-    if (a.L.ks_in != 2 || a.L.ks_h != ksh_for<P>(NT) || a.L.ks_out_t != 2 || a.L.ks_h != DPPO_WAVES * nok_for<P>(NT))
+    if (a.L.ks_in != 2 || a.L.ks_h != ksh_for<P>(NT, WAVES) || a.L.ks_out_t != 2 || a.L.ks_h != WAVES * nok_for<P>(NT))
         return dppo_set_error(DPPO_EUNSUPPORTED, "critic row tile: layout does not match the instantiation");
     const CriticSmem<P, MT> S(a);
     if (S.total > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "critic row tile needs %zu B LDS", S.total);
-    auto k = critic_rowtile_kernel<P, MT, NT, TRAIN>;
+    if ((size_t)4 * WAVES * 16 * MT * 16 > sizeof(typename P::AT) * 16 * MT * (a.HC + lds_pad_elems<P>()))
+        return dppo_set_error(DPPO_EUNSUPPORTED, "critic: partial buffer does not fit");
+    auto k = critic_rowtile_kernel<P, MT, NT, TRAIN, WAVES>;
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S.total));
     // TRAIN mode covers every row of the 64-padded feature-major images (padding rows get
     // finite activations and zero gradients), so the dW kernel never reads unwritten memory
     const int64_t rows = a.mode == ROWS_TRAIN ? (int64_t)a.ws.ldm : a.nrows;
     const int64_t grid = (rows + 16 * MT - 1) / (16 * MT);
     if (grid == 0) return DPPO_OK;
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(DPPO_THREADS), S.total, s, a);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * WAVES), S.total, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
 
-template <class P, int MT>
+template <class P, int MT, int WAVES>
 static int dispatch_critic(const CriticArgs& a, hipStream_t s) {
-    const int NT = a.HC / (16 * DPPO_WAVES);
+    const int NT = a.HC / (16 * WAVES);
     const bool tr = a.mode == ROWS_TRAIN;
-    if (NT == 2) return tr ? launch_critic_t<P, MT, 2, true>(a, s) : launch_critic_t<P, MT, 2, false>(a, s);
+    if (NT == 2) return tr ? launch_critic_t<P, MT, 2, true, WAVES>(a, s) : launch_critic_t<P, MT, 2, false, WAVES>(a, s);
     return dppo_set_error(DPPO_EUNSUPPORTED, "critic: hidden %d not instantiated", a.HC);
 }
 
 int launch_critic_rowtile(const CriticArgs& a, int precision, hipStream_t s) {
-    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2>(a, s) : dispatch_critic<PolicyF32, 2>(a, s);
+    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8>(a, s) : dispatch_critic<PolicyF32, 2, 8>(a, s);
 }
 
 // =============================================================================================

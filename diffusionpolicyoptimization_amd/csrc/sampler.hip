@@ -38,7 +38,7 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
     constexpr int KSH = ksh_for<P>(NT, SW);
     constexpr int NOK = KSH / SW;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int row0 = blockIdx.x * 16;
     const MlpLayout& L = a.L;
     const int pad = lds_pad_elems<P>();
@@ -121,7 +121,8 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
     __syncthreads();
 
     const int ntile0 = wave * NT;
-    auto W = [&](const uint8_t* PK, int seg) { return (const u32x4*)(PK + L.off[seg]); };
+    const __amdgpu_buffer_rsrc_t rs_base = packed_rsrc(a.packed_base), rs_ft = packed_rsrc(a.packed_ft);
+    auto W = [&](const uint8_t* PK, int seg) { return wsrc(PK == a.packed_ft ? rs_ft : rs_base, L.off[seg]); };
     // the stream starts with step 0's in-layer (t = K-1)
     WRing<NT> R;
     ring_prime(R, W(K - 1 < KF ? a.packed_ft : a.packed_base, SEG_W_IN), L.ks_in, ntile0, lane);

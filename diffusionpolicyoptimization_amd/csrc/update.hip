@@ -4,15 +4,24 @@
 
 // ---------------------------------------------------------------------------------------------
 // grouped split-K weight-gradient GEMM:  G[k][n] += sum_m XT[k][m] * DT[n][m]
-// (dW = X^T dH in Keras [in,out] layout). A workgroup owns a 64x64 output tile and one m-chunk;
-// 4 waves each hold a 32x32 sub-tile (2x2 MFMA tiles). Both operands are feature-major, so every
-// fragment is 16 contiguous bytes along m. The k-tile-0 workgroups also produce the "extra" rows:
+// (dW = X^T dH in Keras [in,out] layout). A workgroup (4 waves) owns a 128x128 output tile and
+// one m-chunk; each wave holds a 64x64 sub-tile (4x4 MFMA tiles, 64 accumulator VGPRs). Both
+// operands are feature-major, so a stage of BK rows is one 128-B line per feature: the stage is
+// copied global -> LDS with 16-B global_load_lds (one 1 KiB wave-instruction = 8 features), two
+// LDS buffers so the copy of stage s+1 overlaps the MFMAs of stage s. The LDS image is linear
+// per wave-instruction; the bank swizzle (16-B slot = chunk ^ (feature & 7)) is applied on the
+// global source address, which makes the fragment reads (ds_read_b128) conflict-free.
+// The k-tile-0 workgroups also produce the "extra" rows:
 //   ONES   -> bias gradient  sum_m DT[n][m]
 //   ONEHOT -> per-bucket sums sum_{m: seg[m]=q} DT[n][m]  (actor in-layer: in_b and d t_emb)
 // Partial tiles are added with fp32 atomics (one add per element per m-chunk).
 // ---------------------------------------------------------------------------------------------
 enum { EXTRA_NONE = 0, EXTRA_ONES = 1, EXTRA_ONEHOT = 2 };
 #define DW_MAXP 8
+#define DW_T 128             // output tile edge
+#define DW_LINE 128          // bytes per feature per stage
+#define DW_OPB (DW_T * DW_LINE)   // 16 KiB: one operand's stage image
+#define DW_SEG_MAX 8192           // max rows per m-chunk (the chunk's seg bytes are staged in LDS)
 
 struct DWProb {
     const void* XT; const void* DT; float* G; float* Gx;
@@ -26,84 +35,141 @@ struct DWArgs {
     const int8_t* seg;
 };
 
-template <class P>
-__device__ inline u32x4 load_frag_rows(const typename P::AT* base, size_t ldm, int row, int nrows, size_t m) {
-    const int rr = row < nrows ? row : nrows - 1;
-    u32x4 v = *reinterpret_cast<const u32x4*>(base + (size_t)rr * ldm + m);
-    if (row >= nrows) v = u32x4{0u, 0u, 0u, 0u};
-    return v;
-}
+typedef __attribute__((address_space(3))) void lds_void_t;
 
+// extra A fragment: row q of [ones] or [one-hot(seg == q)] over EPL consecutive rows; the
+// chunk's seg bytes sit in LDS (staged before the glds pipeline starts)
 template <class P>
-__device__ inline u32x4 extra_frag(int extra, int q, const int8_t* seg, size_t m) {
+__device__ inline u32x4 extra_frag(int extra, int q, const int8_t* seg_lds) {
     using AT = typename P::AT;
     AT e[P::EPL];
+    if (extra == EXTRA_ONES) {
 #pragma unroll
-    for (int i = 0; i < P::EPL; ++i) {
-        float v = extra == EXTRA_ONES ? 1.f : ((int)seg[m + i] == q ? 1.f : 0.f);
-        e[i] = P::cvt(v);
+        for (int i = 0; i < P::EPL; ++i) e[i] = P::cvt(1.f);
+    } else {   // EPL bytes in one LDS read (8-B / 4-B aligned by construction)
+        const uint64_t w = P::EPL == 8 ? *reinterpret_cast<const uint64_t*>(seg_lds)
+                                       : (uint64_t)*reinterpret_cast<const uint32_t*>(seg_lds);
+#pragma unroll
+        for (int i = 0; i < P::EPL; ++i) e[i] = P::cvt((int)(int8_t)(w >> (8 * i)) == q ? 1.f : 0.f);
     }
     return __builtin_bit_cast(u32x4, e);
+}
+
+// fragment of a staged operand: feature f (0..127 within the tile), 16-B chunk c (0..7)
+__device__ inline u32x4 dw_lds_frag(const uint8_t* img, int f, int c) {
+    return *reinterpret_cast<const u32x4*>(img + f * DW_LINE + ((c ^ (f & 7)) << 4));
 }
 
 template <class P>
 __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
     using AT = typename P::AT;
+    constexpr int BK = DW_LINE / (int)sizeof(AT);     // rows per stage: 64 bf16 / 32 fp32
+    constexpr int EPC = 16 / (int)sizeof(AT);         // elements per 16-B chunk
+    // one LDS object (a second __shared__ array can make hipcc drain the glds queue at every
+    // fragment read): [buf][A|B] stage images, then the chunk's seg bytes
+    __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * 2 * DW_OPB + DW_SEG_MAX];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int chunk = blockIdx.x % a.nchunks;
-    const int tile = blockIdx.x / a.nchunks;
+    // XCD-aware order: block b runs on XCD b % 8; XCD x takes the contiguous logical range
+    // [x*per, (x+1)*per) of the chunk-major order, so the tiles that share one m-chunk's operand
+    // slabs run together on one XCD and re-read them from its L2 instead of HBM/MALL.
+    const int tiles_all = a.tile_start[a.nprob];
+    const int total = tiles_all * a.nchunks;
+    const int per = (total + 7) >> 3;
+    const int lg = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (lg >= total) return;
+    const int chunk = lg / tiles_all;
+    const int tile = lg % tiles_all;
     int pi = 0;
     while (pi + 1 < a.nprob && tile >= a.tile_start[pi + 1]) ++pi;
     const DWProb& pr = a.p[pi];
     const int lt = tile - a.tile_start[pi];
     const int kt = lt / pr.ntiles, nt = lt % pr.ntiles;
+    const int k_base = kt * DW_T, n_base = nt * DW_T;
     const int wr = wave >> 1, wc = wave & 1;
-    const int k0 = kt * 64 + wr * 32, n0 = nt * 64 + wc * 32;
     const size_t m_begin = (size_t)chunk * a.mchunk;
     const size_t m_end = m_begin + a.mchunk < a.ldm ? m_begin + a.mchunk : a.ldm;
     if (m_begin >= m_end) return;
+    const int nst = (int)((m_end - m_begin) / BK);
     const AT* XT = (const AT*)pr.XT;
     const AT* DT = (const AT*)pr.DT;
     const bool do_extra = pr.extra != EXTRA_NONE && kt == 0 && wr == 0;
-    f32x4 acc[2][2], acce[2];
+    int8_t* seg_lds = (int8_t*)(smem + 4 * DW_OPB);
+    if (pr.extra == EXTRA_ONEHOT && kt == 0) {
+        for (int i = tid; i < (int)(m_end - m_begin); i += 256) seg_lds[i] = a.seg[m_begin + i];
+    }
+
+    // per-lane glds sources for this wave's 4 A + 4 B wave-instructions (features ins*8 + lane/8)
+    const AT* srcA[4];
+    const AT* srcB[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 4; ++i) {
+        const int ins = wave + 4 * i;
+        const int f = ins * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ (f & 7);
+        int fa = k_base + f; fa = fa < pr.Kx ? fa : pr.Kx - 1;
+        int fb = n_base + f; fb = fb < pr.N ? fb : pr.N - 1;
+        srcA[i] = XT + (size_t)fa * a.ldm + m_begin + c * EPC;
+        srcB[i] = DT + (size_t)fb * a.ldm + m_begin + c * EPC;
+    }
+    auto issue = [&](int st, int buf) {
+        uint8_t* base = smem + buf * 2 * DW_OPB;
+        const size_t off = (size_t)st * BK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ins = wave + 4 * i;
+            __builtin_amdgcn_global_load_lds((void*)(srcA[i] + off), (lds_void_t*)(base + ins * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((void*)(srcB[i] + off), (lds_void_t*)(base + DW_OPB + ins * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[4][4], acce[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
         zero_acc(acce[i]);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) zero_acc(acc[i][j]);
+        for (int j = 0; j < 4; ++j) zero_acc(acc[i][j]);
     }
-    const int lr = lane & 15, lq = (lane >> 4) * P::EPL;
-    for (size_t m = m_begin; m < m_end; m += P::KG) {
-        const size_t mm = m + lq;
-        u32x4 A0 = load_frag_rows<P>(XT, a.ldm, k0 + lr, pr.Kx, mm);
-        u32x4 A1 = load_frag_rows<P>(XT, a.ldm, k0 + 16 + lr, pr.Kx, mm);
-        u32x4 B0 = load_frag_rows<P>(DT, a.ldm, n0 + lr, pr.N, mm);
-        u32x4 B1 = load_frag_rows<P>(DT, a.ldm, n0 + 16 + lr, pr.N, mm);
-        acc[0][0] = P::mma(A0, B0, acc[0][0]);
-        acc[0][1] = P::mma(A0, B1, acc[0][1]);
-        acc[1][0] = P::mma(A1, B0, acc[1][0]);
-        acc[1][1] = P::mma(A1, B1, acc[1][1]);
-        if (do_extra) {
-            const u32x4 AE = extra_frag<P>(pr.extra, lr, a.seg, mm);
-            acce[0] = P::mma(AE, B0, acce[0]);
-            acce[1] = P::mma(AE, B1, acce[1]);
+    const int fr = lane & 15, cq = lane >> 4;
+    issue(0, 0);
+    for (int st = 0; st < nst; ++st) {
+        __syncthreads();                         // stage st landed; buffer st+1 no longer read
+        if (st + 1 < nst) issue(st + 1, (st + 1) & 1);
+        const uint8_t* imA = smem + (st & 1) * 2 * DW_OPB;
+        const uint8_t* imB = imA + DW_OPB;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            u32x4 A[4], B[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                A[i] = dw_lds_frag(imA, wr * 64 + i * 16 + fr, ks * 4 + cq);
+                B[i] = dw_lds_frag(imB, wc * 64 + i * 16 + fr, ks * 4 + cq);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(A[i], B[j], acc[i][j]);
+            if (do_extra) {
+                const u32x4 AE = extra_frag<P>(pr.extra, fr, seg_lds + st * BK + ks * P::KG + cq * P::EPL);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acce[j] = P::mma(AE, B[j], acce[j]);
+            }
         }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int n = n0 + j * 16 + ccol(lane);
+        for (int j = 0; j < 4; ++j) {
+            const int n = n_base + wc * 64 + j * 16 + ccol(lane);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int k = k0 + i * 16 + crow(lane, r);
+                const int k = k_base + wr * 64 + i * 16 + crow(lane, r);
                 if (k < pr.Kx && n < pr.N) atomicAdd(pr.G + (size_t)k * pr.N + n, acc[i][j][r]);
             }
         }
     if (do_extra) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int n = n0 + j * 16 + ccol(lane);
+        for (int j = 0; j < 4; ++j) {
+            const int n = n_base + wc * 64 + j * 16 + ccol(lane);
             if (n >= pr.N) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -122,62 +188,70 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
 // time-MLP backward (mlp_diffusion.py:40-45) from the per-t bucket sums of dh1:
 //   in_b' = sum_q G[q];  dtemb[q] = G[q] . W_in[XD:XD+TD]^T;  then Dense/mish/Dense backward.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void time_bwd_kernel(const float* __restrict__ gseg, const float* __restrict__ prm,
+#define TB_THREADS 1024
+__global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __restrict__ gseg, const float* __restrict__ prm,
                                                        float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* dtemb = sm;                  // [KF][TD]
     float* e = dtemb + KF * TD;         // [KF][TD]
     float* a1 = e + KF * TD;            // [KF][2TD]
     float* da1 = a1 + KF * 2 * TD;      // [KF][2TD]
-    const int tid = threadIdx.x;
-    for (int n = tid; n < H; n += 256) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int n = tid; n < H; n += TB_THREADS) {
         float s = 0.f;
         for (int q = 0; q < KF; ++q) s += gseg[q * H + n];
         grad[F.in_b + n] = s;
     }
     const int half = TD / 2;
     const float lnf = logf(10000.f) / (float)(half - 1);
-    for (int i = tid; i < KF * TD; i += 256) {
+    // dtemb[q][j] = G[q] . W_in[XD + j]: one wave per output, lanes over the hidden units
+    for (int i = wave; i < KF * TD; i += TB_THREADS / 64) {
         const int q = i / TD, j = i % TD;
+        const float* g = gseg + q * H;
+        const float* w = prm + F.in_w + (size_t)(XD + j) * H;
         float s = 0.f;
-        for (int n = 0; n < H; ++n) s += gseg[q * H + n] * prm[F.in_w + (size_t)(XD + j) * H + n];
-        dtemb[i] = s;
+        for (int n = lane; n < H; n += 64) s += g[n] * w[n];
+        s = wave_sum(s);
+        if (lane == 0) dtemb[i] = s;
+    }
+    for (int i = tid; i < KF * TD; i += TB_THREADS) {
+        const int q = i / TD, j = i % TD;
         const float f = expf(-(float)(j % half) * lnf) * (float)q;
         e[i] = j < half ? sinf(f) : cosf(f);
     }
     __syncthreads();
-    for (int i = tid; i < KF * 2 * TD; i += 256) {
+    for (int i = tid; i < KF * 2 * TD; i += TB_THREADS) {
         const int q = i / (2 * TD), h = i % (2 * TD);
         float s = prm[F.time_b1 + h];
         for (int k = 0; k < TD; ++k) s += e[q * TD + k] * prm[F.time_w1 + k * 2 * TD + h];
         a1[i] = s;
     }
     __syncthreads();
-    for (int i = tid; i < KF * 2 * TD; i += 256) {
+    for (int i = tid; i < KF * 2 * TD; i += TB_THREADS) {
         const int q = i / (2 * TD), h = i % (2 * TD);
         float dm = 0.f;
         for (int j = 0; j < TD; ++j) dm += dtemb[q * TD + j] * prm[F.time_w2 + h * TD + j];
         da1[i] = dm * mish_gradf(a1[i]);
     }
     __syncthreads();
-    for (int i = tid; i < 2 * TD * TD; i += 256) {            // time_w2 [2TD][TD]
+    for (int i = tid; i < 2 * TD * TD; i += TB_THREADS) {            // time_w2 [2TD][TD]
         const int h = i / TD, j = i % TD;
         float s = 0.f;
         for (int q = 0; q < KF; ++q) s += mishf(a1[q * 2 * TD + h]) * dtemb[q * TD + j];
         grad[F.time_w2 + i] = s;
     }
-    for (int j = tid; j < TD; j += 256) {
+    for (int j = tid; j < TD; j += TB_THREADS) {
         float s = 0.f;
         for (int q = 0; q < KF; ++q) s += dtemb[q * TD + j];
         grad[F.time_b2 + j] = s;
     }
-    for (int i = tid; i < TD * 2 * TD; i += 256) {            // time_w1 [TD][2TD]
+    for (int i = tid; i < TD * 2 * TD; i += TB_THREADS) {            // time_w1 [TD][2TD]
         const int k = i / (2 * TD), h = i % (2 * TD);
         float s = 0.f;
         for (int q = 0; q < KF; ++q) s += e[q * TD + k] * da1[q * 2 * TD + h];
         grad[F.time_w1 + i] = s;
     }
-    for (int h = tid; h < 2 * TD; h += 256) {
+    for (int h = tid; h < 2 * TD; h += TB_THREADS) {
         float s = 0.f;
         for (int q = 0; q < KF; ++q) s += da1[q * 2 * TD + h];
         grad[F.time_b1 + h] = s;
@@ -294,7 +368,7 @@ extern "C" size_t dppo_ppo_workspace_bytes(const dppo_dims* d, int precision, in
 template <class P>
 static int launch_dw(const DWArgs& a, hipStream_t s) {
     const int tiles = a.tile_start[a.nprob];
-    const int64_t blocks = (int64_t)tiles * a.nchunks;
+    const int64_t blocks = 8 * (((int64_t)tiles * a.nchunks + 7) / 8);   // whole XCD rounds
     hipLaunchKernelGGL(dw_kernel<P>, dim3((unsigned)blocks), dim3(256), 0, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
@@ -361,7 +435,7 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
         DWProb& p = w.p[w.nprob];
         p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
-        p.ktiles = dppo_cdiv(Kx, 64); p.ntiles = dppo_cdiv(N, 64);
+        p.ktiles = dppo_cdiv(Kx, DW_T); p.ntiles = dppo_cdiv(N, DW_T);
         w.tile_start[w.nprob + 1] = w.tile_start[w.nprob] + p.ktiles * p.ntiles;
         w.nprob++;
     };
@@ -375,11 +449,13 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     add(ws.ch3T, D.HC, ws.cdvT, 1, gc + FC.out_w, EXTRA_ONES, gc + FC.out_b);
     w.ldm = ws.ldm;
     w.seg = ws.seg;
-    // m-chunks: about 6 workgroups per CU over the whole grid, chunk a multiple of 64 rows
+    // m-chunks: about 2 workgroups per CU over the whole grid, chunk a multiple of 64 rows
     const int tiles = w.tile_start[w.nprob];
-    int nch = dppo_cdiv(256 * 6, tiles);
+    int nch = dppo_cdiv(256 * 2, tiles);
     const int max_ch = (int)(ws.ldm / 64);
+    const int min_ch = dppo_cdiv((int)ws.ldm, DW_SEG_MAX);
     if (nch > max_ch) nch = max_ch;
+    if (nch < min_ch) nch = min_ch;
     if (nch < 1) nch = 1;
     w.mchunk = (int)(dppo_cdiv((int)ws.ldm, nch * 64) * 64);
     w.nchunks = dppo_cdiv((int)ws.ldm, w.mchunk);
@@ -387,7 +463,7 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     if (rc) return rc;
 
     const size_t tsm = sizeof(float) * (size_t)D.KF * (2 * D.TD + 2 * 2 * D.TD);
-    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(256), tsm, s, ws.gseg, actor_params, ga, FA, D.XD, D.TD, D.H, D.KF);
+    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, ws.gseg, actor_params, ga, FA, D.XD, D.TD, D.H, D.KF);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
