@@ -14,6 +14,7 @@
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 
 #define DPPO_WAVES 8
 #define DPPO_THREADS (DPPO_WAVES * 64)
@@ -221,6 +222,9 @@ __device__ inline float mishf(float x) {
     return x > 15.f ? x : x * n * __builtin_amdgcn_rcpf(n + 2.f);
 }
 __device__ inline float mish_gradf(float x) {
+    // opaque copy: stops hipcc from sharing e/n with a forward mishf of the same value, which
+    // would keep them live from the forward to the backward pass (register spills)
+    asm volatile("" : "+v"(x));
     const float e = __expf(fminf(x, 15.f));
     const float n = e * (e + 2.f);
     const float r = __builtin_amdgcn_rcpf(n + 2.f);

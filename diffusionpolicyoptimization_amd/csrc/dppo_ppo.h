@@ -6,6 +6,7 @@
 // feature-major ("transposed") activation / gradient images written by the row-tile kernels and
 // consumed by the split-K weight-gradient kernel: X^T[f][ldm], ldm = rows rounded up to 64.
 struct PpoWorkspace {
+    uint8_t* base;    // start of the workspace (buffer-resource base of the image stores)
     size_t ldm;
     // actor
     void *a0T, *u1T, *u2T, *h3T, *dyT, *dh3T, *dh2T, *dh1T;
@@ -19,6 +20,7 @@ struct PpoWorkspace {
 
 inline PpoWorkspace make_ppo_workspace(const Dims& D, int precision, int rows, uint8_t* base) {
     PpoWorkspace w;
+    w.base = base;
     const size_t es = precision == DPPO_BF16 ? 2 : 4;
     w.ldm = (size_t)dppo_cdiv(rows > 0 ? rows : 1, 64) * 64;
     size_t o = 0;
@@ -36,6 +38,11 @@ inline PpoWorkspace make_ppo_workspace(const Dims& D, int precision, int rows, u
     w.stats = base ? (double*)(base + o) : nullptr; o = dppo_align256(o + 8 * 4);
     w.total = o;
     return w;
+}
+
+// byte offset of an image inside the workspace (< 2 GiB: checked by dppo_ppo_minibatch)
+__host__ __device__ inline uint32_t ws_off(const PpoWorkspace& w, const void* img) {
+    return (uint32_t)((const uint8_t*)img - w.base);
 }
 
 // per-row source of a row-tile launch

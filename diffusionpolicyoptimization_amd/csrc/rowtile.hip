@@ -10,31 +10,41 @@
 //                         writing feature-major activation/gradient images for the dW kernel
 //   critic, mode VALUE  : CriticObs forward (model/common/critic.py:40-54)
 //   critic, mode TRAIN  : forward -> v_loss gradient (diffusion_ppo.py:108-118) -> backward chain
+#include <stdlib.h>
+#include <string.h>
 #include "dppo_ppo.h"
 
 #define LOG_2PI_HALF 0.91893853320467274178f
 
-// 4 consecutive rows of one column into a feature-major image XT[col][row..row+3]
-template <class P>
-__device__ inline void store4T(void* XTv, size_t ldm, int col, size_t row, float v0, float v1, float v2, float v3) {
-    using AT = typename P::AT;
-    AT* XT = (AT*)XTv + (size_t)col * ldm + row;
-    if constexpr (sizeof(AT) == 2) {
-        __bf16 e[4] = {(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)v3};
-        *reinterpret_cast<uint2*>(XT) = __builtin_bit_cast(uint2, e);
-    } else {
-        *reinterpret_cast<float4*>(XT) = make_float4(v0, v1, v2, v3);
-    }
-}
-
+// Accumulator tile -> feature-major image XT[col][row] (4 consecutive rows per lane per MFMA
+// tile). Buffer stores through ONE resource for the whole workspace: the per-lane part of the
+// offset is a single 32-bit VGPR, the image / tile parts are scalar, so no 64-bit address pairs
+// are kept live across the unrolled layers.
 template <class P, int MT, int NT>
-__device__ inline void store_accT(void* XT, size_t ldm, int ntile0, size_t grow0, int lane, const f32x4 (&v)[MT][NT]) {
+__device__ inline void store_accT(__amdgpu_buffer_rsrc_t ws, uint32_t img_off, uint32_t ldm, int ntile0, uint32_t grow0,
+                                  int lane, const f32x4 (&v)[MT][NT]) {
+    using AT = typename P::AT;
+    constexpr uint32_t es = sizeof(AT);
+    const uint32_t vo = ((uint32_t)ccol(lane) * ldm + (uint32_t)((lane >> 4) << 2)) * es;
+    const uint32_t so0 = img_off + ((uint32_t)ntile0 * 16u * ldm + grow0) * es;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
-            store4T<P>(XT, ldm, (ntile0 + n) * 16 + ccol(lane), grow0 + m * 16 + ((lane >> 4) << 2),
-                       v[m][n][0], v[m][n][1], v[m][n][2], v[m][n][3]);
+        for (int n = 0; n < NT; ++n) {
+            const uint32_t so = so0 + ((uint32_t)n * 16u * ldm + (uint32_t)m * 16u) * es;
+            if constexpr (es == 2) {
+                __bf16 e[4] = {(__bf16)v[m][n][0], (__bf16)v[m][n][1], (__bf16)v[m][n][2], (__bf16)v[m][n][3]};
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, e), ws, vo, so, 0);
+            } else {
+                // two 8-B stores: the 16-B buffer_store form came out with a corrupted 4th dword
+                // under hipcc 7.2 for gfx950 in the critic (a store-data hazard the compiler does
+                // not guard); 8-B stores are what the bf16 path uses and are exact here
+                const u32x2 w0 = {__float_as_uint(v[m][n][0]), __float_as_uint(v[m][n][1])};
+                const u32x2 w1 = {__float_as_uint(v[m][n][2]), __float_as_uint(v[m][n][3])};
+                __builtin_amdgcn_raw_buffer_store_b64(w0, ws, vo, so, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(w1, ws, vo, so + 8, 0);
+            }
+        }
 }
 
 template <class P, int MT, int NT>
@@ -92,7 +102,7 @@ struct ActorSmem {
 };
 
 template <class P, int MT, int NT, int NO, int KSI, bool TRAIN, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) {
+__device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     using AT = typename P::AT;
     constexpr int THREADS = 64 * WAVES;
     constexpr int ROWS = 16 * MT;
@@ -125,6 +135,8 @@ __global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) 
     int* rj = (int*)(smem + S.rj);
     float* part = (float*)(smem + S.tB);   // out-layer partials alias tB (u2 is dead by then)
     const size_t grow0 = (size_t)blockIdx.x * ROWS;
+    const __amdgpu_buffer_rsrc_t wsr = packed_rsrc(a.ws.base);
+    const uint32_t ldm32 = (uint32_t)a.ws.ldm, grow32 = (uint32_t)grow0;
 
     // ---- prologue: rows, schedule, time embedding for t < K' (actor_ft) ----
     if (tid < ROWS) {
@@ -209,11 +221,11 @@ __global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) 
     const __amdgpu_buffer_rsrc_t rs = packed_rsrc(a.packed);
     auto W = [&](int seg) { return wsrc(rs, L.off[seg]); };
     f32x4 H1[MT][NT], acc[MT][NT];
-    uint64_t mask1 = 0, mask2 = 0;
+    static_assert(MT * NT * 4 <= 32, "relu masks are 32-bit");
+    uint32_t mask1 = 0, mask2 = 0;
     WRing<NT> R;
     ring_prime(R, W(SEG_W_IN), KSI, ntile0, lane);
     ORing<NOK, NO> ob;
-    out_prefetch<NOK, NO, WAVES>(ob, W(SEG_W_OUT), KSH, wave, lane);
     // ---- L1: h1 = a0 W_in + b (no activation on the input layer) ----
     gemm_stream<P, MT, NT, KSI>(a0, lda0, W(SEG_W_IN), ntile0, H1, lane, R, NextLayer{W(SEG_W_L1), KSH, ntile0});
     add_bias(H1, bias, ntile0, lane);
@@ -224,10 +236,12 @@ __global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 acc[m][n][r] = fmaxf(H1[m][n][r], 0.f);
-                if (H1[m][n][r] > 0.f) mask1 |= 1ull << ((m * NT + n) * 4 + r);
+                if (H1[m][n][r] > 0.f) mask1 |= 1u << ((m * NT + n) * 4 + r);
             }
+    // materialise the mask now (otherwise hipcc keeps the 8*MT*NT floats alive until the backward)
+    asm volatile("" : "+v"(mask1));
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    if constexpr (train) store_accT<P, MT, NT>(a.ws.u1T, a.ws.ldm, ntile0, grow0, lane, acc);
+    if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.u1T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     // ---- L2: h2 = relu(h1) W_l1 + b ----
     gemm_stream<P, MT, NT, KSH>(tA, ldh, W(SEG_W_L1), ntile0, acc, lane, R, NextLayer{W(SEG_W_L2), KSH, ntile0});
@@ -238,12 +252,15 @@ __global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) 
         for (int n = 0; n < NT; ++n)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if (acc[m][n][r] > 0.f) mask2 |= 1ull << ((m * NT + n) * 4 + r);
+                if (acc[m][n][r] > 0.f) mask2 |= 1u << ((m * NT + n) * 4 + r);
                 acc[m][n][r] = fmaxf(acc[m][n][r], 0.f);
             }
+    asm volatile("" : "+v"(mask2));
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
-    if constexpr (train) store_accT<P, MT, NT>(a.ws.u2T, a.ws.ldm, ntile0, grow0, lane, acc);
+    if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.u2T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
+    // out-layer fragments: fetched here so they land during L3 (not held through L1/L2: VGPRs)
+    out_prefetch<NOK, NO, WAVES>(ob, W(SEG_W_OUT), KSH, wave, lane);
     // ---- L3: h3 = relu(h2) W_l2 + b + h1; the stream continues into the backward's W_out^T ----
     gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_W_L2), ntile0, acc, lane, R,
                                 train ? NextLayer{W(SEG_T_OUT), KSO, ntile0} : NextLayer{W(SEG_W_L2), KSH, ntile0});
@@ -255,7 +272,7 @@ __global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) 
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[m][n][r] += H1[m][n][r];
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    if constexpr (train) store_accT<P, MT, NT>(a.ws.h3T, a.ws.ldm, ntile0, grow0, lane, acc);
+    if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.h3T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     // ---- L4: eps = h3 W_out + b (k split over the waves, fragments prefetched before L1) ----
     {
@@ -364,11 +381,10 @@ __global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) 
     lds_sync();
 
     // ---- backward dX chain (weights continue in the same stream) ----
-    // B4: dh3 = dy W_out^T
-    f32x4 DH3[MT][NT];
-    gemm_stream<P, MT, NT, KSO>(a0, lda0, W(SEG_T_OUT), ntile0, DH3, lane, R, NextLayer{W(SEG_T_L2), KSH, ntile0});
-    store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, DH3);
-    store_accT<P, MT, NT>(a.ws.dh3T, a.ws.ldm, ntile0, grow0, lane, DH3);
+    // B4: dh3 = dy W_out^T (kept only in tB: B2 re-reads it from there, which frees 8*MT*NT VGPRs)
+    gemm_stream<P, MT, NT, KSO>(a0, lda0, W(SEG_T_OUT), ntile0, acc, lane, R, NextLayer{W(SEG_T_L2), KSH, ntile0});
+    store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
+    store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.dh3T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     // B3: dh2 = (dh3 W_l2^T) * relu'(h2)
     gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_T_L2), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});
@@ -378,9 +394,9 @@ __global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) 
         for (int n = 0; n < NT; ++n)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                if (!((mask2 >> ((m * NT + n) * 4 + r)) & 1ull)) acc[m][n][r] = 0.f;
+                if (!((mask2 >> ((m * NT + n) * 4 + r)) & 1u)) acc[m][n][r] = 0.f;
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    store_accT<P, MT, NT>(a.ws.dh2T, a.ws.ldm, ntile0, grow0, lane, acc);
+    store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.dh2T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     // B2: dh1 = dh3 + (dh2 W_l1^T) * relu'(h1)
     gemm_stream<P, MT, NT, KSH>(tA, ldh, W(SEG_T_L1), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});
@@ -390,10 +406,11 @@ __global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) 
         for (int n = 0; n < NT; ++n)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const bool on = (mask1 >> ((m * NT + n) * 4 + r)) & 1ull;
-                acc[m][n][r] = DH3[m][n][r] + (on ? acc[m][n][r] : 0.f);
+                const bool on = (mask1 >> ((m * NT + n) * 4 + r)) & 1u;
+                const float dh3 = P::tof(tB[(m * 16 + crow(lane, r)) * ldh + (ntile0 + n) * 16 + ccol(lane)]);
+                acc[m][n][r] = dh3 + (on ? acc[m][n][r] : 0.f);
             }
-    store_accT<P, MT, NT>(a.ws.dh1T, a.ws.ldm, ntile0, grow0, lane, acc);
+    store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.dh1T), ldm32, ntile0, grow32, lane, acc);
 }
 
 // =============================================================================================
@@ -420,7 +437,7 @@ struct CriticSmem {
 };
 
 template <class P, int MT, int NT, bool TRAIN, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void critic_rowtile_kernel(CriticArgs a) {
+__device__ __forceinline__ void critic_rowtile_body(const CriticArgs& a) {
     using AT = typename P::AT;
     constexpr int THREADS = 64 * WAVES;
     constexpr int ROWS = 16 * MT;
@@ -451,6 +468,8 @@ __global__ __launch_bounds__(64 * WAVES) void critic_rowtile_kernel(CriticArgs a
         bias[i] = ((const float*)(a.packed + L.off[seg]))[j];
     }
     const size_t grow0 = (size_t)blockIdx.x * ROWS;
+    const __amdgpu_buffer_rsrc_t wsr = packed_rsrc(a.ws.base);
+    const uint32_t ldm32 = (uint32_t)a.ws.ldm, grow32 = (uint32_t)grow0;
 
     if (tid < ROWS) {
         const int64_t gr = (int64_t)grow0 + tid;
@@ -496,7 +515,7 @@ __global__ __launch_bounds__(64 * WAVES) void critic_rowtile_kernel(CriticArgs a
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[m][n][r] = mishf(H1[m][n][r]);
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    if constexpr (train) store_accT<P, MT, NT>(a.ws.cu1T, a.ws.ldm, ntile0, grow0, lane, acc);
+    if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.cu1T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     // L2: h2 = mish(h1) W_l1 + b
     gemm_stream<P, MT, NT, KSH>(tA, ldh, W(SEG_W_L1), ntile0, H2, lane, R, NextLayer{W(SEG_W_L2), KSH, ntile0});
@@ -508,7 +527,7 @@ __global__ __launch_bounds__(64 * WAVES) void critic_rowtile_kernel(CriticArgs a
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[m][n][r] = mishf(H2[m][n][r]);
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
-    if constexpr (train) store_accT<P, MT, NT>(a.ws.cu2T, a.ws.ldm, ntile0, grow0, lane, acc);
+    if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.cu2T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     // L3: h3 = mish(h2) W_l2 + b + h1
     gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_W_L2), ntile0, acc, lane, R,
@@ -521,7 +540,7 @@ __global__ __launch_bounds__(64 * WAVES) void critic_rowtile_kernel(CriticArgs a
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[m][n][r] += H1[m][n][r];
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    if constexpr (train) store_accT<P, MT, NT>(a.ws.ch3T, a.ws.ldm, ntile0, grow0, lane, acc);
+    if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.ch3T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     // L4: V = h3 W_out + b
     {
@@ -555,11 +574,10 @@ __global__ __launch_bounds__(64 * WAVES) void critic_rowtile_kernel(CriticArgs a
     }
     if constexpr (!train) return;
     lds_sync();
-    // B4: dh3 = dV W_out^T
-    f32x4 DH3[MT][NT];
-    gemm_stream<P, MT, NT, KSO>(a0, lda0, W(SEG_T_OUT), ntile0, DH3, lane, R, NextLayer{W(SEG_T_L2), KSH, ntile0});
-    store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, DH3);
-    store_accT<P, MT, NT>(a.ws.cdh3T, a.ws.ldm, ntile0, grow0, lane, DH3);
+    // B4: dh3 = dV W_out^T (kept only in tB, re-read by B2)
+    gemm_stream<P, MT, NT, KSO>(a0, lda0, W(SEG_T_OUT), ntile0, acc, lane, R, NextLayer{W(SEG_T_L2), KSH, ntile0});
+    store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
+    store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.cdh3T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     // B3: dh2 = (dh3 W_l2^T) * mish'(h2)
     gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_T_L2), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});
@@ -570,7 +588,7 @@ __global__ __launch_bounds__(64 * WAVES) void critic_rowtile_kernel(CriticArgs a
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[m][n][r] *= mish_gradf(H2[m][n][r]);
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    store_accT<P, MT, NT>(a.ws.cdh2T, a.ws.ldm, ntile0, grow0, lane, acc);
+    store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.cdh2T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     // B2: dh1 = dh3 + (dh2 W_l1^T) * mish'(h1)
     gemm_stream<P, MT, NT, KSH>(tA, ldh, W(SEG_T_L1), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});
@@ -579,14 +597,54 @@ __global__ __launch_bounds__(64 * WAVES) void critic_rowtile_kernel(CriticArgs a
 #pragma unroll
         for (int n = 0; n < NT; ++n)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[m][n][r] = DH3[m][n][r] + acc[m][n][r] * mish_gradf(H1[m][n][r]);
-    store_accT<P, MT, NT>(a.ws.cdh1T, a.ws.ldm, ntile0, grow0, lane, acc);
+            for (int r = 0; r < 4; ++r) {
+                const float dh3 = P::tof(tB[(m * 16 + crow(lane, r)) * ldh + (ntile0 + n) * 16 + ccol(lane)]);
+                acc[m][n][r] = dh3 + acc[m][n][r] * mish_gradf(H1[m][n][r]);
+            }
+    store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.cdh1T), ldm32, ntile0, grow32, lane, acc);
+}
+
+// Kernel entry points. The *_o4 forms cap registers at 128 (4 waves per SIMD: two 8-wave row
+// tiles per CU) at the price of a few spills; which form runs is chosen per launch (row_tile_cfg).
+template <class P, int MT, int NT, int NO, int KSI, bool TRAIN, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void actor_rowtile_kernel(ActorArgs a) {
+    actor_rowtile_body<P, MT, NT, NO, KSI, TRAIN, WAVES>(a);
+}
+template <class P, int MT, int NT, int NO, int KSI, bool TRAIN, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4))) void actor_rowtile_kernel_o4(ActorArgs a) {
+    actor_rowtile_body<P, MT, NT, NO, KSI, TRAIN, WAVES>(a);
+}
+template <class P, int MT, int NT, bool TRAIN, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void critic_rowtile_kernel(CriticArgs a) {
+    critic_rowtile_body<P, MT, NT, TRAIN, WAVES>(a);
+}
+template <class P, int MT, int NT, bool TRAIN, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4))) void critic_rowtile_kernel_o4(CriticArgs a) {
+    critic_rowtile_body<P, MT, NT, TRAIN, WAVES>(a);
+}
+
+// Row-tile shape selection: DPPO_ROWTILE = "<actor>,<critic>" with actor in {64x16, 32x8, 32x8o4}
+// and critic in {32x8, 32x8o4}; read once (a tuning knob for measurements, defaults below).
+struct RowTileCfg { int actor; int critic; };   // actor: 0 = 64x16, 1 = 32x8, 2 = 32x8o4; critic: 0 = 32x8, 1 = 32x8o4
+static RowTileCfg row_tile_cfg() {
+    static RowTileCfg c = [] {
+        RowTileCfg r{0, 1};
+        if (const char* e = getenv("DPPO_ROWTILE")) {
+            if (!strncmp(e, "32x8o4", 6)) r.actor = 2;
+            else if (!strncmp(e, "32x8", 4)) r.actor = 1;
+            else if (!strncmp(e, "64x16", 5)) r.actor = 0;
+            const char* c2 = strchr(e, ',');
+            if (c2) r.critic = !strncmp(c2 + 1, "32x8o4", 6) ? 1 : 0;
+        }
+        return r;
+    }();
+    return c;
 }
 
 // =============================================================================================
 // launchers
 // =============================================================================================
-template <class P, int MT, int NT, int NO, int KSI, bool TRAIN, int WAVES>
+template <class P, int MT, int NT, int NO, int KSI, bool TRAIN, int WAVES, bool O4>
 static int launch_actor_t(const ActorArgs& a, hipStream_t s) {
     if (a.L.ks_in != KSI || a.L.ks_h != ksh_for<P>(NT, WAVES) || a.L.ks_out_t != 2 || a.L.ks_h != WAVES * nok_for<P>(NT))
         return dppo_set_error(DPPO_EUNSUPPORTED, "actor row tile: layout does not match the instantiation");
@@ -596,7 +654,7 @@ static int launch_actor_t(const ActorArgs& a, hipStream_t s) {
     const size_t tb_bytes = sizeof(typename P::AT) * 16 * MT * (a.H + pad);
     if (part_bytes > tb_bytes) return dppo_set_error(DPPO_EUNSUPPORTED, "actor: partial buffer does not fit");
     if (S.total > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "actor row tile needs %zu B LDS", S.total);
-    auto k = actor_rowtile_kernel<P, MT, NT, NO, KSI, TRAIN, WAVES>;
+    auto k = O4 ? actor_rowtile_kernel_o4<P, MT, NT, NO, KSI, TRAIN, WAVES> : actor_rowtile_kernel<P, MT, NT, NO, KSI, TRAIN, WAVES>;
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S.total));
     // TRAIN mode covers every row of the 64-padded feature-major images (padding rows get
     // finite activations and zero gradients), so the dW kernel never reads unwritten memory
@@ -608,20 +666,22 @@ static int launch_actor_t(const ActorArgs& a, hipStream_t s) {
     return DPPO_OK;
 }
 
-template <class P, int MT, int NT, int NO, int KSI, int WAVES>
+template <class P, int MT, int NT, int NO, int KSI, int WAVES, bool O4>
 static int launch_actor_m(const ActorArgs& a, hipStream_t s) {
-    return a.mode == ROWS_TRAIN ? launch_actor_t<P, MT, NT, NO, KSI, true, WAVES>(a, s)
-                                : launch_actor_t<P, MT, NT, NO, KSI, false, WAVES>(a, s);
+    return a.mode == ROWS_TRAIN ? launch_actor_t<P, MT, NT, NO, KSI, true, WAVES, O4>(a, s)
+                                : launch_actor_t<P, MT, NT, NO, KSI, false, WAVES, O4>(a, s);
 }
 
 // bf16: 64-row tiles, 16 waves (half the weight stream per row of 32-row tiles; LDS-limited);
 // fp32: 32-row tiles, 8 waves
-template <class P, int MT, int WAVES>
+template <class P, int MT, int WAVES, bool O4 = false>
 static int dispatch_actor(const ActorArgs& a, hipStream_t s) {
     const int NT = a.H / (16 * WAVES), NO = dppo_cdiv(a.XD, 16), KSI = a.L.ks_in;
 #define DPPO_ACTOR_CASE(nt, no, ksi) \
-    if (NT == nt && NO == no && KSI == ksi) return launch_actor_m<P, MT, nt, no, ksi, WAVES>(a, s);
-    if constexpr (P::KG == 32) {   // bf16: the in-layer is 2 k-steps up to 64 inputs, 4 up to 128
+    if (NT == nt && NO == no && KSI == ksi) return launch_actor_m<P, MT, nt, no, ksi, WAVES, O4>(a, s);
+    if constexpr (P::KG == 32 && WAVES == 16) {   // bf16, H = 512 on 16 waves
+        DPPO_ACTOR_CASE(2, 1, 2) DPPO_ACTOR_CASE(2, 2, 2) DPPO_ACTOR_CASE(2, 1, 4) DPPO_ACTOR_CASE(2, 2, 4)
+    } else if constexpr (P::KG == 32) {           // bf16, 8 waves: the in-layer is 2 k-steps up to 64 inputs, 4 up to 128
         DPPO_ACTOR_CASE(4, 1, 2) DPPO_ACTOR_CASE(4, 2, 2) DPPO_ACTOR_CASE(4, 1, 4) DPPO_ACTOR_CASE(4, 2, 4)
         DPPO_ACTOR_CASE(2, 1, 2) DPPO_ACTOR_CASE(2, 2, 2) DPPO_ACTOR_CASE(2, 1, 4) DPPO_ACTOR_CASE(2, 2, 4)
     } else {                       // fp32: 33..64 inputs -> 4 k-steps
@@ -633,10 +693,13 @@ static int dispatch_actor(const ActorArgs& a, hipStream_t s) {
 
 int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
     if (precision != DPPO_BF16) return dispatch_actor<PolicyF32, 2, 8>(a, s);
-    return dispatch_actor<PolicyBF16, 2, 8>(a, s);
+    const int v = row_tile_cfg().actor;
+    // bf16, H = 512: 64-row tiles on 16 waves halve the weight stream per row of 32-row tiles
+    if (a.H == 512 && v == 0) return dispatch_actor<PolicyBF16, 4, 16>(a, s);
+    return v == 2 ? dispatch_actor<PolicyBF16, 2, 8, true>(a, s) : dispatch_actor<PolicyBF16, 2, 8>(a, s);
 }
 
-template <class P, int MT, int NT, bool TRAIN, int WAVES>
+template <class P, int MT, int NT, bool TRAIN, int WAVES, bool O4>
 static int launch_critic_t(const CriticArgs& a, hipStream_t s) {
     if (a.L.ks_in != 2 || a.L.ks_h != ksh_for<P>(NT, WAVES) || a.L.ks_out_t != 2 || a.L.ks_h != WAVES * nok_for<P>(NT))
         return dppo_set_error(DPPO_EUNSUPPORTED, "critic row tile: layout does not match the instantiation");
@@ -644,7 +707,7 @@ static int launch_critic_t(const CriticArgs& a, hipStream_t s) {
     if (S.total > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "critic row tile needs %zu B LDS", S.total);
     if ((size_t)4 * WAVES * 16 * MT * 16 > sizeof(typename P::AT) * 16 * MT * (a.HC + lds_pad_elems<P>()))
         return dppo_set_error(DPPO_EUNSUPPORTED, "critic: partial buffer does not fit");
-    auto k = critic_rowtile_kernel<P, MT, NT, TRAIN, WAVES>;
+    auto k = O4 ? critic_rowtile_kernel_o4<P, MT, NT, TRAIN, WAVES> : critic_rowtile_kernel<P, MT, NT, TRAIN, WAVES>;
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S.total));
     // TRAIN mode covers every row of the 64-padded feature-major images (padding rows get
     // finite activations and zero gradients), so the dW kernel never reads unwritten memory
@@ -656,16 +719,18 @@ static int launch_critic_t(const CriticArgs& a, hipStream_t s) {
     return DPPO_OK;
 }
 
-template <class P, int MT, int WAVES>
+template <class P, int MT, int WAVES, bool O4>
 static int dispatch_critic(const CriticArgs& a, hipStream_t s) {
     const int NT = a.HC / (16 * WAVES);
     const bool tr = a.mode == ROWS_TRAIN;
-    if (NT == 2) return tr ? launch_critic_t<P, MT, 2, true, WAVES>(a, s) : launch_critic_t<P, MT, 2, false, WAVES>(a, s);
+    if (NT == 2) return tr ? launch_critic_t<P, MT, 2, true, WAVES, O4>(a, s) : launch_critic_t<P, MT, 2, false, WAVES, O4>(a, s);
     return dppo_set_error(DPPO_EUNSUPPORTED, "critic: hidden %d not instantiated", a.HC);
 }
 
 int launch_critic_rowtile(const CriticArgs& a, int precision, hipStream_t s) {
-    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8>(a, s) : dispatch_critic<PolicyF32, 2, 8>(a, s);
+    if (row_tile_cfg().critic == 1)
+        return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8, true>(a, s) : dispatch_critic<PolicyF32, 2, 8, true>(a, s);
+    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8, false>(a, s) : dispatch_critic<PolicyF32, 2, 8, false>(a, s);
 }
 
 // =============================================================================================

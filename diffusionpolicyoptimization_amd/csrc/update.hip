@@ -392,6 +392,7 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     DPPO_CHECK(D.KF <= 16, "dppo_ppo_minibatch: ft_denoising_steps > 16 unsupported (bucket sums)");
     hipStream_t s = (hipStream_t)stream;
     const PpoWorkspace ws = make_ppo_workspace(D, precision, rows, (uint8_t*)workspace);
+    DPPO_CHECK(ws.total < ((size_t)1 << 31), "dppo_ppo_minibatch: workspace for %d rows exceeds 2 GiB", rows);
     const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
     const FlatOffsets FC = make_flat_offsets(D.SD, D.HC, 1, 0);
     float* ga = grads;

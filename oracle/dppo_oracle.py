@@ -148,7 +148,7 @@ def residual_mlp_backward(p, cache, dy, act, prefix):
     g[prefix + "l1_w"] = cache["u1"].T @ dh2
     g[prefix + "l1_b"] = dh2.sum(0)
     du1 = dh2 @ R(p[prefix + "l1_w"]).T
-    dh1 = R(dh3 + du1 * ag(cache["h1"]))
+    dh1 = R(dh3r + du1 * ag(cache["h1"]))   # the kernels re-read dh3 from its (rounded) LDS tile
     g[prefix + "in_w"] = cache["x"].T @ dh1
     g[prefix + "in_b"] = dh1.sum(0)
     dx = dh1 @ np.asarray(p[prefix + "in_w"], np.float64).T
