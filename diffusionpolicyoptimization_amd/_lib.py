@@ -52,6 +52,10 @@ _SIGNATURES = {
     "dppo_pack_critic": (_I, [_DIMS, _I, _P, _P, _P]),
     "dppo_sample": (_I, [_DIMS, _I, _P, _P, _P, _P, _I, _P, _P, _U64, _U64, _I, _I, _F, _F, _F, _P, _P, _P]),
     "dppo_sample_step": (_I, [_DIMS, _I, _P, _P, _P, _P, _P, _I, _U64, _U64, _I, _I, _F, _F, _F, _P, _P, _P, _I, _P]),
+    "dppo_host_alloc": (_I, [_SZ, ctypes.POINTER(ctypes.c_void_p)]),
+    "dppo_host_free": (_I, [_P]),
+    "dppo_rollout_enqueue": (_I, [_DIMS, _I, _P, _P, _P, _P, _P, _I, _U64, _U64, _I, _I, _F, _F, _F, _P, _P, _P, _P,
+                                  ctypes.c_uint32, _P, _P]),
     "dppo_logprob": (_I, [_DIMS, _I, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P]),
     "dppo_critic_forward": (_I, [_DIMS, _I, _P, _P, _I, _P, _P]),
     "dppo_reward_scale_workspace_doubles": (_SZ, [_I, _I]),

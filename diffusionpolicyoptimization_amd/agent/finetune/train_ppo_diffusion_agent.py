@@ -77,8 +77,15 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         self.obs_traj = torch.empty(S, E, d.sd, dtype=torch.float32, device=dev)
         self.chains_traj = torch.empty(S, E, d.ft_denoising_steps + 1, d.xd, dtype=torch.float32, device=dev)
         self.act_dev = torch.empty(E, d.xd, dtype=torch.float32, device=dev)
-        self.obs_pin = torch.empty(E, self.n_cond_step, self.obs_dim, dtype=torch.float32).pin_memory()
-        self.act_pin = torch.empty(E, d.xd, dtype=torch.float32).pin_memory()
+        self.pipe = None
+        if self.cfg.train.get("pipelined_rollout", True):
+            # observation / action staging in coherent mapped memory, launches pre-enqueued
+            self.pipe = ops.RolloutPipe(self.model, self.obs_traj, self.act_dev, self.chains_traj)
+            self.obs_pin = self.pipe.obs.view(E, self.n_cond_step, self.obs_dim)
+            self.act_pin = self.pipe.act
+        else:
+            self.obs_pin = torch.empty(E, self.n_cond_step, self.obs_dim, dtype=torch.float32).pin_memory()
+            self.act_pin = torch.empty(E, d.xd, dtype=torch.float32).pin_memory()
         self.reward_pin = torch.empty(S, E, dtype=torch.float64).pin_memory()
         self.term_pin = torch.empty(S, E, dtype=torch.uint8).pin_memory()
         self.firsts = np.zeros((S + 1, E))
@@ -109,21 +116,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         act_view = self.act_pin.numpy().reshape(E, self.horizon_steps, self.action_dim)[:, :self.act_steps]
         stream = torch.cuda.current_stream(self.device)
         rew_np, term_np = self.reward_pin.numpy(), self.term_pin.numpy()
-        if self._stepper is None:
-            self._stepper = self.model.bind_rollout(self.obs_pin, self.obs_traj, self.act_dev, self.act_pin,
-                                                    self.chains_traj)
-        sample_step = self._stepper
-        for step in range(S):
-            if self.sampler_events is not None:
-                ev0 = torch.cuda.Event(enable_timing=True)
-                ev0.record(stream)
-            # H2D obs -> obs_traj[step], K-step sampler -> chains_traj[step], D2H actions, stream wait
-            sample_step(step, eval_mode)
-            if self.sampler_events is not None:
-                ev1 = torch.cuda.Event(enable_timing=True)
-                ev1.record(stream)
-                self.sampler_events.append((ev0, ev1))
-            _, reward, terminated, truncated, _ = self.venv.step(act_view, obs_out=obs_np)
+
+        def bookkeeping(step, reward, terminated, truncated):
             done = terminated | truncated
             rew_np[step] = reward
             term_np[step] = terminated
@@ -131,6 +125,39 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             self.done_venv = done
             if not eval_mode:
                 self.cnt_train_step += self.n_envs_global * self.act_steps
+
+        if self.pipe is not None:
+            # step t+1's launch is enqueued before the envs of step t are stepped; it waits on
+            # the device for the observation the host publishes after the env step
+            pipe = self.pipe
+            pipe.enqueue(0, eval_mode)
+            pipe.publish()
+            for step in range(S):
+                if step + 1 < S:
+                    pipe.enqueue(step + 1, eval_mode)
+                pipe.wait()
+                _, reward, terminated, truncated, _ = self.venv.step(act_view, obs_out=obs_np)
+                if step + 1 < S:
+                    pipe.publish()
+                bookkeeping(step, reward, terminated, truncated)
+            stream.synchronize()
+        else:
+            if self._stepper is None:
+                self._stepper = self.model.bind_rollout(self.obs_pin, self.obs_traj, self.act_dev, self.act_pin,
+                                                        self.chains_traj)
+            sample_step = self._stepper
+            for step in range(S):
+                if self.sampler_events is not None:
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev0.record(stream)
+                # H2D obs -> obs_traj[step], K-step sampler -> chains_traj[step], D2H actions, stream wait
+                sample_step(step, eval_mode)
+                if self.sampler_events is not None:
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev1.record(stream)
+                    self.sampler_events.append((ev0, ev1))
+                _, reward, terminated, truncated, _ = self.venv.step(act_view, obs_out=obs_np)
+                bookkeeping(step, reward, terminated, truncated)
         self.prev_obs_venv = {"state": obs_np}
         return self.episode_stats()
 

@@ -7,6 +7,7 @@
 // (diffusion_vpg.py:198-243, 301-320). Activations never leave LDS; weights stream from L2.
 // The actor used at step t is actor_ft when t < K' else the frozen base actor (diffusion_vpg.py:161-180);
 // the reference's always-computed base forward (:161) does not change the result and is skipped.
+#include <string.h>
 #include "dppo_common.cuh"
 #include "dppo_internal.h"
 
@@ -19,6 +20,14 @@ struct SampleArgs {
     const float* noise;   // [K][E][XD] or null
     float* actions;       // [E][XD]
     float* chains;        // [E][KF+1][XD] or null
+    float* cond_out;      // [E][SD] device copy of cond or null (cond may be mapped host memory)
+    float* actions_host;  // [E][XD] mapped pinned host memory or null (zero-copy action hand-off)
+    // pre-enqueued rollout steps (dppo_rollout_*): wait until *go >= go_value before reading cond,
+    // and add 1 to *done per workgroup after the actions are visible to the host (both counters
+    // live in fine-grained host memory); null = an ordinary launch
+    const uint32_t* go;
+    uint32_t go_value;
+    uint32_t* done;
     uint64_t seed;
     uint32_t call_id;
     int E, env_offset, deterministic;
@@ -75,10 +84,6 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
         else v = ((const float*)(PK + L.off[SEG_B_OUT]))[j - 3 * H];
         bias[i] = v;
     }
-    for (int i = tid; i < 16 * SD; i += ST) {
-        const int r = i / SD, c = i % SD, row = row0 + r;
-        st[i] = row < a.E ? a.cond[(size_t)row * SD + c] : 0.f;
-    }
     // all K steps' noise up front (injected, or the Philox stream), clipped to +-randn_clip (:319),
     // so the denoising loop carries no RNG state and issues no global loads outside the weight stream
     for (int i = tid; i < K * 16 * XD; i += ST) {
@@ -117,6 +122,28 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
         float acc = w2[2 * TD * TD + j];
         for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + j];
         temb[i] = acc;
+    }
+    // a pre-enqueued step waits here (everything above does not depend on the observation) for
+    // the host to publish it; bounded: ~4 s, then the step runs on whatever is in the buffer and
+    // flags the timeout in the high bit of *done so the host reports it
+    if (a.go) {
+        if (tid == 0) {
+            uint32_t spins = 0;
+            while (__hip_atomic_load(a.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
+                __builtin_amdgcn_s_sleep(64);
+                if (++spins == (1u << 22)) {
+                    __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < 16 * SD; i += ST) {
+        const int r = i / SD, c = i % SD, row = row0 + r;
+        const float v = row < a.E ? a.cond[(size_t)row * SD + c] : 0.f;
+        st[i] = v;
+        if (a.cond_out && row < a.E) a.cond_out[(size_t)row * SD + c] = v;
     }
     __syncthreads();
 
@@ -213,10 +240,18 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
             xs[tid] = xn;
             if (row < a.E) {
                 if (a.chains && t <= KF) a.chains[((size_t)row * (KF + 1) + (KF - t)) * XD + q] = xn;
-                if (i == K - 1) a.actions[(size_t)row * XD + q] = xn;
+                if (i == K - 1) {
+                    a.actions[(size_t)row * XD + q] = xn;
+                    if (a.actions_host) a.actions_host[(size_t)row * XD + q] = xn;
+                }
             }
         }
         lds_sync();
+    }
+    if (a.done) {   // publish: every writer's stores reach the system before the counter moves
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -276,11 +311,12 @@ static int dispatch_sample(const SampleArgs& a, hipStream_t s) {
                           a.H, a.XD, KSI);
 }
 
-extern "C" int dppo_sample(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
-                           const float* sched, const float* cond, int n_envs, const float* x_T, const float* noise,
-                           uint64_t seed, uint64_t call_id, int env_offset, int deterministic,
-                           float min_sampling_std, float randn_clip, float final_clip,
-                           float* actions, float* chains, void* stream) {
+static int sample_impl(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
+                       const float* sched, const float* cond, int n_envs, const float* x_T, const float* noise,
+                       uint64_t seed, uint64_t call_id, int env_offset, int deterministic,
+                       float min_sampling_std, float randn_clip, float final_clip,
+                       float* actions, float* chains, float* cond_out, float* actions_host, void* stream,
+                       const uint32_t* go = nullptr, uint32_t go_value = 0, uint32_t* done = nullptr) {
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
@@ -292,6 +328,8 @@ extern "C" int dppo_sample(const dppo_dims* d, int precision, const void* packed
     a.packed_base = (const uint8_t*)packed_base;
     a.packed_ft = (const uint8_t*)packed_ft;
     a.sched = sched; a.cond = cond; a.x_T = x_T; a.noise = noise; a.actions = actions; a.chains = chains;
+    a.cond_out = cond_out; a.actions_host = actions_host;
+    a.go = go; a.go_value = go_value; a.done = done;
     a.seed = seed; a.call_id = (uint32_t)call_id; a.E = n_envs; a.env_offset = env_offset;
     a.deterministic = deterministic; a.min_std = min_sampling_std; a.randn_clip = randn_clip; a.final_clip = final_clip;
     a.XD = D.XD; a.SD = D.SD; a.TD = D.TD; a.H = D.H; a.K = D.K; a.KF = D.KF; a.IN = D.IN;
@@ -300,9 +338,40 @@ extern "C" int dppo_sample(const dppo_dims* d, int precision, const void* packed
     return precision == DPPO_BF16 ? dispatch_sample<PolicyBF16>(a, s) : dispatch_sample<PolicyF32>(a, s);
 }
 
-// One rollout step's device work in one call (train_ppo_diffusion_agent.py:106-122): H2D of the
-// pinned observation into its rollout slot, the K-step sampler, D2H of the actions into pinned
-// memory and (optionally) the stream wait, so the host's per-step overhead is one FFI call.
+extern "C" int dppo_sample(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
+                           const float* sched, const float* cond, int n_envs, const float* x_T, const float* noise,
+                           uint64_t seed, uint64_t call_id, int env_offset, int deterministic,
+                           float min_sampling_std, float randn_clip, float final_clip,
+                           float* actions, float* chains, void* stream) {
+    return sample_impl(d, precision, packed_base, packed_ft, sched, cond, n_envs, x_T, noise, seed, call_id, env_offset,
+                       deterministic, min_sampling_std, randn_clip, final_clip, actions, chains, nullptr, nullptr,
+                       stream);
+}
+
+// device address of pinned host memory (a small cache: the rollout reuses the same staging
+// buffers and counters every step); null if the memory is not mapped
+static void* mapped_ptr(const void* host) {
+    constexpr int N = 8;
+    thread_local const void* keys[N] = {};
+    thread_local void* vals[N] = {};
+    thread_local int next = 0;
+    for (int i = 0; i < N; ++i)
+        if (keys[i] == host && vals[i]) return vals[i];
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, const_cast<void*>(host), 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    keys[next] = host; vals[next] = dev;
+    next = (next + 1) % N;
+    return dev;
+}
+
+// One rollout step's device work in one call (train_ppo_diffusion_agent.py:106-122): the sampler
+// reads the observation straight from the mapped pinned buffer (and copies it into its rollout
+// slot), writes the actions straight into the mapped pinned action buffer, and the host waits
+// for the stream — no copy kernels in the step. Unmapped staging memory falls back to two
+// hipMemcpyAsync around the launch.
 extern "C" int dppo_sample_step(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
                                 const float* sched, const float* cond_host, float* cond, int n_envs, uint64_t seed,
                                 uint64_t call_id, int env_offset, int deterministic, float min_sampling_std,
@@ -314,11 +383,50 @@ extern "C" int dppo_sample_step(const dppo_dims* d, int precision, const void* p
     if (n_envs == 0) return DPPO_OK;
     DPPO_CHECK(cond_host && cond && actions && actions_host, "dppo_sample_step: null pointer argument");
     hipStream_t s = (hipStream_t)stream;
-    DPPO_HIP(hipMemcpyAsync(cond, cond_host, sizeof(float) * (size_t)n_envs * D.SD, hipMemcpyHostToDevice, s));
-    rc = dppo_sample(d, precision, packed_base, packed_ft, sched, cond, n_envs, nullptr, nullptr, seed, call_id,
-                     env_offset, deterministic, min_sampling_std, randn_clip, final_clip, actions, chains, stream);
-    if (rc) return rc;
-    DPPO_HIP(hipMemcpyAsync(actions_host, actions, sizeof(float) * (size_t)n_envs * D.XD, hipMemcpyDeviceToHost, s));
+    const float* cond_dev_view = (const float*)mapped_ptr(cond_host);
+    float* act_dev_view = (float*)mapped_ptr(actions_host);
+    if (cond_dev_view && act_dev_view) {
+        rc = sample_impl(d, precision, packed_base, packed_ft, sched, cond_dev_view, n_envs, nullptr, nullptr, seed,
+                         call_id, env_offset, deterministic, min_sampling_std, randn_clip, final_clip, actions, chains,
+                         cond, act_dev_view, stream);
+        if (rc) return rc;
+    } else {
+        DPPO_HIP(hipMemcpyAsync(cond, cond_host, sizeof(float) * (size_t)n_envs * D.SD, hipMemcpyHostToDevice, s));
+        rc = dppo_sample(d, precision, packed_base, packed_ft, sched, cond, n_envs, nullptr, nullptr, seed, call_id,
+                         env_offset, deterministic, min_sampling_std, randn_clip, final_clip, actions, chains, stream);
+        if (rc) return rc;
+        DPPO_HIP(hipMemcpyAsync(actions_host, actions, sizeof(float) * (size_t)n_envs * D.XD, hipMemcpyDeviceToHost, s));
+    }
     if (synchronize) DPPO_HIP(hipStreamSynchronize(s));
     return DPPO_OK;
+}
+
+// ---- pipelined rollout steps (see include/dppo.h) ----
+extern "C" int dppo_host_alloc(size_t bytes, void** ptr) {
+    DPPO_CHECK(ptr && bytes > 0, "dppo_host_alloc: bad arguments");
+    DPPO_HIP(hipHostMalloc(ptr, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(*ptr, 0, bytes);
+    return DPPO_OK;
+}
+
+extern "C" int dppo_host_free(void* ptr) {
+    if (ptr) DPPO_HIP(hipHostFree(ptr));
+    return DPPO_OK;
+}
+
+extern "C" int dppo_rollout_enqueue(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
+                                    const float* sched, const float* cond_host, float* cond, int n_envs, uint64_t seed,
+                                    uint64_t call_id, int env_offset, int deterministic, float min_sampling_std,
+                                    float randn_clip, float final_clip, float* actions, float* actions_host,
+                                    float* chains, const uint32_t* go, uint32_t go_value, uint32_t* done, void* stream) {
+    DPPO_CHECK(cond_host && cond && actions && actions_host && go && done, "dppo_rollout_enqueue: null pointer argument");
+    const float* cond_dev = (const float*)mapped_ptr(cond_host);
+    float* act_dev = (float*)mapped_ptr(actions_host);
+    const uint32_t* go_dev = (const uint32_t*)mapped_ptr(go);
+    uint32_t* done_dev = (uint32_t*)mapped_ptr(done);
+    DPPO_CHECK(cond_dev && act_dev && go_dev && done_dev,
+               "dppo_rollout_enqueue: staging buffers must come from dppo_host_alloc (mapped, coherent)");
+    return sample_impl(d, precision, packed_base, packed_ft, sched, cond_dev, n_envs, nullptr, nullptr, seed, call_id,
+                       env_offset, deterministic, min_sampling_std, randn_clip, final_clip, actions, chains, cond,
+                       act_dev, stream, go_dev, go_value, done_dev);
 }

@@ -189,6 +189,104 @@ class SampleStepper:
         m._call_id += 1
 
 
+class RolloutPipe:
+    """Pipelined rollout steps (dppo_rollout_enqueue). The observation and action staging buffers
+    and two step counters live in coherent mapped pinned memory (dppo_host_alloc); the launch of
+    step t+1 is enqueued BEFORE the host steps the envs of step t and waits on the `go` counter, so
+    the launch latency overlaps host work and the host learns that step t is done by polling the
+    `done` counter instead of a stream synchronisation.
+        pipe.enqueue(i, det)   step i's launch (waits until its observation is published)
+        pipe.publish()         the observation buffer holds the next step's input
+        pipe.wait()            block until the oldest unfinished step has written its actions
+    obs / act are torch views over the staging memory ([E, SD] / [E, XD] float32)."""
+
+    def __init__(self, model, obs_traj, actions, chains_traj):
+        d = model.dims
+        S, E = obs_traj.shape[0], obs_traj.shape[1]
+        _check(obs_traj, (S, E, d.sd), torch.float32, "obs_traj")
+        _check(chains_traj, (S, E, d.ft_denoising_steps + 1, d.xd), torch.float32, "chains_traj")
+        _check(actions, (E, d.xd), torch.float32, "actions")
+        lib = _lib.load()
+        self._lib, self.model, self.S, self.E = lib, model, S, E
+        self._bufs = []
+
+        def alloc(nbytes):
+            p = ctypes.c_void_p()
+            _lib.call("dppo_host_alloc", ctypes.c_size_t(nbytes), ctypes.byref(p))
+            self._bufs.append(p.value)
+            return p.value
+        po, pa, pc = alloc(4 * E * d.sd), alloc(4 * E * d.xd), alloc(256)
+        self.obs = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_float * (E * d.sd)).from_address(po))).view(E, d.sd)
+        self.act = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_float * (E * d.xd)).from_address(pa))).view(E, d.xd)
+        ctr = np.ctypeslib.as_array((ctypes.c_uint32 * 64).from_address(pc))
+        self._go, self._done = ctr[0:1], ctr[16:17]          # separate 64-B lines
+        self._p = dict(obs=ctypes.c_void_p(po), act=ctypes.c_void_p(pa), go=ctypes.c_void_p(pc),
+                       done=ctypes.c_void_p(pc + 64))
+        self._fn = lib.dppo_rollout_enqueue
+        self._dims = d.c()
+        self._keep = (obs_traj, actions, chains_traj)
+        self._obs0, self._obs_step = obs_traj.data_ptr(), E * d.sd * 4
+        self._ch0, self._ch_step = chains_traj.data_ptr(), E * (d.ft_denoising_steps + 1) * d.xd * 4
+        self._actions = ptr(actions)
+        self._stream = stream_handle(obs_traj.device)
+        self.nwg = (E + 15) // 16
+        self.enqueued = 0      # steps launched so far (step s waits for go >= s + 1)
+        self.published = 0
+        self.finished = 0
+
+    def enqueue(self, i, deterministic=False):
+        if not 0 <= i < self.S:
+            raise IndexError(f"rollout step {i} outside [0, {self.S})")
+        m = self.model
+        fc = m.final_action_clip_value
+        p = self._p
+        self.enqueued += 1
+        rc = self._fn(ctypes.byref(self._dims), _prec(m.precision), ptr(m.packed_base), ptr(m.packed_ft), ptr(m.sched),
+                      p["obs"], ctypes.c_void_p(self._obs0 + i * self._obs_step), self.E,
+                      ctypes.c_uint64(m.seed & (2 ** 64 - 1)), ctypes.c_uint64(m._call_id), m._env_offset,
+                      int(bool(deterministic)), float(m.get_min_sampling_denoising_std()), float(m.randn_clip_value),
+                      float(fc) if fc is not None else 0.0, self._actions, p["act"],
+                      ctypes.c_void_p(self._ch0 + i * self._ch_step), p["go"], ctypes.c_uint32(self.enqueued),
+                      p["done"], self._stream)
+        if rc:
+            raise _lib.DppoError(f"dppo_rollout_enqueue failed ({rc}): {self._lib.dppo_last_error().decode()}")
+        m._call_id += 1
+
+    def publish(self):
+        self.published += 1
+        self._go[0] = self.published          # x86 stores are ordered: the observation is visible first
+
+    def wait(self, timeout_s=30.0):
+        import time
+        self.finished += 1
+        target = self.finished * self.nwg
+        done = self._done
+        t0 = None
+        while True:
+            v = int(done[0])
+            if v & 0x80000000:
+                raise _lib.DppoError("rollout step timed out waiting for its observation (go counter)")
+            if v >= target:
+                return
+            if t0 is None:
+                t0 = time.perf_counter()
+            elif time.perf_counter() - t0 > timeout_s:
+                raise _lib.DppoError(f"rollout step {self.finished - 1} did not finish within {timeout_s} s")
+
+    def close(self):
+        torch.cuda.current_stream(self._keep[0].device).synchronize()
+        for b in self._bufs:
+            self._lib.dppo_host_free(ctypes.c_void_p(b))
+        self._bufs = []
+
+    def __del__(self):
+        try:
+            if self._bufs:
+                self.close()
+        except Exception:
+            pass
+
+
 def logprob(d: ModelDims, precision, packed_ft, sched, cond, chains, min_logprob_std=0.1, reward_horizon=None,
             want_elem=True, want_mean=True, lp_elem=None, lp_mean=None):
     n = cond.shape[0]

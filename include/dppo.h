@@ -98,6 +98,21 @@ DPPO_API int dppo_sample_step(const dppo_dims* d, int precision, const void* pac
                 float randn_clip, float final_clip, float* actions, float* actions_host,
                 float* chains, int synchronize, void* stream);
 
+/* Pipelined rollout (the same step, with the launch taken off the host's critical path):
+ * the host enqueues step t+1 BEFORE stepping the envs of step t; that launch does everything
+ * that does not depend on the observation (noise, time embedding, weights in flight), then waits
+ * until *go >= go_value, reads the observation from cond_host, and after writing the actions to
+ * actions_host adds 1 per workgroup (ceil(n_envs/16)) to *done. cond_host, actions_host, go and
+ * done must come from dppo_host_alloc (mapped, coherent pinned memory). The wait is bounded
+ * (~4 s): on timeout the step proceeds and sets bit 31 of *done. */
+DPPO_API int dppo_host_alloc(size_t bytes, void** ptr);
+DPPO_API int dppo_host_free(void* ptr);
+DPPO_API int dppo_rollout_enqueue(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
+                const float* sched, const float* cond_host, float* cond, int n_envs, uint64_t seed,
+                uint64_t call_id, int env_offset, int deterministic, float min_sampling_std,
+                float randn_clip, float final_clip, float* actions, float* actions_host,
+                float* chains, const uint32_t* go, uint32_t go_value, uint32_t* done, void* stream);
+
 /* ---- a10: VPGDiffusion.get_logprobs (diffusion_vpg.py:343-425) + the clip/mean of c_loss
  * (diffusion_ppo.py:50-59) for the old-logprob pass (agent/finetune/train_ppo_diffusion_agent.py:214-229).
  *   cond [n, To*Do], chains [n, K'+1, Ta*Da]

@@ -59,3 +59,44 @@ def test_bound_rollout_step_matches_model_call(cuda):
         np.testing.assert_array_equal(chains[i].cpu().numpy(), ref.chains.reshape(E, -1, d.xd).cpu().numpy())
     with pytest.raises(IndexError):
         step(S)
+
+
+def test_pipelined_rollout_matches_model_call(cuda):
+    """dppo_rollout_enqueue (pre-enqueued launches gated by the go/done counters) == model(...)."""
+    import torch
+
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
+                      ["model.precision=bf16"])
+    model = instantiate(cfg.model, device=cuda, seed=5)
+    d = model.dims
+    S, E = 4, 40
+    obs_traj = torch.zeros(S, E, d.sd, device=cuda)
+    chains = torch.zeros(S, E, d.ft_denoising_steps + 1, d.xd, device=cuda)
+    act = torch.empty(E, d.xd, device=cuda)
+    pipe = ops.RolloutPipe(model, obs_traj, act, chains)
+    rng = np.random.default_rng(2)
+    obs = [rng.uniform(-1, 1, (E, d.sd)).astype(np.float32) for _ in range(S)]
+    cid0 = model._call_id
+    pipe.obs.numpy()[:] = obs[0]
+    pipe.enqueue(0)
+    pipe.publish()
+    got = []
+    for i in range(S):
+        if i + 1 < S:
+            pipe.enqueue(i + 1)
+        pipe.wait()
+        got.append(pipe.act.numpy().copy())
+        if i + 1 < S:
+            pipe.obs.numpy()[:] = obs[i + 1]
+            pipe.publish()
+    torch.cuda.synchronize()
+    model._call_id = cid0
+    for i in range(S):
+        ref = model(torch.tensor(obs[i], device=cuda), return_chain=True)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(obs_traj[i].cpu().numpy(), obs[i])
+        np.testing.assert_array_equal(got[i], ref.trajectories.reshape(E, -1).cpu().numpy())
+        np.testing.assert_array_equal(chains[i].cpu().numpy(), ref.chains.reshape(E, -1, d.xd).cpu().numpy())
+    pipe.close()
