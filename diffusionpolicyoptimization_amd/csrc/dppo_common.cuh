@@ -157,6 +157,72 @@ __device__ inline void gemm_stream(const typename P::AT* A, int lda, WSrc W, int
     }
 }
 
+// Deeper weight stream for the latency-bound sampler: a D-deep queue of k-steps per wave (D*NT
+// fragments in flight). In fully unrolled code the shifts are register renames; across the
+// runtime denoising loop the queue is loop-carried with the next k-step always in slot 0. The
+// look-ahead may run D k-steps past the end of a layer, through up to two following layers.
+template <int D, int NT>
+struct WQueue {
+    u32x4 b[D][NT];
+};
+
+struct NextLayers {
+    WSrc W1; int KS1;   // the layer after the current one
+    WSrc W2; int KS2;   // and the one after that (for look-ahead past a short layer)
+};
+
+// fragment j of the stream that is at layer W (KS k-steps) and continues into nx.W1, nx.W2
+template <int KS>
+__device__ inline u32x4 stream_frag(WSrc W, const NextLayers& nx, int ntile, int j, int lane) {
+    if (j < KS) return load_bfrag_c(W, KS, ntile, j, lane);                  // compile-time branch
+    const int j1 = j - KS;
+    const bool first = j1 < nx.KS1;                                           // wave-uniform
+    const WSrc src = first ? nx.W1 : nx.W2;
+    return load_bfrag_c(src, first ? nx.KS1 : nx.KS2, ntile, first ? j1 : j1 - nx.KS1, lane);
+}
+
+template <int D, int NT>
+__device__ inline void queue_prime(WQueue<D, NT>& Q, WSrc W, int KS, const NextLayers& nx, int ntile0, int lane) {
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const bool in = d < KS;
+            const int j1 = d - KS;
+            const bool first = j1 < nx.KS1;
+            Q.b[d][n] = in ? load_bfrag_c(W, KS, ntile0 + n, d, lane)
+                           : load_bfrag_c(first ? nx.W1 : nx.W2, first ? nx.KS1 : nx.KS2, ntile0 + n,
+                                          first ? j1 : j1 - nx.KS1, lane);
+        }
+}
+
+template <class P, int MT, int NT, int KS, int D>
+__device__ inline void gemm_queue(const typename P::AT* A, int lda, WSrc W, int ntile0, f32x4 (&acc)[MT][NT], int lane,
+                                  WQueue<D, NT>& Q, const NextLayers& nx) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) zero_acc(acc[m][n]);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        u32x4 c[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) c[n] = Q.b[0][n];
+#pragma unroll
+        for (int d = 0; d + 1 < D; ++d)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) Q.b[d][n] = Q.b[d + 1][n];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) Q.b[D - 1][n] = stream_frag<KS>(W, nx, ntile0 + n, ks + D, lane);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            const u32x4 a = lds_afrag<P>(A, lda, m, ks, lane);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[m][n] = P::mma(a, c[n], acc[m][n]);
+        }
+    }
+}
+
 // hidden-layer k-steps for a precision and n-tiles-per-wave (H = 16*NT*WAVES)
 template <class P> __host__ __device__ constexpr int ksh_for(int NT, int WAVES = DPPO_WAVES) { return NT * 16 * WAVES / P::KG; }
 

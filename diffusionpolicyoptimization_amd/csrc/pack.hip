@@ -3,17 +3,42 @@
 #include "dppo_common.cuh"
 #include "dppo_internal.h"
 
-// one thread per (ntile, ks, lane) fragment slot; writes 16 B
+// All segments of one MLP image in ONE launch (the images are re-derived after every optimiser
+// step, so 12 small launches per model were ~100 us per PPO minibatch). A job is either a packed
+// matrix (one thread per (ntile, ks, lane) fragment slot, 16 B each) or a zero-padded fp32 copy.
+#define PACK_MAXJ 16
+struct PackJob {
+    int kind;            // 0 = packed matrix, 1 = fp32 copy with zero padding
+    int K, N, transposed;
+    int n, npad;         // copy: valid / padded element counts
+    size_t src, dst;     // float offset in params / byte offset in the image
+    int threads;         // work items of this job
+};
+struct PackArgs {
+    PackJob j[PACK_MAXJ];
+    int start[PACK_MAXJ + 1];
+    int njobs;
+    const float* params;
+    uint8_t* out;
+};
+
 template <int KG, int EPL>
-__global__ void pack_matrix_kernel(const float* __restrict__ W, int K, int N, int transposed, uint8_t* __restrict__ out) {
-    const int KS = packed_ksteps(K, KG);
-    const int NTL = (N + 15) / 16;
-    const int total = NTL * KS * 64;
+__global__ void pack_all_kernel(PackArgs a) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= total) return;
-    const int lane = gid & 63;
-    const int ks = (gid >> 6) % KS;
-    const int nt = (gid >> 6) / KS;
+    if (gid >= a.start[a.njobs]) return;
+    int ji = 0;
+    while (ji + 1 < a.njobs && gid >= a.start[ji + 1]) ++ji;
+    const PackJob& J = a.j[ji];
+    const int t = gid - a.start[ji];
+    const float* W = a.params + J.src;
+    if (J.kind == 1) {
+        reinterpret_cast<float*>(a.out + J.dst)[t] = t < J.n ? W[t] : 0.f;
+        return;
+    }
+    const int KS = packed_ksteps(J.K, KG);
+    const int lane = t & 63;
+    const int ks = (t >> 6) % KS;
+    const int nt = (t >> 6) / KS;
     const int n = nt * 16 + (lane & 15);
     u32x4 v;
     if constexpr (EPL == 8) {
@@ -22,7 +47,7 @@ __global__ void pack_matrix_kernel(const float* __restrict__ W, int K, int N, in
         for (int q = 0; q < 8; ++q) {
             const int k = ks * KG + (lane >> 4) * EPL + q;
             float x = 0.f;
-            if (k < K && n < N) x = transposed ? W[(size_t)n * K + k] : W[(size_t)k * N + n];
+            if (k < J.K && n < J.N) x = J.transposed ? W[(size_t)n * J.K + k] : W[(size_t)k * J.N + n];
             e[q] = (__bf16)x;
         }
         v = __builtin_bit_cast(u32x4, e);
@@ -32,60 +57,50 @@ __global__ void pack_matrix_kernel(const float* __restrict__ W, int K, int N, in
         for (int q = 0; q < 4; ++q) {
             const int k = ks * KG + (lane >> 4) * EPL + q;
             float x = 0.f;
-            if (k < K && n < N) x = transposed ? W[(size_t)n * K + k] : W[(size_t)k * N + n];
+            if (k < J.K && n < J.N) x = J.transposed ? W[(size_t)n * J.K + k] : W[(size_t)k * J.N + n];
             e[q] = x;
         }
         v = __builtin_bit_cast(u32x4, e);
     }
-    reinterpret_cast<u32x4*>(out)[gid] = v;
-}
-
-__global__ void copy_pad_kernel(const float* __restrict__ src, int n, int npad, float* __restrict__ dst) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < npad) dst[i] = i < n ? src[i] : 0.f;
-}
-
-static hipError_t pack_matrix(const float* W, int K, int N, bool transposed, int precision, uint8_t* out,
-                              hipStream_t s) {
-    const int KG = precision == DPPO_BF16 ? 32 : 16;
-    const int total = dppo_cdiv(N, 16) * packed_ksteps(K, KG) * 64;
-    const int blocks = dppo_cdiv(total, 256);
-    if (precision == DPPO_BF16)
-        hipLaunchKernelGGL((pack_matrix_kernel<32, 8>), dim3(blocks), dim3(256), 0, s, W, K, N, transposed ? 1 : 0, out);
-    else
-        hipLaunchKernelGGL((pack_matrix_kernel<16, 4>), dim3(blocks), dim3(256), 0, s, W, K, N, transposed ? 1 : 0, out);
-    return hipGetLastError();
-}
-
-static hipError_t copy_pad(const float* src, int n, int npad, void* dst, hipStream_t s) {
-    if (npad <= 0) return hipSuccess;
-    hipLaunchKernelGGL(copy_pad_kernel, dim3(dppo_cdiv(npad, 256)), dim3(256), 0, s, src, n, npad, (float*)dst);
-    return hipGetLastError();
+    reinterpret_cast<u32x4*>(a.out + J.dst)[t] = v;
 }
 
 int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* params,
                   void* packed, hipStream_t s) {
     const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision);
     const FlatOffsets F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
-    uint8_t* P = (uint8_t*)packed;
-    hipError_t e = hipSuccess;
-#define DPPO_TRY(x) do { e = (x); if (e != hipSuccess) return dppo_hip_fail(e, #x); } while (0)
-    if (time_dim > 0) {
-        const int tsz = (int)(F.in_w - F.time_w1);
-        DPPO_TRY(copy_pad(params + F.time_w1, tsz, tsz, P + L.off[SEG_TIME], s));
-    }
-    DPPO_TRY(pack_matrix(params + F.in_w, in_dim, hidden, false, precision, P + L.off[SEG_W_IN], s));
-    DPPO_TRY(copy_pad(params + F.in_b, hidden, hidden, P + L.off[SEG_B_IN], s));
-    DPPO_TRY(pack_matrix(params + F.l1_w, hidden, hidden, false, precision, P + L.off[SEG_W_L1], s));
-    DPPO_TRY(copy_pad(params + F.l1_b, hidden, hidden, P + L.off[SEG_B_L1], s));
-    DPPO_TRY(pack_matrix(params + F.l2_w, hidden, hidden, false, precision, P + L.off[SEG_W_L2], s));
-    DPPO_TRY(copy_pad(params + F.l2_b, hidden, hidden, P + L.off[SEG_B_L2], s));
-    DPPO_TRY(pack_matrix(params + F.out_w, hidden, out_dim, false, precision, P + L.off[SEG_W_OUT], s));
-    DPPO_TRY(copy_pad(params + F.out_b, out_dim, 16 * L.nt_out, P + L.off[SEG_B_OUT], s));
+    const int KG = precision == DPPO_BF16 ? 32 : 16;
+    PackArgs a = {};
+    auto mat = [&](size_t src, int K, int N, bool tr, int seg) {
+        PackJob& J = a.j[a.njobs++];
+        J.kind = 0; J.K = K; J.N = N; J.transposed = tr ? 1 : 0; J.src = src; J.dst = L.off[seg];
+        J.threads = dppo_cdiv(N, 16) * packed_ksteps(K, KG) * 64;
+    };
+    auto cpy = [&](size_t src, int n, int npad, int seg) {
+        PackJob& J = a.j[a.njobs++];
+        J.kind = 1; J.n = n; J.npad = npad; J.src = src; J.dst = L.off[seg]; J.threads = npad;
+    };
+    if (time_dim > 0) cpy(F.time_w1, (int)(F.in_w - F.time_w1), (int)(F.in_w - F.time_w1), SEG_TIME);
+    mat(F.in_w, in_dim, hidden, false, SEG_W_IN);
+    cpy(F.in_b, hidden, hidden, SEG_B_IN);
+    mat(F.l1_w, hidden, hidden, false, SEG_W_L1);
+    cpy(F.l1_b, hidden, hidden, SEG_B_L1);
+    mat(F.l2_w, hidden, hidden, false, SEG_W_L2);
+    cpy(F.l2_b, hidden, hidden, SEG_B_L2);
+    mat(F.out_w, hidden, out_dim, false, SEG_W_OUT);
+    cpy(F.out_b, out_dim, 16 * L.nt_out, SEG_B_OUT);
     // transposed images: W^T viewed as a [K'=out][N'=in] weight, i.e. element (k', n') = W[n'][k']
-    DPPO_TRY(pack_matrix(params + F.out_w, out_dim, hidden, true, precision, P + L.off[SEG_T_OUT], s));
-    DPPO_TRY(pack_matrix(params + F.l2_w, hidden, hidden, true, precision, P + L.off[SEG_T_L2], s));
-    DPPO_TRY(pack_matrix(params + F.l1_w, hidden, hidden, true, precision, P + L.off[SEG_T_L1], s));
-#undef DPPO_TRY
+    mat(F.out_w, out_dim, hidden, true, SEG_T_OUT);
+    mat(F.l2_w, hidden, hidden, true, SEG_T_L2);
+    mat(F.l1_w, hidden, hidden, true, SEG_T_L1);
+    for (int i = 0; i < a.njobs; ++i) a.start[i + 1] = a.start[i] + a.j[i].threads;
+    a.params = params;
+    a.out = (uint8_t*)packed;
+    const int blocks = dppo_cdiv(a.start[a.njobs], 256);
+    if (precision == DPPO_BF16)
+        hipLaunchKernelGGL((pack_all_kernel<32, 8>), dim3(blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((pack_all_kernel<16, 4>), dim3(blocks), dim3(256), 0, s, a);
+    DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }

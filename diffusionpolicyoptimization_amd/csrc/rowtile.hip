@@ -289,40 +289,50 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     lds_sync();
 
     // ---- epilogue: p_mean_var + Normal.log_prob (+ c_loss policy term and its gradient) ----
-    if (wave == 0 && lane < ROWS) {
-        const int r = lane, n = rn[r], j = rj[r], t = KF - 1 - j;
-        const bool valid = n >= 0;
-        const float* bo = bias + 3 * H;
-        const float* sc = sch + t * DPPO_SCHED_COLS;
-        const float sd = fminf(fmaxf(expf(0.5f * sc[4]), a.hp.min_lp_std), 1e6f);   // diffusion_vpg.py:473-474
-        const float inv_var = 1.f / (sd * sd);
-        const float logsd = logf(sd);
-        const int nh = min(a.hp.reward_horizon, XD / a.Da) * a.Da;                  // [:, :reward_horizon]
-        auto elem = [&](int q, float& eps, float& mu, float& lp, bool& unclipped) {
-            eps = bo[q];
+    // Spread over the whole workgroup: (A) one (row, q) element per thread -> log-prob, mean,
+    // clip flags into scratch in tA (h3 is dead once the out layer has run); (B) one row per lane
+    // of wave 0 -> the row's mean log-prob and loss terms; (C) one (row, q) element per thread ->
+    // d loss / d eps into the dy tile (A operand of the backward) and the dyT image.
+    const float* bo = bias + 3 * H;
+    const int nh = min(a.hp.reward_horizon, XD / a.Da) * a.Da;                      // [:, :reward_horizon]
+    float* e_lp = (float*)tA;                  // [ROWS][XD]
+    float* e_mu = e_lp + ROWS * XD;            // [ROWS][XD]
+    float* e_uc = e_mu + ROWS * XD;            // [ROWS][XD] 1 = x_recon not clipped
+    float* e_dn = e_uc + ROWS * XD;            // [ROWS] d loss / d newlogprob
+    auto row_sd = [&](int r) {                 // diffusion_vpg.py:473-474
+        const float* sc = sch + (KF - 1 - rj[r]) * DPPO_SCHED_COLS;
+        return fminf(fmaxf(expf(0.5f * sc[4]), a.hp.min_lp_std), 1e6f);
+    };
+    for (int idx = tid; idx < ROWS * XD; idx += THREADS) {
+        const int r = idx / XD, q = idx % XD;
+        const float* sc = sch + (KF - 1 - rj[r]) * DPPO_SCHED_COLS;
+        const float sd = row_sd(r);
+        float eps = bo[q];
 #pragma unroll
-            for (int w = 0; w < WAVES; ++w) eps += part[(w * ROWS + r) * (16 * NO) + q];
-            const float x = xp[r * XD + q];
-            float xr = sc[0] * x - sc[1] * eps;
-            unclipped = fabsf(xr) <= 1.f;
-            xr = fminf(fmaxf(xr, -1.f), 1.f);
-            mu = sc[2] * xr + sc[3] * x;
-            const float z = (xn[r * XD + q] - mu) / sd;
-            lp = -0.5f * z * z - logsd - LOG_2PI_HALF;
-        };
-        float lpsum = 0.f;
-        for (int q = 0; q < XD; ++q) {
-            float eps, mu, lp; bool uc;
-            elem(q, eps, mu, lp, uc);
-            if (!train && valid && a.lp_elem) a.lp_elem[((size_t)n * KF + j) * XD + q] = lp;
-            if (q < nh) lpsum += fminf(fmaxf(lp, -5.f), 2.f);
-        }
-        const float newlp = lpsum / (float)nh;
-        if (!train) {
-            if (valid && a.lp_mean) a.lp_mean[(size_t)n * KF + j] = newlp;
-        } else {
-            float pg = 0.f, kl = 0.f, cf = 0.f, ra = 0.f, dnewlp = 0.f;
-            if (valid) {
+        for (int w = 0; w < WAVES; ++w) eps += part[(w * ROWS + r) * (16 * NO) + q];
+        const float x = xp[r * XD + q];
+        float xr = sc[0] * x - sc[1] * eps;
+        e_uc[idx] = fabsf(xr) <= 1.f ? 1.f : 0.f;
+        xr = fminf(fmaxf(xr, -1.f), 1.f);
+        const float mu = sc[2] * xr + sc[3] * x;
+        const float z = (xn[r * XD + q] - mu) / sd;
+        const float lp = -0.5f * z * z - logf(sd) - LOG_2PI_HALF;
+        e_lp[idx] = lp;
+        e_mu[idx] = mu;
+        if (!train && rn[r] >= 0 && a.lp_elem) a.lp_elem[((size_t)rn[r] * KF + rj[r]) * XD + q] = lp;
+    }
+    lds_sync();
+    if (tid < 64) {
+        const int r = tid;
+        float pg = 0.f, kl = 0.f, cf = 0.f, ra = 0.f, dnewlp = 0.f;
+        if (r < ROWS) {
+            const int n = rn[r], j = rj[r];
+            float lpsum = 0.f;
+            for (int q = 0; q < nh; ++q) lpsum += fminf(fmaxf(e_lp[r * XD + q], -5.f), 2.f);
+            const float newlp = lpsum / (float)nh;
+            if (!train) {
+                if (n >= 0 && a.lp_mean) a.lp_mean[(size_t)n * KF + j] = newlp;
+            } else if (n >= 0) {
                 const double* S3 = a.adv_stats;
                 float A = a.adv[n];
                 if (a.hp.norm_adv) {   // population std over the minibatch (diffusion_ppo.py:74-75)
@@ -353,23 +363,11 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
                 const float dpg = (pg1 >= pg2) ? -A : (in_r ? -A : 0.f);   // tf.maximum ties -> first arg
                 dnewlp = dpg * ratio * a.hp.grad_scale;
             }
-            // d loss / d eps (through clip(lp), Normal.log_prob, mu, clip(x_recon))
-            AT* dyt = a0;   // a0 tile is dead after L1; dy tile has row stride lda0
-            for (int q = 0; q < ktw; ++q) {
-                float d = 0.f;
-                if (q < XD && valid && q < nh) {
-                    float eps, mu, lp; bool uc;
-                    elem(q, eps, mu, lp, uc);
-                    const bool inc = lp >= -5.f && lp <= 2.f;
-                    const float dlp = inc ? dnewlp / (float)nh : 0.f;
-                    const float dmu = dlp * (xn[r * XD + q] - mu) * inv_var;
-                    d = uc ? -sc[1] * sc[2] * dmu : 0.f;
-                }
-                dyt[r * lda0 + q] = P::cvt(d);
-                if (q < XD) ((AT*)a.ws.dyT)[(size_t)q * a.ws.ldm + grow0 + r] = P::cvt(d);
-            }
+            e_dn[r] = dnewlp;
+        }
+        if (train) {
             pg = wave_sum(pg); kl = wave_sum(kl); cf = wave_sum(cf); ra = wave_sum(ra);
-            if (lane == 0) {
+            if (tid == 0) {
                 atomic_add_metric(a.metrics, 0, pg);
                 atomic_add_metric(a.metrics, 2, kl);
                 atomic_add_metric(a.metrics, 3, cf);
@@ -378,6 +376,25 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         }
     }
     if constexpr (!train) return;
+    lds_sync();
+    // d loss / d eps through clip(lp), Normal.log_prob, mu and clip(x_recon); idx -> (q, r) with r
+    // fastest so the dyT image stores coalesce
+    AT* dyt = a0;   // a0 tile is dead after L1; dy tile has row stride lda0
+    for (int idx = tid; idx < ROWS * ktw; idx += THREADS) {
+        const int q = idx / ROWS, r = idx % ROWS;
+        float d = 0.f;
+        if (q < XD && q < nh && rn[r] >= 0) {
+            const int e = r * XD + q;
+            const float lp = e_lp[e];
+            const float sd = row_sd(r);
+            const float* sc = sch + (KF - 1 - rj[r]) * DPPO_SCHED_COLS;
+            const float dlp = (lp >= -5.f && lp <= 2.f) ? e_dn[r] / (float)nh : 0.f;
+            const float dmu = dlp * (xn[r * XD + q] - e_mu[e]) / (sd * sd);
+            d = e_uc[e] != 0.f ? -sc[1] * sc[2] * dmu : 0.f;
+        }
+        dyt[r * lda0 + q] = P::cvt(d);
+        if (q < XD) ((AT*)a.ws.dyT)[(size_t)q * a.ws.ldm + grow0 + r] = P::cvt(d);
+    }
     lds_sync();
 
     // ---- backward dX chain (weights continue in the same stream) ----

@@ -7,6 +7,7 @@
 // (diffusion_vpg.py:198-243, 301-320). Activations never leave LDS; weights stream from L2.
 // The actor used at step t is actor_ft when t < K' else the frozen base actor (diffusion_vpg.py:161-180);
 // the reference's always-computed base forward (:161) does not change the result and is skipped.
+#include <stdlib.h>
 #include <string.h>
 #include "dppo_common.cuh"
 #include "dppo_internal.h"
@@ -41,7 +42,7 @@ struct SampleArgs {
 #define SW 16
 #define ST (SW * 64)
 
-template <class P, int NT, int NO, int KSI, bool INJ>
+template <class P, int NT, int NO, int KSI, bool INJ, int QD>
 __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
     using AT = typename P::AT;
     constexpr int KSH = ksh_for<P>(NT, SW);
@@ -151,8 +152,12 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
     const __amdgpu_buffer_rsrc_t rs_base = packed_rsrc(a.packed_base), rs_ft = packed_rsrc(a.packed_ft);
     auto W = [&](const uint8_t* PK, int seg) { return wsrc(PK == a.packed_ft ? rs_ft : rs_base, L.off[seg]); };
     // the stream starts with step 0's in-layer (t = K-1)
-    WRing<NT> R;
-    ring_prime(R, W(K - 1 < KF ? a.packed_ft : a.packed_base, SEG_W_IN), L.ks_in, ntile0, lane);
+    // the weight stream: a QD-deep queue per wave, primed with step 0's in-layer (t = K-1)
+    WQueue<QD, NT> R;
+    {
+        const uint8_t* PK0 = K - 1 < KF ? a.packed_ft : a.packed_base;
+        queue_prime(R, W(PK0, SEG_W_IN), KSI, NextLayers{W(PK0, SEG_W_L1), KSH, W(PK0, SEG_W_L2), KSH}, ntile0, lane);
+    }
     for (int i = 0; i < K; ++i) {
         const int t = K - 1 - i;
         const int is_ft = t < KF;
@@ -173,8 +178,8 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
         lds_sync();
         // b) in-Dense: h1 = a0 W_in + b_in  (no activation after the input layer, mlp.py:144)
         f32x4 h1[1][NT], acc[1][NT];
-        gemm_stream<P, 1, NT, KSI>(a0, lda0, W(PK, SEG_W_IN), ntile0, h1, lane, R,
-                              NextLayer{W(PK, SEG_W_L1), L.ks_h, ntile0});
+        gemm_queue<P, 1, NT, KSI, QD>(a0, lda0, W(PK, SEG_W_IN), ntile0, h1, lane, R,
+                                      NextLayers{W(PK, SEG_W_L1), KSH, W(PK, SEG_W_L2), KSH});
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int col = (ntile0 + n) * 16 + ccol(lane);
@@ -187,8 +192,8 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
         }
         lds_sync();
         // c) l1: relu(h1) W_l1 + b -> relu -> tB   (pre-activation block, mlp.py:192-193,202-203)
-        gemm_stream<P, 1, NT, KSH>(tA, ldh, W(PK, SEG_W_L1), ntile0, acc, lane, R,
-                              NextLayer{W(PK, SEG_W_L2), L.ks_h, ntile0});
+        gemm_queue<P, 1, NT, KSH, QD>(tA, ldh, W(PK, SEG_W_L1), ntile0, acc, lane, R,
+                                      NextLayers{W(PK, SEG_W_L2), KSH, W(PKn, SEG_W_IN), KSI});
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int col = (ntile0 + n) * 16 + ccol(lane);
@@ -199,8 +204,8 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
         lds_sync();
         // d) l2: relu(h2) W_l2 + b + h1 (residual, mlp.py:206) -> tA; the stream moves on to the
         //    next denoising step's in-layer (possibly the other actor)
-        gemm_stream<P, 1, NT, KSH>(tB, ldh, W(PK, SEG_W_L2), ntile0, acc, lane, R,
-                              NextLayer{W(PKn, SEG_W_IN), L.ks_in, ntile0});
+        gemm_queue<P, 1, NT, KSH, QD>(tB, ldh, W(PK, SEG_W_L2), ntile0, acc, lane, R,
+                                      NextLayers{W(PKn, SEG_W_IN), KSI, W(PKn, SEG_W_L1), KSH});
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int col = (ntile0 + n) * 16 + ccol(lane);
@@ -275,17 +280,35 @@ static size_t sample_lds_bytes(const SampleArgs& a, int NO) {
     return o;
 }
 
-template <class P, int NT, int NO, int KSI, bool INJ>
-static int launch_sample_k(const SampleArgs& a, hipStream_t s) {
+template <class P, int NT, int NO, int KSI, bool INJ, int QD>
+static int launch_sample_q(const SampleArgs& a, hipStream_t s) {
     if (a.L.ks_h != ksh_for<P>(NT, SW) || a.L.ks_in != KSI || a.L.ks_h % SW != 0)
         return dppo_set_error(DPPO_EUNSUPPORTED, "sampler: hidden %d not supported at this precision", a.H);
     const size_t lds = sample_lds_bytes<P>(a, NO);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "sampler needs %zu B of LDS", lds);
-    auto k = sample_kernel<P, NT, NO, KSI, INJ>;
+    auto k = sample_kernel<P, NT, NO, KSI, INJ, QD>;
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k, dim3(dppo_cdiv(a.E, 16)), dim3(ST), lds, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
+}
+
+// weight-queue depth (k-steps in flight per wave): DPPO_SAMPLER_QD = 2 | 3 | 4 (measurement knob)
+static int sampler_queue_depth() {
+    static int qd = [] {
+        const char* e = getenv("DPPO_SAMPLER_QD");
+        const int v = e ? atoi(e) : 3;
+        return v >= 2 && v <= 4 ? v : 3;
+    }();
+    return qd;
+}
+
+template <class P, int NT, int NO, int KSI, bool INJ>
+static int launch_sample_k(const SampleArgs& a, hipStream_t s) {
+    const int qd = sampler_queue_depth();
+    if (qd == 2) return launch_sample_q<P, NT, NO, KSI, INJ, 2>(a, s);
+    if (qd == 4) return launch_sample_q<P, NT, NO, KSI, INJ, 4>(a, s);
+    return launch_sample_q<P, NT, NO, KSI, INJ, 3>(a, s);
 }
 
 template <class P, int NT, int NO, int KSI>

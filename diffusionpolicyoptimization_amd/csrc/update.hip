@@ -283,6 +283,18 @@ __global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict_
     }
 }
 
+// zero up to 4 byte ranges (4-B aligned, sizes multiple of 4) in one launch
+struct ZeroArgs { void* p[4]; size_t n[4]; };
+__global__ __launch_bounds__(256) void zero_kernel(ZeroArgs z) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (int r = 0; r < 4; ++r) {
+        if (!z.p[r]) continue;
+        uint32_t* q = (uint32_t*)z.p[r];
+        const size_t n = z.n[r] / 4;
+        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) q[i] = 0u;
+    }
+}
+
 __global__ void feistel_kernel(int64_t first, int64_t count, FeistelKey fk, int64_t* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) {
@@ -397,16 +409,23 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     const FlatOffsets FC = make_flat_offsets(D.SD, D.HC, 1, 0);
     float* ga = grads;
     float* gc = grads + FA.count;
-    DPPO_HIP(hipMemsetAsync(grads, 0, sizeof(float) * (FA.count + FC.count), s));
-    DPPO_HIP(hipMemsetAsync(metrics, 0, sizeof(double) * 16, s));
-    DPPO_HIP(hipMemsetAsync(ws.gseg, 0, sizeof(float) * 16 * D.H, s));
+    // one launch zeroes the atomically accumulated outputs (gradients, metrics, bucket sums, stats)
+    ZeroArgs z = {};
+    z.p[0] = grads; z.n[0] = (FA.count + FC.count) * sizeof(float);
+    z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
+    z.p[2] = ws.gseg; z.n[2] = (size_t)16 * D.H * sizeof(float);
+    z.p[3] = ws.stats; z.n[3] = 4 * sizeof(double);
+    hipLaunchKernelGGL(zero_kernel, dim3(256), dim3(256), 0, s, z);
+    DPPO_HIP(hipGetLastError());
+    const FeistelKey fk = feistel_key((uint64_t)total, perm_seed, epoch);
     const double* stats = adv_stats;
     if (!stats) {
-        rc = dppo_ppo_adv_stats(advantages, total, D.KF, perm_seed, epoch, start, rows, row_index, ws.stats, stream);
-        if (rc) return rc;
+        const int blocks = dppo_cdiv(rows, 256) < 512 ? dppo_cdiv(rows, 256) : 512;
+        hipLaunchKernelGGL(adv_stats_kernel, dim3(blocks), dim3(256), 0, s, advantages, fk, D.KF, start, rows,
+                           row_index, ws.stats);
+        DPPO_HIP(hipGetLastError());
         stats = ws.stats;
     }
-    const FeistelKey fk = feistel_key((uint64_t)total, perm_seed, epoch);
     LossHP lh;
     lh.gamma_denoising = hp->gamma_denoising; lh.clip_coef = hp->clip_ploss_coef;
     lh.clip_coef_base = hp->clip_ploss_coef_base; lh.clip_coef_rate = hp->clip_ploss_coef_rate;
