@@ -10,7 +10,8 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime first so the library binds to the same one)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libdppo_hip.so")
+# DPPO_LIB selects a tuning build (tools/variant_build.sh); it must exist like the default one
+LIB_PATH = os.environ.get("DPPO_LIB") or os.path.join(_HERE, "lib", "libdppo_hip.so")
 
 DPPO_F32, DPPO_BF16 = 0, 1
 DPPO_ADAMW_KERAS, DPPO_ADAMW_TORCH = 0, 1

@@ -196,13 +196,17 @@ __device__ inline void queue_prime(WQueue<D, NT>& Q, WSrc W, int KS, const NextL
         }
 }
 
-template <class P, int MT, int NT, int KS, int D>
+// ZERO = false accumulates onto acc (a GEMM over a concatenated K); TAIL = true issues no
+// look-ahead past this layer (the last layer of the kernel: nothing would consume it)
+template <class P, int MT, int NT, int KS, int D, bool ZERO = true, bool TAIL = false>
 __device__ inline void gemm_queue(const typename P::AT* A, int lda, WSrc W, int ntile0, f32x4 (&acc)[MT][NT], int lane,
                                   WQueue<D, NT>& Q, const NextLayers& nx) {
+    if constexpr (ZERO) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int n = 0; n < NT; ++n) zero_acc(acc[m][n]);
+            for (int n = 0; n < NT; ++n) zero_acc(acc[m][n]);
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
         u32x4 c[NT];
@@ -212,8 +216,10 @@ __device__ inline void gemm_queue(const typename P::AT* A, int lda, WSrc W, int 
         for (int d = 0; d + 1 < D; ++d)
 #pragma unroll
             for (int n = 0; n < NT; ++n) Q.b[d][n] = Q.b[d + 1][n];
+        if (!TAIL || ks + D < KS) {
 #pragma unroll
-        for (int n = 0; n < NT; ++n) Q.b[D - 1][n] = stream_frag<KS>(W, nx, ntile0 + n, ks + D, lane);
+            for (int n = 0; n < NT; ++n) Q.b[D - 1][n] = stream_frag<KS>(W, nx, ntile0 + n, ks + D, lane);
+        }
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
             const u32x4 a = lds_afrag<P>(A, lda, m, ks, lane);

@@ -16,6 +16,32 @@
 
 #define LOG_2PI_HALF 0.91893853320467274178f
 
+// Phase timing for tuning builds (tools/variant_build.sh ... -DDPPO_ROWTILE_TIMING): wave 0 of
+// every workgroup adds the shader-clock cycles it spent in each phase (barrier waits included).
+#ifdef DPPO_ROWTILE_TIMING
+__device__ unsigned long long dppo_phase_cycles[32];
+#define PHASE(k)                                                                  \
+    do {                                                                          \
+        if (threadIdx.x == 0) {                                                   \
+            const unsigned long long now_ = __builtin_readcyclecounter();         \
+            atomicAdd(&dppo_phase_cycles[(k)], now_ - t_phase_);                  \
+            t_phase_ = now_;                                                      \
+        }                                                                         \
+    } while (0)
+#define PHASE_START unsigned long long t_phase_ = __builtin_readcyclecounter()
+extern "C" DPPO_API int dppo_debug_phase_cycles(unsigned long long* out, int reset) {
+    DPPO_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dppo_phase_cycles), sizeof(unsigned long long) * 32));
+    if (reset) {
+        unsigned long long z[32] = {};
+        DPPO_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dppo_phase_cycles), z, sizeof(z)));
+    }
+    return DPPO_OK;
+}
+#else
+#define PHASE(k) do {} while (0)
+#define PHASE_START do {} while (0)
+#endif
+
 // Accumulator tile -> feature-major image XT[col][row] (4 consecutive rows per lane per MFMA
 // tile). Buffer stores through ONE resource for the whole workspace: the per-lane part of the
 // offset is a single 32-bit VGPR, the image / tile parts are scalar, so no 64-bit address pairs
@@ -109,7 +135,8 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     static_assert(ROWS <= 64, "the epilogue maps one row per lane of wave 0");
     constexpr int KSH = ksh_for<P>(NT, WAVES);
     constexpr int NOK = nok_for<P>(NT);
-    constexpr int KSO = 2;   // k-steps of the transposed out layer (out dim <= 2*KG, padded even)
+    constexpr int KSO = 2;
+    PHASE_START;   // k-steps of the transposed out layer (out dim <= 2*KG, padded even)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const MlpLayout& L = a.L;
@@ -138,10 +165,12 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     const __amdgpu_buffer_rsrc_t wsr = packed_rsrc(a.ws.base);
     const uint32_t ldm32 = (uint32_t)a.ws.ldm, grow32 = (uint32_t)grow0;
 
-    // ---- prologue: rows, schedule, time embedding for t < K' (actor_ft) ----
-    if (tid < ROWS) {
-        const int64_t gr = (int64_t)grow0 + tid;
-        int n = -1, j = 0;
+    // ---- prologue: rows, gathers, schedule, biases, time embedding for t < K' (actor_ft) ----
+    // Every thread maps its own element to its row (the Feistel step is a few dozen ALU ops), so
+    // the chains / obs gathers issue at once instead of after a barrier on a row table.
+    auto row_of = [&](int r, int& n, int& j) {
+        const int64_t gr = (int64_t)grow0 + r;
+        n = -1; j = 0;
         if (gr < a.nrows) {
             if (train) {
                 const uint64_t idx = minibatch_row(a.row_index, (uint64_t)(a.start + gr), a.fk);
@@ -150,6 +179,27 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
                 n = (int)(gr / KF); j = (int)(gr % KF);
             }
         }
+    };
+    for (int i = tid; i < ROWS * XD; i += THREADS) {
+        const int r = i / XD, q = i % XD;
+        int n, j;
+        row_of(r, n, j);
+        float vp = 0.f, vn = 0.f;
+        if (n >= 0) {
+            const float* c = a.chains + ((size_t)n * (KF + 1) + j) * XD + q;
+            vp = c[0]; vn = c[XD];   // chains_prev = chains[:, j], chains_next = chains[:, j+1]
+        }
+        xp[i] = vp; xn[i] = vn;
+    }
+    for (int i = tid; i < ROWS * SD; i += THREADS) {
+        const int r = i / SD, c = i % SD;
+        int n, j;
+        row_of(r, n, j);
+        st[i] = n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f;
+    }
+    if (tid < ROWS) {
+        int n, j;
+        row_of(tid, n, j);
         rn[tid] = n; rj[tid] = j;
     }
     for (int i = tid; i < KF * DPPO_SCHED_COLS; i += THREADS) sch[i] = a.sched[i];
@@ -158,38 +208,29 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         const int j = i < 3 * H ? i % H : i - 3 * H;
         bias[i] = ((const float*)(a.packed + L.off[seg]))[j];
     }
-    const int half = TD / 2;
-    const float lnf = logf(10000.f) / (float)(half - 1);
-    const float* tw = (const float*)(a.packed + L.off[SEG_TIME]);
-    for (int i = tid; i < KF * 2 * TD; i += THREADS) {
-        const int t = i / (2 * TD), jj = i % (2 * TD);
-        float acc = tw[TD * 2 * TD + jj];
-        for (int k = 0; k < TD; ++k) {
-            const float f = expf(-(float)(k % half) * lnf) * (float)t;
-            acc += (k < half ? sinf(f) : cosf(f)) * tw[k * 2 * TD + jj];
+    if (a.temb_g) {   // precomputed once per minibatch (temb_kernel)
+        for (int i = tid; i < KF * TD; i += THREADS) temb[i] = a.temb_g[i];
+    } else {
+        const int half = TD / 2;
+        const float lnf = logf(10000.f) / (float)(half - 1);
+        const float* tw = (const float*)(a.packed + L.off[SEG_TIME]);
+        for (int i = tid; i < KF * 2 * TD; i += THREADS) {
+            const int t = i / (2 * TD), jj = i % (2 * TD);
+            float acc = tw[TD * 2 * TD + jj];
+            for (int k = 0; k < TD; ++k) {
+                const float f = expf(-(float)(k % half) * lnf) * (float)t;
+                acc += (k < half ? sinf(f) : cosf(f)) * tw[k * 2 * TD + jj];
+            }
+            ta1[i] = mishf(acc);
         }
-        ta1[i] = mishf(acc);
-    }
-    __syncthreads();
-    for (int i = tid; i < KF * TD; i += THREADS) {
-        const int t = i / TD, jj = i % TD;
-        const float* w2 = tw + TD * 2 * TD + 2 * TD;
-        float acc = w2[2 * TD * TD + jj];
-        for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + jj];
-        temb[i] = acc;
-    }
-    for (int i = tid; i < ROWS * XD; i += THREADS) {
-        const int r = i / XD, q = i % XD, n = rn[r];
-        float vp = 0.f, vn = 0.f;
-        if (n >= 0) {
-            const float* c = a.chains + ((size_t)n * (KF + 1) + rj[r]) * XD + q;
-            vp = c[0]; vn = c[XD];   // chains_prev = chains[:, j], chains_next = chains[:, j+1]
+        __syncthreads();
+        for (int i = tid; i < KF * TD; i += THREADS) {
+            const int t = i / TD, jj = i % TD;
+            const float* w2 = tw + TD * 2 * TD + 2 * TD;
+            float acc = w2[2 * TD * TD + jj];
+            for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + jj];
+            temb[i] = acc;
         }
-        xp[i] = vp; xn[i] = vn;
-    }
-    for (int i = tid; i < ROWS * SD; i += THREADS) {
-        const int r = i / SD, c = i % SD, n = rn[r];
-        st[i] = n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f;
     }
     __syncthreads();
     // a0 = [x_prev, temb(t), state] (mlp_diffusion.py:86), t = K'-1-j (diffusion_vpg.py:456-458)
@@ -217,34 +258,42 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     }
     __syncthreads();
 
+    PHASE(0);
     const int ntile0 = wave * NT;
     const __amdgpu_buffer_rsrc_t rs = packed_rsrc(a.packed);
     auto W = [&](int seg) { return wsrc(rs, L.off[seg]); };
-    f32x4 H1[MT][NT], acc[MT][NT];
+    f32x4 acc[MT][NT];
     static_assert(MT * NT * 4 <= 32, "relu masks are 32-bit");
     uint32_t mask1 = 0, mask2 = 0;
-    WRing<NT> R;
-    ring_prime(R, W(SEG_W_IN), KSI, ntile0, lane);
+    // The weight stream is one QD-deep queue per wave through every layer of the kernel:
+    //   in -> l1 -> l2 -> in (again: the residual h1 is recomputed as a0 W_in, 2 more k-steps,
+    //   instead of holding 8*MT*NT fp32 registers from L1 to L3) -> [train] out^T -> l2^T -> l1^T.
+    constexpr int QD = 3;
+    WQueue<QD, NT> R;
+    queue_prime(R, W(SEG_W_IN), KSI, NextLayers{W(SEG_W_L1), KSH, W(SEG_W_L2), KSH}, ntile0, lane);
     ORing<NOK, NO> ob;
     // ---- L1: h1 = a0 W_in + b (no activation on the input layer) ----
-    gemm_stream<P, MT, NT, KSI>(a0, lda0, W(SEG_W_IN), ntile0, H1, lane, R, NextLayer{W(SEG_W_L1), KSH, ntile0});
-    add_bias(H1, bias, ntile0, lane);
+    gemm_queue<P, MT, NT, KSI, QD>(a0, lda0, W(SEG_W_IN), ntile0, acc, lane, R,
+                                   NextLayers{W(SEG_W_L1), KSH, W(SEG_W_L2), KSH});
+    add_bias(acc, bias, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < NT; ++n)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                acc[m][n][r] = fmaxf(H1[m][n][r], 0.f);
-                if (H1[m][n][r] > 0.f) mask1 |= 1u << ((m * NT + n) * 4 + r);
+                if (acc[m][n][r] > 0.f) mask1 |= 1u << ((m * NT + n) * 4 + r);
+                acc[m][n][r] = fmaxf(acc[m][n][r], 0.f);
             }
     // materialise the mask now (otherwise hipcc keeps the 8*MT*NT floats alive until the backward)
     asm volatile("" : "+v"(mask1));
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
     if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.u1T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
+    PHASE(1);
     // ---- L2: h2 = relu(h1) W_l1 + b ----
-    gemm_stream<P, MT, NT, KSH>(tA, ldh, W(SEG_W_L1), ntile0, acc, lane, R, NextLayer{W(SEG_W_L2), KSH, ntile0});
+    gemm_queue<P, MT, NT, KSH, QD>(tA, ldh, W(SEG_W_L1), ntile0, acc, lane, R,
+                                   NextLayers{W(SEG_W_L2), KSH, W(SEG_W_IN), KSI});
     add_bias(acc, bias + H, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -259,21 +308,32 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
     if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.u2T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
+    PHASE(2);
     // out-layer fragments: fetched here so they land during L3 (not held through L1/L2: VGPRs)
     out_prefetch<NOK, NO, WAVES>(ob, W(SEG_W_OUT), KSH, wave, lane);
-    // ---- L3: h3 = relu(h2) W_l2 + b + h1; the stream continues into the backward's W_out^T ----
-    gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_W_L2), ntile0, acc, lane, R,
-                                train ? NextLayer{W(SEG_T_OUT), KSO, ntile0} : NextLayer{W(SEG_W_L2), KSH, ntile0});
-    add_bias(acc, bias + 2 * H, ntile0, lane);
+    // ---- L3: h3 = relu(h2) W_l2 + b_l2 + h1 = [relu(h2) | a0] [W_l2 ; W_in] + b_l2 + b_in ----
+    gemm_queue<P, MT, NT, KSH, QD>(tB, ldh, W(SEG_W_L2), ntile0, acc, lane, R,
+                                   train ? NextLayers{W(SEG_W_IN), KSI, W(SEG_T_OUT), KSO}
+                                         : NextLayers{W(SEG_W_IN), KSI, W(SEG_W_IN), KSI});
+    if constexpr (train)
+        gemm_queue<P, MT, NT, KSI, QD, false>(a0, lda0, W(SEG_W_IN), ntile0, acc, lane, R,
+                                              NextLayers{W(SEG_T_OUT), KSO, W(SEG_T_L2), KSH});
+    else
+        gemm_queue<P, MT, NT, KSI, QD, false, true>(a0, lda0, W(SEG_W_IN), ntile0, acc, lane, R,
+                                                    NextLayers{W(SEG_W_IN), KSI, W(SEG_W_IN), KSI});
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+    for (int n = 0; n < NT; ++n) {
+        const int col = (ntile0 + n) * 16 + ccol(lane);
+        const float bv = bias[2 * H + col] + bias[col];
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[m][n][r] += H1[m][n][r];
+            for (int r = 0; r < 4; ++r) acc[m][n][r] += bv;
+    }
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
     if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.h3T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
+    PHASE(3);
     // ---- L4: eps = h3 W_out + b (k split over the waves, fragments prefetched before L1) ----
     {
         f32x4 po[MT][NO];
@@ -288,6 +348,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     }
     lds_sync();
 
+    PHASE(4);
     // ---- epilogue: p_mean_var + Normal.log_prob (+ c_loss policy term and its gradient) ----
     // Spread over the whole workgroup: (A) one (row, q) element per thread -> log-prob, mean,
     // clip flags into scratch in tA (h3 is dead once the out layer has run); (B) one row per lane
@@ -322,6 +383,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         if (!train && rn[r] >= 0 && a.lp_elem) a.lp_elem[((size_t)rn[r] * KF + rj[r]) * XD + q] = lp;
     }
     lds_sync();
+    PHASE(5);
     if (tid < 64) {
         const int r = tid;
         float pg = 0.f, kl = 0.f, cf = 0.f, ra = 0.f, dnewlp = 0.f;
@@ -377,6 +439,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     }
     if constexpr (!train) return;
     lds_sync();
+    PHASE(6);
     // d loss / d eps through clip(lp), Normal.log_prob, mu and clip(x_recon); idx -> (q, r) with r
     // fastest so the dyT image stores coalesce
     AT* dyt = a0;   // a0 tile is dead after L1; dy tile has row stride lda0
@@ -396,15 +459,19 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         if (q < XD) ((AT*)a.ws.dyT)[(size_t)q * a.ws.ldm + grow0 + r] = P::cvt(d);
     }
     lds_sync();
+    PHASE(7);
 
     // ---- backward dX chain (weights continue in the same stream) ----
     // B4: dh3 = dy W_out^T (kept only in tB: B2 re-reads it from there, which frees 8*MT*NT VGPRs)
-    gemm_stream<P, MT, NT, KSO>(a0, lda0, W(SEG_T_OUT), ntile0, acc, lane, R, NextLayer{W(SEG_T_L2), KSH, ntile0});
+    gemm_queue<P, MT, NT, KSO, QD>(a0, lda0, W(SEG_T_OUT), ntile0, acc, lane, R,
+                                   NextLayers{W(SEG_T_L2), KSH, W(SEG_T_L1), KSH});
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
     store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.dh3T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
+    PHASE(8);
     // B3: dh2 = (dh3 W_l2^T) * relu'(h2)
-    gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_T_L2), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});
+    gemm_queue<P, MT, NT, KSH, QD>(tB, ldh, W(SEG_T_L2), ntile0, acc, lane, R,
+                                   NextLayers{W(SEG_T_L1), KSH, W(SEG_T_L1), KSH});
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -415,8 +482,10 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
     store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.dh2T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
+    PHASE(9);
     // B2: dh1 = dh3 + (dh2 W_l1^T) * relu'(h1)
-    gemm_stream<P, MT, NT, KSH>(tA, ldh, W(SEG_T_L1), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});
+    gemm_queue<P, MT, NT, KSH, QD, true, true>(tA, ldh, W(SEG_T_L1), ntile0, acc, lane, R,
+                                               NextLayers{W(SEG_T_L1), KSH, W(SEG_T_L1), KSH});
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -428,6 +497,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
                 acc[m][n][r] = dh3 + (on ? acc[m][n][r] : 0.f);
             }
     store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.dh1T), ldm32, ntile0, grow32, lane, acc);
+    PHASE(10);
 }
 
 // =============================================================================================

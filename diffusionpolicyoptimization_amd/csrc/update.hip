@@ -60,6 +60,54 @@ __device__ inline u32x4 dw_lds_frag(const uint8_t* img, int f, int c) {
     return *reinterpret_cast<const u32x4*>(img + f * DW_LINE + ((c ^ (f & 7)) << 4));
 }
 
+// the main loop, with or without the extra (bias / bucket) rows: two straight copies, so the
+// register allocator sees one uniform accumulator set per loop (a data-dependent MFMA inside
+// one loop made hipcc shuttle the accumulators between AGPRs and VGPRs every k-step)
+template <class P, bool EXTRA>
+__device__ __forceinline__ void dw_loop(uint8_t* smem, const DWArgs& a, const DWProb& pr, int nst, size_t m_begin,
+                                        int k_base, int n_base, int wave, int lane, const int8_t* seg_lds,
+                                        const typename P::AT* const (&srcA)[4], const typename P::AT* const (&srcB)[4],
+                                        f32x4 (&acc)[4][4], f32x4 (&acce)[4]) {
+    constexpr int BK = DW_LINE / (int)sizeof(typename P::AT);
+    const int wr = wave >> 1, wc = wave & 1;
+    const int fr = lane & 15, cq = lane >> 4;
+    auto issue = [&](int st, int buf) {
+        uint8_t* base = smem + buf * 2 * DW_OPB;
+        const size_t off = (size_t)st * BK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ins = wave + 4 * i;
+            __builtin_amdgcn_global_load_lds((void*)(srcA[i] + off), (lds_void_t*)(base + ins * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((void*)(srcB[i] + off), (lds_void_t*)(base + DW_OPB + ins * 1024), 16, 0, 0);
+        }
+    };
+    issue(0, 0);
+    for (int st = 0; st < nst; ++st) {
+        __syncthreads();                         // stage st landed; buffer st+1 no longer read
+        if (st + 1 < nst) issue(st + 1, (st + 1) & 1);
+        const uint8_t* imA = smem + (st & 1) * 2 * DW_OPB;
+        const uint8_t* imB = imA + DW_OPB;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            u32x4 A[4], B[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                A[i] = dw_lds_frag(imA, wr * 64 + i * 16 + fr, ks * 4 + cq);
+                B[i] = dw_lds_frag(imB, wc * 64 + i * 16 + fr, ks * 4 + cq);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(A[i], B[j], acc[i][j]);
+            if constexpr (EXTRA) {
+                const u32x4 AE = extra_frag<P>(pr.extra, fr, seg_lds + st * BK + ks * P::KG + cq * P::EPL);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acce[j] = P::mma(AE, B[j], acce[j]);
+            }
+        }
+    }
+}
+
 template <class P>
 __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
     using AT = typename P::AT;
@@ -92,7 +140,8 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
     const int nst = (int)((m_end - m_begin) / BK);
     const AT* XT = (const AT*)pr.XT;
     const AT* DT = (const AT*)pr.DT;
-    const bool do_extra = pr.extra != EXTRA_NONE && kt == 0 && wr == 0;
+    const bool wg_extra = pr.extra != EXTRA_NONE && kt == 0;      // uniform over the workgroup
+    const bool do_extra = wg_extra && wr == 0;
     int8_t* seg_lds = (int8_t*)(smem + 4 * DW_OPB);
     if (pr.extra == EXTRA_ONEHOT && kt == 0) {
         for (int i = tid; i < (int)(m_end - m_begin); i += 256) seg_lds[i] = a.seg[m_begin + i];
@@ -111,17 +160,6 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
         srcA[i] = XT + (size_t)fa * a.ldm + m_begin + c * EPC;
         srcB[i] = DT + (size_t)fb * a.ldm + m_begin + c * EPC;
     }
-    auto issue = [&](int st, int buf) {
-        uint8_t* base = smem + buf * 2 * DW_OPB;
-        const size_t off = (size_t)st * BK;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ins = wave + 4 * i;
-            __builtin_amdgcn_global_load_lds((void*)(srcA[i] + off), (lds_void_t*)(base + ins * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((void*)(srcB[i] + off), (lds_void_t*)(base + DW_OPB + ins * 1024), 16, 0, 0);
-        }
-    };
-
     f32x4 acc[4][4], acce[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -129,32 +167,9 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) zero_acc(acc[i][j]);
     }
-    const int fr = lane & 15, cq = lane >> 4;
-    issue(0, 0);
-    for (int st = 0; st < nst; ++st) {
-        __syncthreads();                         // stage st landed; buffer st+1 no longer read
-        if (st + 1 < nst) issue(st + 1, (st + 1) & 1);
-        const uint8_t* imA = smem + (st & 1) * 2 * DW_OPB;
-        const uint8_t* imB = imA + DW_OPB;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            u32x4 A[4], B[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                A[i] = dw_lds_frag(imA, wr * 64 + i * 16 + fr, ks * 4 + cq);
-                B[i] = dw_lds_frag(imB, wc * 64 + i * 16 + fr, ks * 4 + cq);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(A[i], B[j], acc[i][j]);
-            if (do_extra) {
-                const u32x4 AE = extra_frag<P>(pr.extra, fr, seg_lds + st * BK + ks * P::KG + cq * P::EPL);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acce[j] = P::mma(AE, B[j], acce[j]);
-            }
-        }
-    }
+    // waves 2,3 of an extra tile run the plain loop; the barrier count per stage is identical
+    if (do_extra) dw_loop<P, true>(smem, a, pr, nst, m_begin, k_base, n_base, wave, lane, seg_lds, srcA, srcB, acc, acce);
+    else dw_loop<P, false>(smem, a, pr, nst, m_begin, k_base, n_base, wave, lane, seg_lds, srcA, srcB, acc, acce);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -283,6 +298,34 @@ __global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict_
     }
 }
 
+// time-MLP forward for t = 0..KF-1 (mlp_diffusion.py:40-45), once per minibatch; the same
+// arithmetic, in the same order, as the row-tile prologue's fallback path
+__global__ __launch_bounds__(256) void temb_kernel(const uint8_t* __restrict__ packed, size_t time_off, int TD, int KF,
+                                                   float* __restrict__ temb) {
+    __shared__ float ta1[16 * 128];
+    const int tid = threadIdx.x;
+    const int half = TD / 2;
+    const float lnf = logf(10000.f) / (float)(half - 1);
+    const float* tw = (const float*)(packed + time_off);
+    for (int i = tid; i < KF * 2 * TD; i += 256) {
+        const int t = i / (2 * TD), jj = i % (2 * TD);
+        float acc = tw[TD * 2 * TD + jj];
+        for (int k = 0; k < TD; ++k) {
+            const float f = expf(-(float)(k % half) * lnf) * (float)t;
+            acc += (k < half ? sinf(f) : cosf(f)) * tw[k * 2 * TD + jj];
+        }
+        ta1[i] = mishf(acc);
+    }
+    __syncthreads();
+    for (int i = tid; i < KF * TD; i += 256) {
+        const int t = i / TD, jj = i % TD;
+        const float* w2 = tw + TD * 2 * TD + 2 * TD;
+        float acc = w2[2 * TD * TD + jj];
+        for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + jj];
+        temb[i] = acc;
+    }
+}
+
 // zero up to 4 byte ranges (4-B aligned, sizes multiple of 4) in one launch
 struct ZeroArgs { void* p[4]; size_t n[4]; };
 __global__ __launch_bounds__(256) void zero_kernel(ZeroArgs z) {
@@ -386,6 +429,27 @@ static int launch_dw(const DWArgs& a, hipStream_t s) {
     return DPPO_OK;
 }
 
+// one non-blocking side stream (+ fork/join events) per device and host thread, created on first use;
+// null if creation fails (the caller then runs everything on its own stream)
+struct SideStream { hipStream_t stream; hipEvent_t fork, join; };
+static SideStream* side_stream() {
+    constexpr int MAXDEV = 16;
+    thread_local SideStream ss[MAXDEV] = {};
+    thread_local bool tried[MAXDEV] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
+    if (!tried[dev]) {
+        tried[dev] = true;
+        if (hipStreamCreateWithFlags(&ss[dev].stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ss[dev].fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ss[dev].join, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            ss[dev].stream = nullptr;
+        }
+    }
+    return ss[dev].stream ? &ss[dev] : nullptr;
+}
+
 extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
                                   const void* packed_ft, const void* packed_critic, const float* actor_params,
                                   const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
@@ -440,16 +504,33 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     aa.XD = D.XD; aa.SD = D.SD; aa.TD = D.TD; aa.IN = D.IN; aa.H = D.H; aa.KF = D.KF; aa.Da = D.Da;
     aa.mode = ROWS_TRAIN; aa.nrows = rows; aa.fk = fk; aa.start = start; aa.row_index = row_index;
     aa.lp_old = lp_old_mean; aa.adv = advantages; aa.adv_stats = stats; aa.hp = lh; aa.ws = ws; aa.metrics = metrics;
-    rc = launch_actor_rowtile(aa, precision, s);
-    if (rc) return rc;
-
+    hipLaunchKernelGGL(temb_kernel, dim3(1), dim3(256), 0, s, (const uint8_t*)packed_ft, aa.L.off[SEG_TIME], D.TD, D.KF,
+                       ws.temb);
+    DPPO_HIP(hipGetLastError());
+    aa.temb_g = ws.temb;
     CriticArgs ca = {};
     ca.packed = (const uint8_t*)packed_critic;
     ca.L = make_mlp_layout(D.SD, D.HC, 1, 0, precision);
     ca.obs = obs; ca.SD = D.SD; ca.HC = D.HC; ca.KF = D.KF; ca.mode = ROWS_TRAIN; ca.nrows = rows;
     ca.fk = fk; ca.start = start; ca.row_index = row_index; ca.returns = returns; ca.hp = lh; ca.ws = ws; ca.metrics = metrics;
-    rc = launch_critic_rowtile(ca, precision, s);
+    // The critic row tiles are independent of the actor's: they run on a side stream, so they
+    // fill the CUs the actor's last (partial) round of tiles leaves idle. Joined before dW.
+    SideStream* side = side_stream();
+    if (side) {
+        DPPO_HIP(hipEventRecord(side->fork, s));
+        DPPO_HIP(hipStreamWaitEvent(side->stream, side->fork, 0));
+        rc = launch_critic_rowtile(ca, precision, side->stream);
+        if (rc) return rc;
+        DPPO_HIP(hipEventRecord(side->join, side->stream));
+    }
+    rc = launch_actor_rowtile(aa, precision, s);
     if (rc) return rc;
+    if (side) {
+        DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
+    } else {
+        rc = launch_critic_rowtile(ca, precision, s);
+        if (rc) return rc;
+    }
 
     DWArgs w = {};
     auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {

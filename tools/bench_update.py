@@ -48,7 +48,20 @@ def main():
     mb = timed(lambda: m.minibatch(obs, chains, lp_old, adv, ret, 7, 0, 0, args.rows, global_rows=args.rows), args.reps)
     lp = timed(lambda: ops.logprob(d, m.precision, m.packed_ft, m.sched, obs, chains, want_elem=False, lp_mean=lp_old), 3)
     cv = timed(lambda: ops.critic_forward(d, m.precision, m.packed_critic, obs, values=vals), 5)
-    print(json.dumps({"rowtile": os.environ.get("DPPO_ROWTILE", "default"), "minibatch_ms": mb,
+    phases = None
+    from diffusionpolicyoptimization_amd import _lib
+    lib = _lib.load()
+    if hasattr(lib, "dppo_debug_phase_cycles"):   # timing build: per-phase cycles of one minibatch
+        import ctypes
+        buf = (ctypes.c_ulonglong * 32)()
+        lib.dppo_debug_phase_cycles(buf, 1)
+        m.minibatch(obs, chains, lp_old, adv, ret, 7, 0, 0, args.rows, global_rows=args.rows)
+        torch.cuda.synchronize()
+        lib.dppo_debug_phase_cycles(buf, 1)
+        tiles = (args.rows + 63) // 64
+        phases = {f"p{i}": round(buf[i] / tiles) for i in range(11)}
+    print(json.dumps({"rowtile": os.environ.get("DPPO_ROWTILE", "default"), "phase_cycles_per_tile": phases,
+                      "minibatch_ms": mb,
                       "logprob_pass_ms": lp, "value_pass_ms": cv,
                       "grad_finite": bool(torch.isfinite(m.grads).all())}), flush=True)
 
