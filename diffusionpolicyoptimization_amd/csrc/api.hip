@@ -53,7 +53,7 @@ extern "C" size_t dppo_critic_param_count(const dppo_dims* d) {
 extern "C" size_t dppo_actor_packed_bytes(const dppo_dims* d, int precision) {
     Dims D;
     if (dppo_check_dims(d, &D)) return 0;
-    return make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision).total;
+    return make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K).total;
 }
 extern "C" size_t dppo_critic_packed_bytes(const dppo_dims* d, int precision) {
     Dims D;
@@ -66,7 +66,7 @@ extern "C" int dppo_pack_actor(const dppo_dims* d, int precision, const float* p
     if (rc) return rc;
     DPPO_CHECK(params && packed, "dppo_pack_actor: null pointer");
     DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
-    return dppo_pack_mlp(D.IN, D.H, D.XD, D.TD, precision, params, packed, (hipStream_t)stream);
+    return dppo_pack_mlp(D.IN, D.H, D.XD, D.TD, precision, params, packed, (hipStream_t)stream, D.K);
 }
 extern "C" int dppo_pack_critic(const dppo_dims* d, int precision, const float* params, void* packed, void* stream) {
     Dims D;

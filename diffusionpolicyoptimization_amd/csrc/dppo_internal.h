@@ -8,7 +8,7 @@ int dppo_set_error(int code, const char* fmt, ...);
 int dppo_hip_fail(hipError_t e, const char* what);
 
 int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* params,
-                  void* packed, hipStream_t s);
+                  void* packed, hipStream_t s, int temb_steps = 0);
 
 // derived dimensions of a dppo_dims
 struct Dims {

@@ -10,6 +10,8 @@
 //   T_OUT  packed bwd  W_out^T as [K=out][N=H]
 //   T_L2   packed bwd  W_l2^T  as [K=H][N=H]
 //   T_L1   packed bwd  W_l1^T  as [K=H][N=H]
+//   TEMB   fp32 [K][TD] time embeddings t_emb(t) for t = 0..K-1 (actor only; derived from TIME at
+//          pack time, so no kernel re-evaluates the time MLP per launch)
 // A packed matrix [K][N] is ceil(N/16) n-tiles x KS k-steps x 64 lanes x 16 B, with
 // KS = ceil(K / KG) rounded up to EVEN (the weight stream runs in k-step pairs), KG = 32 (bf16)
 // or 16 (fp32). Lane l of (ntile, ks) holds, for e < EPL,
@@ -25,10 +27,10 @@
 #endif
 
 enum MlpSeg { SEG_TIME = 0, SEG_W_IN, SEG_B_IN, SEG_W_L1, SEG_B_L1, SEG_W_L2, SEG_B_L2, SEG_W_OUT, SEG_B_OUT,
-              SEG_T_OUT, SEG_T_L2, SEG_T_L1, SEG_COUNT };
+              SEG_T_OUT, SEG_T_L2, SEG_T_L1, SEG_TEMB, SEG_COUNT };
 
 struct MlpLayout {
-    int in_dim, hidden, out_dim, time_dim, precision;
+    int in_dim, hidden, out_dim, time_dim, precision, temb_steps;
     int KG;                 // 32 bf16 / 16 fp32
     int ks_in, ks_h, ks_out_t;   // k-steps: in layer, hidden layers, transposed out (K = out_dim)
     int nt_h, nt_out;       // n-tiles: hidden, out
@@ -44,9 +46,11 @@ DPPO_HD inline size_t packed_matrix_bytes(int K, int N, int KG) {
     return (size_t)dppo_cdiv(N, 16) * (size_t)packed_ksteps(K, KG) * 64 * 16;
 }
 
-DPPO_HD inline MlpLayout make_mlp_layout(int in_dim, int hidden, int out_dim, int time_dim, int precision) {
+DPPO_HD inline MlpLayout make_mlp_layout(int in_dim, int hidden, int out_dim, int time_dim, int precision,
+                                         int temb_steps = 0) {
     MlpLayout L;
     L.in_dim = in_dim; L.hidden = hidden; L.out_dim = out_dim; L.time_dim = time_dim; L.precision = precision;
+    L.temb_steps = time_dim > 0 ? temb_steps : 0;
     L.KG = precision == 1 ? 32 : 16;
     L.ks_in = packed_ksteps(in_dim, L.KG);
     L.ks_h = packed_ksteps(hidden, L.KG);
@@ -67,6 +71,7 @@ DPPO_HD inline MlpLayout make_mlp_layout(int in_dim, int hidden, int out_dim, in
     L.off[SEG_T_OUT] = o; o = dppo_align256(o + packed_matrix_bytes(out_dim, hidden, L.KG));
     L.off[SEG_T_L2] = o; o = dppo_align256(o + packed_matrix_bytes(hidden, hidden, L.KG));
     L.off[SEG_T_L1] = o; o = dppo_align256(o + packed_matrix_bytes(hidden, hidden, L.KG));
+    L.off[SEG_TEMB] = o; o = dppo_align256(o + (size_t)4 * L.temb_steps * time_dim);
     L.total = o;
     return L;
 }

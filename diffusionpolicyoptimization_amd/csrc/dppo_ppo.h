@@ -15,7 +15,6 @@ struct PpoWorkspace {
     int8_t* seg;      // [ldm] t of each row (bucket id for the one-hot bias/temb sums), -1 invalid
     float* gseg;      // [16][H] per-t sums of dh1 (actor in-layer)
     double* stats;    // [4] adv {count, sum, sumsq}
-    float* temb;      // [16][TD] time embeddings of t = 0..K'-1 (actor_ft), once per minibatch
     size_t total;
 };
 
@@ -37,7 +36,6 @@ inline PpoWorkspace make_ppo_workspace(const Dims& D, int precision, int rows, u
     w.seg = base ? (int8_t*)(base + o) : nullptr; o = dppo_align256(o + w.ldm);
     w.gseg = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * 16 * (size_t)D.H);
     w.stats = base ? (double*)(base + o) : nullptr; o = dppo_align256(o + 8 * 4);
-    w.temb = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * 16 * (size_t)D.TD);
     w.total = o;
     return w;
 }
@@ -72,7 +70,6 @@ struct ActorArgs {
     int64_t start;
     const int64_t* row_index;
     const float* lp_old;   // [nsamp][KF]
-    const float* temb_g;   // [KF][TD] precomputed time embeddings, or null (computed in the prologue)
     const float* adv;      // [nsamp]
     const double* adv_stats;
     LossHP hp;

@@ -65,9 +65,35 @@ __global__ void pack_all_kernel(PackArgs a) {
     reinterpret_cast<u32x4*>(a.out + J.dst)[t] = v;
 }
 
+// t_emb(t) = Dense(2TD->TD)(mish(Dense(TD->2TD)(SinusoidalPosEmb(t)))) (mlp_diffusion.py:40-45,
+// modules.py:4-15), one workgroup per t; the arithmetic and its order match the oracle restatement
+static inline uint8_t* P_out(void* p) { return (uint8_t*)p; }
+
+__global__ __launch_bounds__(128) void temb_table_kernel(const float* __restrict__ params, FlatOffsets F, int TD,
+                                                         float* __restrict__ temb) {
+    __shared__ float ta1[128];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const int half = TD / 2;
+    const float lnf = logf(10000.f) / (float)(half - 1);
+    if (tid < 2 * TD) {
+        float acc = params[F.time_b1 + tid];
+        for (int k = 0; k < TD; ++k) {
+            const float f = expf(-(float)(k % half) * lnf) * (float)t;
+            acc += (k < half ? sinf(f) : cosf(f)) * params[F.time_w1 + k * 2 * TD + tid];
+        }
+        ta1[tid] = mishf(acc);
+    }
+    __syncthreads();
+    if (tid < TD) {
+        float acc = params[F.time_b2 + tid];
+        for (int k = 0; k < 2 * TD; ++k) acc += ta1[k] * params[F.time_w2 + k * TD + tid];
+        temb[(size_t)t * TD + tid] = acc;
+    }
+}
+
 int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* params,
-                  void* packed, hipStream_t s) {
-    const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision);
+                  void* packed, hipStream_t s, int temb_steps) {
+    const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision, temb_steps);
     const FlatOffsets F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
     const int KG = precision == DPPO_BF16 ? 32 : 16;
     PackArgs a = {};
@@ -102,5 +128,10 @@ int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precisi
     else
         hipLaunchKernelGGL((pack_all_kernel<16, 4>), dim3(blocks), dim3(256), 0, s, a);
     DPPO_HIP(hipGetLastError());
+    if (L.temb_steps > 0) {
+        hipLaunchKernelGGL(temb_table_kernel, dim3(L.temb_steps), dim3(128), 0, s, params, F, time_dim,
+                           (float*)(P_out(packed) + L.off[SEG_TEMB]));
+        DPPO_HIP(hipGetLastError());
+    }
     return DPPO_OK;
 }

@@ -105,7 +105,7 @@ __device__ inline void atomic_add_metric(double* m, int i, double v) { atomicAdd
 template <class P, int MT>
 struct ActorSmem {
     static constexpr int ROWS = 16 * MT;
-    size_t tA, tB, a0, xp, xn, st, temb, ta1, sch, rn, rj, bias, total;
+    size_t tA, tB, a0, xp, xn, st, temb, sch, rn, rj, bias, total;
     __host__ __device__ ActorSmem(const ActorArgs& a) {
         using AT = typename P::AT;
         const int pad = lds_pad_elems<P>();
@@ -118,7 +118,6 @@ struct ActorSmem {
         xn = o; o += dppo_align16(4 * ROWS * a.XD);
         st = o; o += dppo_align16(4 * ROWS * a.SD);
         temb = o; o += dppo_align16(4 * a.KF * a.TD);
-        ta1 = o; o += dppo_align16(4 * a.KF * 2 * a.TD);
         sch = o; o += dppo_align16(4 * a.KF * DPPO_SCHED_COLS);
         rn = o; o += dppo_align16(4 * ROWS);
         rj = o; o += dppo_align16(4 * ROWS);
@@ -156,7 +155,6 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     float* xn = (float*)(smem + S.xn);
     float* st = (float*)(smem + S.st);
     float* temb = (float*)(smem + S.temb);
-    float* ta1 = (float*)(smem + S.ta1);
     float* sch = (float*)(smem + S.sch);
     int* rn = (int*)(smem + S.rn);
     int* rj = (int*)(smem + S.rj);
@@ -208,29 +206,9 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         const int j = i < 3 * H ? i % H : i - 3 * H;
         bias[i] = ((const float*)(a.packed + L.off[seg]))[j];
     }
-    if (a.temb_g) {   // precomputed once per minibatch (temb_kernel)
-        for (int i = tid; i < KF * TD; i += THREADS) temb[i] = a.temb_g[i];
-    } else {
-        const int half = TD / 2;
-        const float lnf = logf(10000.f) / (float)(half - 1);
-        const float* tw = (const float*)(a.packed + L.off[SEG_TIME]);
-        for (int i = tid; i < KF * 2 * TD; i += THREADS) {
-            const int t = i / (2 * TD), jj = i % (2 * TD);
-            float acc = tw[TD * 2 * TD + jj];
-            for (int k = 0; k < TD; ++k) {
-                const float f = expf(-(float)(k % half) * lnf) * (float)t;
-                acc += (k < half ? sinf(f) : cosf(f)) * tw[k * 2 * TD + jj];
-            }
-            ta1[i] = mishf(acc);
-        }
-        __syncthreads();
-        for (int i = tid; i < KF * TD; i += THREADS) {
-            const int t = i / TD, jj = i % TD;
-            const float* w2 = tw + TD * 2 * TD + 2 * TD;
-            float acc = w2[2 * TD * TD + jj];
-            for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + jj];
-            temb[i] = acc;
-        }
+    {   // time embeddings t_emb(t), t < K', from the table the pack step derived (SEG_TEMB)
+        const float* tt = (const float*)(a.packed + L.off[SEG_TEMB]);
+        for (int i = tid; i < KF * TD; i += THREADS) temb[i] = tt[i];
     }
     __syncthreads();
     // a0 = [x_prev, temb(t), state] (mlp_diffusion.py:86), t = K'-1-j (diffusion_vpg.py:456-458)
@@ -836,7 +814,7 @@ extern "C" int dppo_logprob(const dppo_dims* d, int precision, const void* packe
     DPPO_CHECK(reward_horizon >= 1, "dppo_logprob: reward_horizon < 1");
     ActorArgs a = {};
     a.packed = (const uint8_t*)packed_ft;
-    a.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision);
+    a.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     a.sched = sched; a.obs = cond; a.chains = chains;
     a.XD = D.XD; a.SD = D.SD; a.TD = D.TD; a.IN = D.IN; a.H = D.H; a.KF = D.KF; a.Da = D.Da;
     a.mode = ROWS_LOGPROB;

@@ -12,6 +12,32 @@
 #include "dppo_common.cuh"
 #include "dppo_internal.h"
 
+// phase timing for tuning builds (-DDPPO_SAMPLER_TIMING): wave 0 of every workgroup adds the
+// shader-clock cycles of each phase of every denoising step (barrier waits included)
+#ifdef DPPO_SAMPLER_TIMING
+__device__ unsigned long long dppo_sampler_cycles[16];
+#define SPHASE(k)                                                                 \
+    do {                                                                          \
+        if (threadIdx.x == 0) {                                                   \
+            const unsigned long long now_ = __builtin_readcyclecounter();         \
+            atomicAdd(&dppo_sampler_cycles[(k)], now_ - t_phase_);                \
+            t_phase_ = now_;                                                      \
+        }                                                                         \
+    } while (0)
+#define SPHASE_START unsigned long long t_phase_ = __builtin_readcyclecounter()
+extern "C" DPPO_API int dppo_debug_sampler_cycles(unsigned long long* out, int reset) {
+    DPPO_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dppo_sampler_cycles), sizeof(unsigned long long) * 16));
+    if (reset) {
+        unsigned long long z[16] = {};
+        DPPO_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dppo_sampler_cycles), z, sizeof(z)));
+    }
+    return DPPO_OK;
+}
+#else
+#define SPHASE(k) do {} while (0)
+#define SPHASE_START do {} while (0)
+#endif
+
 struct SampleArgs {
     const uint8_t* packed_base;
     const uint8_t* packed_ft;
@@ -44,6 +70,7 @@ struct SampleArgs {
 
 template <class P, int NT, int NO, int KSI, bool INJ, int QD>
 __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
+    SPHASE_START;
     using AT = typename P::AT;
     constexpr int KSH = ksh_for<P>(NT, SW);
     constexpr int NOK = KSH / SW;
@@ -67,7 +94,6 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
     float* xs = (float*)(smem + o); o += dppo_align16(4 * 16 * XD);
     float* st = (float*)(smem + o); o += dppo_align16(4 * 16 * SD);
     float* temb = (float*)(smem + o); o += dppo_align16(4 * K * TD);
-    float* ta1 = (float*)(smem + o); o += dppo_align16(4 * K * 2 * TD);
     float* part = (float*)(smem + o); o += dppo_align16(4 * SW * 16 * NOC);
     float* sch = (float*)(smem + o); o += dppo_align16(4 * K * DPPO_SCHED_COLS);
     float* bias = (float*)(smem + o); o += dppo_align16(4 * 2 * (3 * H + NOC));  // [actor][in,l1,l2,out]
@@ -102,27 +128,11 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
         xs[i] = x;
         if (KF == K && a.chains && row < a.E) a.chains[((size_t)row * (KF + 1) + 0) * XD + q] = x;
     }
-    // time MLP (mlp_diffusion.py:40-45): SinusoidalPosEmb -> Dense(TD->2TD, mish) -> Dense(2TD->TD)
-    const int half = TD / 2;
-    const float lnf = logf(10000.f) / (float)(half - 1);
-    for (int i = tid; i < K * 2 * TD; i += ST) {
-        const int t = i / (2 * TD), j = i % (2 * TD);
-        const float* tw = (const float*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIME]);
-        float acc = tw[TD * 2 * TD + j];
-        for (int k = 0; k < TD; ++k) {
-            const float f = expf(-(float)(k % half) * lnf) * (float)t;
-            acc += (k < half ? sinf(f) : cosf(f)) * tw[k * 2 * TD + j];
-        }
-        ta1[i] = mishf(acc);
-    }
-    __syncthreads();
+    // time embeddings t_emb(t) (mlp_diffusion.py:40-45) of the actor each step uses, from the
+    // table the pack step derived (dppo_layout.h SEG_TEMB)
     for (int i = tid; i < K * TD; i += ST) {
-        const int t = i / TD, j = i % TD;
-        const float* tw = (const float*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIME]);
-        const float* w2 = tw + TD * 2 * TD + 2 * TD;  // [2TD][TD]
-        float acc = w2[2 * TD * TD + j];
-        for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + j];
-        temb[i] = acc;
+        const int t = i / TD;
+        temb[i] = ((const float*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TEMB]))[i];
     }
     // a pre-enqueued step waits here (everything above does not depend on the observation) for
     // the host to publish it; bounded: ~4 s, then the step runs on whatever is in the buffer and
@@ -147,35 +157,40 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
         if (a.cond_out && row < a.E) a.cond_out[(size_t)row * SD + c] = v;
     }
     __syncthreads();
+    // a0 = [x, temb(t), state, 0-pad] for step 0 (t = K-1); later steps get x and temb from the
+    // DDPM epilogue of the step before, the state part never changes
+    for (int idx = tid; idx < 16 * k1w; idx += ST) {
+        const int r = idx / k1w, c = idx % k1w;
+        float v = 0.f;
+        if (c < XD) v = xs[r * XD + c];
+        else if (c < XD + TD) v = temb[(K - 1) * TD + c - XD];
+        else if (c < a.IN) v = st[r * SD + c - XD - TD];
+        a0[r * lda0 + c] = P::cvt(v);
+    }
+    __syncthreads();
 
     const int ntile0 = wave * NT;
     const __amdgpu_buffer_rsrc_t rs_base = packed_rsrc(a.packed_base), rs_ft = packed_rsrc(a.packed_ft);
-    auto W = [&](const uint8_t* PK, int seg) { return wsrc(PK == a.packed_ft ? rs_ft : rs_base, L.off[seg]); };
+    // actor selection is wave-uniform: keep it scalar (readfirstlane), or hipcc may treat the buffer
+    // resource as divergent and wrap every weight load in a waterfall loop
+    auto W = [&](int ft, int seg) { return wsrc(ft ? rs_ft : rs_base, L.off[seg]); };
     // the stream starts with step 0's in-layer (t = K-1)
     // the weight stream: a QD-deep queue per wave, primed with step 0's in-layer (t = K-1)
     WQueue<QD, NT> R;
     {
-        const uint8_t* PK0 = K - 1 < KF ? a.packed_ft : a.packed_base;
-        queue_prime(R, W(PK0, SEG_W_IN), KSI, NextLayers{W(PK0, SEG_W_L1), KSH, W(PK0, SEG_W_L2), KSH}, ntile0, lane);
+        const int ft0 = __builtin_amdgcn_readfirstlane(K - 1 < KF ? 1 : 0);
+        queue_prime(R, W(ft0, SEG_W_IN), KSI, NextLayers{W(ft0, SEG_W_L1), KSH, W(ft0, SEG_W_L2), KSH}, ntile0, lane);
     }
     for (int i = 0; i < K; ++i) {
+        SPHASE(0);
         const int t = K - 1 - i;
         const int is_ft = t < KF;
-        const uint8_t* PK = is_ft ? a.packed_ft : a.packed_base;
-        const uint8_t* PKn = (t - 1 >= 0 && t - 1 < KF) ? a.packed_ft : (t - 1 >= 0 ? a.packed_base : PK);
+        const int PK = __builtin_amdgcn_readfirstlane(is_ft);
+        const int PKn = __builtin_amdgcn_readfirstlane(t - 1 >= 0 ? (t - 1 < KF ? 1 : 0) : is_ft);
         const float* bb = bias + is_ft * (3 * H + NOC);
         ORing<NOK, NO> ob;                                 // out-layer fragments, consumed 3 layers later
         out_prefetch<NOK, NO, SW>(ob, W(PK, SEG_W_OUT), L.ks_h, wave, lane);
-        // a) a0 = [x, temb(t), state, 0-pad]
-        for (int idx = tid; idx < 16 * k1w; idx += ST) {
-            const int r = idx / k1w, c = idx % k1w;
-            float v = 0.f;
-            if (c < XD) v = xs[r * XD + c];
-            else if (c < XD + TD) v = temb[t * TD + c - XD];
-            else if (c < a.IN) v = st[r * SD + c - XD - TD];
-            a0[r * lda0 + c] = P::cvt(v);
-        }
-        lds_sync();
+        SPHASE(1);
         // b) in-Dense: h1 = a0 W_in + b_in  (no activation after the input layer, mlp.py:144)
         f32x4 h1[1][NT], acc[1][NT];
         gemm_queue<P, 1, NT, KSI, QD>(a0, lda0, W(PK, SEG_W_IN), ntile0, h1, lane, R,
@@ -191,6 +206,7 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
             }
         }
         lds_sync();
+        SPHASE(2);
         // c) l1: relu(h1) W_l1 + b -> relu -> tB   (pre-activation block, mlp.py:192-193,202-203)
         gemm_queue<P, 1, NT, KSH, QD>(tA, ldh, W(PK, SEG_W_L1), ntile0, acc, lane, R,
                                       NextLayers{W(PK, SEG_W_L2), KSH, W(PKn, SEG_W_IN), KSI});
@@ -202,6 +218,7 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
             for (int r = 0; r < 4; ++r) tB[crow(lane, r) * ldh + col] = P::cvt(fmaxf(acc[0][n][r] + bv, 0.f));
         }
         lds_sync();
+        SPHASE(3);
         // d) l2: relu(h2) W_l2 + b + h1 (residual, mlp.py:206) -> tA; the stream moves on to the
         //    next denoising step's in-layer (possibly the other actor)
         gemm_queue<P, 1, NT, KSH, QD>(tB, ldh, W(PK, SEG_W_L2), ntile0, acc, lane, R,
@@ -214,6 +231,7 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
             for (int r = 0; r < 4; ++r) tA[crow(lane, r) * ldh + col] = P::cvt(acc[0][n][r] + bv + h1[0][n][r]);
         }
         lds_sync();
+        SPHASE(4);
         // e) out-Dense (N = XD <= 16*NO): k split over the 8 waves, partials through LDS
         {
             f32x4 po[1][NO];
@@ -225,6 +243,7 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
                     part[(wave * 16 + crow(lane, r)) * NOC + n * 16 + ccol(lane)] = po[0][n][r];
         }
         lds_sync();
+        SPHASE(5);
         // f) DDPM epilogue, fp32 (diffusion_vpg.py:198-243, 301-320)
         if (tid < 16 * XD) {
             const int r = tid / XD, q = tid % XD, row = row0 + r;
@@ -243,6 +262,7 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
             float xn = mu + sd * zt[i * 16 * XD + tid];
             if (a.final_clip > 0.f && i == K - 1) xn = fminf(fmaxf(xn, -a.final_clip), a.final_clip);
             xs[tid] = xn;
+            a0[r * lda0 + q] = P::cvt(xn);                      // next step's input
             if (row < a.E) {
                 if (a.chains && t <= KF) a.chains[((size_t)row * (KF + 1) + (KF - t)) * XD + q] = xn;
                 if (i == K - 1) {
@@ -250,8 +270,14 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
                     if (a.actions_host) a.actions_host[(size_t)row * XD + q] = xn;
                 }
             }
+        } else if (t > 0) {                                     // the next step's time embedding
+            for (int e = tid - 16 * XD; e < 16 * TD; e += ST - 16 * XD) {
+                const int r = e / TD, c = e % TD;
+                a0[r * lda0 + XD + c] = P::cvt(temb[(t - 1) * TD + c]);
+            }
         }
         lds_sync();
+        SPHASE(6);
     }
     if (a.done) {   // publish: every writer's stores reach the system before the counter moves
         __threadfence_system();
@@ -272,7 +298,6 @@ static size_t sample_lds_bytes(const SampleArgs& a, int NO) {
     o += dppo_align16(4 * 16 * a.XD);
     o += dppo_align16(4 * 16 * a.SD);
     o += dppo_align16(4 * a.K * a.TD);
-    o += dppo_align16(4 * a.K * 2 * a.TD);
     o += dppo_align16(4 * SW * 16 * 16 * NO);
     o += dppo_align16(4 * a.K * DPPO_SCHED_COLS);
     o += dppo_align16(4 * 2 * (3 * a.H + 16 * NO));
@@ -356,7 +381,7 @@ static int sample_impl(const dppo_dims* d, int precision, const void* packed_bas
     a.seed = seed; a.call_id = (uint32_t)call_id; a.E = n_envs; a.env_offset = env_offset;
     a.deterministic = deterministic; a.min_std = min_sampling_std; a.randn_clip = randn_clip; a.final_clip = final_clip;
     a.XD = D.XD; a.SD = D.SD; a.TD = D.TD; a.H = D.H; a.K = D.K; a.KF = D.KF; a.IN = D.IN;
-    a.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision);
+    a.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     hipStream_t s = (hipStream_t)stream;
     return precision == DPPO_BF16 ? dispatch_sample<PolicyBF16>(a, s) : dispatch_sample<PolicyF32>(a, s);
 }

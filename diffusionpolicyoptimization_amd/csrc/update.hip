@@ -298,34 +298,6 @@ __global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict_
     }
 }
 
-// time-MLP forward for t = 0..KF-1 (mlp_diffusion.py:40-45), once per minibatch; the same
-// arithmetic, in the same order, as the row-tile prologue's fallback path
-__global__ __launch_bounds__(256) void temb_kernel(const uint8_t* __restrict__ packed, size_t time_off, int TD, int KF,
-                                                   float* __restrict__ temb) {
-    __shared__ float ta1[16 * 128];
-    const int tid = threadIdx.x;
-    const int half = TD / 2;
-    const float lnf = logf(10000.f) / (float)(half - 1);
-    const float* tw = (const float*)(packed + time_off);
-    for (int i = tid; i < KF * 2 * TD; i += 256) {
-        const int t = i / (2 * TD), jj = i % (2 * TD);
-        float acc = tw[TD * 2 * TD + jj];
-        for (int k = 0; k < TD; ++k) {
-            const float f = expf(-(float)(k % half) * lnf) * (float)t;
-            acc += (k < half ? sinf(f) : cosf(f)) * tw[k * 2 * TD + jj];
-        }
-        ta1[i] = mishf(acc);
-    }
-    __syncthreads();
-    for (int i = tid; i < KF * TD; i += 256) {
-        const int t = i / TD, jj = i % TD;
-        const float* w2 = tw + TD * 2 * TD + 2 * TD;
-        float acc = w2[2 * TD * TD + jj];
-        for (int k = 0; k < 2 * TD; ++k) acc += ta1[t * 2 * TD + k] * w2[k * TD + jj];
-        temb[i] = acc;
-    }
-}
-
 // zero up to 4 byte ranges (4-B aligned, sizes multiple of 4) in one launch
 struct ZeroArgs { void* p[4]; size_t n[4]; };
 __global__ __launch_bounds__(256) void zero_kernel(ZeroArgs z) {
@@ -499,15 +471,12 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
 
     ActorArgs aa = {};
     aa.packed = (const uint8_t*)packed_ft;
-    aa.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision);
+    aa.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     aa.sched = sched; aa.obs = obs; aa.chains = chains;
     aa.XD = D.XD; aa.SD = D.SD; aa.TD = D.TD; aa.IN = D.IN; aa.H = D.H; aa.KF = D.KF; aa.Da = D.Da;
     aa.mode = ROWS_TRAIN; aa.nrows = rows; aa.fk = fk; aa.start = start; aa.row_index = row_index;
     aa.lp_old = lp_old_mean; aa.adv = advantages; aa.adv_stats = stats; aa.hp = lh; aa.ws = ws; aa.metrics = metrics;
-    hipLaunchKernelGGL(temb_kernel, dim3(1), dim3(256), 0, s, (const uint8_t*)packed_ft, aa.L.off[SEG_TIME], D.TD, D.KF,
-                       ws.temb);
-    DPPO_HIP(hipGetLastError());
-    aa.temb_g = ws.temb;
+
     CriticArgs ca = {};
     ca.packed = (const uint8_t*)packed_critic;
     ca.L = make_mlp_layout(D.SD, D.HC, 1, 0, precision);

@@ -43,8 +43,20 @@ def main():
     np.save(os.path.join(ROOT, "gpurun_out", f"sampler_{args.tag}.npy"), ref)
     d = m.dims
     flops = d.denoising_steps * 2 * (d.actor_in * d.actor_hidden + 2 * d.actor_hidden ** 2 + d.actor_hidden * d.xd) * args.envs
+    phases = None
+    from diffusionpolicyoptimization_amd import _lib
+    lib = _lib.load()
+    if hasattr(lib, "dppo_debug_sampler_cycles"):   # timing build: cycles per phase per denoising step
+        import ctypes
+        buf = (ctypes.c_ulonglong * 16)()
+        lib.dppo_debug_sampler_cycles(buf, 1)
+        m(cond)
+        torch.cuda.synchronize()
+        lib.dppo_debug_sampler_cycles(buf, 1)
+        wgs = (args.envs + 15) // 16
+        phases = {f"s{i}": round(buf[i] / wgs / (d.denoising_steps if i else 1)) for i in range(7)}
     print(json.dumps({"tag": args.tag, "envs": args.envs, "precision": args.precision, "ms_per_launch": ms,
-                      "tflops": flops / (ms * 1e-3) / 1e12}), flush=True)
+                      "tflops": flops / (ms * 1e-3) / 1e12, "cycles_per_step": phases}), flush=True)
 
 
 if __name__ == "__main__":
