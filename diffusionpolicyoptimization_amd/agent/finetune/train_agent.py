@@ -11,7 +11,7 @@ import torch.distributed as dist
 
 from ...env.gym_utils import make_async
 from ...util.config import instantiate
-from ...util.dist import shard_envs
+from ...util.dist import broadcast_, shard_envs
 
 log = logging.getLogger(__name__)
 
@@ -35,6 +35,8 @@ class TrainAgent:
         self.rank, self.world_size, self.local_rank = init_distributed()
         dev = str(cfg.get("device", "cuda:0"))
         self.device = torch.device(f"cuda:{self.local_rank}" if dev.startswith("cuda") else dev)
+        if dev.startswith("cuda") and os.environ.get("DPPO_SINGLE_DEVICE"):   # test rig: all ranks share cuda:0
+            self.device = torch.device("cuda:0")
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         self.seed = cfg.get("seed", 42)
@@ -71,7 +73,7 @@ class TrainAgent:
         self.model.set_rng(self.seed, env_offset=self.env_offset)
         if self.world_size > 1:  # identical replicas (same seed already; broadcast guards against drift)
             for t in (self.model.base_params, self.model.train_params):
-                dist.broadcast(t if self.device.type == "cuda" else t.cpu(), src=0)
+                broadcast_(t, src=0)
             self.model.repack()
 
         self.itr = 0

@@ -17,9 +17,30 @@ def world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+def _host_staged(t, group=None):
+    """gloo reduces host tensors; RCCL ("nccl") device tensors."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def allreduce_sum_(t, group=None):
     if world() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        if _host_staged(t, group):
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+def broadcast_(t, src=0, group=None):
+    if world() > 1:
+        if _host_staged(t, group):
+            h = t.cpu()
+            dist.broadcast(h, src=src, group=group)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, src=src, group=group)
     return t
 
 
@@ -50,6 +71,8 @@ def gather_moments(local, group=None):
     """All-gather a local (n, mean, M2) fp64 tensor and merge in rank order."""
     if world() == 1:
         return tuple(float(x) for x in local.cpu())
+    if _host_staged(local, group):
+        local = local.cpu()
     parts = [torch.zeros_like(local) for _ in range(world())]
     dist.all_gather(parts, local, group=group)
     return chan_merge([tuple(p.cpu().tolist()) for p in parts])

@@ -100,3 +100,23 @@ def test_pipelined_rollout_matches_model_call(cuda):
         np.testing.assert_array_equal(got[i], ref.trajectories.reshape(E, -1).cpu().numpy())
         np.testing.assert_array_equal(chains[i].cpu().numpy(), ref.chains.reshape(E, -1, d.xd).cpu().numpy())
     pipe.close()
+
+
+def test_data_parallel_agent_two_ranks_share_one_gpu(tmp_path):
+    """2 ranks (gloo, both on cuda:0) run the DP agent; replicas must stay bit-identical."""
+    import socket
+    import subprocess
+    import sys
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, DPPO_DIST_BACKEND="gloo", DPPO_SINGLE_DEVICE="1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(ROOT, "tools", "dist_smoke.py")],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "replicas_identical=True" in out.stdout
