@@ -33,6 +33,20 @@ def sampler_flops_per_env(d):
     return d.denoising_steps * 2 * macs
 
 
+CU_LOAD_PEAK_GBS = 64 * 2.4   # per-CU vector-memory (TA) path: 64 B/clk at the 2.4 GHz max clock
+
+
+def sampler_stream_bytes_per_tile(d, precision):
+    """Weight bytes ONE 16-row sampler tile (one CU) streams per launch: every denoising step reads
+    the in, l1, l2 and out images of its actor from L2 (dppo_layout.h fragment order)."""
+    kg = 32 if precision == "bf16" else 16
+    ks = lambda k: ((k + kg - 1) // kg + 1) & ~1
+    nt = lambda n: (n + 15) // 16
+    h = d.actor_hidden
+    per_step = (ks(d.actor_in) * nt(h) + 2 * ks(h) * nt(h) + ks(h) * nt(d.xd)) * 1024
+    return per_step * d.denoising_steps
+
+
 def cpu_baseline(cfg, n_envs, S, bs, seconds=12.0):
     """The oracle (float64 NumPy restatement) timed on a bounded sample on this host; extrapolated
     to one iteration of the same workload. kind = "port"."""
@@ -158,6 +172,7 @@ def main():
     env_steps = agent.n_envs_global * cfg.act_steps * cfg.train.n_steps * args.steps
     n_updates = agent.timing["n_updates"]
     flops = sampler_flops_per_env(d) * agent.n_envs
+    stream_b = sampler_stream_bytes_per_tile(d, agent.model.precision)
     achieved = flops / (samp_ms * 1e-3) / 1e12
     prec = agent.model.precision
     traffic = None
@@ -180,14 +195,19 @@ def main():
         "ppo_updates_per_sec": n_updates / elapsed,
         "rollout_env_steps_per_sec": env_steps / t_roll if t_roll > 0 else None,
         "rollout_s_per_iter": t_roll / args.steps, "update_s_per_iter": t_upd / args.steps,
+        "load_path": {"kernel": "sample_kernel", "bytes_per_cu_per_launch": stream_b,
+                      "achieved_GBs_per_cu": stream_b / (samp_ms * 1e-3) / 1e9, "peak_GBs_per_cu": CU_LOAD_PEAK_GBS,
+                      "frac": stream_b / (samp_ms * 1e-3) / 1e9 / CU_LOAD_PEAK_GBS,
+                      "note": "what bounds the sampler at 64 envs: each 16-row tile streams its actor's weights "
+                              "from L2 into one CU every denoising step (time is flat from 16 to 1024 envs)"},
         "roofline": {"bound": "mfma", "kernel": "sample_kernel (K-step DDPM sampler, all layers fused)",
                      "achieved": achieved, "peak": PEAK["bf16" if prec == "bf16" else "fp32"], "unit": "TFLOP/s",
                      "frac": achieved / PEAK["bf16" if prec == "bf16" else "fp32"], "traffic": traffic,
                      "avg_launch_ms": samp_ms, "flops_per_launch": flops, "burst_launches": n_burst,
-                     "in_loop_event_ms": loop_samp_ms, "in_loop_launches": len(agent.sampler_events),
+                     "in_loop_event_ms": loop_samp_ms if agent.sampler_events else None,
                      "note": ("M = envs/GPU rows per GEMM: at 64 rows the dependent 80-GEMM chain is bound by "
                               "streaming ~1.1 MB of bf16 weights per denoising step from L2 into one CU per "
-                              "16-row tile, not by MFMA issue; see DESIGN.md")},
+                              "16-row tile (load_path), not by MFMA issue; see DESIGN.md")},
         "ppo_minibatch_avg_ms": upd_ms,
     }
     if rank == 0 and not args.no_cpu_baseline:
