@@ -132,13 +132,21 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             pipe = self.pipe
             pipe.enqueue(0, eval_mode)
             pipe.publish()
+            gated = getattr(self.venv, "native", None) is not None   # wait + step + publish in C
             for step in range(S):
-                if step + 1 < S:
+                more = step + 1 < S
+                if more:
                     pipe.enqueue(step + 1, eval_mode)
-                pipe.wait()
-                _, reward, terminated, truncated, _ = self.venv.step(act_view, obs_out=obs_np)
-                if step + 1 < S:
-                    pipe.publish()
+                if gated:
+                    _, reward, terminated, truncated, _ = self.venv.step(act_view, obs_out=obs_np,
+                                                                         gate=pipe.gate(publish=more))
+                    if more:
+                        pipe.published_by_gate() if self.venv.published else pipe.publish()
+                else:
+                    pipe.wait()
+                    _, reward, terminated, truncated, _ = self.venv.step(act_view, obs_out=obs_np)
+                    if more:
+                        pipe.publish()
                 bookkeeping(step, reward, terminated, truncated)
             stream.synchronize()
         else:

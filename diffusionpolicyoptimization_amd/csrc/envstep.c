@@ -9,12 +9,13 @@
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
+#include <time.h>
 
 #define DPPO_ENV_API __attribute__((visibility("default")))
 #define EB 16
 #define MAXD 64
 
-DPPO_ENV_API int dppo_env_abi(void) { return 2; }
+DPPO_ENV_API int dppo_env_abi(void) { return 3; }
 
 typedef double v4d __attribute__((vector_size(32)));
 #define NV (EB / 4)
@@ -94,6 +95,47 @@ DPPO_ENV_API int dppo_env_step(int E, int Do, int Da, int act_steps, int Ta, int
             for (int o = 0; o < n_obs_steps; ++o)
                 for (int j = 0; j < Do; ++j) obs_out[((size_t)e * n_obs_steps + o) * Do + j] = (float)s[j][b >> 2][b & 3];
         }
+    }
+    return n_done;
+}
+
+static double env_now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+/* One step of the pipelined rollout (ops.RolloutPipe) with the host's critical path in C: spin
+ * until the device's done counter reaches done_target (the sampler wrote this step's actions into
+ * the mapped action buffer), step the envs, and — when no episode ended, so no host-side reset
+ * still has to rewrite observations — publish go_value to the go counter, releasing the
+ * pre-enqueued sampler launch of the next step. go == NULL: never publish (the last step).
+ * Returns n_done, with DPPO_ENV_PUBLISHED or'ed in when go was published; -1 host timeout;
+ * -2 the device flagged that its own wait for go timed out. */
+#define DPPO_ENV_PUBLISHED (1 << 30)
+DPPO_ENV_API int dppo_env_step_gated(int E, int Do, int Da, int act_steps, int Ta, int max_steps, int n_obs_steps,
+                                     const double* AT, const double* B, const double* c, const double* goal,
+                                     double* state, int64_t* cnt, const float* actions, double* reward,
+                                     uint8_t* terminated, uint8_t* truncated, float* obs_out,
+                                     const volatile uint32_t* done, uint32_t done_target, volatile uint32_t* go,
+                                     uint32_t go_value, double timeout_s) {
+    double t_end = -1.0;
+    for (uint32_t spins = 0;; ++spins) {
+        const uint32_t v = __atomic_load_n(done, __ATOMIC_ACQUIRE);
+        if (v & 0x80000000u) return -2;
+        if (v >= done_target) break;
+        _mm_pause();
+        if ((spins & 1023u) == 1023u) {
+            const double now = env_now_s();
+            if (t_end < 0.0) t_end = now + timeout_s;
+            else if (now > t_end) return -1;
+        }
+    }
+    const int n_done = dppo_env_step(E, Do, Da, act_steps, Ta, max_steps, n_obs_steps, AT, B, c, goal, state, cnt,
+                                     actions, reward, terminated, truncated, obs_out);
+    if (n_done == 0 && go) {
+        __atomic_store_n(go, go_value, __ATOMIC_RELEASE);   /* x86: the obs stores are visible first */
+        return DPPO_ENV_PUBLISHED;
     }
     return n_done;
 }

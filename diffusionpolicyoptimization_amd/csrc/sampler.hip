@@ -63,17 +63,96 @@ struct SampleArgs {
     MlpLayout L;          // same layout for base and ft
 };
 
-// 16 waves per workgroup: each wave streams NT = H/256 n-tiles, so a CU keeps twice the weight
-// fragments in flight of an 8-wave layout at the same ring depth.
-#define SW 16
-#define ST (SW * 64)
+// ---- the sampler's weight stream with resident fragments ----
+// A CU streams its actor's weights from L2 every denoising step, and its vector-memory path
+// (64 B/clk) is what bounds the kernel. Fragments that fit in the register file
+// beside the working set are loaded once per actor instead ("resident"): the in-layer, the
+// out-layer and the first RK k-steps of both hidden layers. Only the rest streams through the
+// QD-deep queue. A streamed segment is {W: matrix offset advanced past its resident k-steps,
+// KSF: the matrix's k-step count (the n-tile stride), KS: k-steps streamed}.
+struct SSeg {
+    WSrc W;
+    int KSF, KS;
+};
+struct SNext {
+    SSeg s1, s2;   // the two streamed segments after the current one
+};
+__device__ inline SSeg sseg(WSrc W, int KSF, int k0) { return SSeg{WSrc{W.rsrc, W.off + ((uint32_t)k0 << 10)}, KSF, KSF - k0}; }
 
-template <class P, int NT, int NO, int KSI, bool INJ, int QD>
-__global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
+template <int KS>
+__device__ inline u32x4 sfrag(WSrc W, int KSF, const SNext& nx, int ntile, int j, int lane) {
+    if (j < KS) return load_bfrag_c(W, KSF, ntile, j, lane);                 // compile-time branch
+    const int j1 = j - KS;
+    const bool first = j1 < nx.s1.KS;                                         // wave-uniform
+    return first ? load_bfrag_c(nx.s1.W, nx.s1.KSF, ntile, j1, lane)
+                 : load_bfrag_c(nx.s2.W, nx.s2.KSF, ntile, j1 - nx.s1.KS, lane);
+}
+
+template <int D, int NT>
+__device__ inline void squeue_prime(WQueue<D, NT>& Q, const SSeg& s0, const SNext& nx, int ntile0, int lane) {
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int j = d;
+            if (j < s0.KS) Q.b[d][n] = load_bfrag_c(s0.W, s0.KSF, ntile0 + n, j, lane);
+            else if (j - s0.KS < nx.s1.KS) Q.b[d][n] = load_bfrag_c(nx.s1.W, nx.s1.KSF, ntile0 + n, j - s0.KS, lane);
+            else Q.b[d][n] = load_bfrag_c(nx.s2.W, nx.s2.KSF, ntile0 + n, j - s0.KS - nx.s1.KS, lane);
+        }
+}
+
+// acc = A[16 rows][KSF*KG] x W[:, ntile0*16 ..): k-steps [0, RKL) from the resident fragments
+// (computed first: they cover the latency of the queue's first loads after the layer barrier),
+// k-steps [RKL, KSF) from the queue, which keeps D k-steps of look-ahead into the next segments.
+// k-steps [RKL, RKL+LKL) come from fragments kept in LDS (lw: [LKL][NTOT n-tiles][64 lanes] x 16 B).
+template <class P, int NT, int KSF, int RKL, int LKL, int NTOT, int D>
+__device__ inline void gemm_res(const typename P::AT* A, int lda, WSrc Ws, const u32x4 (*res)[NT], const u32x4* lw,
+                                int ntile0, f32x4 (&acc)[1][NT], int lane, WQueue<D, NT>& Q, const SNext& nx) {
+    constexpr int KS = KSF - RKL - LKL;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) zero_acc(acc[0][n]);
+#pragma unroll
+    for (int ks = 0; ks < RKL; ++ks) {
+        const u32x4 a = lds_afrag<P>(A, lda, 0, ks, lane);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[0][n] = P::mma(a, res[ks][n], acc[0][n]);
+    }
+#pragma unroll
+    for (int kl = 0; kl < LKL; ++kl) {
+        const u32x4 a = lds_afrag<P>(A, lda, 0, RKL + kl, lane);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[0][n] = P::mma(a, lw[(kl * NTOT + ntile0 + n) * 64 + lane], acc[0][n]);
+    }
+#pragma unroll
+    for (int j = 0; j < KS; ++j) {
+        u32x4 c[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) c[n] = Q.b[0][n];
+#pragma unroll
+        for (int d = 0; d + 1 < D; ++d)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) Q.b[d][n] = Q.b[d + 1][n];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) Q.b[D - 1][n] = sfrag<KS>(Ws, KSF, nx, ntile0 + n, j + D, lane);
+        const u32x4 a = lds_afrag<P>(A, lda, 0, RKL + LKL + j, lane);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[0][n] = P::mma(a, c[n], acc[0][n]);
+    }
+}
+
+// SW waves per workgroup, each owning NT = H/(16*SW) n-tiles of every hidden layer. RK hidden
+// k-steps and (RIO) the whole in- and out-layers are resident in registers, LK more hidden
+// k-steps in LDS; QD k-steps of the rest in flight.
+template <class P, int NT, int NO, int KSI, bool INJ, int QD, int SW, int RK, int LK, bool RIO>
+__global__ __launch_bounds__(SW * 64) void sample_kernel(SampleArgs a) {
     SPHASE_START;
     using AT = typename P::AT;
+    constexpr int ST = SW * 64;
     constexpr int KSH = ksh_for<P>(NT, SW);
     constexpr int NOK = KSH / SW;
+    constexpr int RKI = RIO ? KSI : 0;       // resident in-layer k-steps
+    constexpr int NTOT = NT * SW;            // n-tiles of a hidden layer
+    static_assert(RK + LK < KSH, "at least one streamed hidden k-step");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int row0 = blockIdx.x * 16;
@@ -98,6 +177,55 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
     float* sch = (float*)(smem + o); o += dppo_align16(4 * K * DPPO_SCHED_COLS);
     float* bias = (float*)(smem + o); o += dppo_align16(4 * 2 * (3 * H + NOC));  // [actor][in,l1,l2,out]
     float* zt = (float*)(smem + o); o += dppo_align16(4 * K * 16 * XD);           // clipped noise [i][row][q]
+    u32x4* lw1 = (u32x4*)(smem + o); o += (size_t)LK * NTOT * 1024;                // LDS-resident hidden k-steps
+    u32x4* lw2 = (u32x4*)(smem + o); o += (size_t)LK * NTOT * 1024;
+
+    const int ntile0 = wave * NT;
+    const __amdgpu_buffer_rsrc_t rs_base = packed_rsrc(a.packed_base), rs_ft = packed_rsrc(a.packed_ft);
+    // actor selection is wave-uniform: keep it scalar (readfirstlane), or hipcc may treat the buffer
+    // resource as divergent and wrap every weight load in a waterfall loop
+    auto W = [&](int ft, int seg) { return wsrc(ft ? rs_ft : rs_base, L.off[seg]); };
+    // the streamed segments of a denoising step: [in (unless resident)], l1[RK..], l2[RK..]
+    auto s_in = [&](int ft) { return sseg(W(ft, SEG_W_IN), KSI, 0); };
+    auto s_l1 = [&](int ft) { return sseg(W(ft, SEG_W_L1), KSH, RK + LK); };
+    auto s_l2 = [&](int ft) { return sseg(W(ft, SEG_W_L2), KSH, RK + LK); };
+    // hidden k-steps [RK, RK+LK) of both hidden layers into LDS, [k][n-tile][lane] (callers barrier)
+    auto load_lds = [&](int ft) {
+        const WSrc w1 = W(ft, SEG_W_L1), w2 = W(ft, SEG_W_L2);
+        for (int c = tid; c < LK * NTOT * 64; c += ST) {
+            const int kl = c / (NTOT * 64), nt = (c / 64) % NTOT, ln = c % 64;
+            const uint32_t so = (uint32_t)(nt * KSH + RK + kl) << 10;
+            lw1[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(w1.rsrc, ln << 4, w1.off + so, 0));
+            lw2[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(w2.rsrc, ln << 4, w2.off + so, 0));
+        }
+    };
+
+    // resident fragments of the actor in use (reloaded when the actor changes, once per launch)
+    u32x4 r_in[RKI > 0 ? RKI : 1][NT], r_l1[RK > 0 ? RK : 1][NT], r_l2[RK > 0 ? RK : 1][NT];
+    ORing<NOK, NO> r_out;
+    auto load_resident = [&](int ft) {
+#pragma unroll
+        for (int k = 0; k < RKI; ++k)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) r_in[k][n] = load_bfrag_c(W(ft, SEG_W_IN), KSI, ntile0 + n, k, lane);
+#pragma unroll
+        for (int k = 0; k < RK; ++k)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                r_l1[k][n] = load_bfrag_c(W(ft, SEG_W_L1), KSH, ntile0 + n, k, lane);
+                r_l2[k][n] = load_bfrag_c(W(ft, SEG_W_L2), KSH, ntile0 + n, k, lane);
+            }
+        if constexpr (RIO) out_prefetch<NOK, NO, SW>(r_out, W(ft, SEG_W_OUT), L.ks_h, wave, lane);
+    };
+    // the weight stream starts with step 0 (t = K-1); its first loads and the resident set go out
+    // before anything waits (noise, the host's observation)
+    const int ft0 = __builtin_amdgcn_readfirstlane(K - 1 < KF ? 1 : 0);
+    WQueue<QD, NT> R;
+    if constexpr (RIO) squeue_prime(R, s_l1(ft0), SNext{s_l2(ft0), s_l1(ft0)}, ntile0, lane);
+    else squeue_prime(R, s_in(ft0), SNext{s_l1(ft0), s_l2(ft0)}, ntile0, lane);
+    load_resident(ft0);
+    if constexpr (LK > 0) load_lds(ft0);      // made visible by the prologue's barriers
+    int cur = ft0;
 
     // ---- prologue: schedule, biases, state, x_T, time-embedding table ----
     for (int i = tid; i < K * DPPO_SCHED_COLS; i += ST) sch[i] = a.sched[i];
@@ -139,10 +267,10 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
     // flags the timeout in the high bit of *done so the host reports it
     if (a.go) {
         if (tid == 0) {
-            uint32_t spins = 0;
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;   // 100 MHz clock: 4 s
             while (__hip_atomic_load(a.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
-                __builtin_amdgcn_s_sleep(64);
-                if (++spins == (1u << 22)) {
+                __builtin_amdgcn_s_sleep(8);
+                if (__builtin_amdgcn_s_memrealtime() > t_end) {
                     __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
@@ -169,32 +297,33 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
     }
     __syncthreads();
 
-    const int ntile0 = wave * NT;
-    const __amdgpu_buffer_rsrc_t rs_base = packed_rsrc(a.packed_base), rs_ft = packed_rsrc(a.packed_ft);
-    // actor selection is wave-uniform: keep it scalar (readfirstlane), or hipcc may treat the buffer
-    // resource as divergent and wrap every weight load in a waterfall loop
-    auto W = [&](int ft, int seg) { return wsrc(ft ? rs_ft : rs_base, L.off[seg]); };
-    // the stream starts with step 0's in-layer (t = K-1)
-    // the weight stream: a QD-deep queue per wave, primed with step 0's in-layer (t = K-1)
-    WQueue<QD, NT> R;
-    {
-        const int ft0 = __builtin_amdgcn_readfirstlane(K - 1 < KF ? 1 : 0);
-        queue_prime(R, W(ft0, SEG_W_IN), KSI, NextLayers{W(ft0, SEG_W_L1), KSH, W(ft0, SEG_W_L2), KSH}, ntile0, lane);
-    }
     for (int i = 0; i < K; ++i) {
         SPHASE(0);
         const int t = K - 1 - i;
         const int is_ft = t < KF;
         const int PK = __builtin_amdgcn_readfirstlane(is_ft);
         const int PKn = __builtin_amdgcn_readfirstlane(t - 1 >= 0 ? (t - 1 < KF ? 1 : 0) : is_ft);
+        if (PK != cur) {                                    // the actor switch (t = K'-1): once per launch
+            load_resident(PK);
+            if constexpr (LK > 0) {
+                load_lds(PK);
+                __syncthreads();
+            }
+            cur = PK;
+        }
         const float* bb = bias + is_ft * (3 * H + NOC);
         ORing<NOK, NO> ob;                                 // out-layer fragments, consumed 3 layers later
-        out_prefetch<NOK, NO, SW>(ob, W(PK, SEG_W_OUT), L.ks_h, wave, lane);
+        if constexpr (RIO) ob = r_out;
+        else out_prefetch<NOK, NO, SW>(ob, W(PK, SEG_W_OUT), L.ks_h, wave, lane);
         SPHASE(1);
         // b) in-Dense: h1 = a0 W_in + b_in  (no activation after the input layer, mlp.py:144)
         f32x4 h1[1][NT], acc[1][NT];
-        gemm_queue<P, 1, NT, KSI, QD>(a0, lda0, W(PK, SEG_W_IN), ntile0, h1, lane, R,
-                                      NextLayers{W(PK, SEG_W_L1), KSH, W(PK, SEG_W_L2), KSH});
+        if constexpr (RIO)
+            gemm_res<P, NT, KSI, KSI, 0, NTOT, QD>(a0, lda0, W(PK, SEG_W_IN), r_in, nullptr, ntile0, h1, lane, R,
+                                                   SNext{s_l1(PK), s_l2(PK)});
+        else
+            gemm_res<P, NT, KSI, 0, 0, NTOT, QD>(a0, lda0, s_in(PK).W, r_in, nullptr, ntile0, h1, lane, R,
+                                                 SNext{s_l1(PK), s_l2(PK)});
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int col = (ntile0 + n) * 16 + ccol(lane);
@@ -208,8 +337,8 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
         lds_sync();
         SPHASE(2);
         // c) l1: relu(h1) W_l1 + b -> relu -> tB   (pre-activation block, mlp.py:192-193,202-203)
-        gemm_queue<P, 1, NT, KSH, QD>(tA, ldh, W(PK, SEG_W_L1), ntile0, acc, lane, R,
-                                      NextLayers{W(PK, SEG_W_L2), KSH, W(PKn, SEG_W_IN), KSI});
+        gemm_res<P, NT, KSH, RK, LK, NTOT, QD>(tA, ldh, s_l1(PK).W, r_l1, lw1, ntile0, acc, lane, R,
+                                     RIO ? SNext{s_l2(PK), s_l1(PKn)} : SNext{s_l2(PK), s_in(PKn)});
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int col = (ntile0 + n) * 16 + ccol(lane);
@@ -220,9 +349,9 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
         lds_sync();
         SPHASE(3);
         // d) l2: relu(h2) W_l2 + b + h1 (residual, mlp.py:206) -> tA; the stream moves on to the
-        //    next denoising step's in-layer (possibly the other actor)
-        gemm_queue<P, 1, NT, KSH, QD>(tB, ldh, W(PK, SEG_W_L2), ntile0, acc, lane, R,
-                                      NextLayers{W(PKn, SEG_W_IN), KSI, W(PKn, SEG_W_L1), KSH});
+        //    next denoising step (possibly the other actor)
+        gemm_res<P, NT, KSH, RK, LK, NTOT, QD>(tB, ldh, s_l2(PK).W, r_l2, lw2, ntile0, acc, lane, R,
+                                     RIO ? SNext{s_l1(PKn), s_l2(PKn)} : SNext{s_in(PKn), s_l1(PKn)});
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int col = (ntile0 + n) * 16 + ccol(lane);
@@ -232,7 +361,7 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
         }
         lds_sync();
         SPHASE(4);
-        // e) out-Dense (N = XD <= 16*NO): k split over the 8 waves, partials through LDS
+        // e) out-Dense (N = XD <= 16*NO): k split over the waves, partials through LDS
         {
             f32x4 po[1][NO];
             gemm_narrow_pre<P, 1, NOK, NO, SW>(tA, ldh, ob, po, wave, lane);
@@ -287,7 +416,7 @@ __global__ __launch_bounds__(ST) void sample_kernel(SampleArgs a) {
 }
 
 template <class P>
-static size_t sample_lds_bytes(const SampleArgs& a, int NO) {
+static size_t sample_lds_bytes(const SampleArgs& a, int NO, int SW, int LK) {
     using AT = typename P::AT;
     const int pad = lds_pad_elems<P>();
     const int ldh = a.H + pad;
@@ -302,38 +431,47 @@ static size_t sample_lds_bytes(const SampleArgs& a, int NO) {
     o += dppo_align16(4 * a.K * DPPO_SCHED_COLS);
     o += dppo_align16(4 * 2 * (3 * a.H + 16 * NO));
     o += dppo_align16(4 * a.K * 16 * a.XD);
+    o += (size_t)2 * LK * (a.H / 16) * 1024;
     return o;
 }
 
-template <class P, int NT, int NO, int KSI, bool INJ, int QD>
+template <class P, int NT, int NO, int KSI, bool INJ, int QD, int SW, int RK, int LK, bool RIO>
 static int launch_sample_q(const SampleArgs& a, hipStream_t s) {
     if (a.L.ks_h != ksh_for<P>(NT, SW) || a.L.ks_in != KSI || a.L.ks_h % SW != 0)
         return dppo_set_error(DPPO_EUNSUPPORTED, "sampler: hidden %d not supported at this precision", a.H);
-    const size_t lds = sample_lds_bytes<P>(a, NO);
+    const size_t lds = sample_lds_bytes<P>(a, NO, SW, LK);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "sampler needs %zu B of LDS", lds);
-    auto k = sample_kernel<P, NT, NO, KSI, INJ, QD>;
+    auto k = sample_kernel<P, NT, NO, KSI, INJ, QD, SW, RK, LK, RIO>;
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k, dim3(dppo_cdiv(a.E, 16)), dim3(ST), lds, s, a);
+    hipLaunchKernelGGL(k, dim3(dppo_cdiv(a.E, 16)), dim3(SW * 64), lds, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
 
-// weight-queue depth (k-steps in flight per wave): DPPO_SAMPLER_QD = 2 | 3 | 4 (measurement knob)
-static int sampler_queue_depth() {
-    static int qd = [] {
-        const char* e = getenv("DPPO_SAMPLER_QD");
-        const int v = e ? atoi(e) : 3;
-        return v >= 2 && v <= 4 ? v : 3;
+// Sampler geometry (measurement knob DPPO_SAMPLER_CFG, default "s"):
+//   "s": 16 waves, nothing resident, QD 3 (the streaming-only layout)
+//   "r": 8 waves, in/out layers + 2 hidden k-steps resident, QD 3 (bf16 H = 512)
+//   "l": "r" + 1 more hidden k-step per layer in LDS; "m", "q", "i", "e": fewer resident
+static char sampler_cfg() {
+    static char c = [] {
+        const char* e = getenv("DPPO_SAMPLER_CFG");
+        return e && e[0] ? e[0] : 's';
     }();
-    return qd;
+    return c;
 }
 
-template <class P, int NT, int NO, int KSI, bool INJ>
+template <class P, int NT16, int NO, int KSI, bool INJ>
 static int launch_sample_k(const SampleArgs& a, hipStream_t s) {
-    const int qd = sampler_queue_depth();
-    if (qd == 2) return launch_sample_q<P, NT, NO, KSI, INJ, 2>(a, s);
-    if (qd == 4) return launch_sample_q<P, NT, NO, KSI, INJ, 4>(a, s);
-    return launch_sample_q<P, NT, NO, KSI, INJ, 3>(a, s);
+    if constexpr (P::KG == 32 && NT16 == 2) {   // bf16, H = 512
+        const char c = sampler_cfg();
+        if (c == 'r') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 0, true>(a, s);
+        if (c == 'l') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 1, true>(a, s);
+        if (c == 'm') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 1, true>(a, s);
+        if (c == 'q') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 0, true>(a, s);
+        if (c == 'i') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, true>(a, s);
+        if (c == 'e') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, false>(a, s);
+    }
+    return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, false>(a, s);
 }
 
 template <class P, int NT, int NO, int KSI>
@@ -344,12 +482,12 @@ static int launch_sample(const SampleArgs& a, hipStream_t s) {
 
 template <class P>
 static int dispatch_sample(const SampleArgs& a, hipStream_t s) {
-    const int NT = a.H / (16 * SW);
+    const int NT = a.H / (16 * 16);   // n-tiles per wave of the 16-wave layout
     const int NO = dppo_cdiv(a.XD, 16);
     const int KSI = a.L.ks_in;
 #define DPPO_SAMPLE_CASE(nt, no, ksi) \
     if (NT == nt && NO == no && KSI == ksi) return launch_sample<P, nt, no, ksi>(a, s);
-    if constexpr (P::KG == 32) {   // bf16: H = 512 (NT 2) or 256 (NT 1)
+    if constexpr (P::KG == 32) {   // bf16: H = 512 (NT 2)
         DPPO_SAMPLE_CASE(2, 1, 2) DPPO_SAMPLE_CASE(2, 2, 2) DPPO_SAMPLE_CASE(2, 1, 4) DPPO_SAMPLE_CASE(2, 2, 4)
     } else {                       // fp32: H = 512 or 256
         DPPO_SAMPLE_CASE(2, 1, 4) DPPO_SAMPLE_CASE(2, 2, 4) DPPO_SAMPLE_CASE(1, 1, 4) DPPO_SAMPLE_CASE(1, 2, 4)

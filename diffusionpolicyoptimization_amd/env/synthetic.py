@@ -27,6 +27,9 @@ def _native():
         P = ctypes.c_void_p
         lib.dppo_env_step.argtypes = [ctypes.c_int] * 7 + [P] * 11
         lib.dppo_env_step.restype = ctypes.c_int
+        lib.dppo_env_step_gated.argtypes = [ctypes.c_int] * 7 + [P] * 11 + [P, ctypes.c_uint32, P, ctypes.c_uint32,
+                                                                            ctypes.c_double]
+        lib.dppo_env_step_gated.restype = ctypes.c_int
         _lib = lib
     return _lib
 
@@ -85,9 +88,17 @@ class SyntheticLocomotionVecEnv:
         self.cnt[env_ind] = 0
         return {"state": np.repeat(self.state[env_ind][None], self.n_obs_steps, axis=0)}
 
-    def step(self, actions, obs_out=None):
-        """actions [E, Ta, Da]; obs_out: optional float32 [E, To, Do] buffer (e.g. pinned staging)."""
+    _PUBLISHED = 1 << 30
+
+    def step(self, actions, obs_out=None, gate=None):
+        """actions [E, Ta, Da]; obs_out: optional float32 [E, To, Do] buffer (e.g. pinned staging).
+        gate: (done_addr, done_target, go_addr, go_value) of a pipelined rollout (ops.RolloutPipe.gate):
+        the native stepper waits for the device's done counter, steps, and publishes go itself when
+        no env needs a reset; self.published tells the caller whether it did."""
         E = self.num_envs
+        self.published = False
+        if gate is not None and self.native is None:
+            raise RuntimeError("gated env steps need the native stepper (lib/libdppo_env.so)")
         if self.native is not None:
             a = actions if (isinstance(actions, np.ndarray) and actions.dtype == np.float32
                             and actions.flags.c_contiguous) else np.ascontiguousarray(actions, dtype=np.float32)
@@ -103,9 +114,19 @@ class SyntheticLocomotionVecEnv:
                 self._last_a, self._last_pa = a, _p(a)
             if out is not self._last_o:
                 self._last_o, self._last_po = out, _p(out)
-            n_done = self.native.dppo_env_step(E, self.obs_dim, self.action_dim, self.act_steps, ta,
-                                               self.max_episode_steps, self.n_obs_steps, *self._static_ptrs,
-                                               self._last_pa, *self._tail_ptrs, self._last_po)
+            if gate is None:
+                n_done = self.native.dppo_env_step(E, self.obs_dim, self.action_dim, self.act_steps, ta,
+                                                   self.max_episode_steps, self.n_obs_steps, *self._static_ptrs,
+                                                   self._last_pa, *self._tail_ptrs, self._last_po)
+            else:
+                rc = self.native.dppo_env_step_gated(E, self.obs_dim, self.action_dim, self.act_steps, ta,
+                                                     self.max_episode_steps, self.n_obs_steps, *self._static_ptrs,
+                                                     self._last_pa, *self._tail_ptrs, self._last_po, *gate)
+                if rc < 0:
+                    raise RuntimeError("pipelined rollout: " + ("the device's wait for the observation timed out"
+                                                                if rc == -2 else "the sampler step did not finish"))
+                self.published = bool(rc & self._PUBLISHED)
+                n_done = rc & (self._PUBLISHED - 1)
             reward = self._reward.copy()
             terminated, truncated = self._term.astype(bool), self._trunc.astype(bool)
         else:

@@ -256,6 +256,18 @@ class RolloutPipe:
         self.published += 1
         self._go[0] = self.published          # x86 stores are ordered: the observation is visible first
 
+    def gate(self, publish, timeout_s=30.0):
+        """Arguments of a gated env step (env.step(..., gate=...)): the native stepper waits for
+        this step's done count itself and, if publish, releases the next launch. Call
+        published() after a step that did publish, publish() after one that did not."""
+        self.finished += 1
+        go = (self._p["go"], self.published + 1) if publish else (None, 0)
+        return (self._p["done"], ctypes.c_uint32(self.finished * self.nwg), go[0], ctypes.c_uint32(go[1]),
+                ctypes.c_double(timeout_s))
+
+    def published_by_gate(self):
+        self.published += 1
+
     def wait(self, timeout_s=30.0):
         import time
         self.finished += 1

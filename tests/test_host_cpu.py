@@ -109,6 +109,48 @@ def test_native_env_matches_numpy_spec():
     assert n_trunc == 2 * E  # 40 sub-steps = 10 chunks; 25 chunks cross two truncations
 
 
+def test_gated_env_step_publishes_only_without_resets():
+    """dppo_env_step_gated: waits for the done counter, steps like the ungated stepper, and
+    publishes go only when no env needs a host-side reset (else the caller resets, then publishes)."""
+    import ctypes
+
+    from diffusionpolicyoptimization_amd.env.synthetic import SyntheticLocomotionVecEnv, _native
+    if _native() is None:
+        subprocess.run(["make", "-C", os.path.join(ROOT, "diffusionpolicyoptimization_amd", "csrc"), "-j8"],
+                       check=True)
+    E, Do, Da = 5, 11, 3
+    envs = [SyntheticLocomotionVecEnv(E, Do, Da, act_steps=4, max_episode_steps=12, family_seed=1) for _ in range(2)]
+    for e in envs:
+        e.seed(range(E))
+        e.reset_arg()
+    ctr = np.zeros(32, dtype=np.uint32)        # done at [0], go at [16]
+    done_p = ctypes.c_void_p(ctr.ctypes.data)
+    go_p = ctypes.c_void_p(ctr.ctypes.data + 64)
+    obs = [np.zeros((E, 1, Do), np.float32) for _ in range(2)]
+    rng = np.random.default_rng(1)
+    pubs = []
+    for i in range(5):                          # 12 sub-steps = 3 chunks: step 2 truncates every env
+        a = rng.normal(0, 0.5, (E, 4, Da)).astype(np.float32)
+        ctr[0] = i + 1                          # the "device" has finished step i
+        g = envs[0].step(a, obs_out=obs[0], gate=(done_p, ctypes.c_uint32(i + 1), go_p, ctypes.c_uint32(i + 2),
+                                                  ctypes.c_double(1.0)))
+        r = envs[1].step(a, obs_out=obs[1])
+        np.testing.assert_array_equal(obs[0], obs[1])
+        np.testing.assert_array_equal(g[1], r[1])
+        np.testing.assert_array_equal(g[3], r[3])
+        pubs.append(envs[0].published)
+        if envs[0].published:
+            assert ctr[16] == i + 2
+    assert pubs == [True, True, False, True, True]
+    with pytest.raises(RuntimeError, match="did not finish"):     # done never reaches the target
+        envs[0].step(a, obs_out=obs[0], gate=(done_p, ctypes.c_uint32(99), None, ctypes.c_uint32(0),
+                                              ctypes.c_double(0.01)))
+    ctr[0] = 0x80000000                                           # the device's go-wait timed out
+    with pytest.raises(RuntimeError, match="timed out"):
+        envs[0].step(a, obs_out=obs[0], gate=(done_p, ctypes.c_uint32(1), None, ctypes.c_uint32(0),
+                                              ctypes.c_double(1.0)))
+
+
 def test_lr_schedules():
     from diffusionpolicyoptimization_amd.util.scheduler import (CosineAnnealingWarmupRestarts,
                                                                 CosineAnnealingWarmupRestarts2)
