@@ -37,14 +37,16 @@ CU_LOAD_PEAK_GBS = 64 * 2.4   # per-CU vector-memory (TA) path: 64 B/clk at the 
 
 
 def sampler_stream_bytes_per_tile(d, precision):
-    """Weight bytes ONE 16-row sampler tile (one CU) streams per launch: every denoising step reads
-    the in, l1, l2 and out images of its actor from L2 (dppo_layout.h fragment order)."""
-    kg = 32 if precision == "bf16" else 16
-    ks = lambda k: ((k + kg - 1) // kg + 1) & ~1
-    nt = lambda n: (n + 15) // 16
-    h = d.actor_hidden
-    per_step = (ks(d.actor_in) * nt(h) + 2 * ks(h) * nt(h) + ks(h) * nt(d.xd)) * 1024
-    return per_step * d.denoising_steps
+    """Weight bytes ONE 16-row sampler tile (one CU) loads per launch (the library reports it for
+    the sampler geometry in use: streamed k-steps every denoising step + the resident set once
+    per actor; include/dppo.h dppo_sampler_stream_bytes)."""
+    import ctypes
+
+    from diffusionpolicyoptimization_amd import _lib
+    out, waves = ctypes.c_int64(), ctypes.c_int()
+    _lib.call("dppo_sampler_stream_bytes", ctypes.byref(d.c()), 1 if precision == "bf16" else 0,
+              ctypes.byref(out), ctypes.byref(waves))
+    return out.value
 
 
 def cpu_baseline(cfg, n_envs, S, bs, seconds=12.0):

@@ -334,6 +334,16 @@ __device__ inline float philox_normal(uint64_t seed, uint32_t group, uint32_t ro
     return (q & 1) ? r * sinf(ang) : r * cosf(ang);
 }
 
+// all 4 normals of the block: the same values philox_normal gives for q = 0..3
+__device__ inline void philox_normal4(uint64_t seed, uint32_t group, uint32_t row, uint32_t slot, uint32_t call,
+                                      float (&z)[4]) {
+    const u32x4s w = philox4x32_10(group, row, slot, call, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float r0 = sqrtf(-2.0f * logf(u32_unit(w.x))), a0 = 6.283185307179586f * u32_unit(w.y);
+    const float r1 = sqrtf(-2.0f * logf(u32_unit(w.z))), a1 = 6.283185307179586f * u32_unit(w.w);
+    z[0] = r0 * cosf(a0); z[1] = r0 * sinf(a0);
+    z[2] = r1 * cosf(a1); z[3] = r1 * sinf(a1);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Feistel minibatch permutation (restated by oracle/philox.py:feistel_permute)
 // ------------------------------------------------------------------------------------------------

@@ -143,14 +143,15 @@ __device__ inline void gemm_res(const typename P::AT* A, int lda, WSrc Ws, const
 // SW waves per workgroup, each owning NT = H/(16*SW) n-tiles of every hidden layer. RK hidden
 // k-steps and (RIO) the whole in- and out-layers are resident in registers, LK more hidden
 // k-steps in LDS; QD k-steps of the rest in flight.
-template <class P, int NT, int NO, int KSI, bool INJ, int QD, int SW, int RK, int LK, bool RIO>
+template <class P, int NT, int NO, int KSI, bool INJ, int QD, int SW, int RK, int LK, int RIO>
 __global__ __launch_bounds__(SW * 64) void sample_kernel(SampleArgs a) {
     SPHASE_START;
     using AT = typename P::AT;
     constexpr int ST = SW * 64;
     constexpr int KSH = ksh_for<P>(NT, SW);
     constexpr int NOK = KSH / SW;
-    constexpr int RKI = RIO ? KSI : 0;       // resident in-layer k-steps
+    constexpr bool RIN = RIO & 1, ROUT = RIO & 2;   // in-layer / out-layer resident
+    constexpr int RKI = RIN ? KSI : 0;       // resident in-layer k-steps
     constexpr int NTOT = NT * SW;            // n-tiles of a hidden layer
     static_assert(RK + LK < KSH, "at least one streamed hidden k-step");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -215,53 +216,84 @@ __global__ __launch_bounds__(SW * 64) void sample_kernel(SampleArgs a) {
                 r_l1[k][n] = load_bfrag_c(W(ft, SEG_W_L1), KSH, ntile0 + n, k, lane);
                 r_l2[k][n] = load_bfrag_c(W(ft, SEG_W_L2), KSH, ntile0 + n, k, lane);
             }
-        if constexpr (RIO) out_prefetch<NOK, NO, SW>(r_out, W(ft, SEG_W_OUT), L.ks_h, wave, lane);
+        if constexpr (ROUT) out_prefetch<NOK, NO, SW>(r_out, W(ft, SEG_W_OUT), L.ks_h, wave, lane);
     };
     // the weight stream starts with step 0 (t = K-1); its first loads and the resident set go out
     // before anything waits (noise, the host's observation)
     const int ft0 = __builtin_amdgcn_readfirstlane(K - 1 < KF ? 1 : 0);
     WQueue<QD, NT> R;
-    if constexpr (RIO) squeue_prime(R, s_l1(ft0), SNext{s_l2(ft0), s_l1(ft0)}, ntile0, lane);
+    if constexpr (RIN) squeue_prime(R, s_l1(ft0), SNext{s_l2(ft0), s_l1(ft0)}, ntile0, lane);
     else squeue_prime(R, s_in(ft0), SNext{s_l1(ft0), s_l2(ft0)}, ntile0, lane);
     load_resident(ft0);
     if constexpr (LK > 0) load_lds(ft0);      // made visible by the prologue's barriers
     int cur = ft0;
 
     // ---- prologue: schedule, biases, state, x_T, time-embedding table ----
-    for (int i = tid; i < K * DPPO_SCHED_COLS; i += ST) sch[i] = a.sched[i];
-    for (int i = tid; i < 2 * (3 * H + NOC); i += ST) {
-        const int w = i / (3 * H + NOC), j = i % (3 * H + NOC);
+    // All global loads go out first (16 B per lane), the Philox/Box-Muller noise is computed while
+    // they are in flight, then everything lands in LDS: the prologue runs before the host's
+    // observation arrives, and in a pipelined rollout it is what the env step has to cover.
+    const int NB4 = 2 * (3 * H + NOC) / 4;                  // float4s of both actors' biases
+    float4 bv[4];
+    auto bias_src = [&](int i4) {
+        const int w = i4 / ((3 * H + NOC) / 4), j = 4 * (i4 % ((3 * H + NOC) / 4));
         const uint8_t* PK = w ? a.packed_ft : a.packed_base;
-        float v;
-        if (j < H) v = ((const float*)(PK + L.off[SEG_B_IN]))[j];
-        else if (j < 2 * H) v = ((const float*)(PK + L.off[SEG_B_L1]))[j - H];
-        else if (j < 3 * H) v = ((const float*)(PK + L.off[SEG_B_L2]))[j - 2 * H];
-        else v = ((const float*)(PK + L.off[SEG_B_OUT]))[j - 3 * H];
-        bias[i] = v;
+        const int seg = j < H ? SEG_B_IN : (j < 2 * H ? SEG_B_L1 : (j < 3 * H ? SEG_B_L2 : SEG_B_OUT));
+        const int jj = j < 3 * H ? j % H : j - 3 * H;
+        return (const float4*)(PK + L.off[seg]) + jj / 4;
+    };
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (tid + u * ST < NB4) bv[u] = *bias_src(tid + u * ST);
+    float tv = 0.f;
+    if (tid < K * TD) {
+        const int t = tid / TD;
+        tv = ((const float*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TEMB]))[tid];
     }
-    // all K steps' noise up front (injected, or the Philox stream), clipped to +-randn_clip (:319),
-    // so the denoising loop carries no RNG state and issues no global loads outside the weight stream
-    for (int i = tid; i < K * 16 * XD; i += ST) {
-        const int step = i / (16 * XD), r = (i / XD) % 16, q = i % XD, row = row0 + r;
-        float z;
-        if constexpr (INJ) z = row < a.E ? a.noise[((size_t)step * a.E + row) * XD + q] : 0.f;
-        else z = philox_normal(a.seed, (uint32_t)(q >> 2), (uint32_t)(a.env_offset + row), (uint32_t)step, a.call_id, q & 3);
-        zt[i] = fminf(fmaxf(z, -a.randn_clip), a.randn_clip);
+    float scv = tid < K * DPPO_SCHED_COLS ? a.sched[tid] : 0.f;
+    // noise: all K steps' draws up front (injected, or the Philox stream: one block gives the 4
+    // normals of a group of 4 action coordinates), clipped to +-randn_clip (:319), so the
+    // denoising loop carries no RNG state; slot K is x_T
+    const int XG = (XD + 3) / 4;
+    for (int it = tid; it < (K + 1) * 16 * XG; it += ST) {
+        const int step = it / (16 * XG), r = (it / XG) % 16, g = it % XG, row = row0 + r;
+        float z[4];
+        if (step == K && a.x_T) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z[k] = (row < a.E && 4 * g + k < XD) ? a.x_T[(size_t)row * XD + 4 * g + k] : 0.f;
+        } else if (INJ && step < K) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                z[k] = (row < a.E && 4 * g + k < XD) ? a.noise[((size_t)step * a.E + row) * XD + 4 * g + k] : 0.f;
+        } else {
+            philox_normal4(a.seed, (uint32_t)g, (uint32_t)(a.env_offset + row), (uint32_t)step, a.call_id, z);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = 4 * g + k;
+            if (q >= XD) break;
+            if (step < K) {
+                zt[(step * 16 + r) * XD + q] = fminf(fmaxf(z[k], -a.randn_clip), a.randn_clip);
+            } else {
+                xs[r * XD + q] = z[k];
+                if (KF == K && a.chains && row < a.E) a.chains[((size_t)row * (KF + 1) + 0) * XD + q] = z[k];
+            }
+        }
     }
-    for (int i = tid; i < 16 * XD; i += ST) {
-        const int r = i / XD, q = i % XD, row = row0 + r;
-        float x;
-        if (a.x_T) x = row < a.E ? a.x_T[(size_t)row * XD + q] : 0.f;
-        else x = philox_normal(a.seed, (uint32_t)(q >> 2), (uint32_t)(a.env_offset + row), (uint32_t)K, a.call_id, q & 3);
-        xs[i] = x;
-        if (KF == K && a.chains && row < a.E) a.chains[((size_t)row * (KF + 1) + 0) * XD + q] = x;
-    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (tid + u * ST < NB4) ((float4*)bias)[tid + u * ST] = bv[u];
+    for (int i4 = tid + 4 * ST; i4 < NB4; i4 += ST) ((float4*)bias)[i4] = *bias_src(i4);
     // time embeddings t_emb(t) (mlp_diffusion.py:40-45) of the actor each step uses, from the
     // table the pack step derived (dppo_layout.h SEG_TEMB)
-    for (int i = tid; i < K * TD; i += ST) {
-        const int t = i / TD;
-        temb[i] = ((const float*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TEMB]))[i];
-    }
+    if (tid < K * TD) temb[tid] = tv;
+    for (int i = tid + ST; i < K * TD; i += ST)
+        temb[i] = ((const float*)((i / TD < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TEMB]))[i];
+    if (tid < K * DPPO_SCHED_COLS) sch[tid] = scv;
+    for (int i = tid + ST; i < K * DPPO_SCHED_COLS; i += ST) sch[i] = a.sched[i];
+    // the resident set and the queue's first loads have landed by now; say so with a real wait
+    // (not inline asm), or the waitcnt pass carries them into the loop as possibly in flight and
+    // drains the queue before their first use in every layer
+    __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0)
     // a pre-enqueued step waits here (everything above does not depend on the observation) for
     // the host to publish it; bounded: ~4 s, then the step runs on whatever is in the buffer and
     // flags the timeout in the high bit of *done so the host reports it
@@ -305,20 +337,22 @@ __global__ __launch_bounds__(SW * 64) void sample_kernel(SampleArgs a) {
         const int PKn = __builtin_amdgcn_readfirstlane(t - 1 >= 0 ? (t - 1 < KF ? 1 : 0) : is_ft);
         if (PK != cur) {                                    // the actor switch (t = K'-1): once per launch
             load_resident(PK);
-            if constexpr (LK > 0) {
-                load_lds(PK);
-                __syncthreads();
-            }
+            if constexpr (LK > 0) load_lds(PK);
+            // wait for the reload HERE (a real s_waitcnt the waitcnt pass sees, not inline asm):
+            // otherwise the pass treats the resident registers as possibly in flight on every
+            // iteration and drains the weight queue before their first use in each layer
+            __builtin_amdgcn_s_waitcnt(0x0F70);             // vmcnt(0)
+            if constexpr (LK > 0) __syncthreads();
             cur = PK;
         }
         const float* bb = bias + is_ft * (3 * H + NOC);
         ORing<NOK, NO> ob;                                 // out-layer fragments, consumed 3 layers later
-        if constexpr (RIO) ob = r_out;
+        if constexpr (ROUT) ob = r_out;
         else out_prefetch<NOK, NO, SW>(ob, W(PK, SEG_W_OUT), L.ks_h, wave, lane);
         SPHASE(1);
         // b) in-Dense: h1 = a0 W_in + b_in  (no activation after the input layer, mlp.py:144)
         f32x4 h1[1][NT], acc[1][NT];
-        if constexpr (RIO)
+        if constexpr (RIN)
             gemm_res<P, NT, KSI, KSI, 0, NTOT, QD>(a0, lda0, W(PK, SEG_W_IN), r_in, nullptr, ntile0, h1, lane, R,
                                                    SNext{s_l1(PK), s_l2(PK)});
         else
@@ -338,7 +372,7 @@ __global__ __launch_bounds__(SW * 64) void sample_kernel(SampleArgs a) {
         SPHASE(2);
         // c) l1: relu(h1) W_l1 + b -> relu -> tB   (pre-activation block, mlp.py:192-193,202-203)
         gemm_res<P, NT, KSH, RK, LK, NTOT, QD>(tA, ldh, s_l1(PK).W, r_l1, lw1, ntile0, acc, lane, R,
-                                     RIO ? SNext{s_l2(PK), s_l1(PKn)} : SNext{s_l2(PK), s_in(PKn)});
+                                     RIN ? SNext{s_l2(PK), s_l1(PKn)} : SNext{s_l2(PK), s_in(PKn)});
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int col = (ntile0 + n) * 16 + ccol(lane);
@@ -351,7 +385,7 @@ __global__ __launch_bounds__(SW * 64) void sample_kernel(SampleArgs a) {
         // d) l2: relu(h2) W_l2 + b + h1 (residual, mlp.py:206) -> tA; the stream moves on to the
         //    next denoising step (possibly the other actor)
         gemm_res<P, NT, KSH, RK, LK, NTOT, QD>(tB, ldh, s_l2(PK).W, r_l2, lw2, ntile0, acc, lane, R,
-                                     RIO ? SNext{s_l1(PKn), s_l2(PKn)} : SNext{s_in(PKn), s_l1(PKn)});
+                                     RIN ? SNext{s_l1(PKn), s_l2(PKn)} : SNext{s_in(PKn), s_l1(PKn)});
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int col = (ntile0 + n) * 16 + ccol(lane);
@@ -435,7 +469,7 @@ static size_t sample_lds_bytes(const SampleArgs& a, int NO, int SW, int LK) {
     return o;
 }
 
-template <class P, int NT, int NO, int KSI, bool INJ, int QD, int SW, int RK, int LK, bool RIO>
+template <class P, int NT, int NO, int KSI, bool INJ, int QD, int SW, int RK, int LK, int RIO>
 static int launch_sample_q(const SampleArgs& a, hipStream_t s) {
     if (a.L.ks_h != ksh_for<P>(NT, SW) || a.L.ks_in != KSI || a.L.ks_h % SW != 0)
         return dppo_set_error(DPPO_EUNSUPPORTED, "sampler: hidden %d not supported at this precision", a.H);
@@ -448,14 +482,14 @@ static int launch_sample_q(const SampleArgs& a, hipStream_t s) {
     return DPPO_OK;
 }
 
-// Sampler geometry (measurement knob DPPO_SAMPLER_CFG, default "s"):
+// Sampler geometry (measurement knob DPPO_SAMPLER_CFG, default "r"):
 //   "s": 16 waves, nothing resident, QD 3 (the streaming-only layout)
 //   "r": 8 waves, in/out layers + 2 hidden k-steps resident, QD 3 (bf16 H = 512)
 //   "l": "r" + 1 more hidden k-step per layer in LDS; "m", "q", "i", "e": fewer resident
 static char sampler_cfg() {
     static char c = [] {
         const char* e = getenv("DPPO_SAMPLER_CFG");
-        return e && e[0] ? e[0] : 's';
+        return e && e[0] ? e[0] : 'r';
     }();
     return c;
 }
@@ -464,14 +498,16 @@ template <class P, int NT16, int NO, int KSI, bool INJ>
 static int launch_sample_k(const SampleArgs& a, hipStream_t s) {
     if constexpr (P::KG == 32 && NT16 == 2) {   // bf16, H = 512
         const char c = sampler_cfg();
-        if (c == 'r') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 0, true>(a, s);
-        if (c == 'l') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 1, true>(a, s);
-        if (c == 'm') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 1, true>(a, s);
-        if (c == 'q') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 0, true>(a, s);
-        if (c == 'i') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, true>(a, s);
-        if (c == 'e') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, false>(a, s);
+        if (c == 'r') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 0, 3>(a, s);
+        if (c == 'l') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 1, 3>(a, s);
+        if (c == 'm') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 1, 3>(a, s);
+        if (c == 'q') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 0, 3>(a, s);
+        if (c == 'i') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, 3>(a, s);
+        if (c == 'e') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, 0>(a, s);
     }
-    return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, false>(a, s);
+    if (sampler_cfg() == 'I') return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 1>(a, s);
+    if (sampler_cfg() == 'O') return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 3>(a, s);
+    return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 0>(a, s);
 }
 
 template <class P, int NT, int NO, int KSI>
@@ -495,6 +531,44 @@ static int dispatch_sample(const SampleArgs& a, hipStream_t s) {
 #undef DPPO_SAMPLE_CASE
     return dppo_set_error(DPPO_EUNSUPPORTED, "sampler: hidden %d / action chunk %d / in-layer k-steps %d not instantiated",
                           a.H, a.XD, KSI);
+}
+
+// the geometry launch_sample_k picks, for dppo_sampler_stream_bytes
+struct SamplerGeom { int SW, RK, LK, RIO; };
+static SamplerGeom sampler_geom(int precision, int H) {
+    if (precision == DPPO_BF16 && H == 512) {
+        switch (sampler_cfg()) {
+            case 'r': return {8, 2, 0, 3};
+            case 'l': return {8, 2, 1, 3};
+            case 'm': return {8, 1, 1, 3};
+            case 'q': return {8, 1, 0, 3};
+            case 'i': return {8, 0, 0, 3};
+            case 'e': return {8, 0, 0, 0};
+            default: break;
+        }
+    }
+    if (sampler_cfg() == 'I') return {16, 0, 0, 1};
+    if (sampler_cfg() == 'O') return {16, 0, 0, 3};
+    return {16, 0, 0, 0};
+}
+
+extern "C" int dppo_sampler_stream_bytes(const dppo_dims* d, int precision, int64_t* bytes_per_tile, int* waves) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(bytes_per_tile, "dppo_sampler_stream_bytes: null output");
+    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "dppo_sampler_stream_bytes: bad precision %d", precision);
+    const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+    const SamplerGeom g = sampler_geom(precision, D.H);
+    const int64_t ntot = D.H / 16, no = dppo_cdiv(D.XD, 16);
+    const int64_t in_f = (int64_t)L.ks_in * ntot, out_f = (int64_t)L.ks_h * no;
+    const int64_t rin = (g.RIO & 1) ? in_f : 0, rout = (g.RIO & 2) ? out_f : 0;
+    const int64_t per_step = (in_f - rin) + 2 * (L.ks_h - g.RK - g.LK) * ntot + (out_f - rout);
+    const int64_t resident = rin + rout + 2 * (int64_t)(g.RK + g.LK) * ntot;
+    const int actors = (D.KF > 0 && D.KF < D.K) ? 2 : 1;        // the resident set is reloaded at the switch
+    *bytes_per_tile = ((int64_t)D.K * per_step + actors * resident) * 1024;
+    if (waves) *waves = g.SW;
+    return DPPO_OK;
 }
 
 static int sample_impl(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,

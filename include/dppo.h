@@ -89,6 +89,12 @@ DPPO_API int dppo_sample(const dppo_dims* d, int precision, const void* packed_b
                 float min_sampling_std, float randn_clip, float final_clip,
                 float* actions, float* chains, void* stream);
 
+/* Measurement aid (no reference counterpart): bytes of weight fragments one 16-env sampler tile
+ * (one CU) loads per dppo_sample launch with the sampler geometry in use — every denoising step's
+ * streamed k-steps plus the resident set, loaded once per actor. bench.py divides it by the launch
+ * time for the per-CU load-path figure. Also returns the waves per workgroup. */
+DPPO_API int dppo_sampler_stream_bytes(const dppo_dims* d, int precision, int64_t* bytes_per_tile, int* waves);
+
 /* One rollout step (agent/finetune/train_ppo_diffusion_agent.py:106-122) in one call:
  * hipMemcpyAsync(cond <- cond_host [host, pinned]), dppo_sample with the Philox noise, hipMemcpyAsync
  * (actions_host [host, pinned] <- actions), then hipStreamSynchronize when synchronize != 0. */

@@ -6,6 +6,7 @@ import math
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -149,6 +150,27 @@ def test_gated_env_step_publishes_only_without_resets():
     with pytest.raises(RuntimeError, match="timed out"):
         envs[0].step(a, obs_out=obs[0], gate=(done_p, ctypes.c_uint32(1), None, ctypes.c_uint32(0),
                                               ctypes.c_double(1.0)))
+
+
+def test_sampler_stream_bytes_per_geometry():
+    """The load-path accounting bench.py divides by the launch time (hopper, bf16, H = 512):
+    "s" streams all four layers every step; "r" keeps the in/out layers and 2 k-steps of each
+    hidden layer resident (loaded once per actor, twice per launch) and streams 14 of 16."""
+    code = ("import ctypes, sys; sys.path.insert(0, %r)\n"
+            "from diffusionpolicyoptimization_amd import _lib\n"
+            "from diffusionpolicyoptimization_amd.ops import ModelDims as Dims\n"
+            "d = Dims(obs_dim=11, action_dim=3, horizon_steps=4, cond_steps=1, time_dim=16, actor_hidden=512,"
+            " critic_hidden=256, denoising_steps=20, ft_denoising_steps=10)\n"
+            "b, w = ctypes.c_int64(), ctypes.c_int()\n"
+            "_lib.call('dppo_sampler_stream_bytes', ctypes.byref(d.c()), 1, ctypes.byref(b), ctypes.byref(w))\n"
+            "print(b.value, w.value)\n") % ROOT
+    got = {}
+    for cfg in ("s", "r"):
+        out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, DPPO_SAMPLER_CFG=cfg),
+                             capture_output=True, text=True, check=True).stdout.split()
+        got[cfg] = (int(out[0]), int(out[1]))
+    assert got["s"] == ((64 + 2 * 16 * 32 + 16) * 20 * 1024, 16)
+    assert got["r"] == ((20 * 2 * 14 * 32 + 2 * (64 + 16 + 2 * 2 * 32)) * 1024, 8)
 
 
 def test_lr_schedules():
