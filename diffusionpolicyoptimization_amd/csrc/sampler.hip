@@ -11,6 +11,7 @@
 #include <string.h>
 #include "dppo_common.cuh"
 #include "dppo_internal.h"
+#include "dppo_sampler.h"
 
 // phase timing for tuning builds (-DDPPO_SAMPLER_TIMING): wave 0 of every workgroup adds the
 // shader-clock cycles of each phase of every denoising step (barrier waits included)
@@ -37,31 +38,6 @@ extern "C" DPPO_API int dppo_debug_sampler_cycles(unsigned long long* out, int r
 #define SPHASE(k) do {} while (0)
 #define SPHASE_START do {} while (0)
 #endif
-
-struct SampleArgs {
-    const uint8_t* packed_base;
-    const uint8_t* packed_ft;
-    const float* sched;   // [K][8]
-    const float* cond;    // [E][SD]
-    const float* x_T;     // [E][XD] or null
-    const float* noise;   // [K][E][XD] or null
-    float* actions;       // [E][XD]
-    float* chains;        // [E][KF+1][XD] or null
-    float* cond_out;      // [E][SD] device copy of cond or null (cond may be mapped host memory)
-    float* actions_host;  // [E][XD] mapped pinned host memory or null (zero-copy action hand-off)
-    // pre-enqueued rollout steps (dppo_rollout_*): wait until *go >= go_value before reading cond,
-    // and add 1 to *done per workgroup after the actions are visible to the host (both counters
-    // live in fine-grained host memory); null = an ordinary launch
-    const uint32_t* go;
-    uint32_t go_value;
-    uint32_t* done;
-    uint64_t seed;
-    uint32_t call_id;
-    int E, env_offset, deterministic;
-    float min_std, randn_clip, final_clip;
-    int XD, SD, TD, H, K, KF, IN;
-    MlpLayout L;          // same layout for base and ft
-};
 
 // ---- the sampler's weight stream with resident fragments ----
 // A CU streams its actor's weights from L2 every denoising step, and its vector-memory path
@@ -482,14 +458,16 @@ static int launch_sample_q(const SampleArgs& a, hipStream_t s) {
     return DPPO_OK;
 }
 
-// Sampler geometry (measurement knob DPPO_SAMPLER_CFG, default "r"):
+// Sampler geometry (measurement knob DPPO_SAMPLER_CFG, default "x"):
+//   "x": the split register-resident kernel (sampler_split.hip) where it applies (bf16, H = 512,
+//        <= 512 envs), else "r"
 //   "s": 16 waves, nothing resident, QD 3 (the streaming-only layout)
 //   "r": 8 waves, in/out layers + 2 hidden k-steps resident, QD 3 (bf16 H = 512)
 //   "l": "r" + 1 more hidden k-step per layer in LDS; "m", "q", "i", "e": fewer resident
 static char sampler_cfg() {
     static char c = [] {
         const char* e = getenv("DPPO_SAMPLER_CFG");
-        return e && e[0] ? e[0] : 'r';
+        return e && e[0] ? e[0] : 'x';
     }();
     return c;
 }
@@ -498,7 +476,7 @@ template <class P, int NT16, int NO, int KSI, bool INJ>
 static int launch_sample_k(const SampleArgs& a, hipStream_t s) {
     if constexpr (P::KG == 32 && NT16 == 2) {   // bf16, H = 512
         const char c = sampler_cfg();
-        if (c == 'r') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 0, 3>(a, s);
+        if (c == 'r' || c == 'x') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 0, 3>(a, s);
         if (c == 'l') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 1, 3>(a, s);
         if (c == 'm') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 1, 3>(a, s);
         if (c == 'q') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 0, 3>(a, s);
@@ -538,7 +516,7 @@ struct SamplerGeom { int SW, RK, LK, RIO; };
 static SamplerGeom sampler_geom(int precision, int H) {
     if (precision == DPPO_BF16 && H == 512) {
         switch (sampler_cfg()) {
-            case 'r': return {8, 2, 0, 3};
+            case 'r': case 'x': return {8, 2, 0, 3};
             case 'l': return {8, 2, 1, 3};
             case 'm': return {8, 1, 1, 3};
             case 'q': return {8, 1, 0, 3};
@@ -595,7 +573,22 @@ static int sample_impl(const dppo_dims* d, int precision, const void* packed_bas
     a.XD = D.XD; a.SD = D.SD; a.TD = D.TD; a.H = D.H; a.K = D.K; a.KF = D.KF; a.IN = D.IN;
     a.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     hipStream_t s = (hipStream_t)stream;
+    if (sampler_cfg() == 'x') {
+        rc = launch_sample_split(a, precision, s);
+        if (rc != DPPO_EUNSUPPORTED) return rc;
+    }
     return precision == DPPO_BF16 ? dispatch_sample<PolicyBF16>(a, s) : dispatch_sample<PolicyF32>(a, s);
+}
+
+extern "C" int dppo_sampler_layout(const dppo_dims* d, int precision, int n_envs, int* members) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(members, "dppo_sampler_layout: null output");
+    const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+    *members = (sampler_cfg() == 'x' && sample_split_supported(precision, D.H, D.XD, L.ks_in, n_envs, D.K))
+                   ? split_sampler_members() : 0;
+    return DPPO_OK;
 }
 
 extern "C" int dppo_sample(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,

@@ -1,0 +1,600 @@
+// sampler_split.hip — a9: VPGDiffusion.call (model/diffusion/diffusion_vpg.py:250-339), DDPM branch,
+// as a register-resident SPLIT kernel (the default for the bf16 denoiser at <= 512 envs per GPU).
+//
+// Why: the weight-streaming kernel (sampler.hip) gives each 16-env tile one CU, which must pull the
+// whole 1.1 MB bf16 actor through its 64 B/clk load path every denoising step (~8 us a step at 64
+// envs). Here each 16-env tile is owned by a GROUP of P = 8 workgroups (one per CU), and member c
+// keeps 1/8 of the actor in its register file for the whole launch:
+//   in-Dense   all 512 outputs (64 KB, replicated: its input is tiny and local)
+//   l1         output columns [64c, 64c+64)                      (W_l1[:, slice],  64 KB)
+//   l2         input rows     [64c, 64c+64), all 512 outputs     (W_l2[slice, :],  64 KB)
+//   out-Dense  all of it (16 KB), applied to the member's PARTIAL l2 sum
+// so the only cross-CU traffic of a denoising step is one exchange of 16 x XD fp32 out-layer
+// partial sums between the 8 members (mlp.py:186-206 is linear from the l2 product to the
+// out-Dense: eps = sum_c (P_c [+ b_l2 + h1 on member 0]) W_out + b_out). Every member then runs
+// the same fp32 DDPM epilogue on the same sum (fixed member order: bit-identical x on all eight).
+//
+// The exchange is in-launch (MI355X_MICROARCH.md "handoff-1to1"/R2 granules): each member stores
+// its partials as 8-byte {tag, value} granules with write-through agent-scope stores; wave 0 of
+// every member sweeps the group's granules with agent-scope loads until every tag matches. Tags
+// carry a per-launch sequence number and the step index, so nothing is zeroed between launches;
+// slots alternate by step parity (a member can be at most one step ahead of a peer). The wait is
+// bounded (100 ms): a launch that times out writes NaN actions and flags bit 31 of *done.
+//
+// Layout per step (member c, 8 waves; all GEMMs computed TRANSPOSED, W^T x^T, so an MFMA result
+// lane holds 4 consecutive features of one env):
+//   in-layer   wave w: h1 features [64w, 64w+64)    -> u1 = bf16 relu(h1) to LDS (8-B stores)
+//   l1         wave w: l1 n-tile (w % 4), K-half (w / 4) -> fp32 partial to LDS
+//   l2         wave w: h3 features [64w, 64w+64) of this member's K-slice (+ b_l2 + h1 on c = 0)
+//   out-Dense  wave w: its own h3 registers as the B operand (hi/lo bf16 split: fp32-accurate),
+//              W_out fragments pre-permuted to the MFMA result lane order -> partial to LDS
+//   wave 0: sum the 8 wave partials, publish, sweep the group, DDPM epilogue; waves 1-7 write
+//   the next step's time embedding.
+// Block -> (group, member): members of a group share blockIdx % 8 (one XCD under the observed
+// round-robin placement: a speed choice only; correctness does not depend on placement).
+#include <mutex>
+#include <string.h>
+#include "dppo_common.cuh"
+#include "dppo_internal.h"
+#include "dppo_sampler.h"
+
+// phase timing for tuning builds (-DDPPO_SAMPLER_TIMING): thread 0 of every workgroup adds the
+// shader-clock cycles of each phase (0 prologue, 1 actor switch, 2 in-Dense, 3 l1, 4 l2 + out,
+// 5 publish + sweep, 6 epilogue)
+#ifdef DPPO_SAMPLER_TIMING
+__device__ unsigned long long dppo_split_cycles[16 + 64 * 8];
+// [0, 16): phase sums over all workgroups; [16 + 8 i + k): phase k of step i of workgroup 0 alone
+#define XPHASE(k)                                                                 \
+    do {                                                                          \
+        if (threadIdx.x == 0) {                                                   \
+            const unsigned long long now_ = __builtin_readcyclecounter();         \
+            atomicAdd(&dppo_split_cycles[(k)], now_ - t_phase_);                  \
+            if (blockIdx.x == 0 && t_step_ < 64) dppo_split_cycles[16 + 8 * t_step_ + (k)] = now_ - t_phase_; \
+            t_phase_ = now_;                                                      \
+        }                                                                         \
+    } while (0)
+#define XPHASE_START unsigned long long t_phase_ = __builtin_readcyclecounter(); int t_step_ = 0
+#define XSTEP(i) t_step_ = (i)
+extern "C" DPPO_API int dppo_debug_split_cycles(unsigned long long* out, int reset) {
+    DPPO_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dppo_split_cycles), sizeof(unsigned long long) * (16 + 64 * 8)));
+    if (reset) {
+        unsigned long long z[16 + 64 * 8] = {};
+        DPPO_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dppo_split_cycles), z, sizeof(z)));
+    }
+    return DPPO_OK;
+}
+#else
+#define XPHASE(k) do {} while (0)
+#define XPHASE_START do {} while (0)
+#define XSTEP(i) do {} while (0)
+#endif
+
+namespace {
+
+constexpr int SW = 8;              // waves per workgroup
+constexpr int SPLIT_P = 8;         // workgroups (CUs) per 16-env group
+constexpr int SPLIT_H = 512;       // actor hidden width the split layout is built for
+constexpr int XMAX_NV = 16 * 32;   // granules per member per step at XD <= 32
+constexpr int XMAX_G = 32;         // groups per launch (512 envs): 8*P*G/8 = 256 workgroups
+
+struct SplitArgs {
+    SampleArgs a;
+    uint64_t* xbuf;   // granules [2 slots][G][P][NV]
+    uint32_t seq;     // launch sequence number (tag high bits)
+    int G;            // 16-env groups
+};
+
+// one k-slot -> feature map of the transposed-result lane order: slot (j, e) of a 32-wide
+// k-step holds feature e < 4 ? 4j + e : 16 + 4j + (e - 4)
+__device__ inline int slot_feature(int j, int e) { return e < 4 ? 4 * j + e : 16 + 4 * j + (e - 4); }
+
+__device__ inline uint32_t pack_bf16x2(float lo, float hi) {
+    const __bf16 a = (__bf16)lo, b = (__bf16)hi;
+    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+
+// XQ = XD / 4 (compile time: the sweep's loads must all be in flight before the first wait)
+template <int P, int XQ, int KSI, bool INJ>
+__global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
+    constexpr int NO = (4 * XQ + 15) / 16;
+    using Pol = PolicyBF16;
+    using AT = __bf16;
+    constexpr int H = SPLIT_H, NTH = H / 16, KSH = H / 32;
+    constexpr int NT1 = NTH / P;           // l1 n-tiles per member
+    constexpr int KP = SW / NT1;           // l1 K-parts (waves per l1 n-tile)
+    constexpr int KS1 = KSH / KP;          // l1 k-steps per wave
+    constexpr int HS = H / P;              // features per member slice
+    constexpr int KS2 = HS / 32;           // l2 k-steps per member
+    constexpr int NOC = 16 * NO;
+    constexpr int ST = SW * 64;
+    static_assert(NT1 * KP == SW && KS2 >= 1 && 4 * SW == NTH, "split geometry");
+    constexpr int pad = 16;                // bf16 elements (32 B) of row padding
+    constexpr int ldh = H + pad;           // u1 row stride (bf16)
+    constexpr int lda0 = KSI * 32 + pad;   // a0 row stride (bf16)
+    constexpr int ldp = HS + 4;            // l1 partial row stride (fp32)
+    static_assert(P == 8, "the member sum is a 3-level lane butterfly");
+
+    const SampleArgs& a = sa.a;
+    const int b = blockIdx.x;
+    const int g = (b / (8 * P)) * 8 + b % 8, c = (b / 8) % P;
+    if (g >= sa.G) return;                 // whole workgroup: no barrier is skipped
+    XPHASE_START;
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int row0 = g * 16;
+    const MlpLayout& L = a.L;
+    constexpr int XD = 4 * XQ;
+    const int SD = a.SD, TD = a.TD, K = a.K, KF = a.KF;
+    constexpr int NV = 16 * XD;            // coordinates of a 16-env eps block
+    constexpr int NVW = NV / SW;           // per wave: 2 XD (a multiple of 8)
+    constexpr int KW = XQ;                 // sweep loads per lane: NVW * P / 64 = XD / 4
+
+    // ---- LDS carve (all offsets multiples of 16 B) ----
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    size_t o = 0;
+    AT* a0 = (AT*)(smem + o); o += dppo_align16(2 * 16 * lda0);
+    AT* u1 = (AT*)(smem + o); o += dppo_align16(2 * 16 * ldh);
+    float* p1 = (float*)(smem + o); o += dppo_align16(4 * KP * 16 * ldp);
+    float* part = (float*)(smem + o); o += dppo_align16(4 * SW * NV);      // [wave][16 x XD]
+    int* xfail = (int*)(smem + o); o += 16;
+    float* xs = (float*)(smem + o); o += dppo_align16(4 * 16 * XD);
+    float* st = (float*)(smem + o); o += dppo_align16(4 * 16 * SD);
+    float* temb = (float*)(smem + o); o += dppo_align16(4 * K * TD);
+    float* sch = (float*)(smem + o); o += dppo_align16(4 * K * DPPO_SCHED_COLS);
+    float* bias = (float*)(smem + o); o += dppo_align16(4 * 2 * (3 * H + NOC));
+    float* zt = (float*)(smem + o); o += dppo_align16(4 * K * 16 * XD);
+    u32x4* stage = (u32x4*)(smem + o); o += (size_t)SW * 2 * NO * 1024;
+
+    // ---- resident weight fragments (one actor at a time) ----
+    const __amdgpu_buffer_rsrc_t rs_base = packed_rsrc(a.packed_base), rs_ft = packed_rsrc(a.packed_ft);
+    auto W = [&](int ft, int seg) { return wsrc(ft ? rs_ft : rs_base, L.off[seg]); };
+    const int t1 = wave % NT1, kp = wave / NT1;
+    u32x4 rin[KSI][4], rl1[KS1], rl2[KS2][4], rout[2][NO];
+    auto load_in = [&](int ft) {
+#pragma unroll
+        for (int ks = 0; ks < KSI; ++ks)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) rin[ks][n] = load_bfrag_c(W(ft, SEG_W_IN), KSI, 4 * wave + n, ks, lane);
+    };
+    auto load_l1 = [&](int ft) {
+#pragma unroll
+        for (int j = 0; j < KS1; ++j) rl1[j] = load_bfrag_c(W(ft, SEG_W_L1), KSH, NT1 * c + t1, kp * KS1 + j, lane);
+    };
+    auto load_l2 = [&](int ft) {
+#pragma unroll
+        for (int s = 0; s < KS2; ++s)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) rl2[s][n] = load_bfrag_c(W(ft, SEG_W_L2), KSH, 4 * wave + n, c * KS2 + s, lane);
+    };
+    auto load_out = [&](int ft) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int n = 0; n < NO; ++n) rout[s][n] = load_bfrag_c(W(ft, SEG_W_OUT), KSH, n, 2 * wave + s, lane);
+    };
+    // re-order the out-Dense fragments to the transposed-result k-slot order (slot_feature), once
+    // per actor, through this wave's own LDS staging area (one wave's LDS ops complete in order)
+    auto permute_out = [&]() {
+        u32x4* stg = stage + wave * 2 * NO * 64;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int n = 0; n < NO; ++n) stg[(s * NO + n) * 64 + lane] = rout[s][n];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int j = lane >> 4, q = lane & 15;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int n = 0; n < NO; ++n) {
+                const uint16_t* src = (const uint16_t*)(stg + (s * NO + n) * 64);
+                uint32_t w[4];
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2) {
+                    const int f0 = slot_feature(j, 2 * e2), f1 = slot_feature(j, 2 * e2 + 1);
+                    const uint32_t lo = src[(16 * (f0 >> 3) + q) * 8 + (f0 & 7)];
+                    const uint32_t hi = src[(16 * (f1 >> 3) + q) * 8 + (f1 & 7)];
+                    w[e2] = lo | (hi << 16);
+                }
+                rout[s][n] = u32x4{w[0], w[1], w[2], w[3]};
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+
+    const int ft0 = __builtin_amdgcn_readfirstlane(K - 1 < KF ? 1 : 0);
+    load_in(ft0); load_l1(ft0); load_l2(ft0); load_out(ft0);
+    int cur = ft0;
+
+    // ---- prologue: biases, time embeddings, schedule, noise (as sampler.hip) ----
+    const int NB4 = 2 * (3 * H + NOC) / 4;
+    auto bias_src = [&](int i4) {
+        const int w = i4 / ((3 * H + NOC) / 4), j = 4 * (i4 % ((3 * H + NOC) / 4));
+        const uint8_t* PK = w ? a.packed_ft : a.packed_base;
+        const int seg = j < H ? SEG_B_IN : (j < 2 * H ? SEG_B_L1 : (j < 3 * H ? SEG_B_L2 : SEG_B_OUT));
+        const int jj = j < 3 * H ? j % H : j - 3 * H;
+        return (const float4*)(PK + L.off[seg]) + jj / 4;
+    };
+    for (int i4 = tid; i4 < NB4; i4 += ST) ((float4*)bias)[i4] = *bias_src(i4);
+    for (int i = tid; i < K * TD; i += ST)
+        temb[i] = ((const float*)((i / TD < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TEMB]))[i];
+    for (int i = tid; i < K * DPPO_SCHED_COLS; i += ST) sch[i] = a.sched[i];
+    const int XG = (XD + 3) / 4;
+    for (int it = tid; it < (K + 1) * 16 * XG; it += ST) {
+        const int step = it / (16 * XG), r = (it / XG) % 16, gq = it % XG, row = row0 + r;
+        float z[4];
+        if (step == K && a.x_T) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z[k] = (row < a.E && 4 * gq + k < XD) ? a.x_T[(size_t)row * XD + 4 * gq + k] : 0.f;
+        } else if (INJ && step < K) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                z[k] = (row < a.E && 4 * gq + k < XD) ? a.noise[((size_t)step * a.E + row) * XD + 4 * gq + k] : 0.f;
+        } else {
+            philox_normal4(a.seed, (uint32_t)gq, (uint32_t)(a.env_offset + row), (uint32_t)step, a.call_id, z);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = 4 * gq + k;
+            if (q >= XD) break;
+            if (step < K) {
+                zt[(step * 16 + r) * XD + q] = fminf(fmaxf(z[k], -a.randn_clip), a.randn_clip);
+            } else {
+                xs[r * XD + q] = z[k];
+                if (KF == K && c == 0 && a.chains && row < a.E) a.chains[((size_t)row * (KF + 1) + 0) * XD + q] = z[k];
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0): the resident set has landed
+    permute_out();
+    // pre-enqueued rollout step: wait for the host's observation (bounded, as sampler.hip)
+    if (a.go) {
+        if (tid == 0) {
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;   // 100 MHz: 4 s
+            while (__hip_atomic_load(a.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
+                __builtin_amdgcn_s_sleep(8);
+                if (__builtin_amdgcn_s_memrealtime() > t_end) {
+                    if (c == 0) __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < 16 * SD; i += ST) {
+        const int r = i / SD, cc = i % SD, row = row0 + r;
+        const float v = row < a.E ? a.cond[(size_t)row * SD + cc] : 0.f;
+        st[i] = v;
+        if (a.cond_out && c == 0 && row < a.E) a.cond_out[(size_t)row * SD + cc] = v;
+    }
+    __syncthreads();
+    const int k1w = KSI * 32;
+    for (int idx = tid; idx < 16 * k1w; idx += ST) {
+        const int r = idx / k1w, cc = idx % k1w;
+        float v = 0.f;
+        if (cc < XD) v = xs[r * XD + cc];
+        else if (cc < XD + TD) v = temb[(K - 1) * TD + cc - XD];
+        else if (cc < a.IN) v = st[r * SD + cc - XD - TD];
+        a0[r * lda0 + cc] = Pol::cvt(v);
+    }
+    __syncthreads();
+
+    if (tid == 0) *xfail = 0;
+    __syncthreads();
+    const int env = lane & 15, jq = lane >> 4;
+    XPHASE(0);
+    for (int i = 0; i < K; ++i) {
+        XSTEP(i);
+        const int t = K - 1 - i;
+        const int PK = __builtin_amdgcn_readfirstlane(t < KF ? 1 : 0);
+        // the actor switch (t = K'-1, once per launch): the step before reloaded each layer's
+        // fragments right after their last use, so only the out-Dense re-order is left here
+        const int PKn = __builtin_amdgcn_readfirstlane(t >= 1 && t - 1 < KF ? 1 : 0);
+        const bool pre = t >= 1 && PKn != PK;             // this step is the last of its actor
+        if (PK != cur) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            permute_out();
+            cur = PK;
+        }
+        XPHASE(1);
+        const float* bb = bias + PK * (3 * H + NOC);
+        // ---- in-Dense (transposed): h1 features 16(4w+n) + 4jq + r of env; no activation (mlp.py:144)
+        f32x4 h1[4];
+        {
+            u32x4 af[KSI];
+#pragma unroll
+            for (int ks = 0; ks < KSI; ++ks) af[ks] = lds_afrag<Pol>(a0, lda0, 0, ks, lane);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                zero_acc(h1[n]);
+#pragma unroll
+                for (int ks = 0; ks < KSI; ++ks) h1[n] = Pol::mma(rin[ks][n], af[ks], h1[n]);
+                if (pre && n == 3) load_in(PKn);
+                const int f = 16 * (4 * wave + n) + 4 * jq;
+                const float4 bv = *(const float4*)(bb + f);
+                h1[n][0] += bv.x; h1[n][1] += bv.y; h1[n][2] += bv.z; h1[n][3] += bv.w;
+                u32x2 pk;
+                pk[0] = pack_bf16x2(fmaxf(h1[n][0], 0.f), fmaxf(h1[n][1], 0.f));
+                pk[1] = pack_bf16x2(fmaxf(h1[n][2], 0.f), fmaxf(h1[n][3], 0.f));
+                *(u32x2*)(u1 + env * ldh + f) = pk;
+            }
+        }
+        lds_sync();
+        XPHASE(2);
+        // ---- l1 (transposed): this member's output columns, K split over KP waves
+        {
+            f32x4 acc0, acc1;
+            zero_acc(acc0); zero_acc(acc1);
+#pragma unroll
+            for (int j = 0; j < KS1; ++j) {
+                const u32x4 bfr = lds_afrag<Pol>(u1, ldh, 0, kp * KS1 + j, lane);
+                if (j & 1) acc1 = Pol::mma(rl1[j], bfr, acc1);
+                else acc0 = Pol::mma(rl1[j], bfr, acc0);
+            }
+            if (pre) load_l1(PKn);
+            const f32x4 s = acc0 + acc1;
+            *(f32x4*)(p1 + (kp * 16 + env) * ldp + 16 * t1 + 4 * jq) = s;
+        }
+        lds_sync();
+        XPHASE(3);
+        // ---- l2 (transposed) over this member's K-slice: u2 = bf16 relu(h2 + b_l1) (mlp.py:202-206)
+        f32x4 h3[4];
+        {
+            u32x4 u2[KS2];
+#pragma unroll
+            for (int s = 0; s < KS2; ++s) {
+                const int k0 = 32 * s + 8 * jq;
+                f32x4 v0 = *(const f32x4*)(bb + H + HS * c + k0);
+                f32x4 v1 = *(const f32x4*)(bb + H + HS * c + k0 + 4);
+#pragma unroll
+                for (int q = 0; q < KP; ++q) {
+                    v0 += *(const f32x4*)(p1 + (q * 16 + env) * ldp + k0);
+                    v1 += *(const f32x4*)(p1 + (q * 16 + env) * ldp + k0 + 4);
+                }
+                u2[s] = u32x4{pack_bf16x2(fmaxf(v0[0], 0.f), fmaxf(v0[1], 0.f)),
+                              pack_bf16x2(fmaxf(v0[2], 0.f), fmaxf(v0[3], 0.f)),
+                              pack_bf16x2(fmaxf(v1[0], 0.f), fmaxf(v1[1], 0.f)),
+                              pack_bf16x2(fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f))};
+            }
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                zero_acc(h3[n]);
+#pragma unroll
+                for (int s = 0; s < KS2; ++s) h3[n] = Pol::mma(rl2[s][n], u2[s], h3[n]);
+            }
+            if (pre) load_l2(PKn);
+            if (c == 0) {                                    // + b_l2 + h1 (residual), once per group
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const f32x4 bv = *(const f32x4*)(bb + 2 * H + 16 * (4 * wave + n) + 4 * jq);
+                    h3[n] += bv + h1[n];
+                }
+            }
+        }
+        // ---- out-Dense partial (transposed) from this wave's own h3 registers: k-step s covers
+        //      h3 tiles 2s, 2s+1 in slot_feature order; hi/lo bf16 split keeps h3 fp32-accurate
+        {
+            f32x4 po[NO];
+#pragma unroll
+            for (int n = 0; n < NO; ++n) zero_acc(po[n]);
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                float hv[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { hv[e] = h3[2 * s][e]; hv[4 + e] = h3[2 * s + 1][e]; }
+                u32x4 hi, lo;
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2) {
+                    const float x0 = hv[2 * e2], x1 = hv[2 * e2 + 1];
+                    const float r0 = (float)(__bf16)x0, r1 = (float)(__bf16)x1;
+                    hi[e2] = pack_bf16x2(x0, x1);
+                    lo[e2] = pack_bf16x2(x0 - r0, x1 - r1);
+                }
+#pragma unroll
+                for (int n = 0; n < NO; ++n) {
+                    po[n] = Pol::mma(rout[s][n], hi, po[n]);
+                    po[n] = Pol::mma(rout[s][n], lo, po[n]);
+                }
+            }
+            if (pre) load_out(PKn);
+#pragma unroll
+            for (int n = 0; n < NO; ++n)
+                if (16 * n + 4 * jq < XD) *(f32x4*)(part + wave * NV + env * XD + 16 * n + 4 * jq) = po[n];
+        }
+        lds_sync();
+        XPHASE(4);
+        // ---- exchange + DDPM epilogue. Wave w owns coordinates [w*NVW, (w+1)*NVW) of the 16 x XD
+        //      eps block: it sums the 8 wave partials of them and publishes that slice, sweeps the
+        //      slice from all P members (lane = 8 * slot + member), adds the members with a fixed
+        //      xor-butterfly (bit-identical on every member) and runs the fp32 DDPM epilogue
+        //      (diffusion_vpg.py:198-243, 301-320) for them. No workgroup barrier in between.
+        {
+            const uint32_t tag = (sa.seq << 6) | (uint32_t)(i + 1);
+            uint64_t* xb = sa.xbuf + ((size_t)((i & 1) * sa.G + g) * P) * NV;
+            const int vw = wave * NVW;
+            if (lane < NVW) {
+                float sum = part[vw + lane];
+#pragma unroll
+                for (int w = 1; w < SW; ++w) sum += part[w * NV + vw + lane];
+                __hip_atomic_store(xb + (size_t)c * NV + vw + lane, ((uint64_t)tag << 32) | __float_as_uint(sum),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            // the next step's time embedding into a0 while the members arrive (a0 was last read by
+            // this step's in-Dense, two barriers ago)
+            if (t > 0 && lane < 16 * TD / SW) {
+                const int e = wave * (16 * TD / SW) + lane, r = e / TD, cc = e % TD;
+                a0[r * lda0 + XD + cc] = Pol::cvt(temb[(t - 1) * TD + cc]);
+            }
+            const int m = lane & 7, sl = lane >> 3;
+            const uint64_t* src = xb + (size_t)m * NV + vw + sl;
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
+            float val[KW];
+            bool failed = false;
+            for (;;) {
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < KW; ++k) {
+                    const uint64_t x = __hip_atomic_load(src + 8 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok &= (uint32_t)(x >> 32) == tag;
+                    val[k] = __uint_as_float((uint32_t)x);
+                }
+                if (__all(ok)) break;
+                if (__builtin_amdgcn_s_memrealtime() > t_end) {
+                    failed = true;
+                    if (lane == 0) *xfail = 1;
+                    break;
+                }
+            }
+            XPHASE(5);
+#pragma unroll
+            for (int k = 0; k < KW; ++k) {
+                val[k] += __shfl_xor(val[k], 1, 64);
+                val[k] += __shfl_xor(val[k], 2, 64);
+                val[k] += __shfl_xor(val[k], 4, 64);
+            }
+            // lane (slot sl, member m) finishes coordinate sl + 8m when m < KW
+            if (m < KW) {
+                float ep = val[0];
+#pragma unroll
+                for (int k = 1; k < KW; ++k) ep = m == k ? val[k] : ep;
+                const int v = vw + sl + 8 * m, r = v / XD, q = v % XD, row = row0 + r;
+                ep += bb[3 * H + q];
+                const float* sc = sch + t * DPPO_SCHED_COLS;
+                float sd = expf(0.5f * sc[4]);
+                if (a.deterministic && t == 0) sd = 0.f;
+                else if (a.deterministic) sd = fminf(fmaxf(sd, 1e-3f), 1e6f);
+                else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
+                const float x = xs[v];
+                float xr = sc[0] * x - sc[1] * ep;                   // x0 reconstruction (:198-201)
+                xr = fminf(fmaxf(xr, -1.f), 1.f);                    // denoised_clip_value = 1 (diffusion.py:28)
+                const float mu = sc[2] * xr + sc[3] * x;             // posterior mean (:239-242)
+                float y = mu + sd * zt[i * 16 * XD + v];             // (:301-320)
+                if (a.final_clip > 0.f && i == K - 1) y = fminf(fmaxf(y, -a.final_clip), a.final_clip);
+                if (failed) y = __builtin_nanf("");
+                xs[v] = y;
+                a0[r * lda0 + q] = Pol::cvt(y);
+                if (c == 0 && row < a.E) {
+                    if (a.chains && t <= KF) a.chains[((size_t)row * (KF + 1) + (KF - t)) * XD + q] = y;
+                    if (i == K - 1) {
+                        a.actions[(size_t)row * XD + q] = y;
+                        if (a.actions_host) a.actions_host[(size_t)row * XD + q] = y;
+                    }
+                }
+            }
+        }
+        lds_sync();
+        XPHASE(6);
+    }
+    if (c == 0 && a.done) {   // publish: every writer's stores reach the system before the counter moves
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) {
+            if (*xfail) __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+size_t split_lds_bytes(int XD, int SD, int TD, int K, int KSI, int NO) {
+    const int pad = 16, ldh = SPLIT_H + pad, lda0 = KSI * 32 + pad, KP = SW / (SPLIT_H / 16 / SPLIT_P);
+    const int ldp = SPLIT_H / SPLIT_P + 4;
+    size_t o = 0;
+    o += dppo_align16(2 * 16 * lda0);
+    o += dppo_align16(2 * 16 * ldh);
+    o += dppo_align16(4 * KP * 16 * ldp);
+    o += dppo_align16(4 * SW * 16 * XD);
+    o += 16;
+    o += dppo_align16(4 * 16 * XD);
+    o += dppo_align16(4 * 16 * SD);
+    o += dppo_align16(4 * K * TD);
+    o += dppo_align16(4 * K * DPPO_SCHED_COLS);
+    o += dppo_align16(4 * 2 * (3 * SPLIT_H + 16 * NO));
+    o += dppo_align16(4 * K * 16 * XD);
+    o += (size_t)SW * 2 * NO * 1024;
+    return o;
+}
+
+// exchange buffers: one per stream (launches on one stream are ordered, so they can share one)
+struct XchgBuf {
+    hipStream_t stream;
+    int device;
+    uint64_t* buf;
+    uint32_t seq;
+};
+std::mutex g_xmu;
+XchgBuf g_xb[16];
+int g_nxb = 0;
+int g_cus = 0;
+
+int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq) {
+    int dev = 0;
+    DPPO_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_xmu);
+    for (int i = 0; i < g_nxb; ++i)
+        if (g_xb[i].stream == s && g_xb[i].device == dev) {
+            *buf = g_xb[i].buf;
+            *seq = g_xb[i].seq = (g_xb[i].seq + 1) & 0x03FFFFFFu;
+            return DPPO_OK;
+        }
+    if (g_nxb == 16) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler: more than 16 streams");
+    XchgBuf& x = g_xb[g_nxb];
+    const size_t bytes = sizeof(uint64_t) * 2 * XMAX_G * SPLIT_P * XMAX_NV;
+    DPPO_HIP(hipMalloc((void**)&x.buf, bytes));
+    DPPO_HIP(hipMemset(x.buf, 0, bytes));
+    x.stream = s; x.device = dev; x.seq = 1;
+    ++g_nxb;
+    *buf = x.buf;
+    *seq = x.seq;
+    return DPPO_OK;
+}
+
+int device_cus() {
+    if (!g_cus) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            g_cus = n;
+    }
+    return g_cus;
+}
+
+template <int XQ, int KSI, bool INJ>
+int launch_split_k(const SplitArgs& sa, hipStream_t s) {
+    constexpr int NO = (4 * XQ + 15) / 16;
+    auto k = sample_split_kernel<SPLIT_P, XQ, KSI, INJ>;
+    const SampleArgs& a = sa.a;
+    const size_t lds = split_lds_bytes(a.XD, a.SD, a.TD, a.K, KSI, NO);
+    if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler needs %zu B of LDS", lds);
+    DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int blocks = 8 * SPLIT_P * ((sa.G + 7) / 8);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(SW * 64), lds, s, sa);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+}  // namespace
+
+bool sample_split_supported(int precision, int H, int XD, int ks_in, int E, int K) {
+    if (precision != DPPO_BF16 || H != SPLIT_H || XD % 4 != 0 || XD > 32 || ks_in != 2 || K > 63) return false;
+    const int G = dppo_cdiv(E, 16);
+    if (G < 1 || G > XMAX_G) return false;
+    const int cus = device_cus();
+    return cus == 0 || 8 * SPLIT_P * ((G + 7) / 8) <= cus;   // every workgroup of the launch co-resident
+}
+
+int split_sampler_members() { return SPLIT_P; }
+
+int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s) {
+    if (!sample_split_supported(precision, a.H, a.XD, a.L.ks_in, a.E, a.K)) return DPPO_EUNSUPPORTED;
+    SplitArgs sa;
+    sa.a = a;
+    sa.G = dppo_cdiv(a.E, 16);
+    int rc = xchg_for(s, &sa.xbuf, &sa.seq);
+    if (rc) return rc;
+    const bool inj = a.noise != nullptr;
+    switch (a.XD / 4) {
+#define DPPO_SPLIT_CASE(xq) \
+    case xq: return inj ? launch_split_k<xq, 2, true>(sa, s) : launch_split_k<xq, 2, false>(sa, s);
+        DPPO_SPLIT_CASE(1) DPPO_SPLIT_CASE(2) DPPO_SPLIT_CASE(3) DPPO_SPLIT_CASE(4)
+        DPPO_SPLIT_CASE(5) DPPO_SPLIT_CASE(6) DPPO_SPLIT_CASE(7) DPPO_SPLIT_CASE(8)
+#undef DPPO_SPLIT_CASE
+        default: return DPPO_EUNSUPPORTED;
+    }
+}

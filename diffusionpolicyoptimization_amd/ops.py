@@ -149,6 +149,14 @@ def sample(d: ModelDims, precision, packed_base, packed_ft, sched, cond, x_T=Non
     return actions, chains
 
 
+def sampler_layout(d: ModelDims, precision, n_envs):
+    """Workgroups per 16-env tile of the sampler dppo_sample runs for n_envs envs: 0 = the
+    weight-streaming kernel, P > 0 = the split register-resident kernel (include/dppo.h)."""
+    m = ctypes.c_int()
+    _lib.call("dppo_sampler_layout", ctypes.byref(d.c()), _prec(precision), int(n_envs), ctypes.byref(m))
+    return m.value
+
+
 class SampleStepper:
     """dppo_sample_step with every argument but the step index, call counter and mode bound once
     (the rollout's buffers never move), so a rollout step costs one ctypes call."""

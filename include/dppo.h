@@ -95,6 +95,14 @@ DPPO_API int dppo_sample(const dppo_dims* d, int precision, const void* packed_b
  * time for the per-CU load-path figure. Also returns the waves per workgroup. */
 DPPO_API int dppo_sampler_stream_bytes(const dppo_dims* d, int precision, int64_t* bytes_per_tile, int* waves);
 
+/* Which sampler layout dppo_sample runs for n_envs envs: *members = 0 for the weight-streaming
+ * kernel (one workgroup per 16-env tile), or P > 0 for the split register-resident kernel (P
+ * workgroups per 16-env tile, one in-launch partial-sum exchange per denoising step; bf16,
+ * actor_hidden 512, horizon*action_dim a multiple of 4, <= 512 envs). The split kernel keeps one
+ * 2 MiB exchange buffer per stream, allocated by the library on the first launch on that stream
+ * (the one allocation outside a caller workspace). */
+DPPO_API int dppo_sampler_layout(const dppo_dims* d, int precision, int n_envs, int* members);
+
 /* One rollout step (agent/finetune/train_ppo_diffusion_agent.py:106-122) in one call:
  * hipMemcpyAsync(cond <- cond_host [host, pinned]), dppo_sample with the Philox noise, hipMemcpyAsync
  * (actions_host [host, pinned] <- actions), then hipStreamSynchronize when synchronize != 0. */

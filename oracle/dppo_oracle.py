@@ -114,9 +114,11 @@ def _ident(x):
     return np.asarray(x, np.float64)
 
 
-def residual_mlp_forward(p, x, act, prefix, rnd=None):
+def residual_mlp_forward(p, x, act, prefix, rnd=None, round_h3=True):
     """rnd: optional operand-rounding function applied exactly where the bf16 kernels round
-    (GEMM A/B operands; accumulators, residual h1 and epilogues stay fp32). None = exact f64."""
+    (GEMM A/B operands; accumulators, residual h1 and epilogues stay fp32). None = exact f64.
+    round_h3=False: the out-Dense input is not rounded (the split sampler feeds it as a hi/lo
+    bf16 pair, sampler_split.hip), only its weights are."""
     a, _ = ACT[act]
     R = rnd or _ident
     xr = R(x)
@@ -125,7 +127,7 @@ def residual_mlp_forward(p, x, act, prefix, rnd=None):
     h2 = u1 @ R(p[prefix + "l1_w"]) + np.asarray(p[prefix + "l1_b"], np.float64)
     u2 = R(a(h2))
     h3 = u2 @ R(p[prefix + "l2_w"]) + np.asarray(p[prefix + "l2_b"], np.float64) + h1
-    h3r = R(h3)
+    h3r = R(h3) if round_h3 else np.asarray(h3, np.float64)
     y = h3r @ R(p[prefix + "out_w"]) + np.asarray(p[prefix + "out_b"], np.float64)
     return y, dict(x=xr, h1=h1, u1=u1, h2=h2, u2=u2, h3=h3r, R=R)
 
@@ -175,12 +177,12 @@ def time_mlp_backward(p, cache, dtemb):
     return g
 
 
-def diffusion_mlp_forward(p, x, t, state, act="ReLU", rnd=None):
+def diffusion_mlp_forward(p, x, t, state, act="ReLU", rnd=None, round_h3=True):
     """x [B,Ta,Da], t [B] int, state [B,To,Do] -> eps [B,Ta,Da]; cond concat [x, t_emb, state] (:86)."""
     B = x.shape[0]
     temb, tcache = time_mlp_forward(p, t)
     inp = np.concatenate([x.reshape(B, -1), temb, state.reshape(B, -1)], axis=-1).astype(np.float64)
-    y, cache = residual_mlp_forward(p, inp, act, "", rnd)
+    y, cache = residual_mlp_forward(p, inp, act, "", rnd, round_h3)
     cache["time"] = tcache
     cache["t"] = np.asarray(t)
     return y.reshape(x.shape), cache
@@ -226,9 +228,9 @@ def p_mean_var(sched, eps, x, t, denoised_clip=1.0):
 # a9: sampler VPGDiffusion.call (diffusion_vpg.py:250-339), DDPM, with injected noise
 # ----------------------------------------------------------------------------------------------
 def sample(p_base, p_ft, sched, state, x_T, z, ft_steps, deterministic=False, min_std=0.1,
-           randn_clip=3.0, final_clip=None, rnd=None):
+           randn_clip=3.0, final_clip=None, rnd=None, round_h3=True):
     """state [E,To,Do]; x_T [E,Ta,Da]; z [K,E,Ta,Da] raw N(0,1) draws for loop index i (t=K-1-i).
-    Returns (trajectories [E,Ta,Da], chains [E,K'+1,Ta,Da])."""
+    Returns (trajectories [E,Ta,Da], chains [E,K'+1,Ta,Da]). round_h3: see residual_mlp_forward."""
     K = z.shape[0]
     x = np.asarray(x_T, np.float64)
     chain = []
@@ -238,7 +240,7 @@ def sample(p_base, p_ft, sched, state, x_T, z, ft_steps, deterministic=False, mi
         t = K - 1 - i
         tb = np.full(x.shape[0], t)
         params = p_ft if t < ft_steps else p_base                # :161-180
-        eps, _ = diffusion_mlp_forward(params, x, tb, state, rnd=rnd)
+        eps, _ = diffusion_mlp_forward(params, x, tb, state, rnd=rnd, round_h3=round_h3)
         mu, logvar, _ = p_mean_var(sched, eps, x, tb)
         std = np.exp(0.5 * logvar)                               # :301
         if deterministic and t == 0:                             # :310-315

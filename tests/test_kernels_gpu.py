@@ -43,8 +43,10 @@ def test_sampler_injected_noise(cuda, precision, tol, dims):
     state = rng.uniform(-1, 1, (E, d.cond_steps, d.obs_dim)).astype(np.float32)
     xT = rng.standard_normal((E, d.horizon_steps, d.action_dim)).astype(np.float32)
     z = rng.standard_normal((d.denoising_steps, E, d.horizon_steps, d.action_dim)).astype(np.float32)
+    split = ops.sampler_layout(d, precision, E) > 0
+    assert split == (precision == "bf16"), "bf16 at 37 envs runs the split sampler by default"
     ref_a, ref_c = O.sample(to_f64(base), to_f64(ft), sched, state.astype(np.float64), xT, z, d.ft_denoising_steps,
-                            rnd=_rnd(precision))
+                            rnd=_rnd(precision), round_h3=not split)
     packb, packf = ops.pack_actor(d, pb, precision), ops.pack_actor(d, pf, precision)
     act, ch = ops.sample(d, precision, packb, packf, tab, torch.tensor(state.reshape(E, -1), device=cuda),
                          x_T=torch.tensor(xT.reshape(E, -1), device=cuda),
@@ -79,6 +81,53 @@ def test_sampler_philox_stream(cuda):
                          seed=seed, call_id=call)
     torch.cuda.synchronize()
     assert np.abs(act.cpu().numpy().reshape(ref_a.shape) - ref_a).max() < 1e-3
+
+
+@pytest.mark.parametrize("E", [1, 16, 130, 512, 513])
+def test_sampler_bf16_sizes_philox(cuda, E):
+    """bf16 sampler with its own Philox noise at group boundaries (1, 16), a ragged multi-XCD size
+    (130 envs = 9 groups), the split kernel's maximum (512 envs = 256 workgroups) and one env past
+    it (513: the weight-streaming kernel). Checked against the oracle rounding at the kernel's
+    rounding points, given the same Philox draws."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    split = ops.sampler_layout(d, "bf16", E) > 0
+    assert split == (E <= 512)
+    seed, call = 987654321, 3
+    rng = np.random.default_rng(E)
+    state = rng.uniform(-1, 1, (E, 1, d.obs_dim)).astype(np.float32)
+    xT = PX.sampler_normals(seed, call, 0, E, d.xd, d.denoising_steps).reshape(E, d.horizon_steps, d.action_dim)
+    z = np.stack([PX.sampler_normals(seed, call, 0, E, d.xd, i) for i in range(d.denoising_steps)])
+    z = z.reshape(d.denoising_steps, E, d.horizon_steps, d.action_dim)
+    ref_a, ref_c = O.sample(to_f64(base), to_f64(ft), sched, state.astype(np.float64), xT, z, d.ft_denoising_steps,
+                            rnd=O.round_bf16, round_h3=not split)
+    packb, packf = ops.pack_actor(d, pb, "bf16"), ops.pack_actor(d, pf, "bf16")
+    act, ch = ops.sample(d, "bf16", packb, packf, tab, torch.tensor(state.reshape(E, -1), device=cuda),
+                         seed=seed, call_id=call)
+    torch.cuda.synchronize()
+    act = act.cpu().numpy().reshape(ref_a.shape)
+    ch = ch.cpu().numpy().reshape(ref_c.shape)
+    assert np.isfinite(act).all() and np.isfinite(ch).all()
+    dev = np.abs(act - ref_a)
+    assert np.quantile(dev, 0.99) < 2e-3 and np.abs(ch - ref_c).mean() < 2e-3, (dev.max(), np.quantile(dev, 0.99))
+
+
+def test_sampler_split_repeatable(cuda):
+    """Back-to-back launches of the split sampler on the same stream reuse one exchange buffer with
+    new tags: identical inputs give bit-identical outputs, launch after launch."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    E = 64
+    assert ops.sampler_layout(d, "bf16", E) > 0
+    rng = np.random.default_rng(9)
+    cond = torch.tensor(rng.uniform(-1, 1, (E, d.sd)).astype(np.float32), device=cuda)
+    packb, packf = ops.pack_actor(d, pb, "bf16"), ops.pack_actor(d, pf, "bf16")
+    outs = [ops.sample(d, "bf16", packb, packf, tab, cond, seed=5, call_id=11)[0].clone() for _ in range(20)]
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
 
 
 def test_sampler_deterministic_and_empty(cuda):

@@ -11,6 +11,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def _split(m, envs):
+    from diffusionpolicyoptimization_amd import ops
+    return ops.sampler_layout(m.dims, m.precision, envs) > 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=64)
@@ -55,6 +60,17 @@ def main():
         lib.dppo_debug_sampler_cycles(buf, 1)
         wgs = (args.envs + 15) // 16
         phases = {f"s{i}": round(buf[i] / wgs / (d.denoising_steps if i else 1)) for i in range(7)}
+    if hasattr(lib, "dppo_debug_split_cycles") and _split(m, args.envs):   # split kernel phases
+        import ctypes
+        buf = (ctypes.c_ulonglong * (16 + 64 * 8))()
+        lib.dppo_debug_split_cycles(buf, 1)
+        m(cond)
+        torch.cuda.synchronize()
+        lib.dppo_debug_split_cycles(buf, 1)
+        wgs = 8 * ((args.envs + 15) // 16)
+        names = ["prologue", "switch", "in", "l1", "l2_out", "xchg", "epilogue"]
+        phases = {n: round(buf[i] / wgs / (1 if i < 2 else d.denoising_steps)) for i, n in enumerate(names)}
+        phases["wg0_steps"] = [[int(buf[16 + 8 * i + k]) for k in range(1, 7)] for i in range(d.denoising_steps)]
     print(json.dumps({"tag": args.tag, "envs": args.envs, "precision": args.precision, "ms_per_launch": ms,
                       "tflops": flops / (ms * 1e-3) / 1e12, "cycles_per_step": phases}), flush=True)
 

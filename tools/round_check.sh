@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU tests + bench + sampler profile in one gpurun call (each step time-limited, chained).
+# usage: tools/round_check.sh <tag>
+set -o pipefail
+tag=${1:-chk}
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_$tag.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/gpu_tests_$tag.log; exit 1; }
+tail -3 gpurun_out/gpu_tests_$tag.log
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_$tag.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench_$tag.log; exit 1; }
+tail -1 gpurun_out/bench_$tag.log
+timeout -k 10 100 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$tag.log 2>&1 || { echo smoke failed; tail -20 gpurun_out/smoke_$tag.log; exit 1; }
+tail -1 gpurun_out/smoke_$tag.log
+bash tools/profile_sampler.sh $tag && echo profiled
