@@ -315,6 +315,9 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 pk[1] = pack_bf16x2(fmaxf(h1[n][2], 0.f), fmaxf(h1[n][3], 0.f));
                 *(u32x2*)(u1 + env * ldh + f) = pk;
             }
+            // the residual term member 0 adds to its l2 partial: h1 + b_l2 (mlp.py:206)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) h1[n] += *(const f32x4*)(bb + 2 * H + 16 * (4 * wave + n) + 4 * jq);
         }
         lds_sync();
         XPHASE(2);
@@ -362,10 +365,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
             if (pre) load_l2(PKn);
             if (c == 0) {                                    // + b_l2 + h1 (residual), once per group
 #pragma unroll
-                for (int n = 0; n < 4; ++n) {
-                    const f32x4 bv = *(const f32x4*)(bb + 2 * H + 16 * (4 * wave + n) + 4 * jq);
-                    h3[n] += bv + h1[n];
-                }
+                for (int n = 0; n < 4; ++n) h3[n] += h1[n];
             }
         }
         // ---- out-Dense partial (transposed) from this wave's own h3 registers: k-step s covers
@@ -423,6 +423,15 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 a0[r * lda0 + XD + cc] = Pol::cvt(temb[(t - 1) * TD + cc]);
             }
             const int m = lane & 7, sl = lane >> 3;
+            // this lane's epilogue inputs, read while the members arrive
+            const int ve = vw + sl + 8 * (m < KW ? m : 0), re = ve / XD, qe = ve % XD;
+            const float* sc = sch + t * DPPO_SCHED_COLS;
+            const float c0 = sc[0], c1 = sc[1], c2 = sc[2], c3 = sc[3];
+            float sd = expf(0.5f * sc[4]);
+            if (a.deterministic && t == 0) sd = 0.f;
+            else if (a.deterministic) sd = fminf(fmaxf(sd, 1e-3f), 1e6f);
+            else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
+            const float xe = xs[ve], ze = zt[i * 16 * XD + ve], be = bb[3 * H + qe];
             const uint64_t* src = xb + (size_t)m * NV + vw + sl;
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
             float val[KW];
@@ -454,18 +463,13 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 float ep = val[0];
 #pragma unroll
                 for (int k = 1; k < KW; ++k) ep = m == k ? val[k] : ep;
-                const int v = vw + sl + 8 * m, r = v / XD, q = v % XD, row = row0 + r;
-                ep += bb[3 * H + q];
-                const float* sc = sch + t * DPPO_SCHED_COLS;
-                float sd = expf(0.5f * sc[4]);
-                if (a.deterministic && t == 0) sd = 0.f;
-                else if (a.deterministic) sd = fminf(fmaxf(sd, 1e-3f), 1e6f);
-                else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
-                const float x = xs[v];
-                float xr = sc[0] * x - sc[1] * ep;                   // x0 reconstruction (:198-201)
+                const int v = ve, r = re, q = qe, row = row0 + r;
+                ep += be;
+                const float x = xe;
+                float xr = c0 * x - c1 * ep;                         // x0 reconstruction (:198-201)
                 xr = fminf(fmaxf(xr, -1.f), 1.f);                    // denoised_clip_value = 1 (diffusion.py:28)
-                const float mu = sc[2] * xr + sc[3] * x;             // posterior mean (:239-242)
-                float y = mu + sd * zt[i * 16 * XD + v];             // (:301-320)
+                const float mu = c2 * xr + c3 * x;                   // posterior mean (:239-242)
+                float y = mu + sd * ze;                              // (:301-320)
                 if (a.final_clip > 0.f && i == K - 1) y = fminf(fmaxf(y, -a.final_clip), a.final_clip);
                 if (failed) y = __builtin_nanf("");
                 xs[v] = y;
