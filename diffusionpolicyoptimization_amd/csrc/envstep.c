@@ -33,30 +33,36 @@ DPPO_ENV_API int dppo_env_step(int E, int Do, int Da, int act_steps, int Ta, int
                                 double* __restrict__ state, int64_t* __restrict__ cnt, const float* __restrict__ actions,
                                 double* __restrict__ reward, uint8_t* __restrict__ terminated,
                                 uint8_t* __restrict__ truncated, float* __restrict__ obs_out) {
-    v4d s[MAXD][NV], ac[MAXD][NV];
-    double rsum[EB], alive[EB];
-    int64_t ct[EB];
+    v4d s[MAXD][NV], s2[MAXD][NV], acl[MAXD][NV];
+    double sbuf[EB];
     const int nsub = act_steps < Ta ? act_steps : Ta;
+    const v4d vmax = v4_splat((double)max_steps), one = v4_splat(1.0), zero = v4_splat(0.0);
+    const v4d inv_do = v4_splat(1.0 / Do), c_a = v4_splat(0.01 / Da);
     int n_done = 0;
     for (int e0 = 0; e0 < E; e0 += EB) {
         const int nb = E - e0 < EB ? E - e0 : EB;
-        for (int b = 0; b < EB; ++b) {
-            const int e = e0 + (b < nb ? b : 0);
-            for (int j = 0; j < Do; ++j) s[j][b >> 2][b & 3] = state[(size_t)e * Do + j];
-            ct[b] = cnt[e];
-            rsum[b] = 0.0;
-            alive[b] = b < nb ? 1.0 : 0.0;
+        v4d ct[NV], rsum[NV], alive[NV];   /* alive: 1.0 / 0.0 per env */
+        for (int j = 0; j < Do; ++j) {
+            for (int b = 0; b < EB; ++b) sbuf[b] = state[(size_t)(e0 + (b < nb ? b : 0)) * Do + j];
+            for (int v = 0; v < NV; ++v) s[j][v] = (v4d){sbuf[4 * v], sbuf[4 * v + 1], sbuf[4 * v + 2], sbuf[4 * v + 3]};
+        }
+        for (int b = 0; b < EB; ++b) sbuf[b] = (double)cnt[e0 + (b < nb ? b : 0)];
+        for (int v = 0; v < NV; ++v) {
+            ct[v] = (v4d){sbuf[4 * v], sbuf[4 * v + 1], sbuf[4 * v + 2], sbuf[4 * v + 3]};
+            rsum[v] = zero;
+            alive[v] = (v4d){4 * v < nb, 4 * v + 1 < nb, 4 * v + 2 < nb, 4 * v + 3 < nb};
         }
         for (int k = 0; k < nsub; ++k) {
-            for (int b = 0; b < EB; ++b) {
-                const float* a = actions + ((size_t)(e0 + (b < nb ? b : 0)) * Ta + k) * Da;
-                for (int i = 0; i < Da; ++i) ac[i][b >> 2][b & 3] = (double)a[i];
+            v4d asq[NV], err[NV];
+            for (int v = 0; v < NV; ++v) { asq[v] = zero; err[v] = zero; }
+            for (int i = 0; i < Da; ++i) {
+                for (int b = 0; b < EB; ++b) sbuf[b] = (double)actions[((size_t)(e0 + (b < nb ? b : 0)) * Ta + k) * Da + i];
+                for (int v = 0; v < NV; ++v) {
+                    const v4d x = (v4d){sbuf[4 * v], sbuf[4 * v + 1], sbuf[4 * v + 2], sbuf[4 * v + 3]};
+                    asq[v] += x * x;
+                    acl[i][v] = v4_clamp1(x);
+                }
             }
-            v4d asq[NV], err[NV], acl[MAXD][NV];
-            for (int v = 0; v < NV; ++v) { asq[v] = v4_splat(0.0); err[v] = v4_splat(0.0); }
-            for (int i = 0; i < Da; ++i)
-                for (int v = 0; v < NV; ++v) { asq[v] += ac[i][v] * ac[i][v]; acl[i][v] = v4_clamp1(ac[i][v]); }
-            v4d s2[MAXD][NV];
             for (int j = 0; j < Do; ++j) {
                 v4d acc[NV];
                 for (int v = 0; v < NV; ++v) acc[v] = v4_splat(c[j]);
@@ -70,31 +76,40 @@ DPPO_ENV_API int dppo_env_step(int E, int Do, int Da, int act_steps, int Ta, int
                 }
                 const v4d gj = v4_splat(goal[j]);
                 for (int v = 0; v < NV; ++v) {
-                    s2[j][v] = v4_clamp1(acc[v]);
-                    const v4d d = s2[j][v] - gj;
+                    const v4d n = v4_clamp1(acc[v]);
+                    const v4d d = n - gj;
                     err[v] += d * d;
+                    acc[v] = n;
                 }
+                /* s[j] is read by later rows j' of this sub-step: keep the new row aside */
+                for (int v = 0; v < NV; ++v) s2[j][v] = acc[v];
             }
-            for (int b = 0; b < EB; ++b) {
-                if (alive[b] != 0.0) {
-                    for (int j = 0; j < Do; ++j) s[j][b >> 2][b & 3] = s2[j][b >> 2][b & 3];
-                    ct[b] += 1;
-                    rsum[b] += 1.0 - err[b >> 2][b & 3] / Do - 0.01 * asq[b >> 2][b & 3] / Da;
-                    if (ct[b] >= max_steps) alive[b] = 0.0;
-                }
+            for (int v = 0; v < NV; ++v) {
+                const __m256d m = _mm256_cmp_pd((__m256d)alive[v], (__m256d)zero, _CMP_NEQ_OQ);
+                for (int j = 0; j < Do; ++j) s[j][v] = (v4d)_mm256_blendv_pd((__m256d)s[j][v], (__m256d)s2[j][v], m);
+                ct[v] += alive[v];
+                rsum[v] += alive[v] * (one - err[v] * inv_do - asq[v] * c_a);
+                alive[v] = (v4d)_mm256_and_pd((__m256d)alive[v], _mm256_cmp_pd((__m256d)ct[v], (__m256d)vmax, _CMP_LT_OQ));
             }
         }
-        for (int b = 0; b < nb; ++b) {
-            const int e = e0 + b;
-            for (int j = 0; j < Do; ++j) state[(size_t)e * Do + j] = s[j][b >> 2][b & 3];
-            cnt[e] = ct[b];
-            reward[e] = rsum[b];
-            terminated[e] = 0;
-            truncated[e] = ct[b] >= max_steps;
-            n_done += truncated[e];
-            for (int o = 0; o < n_obs_steps; ++o)
-                for (int j = 0; j < Do; ++j) obs_out[((size_t)e * n_obs_steps + o) * Do + j] = (float)s[j][b >> 2][b & 3];
+        for (int j = 0; j < Do; ++j) {
+            for (int v = 0; v < NV; ++v) for (int q = 0; q < 4; ++q) sbuf[4 * v + q] = s[j][v][q];
+            for (int b = 0; b < nb; ++b) {
+                const int e = e0 + b;
+                state[(size_t)e * Do + j] = sbuf[b];
+                for (int o = 0; o < n_obs_steps; ++o) obs_out[((size_t)e * n_obs_steps + o) * Do + j] = (float)sbuf[b];
+            }
         }
+        for (int v = 0; v < NV; ++v)
+            for (int q = 0; q < 4; ++q) {
+                const int b = 4 * v + q, e = e0 + b;
+                if (b >= nb) continue;
+                cnt[e] = (int64_t)ct[v][q];
+                reward[e] = rsum[v][q];
+                terminated[e] = 0;
+                truncated[e] = ct[v][q] >= (double)max_steps;
+                n_done += truncated[e];
+            }
     }
     return n_done;
 }

@@ -69,7 +69,25 @@ extern "C" DPPO_API int dppo_debug_split_cycles(unsigned long long* out, int res
 #define XSTEP(i) do {} while (0)
 #endif
 
+// Host hand-off of a pipelined step (DPPO_SPLIT_SIGNAL, tuning knob):
+//   0: acquire poll of go per iteration; plain output stores; __threadfence_system() + release add
+//   1: relaxed poll of go + one system acquire after it matches
+//   2: 1 + the launch's device outputs stored write-through (sc1), so the final system release
+//      has no dirty L2 lines to write back
+#ifndef DPPO_SPLIT_SIGNAL
+#define DPPO_SPLIT_SIGNAL 2
+#endif
+
 namespace {
+
+// a store of a kernel output that leaves no dirty line in L2 (write-through; see DPPO_SPLIT_SIGNAL)
+__device__ inline void store_out(float* p, float v) {
+#if DPPO_SPLIT_SIGNAL >= 2
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p = v;
+#endif
+}
 
 constexpr int SW = 8;              // waves per workgroup
 constexpr int SPLIT_P = 8;         // workgroups (CUs) per 16-env group
@@ -238,31 +256,40 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 zt[(step * 16 + r) * XD + q] = fminf(fmaxf(z[k], -a.randn_clip), a.randn_clip);
             } else {
                 xs[r * XD + q] = z[k];
-                if (KF == K && c == 0 && a.chains && row < a.E) a.chains[((size_t)row * (KF + 1) + 0) * XD + q] = z[k];
+                if (KF == K && c == 0 && a.chains && row < a.E) store_out(a.chains + ((size_t)row * (KF + 1) + 0) * XD + q, z[k]);
             }
         }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0): the resident set has landed
     permute_out();
     // pre-enqueued rollout step: wait for the host's observation (bounded, as sampler.hip)
+    XPHASE(7);                                              // timing builds: phase 7 = prologue before the wait
     if (a.go) {
         if (tid == 0) {
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;   // 100 MHz: 4 s
+#if DPPO_SPLIT_SIGNAL >= 1
+            while (__hip_atomic_load(a.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
+#else
             while (__hip_atomic_load(a.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
+#endif
                 __builtin_amdgcn_s_sleep(8);
                 if (__builtin_amdgcn_s_memrealtime() > t_end) {
                     if (c == 0) __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
             }
+#if DPPO_SPLIT_SIGNAL >= 1
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");    // one system acquire after the match
+#endif
         }
         __syncthreads();
     }
+    XPHASE(8);                                              // phase 8 = the wait for go
     for (int i = tid; i < 16 * SD; i += ST) {
         const int r = i / SD, cc = i % SD, row = row0 + r;
         const float v = row < a.E ? a.cond[(size_t)row * SD + cc] : 0.f;
         st[i] = v;
-        if (a.cond_out && c == 0 && row < a.E) a.cond_out[(size_t)row * SD + cc] = v;
+        if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, v);
     }
     __syncthreads();
     const int k1w = KSI * 32;
@@ -475,9 +502,9 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 xs[v] = y;
                 a0[r * lda0 + q] = Pol::cvt(y);
                 if (c == 0 && row < a.E) {
-                    if (a.chains && t <= KF) a.chains[((size_t)row * (KF + 1) + (KF - t)) * XD + q] = y;
+                    if (a.chains && t <= KF) store_out(a.chains + ((size_t)row * (KF + 1) + (KF - t)) * XD + q, y);
                     if (i == K - 1) {
-                        a.actions[(size_t)row * XD + q] = y;
+                        store_out(a.actions + (size_t)row * XD + q, y);
                         if (a.actions_host) a.actions_host[(size_t)row * XD + q] = y;
                     }
                 }
@@ -486,6 +513,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
         lds_sync();
         XPHASE(6);
     }
+    XPHASE(9);                                              // phase 9 = loop end -> done signal
     if (c == 0 && a.done) {   // publish: every writer's stores reach the system before the counter moves
         __threadfence_system();
         __syncthreads();
@@ -494,6 +522,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
             __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+    XPHASE(10);                                             // phase 10 = the done signal (member 0)
 }
 
 size_t split_lds_bytes(int XD, int SD, int TD, int K, int KSI, int NO) {
