@@ -42,35 +42,73 @@ extern "C" DPPO_API int dppo_debug_phase_cycles(unsigned long long* out, int res
 #define PHASE_START do {} while (0)
 #endif
 
-// Accumulator tile -> feature-major image XT[col][row] (4 consecutive rows per lane per MFMA
-// tile). Buffer stores through ONE resource for the whole workspace: the per-lane part of the
-// offset is a single 32-bit VGPR, the image / tile parts are scalar, so no 64-bit address pairs
-// are kept live across the unrolled layers.
+// Feature-major images XT[col][row] hold the rows of each 16*MT-row tile in a PERMUTED order:
+// position p of a tile holds row img_row(p), so that the 8 rows one lane holds for a column across
+// an (even, odd) pair of MFMA tiles (rows 16m + 4j + 0..3 of tiles m = 2P, 2P+1, j = lane >> 4) are
+// 8 consecutive positions and leave as ONE 16-byte store (8-byte per-lane stores made the image
+// writes store-issue bound). Every image of a dW pair and the actor's seg[] use the same order;
+// the dW GEMM sums over rows, so the order is invisible in its result.
+__device__ inline int img_pos(int r) {
+    const int m = r >> 4;
+    return 32 * (m >> 1) + 8 * ((r >> 2) & 3) + 4 * (m & 1) + (r & 3);
+}
+__device__ inline int img_row(int p) {
+    return 16 * (2 * (p >> 5) + ((p >> 2) & 1)) + 4 * ((p >> 3) & 3) + (p & 3);
+}
+
+// Accumulator tile -> feature-major image. Buffer stores through ONE resource for the whole
+// workspace: the per-lane part of the offset is a single 32-bit VGPR, the image / tile parts are
+// scalar, so no 64-bit address pairs are kept live across the unrolled layers.
 template <class P, int MT, int NT>
 __device__ inline void store_accT(__amdgpu_buffer_rsrc_t ws, uint32_t img_off, uint32_t ldm, int ntile0, uint32_t grow0,
                                   int lane, const f32x4 (&v)[MT][NT]) {
+    static_assert(MT % 2 == 0, "image rows are permuted over MFMA tile pairs");
     using AT = typename P::AT;
     constexpr uint32_t es = sizeof(AT);
-    const uint32_t vo = ((uint32_t)ccol(lane) * ldm + (uint32_t)((lane >> 4) << 2)) * es;
+    const uint32_t vo = ((uint32_t)ccol(lane) * ldm + (uint32_t)((lane >> 4) << 3)) * es;
     const uint32_t so0 = img_off + ((uint32_t)ntile0 * 16u * ldm + grow0) * es;
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+    for (int mp = 0; mp < MT / 2; ++mp)
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
-            const uint32_t so = so0 + ((uint32_t)n * 16u * ldm + (uint32_t)m * 16u) * es;
+            const uint32_t so = so0 + ((uint32_t)n * 16u * ldm + (uint32_t)mp * 32u) * es;
+            const f32x4 lo = v[2 * mp][n], hi = v[2 * mp + 1][n];
             if constexpr (es == 2) {
-                __bf16 e[4] = {(__bf16)v[m][n][0], (__bf16)v[m][n][1], (__bf16)v[m][n][2], (__bf16)v[m][n][3]};
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, e), ws, vo, so, 0);
+                __bf16 e[8] = {(__bf16)lo[0], (__bf16)lo[1], (__bf16)lo[2], (__bf16)lo[3],
+                               (__bf16)hi[0], (__bf16)hi[1], (__bf16)hi[2], (__bf16)hi[3]};
+                // soffset must be the literal 0: with an SGPR there, hipcc (ROCm 7.2) does not guard
+                // the >8-byte store-data hazard (a following VALU overwrote the 4th dword)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, e), ws, vo + so, 0, 0);
             } else {
-                // two 8-B stores: the 16-B buffer_store form came out with a corrupted 4th dword
-                // under hipcc 7.2 for gfx950 in the critic (a store-data hazard the compiler does
-                // not guard); 8-B stores are what the bf16 path uses and are exact here
-                const u32x2 w0 = {__float_as_uint(v[m][n][0]), __float_as_uint(v[m][n][1])};
-                const u32x2 w1 = {__float_as_uint(v[m][n][2]), __float_as_uint(v[m][n][3])};
-                __builtin_amdgcn_raw_buffer_store_b64(w0, ws, vo, so, 0);
-                __builtin_amdgcn_raw_buffer_store_b64(w1, ws, vo, so + 8, 0);
+                // 8-B stores: the 16-B buffer_store form came out with a corrupted 4th dword under
+                // hipcc 7.2 for gfx950 in the fp32 critic (a store-data hazard the compiler does
+                // not guard); fp32 is the parity mode, so exactness wins here
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(lo[0]), __float_as_uint(lo[1])}, ws, vo, so, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(lo[2]), __float_as_uint(lo[3])}, ws, vo, so + 8, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(hi[0]), __float_as_uint(hi[1])}, ws, vo, so + 16, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(hi[2]), __float_as_uint(hi[3])}, ws, vo, so + 24, 0);
             }
         }
+}
+
+// image positions [8g, 8g + 8) of column c (rows img_row(p), value(r)) in one 16-B store (bf16)
+// or four 8-B stores (fp32)
+template <class P, class F>
+__device__ inline void store_img8(void* img, size_t ldm, size_t grow0, int c, int g, F value) {
+    using AT = typename P::AT;
+    float e[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = value(img_row(8 * g + k));
+    AT* dst = (AT*)img + (size_t)c * ldm + grow0 + 8 * g;
+    if constexpr (sizeof(AT) == 2) {
+        __bf16 b[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[k] = (__bf16)e[k];
+        *(u32x4*)dst = __builtin_bit_cast(u32x4, b);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) *(u32x2*)(dst + k) = u32x2{__float_as_uint(e[k]), __float_as_uint(e[k + 1])};
+    }
 }
 
 template <class P, int MT, int NT>
@@ -105,7 +143,7 @@ __device__ inline void atomic_add_metric(double* m, int i, double v) { atomicAdd
 template <class P, int MT>
 struct ActorSmem {
     static constexpr int ROWS = 16 * MT;
-    size_t tA, tB, a0, xp, xn, st, temb, sch, rn, rj, bias, total;
+    size_t tA, tB, a0, xp, xn, st, temb, sch, rn, rj, radv, rlpo, nrm, bias, total;
     __host__ __device__ ActorSmem(const ActorArgs& a) {
         using AT = typename P::AT;
         const int pad = lds_pad_elems<P>();
@@ -121,6 +159,9 @@ struct ActorSmem {
         sch = o; o += dppo_align16(4 * a.KF * DPPO_SCHED_COLS);
         rn = o; o += dppo_align16(4 * ROWS);
         rj = o; o += dppo_align16(4 * ROWS);
+        radv = o; o += dppo_align16(4 * ROWS);
+        rlpo = o; o += dppo_align16(4 * ROWS);
+        nrm = o; o += 16;
         bias = o; o += dppo_align16(4 * (3 * a.H + 16 * dppo_cdiv(a.XD, 16)));
         total = o;
     }
@@ -158,47 +199,50 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     float* sch = (float*)(smem + S.sch);
     int* rn = (int*)(smem + S.rn);
     int* rj = (int*)(smem + S.rj);
+    float* radv = (float*)(smem + S.radv);   // per row: the row's advantage (train)
+    float* rlpo = (float*)(smem + S.rlpo);   // per row: its old log-prob (train)
+    float* nrm = (float*)(smem + S.nrm);     // advantage normalisation: mean, std + 1e-8
     float* part = (float*)(smem + S.tB);   // out-layer partials alias tB (u2 is dead by then)
     const size_t grow0 = (size_t)blockIdx.x * ROWS;
     const __amdgpu_buffer_rsrc_t wsr = packed_rsrc(a.ws.base);
     const uint32_t ldm32 = (uint32_t)a.ws.ldm, grow32 = (uint32_t)grow0;
 
     // ---- prologue: rows, gathers, schedule, biases, time embedding for t < K' (actor_ft) ----
-    // Every thread maps its own element to its row (the Feistel step is a few dozen ALU ops), so
-    // the chains / obs gathers issue at once instead of after a barrier on a row table.
-    auto row_of = [&](int r, int& n, int& j) {
-        const int64_t gr = (int64_t)grow0 + r;
-        n = -1; j = 0;
+    // The weight stream starts first (its latency overlaps everything below). One thread per row
+    // maps it through the minibatch permutation (Feistel cycle-walk: done once per row) and
+    // fetches the row's per-sample scalars; the chains / obs gathers follow one barrier later.
+    const int ntile0 = wave * NT;
+    const __amdgpu_buffer_rsrc_t rs = packed_rsrc(a.packed);
+    auto W = [&](int seg) { return wsrc(rs, L.off[seg]); };
+    constexpr int QD = 3;
+    WQueue<QD, NT> R;
+    queue_prime(R, W(SEG_W_IN), KSI, NextLayers{W(SEG_W_L1), KSH, W(SEG_W_L2), KSH}, ntile0, lane);
+    if (tid < ROWS) {
+        const int64_t gr = (int64_t)grow0 + tid;
+        int n = -1, j = 0;
         if (gr < a.nrows) {
             if (train) {
                 const uint64_t idx = minibatch_row(a.row_index, (uint64_t)(a.start + gr), a.fk);
-                if (idx < a.fk.n) { n = (int)(idx / KF); j = (int)(idx % KF); }   // tf.unravel_index
+                if (idx < a.fk.n) {   // tf.unravel_index; sample counts are < 2^32 (host-checked)
+                    n = (int)((uint32_t)idx / (uint32_t)KF);
+                    j = (int)((uint32_t)idx - (uint32_t)n * (uint32_t)KF);
+                }
             } else {
-                n = (int)(gr / KF); j = (int)(gr % KF);
+                n = (int)((uint64_t)gr / (uint64_t)KF);
+                j = (int)((uint64_t)gr - (uint64_t)n * (uint64_t)KF);
             }
         }
-    };
-    for (int i = tid; i < ROWS * XD; i += THREADS) {
-        const int r = i / XD, q = i % XD;
-        int n, j;
-        row_of(r, n, j);
-        float vp = 0.f, vn = 0.f;
-        if (n >= 0) {
-            const float* c = a.chains + ((size_t)n * (KF + 1) + j) * XD + q;
-            vp = c[0]; vn = c[XD];   // chains_prev = chains[:, j], chains_next = chains[:, j+1]
-        }
-        xp[i] = vp; xn[i] = vn;
-    }
-    for (int i = tid; i < ROWS * SD; i += THREADS) {
-        const int r = i / SD, c = i % SD;
-        int n, j;
-        row_of(r, n, j);
-        st[i] = n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f;
-    }
-    if (tid < ROWS) {
-        int n, j;
-        row_of(tid, n, j);
         rn[tid] = n; rj[tid] = j;
+        if (train) {
+            radv[tid] = n >= 0 ? a.adv[n] : 0.f;
+            rlpo[tid] = n >= 0 ? a.lp_old[(size_t)n * KF + j] : 0.f;
+        }
+    } else if (train && tid == ROWS) {   // population mean / std of the minibatch (diffusion_ppo.py:74-75)
+        const double* S3 = a.adv_stats;
+        const double mean = S3[1] / S3[0];
+        const double var = fmax(S3[2] / S3[0] - mean * mean, 0.0);
+        nrm[0] = (float)mean;
+        nrm[1] = (float)(sqrt(var) + 1e-8);
     }
     for (int i = tid; i < KF * DPPO_SCHED_COLS; i += THREADS) sch[i] = a.sched[i];
     for (int i = tid; i < 3 * H + 16 * NO; i += THREADS) {
@@ -211,6 +255,20 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         for (int i = tid; i < KF * TD; i += THREADS) temb[i] = tt[i];
     }
     __syncthreads();
+    for (int i = tid; i < ROWS * XD; i += THREADS) {
+        const int r = i / XD, q = i % XD, n = rn[r];
+        float vp = 0.f, vn = 0.f;
+        if (n >= 0) {
+            const float* c = a.chains + ((size_t)n * (KF + 1) + rj[r]) * XD + q;
+            vp = c[0]; vn = c[XD];   // chains_prev = chains[:, j], chains_next = chains[:, j+1]
+        }
+        xp[i] = vp; xn[i] = vn;
+    }
+    for (int i = tid; i < ROWS * SD; i += THREADS) {
+        const int r = i / SD, c = i % SD, n = rn[r];
+        st[i] = n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f;
+    }
+    __syncthreads();
     // a0 = [x_prev, temb(t), state] (mlp_diffusion.py:86), t = K'-1-j (diffusion_vpg.py:456-458)
     for (int i = tid; i < ROWS * k1w; i += THREADS) {
         const int r = i / k1w, c = i % k1w;
@@ -221,34 +279,25 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         else if (c < IN) v = st[r * SD + c - XD - TD];
         a0[r * lda0 + c] = P::cvt(v);
     }
-    if (train) {
-        AT* a0T = (AT*)a.ws.a0T;
-        for (int i = tid; i < ROWS * IN; i += THREADS) {
-            const int c = i / ROWS, r = i % ROWS;
-            const int t = KF - 1 - rj[r];
-            float v;
-            if (c < XD) v = xp[r * XD + c];
-            else if (c < XD + TD) v = temb[t * TD + c - XD];
-            else v = st[r * SD + c - XD - TD];
-            a0T[(size_t)c * a.ws.ldm + grow0 + r] = P::cvt(v);
+    if (train) {   // a0T image (permuted row order, img_pos) and the per-row t bucket
+        for (int i = tid; i < (ROWS / 8) * IN; i += THREADS) {
+            const int c = i / (ROWS / 8), g = i % (ROWS / 8);
+            store_img8<P>(a.ws.a0T, a.ws.ldm, grow0, c, g, [&](int r) {
+                const int t = KF - 1 - rj[r];
+                return c < XD ? xp[r * XD + c] : (c < XD + TD ? temb[t * TD + c - XD] : st[r * SD + c - XD - TD]);
+            });
         }
-        if (tid < ROWS) a.ws.seg[grow0 + tid] = rn[tid] >= 0 ? (int8_t)(KF - 1 - rj[tid]) : (int8_t)-1;
+        if (tid < ROWS) a.ws.seg[grow0 + img_pos(tid)] = rn[tid] >= 0 ? (int8_t)(KF - 1 - rj[tid]) : (int8_t)-1;
     }
     __syncthreads();
 
     PHASE(0);
-    const int ntile0 = wave * NT;
-    const __amdgpu_buffer_rsrc_t rs = packed_rsrc(a.packed);
-    auto W = [&](int seg) { return wsrc(rs, L.off[seg]); };
     f32x4 acc[MT][NT];
     static_assert(MT * NT * 4 <= 32, "relu masks are 32-bit");
     uint32_t mask1 = 0, mask2 = 0;
     // The weight stream is one QD-deep queue per wave through every layer of the kernel:
     //   in -> l1 -> l2 -> in (again: the residual h1 is recomputed as a0 W_in, 2 more k-steps,
     //   instead of holding 8*MT*NT fp32 registers from L1 to L3) -> [train] out^T -> l2^T -> l1^T.
-    constexpr int QD = 3;
-    WQueue<QD, NT> R;
-    queue_prime(R, W(SEG_W_IN), KSI, NextLayers{W(SEG_W_L1), KSH, W(SEG_W_L2), KSH}, ntile0, lane);
     ORing<NOK, NO> ob;
     // ---- L1: h1 = a0 W_in + b (no activation on the input layer) ----
     gemm_queue<P, MT, NT, KSI, QD>(a0, lda0, W(SEG_W_IN), ntile0, acc, lane, R,
@@ -373,15 +422,10 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
             if (!train) {
                 if (n >= 0 && a.lp_mean) a.lp_mean[(size_t)n * KF + j] = newlp;
             } else if (n >= 0) {
-                const double* S3 = a.adv_stats;
-                float A = a.adv[n];
-                if (a.hp.norm_adv) {   // population std over the minibatch (diffusion_ppo.py:74-75)
-                    const double mean = S3[1] / S3[0];
-                    const double var = fmax(S3[2] / S3[0] - mean * mean, 0.0);
-                    A = (float)(((double)A - mean) / (sqrt(var) + 1e-8));
-                }
+                float A = radv[r];
+                if (a.hp.norm_adv) A = (A - nrm[0]) / nrm[1];   // population std over the minibatch (:74-75)
                 A *= powf(a.hp.gamma_denoising, (float)(KF - j - 1));                 // :83-86
-                const float oldlp = a.lp_old[(size_t)n * KF + j];
+                const float oldlp = rlpo[r];
                 const float logratio = newlp - oldlp;
                 const float ratio = expf(logratio);
                 float cc;                                                              // :93-101
@@ -434,9 +478,12 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
             d = e_uc[e] != 0.f ? -sc[1] * sc[2] * dmu : 0.f;
         }
         dyt[r * lda0 + q] = P::cvt(d);
-        if (q < XD) ((AT*)a.ws.dyT)[(size_t)q * a.ws.ldm + grow0 + r] = P::cvt(d);
     }
     lds_sync();
+    for (int i = tid; i < (ROWS / 8) * XD; i += THREADS) {   // dyT image from the dy tile
+        const int q = i / (ROWS / 8), g = i % (ROWS / 8);
+        store_img8<P>(a.ws.dyT, a.ws.ldm, grow0, q, g, [&](int r) { return P::tof(dyt[r * lda0 + q]); });
+    }
     PHASE(7);
 
     // ---- backward dX chain (weights continue in the same stream) ----
@@ -554,13 +601,13 @@ __device__ __forceinline__ void critic_rowtile_body(const CriticArgs& a) {
         const int r = i / k1w, c = i % k1w, n = rn[r];
         a0[r * lda0 + c] = P::cvt((n >= 0 && c < SD) ? a.obs[(size_t)n * SD + c] : 0.f);
     }
-    if (train) {
-        for (int i = tid; i < ROWS * SD; i += THREADS) {
-            const int c = i / ROWS, r = i % ROWS, n = rn[r];
-            ((AT*)a.ws.csT)[(size_t)c * a.ws.ldm + grow0 + r] = P::cvt(n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f);
+    __syncthreads();
+    if (train) {   // csT image (permuted row order, img_pos) from the input tile
+        for (int i = tid; i < (ROWS / 8) * SD; i += THREADS) {
+            const int c = i / (ROWS / 8), g = i % (ROWS / 8);
+            store_img8<P>(a.ws.csT, a.ws.ldm, grow0, c, g, [&](int r) { return P::tof(a0[r * lda0 + c]); });
         }
     }
-    __syncthreads();
 
     const int ntile0 = wave * NT;
     const __amdgpu_buffer_rsrc_t rs = packed_rsrc(a.packed);
@@ -632,7 +679,7 @@ __device__ __forceinline__ void critic_rowtile_body(const CriticArgs& a) {
                 dv = a.hp.vf_coef * diff * a.hp.grad_scale;      // loss = pg + vf_coef * v_loss (agent :340)
             }
             for (int q = 0; q < ktw; ++q) a0[r * lda0 + q] = P::cvt(q == 0 ? dv : 0.f);
-            ((AT*)a.ws.cdvT)[grow0 + r] = P::cvt(dv);
+            ((AT*)a.ws.cdvT)[grow0 + img_pos(r)] = P::cvt(dv);
             vl = wave_sum(vl);
             if (lane == 0) atomic_add_metric(a.metrics, 1, vl);
         }

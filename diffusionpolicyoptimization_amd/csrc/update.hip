@@ -453,6 +453,8 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     z.p[3] = ws.stats; z.n[3] = 4 * sizeof(double);
     hipLaunchKernelGGL(zero_kernel, dim3(256), dim3(256), 0, s, z);
     DPPO_HIP(hipGetLastError());
+    DPPO_CHECK((uint64_t)total < ((uint64_t)1 << 32), "dppo_ppo_minibatch: %lld samples x steps exceed 2^32",
+               (long long)total);
     const FeistelKey fk = feistel_key((uint64_t)total, perm_seed, epoch);
     const double* stats = adv_stats;
     if (!stats) {
