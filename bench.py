@@ -35,6 +35,21 @@ def sampler_flops_per_env(d):
 
 CU_LOAD_PEAK_GBS = 64 * 2.4   # per-CU vector-memory (TA) path: 64 B/clk at the 2.4 GHz max clock
 
+# Latency floor of one denoising step of the split sampler (csrc/sampler_split.hip), the figure
+# its per-step time is compared with: one in-launch exchange of partial sums between the 8
+# workgroups of a 16-env group (tools/xchg_probe.hip measured 1.10 us per step with the members on
+# one XCD, 1.68 us spread) + the step's MFMA issue on one SIMD (2 waves x 28
+# v_mfma_f32_16x16x32_bf16 x 16 cycles at 2.4 GHz = 0.37 us). Everything else in a step (LDS
+# round trips, barriers, the DDPM epilogue) is latency this floor does not count.
+SPLIT_XCHG_US = 1.10
+SPLIT_MFMA_US = 2 * 28 * 16 / 2.4e3
+
+
+def sampler_layout(d, precision, envs):
+    """Workgroups per 16-env group of the sampler the library runs (0 = weight-streaming kernel)."""
+    from diffusionpolicyoptimization_amd import ops
+    return ops.sampler_layout(d, precision, envs)
+
 
 def sampler_stream_bytes_per_tile(d, precision):
     """Weight bytes ONE 16-row sampler tile (one CU) loads per launch (the library reports it for
@@ -174,16 +189,31 @@ def main():
     env_steps = agent.n_envs_global * cfg.act_steps * cfg.train.n_steps * args.steps
     n_updates = agent.timing["n_updates"]
     flops = sampler_flops_per_env(d) * agent.n_envs
-    stream_b = sampler_stream_bytes_per_tile(d, agent.model.precision)
-    achieved = flops / (samp_ms * 1e-3) / 1e12
     prec = agent.model.precision
+    members = sampler_layout(d, prec, agent.n_envs)
+    kname = "sample_split_kernel" if members else "sample_kernel"
+    achieved = flops / (samp_ms * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if "sample_kernel" in tj.get("kernel", "") and tj.get("precision") == prec \
-                and tj.get("envs") == agent.n_envs:
+        if kname + "<" in tj.get("kernel", "") and tj.get("precision") == prec and tj.get("envs") == agent.n_envs:
             traffic = tj.get("hbm_bytes_per_launch")
+    if members:
+        step_us = samp_ms * 1e3 / d.denoising_steps
+        floor_us = SPLIT_XCHG_US + SPLIT_MFMA_US
+        bound = {"kind": "latency", "kernel": kname, "workgroups_per_16_envs": members,
+                 "us_per_denoising_step": step_us, "floor_us_per_step": floor_us, "frac": floor_us / step_us,
+                 "note": ("each 16-env group runs on 8 CUs with 1/8 of the actor resident in registers; a "
+                          "denoising step is a dependent chain of 4 GEMMs (M = 16 envs) and one cross-CU "
+                          "partial-sum exchange, so its floor is that exchange (tools/xchg_probe.hip) plus "
+                          "the step's MFMA issue, not bytes or FLOPs; see DESIGN.md")}
+    else:
+        stream_b = sampler_stream_bytes_per_tile(d, prec)
+        bound = {"kind": "load_path", "kernel": kname, "bytes_per_cu_per_launch": stream_b,
+                 "achieved_GBs_per_cu": stream_b / (samp_ms * 1e-3) / 1e9, "peak_GBs_per_cu": CU_LOAD_PEAK_GBS,
+                 "frac": stream_b / (samp_ms * 1e-3) / 1e9 / CU_LOAD_PEAK_GBS,
+                 "note": "each 16-row tile streams its actor's weights from L2 into one CU every denoising step"}
     out = {
         "metric": METRIC, "value": env_steps / elapsed, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -197,19 +227,15 @@ def main():
         "ppo_updates_per_sec": n_updates / elapsed,
         "rollout_env_steps_per_sec": env_steps / t_roll if t_roll > 0 else None,
         "rollout_s_per_iter": t_roll / args.steps, "update_s_per_iter": t_upd / args.steps,
-        "load_path": {"kernel": "sample_kernel", "bytes_per_cu_per_launch": stream_b,
-                      "achieved_GBs_per_cu": stream_b / (samp_ms * 1e-3) / 1e9, "peak_GBs_per_cu": CU_LOAD_PEAK_GBS,
-                      "frac": stream_b / (samp_ms * 1e-3) / 1e9 / CU_LOAD_PEAK_GBS,
-                      "note": "what bounds the sampler at 64 envs: each 16-row tile streams its actor's weights "
-                              "from L2 into one CU every denoising step (time is flat from 16 to 1024 envs)"},
-        "roofline": {"bound": "mfma", "kernel": "sample_kernel (K-step DDPM sampler, all layers fused)",
+        "sampler_bound": bound,
+        "roofline": {"bound": "mfma", "kernel": kname + " (K-step DDPM sampler, all layers fused)",
                      "achieved": achieved, "peak": PEAK["bf16" if prec == "bf16" else "fp32"], "unit": "TFLOP/s",
                      "frac": achieved / PEAK["bf16" if prec == "bf16" else "fp32"], "traffic": traffic,
                      "avg_launch_ms": samp_ms, "flops_per_launch": flops, "burst_launches": n_burst,
                      "in_loop_event_ms": loop_samp_ms if agent.sampler_events else None,
-                     "note": ("M = envs/GPU rows per GEMM: at 64 rows the dependent 80-GEMM chain is bound by "
-                              "streaming ~1.1 MB of bf16 weights per denoising step from L2 into one CU per "
-                              "16-row tile (load_path), not by MFMA issue; see DESIGN.md")},
+                     "note": ("M = envs/GPU rows per GEMM: at 64 envs the sampler is a dependent chain of "
+                              "K x 4 small GEMMs, far below MFMA peak by construction; sampler_bound gives "
+                              "the figure that bounds it")},
         "ppo_minibatch_avg_ms": upd_ms,
     }
     if rank == 0 and not args.no_cpu_baseline:
