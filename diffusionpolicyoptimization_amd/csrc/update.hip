@@ -1,19 +1,23 @@
 // update.hip — weight gradients, time-MLP backward, minibatch statistics, optimiser, and the
 // dppo_ppo_minibatch orchestration (agent/finetune/train_ppo_diffusion_agent.py:287-356).
+#include <stdlib.h>
 #include "dppo_ppo.h"
 
 // ---------------------------------------------------------------------------------------------
 // grouped split-K weight-gradient GEMM:  G[k][n] += sum_m XT[k][m] * DT[n][m]
-// (dW = X^T dH in Keras [in,out] layout). A workgroup (4 waves) owns a 128x128 output tile and
-// one m-chunk; each wave holds a 64x64 sub-tile (4x4 MFMA tiles, 64 accumulator VGPRs). Both
-// operands are feature-major, so a stage of BK rows is one 128-B line per feature: the stage is
-// copied global -> LDS with 16-B global_load_lds (one 1 KiB wave-instruction = 8 features), two
-// LDS buffers so the copy of stage s+1 overlaps the MFMAs of stage s. The LDS image is linear
-// per wave-instruction; the bank swizzle (16-B slot = chunk ^ (feature & 7)) is applied on the
-// global source address, which makes the fragment reads (ds_read_b128) conflict-free.
+// (dW = X^T dH in Keras [in,out] layout). A workgroup (4 waves, one per CU) owns a 128x128 output
+// tile and one m-chunk; each wave holds a 64x64 sub-tile (4x4 MFMA tiles, 64 accumulator VGPRs).
+// Both operands are feature-major, so a stage of BK rows is one 128-B line per feature: the stage
+// is copied global -> LDS with 16-B global_load_lds (one 1 KiB wave-instruction = 8 features) into
+// a ring of DW_RING slots, DW_RING - 1 stages in flight: each wave waits with a counted vmcnt for
+// its own copies of the oldest stage only, then one barrier (the kernel reads ~470 MB of images
+// per minibatch; one stage in flight behind a vmcnt(0) barrier left it latency bound at ~2.5 TB/s).
+// The LDS image is linear per wave-instruction; the bank swizzle (16-B slot = chunk ^ (feature & 7))
+// is applied on the global source address, which makes the fragment reads (ds_read_b128) conflict-free.
 // The k-tile-0 workgroups also produce the "extra" rows:
 //   ONES   -> bias gradient  sum_m DT[n][m]
-//   ONEHOT -> per-bucket sums sum_{m: seg[m]=q} DT[n][m]  (actor in-layer: in_b and d t_emb)
+//   ONEHOT -> per-bucket sums sum_{m: seg[m]=q} DT[n][m]  (actor in-layer: in_b and d t_emb); the
+//             stage's 64 seg bytes travel in the same ring slot
 // Partial tiles are added with fp32 atomics (one add per element per m-chunk).
 // ---------------------------------------------------------------------------------------------
 enum { EXTRA_NONE = 0, EXTRA_ONES = 1, EXTRA_ONEHOT = 2 };
@@ -21,7 +25,8 @@ enum { EXTRA_NONE = 0, EXTRA_ONES = 1, EXTRA_ONEHOT = 2 };
 #define DW_T 128             // output tile edge
 #define DW_LINE 128          // bytes per feature per stage
 #define DW_OPB (DW_T * DW_LINE)   // 16 KiB: one operand's stage image
-#define DW_SEG_MAX 8192           // max rows per m-chunk (the chunk's seg bytes are staged in LDS)
+#define DW_RING 4                 // ring slots (stages in flight: DW_RING - 1)
+#define DW_SLOT (2 * DW_OPB + 1024)   // A | B | the stage's seg bytes (padded)
 
 struct DWProb {
     const void* XT; const void* DT; float* G; float* Gx;
@@ -60,19 +65,28 @@ __device__ inline u32x4 dw_lds_frag(const uint8_t* img, int f, int c) {
     return *reinterpret_cast<const u32x4*>(img + f * DW_LINE + ((c ^ (f & 7)) << 4));
 }
 
+// wait until at most N of this wave's vector-memory operations are outstanding
+template <int N>
+__device__ inline void vm_wait() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 // the main loop, with or without the extra (bias / bucket) rows: two straight copies, so the
 // register allocator sees one uniform accumulator set per loop (a data-dependent MFMA inside
-// one loop made hipcc shuttle the accumulators between AGPRs and VGPRs every k-step)
-template <class P, bool EXTRA>
+// one loop made hipcc shuttle the accumulators between AGPRs and VGPRs every k-step).
+// SEGLD: this wave also copies the stage's seg bytes (ONEHOT extra rows).
+template <class P, bool EXTRA, bool SEGLD>
 __device__ __forceinline__ void dw_loop(uint8_t* smem, const DWArgs& a, const DWProb& pr, int nst, size_t m_begin,
-                                        int k_base, int n_base, int wave, int lane, const int8_t* seg_lds,
+                                        int k_base, int n_base, int wave, int lane,
                                         const typename P::AT* const (&srcA)[4], const typename P::AT* const (&srcB)[4],
                                         f32x4 (&acc)[4][4], f32x4 (&acce)[4]) {
     constexpr int BK = DW_LINE / (int)sizeof(typename P::AT);
+    constexpr int OPS = 8 + (SEGLD ? 1 : 0);            // vector-memory ops per stage per wave
     const int wr = wave >> 1, wc = wave & 1;
     const int fr = lane & 15, cq = lane >> 4;
-    auto issue = [&](int st, int buf) {
-        uint8_t* base = smem + buf * 2 * DW_OPB;
+    auto issue = [&](int st) {
+        uint8_t* base = smem + (st % DW_RING) * DW_SLOT;
         const size_t off = (size_t)st * BK;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -80,13 +94,28 @@ __device__ __forceinline__ void dw_loop(uint8_t* smem, const DWArgs& a, const DW
             __builtin_amdgcn_global_load_lds((void*)(srcA[i] + off), (lds_void_t*)(base + ins * 1024), 16, 0, 0);
             __builtin_amdgcn_global_load_lds((void*)(srcB[i] + off), (lds_void_t*)(base + DW_OPB + ins * 1024), 16, 0, 0);
         }
+        if constexpr (SEGLD) {   // BK seg bytes, 4 per lane (lanes past BK/4 fetch bytes nobody reads)
+            const int8_t* sg = a.seg + m_begin + off + 4 * (lane < BK / 4 ? lane : 0);
+            __builtin_amdgcn_global_load_lds((void*)sg, (lds_void_t*)(base + 2 * DW_OPB), 4, 0, 0);
+        }
     };
-    issue(0, 0);
+#pragma unroll
+    for (int p = 0; p < DW_RING - 1; ++p)
+        if (p < nst) issue(p);
     for (int st = 0; st < nst; ++st) {
-        __syncthreads();                         // stage st landed; buffer st+1 no longer read
-        if (st + 1 < nst) issue(st + 1, (st + 1) & 1);
-        const uint8_t* imA = smem + (st & 1) * 2 * DW_OPB;
+        // this wave's copies of stage st have landed once at most (stages issued after it) * OPS
+        // operations are outstanding; the barrier then covers every wave's copies, and every wave
+        // has finished reading stage st - 1, whose slot the next issue reuses
+        const int ahead = nst - 1 - st;
+        if (ahead >= DW_RING - 2) vm_wait<(DW_RING - 2) * OPS>();
+        else if (ahead == 1) vm_wait<OPS>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (st + DW_RING - 1 < nst) issue(st + DW_RING - 1);
+        const uint8_t* imA = smem + (st % DW_RING) * DW_SLOT;
         const uint8_t* imB = imA + DW_OPB;
+        const int8_t* seg_lds = (const int8_t*)(imA + 2 * DW_OPB);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             u32x4 A[4], B[4];
@@ -100,12 +129,22 @@ __device__ __forceinline__ void dw_loop(uint8_t* smem, const DWArgs& a, const DW
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(A[i], B[j], acc[i][j]);
             if constexpr (EXTRA) {
-                const u32x4 AE = extra_frag<P>(pr.extra, fr, seg_lds + st * BK + ks * P::KG + cq * P::EPL);
+                const u32x4 AE = extra_frag<P>(pr.extra, fr, seg_lds + ks * P::KG + cq * P::EPL);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acce[j] = P::mma(AE, B[j], acce[j]);
             }
         }
     }
+}
+
+static int dw_device_cus() {
+    static int n = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            c = 256;
+        return c > 0 ? c : 256;
+    }();
+    return n;
 }
 
 template <class P>
@@ -114,8 +153,8 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
     constexpr int BK = DW_LINE / (int)sizeof(AT);     // rows per stage: 64 bf16 / 32 fp32
     constexpr int EPC = 16 / (int)sizeof(AT);         // elements per 16-B chunk
     // one LDS object (a second __shared__ array can make hipcc drain the glds queue at every
-    // fragment read): [buf][A|B] stage images, then the chunk's seg bytes
-    __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * 2 * DW_OPB + DW_SEG_MAX];
+    // fragment read): the ring of [A | B | seg] stage slots
+    __shared__ __attribute__((aligned(1024))) uint8_t smem[DW_RING * DW_SLOT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // XCD-aware order: block b runs on XCD b % 8; XCD x takes the contiguous logical range
     // [x*per, (x+1)*per) of the chunk-major order, so the tiles that share one m-chunk's operand
@@ -142,10 +181,7 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
     const AT* DT = (const AT*)pr.DT;
     const bool wg_extra = pr.extra != EXTRA_NONE && kt == 0;      // uniform over the workgroup
     const bool do_extra = wg_extra && wr == 0;
-    int8_t* seg_lds = (int8_t*)(smem + 4 * DW_OPB);
-    if (pr.extra == EXTRA_ONEHOT && kt == 0) {
-        for (int i = tid; i < (int)(m_end - m_begin); i += 256) seg_lds[i] = a.seg[m_begin + i];
-    }
+    const bool seg_ld = do_extra && pr.extra == EXTRA_ONEHOT;
 
     // per-lane glds sources for this wave's 4 A + 4 B wave-instructions (features ins*8 + lane/8)
     const AT* srcA[4];
@@ -168,8 +204,9 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
         for (int j = 0; j < 4; ++j) zero_acc(acc[i][j]);
     }
     // waves 2,3 of an extra tile run the plain loop; the barrier count per stage is identical
-    if (do_extra) dw_loop<P, true>(smem, a, pr, nst, m_begin, k_base, n_base, wave, lane, seg_lds, srcA, srcB, acc, acce);
-    else dw_loop<P, false>(smem, a, pr, nst, m_begin, k_base, n_base, wave, lane, seg_lds, srcA, srcB, acc, acce);
+    if (seg_ld) dw_loop<P, true, true>(smem, a, pr, nst, m_begin, k_base, n_base, wave, lane, srcA, srcB, acc, acce);
+    else if (do_extra) dw_loop<P, true, false>(smem, a, pr, nst, m_begin, k_base, n_base, wave, lane, srcA, srcB, acc, acce);
+    else dw_loop<P, false, false>(smem, a, pr, nst, m_begin, k_base, n_base, wave, lane, srcA, srcB, acc, acce);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -484,55 +521,67 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     ca.L = make_mlp_layout(D.SD, D.HC, 1, 0, precision);
     ca.obs = obs; ca.SD = D.SD; ca.HC = D.HC; ca.KF = D.KF; ca.mode = ROWS_TRAIN; ca.nrows = rows;
     ca.fk = fk; ca.start = start; ca.row_index = row_index; ca.returns = returns; ca.hp = lh; ca.ws = ws; ca.metrics = metrics;
-    // The critic row tiles are independent of the actor's: they run on a side stream, so they
-    // fill the CUs the actor's last (partial) round of tiles leaves idle. Joined before dW.
+    // weight-gradient problems of one network, launched as one grouped dW kernel on stream st.
+    // m-chunks: about one workgroup per CU (the ring takes 132 KB of LDS) in a single round.
+    // DPPO_DW_CHUNKS overrides the chunk count (a measurement knob).
+    static const int env_ch = [] { const char* e = getenv("DPPO_DW_CHUNKS"); return e ? atoi(e) : 0; }();
+    auto launch_grads = [&](bool actor, hipStream_t st) -> int {
+        DWArgs w = {};
+        auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
+            DWProb& p = w.p[w.nprob];
+            p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
+            p.ktiles = dppo_cdiv(Kx, DW_T); p.ntiles = dppo_cdiv(N, DW_T);
+            w.tile_start[w.nprob + 1] = w.tile_start[w.nprob] + p.ktiles * p.ntiles;
+            w.nprob++;
+        };
+        if (actor) {
+            add(ws.a0T, D.IN, ws.dh1T, D.H, ga + FA.in_w, EXTRA_ONEHOT, ws.gseg);
+            add(ws.u1T, D.H, ws.dh2T, D.H, ga + FA.l1_w, EXTRA_ONES, ga + FA.l1_b);
+            add(ws.u2T, D.H, ws.dh3T, D.H, ga + FA.l2_w, EXTRA_ONES, ga + FA.l2_b);
+            add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
+        } else {
+            add(ws.csT, D.SD, ws.cdh1T, D.HC, gc + FC.in_w, EXTRA_ONES, gc + FC.in_b);
+            add(ws.cu1T, D.HC, ws.cdh2T, D.HC, gc + FC.l1_w, EXTRA_ONES, gc + FC.l1_b);
+            add(ws.cu2T, D.HC, ws.cdh3T, D.HC, gc + FC.l2_w, EXTRA_ONES, gc + FC.l2_b);
+            add(ws.ch3T, D.HC, ws.cdvT, 1, gc + FC.out_w, EXTRA_ONES, gc + FC.out_b);
+        }
+        w.ldm = ws.ldm;
+        w.seg = ws.seg;
+        const int tiles = w.tile_start[w.nprob];
+        int nch = env_ch > 0 ? env_ch : dw_device_cus() / tiles;
+        const int max_ch = (int)(ws.ldm / 64);
+        if (nch > max_ch) nch = max_ch;
+        if (nch < 1) nch = 1;
+        w.mchunk = (int)(dppo_cdiv((int)ws.ldm, nch * 64) * 64);
+        w.nchunks = dppo_cdiv((int)ws.ldm, w.mchunk);
+        return precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, st) : launch_dw<PolicyF32>(w, st);
+    };
+
+    // The critic is independent of the actor: its row tiles and then its weight gradients run on a
+    // side stream, filling the CUs the actor's row tiles leave idle (the actor's last partial round)
+    // and overlapping the critic's HBM-bound dW with the actor's tiles. Joined before the
+    // actor's dW completes the minibatch.
     SideStream* side = side_stream();
     if (side) {
         DPPO_HIP(hipEventRecord(side->fork, s));
         DPPO_HIP(hipStreamWaitEvent(side->stream, side->fork, 0));
         rc = launch_critic_rowtile(ca, precision, side->stream);
         if (rc) return rc;
+        rc = launch_grads(false, side->stream);
+        if (rc) return rc;
         DPPO_HIP(hipEventRecord(side->join, side->stream));
     }
     rc = launch_actor_rowtile(aa, precision, s);
     if (rc) return rc;
-    if (side) {
-        DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
-    } else {
+    if (!side) {
         rc = launch_critic_rowtile(ca, precision, s);
         if (rc) return rc;
+        rc = launch_grads(false, s);
+        if (rc) return rc;
     }
-
-    DWArgs w = {};
-    auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
-        DWProb& p = w.p[w.nprob];
-        p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
-        p.ktiles = dppo_cdiv(Kx, DW_T); p.ntiles = dppo_cdiv(N, DW_T);
-        w.tile_start[w.nprob + 1] = w.tile_start[w.nprob] + p.ktiles * p.ntiles;
-        w.nprob++;
-    };
-    add(ws.a0T, D.IN, ws.dh1T, D.H, ga + FA.in_w, EXTRA_ONEHOT, ws.gseg);
-    add(ws.u1T, D.H, ws.dh2T, D.H, ga + FA.l1_w, EXTRA_ONES, ga + FA.l1_b);
-    add(ws.u2T, D.H, ws.dh3T, D.H, ga + FA.l2_w, EXTRA_ONES, ga + FA.l2_b);
-    add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
-    add(ws.csT, D.SD, ws.cdh1T, D.HC, gc + FC.in_w, EXTRA_ONES, gc + FC.in_b);
-    add(ws.cu1T, D.HC, ws.cdh2T, D.HC, gc + FC.l1_w, EXTRA_ONES, gc + FC.l1_b);
-    add(ws.cu2T, D.HC, ws.cdh3T, D.HC, gc + FC.l2_w, EXTRA_ONES, gc + FC.l2_b);
-    add(ws.ch3T, D.HC, ws.cdvT, 1, gc + FC.out_w, EXTRA_ONES, gc + FC.out_b);
-    w.ldm = ws.ldm;
-    w.seg = ws.seg;
-    // m-chunks: about 2 workgroups per CU over the whole grid, chunk a multiple of 64 rows
-    const int tiles = w.tile_start[w.nprob];
-    int nch = dppo_cdiv(256 * 2, tiles);
-    const int max_ch = (int)(ws.ldm / 64);
-    const int min_ch = dppo_cdiv((int)ws.ldm, DW_SEG_MAX);
-    if (nch > max_ch) nch = max_ch;
-    if (nch < min_ch) nch = min_ch;
-    if (nch < 1) nch = 1;
-    w.mchunk = (int)(dppo_cdiv((int)ws.ldm, nch * 64) * 64);
-    w.nchunks = dppo_cdiv((int)ws.ldm, w.mchunk);
-    rc = precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, s) : launch_dw<PolicyF32>(w, s);
+    rc = launch_grads(true, s);
     if (rc) return rc;
+    if (side) DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
 
     const size_t tsm = sizeof(float) * (size_t)D.KF * (2 * D.TD + 2 * 2 * D.TD);
     hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, ws.gseg, actor_params, ga, FA, D.XD, D.TD, D.H, D.KF);
