@@ -23,7 +23,7 @@ class DppoDims(ctypes.Structure):
     _fields_ = [("obs_dim", ctypes.c_int32), ("action_dim", ctypes.c_int32), ("horizon_steps", ctypes.c_int32),
                 ("cond_steps", ctypes.c_int32), ("time_dim", ctypes.c_int32), ("actor_hidden", ctypes.c_int32),
                 ("critic_hidden", ctypes.c_int32), ("denoising_steps", ctypes.c_int32),
-                ("ft_denoising_steps", ctypes.c_int32)]
+                ("ft_denoising_steps", ctypes.c_int32), ("time_stride", ctypes.c_int32)]
 
 
 class DppoPpoHparams(ctypes.Structure):
@@ -79,6 +79,9 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
+ABI_VERSION = 2
+
+
 class DppoError(RuntimeError):
     pass
 
@@ -97,7 +100,7 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.dppo_abi_version() != 1:
+    if lib.dppo_abi_version() != ABI_VERSION:
         raise DppoError("libdppo_hip.so ABI version mismatch")
     _lib = lib
     return lib

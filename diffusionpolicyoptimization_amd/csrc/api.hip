@@ -23,6 +23,8 @@ int dppo_check_dims(const dppo_dims* d, Dims* o) {
     o->Do = d->obs_dim; o->Da = d->action_dim; o->Ta = d->horizon_steps; o->To = d->cond_steps;
     o->TD = d->time_dim; o->H = d->actor_hidden; o->HC = d->critic_hidden;
     o->K = d->denoising_steps; o->KF = d->ft_denoising_steps;
+    o->TS = d->time_stride > 0 ? d->time_stride : 1;
+    DPPO_CHECK(d->time_stride >= 0 && (int64_t)o->K * o->TS <= 1000, "time_stride out of range");
     DPPO_CHECK(o->Do > 0 && o->Da > 0 && o->Ta > 0 && o->To > 0, "obs/action/horizon/cond dims must be > 0");
     DPPO_CHECK(o->TD >= 4 && o->TD % 2 == 0 && o->TD <= 64, "time_dim must be even, in [4, 64]");
     DPPO_CHECK(o->H % 128 == 0 && o->H >= 128 && o->H <= 512, "actor_hidden must be 128/256/384/512");
@@ -66,7 +68,7 @@ extern "C" int dppo_pack_actor(const dppo_dims* d, int precision, const float* p
     if (rc) return rc;
     DPPO_CHECK(params && packed, "dppo_pack_actor: null pointer");
     DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
-    return dppo_pack_mlp(D.IN, D.H, D.XD, D.TD, precision, params, packed, (hipStream_t)stream, D.K);
+    return dppo_pack_mlp(D.IN, D.H, D.XD, D.TD, precision, params, packed, (hipStream_t)stream, D.K, D.TS);
 }
 extern "C" int dppo_pack_critic(const dppo_dims* d, int precision, const float* params, void* packed, void* stream) {
     Dims D;

@@ -8,11 +8,11 @@ int dppo_set_error(int code, const char* fmt, ...);
 int dppo_hip_fail(hipError_t e, const char* what);
 
 int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* params,
-                  void* packed, hipStream_t s, int temb_steps = 0);
+                  void* packed, hipStream_t s, int temb_steps = 0, int time_stride = 1);
 
 // derived dimensions of a dppo_dims
 struct Dims {
-    int Do, Da, Ta, To, TD, H, HC, K, KF;
+    int Do, Da, Ta, To, TD, H, HC, K, KF, TS;   // K = sampling steps, TS = time stride
     int XD, SD, IN;   // XD = Ta*Da, SD = To*Do, IN = XD + TD + SD
 };
 int dppo_check_dims(const dppo_dims* d, Dims* out);

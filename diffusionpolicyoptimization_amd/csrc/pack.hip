@@ -70,9 +70,9 @@ __global__ void pack_all_kernel(PackArgs a) {
 static inline uint8_t* P_out(void* p) { return (uint8_t*)p; }
 
 __global__ __launch_bounds__(128) void temb_table_kernel(const float* __restrict__ params, FlatOffsets F, int TD,
-                                                         float* __restrict__ temb) {
+                                                         int stride, float* __restrict__ temb) {
     __shared__ float ta1[128];
-    const int t = blockIdx.x, tid = threadIdx.x;
+    const int row = blockIdx.x, t = row * stride, tid = threadIdx.x;   // row r holds t_emb(r * stride)
     const int half = TD / 2;
     const float lnf = logf(10000.f) / (float)(half - 1);
     if (tid < 2 * TD) {
@@ -87,12 +87,12 @@ __global__ __launch_bounds__(128) void temb_table_kernel(const float* __restrict
     if (tid < TD) {
         float acc = params[F.time_b2 + tid];
         for (int k = 0; k < 2 * TD; ++k) acc += ta1[k] * params[F.time_w2 + k * TD + tid];
-        temb[(size_t)t * TD + tid] = acc;
+        temb[(size_t)row * TD + tid] = acc;
     }
 }
 
 int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* params,
-                  void* packed, hipStream_t s, int temb_steps) {
+                  void* packed, hipStream_t s, int temb_steps, int time_stride) {
     const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision, temb_steps);
     const FlatOffsets F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
     const int KG = precision == DPPO_BF16 ? 32 : 16;
@@ -129,7 +129,7 @@ int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precisi
         hipLaunchKernelGGL((pack_all_kernel<16, 4>), dim3(blocks), dim3(256), 0, s, a);
     DPPO_HIP(hipGetLastError());
     if (L.temb_steps > 0) {
-        hipLaunchKernelGGL(temb_table_kernel, dim3(L.temb_steps), dim3(128), 0, s, params, F, time_dim,
+        hipLaunchKernelGGL(temb_table_kernel, dim3(L.temb_steps), dim3(128), 0, s, params, F, time_dim, time_stride,
                            (float*)(P_out(packed) + L.off[SEG_TEMB]));
         DPPO_HIP(hipGetLastError());
     }

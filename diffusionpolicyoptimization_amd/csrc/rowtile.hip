@@ -806,8 +806,10 @@ static int dispatch_actor(const ActorArgs& a, hipStream_t s) {
 int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
     if (precision != DPPO_BF16) return dispatch_actor<PolicyF32, 2, 8>(a, s);
     const int v = row_tile_cfg().actor;
-    // bf16, H = 512: 64-row tiles on 16 waves halve the weight stream per row of 32-row tiles
-    if (a.H == 512 && v == 0) return dispatch_actor<PolicyBF16, 4, 16>(a, s);
+    // bf16, H = 512: 64-row tiles on 16 waves halve the weight stream per row of 32-row tiles; their
+    // out-layer partials (16 waves x 64 rows x 16*NO) only fit the aliased LDS tile for XD <= 16
+    // (walker2d / halfcheetah, XD = 24, run the 32-row tile)
+    if (a.H == 512 && v == 0 && a.XD <= 16) return dispatch_actor<PolicyBF16, 4, 16>(a, s);
     return v == 2 ? dispatch_actor<PolicyBF16, 2, 8, true>(a, s) : dispatch_actor<PolicyBF16, 2, 8>(a, s);
 }
 

@@ -455,8 +455,10 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
             const float* sc = sch + t * DPPO_SCHED_COLS;
             const float c0 = sc[0], c1 = sc[1], c2 = sc[2], c3 = sc[3];
             float sd = expf(0.5f * sc[4]);
-            if (a.deterministic && t == 0) sd = 0.f;
-            else if (a.deterministic) sd = fminf(fmaxf(sd, 1e-3f), 1e6f);
+            // eval noise rule of the table row (include/dppo.h: DDPM t = 0 or any DDIM row -> 0;
+            // other DDPM rows clip at 1e-3; diffusion_vpg.py:303-315)
+            if (a.deterministic && sc[6] != 0.f) sd = 0.f;
+            else if (a.deterministic) sd = fminf(fmaxf(sd, sc[5]), 1e6f);
             else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
             const float xe = xs[ve], ze = zt[i * 16 * XD + ve], be = bb[3 * H + qe];
             const uint64_t* src = xb + (size_t)m * NV + vw + sl;

@@ -242,7 +242,8 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
 // ---------------------------------------------------------------------------------------------
 #define TB_THREADS 1024
 __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __restrict__ gseg, const float* __restrict__ prm,
-                                                       float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF) {
+                                                       float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF,
+                                                       int TS) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* dtemb = sm;                  // [KF][TD]
     float* e = dtemb + KF * TD;         // [KF][TD]
@@ -268,7 +269,7 @@ __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __res
     }
     for (int i = tid; i < KF * TD; i += TB_THREADS) {
         const int q = i / TD, j = i % TD;
-        const float f = expf(-(float)(j % half) * lnf) * (float)q;
+        const float f = expf(-(float)(j % half) * lnf) * (float)(q * TS);   // bucket q = row q: t = q * TS
         e[i] = j < half ? sinf(f) : cosf(f);
     }
     __syncthreads();
@@ -584,7 +585,7 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     if (side) DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
 
     const size_t tsm = sizeof(float) * (size_t)D.KF * (2 * D.TD + 2 * 2 * D.TD);
-    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, ws.gseg, actor_params, ga, FA, D.XD, D.TD, D.H, D.KF);
+    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, ws.gseg, actor_params, ga, FA, D.XD, D.TD, D.H, D.KF, D.TS);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }

@@ -7,7 +7,7 @@ import numpy as np
 import torch
 
 from ... import ops
-from .sampling import ddpm_buffers
+from .sampling import ddim_buffers, ddpm_buffers
 
 log = logging.getLogger(__name__)
 
@@ -18,16 +18,14 @@ class DiffusionModel:
     def __init__(self, network, horizon_steps, obs_dim, action_dim, network_path=None, device="cuda:0",
                  denoised_clip_value=1.0, randn_clip_value=10.0, final_action_clip_value=None, eps_clip_value=None,
                  denoising_steps=100, predict_epsilon=True, use_ddim=False, ddim_discretize="uniform", ddim_steps=None,
-                 precision="fp32", seed=42, **kwargs):
+                 precision="fp32", seed=42, ddim_eta=1.0, **kwargs):
         if not predict_epsilon:
             raise NotImplementedError("predict_epsilon=False is not used by the DPPO cfgs")
         if denoised_clip_value != 1.0:
             raise NotImplementedError("the sampler epilogue implements denoised_clip_value = 1.0 (diffusion.py:28)")
-        if use_ddim:
-            raise NotImplementedError("DDIM sampling: SURVEY.md §8(f) rank 4 (the reference DDIM path is broken, "
-                                      "quirk 6); not implemented this round")
         if eps_clip_value is not None:
-            log.info("eps_clip_value only affects DDIM; ignored for DDPM as in the reference")
+            # DDIM: the reference computes the clip and discards it (diffusion_vpg.py:213-214)
+            log.info("eps_clip_value has no effect (the reference discards the clipped eps)")
         if precision not in ops._lib.PRECISION:
             raise ValueError(f"precision must be one of {sorted(ops._lib.PRECISION)}")
         self.device = torch.device(device)
@@ -49,4 +47,21 @@ class DiffusionModel:
         buf = ddpm_buffers(self.denoising_steps)
         for k, v in buf.items():
             setattr(self, k, v)
-        self.sched = torch.tensor(ops.sched_table(buf), device=self.device)
+        if use_ddim:
+            # DDIM (BASELINE config 5): ddim_steps sampling rows at t = j K/S;
+            # train/logprob use eta, eval (deterministic) sampling eta = 0 (diffusion_vpg.py:222-224)
+            dd = ddim_buffers(self.denoising_steps, ddim_steps, ddim_eta)
+            for k, v in dd.items():
+                setattr(self, k, v)
+            self.sampling_steps, self.time_stride = int(ddim_steps), dd["time_stride"]
+            self.sched = torch.tensor(ops.sched_table(dd), device=self.device)
+            self.sched_eval = torch.tensor(ops.sched_table(ddim_buffers(self.denoising_steps, ddim_steps, 0.0)),
+                                           device=self.device)
+        else:
+            self.sampling_steps, self.time_stride = self.denoising_steps, 1
+            self.sched = torch.tensor(ops.sched_table(buf), device=self.device)
+            self.sched_eval = self.sched
+
+    def sched_for(self, deterministic):
+        """The schedule table of a sampling call (DDIM eval sampling runs eta = 0)."""
+        return self.sched_eval if deterministic else self.sched

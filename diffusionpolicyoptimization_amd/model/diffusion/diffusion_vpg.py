@@ -31,10 +31,11 @@ class VPGDiffusion(DiffusionModel):
     def __init__(self, actor, critic, ft_denoising_steps, ft_denoising_steps_d=0, ft_denoising_steps_t=0,
                  network_path=None, min_sampling_denoising_std=0.1, min_logprob_denoising_std=0.1, eta=None,
                  learn_eta=False, **kwargs):
-        super().__init__(network=actor, network_path=network_path, **kwargs)
-        assert ft_denoising_steps <= self.denoising_steps
-        if learn_eta or eta is not None:
-            raise NotImplementedError("eta / learn_eta belong to DDIM (not implemented this round)")
+        if learn_eta:
+            raise NotImplementedError("learn_eta: the reference's eta module is absent from it (model/diffusion/"
+                                      "eta.py is not in the repository); a fixed eta (EtaFixed) is supported")
+        super().__init__(network=actor, network_path=network_path, ddim_eta=self._fixed_eta(eta), **kwargs)
+        assert ft_denoising_steps <= self.sampling_steps
         self.ft_denoising_steps = int(ft_denoising_steps)
         self.ft_denoising_steps_d = ft_denoising_steps_d
         self.ft_denoising_steps_t = ft_denoising_steps_t
@@ -49,7 +50,8 @@ class VPGDiffusion(DiffusionModel):
         self.dims = ops.ModelDims(obs_dim=self.obs_dim, action_dim=self.action_dim,
                                   horizon_steps=self.horizon_steps, cond_steps=cond_steps, time_dim=actor.time_dim,
                                   actor_hidden=actor.hidden, critic_hidden=critic.hidden,
-                                  denoising_steps=self.denoising_steps, ft_denoising_steps=self.ft_denoising_steps)
+                                  denoising_steps=self.sampling_steps, ft_denoising_steps=self.ft_denoising_steps,
+                                  time_stride=self.time_stride)
         self.actor_spec = ops.actor_param_spec(self.dims)
         self.critic_spec = ops.critic_param_spec(self.dims)
         self.n_actor = ops.spec_count(self.actor_spec)
@@ -71,6 +73,18 @@ class VPGDiffusion(DiffusionModel):
         self._call_id = 0
         self._env_offset = 0
         log.info("Number of finetuned parameters: %d (actor_ft) + %d (critic)", self.n_actor, self.n_critic)
+
+    @staticmethod
+    def _fixed_eta(eta):
+        """eta of the DDIM mean/variance: a number, or an EtaFixed-style config {base_eta: x}
+        (the original DPPO's model.diffusion.eta.EtaFixed; default 1)."""
+        if eta is None:
+            return 1.0
+        if isinstance(eta, (int, float)):
+            return float(eta)
+        if hasattr(eta, "get") and eta.get("base_eta") is not None:
+            return float(eta.get("base_eta"))
+        raise ValueError(f"eta must be a number or an EtaFixed config with base_eta, got {eta!r}")
 
     # ------------------------------------------------------------------ parameters
     @property
@@ -160,7 +174,8 @@ class VPGDiffusion(DiffusionModel):
         E = state.shape[0]
         packed_ft = self.packed_base if use_base_policy else self.packed_ft
         acts, chains = ops.sample(
-            self.dims, self.precision, self.packed_base, packed_ft, self.sched, state, x_T=x_T, noise=noise,
+            self.dims, self.precision, self.packed_base, packed_ft, self.sched_for(deterministic), state, x_T=x_T,
+            noise=noise,
             seed=self.seed, call_id=self._call_id, env_offset=self._env_offset, deterministic=deterministic,
             min_sampling_std=self.get_min_sampling_denoising_std(), randn_clip=self.randn_clip_value,
             final_clip=self.final_action_clip_value, actions=actions_out, chains=chains_out,

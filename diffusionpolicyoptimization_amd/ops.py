@@ -24,8 +24,9 @@ class ModelDims:
     time_dim: int = 16
     actor_hidden: int = 512
     critic_hidden: int = 256
-    denoising_steps: int = 20
+    denoising_steps: int = 20       # sampling steps (DDIM: ddim_steps)
     ft_denoising_steps: int = 10
+    time_stride: int = 1            # diffusion time of sampling row r is r * time_stride (DDIM: K / S)
 
     @property
     def xd(self):
@@ -41,7 +42,8 @@ class ModelDims:
 
     def c(self):
         return _lib.DppoDims(self.obs_dim, self.action_dim, self.horizon_steps, self.cond_steps, self.time_dim,
-                             self.actor_hidden, self.critic_hidden, self.denoising_steps, self.ft_denoising_steps)
+                             self.actor_hidden, self.critic_hidden, self.denoising_steps, self.ft_denoising_steps,
+                             self.time_stride)
 
 
 def actor_param_spec(d: ModelDims):
@@ -186,7 +188,7 @@ class SampleStepper:
         m = self.model
         fc = m.final_action_clip_value
         cond_host, actions, actions_host = self._fixed
-        rc = self._fn(ctypes.byref(self._dims), _prec(m.precision), ptr(m.packed_base), ptr(m.packed_ft), ptr(m.sched),
+        rc = self._fn(ctypes.byref(self._dims), _prec(m.precision), ptr(m.packed_base), ptr(m.packed_ft), ptr(m.sched_for(deterministic)),
                       cond_host, ctypes.c_void_p(self._obs0 + i * self._obs_step), self.E,
                       ctypes.c_uint64(m.seed & (2 ** 64 - 1)), ctypes.c_uint64(m._call_id), m._env_offset,
                       int(bool(deterministic)), float(m.get_min_sampling_denoising_std()), float(m.randn_clip_value),
@@ -249,7 +251,7 @@ class RolloutPipe:
         fc = m.final_action_clip_value
         p = self._p
         self.enqueued += 1
-        rc = self._fn(ctypes.byref(self._dims), _prec(m.precision), ptr(m.packed_base), ptr(m.packed_ft), ptr(m.sched),
+        rc = self._fn(ctypes.byref(self._dims), _prec(m.precision), ptr(m.packed_base), ptr(m.packed_ft), ptr(m.sched_for(deterministic)),
                       p["obs"], ctypes.c_void_p(self._obs0 + i * self._obs_step), self.E,
                       ctypes.c_uint64(m.seed & (2 ** 64 - 1)), ctypes.c_uint64(m._call_id), m._env_offset,
                       int(bool(deterministic)), float(m.get_min_sampling_denoising_std()), float(m.randn_clip_value),
@@ -456,7 +458,15 @@ def adamw(params, grads, m, v, step, lr, weight_decay=0.004, beta1=0.9, beta2=0.
 
 
 def sched_table(schedule):
-    """[K][8] fp32 table from the fp32 DDPM buffers (see model/diffusion/sampling.py)."""
+    """[rows][8] fp32 table (include/dppo.h) from the fp32 DDPM buffers, or from the DDIM
+    sub-sequence coefficients (model/diffusion/sampling.py: ddpm_buffers / ddim_buffers)."""
+    if "ddim_c0" in schedule:
+        tab = np.zeros((len(schedule["ddim_c0"]), _lib.SCHED_COLS), np.float32)
+        for j, k in enumerate(("ddim_c0", "ddim_c1", "ddim_c2", "ddim_c3", "ddim_logvar")):
+            tab[:, j] = schedule[k]
+        tab[:, 5] = 0.0                      # eval: no noise on any DDIM row (diffusion_vpg.py:303-306)
+        tab[:, 6] = 1.0
+        return tab
     K = len(schedule["betas"])
     tab = np.zeros((K, _lib.SCHED_COLS), np.float32)
     tab[:, 0] = schedule["sqrt_recip_alphas_cumprod"]
@@ -464,6 +474,8 @@ def sched_table(schedule):
     tab[:, 2] = schedule["ddpm_mu_coef1"]
     tab[:, 3] = schedule["ddpm_mu_coef2"]
     tab[:, 4] = schedule["ddpm_logvar_clipped"]
+    tab[:, 5] = 1e-3                         # eval: t > 0 clips at 1e-3, t = 0 has no noise (:308-312)
+    tab[0, 6] = 1.0
     return tab
 
 

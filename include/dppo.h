@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 1
+#define DPPO_ABI_VERSION 2
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -52,12 +52,25 @@ typedef struct dppo_dims {
     int32_t time_dim;         /* TD (16) */
     int32_t actor_hidden;     /* H  (512), multiple of 128 */
     int32_t critic_hidden;    /* HC (256), multiple of 128 */
-    int32_t denoising_steps;  /* K  (20) */
+    int32_t denoising_steps;  /* sampling steps: K (20) for DDPM, ddim_steps S (10) for DDIM */
     int32_t ft_denoising_steps; /* K' (10) */
+    int32_t time_stride;      /* diffusion time of sampling row r = r * time_stride: 1 (or 0) for DDPM,
+                                 K / S for DDIM (diffusion.py:76-82 uniform discretisation); since ABI 2 */
 } dppo_dims;
 
-/* DDPM schedule table, one row per t: {sqrt_recip_ac, sqrt_recipm1_ac, mu_coef1, mu_coef2,
- * logvar_clipped, 0, 0, 0} fp32 — the buffers of model/diffusion/diffusion.py:57-73. */
+/* Schedule table, one fp32 row per sampling row r (r = t for DDPM; the DDIM sub-sequence index for
+ * DDIM): {c0, c1, c2, c3, logvar, eval_floor, eval_zero, 0} with
+ *   x0 = clip(c0 x - c1 eps, -1, 1);  mu = c2 x0 + c3 x;  sigma = exp(logvar / 2)
+ * and the eval-mode (deterministic) noise rule sigma = eval_zero ? 0 : clip(sigma, eval_floor, 1e6).
+ *   DDPM (model/diffusion/diffusion.py:57-73, diffusion_vpg.py:198-243, 303-315): c0 = sqrt(1/abar_t),
+ *     c1 = sqrt(1/abar_t - 1), c2 = mu_coef1, c3 = mu_coef2, logvar = logvar_clipped; eval_floor
+ *     1e-3, eval_zero = (t == 0).
+ *   DDIM (diffusion.py:76-96, diffusion_vpg.py:184-234, the documented formulas): with abar, abar_prev
+ *     of the sub-sequence and eps' = (x - sqrt(abar) x0) / sqrt(1 - abar) after the clip,
+ *     mu = sqrt(abar_prev) x0 + d eps', d = sqrt(max(1 - abar_prev - sigma^2, 0)), which is the same
+ *     affine form: c2 = sqrt(abar_prev) - d sqrt(abar) / sqrt(1 - abar), c3 = d / sqrt(1 - abar);
+ *     c0 = 1 / sqrt(abar), c1 = sqrt(1/abar - 1); logvar = log(sigma^2), sigma = max(eta sqrt((1 - abar_prev)
+ *     / (1 - abar) (1 - abar / abar_prev)), 1e-10); eval_floor 0, eval_zero 1. */
 #define DPPO_SCHED_COLS 8
 
 DPPO_API int         dppo_abi_version(void);

@@ -54,6 +54,46 @@ def ddpm_schedule(K):
                 ddpm_var=var, ddpm_logvar_clipped=logvar, ddpm_mu_coef1=coef1, ddpm_mu_coef2=coef2)
 
 
+def ddim_schedule(K, S, eta=1.0):
+    """DDIM sub-sequence (diffusion.py:76-96; diffusion_vpg.py:184-234 documented formulas) with
+    the corrections of SURVEY.md §8 quirk 6: walked from the largest t down, alpha_prev = the
+    previous SUB-SEQUENCE element, fixed eta, eps recomputed from the clipped x0. PARITY
+    UNPINNED: the reference DDIM path cannot run (quirk 6), so this restates the formulas.
+    Returns the affine per-row coefficients under the DDPM keys p_mean_var reads (row j = DDIM
+    index, diffusion time j*K/S), plus the raw sub-sequence arrays (p_mean_var_ddim_direct)."""
+    f = np.float32
+    one = f(1.0)
+    ratio = K // S
+    ac = ddpm_schedule(K)["alphas_cumprod"]
+    a = ac[np.arange(S) * ratio].astype(f)
+    ap = np.concatenate([np.ones(1, f), a[:-1]]).astype(f)
+    sig = np.maximum((f(eta) * np.sqrt((one - ap) / (one - a) * (one - a / ap))).astype(f), f(1e-10))
+    d = np.sqrt(np.clip(one - ap - sig * sig, 0, 1e6)).astype(f)
+    sa, s1a = np.sqrt(a).astype(f), np.sqrt(one - a).astype(f)
+    return dict(sqrt_recip_alphas_cumprod=(one / sa).astype(f), sqrt_recipm1_alphas_cumprod=(s1a / sa).astype(f),
+                ddpm_mu_coef1=(np.sqrt(ap) - d * sa / s1a).astype(f), ddpm_mu_coef2=(d / s1a).astype(f),
+                ddpm_logvar_clipped=np.log(sig * sig).astype(f), time_stride=ratio, eval_floor=0.0,
+                eval_zero=np.ones(S, bool), ddim_alphas=a, ddim_alphas_prev=ap, ddim_sigmas=sig, ddim_dir=d)
+
+
+def p_mean_var_ddim_direct(sched, eps, x, j, denoised_clip=1.0):
+    """The documented DDIM mean, term by term (diffusion_vpg.py:193-196, 204-212, 221-232):
+    x0 = (x - sqrt(1-a) eps)/sqrt(a); clip; eps = (x - sqrt(a) x0)/sqrt(1-a);
+    mu = sqrt(a_prev) x0 + sqrt(1 - a_prev - sigma^2) eps."""
+    sh = (-1,) + (1,) * (x.ndim - 1)
+    a = sched["ddim_alphas"].astype(np.float64)[j].reshape(sh)
+    ap = sched["ddim_alphas_prev"].astype(np.float64)[j].reshape(sh)
+    sig = sched["ddim_sigmas"].astype(np.float64)[j].reshape(sh)
+    x0 = np.clip((x - np.sqrt(1 - a) * eps) / np.sqrt(a), -denoised_clip, denoised_clip)
+    e2 = (x - np.sqrt(a) * x0) / np.sqrt(1 - a)
+    mu = np.sqrt(ap) * x0 + np.sqrt(np.clip(1 - ap - sig ** 2, 0, 1e6)) * e2
+    return mu, np.log(sig ** 2)
+
+
+def _tstride(sched):
+    return int(sched.get("time_stride", 1))
+
+
 # ----------------------------------------------------------------------------------------------
 # activations (model/common/mlp.py:6-14) and Dense
 # ----------------------------------------------------------------------------------------------
@@ -240,13 +280,14 @@ def sample(p_base, p_ft, sched, state, x_T, z, ft_steps, deterministic=False, mi
         t = K - 1 - i
         tb = np.full(x.shape[0], t)
         params = p_ft if t < ft_steps else p_base                # :161-180
-        eps, _ = diffusion_mlp_forward(params, x, tb, state, rnd=rnd, round_h3=round_h3)
+        eps, _ = diffusion_mlp_forward(params, x, tb * _tstride(sched), state, rnd=rnd, round_h3=round_h3)
         mu, logvar, _ = p_mean_var(sched, eps, x, tb)
         std = np.exp(0.5 * logvar)                               # :301
-        if deterministic and t == 0:                             # :310-315
+        ez = sched["eval_zero"][t] if "eval_zero" in sched else t == 0
+        if deterministic and ez:                                 # :303-315 (DDIM: always 0)
             std = np.zeros_like(std)
         elif deterministic:
-            std = np.clip(std, 1e-3, 1e6)
+            std = np.clip(std, sched.get("eval_floor", 1e-3), 1e6)
         else:
             std = np.clip(std, min_std, 1e6)
         noise = np.clip(z[i], -randn_clip, randn_clip)           # :319
@@ -273,7 +314,7 @@ def get_logprobs(p_ft, sched, state, chains, ft_steps, min_logprob_std=0.1, rnd=
     t_all = np.tile(np.arange(ft_steps - 1, -1, -1), n)          # :385-390
     prev = chains[:, :-1].reshape(-1, *chains.shape[2:])          # :402-407
     nxt = chains[:, 1:].reshape(-1, *chains.shape[2:])
-    eps, _ = diffusion_mlp_forward(p_ft, prev, t_all, cond, rnd=rnd)
+    eps, _ = diffusion_mlp_forward(p_ft, prev, t_all * _tstride(sched), cond, rnd=rnd)
     mu, logvar, _ = p_mean_var(sched, eps, prev, t_all)
     std = np.clip(np.exp(0.5 * logvar), min_logprob_std, 1e6)    # :417-418
     return gaussian_logprob(nxt, mu, std)
@@ -299,7 +340,7 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
     b = obs.shape[0]
     j = np.asarray(denoising_inds)
     t = ft_steps - 1 - j                                          # :456-458
-    eps, acache = diffusion_mlp_forward(p_ft, chains_prev, t, obs, rnd=rnd)
+    eps, acache = diffusion_mlp_forward(p_ft, chains_prev, t * _tstride(sched), obs, rnd=rnd)
     mu, logvar, pm = p_mean_var(sched, eps, chains_prev, t)
     std = np.clip(np.exp(0.5 * logvar), min_logprob_std, 1e6)
     lp_el = gaussian_logprob(chains_next, mu, std)

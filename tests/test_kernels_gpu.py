@@ -8,19 +8,26 @@ import pytest
 
 from oracle import dppo_oracle as O
 from oracle import philox as PX
-from tests.helpers import HOPPER, WALKER, make_models, to_f64
+from tests.helpers import HOPPER, HOPPER_DDIM, WALKER, make_models, to_f64
 
 pytestmark = pytest.mark.gpu
 
 
-def _setup(dims, cuda, seed=0):
+def _setup(dims, cuda, seed=0, eta=1.0):
+    """dims with time_stride > 1 are DDIM: sched is then the oracle's DDIM restatement and tab the
+    product's table (model/diffusion/sampling.py ddim_buffers) for the same (K, S, eta)."""
     import torch
     from diffusionpolicyoptimization_amd import ops
-    from diffusionpolicyoptimization_amd.model.diffusion.sampling import ddpm_buffers
+    from diffusionpolicyoptimization_amd.model.diffusion.sampling import ddim_buffers, ddpm_buffers
     d = ops.ModelDims(**dims)
-    base, ft, critic = make_models(seed, dims)
-    sched = ddpm_buffers(d.denoising_steps)
-    tab = torch.tensor(ops.sched_table(sched), device=cuda)
+    base, ft, critic = make_models(seed, {k: v for k, v in dims.items() if k != "time_stride"})
+    if d.time_stride > 1:
+        K = d.denoising_steps * d.time_stride
+        sched = O.ddim_schedule(K, d.denoising_steps, eta)
+        tab = torch.tensor(ops.sched_table(ddim_buffers(K, d.denoising_steps, eta)), device=cuda)
+    else:
+        sched = ddpm_buffers(d.denoising_steps)
+        tab = torch.tensor(ops.sched_table(sched), device=cuda)
     fa = lambda p: torch.tensor(ops.flatten_params(ops.actor_param_spec(d), p), device=cuda)
     fc = lambda p: torch.tensor(ops.flatten_params(ops.critic_param_spec(d), p), device=cuda)
     return d, base, ft, critic, sched, tab, fa(base), fa(ft), fc(critic)
@@ -130,6 +137,72 @@ def test_sampler_split_repeatable(cuda):
         assert torch.equal(o, outs[0])
 
 
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-4), ("bf16", 3e-3)])
+def test_sampler_ddim(cuda, precision, tol):
+    """BASELINE config 5's DDIM sampler (10 rows over K = 20, eta = 1) vs the oracle's DDIM
+    restatement (parity-unpinned: the reference DDIM path cannot run)."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER_DDIM, cuda)
+    E, S = 37, d.denoising_steps
+    rng = np.random.default_rng(21)
+    state = rng.uniform(-1, 1, (E, 1, d.obs_dim)).astype(np.float32)
+    xT = rng.standard_normal((E, 4, 3)).astype(np.float32)
+    z = rng.standard_normal((S, E, 4, 3)).astype(np.float32)
+    split = ops.sampler_layout(d, precision, E) > 0
+    ref_a, ref_c = O.sample(to_f64(base), to_f64(ft), sched, state.astype(np.float64), xT, z, d.ft_denoising_steps,
+                            rnd=_rnd(precision), round_h3=not split)
+    packb, packf = ops.pack_actor(d, pb, precision), ops.pack_actor(d, pf, precision)
+    act, ch = ops.sample(d, precision, packb, packf, tab, torch.tensor(state.reshape(E, -1), device=cuda),
+                         x_T=torch.tensor(xT.reshape(E, -1), device=cuda),
+                         noise=torch.tensor(z.reshape(S, E, -1), device=cuda))
+    torch.cuda.synchronize()
+    act = act.cpu().numpy().reshape(ref_a.shape)
+    ch = ch.cpu().numpy().reshape(ref_c.shape)
+    assert ch.shape[1] == d.ft_denoising_steps + 1
+    if precision == "fp32":
+        assert np.abs(act - ref_a).max() < tol and np.abs(ch - ref_c).max() < tol
+    else:
+        assert np.quantile(np.abs(act - ref_a), 0.99) < tol and np.abs(ch - ref_c).mean() < tol
+
+
+def test_sampler_ddim_eval(cuda):
+    """Deterministic DDIM sampling: the eta = 0 table and no noise on any row (diffusion_vpg.py:222-224,
+    303-306), fp32 vs the oracle."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER_DDIM, cuda, eta=0.0)
+    E, S = 16, d.denoising_steps
+    rng = np.random.default_rng(22)
+    state = rng.uniform(-1, 1, (E, 1, d.obs_dim)).astype(np.float32)
+    xT = rng.standard_normal((E, 4, 3)).astype(np.float32)
+    z = rng.standard_normal((S, E, 4, 3)).astype(np.float32)
+    ref_a, _ = O.sample(to_f64(base), to_f64(ft), sched, state.astype(np.float64), xT, z, d.ft_denoising_steps,
+                        deterministic=True)
+    packb, packf = ops.pack_actor(d, pb, "fp32"), ops.pack_actor(d, pf, "fp32")
+    act, _ = ops.sample(d, "fp32", packb, packf, tab, torch.tensor(state.reshape(E, -1), device=cuda),
+                        x_T=torch.tensor(xT.reshape(E, -1), device=cuda),
+                        noise=torch.tensor(z.reshape(S, E, -1), device=cuda), deterministic=True)
+    torch.cuda.synchronize()
+    assert np.abs(act.cpu().numpy().reshape(ref_a.shape) - ref_a).max() < 2e-4
+
+
+def test_logprob_ddim(cuda):
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER_DDIM, cuda)
+    n, kf = 29, d.ft_denoising_steps
+    rng = np.random.default_rng(23)
+    state = rng.uniform(-1, 1, (n, 1, d.obs_dim)).astype(np.float32)
+    chains = (rng.standard_normal((n, kf + 1, 4, 3)) * 0.5).astype(np.float32)
+    ref = O.get_logprobs(to_f64(ft), sched, state.astype(np.float64), chains.astype(np.float64), kf)
+    lpe, _ = ops.logprob(d, "fp32", ops.pack_actor(d, pf, "fp32"), tab, torch.tensor(state.reshape(n, -1), device=cuda),
+                         torch.tensor(chains.reshape(n, kf + 1, -1), device=cuda))
+    torch.cuda.synchronize()
+    rel = np.abs(lpe.cpu().numpy().reshape(ref.shape) - ref) / (1 + np.abs(ref))
+    assert rel.max() < 1e-3, rel.max()
+
+
 def test_sampler_deterministic_and_empty(cuda):
     import torch
     from diffusionpolicyoptimization_amd import ops
@@ -151,14 +224,15 @@ def test_sampler_deterministic_and_empty(cuda):
 
 
 @pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 2e-3)])
-def test_logprob(cuda, precision, tol):
+@pytest.mark.parametrize("dims", [HOPPER, WALKER], ids=["hopper", "walker"])
+def test_logprob(cuda, precision, tol, dims):
     import torch
     from diffusionpolicyoptimization_amd import ops
-    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(dims, cuda)
     n = 45
     rng = np.random.default_rng(4)
     state = rng.uniform(-1, 1, (n, 1, d.obs_dim)).astype(np.float32)
-    chains = (rng.standard_normal((n, d.ft_denoising_steps + 1, 4, 3)) * 0.5).astype(np.float32)
+    chains = (rng.standard_normal((n, d.ft_denoising_steps + 1, d.horizon_steps, d.action_dim)) * 0.5).astype(np.float32)
     ref = O.get_logprobs(to_f64(ft), sched, state.astype(np.float64), chains.astype(np.float64), d.ft_denoising_steps,
                          rnd=_rnd(precision))
     packf = ops.pack_actor(d, pf, precision)
@@ -254,7 +328,9 @@ def test_adamw(cuda, mode):
 
 
 @pytest.mark.parametrize("precision,case,rtol", [("fp32", "perturbed", 2e-3), ("fp32", "ratio1", 2e-3),
-                                                  ("bf16", "ratio1", 1e-2), ("bf16", "perturbed", 2e-2)])
+                                                  ("bf16", "ratio1", 1e-2), ("bf16", "perturbed", 2e-2),
+                                                  ("fp32", "perturbed-ddim", 2e-3), ("fp32", "perturbed-walker", 2e-3),
+                                                  ("bf16", "ratio1-walker", 1e-2)])
 def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     """c_loss forward metrics and gradients of pg_loss + 0.5 v_loss vs the oracle.
 
@@ -266,7 +342,9 @@ def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     because these minibatch sums cancel ~12x and clip branches flip under rounding)."""
     import torch
     from diffusionpolicyoptimization_amd import ops
-    dims = HOPPER
+    # DDIM: time-MLP gradient at t = 2j; walker: XD = 24 through the 32-row actor tile
+    dims = HOPPER_DDIM if case.endswith("-ddim") else (WALKER if case.endswith("-walker") else HOPPER)
+    case = case.replace("-ddim", "").replace("-walker", "")
     d, base, ft, critic, sched, tab, pb, pf, pc = _setup(dims, cuda)
     rng = np.random.default_rng(12)
     N = 40                                  # samples (steps*envs)
@@ -279,7 +357,7 @@ def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     T = lambda x: torch.tensor(x, device=cuda)
     packf = ops.pack_actor(d, pf, precision)
     lp_ref = O.get_logprobs(to_f64(ft), sched, obs.reshape(N, 1, -1).astype(np.float64),
-                            chains.reshape(N, kf + 1, 4, 3).astype(np.float64), kf, rnd=_rnd(precision))
+                            chains.reshape(N, kf + 1, d.horizon_steps, d.action_dim).astype(np.float64), kf, rnd=_rnd(precision))
     lp_ref_mean = np.clip(lp_ref, -5, 2).mean(axis=(1, 2)).reshape(N, kf)
     if case == "perturbed":
         lp_old = (lp_ref_mean + rng.normal(0, 0.02, (N, kf))).astype(np.float32)
@@ -294,7 +372,7 @@ def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     bi, di = perm // kf, perm % kf
     metrics_ref, ga_ref, gc_ref = O.c_loss(
         to_f64(ft), to_f64(critic), sched, obs[bi].reshape(rows, 1, -1).astype(np.float64),
-        chains[bi, di].reshape(rows, 4, 3).astype(np.float64), chains[bi, di + 1].reshape(rows, 4, 3).astype(np.float64),
+        chains[bi, di].reshape(rows, d.horizon_steps, d.action_dim).astype(np.float64), chains[bi, di + 1].reshape(rows, d.horizon_steps, d.action_dim).astype(np.float64),
         di, ret[bi].astype(np.float64), None, adv[bi].astype(np.float64), lp_old_ref[bi, di], kf,
         rnd=_rnd(precision))
     na = ops.spec_count(ops.actor_param_spec(d))
