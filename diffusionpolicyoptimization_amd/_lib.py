@@ -57,6 +57,8 @@ _SIGNATURES = {
     "dppo_host_free": (_I, [_P]),
     "dppo_rollout_enqueue": (_I, [_DIMS, _I, _P, _P, _P, _P, _P, _I, _U64, _U64, _I, _I, _F, _F, _F, _P, _P, _P, _P,
                                   ctypes.c_uint32, _P, _P]),
+    "dppo_rollout_enqueue_tagged": (_I, [_DIMS, _I, _P, _P, _P, _P, _P, _I, _U64, _U64, _I, _I, _F, _F, _F, _P, _P,
+                                         _P, ctypes.c_uint32, _P, _P]),
     "dppo_sampler_stream_bytes": (_I, [_DIMS, _I, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]),
     "dppo_sampler_layout": (_I, [_DIMS, _I, _I, ctypes.POINTER(ctypes.c_int)]),
     "dppo_logprob": (_I, [_DIMS, _I, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P]),

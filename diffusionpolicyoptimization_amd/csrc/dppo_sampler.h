@@ -22,6 +22,10 @@ struct SampleArgs {
     const uint32_t* go;
     uint32_t go_value;
     uint32_t* done;
+    // tagged observation (dppo_rollout_enqueue_tagged): [E][SD] granules {tag << 32 | fp32 bits}
+    // polled until every tag equals cond_tag (then cond is unused); null = cond / go as above
+    const uint64_t* cond_tagged;
+    uint32_t cond_tag;
     uint64_t seed;
     uint32_t call_id;
     int E, env_offset, deterministic;
@@ -29,6 +33,53 @@ struct SampleArgs {
     int XD, SD, TD, H, K, KF, IN;
     MlpLayout L;          // same layout for base and ft
 };
+
+// This workgroup's 16 env rows of a TAGGED observation into st[16][SD]: every thread polls its
+// granules (system-scope relaxed loads of mapped host memory) until each carries a.cond_tag — the
+// value arrives with its own ready flag, so there is no separate flag round trip. Bounded (4 s):
+// on timeout the step runs on what it read and (flag_timeout) sets bit 31 of *done.
+template <int ST>
+__device__ inline void sampler_load_state_tagged(const SampleArgs& a, int row0, float* st, bool flag_timeout, int tid) {
+    const int SD = a.SD, n = 16 * SD;
+    constexpr int NG = (16 * 64 + ST - 1) / ST;     // SD <= 64 (dppo_check_dims)
+    float v[NG];
+    bool ok[NG];
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+        const int i = tid + u * ST;
+        ok[u] = !(i < n && row0 + i / SD < a.E);
+        v[u] = 0.f;
+    }
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;   // 100 MHz: 4 s
+    for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int u = 0; u < NG; ++u) {
+            const int i = tid + u * ST;
+            if (!ok[u]) {
+                const uint64_t x = __hip_atomic_load(a.cond_tagged + (size_t)(row0 + i / SD) * SD + i % SD,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((uint32_t)(x >> 32) == a.cond_tag) {
+                    ok[u] = true;
+                    v[u] = __uint_as_float((uint32_t)x);
+                }
+            }
+            all = all && ok[u];
+        }
+        if (__syncthreads_and(all)) break;
+        if (__syncthreads_or(__builtin_amdgcn_s_memrealtime() > t_end)) {
+            if (flag_timeout && tid == 0 && a.done)
+                __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+        const int i = tid + u * ST;
+        if (i < n) st[i] = v[u];
+    }
+}
 
 // The split sampler (sampler_split.hip): returns DPPO_OK after launching, DPPO_EUNSUPPORTED (without
 // touching the error message) when the shape is outside what it instantiates, or another error code.

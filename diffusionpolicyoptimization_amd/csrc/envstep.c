@@ -154,3 +154,33 @@ DPPO_ENV_API int dppo_env_step_gated(int E, int Do, int Da, int act_steps, int T
     }
     return n_done;
 }
+
+/* Write the [E][n] float observation as tagged granules {tag << 32 | fp32 bits} (the tagged
+ * rollout protocol, dppo_rollout_enqueue_tagged): each granule is one aligned 8-byte store, so the
+ * device never sees a torn value, and a value with the new tag is the new observation. */
+DPPO_ENV_API void dppo_env_publish_tagged(int64_t count, const float* obs, uint64_t* obs_tagged, uint32_t tag) {
+    const uint64_t hi = (uint64_t)tag << 32;
+    for (int64_t i = 0; i < count; ++i) {
+        uint32_t bits;
+        memcpy(&bits, obs + i, 4);
+        __atomic_store_n(obs_tagged + i, hi | bits, __ATOMIC_RELAXED);
+    }
+}
+
+/* dppo_env_step_gated with the tagged protocol: after the step, when no episode ended (no reset
+ * left for the host to apply), the observation is published as granules with `tag`. */
+DPPO_ENV_API int dppo_env_step_gated_tagged(int E, int Do, int Da, int act_steps, int Ta, int max_steps, int n_obs_steps,
+                                            const double* AT, const double* B, const double* c, const double* goal,
+                                            double* state, int64_t* cnt, const float* actions, double* reward,
+                                            uint8_t* terminated, uint8_t* truncated, float* obs_out,
+                                            const volatile uint32_t* done, uint32_t done_target, uint64_t* obs_tagged,
+                                            uint32_t tag, double timeout_s) {
+    const int rc = dppo_env_step_gated(E, Do, Da, act_steps, Ta, max_steps, n_obs_steps, AT, B, c, goal, state, cnt,
+                                       actions, reward, terminated, truncated, obs_out, done, done_target, NULL, 0,
+                                       timeout_s);
+    if (rc == 0 && obs_tagged) {
+        dppo_env_publish_tagged((int64_t)E * n_obs_steps * Do, obs_out, obs_tagged, tag);
+        return DPPO_ENV_PUBLISHED;
+    }
+    return rc;
+}

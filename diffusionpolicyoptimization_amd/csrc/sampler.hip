@@ -273,6 +273,13 @@ __global__ __launch_bounds__(SW * 64) void sample_kernel(SampleArgs a) {
     // a pre-enqueued step waits here (everything above does not depend on the observation) for
     // the host to publish it; bounded: ~4 s, then the step runs on whatever is in the buffer and
     // flags the timeout in the high bit of *done so the host reports it
+    if (a.cond_tagged) {
+        sampler_load_state_tagged<ST>(a, row0, st, true, tid);
+        for (int i = tid; i < 16 * SD; i += ST) {
+            const int row = row0 + i / SD;
+            if (a.cond_out && row < a.E) a.cond_out[(size_t)row * SD + i % SD] = st[i];
+        }
+    } else {
     if (a.go) {
         if (tid == 0) {
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;   // 100 MHz clock: 4 s
@@ -291,6 +298,7 @@ __global__ __launch_bounds__(SW * 64) void sample_kernel(SampleArgs a) {
         const float v = row < a.E ? a.cond[(size_t)row * SD + c] : 0.f;
         st[i] = v;
         if (a.cond_out && row < a.E) a.cond_out[(size_t)row * SD + c] = v;
+    }
     }
     __syncthreads();
     // a0 = [x, temb(t), state, 0-pad] for step 0 (t = K-1); later steps get x and temb from the
@@ -556,20 +564,22 @@ static int sample_impl(const dppo_dims* d, int precision, const void* packed_bas
                        uint64_t seed, uint64_t call_id, int env_offset, int deterministic,
                        float min_sampling_std, float randn_clip, float final_clip,
                        float* actions, float* chains, float* cond_out, float* actions_host, void* stream,
-                       const uint32_t* go = nullptr, uint32_t go_value = 0, uint32_t* done = nullptr) {
+                       const uint32_t* go = nullptr, uint32_t go_value = 0, uint32_t* done = nullptr,
+                       const uint64_t* cond_tagged = nullptr, uint32_t cond_tag = 0) {
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
     DPPO_CHECK(n_envs >= 0, "dppo_sample: n_envs < 0");
     DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "dppo_sample: bad precision %d", precision);
     if (n_envs == 0) return DPPO_OK;
-    DPPO_CHECK(packed_base && packed_ft && sched && cond && actions, "dppo_sample: null pointer argument");
+    DPPO_CHECK(packed_base && packed_ft && sched && (cond || cond_tagged) && actions, "dppo_sample: null pointer argument");
     SampleArgs a;
     a.packed_base = (const uint8_t*)packed_base;
     a.packed_ft = (const uint8_t*)packed_ft;
     a.sched = sched; a.cond = cond; a.x_T = x_T; a.noise = noise; a.actions = actions; a.chains = chains;
     a.cond_out = cond_out; a.actions_host = actions_host;
     a.go = go; a.go_value = go_value; a.done = done;
+    a.cond_tagged = cond_tagged; a.cond_tag = cond_tag;
     a.seed = seed; a.call_id = (uint32_t)call_id; a.E = n_envs; a.env_offset = env_offset;
     a.deterministic = deterministic; a.min_std = min_sampling_std; a.randn_clip = randn_clip; a.final_clip = final_clip;
     a.XD = D.XD; a.SD = D.SD; a.TD = D.TD; a.H = D.H; a.K = D.K; a.KF = D.KF; a.IN = D.IN;
@@ -684,4 +694,22 @@ extern "C" int dppo_rollout_enqueue(const dppo_dims* d, int precision, const voi
     return sample_impl(d, precision, packed_base, packed_ft, sched, cond_dev, n_envs, nullptr, nullptr, seed, call_id,
                        env_offset, deterministic, min_sampling_std, randn_clip, final_clip, actions, chains, cond,
                        act_dev, stream, go_dev, go_value, done_dev);
+}
+
+extern "C" int dppo_rollout_enqueue_tagged(const dppo_dims* d, int precision, const void* packed_base,
+                                           const void* packed_ft, const float* sched, const uint64_t* obs_tagged,
+                                           float* cond, int n_envs, uint64_t seed, uint64_t call_id, int env_offset,
+                                           int deterministic, float min_sampling_std, float randn_clip,
+                                           float final_clip, float* actions, float* actions_host, float* chains,
+                                           uint32_t tag, uint32_t* done, void* stream) {
+    DPPO_CHECK(obs_tagged && cond && actions && actions_host && done, "dppo_rollout_enqueue_tagged: null pointer argument");
+    DPPO_CHECK(tag != 0, "dppo_rollout_enqueue_tagged: tag 0 is the buffer's initial value");
+    const uint64_t* obs_dev = (const uint64_t*)mapped_ptr(obs_tagged);
+    float* act_dev = (float*)mapped_ptr(actions_host);
+    uint32_t* done_dev = (uint32_t*)mapped_ptr(done);
+    DPPO_CHECK(obs_dev && act_dev && done_dev,
+               "dppo_rollout_enqueue_tagged: staging buffers must come from dppo_host_alloc (mapped, coherent)");
+    return sample_impl(d, precision, packed_base, packed_ft, sched, nullptr, n_envs, nullptr, nullptr, seed, call_id,
+                       env_offset, deterministic, min_sampling_std, randn_clip, final_clip, actions, chains, cond,
+                       act_dev, stream, nullptr, 0, done_dev, obs_dev, tag);
 }

@@ -264,6 +264,13 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
     permute_out();
     // pre-enqueued rollout step: wait for the host's observation (bounded, as sampler.hip)
     XPHASE(7);                                              // timing builds: phase 7 = prologue before the wait
+    if (a.cond_tagged) {
+        sampler_load_state_tagged<ST>(a, row0, st, c == 0, tid);
+        for (int i = tid; i < 16 * SD; i += ST) {
+            const int r = i / SD, cc = i % SD, row = row0 + r;
+            if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, st[i]);
+        }
+    } else {
     if (a.go) {
         if (tid == 0) {
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;   // 100 MHz: 4 s
@@ -290,6 +297,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
         const float v = row < a.E ? a.cond[(size_t)row * SD + cc] : 0.f;
         st[i] = v;
         if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, v);
+    }
     }
     __syncthreads();
     const int k1w = KSI * 32;

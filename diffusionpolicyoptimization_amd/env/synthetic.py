@@ -30,6 +30,11 @@ def _native():
         lib.dppo_env_step_gated.argtypes = [ctypes.c_int] * 7 + [P] * 11 + [P, ctypes.c_uint32, P, ctypes.c_uint32,
                                                                             ctypes.c_double]
         lib.dppo_env_step_gated.restype = ctypes.c_int
+        lib.dppo_env_step_gated_tagged.argtypes = [ctypes.c_int] * 7 + [P] * 11 + [P, ctypes.c_uint32, P,
+                                                                                   ctypes.c_uint32, ctypes.c_double]
+        lib.dppo_env_step_gated_tagged.restype = ctypes.c_int
+        lib.dppo_env_publish_tagged.argtypes = [ctypes.c_int64, P, P, ctypes.c_uint32]
+        lib.dppo_env_publish_tagged.restype = None
         _lib = lib
     return _lib
 
@@ -92,9 +97,10 @@ class SyntheticLocomotionVecEnv:
 
     def step(self, actions, obs_out=None, gate=None):
         """actions [E, Ta, Da]; obs_out: optional float32 [E, To, Do] buffer (e.g. pinned staging).
-        gate: (done_addr, done_target, go_addr, go_value) of a pipelined rollout (ops.RolloutPipe.gate):
-        the native stepper waits for the device's done counter, steps, and publishes go itself when
-        no env needs a reset; self.published tells the caller whether it did."""
+        gate: (protocol, done_addr, done_target, publish_addr, tag, timeout) of a pipelined rollout
+        (ops.RolloutPipe.gate): the native stepper waits for the device's done counter, steps, and
+        publishes the observation itself (go counter, or tagged granules) when no env needs a reset;
+        self.published tells the caller whether it did."""
         E = self.num_envs
         self.published = False
         if gate is not None and self.native is None:
@@ -119,9 +125,10 @@ class SyntheticLocomotionVecEnv:
                                                    self.max_episode_steps, self.n_obs_steps, *self._static_ptrs,
                                                    self._last_pa, *self._tail_ptrs, self._last_po)
             else:
-                rc = self.native.dppo_env_step_gated(E, self.obs_dim, self.action_dim, self.act_steps, ta,
-                                                     self.max_episode_steps, self.n_obs_steps, *self._static_ptrs,
-                                                     self._last_pa, *self._tail_ptrs, self._last_po, *gate)
+                # gate[0] names the protocol: "go" (counter) or "tagged" (tagged observation granules)
+                fn = self.native.dppo_env_step_gated_tagged if gate[0] == "tagged" else self.native.dppo_env_step_gated
+                rc = fn(E, self.obs_dim, self.action_dim, self.act_steps, ta, self.max_episode_steps,
+                        self.n_obs_steps, *self._static_ptrs, self._last_pa, *self._tail_ptrs, self._last_po, *gate[1:])
                 if rc < 0:
                     raise RuntimeError("pipelined rollout: " + ("the device's wait for the observation timed out"
                                                                 if rc == -2 else "the sampler step did not finish"))

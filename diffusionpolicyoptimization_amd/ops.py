@@ -5,6 +5,7 @@ stream of the tensor's device. Shapes/dtypes are checked here before any launch 
 call can never reach a kernel with mismatched extents.
 """
 import ctypes
+import os
 import math
 from dataclasses import dataclass
 
@@ -226,13 +227,21 @@ class RolloutPipe:
             self._bufs.append(p.value)
             return p.value
         po, pa, pc = alloc(4 * E * d.sd), alloc(4 * E * d.xd), alloc(256)
+        # the observation protocol: "tagged" (default: the observation is published as tagged
+        # granules the launch polls itself, dppo_rollout_enqueue_tagged) or "go" (a go counter, then
+        # the launch reads the float buffer); DPPO_ROLLOUT_PROTOCOL=go selects the latter
+        self.protocol = os.environ.get("DPPO_ROLLOUT_PROTOCOL", "tagged")
+        if self.protocol not in ("tagged", "go"):
+            raise ValueError(f"DPPO_ROLLOUT_PROTOCOL must be 'tagged' or 'go', got {self.protocol!r}")
+        pt = alloc(8 * E * d.sd)
+        self._obs_tag = np.ctypeslib.as_array((ctypes.c_uint64 * (E * d.sd)).from_address(pt))
         self.obs = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_float * (E * d.sd)).from_address(po))).view(E, d.sd)
         self.act = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_float * (E * d.xd)).from_address(pa))).view(E, d.xd)
         ctr = np.ctypeslib.as_array((ctypes.c_uint32 * 64).from_address(pc))
         self._go, self._done = ctr[0:1], ctr[16:17]          # separate 64-B lines
         self._p = dict(obs=ctypes.c_void_p(po), act=ctypes.c_void_p(pa), go=ctypes.c_void_p(pc),
-                       done=ctypes.c_void_p(pc + 64))
-        self._fn = lib.dppo_rollout_enqueue
+                       done=ctypes.c_void_p(pc + 64), obs_tag=ctypes.c_void_p(pt))
+        self._fn = lib.dppo_rollout_enqueue_tagged if self.protocol == "tagged" else lib.dppo_rollout_enqueue
         self._dims = d.c()
         self._keep = (obs_traj, actions, chains_traj)
         self._obs0, self._obs_step = obs_traj.data_ptr(), E * d.sd * 4
@@ -251,29 +260,40 @@ class RolloutPipe:
         fc = m.final_action_clip_value
         p = self._p
         self.enqueued += 1
-        rc = self._fn(ctypes.byref(self._dims), _prec(m.precision), ptr(m.packed_base), ptr(m.packed_ft), ptr(m.sched_for(deterministic)),
-                      p["obs"], ctypes.c_void_p(self._obs0 + i * self._obs_step), self.E,
-                      ctypes.c_uint64(m.seed & (2 ** 64 - 1)), ctypes.c_uint64(m._call_id), m._env_offset,
-                      int(bool(deterministic)), float(m.get_min_sampling_denoising_std()), float(m.randn_clip_value),
-                      float(fc) if fc is not None else 0.0, self._actions, p["act"],
-                      ctypes.c_void_p(self._ch0 + i * self._ch_step), p["go"], ctypes.c_uint32(self.enqueued),
-                      p["done"], self._stream)
+        common = (ctypes.byref(self._dims), _prec(m.precision), ptr(m.packed_base), ptr(m.packed_ft),
+                  ptr(m.sched_for(deterministic)))
+        tail = (self.E, ctypes.c_uint64(m.seed & (2 ** 64 - 1)), ctypes.c_uint64(m._call_id), m._env_offset,
+                int(bool(deterministic)), float(m.get_min_sampling_denoising_std()), float(m.randn_clip_value),
+                float(fc) if fc is not None else 0.0, self._actions, p["act"],
+                ctypes.c_void_p(self._ch0 + i * self._ch_step))
+        obs_dev = ctypes.c_void_p(self._obs0 + i * self._obs_step)
+        if self.protocol == "tagged":   # step s waits for granules tagged s + 1 (= its publish count)
+            rc = self._fn(*common, p["obs_tag"], obs_dev, *tail, ctypes.c_uint32(self.enqueued), p["done"],
+                          self._stream)
+        else:
+            rc = self._fn(*common, p["obs"], obs_dev, *tail, p["go"], ctypes.c_uint32(self.enqueued), p["done"],
+                          self._stream)
         if rc:
             raise _lib.DppoError(f"dppo_rollout_enqueue failed ({rc}): {self._lib.dppo_last_error().decode()}")
         m._call_id += 1
 
     def publish(self):
         self.published += 1
-        self._go[0] = self.published          # x86 stores are ordered: the observation is visible first
+        if self.protocol == "tagged":         # one aligned 8-byte store per value: never torn
+            bits = self.obs.numpy().reshape(-1).view(np.uint32).astype(np.uint64)
+            self._obs_tag[:] = (np.uint64(self.published) << np.uint64(32)) | bits
+        else:
+            self._go[0] = self.published      # x86 stores are ordered: the observation is visible first
 
     def gate(self, publish, timeout_s=30.0):
         """Arguments of a gated env step (env.step(..., gate=...)): the native stepper waits for
         this step's done count itself and, if publish, releases the next launch. Call
         published() after a step that did publish, publish() after one that did not."""
         self.finished += 1
-        go = (self._p["go"], self.published + 1) if publish else (None, 0)
-        return (self._p["done"], ctypes.c_uint32(self.finished * self.nwg), go[0], ctypes.c_uint32(go[1]),
-                ctypes.c_double(timeout_s))
+        dst = self._p["obs_tag"] if self.protocol == "tagged" else self._p["go"]
+        pub = (dst, self.published + 1) if publish else (None, 0)
+        return (self.protocol, self._p["done"], ctypes.c_uint32(self.finished * self.nwg), pub[0],
+                ctypes.c_uint32(pub[1]), ctypes.c_double(timeout_s))
 
     def published_by_gate(self):
         self.published += 1

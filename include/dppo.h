@@ -140,6 +140,19 @@ DPPO_API int dppo_rollout_enqueue(const dppo_dims* d, int precision, const void*
                 float randn_clip, float final_clip, float* actions, float* actions_host,
                 float* chains, const uint32_t* go, uint32_t go_value, uint32_t* done, void* stream);
 
+/* The same pipelined step with a TAGGED observation (ABI 2): no go counter; the host writes each
+ * observation value as an 8-byte granule {tag in the high 32 bits, fp32 bits in the low 32} into
+ * obs_tagged ([n_envs][To*Do] uint64, from dppo_host_alloc), and the launch polls its envs'
+ * granules until every tag equals `tag` (nonzero, unique among the tags the buffer may hold, e.g.
+ * the step count). The observation carries its own ready flag: one PCIe round trip instead of a
+ * flag poll followed by a read. done / timeout as dppo_rollout_enqueue; cond receives the device
+ * copy of the observation. */
+DPPO_API int dppo_rollout_enqueue_tagged(const dppo_dims* d, int precision, const void* packed_base,
+                const void* packed_ft, const float* sched, const uint64_t* obs_tagged, float* cond,
+                int n_envs, uint64_t seed, uint64_t call_id, int env_offset, int deterministic,
+                float min_sampling_std, float randn_clip, float final_clip, float* actions,
+                float* actions_host, float* chains, uint32_t tag, uint32_t* done, void* stream);
+
 /* ---- a10: VPGDiffusion.get_logprobs (diffusion_vpg.py:343-425) + the clip/mean of c_loss
  * (diffusion_ppo.py:50-59) for the old-logprob pass (agent/finetune/train_ppo_diffusion_agent.py:214-229).
  *   cond [n, To*Do], chains [n, K'+1, Ta*Da]

@@ -61,14 +61,18 @@ def test_bound_rollout_step_matches_model_call(cuda):
         step(S)
 
 
-def test_pipelined_rollout_matches_model_call(cuda):
-    """dppo_rollout_enqueue (pre-enqueued launches gated by the go/done counters) == model(...)."""
+@pytest.mark.parametrize("protocol,precision", [("tagged", "bf16"), ("go", "bf16"), ("tagged", "fp32")])
+def test_pipelined_rollout_matches_model_call(cuda, protocol, precision, monkeypatch):
+    """Pre-enqueued launches fed by the host == model(...), for both observation protocols:
+    dppo_rollout_enqueue_tagged (the launch polls tagged observation granules) and
+    dppo_rollout_enqueue (a go counter, then the float buffer)."""
     import torch
 
+    monkeypatch.setenv("DPPO_ROLLOUT_PROTOCOL", protocol)
     from diffusionpolicyoptimization_amd import ops
     from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
     cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
-                      ["model.precision=bf16"])
+                      [f"model.precision={precision}"])
     model = instantiate(cfg.model, device=cuda, seed=5)
     d = model.dims
     S, E = 4, 40
@@ -76,6 +80,7 @@ def test_pipelined_rollout_matches_model_call(cuda):
     chains = torch.zeros(S, E, d.ft_denoising_steps + 1, d.xd, device=cuda)
     act = torch.empty(E, d.xd, device=cuda)
     pipe = ops.RolloutPipe(model, obs_traj, act, chains)
+    assert pipe.protocol == protocol
     rng = np.random.default_rng(2)
     obs = [rng.uniform(-1, 1, (E, d.sd)).astype(np.float32) for _ in range(S)]
     cid0 = model._call_id

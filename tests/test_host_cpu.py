@@ -133,7 +133,7 @@ def test_gated_env_step_publishes_only_without_resets():
     for i in range(5):                          # 12 sub-steps = 3 chunks: step 2 truncates every env
         a = rng.normal(0, 0.5, (E, 4, Da)).astype(np.float32)
         ctr[0] = i + 1                          # the "device" has finished step i
-        g = envs[0].step(a, obs_out=obs[0], gate=(done_p, ctypes.c_uint32(i + 1), go_p, ctypes.c_uint32(i + 2),
+        g = envs[0].step(a, obs_out=obs[0], gate=("go", done_p, ctypes.c_uint32(i + 1), go_p, ctypes.c_uint32(i + 2),
                                                   ctypes.c_double(1.0)))
         r = envs[1].step(a, obs_out=obs[1])
         np.testing.assert_array_equal(obs[0], obs[1])
@@ -144,12 +144,49 @@ def test_gated_env_step_publishes_only_without_resets():
             assert ctr[16] == i + 2
     assert pubs == [True, True, False, True, True]
     with pytest.raises(RuntimeError, match="did not finish"):     # done never reaches the target
-        envs[0].step(a, obs_out=obs[0], gate=(done_p, ctypes.c_uint32(99), None, ctypes.c_uint32(0),
+        envs[0].step(a, obs_out=obs[0], gate=("go", done_p, ctypes.c_uint32(99), None, ctypes.c_uint32(0),
                                               ctypes.c_double(0.01)))
     ctr[0] = 0x80000000                                           # the device's go-wait timed out
     with pytest.raises(RuntimeError, match="timed out"):
-        envs[0].step(a, obs_out=obs[0], gate=(done_p, ctypes.c_uint32(1), None, ctypes.c_uint32(0),
+        envs[0].step(a, obs_out=obs[0], gate=("go", done_p, ctypes.c_uint32(1), None, ctypes.c_uint32(0),
                                               ctypes.c_double(1.0)))
+
+
+def test_gated_env_step_tagged_publishes_granules():
+    """dppo_env_step_gated_tagged: like the go protocol, but the observation is published as tagged
+    granules {tag << 32 | fp32 bits} (what the sampler polls, dppo_rollout_enqueue_tagged)."""
+    import ctypes
+
+    from diffusionpolicyoptimization_amd.env.synthetic import SyntheticLocomotionVecEnv, _native
+    if _native() is None:
+        subprocess.run(["make", "-C", os.path.join(ROOT, "diffusionpolicyoptimization_amd", "csrc"), "-j8"],
+                       check=True)
+    E, Do, Da = 5, 11, 3
+    envs = [SyntheticLocomotionVecEnv(E, Do, Da, act_steps=4, max_episode_steps=12, family_seed=1) for _ in range(2)]
+    for e in envs:
+        e.seed(range(E))
+        e.reset_arg()
+    ctr = np.zeros(16, dtype=np.uint32)
+    done_p = ctypes.c_void_p(ctr.ctypes.data)
+    tagged = np.zeros(E * Do, np.uint64)
+    tag_p = ctypes.c_void_p(tagged.ctypes.data)
+    obs = [np.zeros((E, 1, Do), np.float32) for _ in range(2)]
+    rng = np.random.default_rng(1)
+    pubs = []
+    for i in range(5):
+        a = rng.normal(0, 0.5, (E, 4, Da)).astype(np.float32)
+        ctr[0] = i + 1
+        g = envs[0].step(a, obs_out=obs[0], gate=("tagged", done_p, ctypes.c_uint32(i + 1), tag_p,
+                                                  ctypes.c_uint32(i + 2), ctypes.c_double(1.0)))
+        r = envs[1].step(a, obs_out=obs[1])
+        np.testing.assert_array_equal(obs[0], obs[1])
+        np.testing.assert_array_equal(g[1], r[1])
+        pubs.append(envs[0].published)
+        if envs[0].published:
+            assert np.all((tagged >> np.uint64(32)) == i + 2)
+            np.testing.assert_array_equal((tagged & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.float32),
+                                          obs[0].reshape(-1))
+    assert pubs == [True, True, False, True, True]
 
 
 def test_sampler_stream_bytes_per_geometry():
