@@ -15,6 +15,14 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+
+// two floats -> packed bf16 pair (RNE) in ONE v_cvt_pk_bf16_f32; two scalar (__bf16) casts
+// compile to two conversions plus a shift and an or
+__device__ inline unsigned int dppo_pack_bf16x2(float lo, float hi) {
+    return __builtin_bit_cast(unsigned int, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
+}
 
 #define DPPO_WAVES 8
 #define DPPO_THREADS (DPPO_WAVES * 64)

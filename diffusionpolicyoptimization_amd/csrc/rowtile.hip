@@ -74,11 +74,11 @@ __device__ inline void store_accT(__amdgpu_buffer_rsrc_t ws, uint32_t img_off, u
             const uint32_t so = so0 + ((uint32_t)n * 16u * ldm + (uint32_t)mp * 32u) * es;
             const f32x4 lo = v[2 * mp][n], hi = v[2 * mp + 1][n];
             if constexpr (es == 2) {
-                __bf16 e[8] = {(__bf16)lo[0], (__bf16)lo[1], (__bf16)lo[2], (__bf16)lo[3],
-                               (__bf16)hi[0], (__bf16)hi[1], (__bf16)hi[2], (__bf16)hi[3]};
+                const u32x4 e = {dppo_pack_bf16x2(lo[0], lo[1]), dppo_pack_bf16x2(lo[2], lo[3]),
+                                 dppo_pack_bf16x2(hi[0], hi[1]), dppo_pack_bf16x2(hi[2], hi[3])};
                 // soffset must be the literal 0: with an SGPR there, hipcc (ROCm 7.2) does not guard
                 // the >8-byte store-data hazard (a following VALU overwrote the 4th dword)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, e), ws, vo + so, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(e, ws, vo + so, 0, 0);
             } else {
                 // 8-B stores: the 16-B buffer_store form came out with a corrupted 4th dword under
                 // hipcc 7.2 for gfx950 in the fp32 critic (a store-data hazard the compiler does
@@ -101,10 +101,8 @@ __device__ inline void store_img8(void* img, size_t ldm, size_t grow0, int c, in
     for (int k = 0; k < 8; ++k) e[k] = value(img_row(8 * g + k));
     AT* dst = (AT*)img + (size_t)c * ldm + grow0 + 8 * g;
     if constexpr (sizeof(AT) == 2) {
-        __bf16 b[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) b[k] = (__bf16)e[k];
-        *(u32x4*)dst = __builtin_bit_cast(u32x4, b);
+        *(u32x4*)dst = u32x4{dppo_pack_bf16x2(e[0], e[1]), dppo_pack_bf16x2(e[2], e[3]),
+                             dppo_pack_bf16x2(e[4], e[5]), dppo_pack_bf16x2(e[6], e[7])};
     } else {
 #pragma unroll
         for (int k = 0; k < 8; k += 2) *(u32x2*)(dst + k) = u32x2{__float_as_uint(e[k]), __float_as_uint(e[k + 1])};

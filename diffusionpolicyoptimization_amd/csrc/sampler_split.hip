@@ -40,7 +40,8 @@
 
 // phase timing for tuning builds (-DDPPO_SAMPLER_TIMING): thread 0 of every workgroup adds the
 // shader-clock cycles of each phase (0 prologue, 1 actor switch, 2 in-Dense, 3 l1, 4 l2 + out,
-// 5 publish + sweep, 6 epilogue)
+// 5 publish + sweep, 6 epilogue); 11-15 split phases 2-5 at the point wave 0 reaches the barrier
+// (11 in-Dense, 12 l1, 13 l2 GEMM, 14 out-Dense + partial store, 15 partial sum + publish)
 #ifdef DPPO_SAMPLER_TIMING
 __device__ unsigned long long dppo_split_cycles[16 + 64 * 8];
 // [0, 16): phase sums over all workgroups; [16 + 8 i + k): phase k of step i of workgroup 0 alone
@@ -49,7 +50,7 @@ __device__ unsigned long long dppo_split_cycles[16 + 64 * 8];
         if (threadIdx.x == 0) {                                                   \
             const unsigned long long now_ = __builtin_readcyclecounter();         \
             atomicAdd(&dppo_split_cycles[(k)], now_ - t_phase_);                  \
-            if (blockIdx.x == 0 && t_step_ < 64) dppo_split_cycles[16 + 8 * t_step_ + (k)] = now_ - t_phase_; \
+            if (blockIdx.x == 0 && t_step_ < 64 && (k) < 8) dppo_split_cycles[16 + 8 * t_step_ + (k)] = now_ - t_phase_; \
             t_phase_ = now_;                                                      \
         }                                                                         \
     } while (0)
@@ -106,10 +107,7 @@ struct SplitArgs {
 // k-step holds feature e < 4 ? 4j + e : 16 + 4j + (e - 4)
 __device__ inline int slot_feature(int j, int e) { return e < 4 ? 4 * j + e : 16 + 4 * j + (e - 4); }
 
-__device__ inline uint32_t pack_bf16x2(float lo, float hi) {
-    const __bf16 a = (__bf16)lo, b = (__bf16)hi;
-    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
-}
+__device__ inline uint32_t pack_bf16x2(float lo, float hi) { return dppo_pack_bf16x2(lo, hi); }
 
 // XQ = XD / 4 (compile time: the sweep's loads must all be in flight before the first wait)
 template <int P, int XQ, int KSI, bool INJ>
@@ -336,15 +334,26 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
             u32x4 af[KSI];
 #pragma unroll
             for (int ks = 0; ks < KSI; ++ks) af[ks] = lds_afrag<Pol>(a0, lda0, 0, ks, lane);
+            // this wave's in-Dense and l2 biases, read with the fragments (not between the chains)
+            f32x4 bin[4], bl2[4];
 #pragma unroll
             for (int n = 0; n < 4; ++n) {
-                zero_acc(h1[n]);
+                bin[n] = *(const f32x4*)(bb + 16 * (4 * wave + n) + 4 * jq);
+                bl2[n] = *(const f32x4*)(bb + 2 * H + 16 * (4 * wave + n) + 4 * jq);
+            }
+            // k-step outer: four independent accumulator chains in flight (n-outer made hipcc
+            // finish each tile's chain and its relu/pack/store before issuing the next)
 #pragma unroll
-                for (int ks = 0; ks < KSI; ++ks) h1[n] = Pol::mma(rin[ks][n], af[ks], h1[n]);
-                if (pre && n == 3) load_in(PKn);
+            for (int n = 0; n < 4; ++n) zero_acc(h1[n]);
+#pragma unroll
+            for (int ks = 0; ks < KSI; ++ks)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) h1[n] = Pol::mma(rin[ks][n], af[ks], h1[n]);
+            if (pre) load_in(PKn);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
                 const int f = 16 * (4 * wave + n) + 4 * jq;
-                const float4 bv = *(const float4*)(bb + f);
-                h1[n][0] += bv.x; h1[n][1] += bv.y; h1[n][2] += bv.z; h1[n][3] += bv.w;
+                h1[n] += bin[n];
                 u32x2 pk;
                 pk[0] = pack_bf16x2(fmaxf(h1[n][0], 0.f), fmaxf(h1[n][1], 0.f));
                 pk[1] = pack_bf16x2(fmaxf(h1[n][2], 0.f), fmaxf(h1[n][3], 0.f));
@@ -352,24 +361,28 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
             }
             // the residual term member 0 adds to its l2 partial: h1 + b_l2 (mlp.py:206)
 #pragma unroll
-            for (int n = 0; n < 4; ++n) h1[n] += *(const f32x4*)(bb + 2 * H + 16 * (4 * wave + n) + 4 * jq);
+            for (int n = 0; n < 4; ++n) h1[n] += bl2[n];
         }
+        XPHASE(11);
         lds_sync();
         XPHASE(2);
         // ---- l1 (transposed): this member's output columns, K split over KP waves
         {
             f32x4 acc0, acc1;
             zero_acc(acc0); zero_acc(acc1);
+            u32x4 bfr[KS1];                    // every fragment read in flight before the chains
+#pragma unroll
+            for (int j = 0; j < KS1; ++j) bfr[j] = lds_afrag<Pol>(u1, ldh, 0, kp * KS1 + j, lane);
 #pragma unroll
             for (int j = 0; j < KS1; ++j) {
-                const u32x4 bfr = lds_afrag<Pol>(u1, ldh, 0, kp * KS1 + j, lane);
-                if (j & 1) acc1 = Pol::mma(rl1[j], bfr, acc1);
-                else acc0 = Pol::mma(rl1[j], bfr, acc0);
+                if (j & 1) acc1 = Pol::mma(rl1[j], bfr[j], acc1);
+                else acc0 = Pol::mma(rl1[j], bfr[j], acc0);
             }
             if (pre) load_l1(PKn);
             const f32x4 s = acc0 + acc1;
             *(f32x4*)(p1 + (kp * 16 + env) * ldp + 16 * t1 + 4 * jq) = s;
         }
+        XPHASE(12);
         lds_sync();
         XPHASE(3);
         // ---- l2 (transposed) over this member's K-slice: u2 = bf16 relu(h2 + b_l1) (mlp.py:202-206)
@@ -392,23 +405,24 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                               pack_bf16x2(fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f))};
             }
 #pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                zero_acc(h3[n]);
+            for (int n = 0; n < 4; ++n) zero_acc(h3[n]);
 #pragma unroll
-                for (int s = 0; s < KS2; ++s) h3[n] = Pol::mma(rl2[s][n], u2[s], h3[n]);
-            }
+            for (int s = 0; s < KS2; ++s)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) h3[n] = Pol::mma(rl2[s][n], u2[s], h3[n]);
             if (pre) load_l2(PKn);
             if (c == 0) {                                    // + b_l2 + h1 (residual), once per group
 #pragma unroll
                 for (int n = 0; n < 4; ++n) h3[n] += h1[n];
             }
         }
+        XPHASE(13);
         // ---- out-Dense partial (transposed) from this wave's own h3 registers: k-step s covers
         //      h3 tiles 2s, 2s+1 in slot_feature order; hi/lo bf16 split keeps h3 fp32-accurate
         {
-            f32x4 po[NO];
+            f32x4 po[NO], pl[NO];              // hi and lo products: two independent chains
 #pragma unroll
-            for (int n = 0; n < NO; ++n) zero_acc(po[n]);
+            for (int n = 0; n < NO; ++n) { zero_acc(po[n]); zero_acc(pl[n]); }
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 float hv[8];
@@ -418,21 +432,24 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
 #pragma unroll
                 for (int e2 = 0; e2 < 4; ++e2) {
                     const float x0 = hv[2 * e2], x1 = hv[2 * e2 + 1];
-                    const float r0 = (float)(__bf16)x0, r1 = (float)(__bf16)x1;
                     hi[e2] = pack_bf16x2(x0, x1);
+                    const float r0 = __uint_as_float(hi[e2] << 16), r1 = __uint_as_float(hi[e2] & 0xffff0000u);
                     lo[e2] = pack_bf16x2(x0 - r0, x1 - r1);
                 }
 #pragma unroll
                 for (int n = 0; n < NO; ++n) {
                     po[n] = Pol::mma(rout[s][n], hi, po[n]);
-                    po[n] = Pol::mma(rout[s][n], lo, po[n]);
+                    pl[n] = Pol::mma(rout[s][n], lo, pl[n]);
                 }
             }
+#pragma unroll
+            for (int n = 0; n < NO; ++n) po[n] += pl[n];
             if (pre) load_out(PKn);
 #pragma unroll
             for (int n = 0; n < NO; ++n)
                 if (16 * n + 4 * jq < XD) *(f32x4*)(part + wave * NV + env * XD + 16 * n + 4 * jq) = po[n];
         }
+        XPHASE(14);
         lds_sync();
         XPHASE(4);
         // ---- exchange + DDPM epilogue. Wave w owns coordinates [w*NVW, (w+1)*NVW) of the 16 x XD
@@ -451,6 +468,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 __hip_atomic_store(xb + (size_t)c * NV + vw + lane, ((uint64_t)tag << 32) | __float_as_uint(sum),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            XPHASE(15);
             // the next step's time embedding into a0 while the members arrive (a0 was last read by
             // this step's in-Dense, two barriers ago)
             if (t > 0 && lane < 16 * TD / SW) {

@@ -70,6 +70,8 @@ def main():
         wgs = 8 * ((args.envs + 15) // 16)
         names = ["prologue", "switch", "in", "l1", "l2_out", "xchg", "epilogue"]
         phases = {n: round(buf[i] / wgs / (1 if i < 2 else d.denoising_steps)) for i, n in enumerate(names)}
+        for i, n in zip(range(11, 16), ["in_mm", "l1_mm", "l2_mm", "out_mm", "publish"]):
+            phases[n] = round(buf[i] / wgs / d.denoising_steps)
         phases["wg0_steps"] = [[int(buf[16 + 8 * i + k]) for k in range(1, 7)] for i in range(d.denoising_steps)]
     print(json.dumps({"tag": args.tag, "envs": args.envs, "precision": args.precision, "ms_per_launch": ms,
                       "tflops": flops / (ms * 1e-3) / 1e12, "cycles_per_step": phases}), flush=True)
