@@ -109,6 +109,11 @@ __device__ inline int slot_feature(int j, int e) { return e < 4 ? 4 * j + e : 16
 
 __device__ inline uint32_t pack_bf16x2(float lo, float hi) { return dppo_pack_bf16x2(lo, hi); }
 
+template <int CTRL>
+__device__ inline float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
 // XQ = XD / 4 (compile time: the sweep's loads must all be in flight before the first wait)
 template <int P, int XQ, int KSI, bool INJ>
 __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
@@ -370,6 +375,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
         {
             f32x4 acc0, acc1;
             zero_acc(acc0); zero_acc(acc1);
+            const f32x4 bl1 = *(const f32x4*)(bb + H + HS * c + 16 * t1 + 4 * jq);
             u32x4 bfr[KS1];                    // every fragment read in flight before the chains
 #pragma unroll
             for (int j = 0; j < KS1; ++j) bfr[j] = lds_afrag<Pol>(u1, ldh, 0, kp * KS1 + j, lane);
@@ -379,7 +385,8 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 else acc0 = Pol::mma(rl1[j], bfr[j], acc0);
             }
             if (pre) load_l1(PKn);
-            const f32x4 s = acc0 + acc1;
+            f32x4 s = acc0 + acc1;
+            if (kp == 0) s += bl1;                 // the l1 bias rides on K-part 0
             *(f32x4*)(p1 + (kp * 16 + env) * ldp + 16 * t1 + 4 * jq) = s;
         }
         XPHASE(12);
@@ -392,10 +399,10 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
 #pragma unroll
             for (int s = 0; s < KS2; ++s) {
                 const int k0 = 32 * s + 8 * jq;
-                f32x4 v0 = *(const f32x4*)(bb + H + HS * c + k0);
-                f32x4 v1 = *(const f32x4*)(bb + H + HS * c + k0 + 4);
+                f32x4 v0 = *(const f32x4*)(p1 + env * ldp + k0);          // K-part 0 (+ bias)
+                f32x4 v1 = *(const f32x4*)(p1 + env * ldp + k0 + 4);
 #pragma unroll
-                for (int q = 0; q < KP; ++q) {
+                for (int q = 1; q < KP; ++q) {
                     v0 += *(const f32x4*)(p1 + (q * 16 + env) * ldp + k0);
                     v1 += *(const f32x4*)(p1 + (q * 16 + env) * ldp + k0 + 4);
                 }
@@ -507,11 +514,14 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 }
             }
             XPHASE(5);
+            // member sum over the 8 lanes of a slot in DPP (no LDS crossbar): xor 1 and xor 2 inside
+            // the quad, then the half-row mirror pairs each lane with the other quad. Every lane
+            // adds the same two partial sums (a + b == b + a), so all 8 hold the same bits
 #pragma unroll
             for (int k = 0; k < KW; ++k) {
-                val[k] += __shfl_xor(val[k], 1, 64);
-                val[k] += __shfl_xor(val[k], 2, 64);
-                val[k] += __shfl_xor(val[k], 4, 64);
+                val[k] += dpp_f32<0xB1>(val[k]);     // quad_perm [1,0,3,2]
+                val[k] += dpp_f32<0x4E>(val[k]);     // quad_perm [2,3,0,1]
+                val[k] += dpp_f32<0x141>(val[k]);    // row_half_mirror
             }
             // lane (slot sl, member m) finishes coordinate sl + 8m when m < KW
             if (m < KW) {
