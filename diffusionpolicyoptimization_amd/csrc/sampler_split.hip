@@ -79,6 +79,17 @@ extern "C" DPPO_API int dppo_debug_split_cycles(unsigned long long* out, int res
 #define DPPO_SPLIT_SIGNAL 2
 #endif
 
+// exchange sweeps in flight per wave (DPPO_SPLIT_POLL, tuning knob): 1 = load, check, repeat;
+// 2 = the next sweep is issued before the previous one is checked. Measured: 2 is SLOWER (81 vs
+// 67 us per launch): the extra polls queue in front of the granules' own arrival at the consumer.
+// DPPO_SPLIT_POLL_SLEEP > 0 inserts s_sleep(N) between serial sweeps
+#ifndef DPPO_SPLIT_POLL
+#define DPPO_SPLIT_POLL 1
+#endif
+#ifndef DPPO_SPLIT_POLL_SLEEP
+#define DPPO_SPLIT_POLL_SLEEP 0
+#endif
+
 namespace {
 
 // a store of a kernel output that leaves no dirty line in L2 (write-through; see DPPO_SPLIT_SIGNAL)
@@ -498,21 +509,56 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
             float val[KW];
             bool failed = false;
-            for (;;) {
+            auto poll = [&](uint64_t (&x)[KW]) {
+#pragma unroll
+                for (int k = 0; k < KW; ++k) x[k] = __hip_atomic_load(src + 8 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            };
+            auto arrived = [&](const uint64_t (&x)[KW]) {
                 bool ok = true;
 #pragma unroll
-                for (int k = 0; k < KW; ++k) {
-                    const uint64_t x = __hip_atomic_load(src + 8 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok &= (uint32_t)(x >> 32) == tag;
-                    val[k] = __uint_as_float((uint32_t)x);
+                for (int k = 0; k < KW; ++k) ok &= (uint32_t)(x[k] >> 32) == tag;
+                if (!__all(ok)) return false;
+#pragma unroll
+                for (int k = 0; k < KW; ++k) val[k] = __uint_as_float((uint32_t)x[k]);
+                return true;
+            };
+#if DPPO_SPLIT_POLL >= 2
+            // two sweeps in flight: the next is issued before the previous one is checked, so a
+            // granule is seen about half an L2 round trip after it lands instead of a whole one
+            uint64_t xa[KW], xc[KW];
+            poll(xa);
+            for (;;) {
+                bool got = false;
+#pragma unroll 1
+                for (int r = 0; r < 16 && !got; ++r) {
+                    poll(xc);
+                    got = arrived(xa);
+                    if (got) break;
+                    poll(xa);
+                    got = arrived(xc);
                 }
-                if (__all(ok)) break;
+                if (got) break;
                 if (__builtin_amdgcn_s_memrealtime() > t_end) {
                     failed = true;
                     if (lane == 0) *xfail = 1;
                     break;
                 }
             }
+#else
+            uint64_t xa[KW];
+            for (;;) {
+                poll(xa);
+                if (arrived(xa)) break;
+#if DPPO_SPLIT_POLL_SLEEP > 0
+                __builtin_amdgcn_s_sleep(DPPO_SPLIT_POLL_SLEEP);
+#endif
+                if (__builtin_amdgcn_s_memrealtime() > t_end) {
+                    failed = true;
+                    if (lane == 0) *xfail = 1;
+                    break;
+                }
+            }
+#endif
             XPHASE(5);
             // member sum over the 8 lanes of a slot in DPP (no LDS crossbar): xor 1 and xor 2 inside
             // the quad, then the half-row mirror pairs each lane with the other quad. Every lane
