@@ -396,10 +396,23 @@ __host__ __device__ inline uint64_t feistel_permute(uint64_t i, const FeistelKey
 // ------------------------------------------------------------------------------------------------
 // wave reductions
 // ------------------------------------------------------------------------------------------------
+// DPP inside each 16-lane row (quad xor 1, xor 2, half-row mirror, row mirror: every lane of a row
+// holds the row sum), then the four row sums through readlane; every lane returns the same total.
+// The LDS-crossbar butterfly (__shfl_xor = ds_bpermute) cost ~6 dependent LDS round trips.
+template <int CTRL>
+__device__ inline float dpp_movf(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
 __device__ inline float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += dpp_movf<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_movf<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_movf<0x141>(v);   // row_half_mirror
+    v += dpp_movf<0x140>(v);   // row_mirror
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return (r0 + r1) + (r2 + r3);
 }
 __device__ inline double wave_sumd(double v) {
 #pragma unroll

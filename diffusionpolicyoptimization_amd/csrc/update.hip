@@ -241,52 +241,71 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
 //   in_b' = sum_q G[q];  dtemb[q] = G[q] . W_in[XD:XD+TD]^T;  then Dense/mish/Dense backward.
 // ---------------------------------------------------------------------------------------------
 #define TB_THREADS 1024
+// One workgroup; every parameter it reads (the TD temb rows of W_in and the time MLP) is staged into
+// LDS in one batch of coalesced loads at the start, so the dependent phases below run from LDS and
+// the kernel pays global-load latency about twice (staging, then G) instead of once per phase.
 __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __restrict__ gseg, const float* __restrict__ prm,
                                                        float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF,
-                                                       int TS) {
+                                                       int TS, int stage_g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* dtemb = sm;                  // [KF][TD]
+    float* win = sm;                    // [TD][H]   W_in rows XD .. XD+TD-1
+    float* w1 = win + TD * H;           // [TD][2TD]
+    float* b1 = w1 + TD * 2 * TD;       // [2TD]
+    float* w2 = b1 + 2 * TD;            // [2TD][TD]
+    float* dtemb = w2 + 2 * TD * TD;    // [KF][TD]
     float* e = dtemb + KF * TD;         // [KF][TD]
     float* a1 = e + KF * TD;            // [KF][2TD]
     float* da1 = a1 + KF * 2 * TD;      // [KF][2TD]
+    float* gs = stage_g ? da1 + KF * 2 * TD : nullptr;   // [KF][H] copy of G when it fits
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int n = tid; n < H; n += TB_THREADS) {
-        float s = 0.f;
-        for (int q = 0; q < KF; ++q) s += gseg[q * H + n];
-        grad[F.in_b + n] = s;
+    if (gs) {
+#pragma unroll 8
+        for (int i = tid; i < KF * H; i += TB_THREADS) gs[i] = gseg[i];
     }
+    // (loops with global loads are unrolled so their loads issue together: a runtime-bound loop
+    // otherwise waits out one load latency per iteration)
+#pragma unroll 8
+    for (int i = tid; i < TD * H; i += TB_THREADS) win[i] = prm[F.in_w + (size_t)XD * H + i];
+    for (int i = tid; i < TD * 2 * TD; i += TB_THREADS) { w1[i] = prm[F.time_w1 + i]; w2[i] = prm[F.time_w2 + i]; }
+    for (int i = tid; i < 2 * TD; i += TB_THREADS) b1[i] = prm[F.time_b1 + i];
     const int half = TD / 2;
     const float lnf = logf(10000.f) / (float)(half - 1);
-    // dtemb[q][j] = G[q] . W_in[XD + j]: one wave per output, lanes over the hidden units
-    for (int i = wave; i < KF * TD; i += TB_THREADS / 64) {
-        const int q = i / TD, j = i % TD;
-        const float* g = gseg + q * H;
-        const float* w = prm + F.in_w + (size_t)(XD + j) * H;
-        float s = 0.f;
-        for (int n = lane; n < H; n += 64) s += g[n] * w[n];
-        s = wave_sum(s);
-        if (lane == 0) dtemb[i] = s;
-    }
     for (int i = tid; i < KF * TD; i += TB_THREADS) {
         const int q = i / TD, j = i % TD;
         const float f = expf(-(float)(j % half) * lnf) * (float)(q * TS);   // bucket q = row q: t = q * TS
         e[i] = j < half ? sinf(f) : cosf(f);
     }
+    for (int n = tid; n < H; n += TB_THREADS) {       // in_b' = sum_q G[q]
+        float s = 0.f;
+#pragma unroll 8
+        for (int q = 0; q < KF; ++q) s += gseg[q * H + n];
+        grad[F.in_b + n] = s;
+    }
     __syncthreads();
+    // dtemb[q][j] = G[q] . W_in[XD + j]: one wave per (q, j), lanes over the hidden units, G from
+    // LDS when it was staged (gs != nullptr), W_in rows from LDS
+    for (int i = wave; i < KF * TD; i += TB_THREADS / 64) {
+        const int q = i / TD, j = i % TD;
+        const float* g = (gs ? gs : gseg) + q * H;
+        float s = 0.f;
+#pragma unroll 8
+        for (int n = lane; n < H; n += 64) s += g[n] * win[j * H + n];
+        s = wave_sum(s);
+        if (lane == 0) dtemb[i] = s;
+    }
     for (int i = tid; i < KF * 2 * TD; i += TB_THREADS) {
         const int q = i / (2 * TD), h = i % (2 * TD);
-        float s = prm[F.time_b1 + h];
-        for (int k = 0; k < TD; ++k) s += e[q * TD + k] * prm[F.time_w1 + k * 2 * TD + h];
+        float s = b1[h];
+        for (int k = 0; k < TD; ++k) s += e[q * TD + k] * w1[k * 2 * TD + h];
         a1[i] = s;
     }
     __syncthreads();
     for (int i = tid; i < KF * 2 * TD; i += TB_THREADS) {
         const int q = i / (2 * TD), h = i % (2 * TD);
         float dm = 0.f;
-        for (int j = 0; j < TD; ++j) dm += dtemb[q * TD + j] * prm[F.time_w2 + h * TD + j];
+        for (int j = 0; j < TD; ++j) dm += dtemb[q * TD + j] * w2[h * TD + j];
         da1[i] = dm * mish_gradf(a1[i]);
     }
-    __syncthreads();
     for (int i = tid; i < 2 * TD * TD; i += TB_THREADS) {            // time_w2 [2TD][TD]
         const int h = i / TD, j = i % TD;
         float s = 0.f;
@@ -298,6 +317,7 @@ __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __res
         for (int q = 0; q < KF; ++q) s += dtemb[q * TD + j];
         grad[F.time_b2 + j] = s;
     }
+    __syncthreads();
     for (int i = tid; i < TD * 2 * TD; i += TB_THREADS) {            // time_w1 [TD][2TD]
         const int k = i / (2 * TD), h = i % (2 * TD);
         float s = 0.f;
@@ -584,8 +604,19 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     if (rc) return rc;
     if (side) DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
 
-    const size_t tsm = sizeof(float) * (size_t)D.KF * (2 * D.TD + 2 * 2 * D.TD);
-    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, ws.gseg, actor_params, ga, FA, D.XD, D.TD, D.H, D.KF, D.TS);
+    size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
+                                  (size_t)D.KF * (2 * D.TD + 2 * 2 * D.TD));
+    DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
+    const int stage_g = tsm + sizeof(float) * (size_t)D.KF * D.H <= 160 * 1024;
+    if (stage_g) tsm += sizeof(float) * (size_t)D.KF * D.H;
+    if (tsm > 64 * 1024) {
+        static bool attr = false;   // opt in to more than 64 KB of dynamic LDS once
+        if (!attr) {
+            DPPO_HIP(hipFuncSetAttribute((const void*)time_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            attr = true;
+        }
+    }
+    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, ws.gseg, actor_params, ga, FA, D.XD, D.TD, D.H, D.KF, D.TS, stage_g);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
