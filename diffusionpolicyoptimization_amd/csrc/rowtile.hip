@@ -291,8 +291,10 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
 
     PHASE(0);
     f32x4 acc[MT][NT];
-    static_assert(MT * NT * 4 <= 32, "relu masks are 32-bit");
-    uint32_t mask1 = 0, mask2 = 0;
+    // relu masks: one bit per accumulator element (64-bit for 64x64 wave tiles)
+    using MaskT = typename std::conditional<(MT * NT * 4 > 32), uint64_t, uint32_t>::type;
+    static_assert(MT * NT * 4 <= 64, "relu masks are at most 64-bit");
+    MaskT mask1 = 0, mask2 = 0;
     // The weight stream is one QD-deep queue per wave through every layer of the kernel:
     //   in -> l1 -> l2 -> in (again: the residual h1 is recomputed as a0 W_in, 2 more k-steps,
     //   instead of holding 8*MT*NT fp32 registers from L1 to L3) -> [train] out^T -> l2^T -> l1^T.
@@ -307,7 +309,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         for (int n = 0; n < NT; ++n)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if (acc[m][n][r] > 0.f) mask1 |= 1u << ((m * NT + n) * 4 + r);
+                if (acc[m][n][r] > 0.f) mask1 |= MaskT(1) << ((m * NT + n) * 4 + r);
                 acc[m][n][r] = fmaxf(acc[m][n][r], 0.f);
             }
     // materialise the mask now (otherwise hipcc keeps the 8*MT*NT floats alive until the backward)
@@ -326,7 +328,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         for (int n = 0; n < NT; ++n)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if (acc[m][n][r] > 0.f) mask2 |= 1u << ((m * NT + n) * 4 + r);
+                if (acc[m][n][r] > 0.f) mask2 |= MaskT(1) << ((m * NT + n) * 4 + r);
                 acc[m][n][r] = fmaxf(acc[m][n][r], 0.f);
             }
     asm volatile("" : "+v"(mask2));
@@ -733,14 +735,16 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4)))
     critic_rowtile_body<P, MT, NT, TRAIN, WAVES>(a);
 }
 
-// Row-tile shape selection: DPPO_ROWTILE = "<actor>,<critic>" with actor in {64x16, 32x8, 32x8o4}
+// Row-tile shape selection: DPPO_ROWTILE = "<actor>,<critic>" with actor in {64x16, 32x8, 32x8o4, 64x8}
 // and critic in {32x8, 32x8o4}; read once (a tuning knob for measurements, defaults below).
-struct RowTileCfg { int actor; int critic; };   // actor: 0 = 64x16, 1 = 32x8, 2 = 32x8o4; critic: 0 = 32x8, 1 = 32x8o4
+// actor: 0 = 64x16, 1 = 32x8, 2 = 32x8o4, 3 = 64x8 (64 rows on 8 waves of 64x64); critic: 0 = 32x8, 1 = 32x8o4
+struct RowTileCfg { int actor; int critic; };
 static RowTileCfg row_tile_cfg() {
     static RowTileCfg c = [] {
         RowTileCfg r{0, 1};
         if (const char* e = getenv("DPPO_ROWTILE")) {
-            if (!strncmp(e, "32x8o4", 6)) r.actor = 2;
+            if (!strncmp(e, "64x8", 4)) r.actor = 3;
+            else if (!strncmp(e, "32x8o4", 6)) r.actor = 2;
             else if (!strncmp(e, "32x8", 4)) r.actor = 1;
             else if (!strncmp(e, "64x16", 5)) r.actor = 0;
             const char* c2 = strchr(e, ',');
@@ -808,6 +812,7 @@ int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
     // out-layer partials (16 waves x 64 rows x 16*NO) only fit the aliased LDS tile for XD <= 16
     // (walker2d / halfcheetah, XD = 24, run the 32-row tile)
     if (a.H == 512 && v == 0 && a.XD <= 16) return dispatch_actor<PolicyBF16, 4, 16>(a, s);
+    if (a.H == 512 && v == 3 && a.XD <= 16) return dispatch_actor<PolicyBF16, 4, 8>(a, s);
     return v == 2 ? dispatch_actor<PolicyBF16, 2, 8, true>(a, s) : dispatch_actor<PolicyBF16, 2, 8>(a, s);
 }
 
