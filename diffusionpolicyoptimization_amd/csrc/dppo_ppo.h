@@ -13,7 +13,7 @@ struct PpoWorkspace {
     // critic
     void *csT, *cu1T, *cu2T, *ch3T, *cdvT, *cdh3T, *cdh2T, *cdh1T;
     int8_t* seg;      // [ldm] t of each row (bucket id for the one-hot bias/temb sums), -1 invalid
-    float* gseg;      // [16][H] per-t sums of dh1 (actor in-layer)
+    float* gseg;      // [64][H] per-t sums of dh1 (actor in-layer; 16 buckets in PPO, K in pretraining)
     double* stats;    // [4] adv {count, sum, sumsq}
     size_t total;
 };
@@ -34,7 +34,7 @@ inline PpoWorkspace make_ppo_workspace(const Dims& D, int precision, int rows, u
     w.csT = take(D.SD); w.cu1T = take(D.HC); w.cu2T = take(D.HC); w.ch3T = take(D.HC);
     w.cdvT = take(1); w.cdh3T = take(D.HC); w.cdh2T = take(D.HC); w.cdh1T = take(D.HC);
     w.seg = base ? (int8_t*)(base + o) : nullptr; o = dppo_align256(o + w.ldm);
-    w.gseg = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * 16 * (size_t)D.H);
+    w.gseg = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * 64 * (size_t)D.H);
     w.stats = base ? (double*)(base + o) : nullptr; o = dppo_align256(o + 8 * 4);
     w.total = o;
     return w;
@@ -46,7 +46,9 @@ __host__ __device__ inline uint32_t ws_off(const PpoWorkspace& w, const void* im
 }
 
 // per-row source of a row-tile launch
-enum { ROWS_LOGPROB = 0, ROWS_TRAIN = 1, ROWS_VALUE = 2 };
+// ROWS_PRETRAIN: the pretraining loss p_losses (diffusion.py:179-202) through the TRAIN row tile:
+// row r is sample r, t and noise come with it, KF holds K (every t is a bucket)
+enum { ROWS_LOGPROB = 0, ROWS_TRAIN = 1, ROWS_VALUE = 2, ROWS_PRETRAIN = 3 };
 
 struct LossHP {
     float gamma_denoising, clip_coef, clip_coef_base, clip_coef_rate, min_lp_std, vf_coef;
@@ -75,6 +77,11 @@ struct ActorArgs {
     LossHP hp;
     PpoWorkspace ws;
     double* metrics;
+    // pretrain (ROWS_PRETRAIN): chains = x_start [rows][XD], obs = cond [rows][SD]
+    const int* tsteps;     // [rows] t in [0, K)
+    const float* noise;    // [rows][XD]
+    const float* qsched;   // [K][2] sqrt(alphas_cumprod), sqrt(1 - alphas_cumprod)
+    float pre_scale;       // d loss / d eps = pre_scale * (eps - noise)
 };
 
 struct CriticArgs {

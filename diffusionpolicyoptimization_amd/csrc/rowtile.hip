@@ -16,6 +16,11 @@
 
 #define LOG_2PI_HALF 0.91893853320467274178f
 
+// weight-stream queue depth of the actor row tile (k-steps in flight per wave; tuning knob)
+#ifndef DPPO_ROWTILE_QD
+#define DPPO_ROWTILE_QD 3
+#endif
+
 // Phase timing for tuning builds (tools/variant_build.sh ... -DDPPO_ROWTILE_TIMING): wave 0 of
 // every workgroup adds the shader-clock cycles it spent in each phase (barrier waits included).
 #ifdef DPPO_ROWTILE_TIMING
@@ -185,6 +190,8 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     const int ktw = L.ks_out_t * P::KG;   // width of the dy tile (A operand of dh3 = dy W_out^T)
     const int XD = a.XD, SD = a.SD, TD = a.TD, KF = a.KF, IN = a.IN;
     constexpr bool train = TRAIN;
+    // pretraining (ROWS_PRETRAIN) runs the TRAIN body with its own prologue rows and epilogue loss
+    const bool pre = train && a.mode == ROWS_PRETRAIN;
     const int H = a.H;
     AT* tA = (AT*)(smem + S.tA);
     AT* tB = (AT*)(smem + S.tB);
@@ -212,14 +219,17 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     const int ntile0 = wave * NT;
     const __amdgpu_buffer_rsrc_t rs = packed_rsrc(a.packed);
     auto W = [&](int seg) { return wsrc(rs, L.off[seg]); };
-    constexpr int QD = 3;
+    constexpr int QD = DPPO_ROWTILE_QD;   // weight k-steps in flight per wave
     WQueue<QD, NT> R;
     queue_prime(R, W(SEG_W_IN), KSI, NextLayers{W(SEG_W_L1), KSH, W(SEG_W_L2), KSH}, ntile0, lane);
     if (tid < ROWS) {
         const int64_t gr = (int64_t)grow0 + tid;
         int n = -1, j = 0;
         if (gr < a.nrows) {
-            if (train) {
+            if (pre) {                         // row = sample; t = KF-1-j below, KF = K
+                n = (int)gr;
+                j = KF - 1 - a.tsteps[gr];
+            } else if (train) {
                 const uint64_t idx = minibatch_row(a.row_index, (uint64_t)(a.start + gr), a.fk);
                 if (idx < a.fk.n) {   // tf.unravel_index; sample counts are < 2^32 (host-checked)
                     n = (int)((uint32_t)idx / (uint32_t)KF);
@@ -231,11 +241,11 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
             }
         }
         rn[tid] = n; rj[tid] = j;
-        if (train) {
+        if (train && !pre) {
             radv[tid] = n >= 0 ? a.adv[n] : 0.f;
             rlpo[tid] = n >= 0 ? a.lp_old[(size_t)n * KF + j] : 0.f;
         }
-    } else if (train && tid == ROWS) {   // population mean / std of the minibatch (diffusion_ppo.py:74-75)
+    } else if (train && !pre && tid == ROWS) {   // population mean / std of the minibatch (diffusion_ppo.py:74-75)
         const double* S3 = a.adv_stats;
         const double mean = S3[1] / S3[0];
         const double var = fmax(S3[2] / S3[0] - mean * mean, 0.0);
@@ -256,7 +266,13 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     for (int i = tid; i < ROWS * XD; i += THREADS) {
         const int r = i / XD, q = i % XD, n = rn[r];
         float vp = 0.f, vn = 0.f;
-        if (n >= 0) {
+        if (n >= 0 && pre) {
+            // q_sample (diffusion.py:196-202): x_t = sqrt(ac_t) x_0 + sqrt(1 - ac_t) noise; xn keeps the noise
+            const int t = KF - 1 - rj[r];
+            const float z = a.noise[(size_t)n * XD + q];
+            vp = a.qsched[2 * t] * a.chains[(size_t)n * XD + q] + a.qsched[2 * t + 1] * z;
+            vn = z;
+        } else if (n >= 0) {
             const float* c = a.chains + ((size_t)n * (KF + 1) + rj[r]) * XD + q;
             vp = c[0]; vn = c[XD];   // chains_prev = chains[:, j], chains_next = chains[:, j+1]
         }
@@ -391,7 +407,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         const float* sc = sch + (KF - 1 - rj[r]) * DPPO_SCHED_COLS;
         return fminf(fmaxf(expf(0.5f * sc[4]), a.hp.min_lp_std), 1e6f);
     };
-    for (int idx = tid; idx < ROWS * XD; idx += THREADS) {
+    for (int idx = tid; idx < ROWS * XD && !pre; idx += THREADS) {
         const int r = idx / XD, q = idx % XD;
         const float* sc = sch + (KF - 1 - rj[r]) * DPPO_SCHED_COLS;
         const float sd = row_sd(r);
@@ -411,7 +427,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     }
     lds_sync();
     PHASE(5);
-    if (tid < 64) {
+    if (tid < 64 && !pre) {
         const int r = tid;
         float pg = 0.f, kl = 0.f, cf = 0.f, ra = 0.f, dnewlp = 0.f;
         if (r < ROWS) {
@@ -465,10 +481,21 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     // d loss / d eps through clip(lp), Normal.log_prob, mu and clip(x_recon); idx -> (q, r) with r
     // fastest so the dyT image stores coalesce
     AT* dyt = a0;   // a0 tile is dead after L1; dy tile has row stride lda0
+    float sq = 0.f;                      // pretrain: this thread's sum of (eps - noise)^2
     for (int idx = tid; idx < ROWS * ktw; idx += THREADS) {
         const int q = idx / ROWS, r = idx % ROWS;
         float d = 0.f;
-        if (q < XD && q < nh && rn[r] >= 0) {
+        if (pre) {
+            // p_losses, predict_epsilon (diffusion.py:186-194): mean((eps - noise)^2)
+            if (q < XD && rn[r] >= 0) {
+                float eps = bo[q];
+#pragma unroll
+                for (int w = 0; w < WAVES; ++w) eps += part[(w * ROWS + r) * (16 * NO) + q];
+                const float e = eps - xn[r * XD + q];
+                sq += e * e;
+                d = a.pre_scale * e;
+            }
+        } else if (q < XD && q < nh && rn[r] >= 0) {
             const int e = r * XD + q;
             const float lp = e_lp[e];
             const float sd = row_sd(r);
@@ -478,6 +505,10 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
             d = e_uc[e] != 0.f ? -sc[1] * sc[2] * dmu : 0.f;
         }
         dyt[r * lda0 + q] = P::cvt(d);
+    }
+    if (pre) {
+        sq = wave_sum(sq);
+        if (lane == 0) atomic_add_metric(a.metrics, 0, sq);
     }
     lds_sync();
     for (int i = tid; i < (ROWS / 8) * XD; i += THREADS) {   // dyT image from the dy tile
@@ -772,7 +803,7 @@ static int launch_actor_t(const ActorArgs& a, hipStream_t s) {
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S.total));
     // TRAIN mode covers every row of the 64-padded feature-major images (padding rows get
     // finite activations and zero gradients), so the dW kernel never reads unwritten memory
-    const int64_t rows = a.mode == ROWS_TRAIN ? (int64_t)a.ws.ldm : a.nrows;
+    const int64_t rows = (a.mode == ROWS_TRAIN || a.mode == ROWS_PRETRAIN) ? (int64_t)a.ws.ldm : a.nrows;
     const int64_t grid = (rows + 16 * MT - 1) / (16 * MT);
     if (grid == 0) return DPPO_OK;
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * WAVES), S.total, s, a);
@@ -782,7 +813,7 @@ static int launch_actor_t(const ActorArgs& a, hipStream_t s) {
 
 template <class P, int MT, int NT, int NO, int KSI, int WAVES, bool O4>
 static int launch_actor_m(const ActorArgs& a, hipStream_t s) {
-    return a.mode == ROWS_TRAIN ? launch_actor_t<P, MT, NT, NO, KSI, true, WAVES, O4>(a, s)
+    return (a.mode == ROWS_TRAIN || a.mode == ROWS_PRETRAIN) ? launch_actor_t<P, MT, NT, NO, KSI, true, WAVES, O4>(a, s)
                                 : launch_actor_t<P, MT, NT, NO, KSI, false, WAVES, O4>(a, s);
 }
 

@@ -480,6 +480,28 @@ static SideStream* side_stream() {
     return ss[dev].stream ? &ss[dev] : nullptr;
 }
 
+// time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg)
+static int launch_time_bwd(const Dims& D, const float* gseg, const float* actor_params, float* ga, int nb, int TS,
+                           hipStream_t s) {
+    const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
+    size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
+                                  (size_t)nb * (2 * D.TD + 2 * 2 * D.TD));
+    DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
+    const int stage_g = tsm + sizeof(float) * (size_t)nb * D.H <= 160 * 1024;
+    if (stage_g) tsm += sizeof(float) * (size_t)nb * D.H;
+    if (tsm > 64 * 1024) {
+        static bool attr = false;   // opt in to more than 64 KB of dynamic LDS once
+        if (!attr) {
+            DPPO_HIP(hipFuncSetAttribute((const void*)time_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            attr = true;
+        }
+    }
+    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD, D.TD, D.H, nb,
+                       TS, stage_g);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
 extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
                                   const void* packed_ft, const void* packed_critic, const float* actor_params,
                                   const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
@@ -604,19 +626,98 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     if (rc) return rc;
     if (side) DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
 
-    size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
-                                  (size_t)D.KF * (2 * D.TD + 2 * 2 * D.TD));
-    DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
-    const int stage_g = tsm + sizeof(float) * (size_t)D.KF * D.H <= 160 * 1024;
-    if (stage_g) tsm += sizeof(float) * (size_t)D.KF * D.H;
-    if (tsm > 64 * 1024) {
-        static bool attr = false;   // opt in to more than 64 KB of dynamic LDS once
-        if (!attr) {
-            DPPO_HIP(hipFuncSetAttribute((const void*)time_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            attr = true;
-        }
+    return launch_time_bwd(D, ws.gseg, actor_params, ga, D.KF, D.TS, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// pretraining loss: DiffusionModel.p_losses / q_sample (diffusion.py:179-202)
+// ---------------------------------------------------------------------------------------------
+// per-t bucket sums of dh1 for t in [0, nb): G[q][n] = sum over rows with seg == q of dh1T[n][row].
+// One workgroup per hidden unit n; each wave bins its rows in LDS (nb <= 64), then the waves' bins
+// are added in a fixed order (no global atomics: one writer per (q, n)).
+template <class AT>
+__global__ __launch_bounds__(256) void seg_reduce_kernel(const AT* __restrict__ dT, const int8_t* __restrict__ seg,
+                                                         size_t ldm, int nb, float* __restrict__ G, int H) {
+    __shared__ float bins[4][64];
+    const int n = blockIdx.x, tid = threadIdx.x, wave = tid >> 6;
+    for (int i = tid; i < 4 * 64; i += 256) (&bins[0][0])[i] = 0.f;
+    __syncthreads();
+    const AT* row = dT + (size_t)n * ldm;
+#pragma unroll 4
+    for (size_t r = tid; r < ldm; r += 256) {
+        const int q = seg[r];
+        if (q >= 0 && q < nb) atomicAdd(&bins[wave][q], (float)row[r]);
     }
-    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, ws.gseg, actor_params, ga, FA, D.XD, D.TD, D.H, D.KF, D.TS, stage_g);
+    __syncthreads();
+    if (tid < nb) G[(size_t)tid * H + n] = (bins[0][tid] + bins[1][tid]) + (bins[2][tid] + bins[3][tid]);
+}
+
+extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const void* packed_actor, const float* actor_params,
+                                       const float* sched, const float* qsched, const float* x_start, const float* cond,
+                                       const int32_t* t, const float* noise, int rows, int64_t global_rows,
+                                       float loss_scale, void* workspace, float* grads, double* metrics, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    DPPO_CHECK(packed_actor && actor_params && sched && qsched && x_start && cond && t && noise && workspace && grads &&
+               metrics, "dppo_pretrain_minibatch: null pointer");
+    DPPO_CHECK(rows > 0 && global_rows >= rows, "dppo_pretrain_minibatch: bad rows / global_rows");
+    DPPO_CHECK(D.TS == 1, "dppo_pretrain_minibatch: the time-embedding table must be unstrided (time_stride 1)");
+    DPPO_CHECK(D.K <= 64, "dppo_pretrain_minibatch: denoising_steps > 64 unsupported (bucket sums)");
+    hipStream_t s = (hipStream_t)stream;
+    const PpoWorkspace ws = make_ppo_workspace(D, precision, rows, (uint8_t*)workspace);
+    DPPO_CHECK(ws.total < ((size_t)1 << 31), "dppo_pretrain_minibatch: workspace for %d rows exceeds 2 GiB", rows);
+    const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
+    float* ga = grads;
+    ZeroArgs z = {};
+    z.p[0] = grads; z.n[0] = FA.count * sizeof(float);
+    z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
+    hipLaunchKernelGGL(zero_kernel, dim3(256), dim3(256), 0, s, z);
     DPPO_HIP(hipGetLastError());
-    return DPPO_OK;
+
+    ActorArgs aa = {};
+    aa.packed = (const uint8_t*)packed_actor;
+    aa.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+    aa.sched = sched; aa.obs = cond; aa.chains = x_start;
+    aa.XD = D.XD; aa.SD = D.SD; aa.TD = D.TD; aa.IN = D.IN; aa.H = D.H; aa.KF = D.K; aa.Da = D.Da;
+    aa.mode = ROWS_PRETRAIN; aa.nrows = rows; aa.ws = ws; aa.metrics = metrics;
+    aa.tsteps = t; aa.noise = noise; aa.qsched = qsched;
+    // loss = mean over global_rows * XD elements of (eps - noise)^2 (diffusion.py:192)
+    aa.pre_scale = 2.f * loss_scale / ((float)global_rows * (float)D.XD);
+    rc = launch_actor_rowtile(aa, precision, s);
+    if (rc) return rc;
+
+    DWArgs w = {};
+    auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
+        DWProb& p = w.p[w.nprob];
+        p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
+        p.ktiles = dppo_cdiv(Kx, DW_T); p.ntiles = dppo_cdiv(N, DW_T);
+        w.tile_start[w.nprob + 1] = w.tile_start[w.nprob] + p.ktiles * p.ntiles;
+        w.nprob++;
+    };
+    // the in-layer's bias and time-MLP gradients come from K bucket sums (seg_reduce + time_bwd)
+    add(ws.a0T, D.IN, ws.dh1T, D.H, ga + FA.in_w, EXTRA_NONE, nullptr);
+    add(ws.u1T, D.H, ws.dh2T, D.H, ga + FA.l1_w, EXTRA_ONES, ga + FA.l1_b);
+    add(ws.u2T, D.H, ws.dh3T, D.H, ga + FA.l2_w, EXTRA_ONES, ga + FA.l2_b);
+    add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
+    w.ldm = ws.ldm;
+    w.seg = ws.seg;
+    const int tiles = w.tile_start[w.nprob];
+    int nch = dw_device_cus() / tiles;
+    const int max_ch = (int)(ws.ldm / 64);
+    if (nch > max_ch) nch = max_ch;
+    if (nch < 1) nch = 1;
+    w.mchunk = (int)(dppo_cdiv((int)ws.ldm, nch * 64) * 64);
+    w.nchunks = dppo_cdiv((int)ws.ldm, w.mchunk);
+    rc = precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, s) : launch_dw<PolicyF32>(w, s);
+    if (rc) return rc;
+    if (precision == DPPO_BF16)
+        hipLaunchKernelGGL(seg_reduce_kernel<__bf16>, dim3(D.H), dim3(256), 0, s, (const __bf16*)ws.dh1T, ws.seg, ws.ldm,
+                           D.K, ws.gseg, D.H);
+    else
+        hipLaunchKernelGGL(seg_reduce_kernel<float>, dim3(D.H), dim3(256), 0, s, (const float*)ws.dh1T, ws.seg, ws.ldm,
+                           D.K, ws.gseg, D.H);
+    DPPO_HIP(hipGetLastError());
+    return launch_time_bwd(D, ws.gseg, actor_params, ga, D.K, 1, s);
 }

@@ -468,6 +468,38 @@ def ppo_minibatch(d: ModelDims, precision, hp, packed_ft, packed_critic, actor_p
               ptr(row_index), ptr(adv_stats), ptr(workspace), ptr(grads), ptr(metrics), stream_handle(obs.device))
 
 
+def q_sched_table(schedule):
+    """[K][2] fp32 {sqrt(alphas_cumprod), sqrt(1 - alphas_cumprod)}: the q_sample buffers of
+    diffusion.py:62-65 (computed in fp32 like the TF buffers)."""
+    ac = np.asarray(schedule["alphas_cumprod"], np.float32)
+    return np.stack([np.sqrt(ac), np.sqrt(np.float32(1.0) - ac)], axis=1).astype(np.float32)
+
+
+def pretrain_minibatch(d: ModelDims, precision, packed_actor, actor_params, sched, qsched, x_start, cond, t, noise,
+                       workspace, grads, metrics, global_rows=None, loss_scale=1.0):
+    """p_losses (diffusion.py:186-194) and its actor gradient for one batch; see include/dppo.h.
+    Returns the loss as a device scalar (metrics[0] / (global_rows * xd) * loss_scale)."""
+    n = x_start.shape[0]
+    g = n if global_rows is None else int(global_rows)
+    _check(x_start, (n, d.xd), torch.float32, "x_start")
+    _check(cond, (n, d.sd), torch.float32, "cond")
+    _check(t, (n,), torch.int32, "t")
+    _check(noise, (n, d.xd), torch.float32, "noise")
+    _check(qsched, (d.denoising_steps, 2), torch.float32, "qsched")
+    na = spec_count(actor_param_spec(d))
+    _check(actor_params, (na,), torch.float32, "actor_params")
+    if grads.numel() < na:
+        raise ValueError("grads: needs at least the actor parameter count")
+    _check(metrics, (16,), torch.float64, "metrics")
+    need = int(_lib.query("dppo_ppo_workspace_bytes", ctypes.byref(d.c()), _prec(precision), int(n)))
+    if workspace.numel() < need:
+        raise ValueError(f"workspace too small: {workspace.numel()} < {need}")
+    _lib.call("dppo_pretrain_minibatch", ctypes.byref(d.c()), _prec(precision), ptr(packed_actor), ptr(actor_params),
+              ptr(sched), ptr(qsched), ptr(x_start), ptr(cond), ptr(t), ptr(noise), int(n), int(g), float(loss_scale),
+              ptr(workspace), ptr(grads), ptr(metrics), stream_handle(x_start.device))
+    return metrics[0] * (float(loss_scale) / (g * d.xd))
+
+
 def adamw(params, grads, m, v, step, lr, weight_decay=0.004, beta1=0.9, beta2=0.999, eps=1e-7, mode="keras"):
     n = params.numel()
     for t, nm in ((grads, "grads"), (m, "m"), (v, "v")):

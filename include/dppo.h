@@ -218,6 +218,23 @@ DPPO_API int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_pp
                        int epoch, int64_t start, int rows, const int64_t* row_index, const double* adv_stats,
                        void* workspace, float* grads, double* metrics, void* stream);
 
+/* ---- §8(f) row 3: the pretraining loss DiffusionModel.c_loss -> p_losses / q_sample
+ * (model/diffusion/diffusion.py:179-202; predict_epsilon = True), loss and actor gradients.
+ * Replaces the TF tape over `self.model.c_loss(**batch)` in agent/pretrain/train_diffusion_agent.py.
+ * Row r is sample r: x_start [rows][horizon*action_dim], cond [rows][cond_steps*obs_dim],
+ * t [rows] int32 in [0, denoising_steps), noise [rows][horizon*action_dim] (the host draws t and
+ * noise, tf.random.uniform / tf.random.normal at diffusion.py:182,187).
+ * sched: the DDPM schedule table (denoising_steps rows); qsched [denoising_steps][2] fp32 =
+ * {sqrt(alphas_cumprod), sqrt(1 - alphas_cumprod)} (the TF buffers, diffusion.py:62-65).
+ * loss = loss_scale * sum((eps - noise)^2) / (global_rows * horizon*action_dim): metrics[0] (fp64,
+ * device) receives the local sum of squares; grads [actor_count] fp32 are OVERWRITTEN with
+ * d loss / d params. Workspace: dppo_ppo_workspace_bytes(d, precision, rows). Requires
+ * time_stride == 1 and denoising_steps <= 64. ---- */
+DPPO_API int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const void* packed_actor, const float* actor_params,
+                            const float* sched, const float* qsched, const float* x_start, const float* cond,
+                            const int32_t* t, const float* noise, int rows, int64_t global_rows, float loss_scale,
+                            void* workspace, float* grads, double* metrics, void* stream);
+
 /* Feistel permutation used above, exposed for tests: out[i] = perm(first + i), i < count. */
 DPPO_API int dppo_feistel_permute(int64_t first, int64_t count, int64_t n, uint64_t seed, int epoch, int64_t* out,
                          void* stream);

@@ -409,6 +409,34 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
 
 
 # ----------------------------------------------------------------------------------------------
+# §8(f) row 3: pretraining loss (model/diffusion/diffusion.py:179-202, predict_epsilon = True)
+# ----------------------------------------------------------------------------------------------
+def q_sample(sched, x_start, t, noise):
+    """diffusion.py:196-202: sqrt(ac_t) x_0 + sqrt(1 - ac_t) noise, the buffers in fp32 (:62-65)."""
+    ac = np.asarray(sched["alphas_cumprod"], np.float32)
+    sa = np.sqrt(ac).astype(np.float32)[t]
+    s1 = np.sqrt(np.float32(1.0) - ac).astype(np.float32)[t]
+    shape = (-1,) + (1,) * (np.ndim(x_start) - 1)
+    return sa.reshape(shape).astype(np.float64) * x_start + s1.reshape(shape).astype(np.float64) * noise
+
+
+def p_losses(p, sched, x_start, state, t, noise, with_grad=True, rnd=None, denom=None):
+    """diffusion.py:186-194: loss = mean((network(q_sample(x_0, t, noise), t, cond) - noise)^2) and
+    its parameter gradient. x_start, noise [B,Ta,Da]; state [B,To,Do]; t [B] int (the draws of
+    :182 and :187 are inputs here). denom overrides the element count of the mean (data-parallel
+    shards: summing per-shard gradients with the global count gives the full-batch one)."""
+    xn = q_sample(sched, x_start, np.asarray(t), noise)
+    eps, cache = diffusion_mlp_forward(p, xn, np.asarray(t), state, rnd=rnd)
+    e = eps - noise
+    n = e.size if denom is None else denom
+    loss = float((e ** 2).sum() / n)
+    if not with_grad:
+        return loss, None
+    deps = 2.0 * e / n
+    return loss, diffusion_mlp_backward(p, cache, deps, x_start.shape[1] * x_start.shape[2])
+
+
+# ----------------------------------------------------------------------------------------------
 # a14: Keras 3 AdamW step (train_ppo_agent.py:45-49; semantics in SURVEY.md §8 quirk 2)
 # ----------------------------------------------------------------------------------------------
 def keras_adamw_step(param, grad, m, v, step, lr=1e-4, wd=0.004, beta1=0.9, beta2=0.999, eps=1e-7):

@@ -399,3 +399,39 @@ def test_ppo_minibatch_grads(cuda, precision, case, rtol):
         errs["critic." + name] = np.abs(gc[name] - ref).max() / (np.abs(ref).max() + 1e-12)
     bad = {k: float(v) for k, v in errs.items() if not v < rtol}
     assert not bad, (bad, {k: float(v) for k, v in errs.items()})
+
+
+@pytest.mark.parametrize("precision,rtol", [("fp32", 2e-3), ("bf16", 1e-2)])
+@pytest.mark.parametrize("dims", [HOPPER, WALKER], ids=["hopper", "walker"])
+def test_pretrain_loss_grads(cuda, precision, rtol, dims):
+    """§8(f) row 3: p_losses / q_sample (diffusion.py:179-202) through the TRAIN row tile
+    (dppo_pretrain_minibatch): loss and every actor gradient vs the oracle, t over all K = 20 steps
+    (bucket sums of the time-MLP gradient over 20 t's), ragged rows. bf16 compares against the
+    oracle rounding operands at the kernels' rounding points."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(dims, cuda)
+    rng = np.random.default_rng(21)
+    rows = 150
+    K = d.denoising_steps
+    x0 = rng.uniform(-1, 1, (rows, d.xd)).astype(np.float32)
+    cond = rng.uniform(-1, 1, (rows, d.sd)).astype(np.float32)
+    t = rng.integers(0, K, rows).astype(np.int32)
+    noise = rng.standard_normal((rows, d.xd)).astype(np.float32)
+    loss_ref, g_ref = O.p_losses(to_f64(ft), sched, x0.reshape(rows, d.horizon_steps, d.action_dim).astype(np.float64),
+                                 cond.reshape(rows, d.cond_steps, d.obs_dim).astype(np.float64), t,
+                                 noise.reshape(rows, d.horizon_steps, d.action_dim).astype(np.float64),
+                                 rnd=_rnd(precision))
+    T = lambda x: torch.tensor(x, device=cuda)
+    na = ops.spec_count(ops.actor_param_spec(d))
+    grads = torch.zeros(na, dtype=torch.float32, device=cuda)
+    metrics = torch.zeros(16, dtype=torch.float64, device=cuda)
+    ws = ops.ppo_workspace(d, precision, rows, cuda)
+    loss = ops.pretrain_minibatch(d, precision, ops.pack_actor(d, pf, precision), pf, tab, T(ops.q_sched_table(sched)),
+                                  T(x0), T(cond), T(t), T(noise), ws, grads, metrics)
+    torch.cuda.synchronize()
+    assert abs(float(loss) - loss_ref) < rtol * loss_ref
+    ga = ops.unflatten_params(ops.actor_param_spec(d), grads.cpu().numpy())
+    errs = {k: float(np.abs(ga[k] - ref).max() / (np.abs(ref).max() + 1e-12)) for k, ref in g_ref.items()}
+    bad = {k: v for k, v in errs.items() if not v < rtol}
+    assert not bad, (bad, errs)

@@ -202,3 +202,40 @@ def test_ddim_host_buffers_match_oracle():
     from diffusionpolicyoptimization_amd.model.diffusion.sampling import ddpm_buffers
     tab = ops.sched_table(ddpm_buffers(20))
     assert tab[0, 6] == 1 and (tab[1:, 6] == 0).all() and np.allclose(tab[:, 5], 1e-3)
+
+
+def test_oracle_pretrain_loss_gradient_matches_autograd():
+    """p_losses (diffusion.py:186-194) in the oracle vs an independent torch float64 autograd of the
+    same loss: q_sample with the fp32 buffers, DiffusionMLP, mean((eps - noise)^2)."""
+    import torch
+    _, ft, _ = make_models(0, HOPPER)
+    sched = O.ddpm_schedule(20)
+    rng = np.random.default_rng(3)
+    b = 48
+    x0 = rng.uniform(-1, 1, (b, 4, 3))
+    obs = rng.uniform(-1, 1, (b, 1, 11))
+    t = rng.integers(0, 20, b)
+    noise = rng.standard_normal((b, 4, 3))
+    loss, g = O.p_losses(to_f64(ft), sched, x0, obs, t, noise)
+    T = lambda x: torch.tensor(np.asarray(x, np.float64))
+    P = {k: T(v).requires_grad_(True) for k, v in ft.items()}
+    mish = lambda x: x * torch.tanh(torch.nn.functional.softplus(x))
+    half = 8
+    freqs = torch.exp(torch.arange(half, dtype=torch.float64) * -(np.log(10000) / (half - 1)))
+    e = T(t)[:, None] * freqs[None]
+    e = torch.cat([torch.sin(e), torch.cos(e)], -1)
+    temb = mish(e @ P["time_w1"] + P["time_b1"]) @ P["time_w2"] + P["time_b2"]
+    ac = sched["alphas_cumprod"].astype(np.float32)
+    sa = T(np.sqrt(ac).astype(np.float32)[t])[:, None]
+    s1 = T(np.sqrt(np.float32(1) - ac).astype(np.float32)[t])[:, None]
+    xn = sa * T(x0).reshape(b, -1) + s1 * T(noise).reshape(b, -1)
+    inp = torch.cat([xn, temb, T(obs).reshape(b, -1)], -1)
+    h1 = inp @ P["in_w"] + P["in_b"]
+    h2 = torch.relu(h1) @ P["l1_w"] + P["l1_b"]
+    h3 = torch.relu(h2) @ P["l2_w"] + P["l2_b"] + h1
+    eps = h3 @ P["out_w"] + P["out_b"]
+    L = ((eps - T(noise).reshape(b, -1)) ** 2).mean()
+    L.backward()
+    assert abs(loss - float(L)) < 1e-12
+    for k, v in P.items():
+        np.testing.assert_allclose(g[k], v.grad.numpy(), rtol=1e-8, atol=1e-12, err_msg=k)
