@@ -1,6 +1,8 @@
 """DiffusionModel base (reference model/diffusion/diffusion.py:19-110): DDPM schedule buffers and
-the shared configuration of the diffusion policy."""
+the shared configuration of the diffusion policy; standalone (the pretrain cfgs' `model`), it also
+owns its network's parameters and the pretraining loss c_loss / p_losses / q_sample (:179-202)."""
 import logging
+import os
 from collections import namedtuple
 
 import numpy as np
@@ -65,3 +67,80 @@ class DiffusionModel:
     def sched_for(self, deterministic):
         """The schedule table of a sampling call (DDIM eval sampling runs eta = 0)."""
         return self.sched_eval if deterministic else self.sched
+
+    # ------------------------------------------------------------------ pretraining (diffusion.py:179-202)
+    def _pretrain_init(self):
+        """Parameters of the standalone model's network (the pretrain cfgs: DiffusionMLP), packed for
+        the row-tile kernels, on first use."""
+        if getattr(self, "pre_dims", None) is not None:
+            return
+        net = self.network
+        self.pre_dims = ops.ModelDims(obs_dim=self.obs_dim, action_dim=self.action_dim,
+                                      horizon_steps=self.horizon_steps, cond_steps=net.cond_dim // self.obs_dim,
+                                      time_dim=net.time_dim, actor_hidden=net.hidden,
+                                      denoising_steps=self.denoising_steps, ft_denoising_steps=1, time_stride=1)
+        self.pre_spec = ops.actor_param_spec(self.pre_dims)
+        path = self.network_path
+        if path is not None and str(path).endswith(".npz") and os.path.exists(str(path)):
+            with np.load(str(path), allow_pickle=False) as f:
+                pref = "network." if any(k.startswith("network.") for k in f.files) else ""
+                p = {n: np.asarray(f[pref + n], np.float32).reshape(s) for n, s in self.pre_spec}
+        else:
+            if path is not None:
+                log.warning("network_path %s not loaded (.npz checkpoints only): seeded glorot_uniform init", path)
+            p = net.init_params(np.random.default_rng(self.seed))
+        dev = self.device
+        self.params = torch.tensor(ops.flatten_params(self.pre_spec, p), device=dev)
+        self.pre_grads = torch.zeros_like(self.params)
+        self.packed = ops.pack_actor(self.pre_dims, self.params, self.precision)
+        # q_sample buffers and the DDPM table over all K training steps (DDIM only changes sampling)
+        ddpm = ddpm_buffers(self.denoising_steps)
+        self.q_sched = torch.tensor(ops.q_sched_table(ddpm), device=dev)
+        self.pre_sched = torch.tensor(ops.sched_table(ddpm), device=dev)
+        self.pre_metrics = torch.zeros(16, dtype=torch.float64, device=dev)
+        self._pre_gen = torch.Generator(device=dev).manual_seed(self.seed)
+        self._pre_ws, self._pre_ws_rows = None, 0
+
+    def repack_network(self):
+        """Re-derive the packed image after an optimiser step on self.params."""
+        ops.pack_actor(self.pre_dims, self.params, self.precision, out=self.packed)
+
+    def q_sample(self, x_start, t, noise):
+        """diffusion.py:196-202 (device tensors, fp32 buffers)."""
+        self._pretrain_init()
+        q = self.q_sched[t.long()]
+        shape = (-1,) + (1,) * (x_start.dim() - 1)
+        return q[:, 0].reshape(shape) * x_start + q[:, 1].reshape(shape) * noise
+
+    def p_losses(self, x_start, cond, t, noise=None, global_rows=None, loss_scale=1.0):
+        """diffusion.py:186-194 (predict_epsilon): loss = mean((network(q_sample(x_0, t, noise), t, cond)
+        - noise)^2) on the device; d loss / d params lands in self.pre_grads (dppo_pretrain_minibatch).
+        x_start [B, Ta, Da] or [B, Ta*Da]; cond [B, To, Do] or a dict with "state"; t [B] int."""
+        self._pretrain_init()
+        d = self.pre_dims
+        if isinstance(cond, dict):
+            cond = cond["state"]
+        B = x_start.shape[0]
+        x0 = x_start.reshape(B, d.xd).to(self.device, torch.float32).contiguous()
+        c = cond.reshape(B, d.sd).to(self.device, torch.float32).contiguous()
+        t = t.to(self.device, torch.int32).contiguous()
+        if noise is None:
+            noise = torch.randn(B, d.xd, device=self.device, generator=self._pre_gen)
+        noise = noise.reshape(B, d.xd).to(self.device, torch.float32).contiguous()
+        if self._pre_ws is None or self._pre_ws_rows < B:
+            self._pre_ws, self._pre_ws_rows = ops.ppo_workspace(d, self.precision, B, self.device), B
+        return ops.pretrain_minibatch(d, self.precision, self.packed, self.params, self.pre_sched, self.q_sched, x0, c,
+                                      t, noise, self._pre_ws, self.pre_grads, self.pre_metrics,
+                                      global_rows=global_rows, loss_scale=loss_scale)
+
+    def c_loss(self, actions, conditions, **kwargs):
+        """diffusion.py:178-184: t ~ U{0, .., K-1} per sample (:182), then p_losses."""
+        self._pretrain_init()
+        B = actions.shape[0]
+        t = torch.randint(0, self.denoising_steps, (B,), device=self.device, generator=self._pre_gen,
+                          dtype=torch.int32)
+        return self.p_losses(actions, conditions, t, **kwargs)
+
+    def save_network(self, path):
+        np.savez(path, **{"network." + n: v for n, v in
+                          ops.unflatten_params(self.pre_spec, self.params.detach().cpu().numpy()).items()})

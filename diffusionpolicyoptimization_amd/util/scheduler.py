@@ -72,3 +72,27 @@ class CosineAnnealingWarmupRestarts:
             return self.min_lr + (max_lr - self.min_lr) * s / self.warmup_steps
         prog = (s - self.warmup_steps) / (cyc - self.warmup_steps)
         return self.min_lr + (max_lr - self.min_lr) * (1 + math.cos(math.pi * prog)) / 2
+
+
+class CosineDecayRestarts:
+    """tf.keras.optimizers.schedules.CosineDecayRestarts as the pretrain agent builds it
+    (agent/pretrain/train_agent.py:117-123): lr(step) = initial * ((1 - alpha) * m_mul^i *
+    (1 + cos(pi * frac)) / 2 + alpha), with the restart index i and in-cycle fraction frac of
+    step / first_decay_steps under t_mul."""
+
+    def __init__(self, initial_learning_rate, first_decay_steps, t_mul=2.0, m_mul=1.0, alpha=0.0):
+        self.initial_learning_rate = float(initial_learning_rate)
+        self.first_decay_steps = float(first_decay_steps)
+        self.t_mul, self.m_mul, self.alpha = float(t_mul), float(m_mul), float(alpha)
+
+    def __call__(self, step):
+        frac = float(step) / self.first_decay_steps
+        if self.t_mul == 1.0:
+            i = math.floor(frac)
+            frac -= i
+        else:
+            i = math.floor(math.log(1.0 - frac * (1.0 - self.t_mul)) / math.log(self.t_mul))
+            sum_r = (1.0 - self.t_mul ** i) / (1.0 - self.t_mul)
+            frac = (frac - sum_r) / self.t_mul ** i
+        cos_decay = 0.5 * self.m_mul ** i * (1.0 + math.cos(math.pi * frac))
+        return self.initial_learning_rate * ((1.0 - self.alpha) * cos_decay + self.alpha)

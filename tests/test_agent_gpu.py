@@ -125,3 +125,33 @@ def test_data_parallel_agent_two_ranks_share_one_gpu(tmp_path):
                          env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "replicas_identical=True" in out.stdout
+
+
+def test_pretrain_agent_trains(cuda, tmp_path):
+    """§8(f) row 3 end to end: TrainDiffusionAgent (agent/pretrain/train_diffusion_agent.py) on a
+    synthetic stitched dataset: the diffusion loss falls over epochs, EMA and checkpoints are
+    written, and DiffusionModel.p_losses on the loaded checkpoint reproduces the loss of the model."""
+    import torch
+
+    from diffusionpolicyoptimization_amd.agent.dataset.sequence import synthetic_dataset
+    from diffusionpolicyoptimization_amd.util.config import get_class, load_config, instantiate
+    data = synthetic_dataset(str(tmp_path / "train.npz"), n_episodes=6, episode_len=160, seed=1)
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/pretrain/hopper-medium-v2"), "pre_diffusion_mlp",
+                      [f"train_dataset_path={data}", f"logdir={tmp_path}/log", "train.n_epochs=4",
+                       "train.batch_size=256", "train.epoch_start_ema=2", "train.update_ema_freq=1",
+                       "train.save_model_freq=2", "train.learning_rate=1e-3"])
+    agent = get_class(cfg._target_)(cfg)
+    b = next(agent.dataset_train.batches(512))
+    t = torch.randint(0, 20, (512,), device=cuda, dtype=torch.int32)
+    z = torch.randn(512, 12, device=cuda)
+    first = float(agent.model.p_losses(b["actions"], b["conditions"], t, z))
+    last_epoch = agent.run()
+    last = float(agent.model.p_losses(b["actions"], b["conditions"], t, z))
+    assert np.isfinite(last_epoch) and np.isfinite(first) and last < 0.8 * first, (first, last)
+    ck = os.path.join(agent.checkpoint_dir, "state_4.npz")
+    assert os.path.exists(ck) and os.path.exists(ck.replace("state_", "ema_state_"))
+    assert not torch.equal(agent.ema_params, agent.model.params)
+    m2 = instantiate(cfg.model, network_path=ck)
+    m2._pretrain_init()
+    torch.testing.assert_close(m2.params, agent.model.params)
+    assert float(m2.p_losses(b["actions"], b["conditions"], t, z)) == last
