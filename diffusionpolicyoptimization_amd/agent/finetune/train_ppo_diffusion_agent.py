@@ -209,8 +209,29 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         rows_local_full = self.batch_size // self.world_size
         clipfracs, info = [], {}
         stream = torch.cuda.current_stream(self.device)
+        # The target_kl check (:366-370) reads each minibatch's approx_kl on the host. It runs one
+        # minibatch behind: minibatch i's gradients are enqueued before the host waits for i-1's
+        # metrics (an event right after i-1's kernels, the metrics copied to pinned memory), so the
+        # GPU never idles on that read. Only the AdamW step of i waits for the verdict: a stop
+        # leaves i's gradients unapplied, exactly as the reference never computes them.
+        if not hasattr(self, "_met_pin"):
+            self._met_pin = [torch.zeros(5, dtype=torch.float64).pin_memory() for _ in range(2)]
+        pending = None
+
+        def finish(p):
+            slot, ev, grows = p
+            ev.synchronize()
+            met = self._met_pin[slot].numpy() / grows
+            self.timing["n_updates"] += 1
+            inf = dict(pg_loss=float(met[0]), v_loss=float(met[1]), approx_kl=float(met[2]),
+                       clipfrac=float(met[3]), ratio=float(met[4]), bc_loss=0.0, eta=1.0,
+                       entropy_loss=-1.0, loss=float(met[0] + self.vf_coef * met[1]))
+            clipfracs.append(inf["clipfrac"])
+            return inf, self.target_kl is not None and inf["approx_kl"] > self.target_kl
+
+        k = 0
+        stop = False
         for update_epoch in range(self.update_epochs):
-            flag_break = False
             for batch in range(num_batch):
                 start = batch * rows_local_full
                 rows = min(rows_local_full, total_local - start)
@@ -232,6 +253,14 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 if self.world_size > 1:
                     self._allreduce(m.grads)
                     self._allreduce(m.metrics)
+                slot = k % 2
+                self._met_pin[slot].copy_(m.metrics[:5], non_blocking=True)
+                ev_m = torch.cuda.Event()
+                ev_m.record(stream)
+                if pending is not None:
+                    info, stop = finish(pending)
+                    if stop:                                                   # :366-370
+                        break
                 if self.itr >= self.n_critic_warmup_itr:
                     if self.max_grad_norm is not None:
                         self._clip_by_norm_per_tensor()
@@ -241,17 +270,12 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     ev1 = torch.cuda.Event(enable_timing=True)
                     ev1.record(stream)
                     self.update_events.append((ev0, ev1))
-                met = (m.metrics[:5] / global_rows).cpu().numpy()                       # host sync (KL stop)
-                self.timing["n_updates"] += 1
-                info = dict(pg_loss=float(met[0]), v_loss=float(met[1]), approx_kl=float(met[2]),
-                            clipfrac=float(met[3]), ratio=float(met[4]), bc_loss=0.0, eta=1.0,
-                            entropy_loss=-1.0, loss=float(met[0] + self.vf_coef * met[1]))
-                clipfracs.append(info["clipfrac"])
-                if self.target_kl is not None and info["approx_kl"] > self.target_kl:       # :366-370
-                    flag_break = True
-                    break
-            if flag_break:
+                pending = (slot, ev_m, global_rows)
+                k += 1
+            if stop:
                 break
+        if pending is not None and not stop:
+            info, _ = finish(pending)
         # explained variance (:373-377)
         info["explained_var"] = explained_variance(self.values, ret_flat)
         info["clipfrac"] = float(np.mean(clipfracs)) if clipfracs else 0.0

@@ -22,9 +22,27 @@ def test_agent_iterations(cuda, precision, tmp_path):
     for k in ("pg_loss", "v_loss", "approx_kl", "explained_var"):
         assert math.isfinite(tr[k]), (k, tr[k])
     assert agent.timing["n_updates"] == 5 * ((20 * 4 * 10) // 200)
+    assert agent.actor_optimizer.iterations == agent.timing["n_updates"]
     p = agent.model.train_params.cpu().numpy()
     assert np.isfinite(p).all()
     assert os.path.exists(os.path.join(tmp_path, "checkpoint", "state_0.npz"))
+
+
+def test_target_kl_stops_without_applying_the_next_minibatch(cuda, tmp_path):
+    """The target_kl early stop (agent :366-370) with the check one minibatch behind: at
+    target_kl = 0 the first minibatch whose approx_kl > 0 ends the update (it WAS applied); the
+    gradients already computed for the next minibatch are dropped. So every counted minibatch
+    had exactly one AdamW step, and the update stopped early."""
+    from diffusionpolicyoptimization_amd.util.config import get_class, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
+                      ["model.precision=fp32", "train.n_steps=20", "train.batch_size=200", "train.n_train_itr=2",
+                       "train.val_freq=100", "train.target_kl=0.0", f"logdir={tmp_path}"])
+    a = get_class(cfg._target_)(cfg)
+    a.run()
+    n = a.timing["n_updates"]
+    assert 1 <= n < 5 * ((20 * 4 * 10) // 200), n
+    assert a.actor_optimizer.iterations == n
+    assert np.isfinite(a.model.train_params.cpu().numpy()).all()
 
 
 def test_bound_rollout_step_matches_model_call(cuda):
