@@ -70,6 +70,7 @@ _SIGNATURES = {
     "dppo_gae": (_I, [_P, _P, _P, _P, _I, _I, _D, _D, _D, _P, _P, _P]),
     "dppo_ppo_workspace_bytes": (_SZ, [_DIMS, _I, _I]),
     "dppo_ppo_adv_stats": (_I, [_P, _I64, _I, _U64, _I, _I64, _I, _P, _P, _P]),
+    "dppo_ppo_adv_stats_all": (_I, [_P, _I64, _I, _U64, _I, _I, _I64, _I, _P, _P]),
     "dppo_ppo_minibatch": (_I, [_DIMS, _I, ctypes.POINTER(DppoPpoHparams), _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                _I64, _U64, _I, _I64, _I, _P, _P, _P, _P, _P, _P]),
     "dppo_pretrain_minibatch": (_I, [_DIMS, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I64, _F, _P, _P, _P, _P]),

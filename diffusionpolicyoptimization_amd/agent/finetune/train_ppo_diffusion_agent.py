@@ -229,6 +229,15 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             clipfracs.append(inf["clipfrac"])
             return inf, self.target_kl is not None and inf["approx_kl"] > self.target_kl
 
+        # every minibatch's advantage moments (norm_adv, diffusion_ppo.py:74-75) in one launch, and
+        # on several GPUs one all-reduce of the whole table instead of one per minibatch
+        n_mb = self.update_epochs * num_batch
+        if getattr(self, "_adv_all", None) is None or self._adv_all.shape[0] != n_mb:
+            self._adv_all = torch.zeros(n_mb, 3, dtype=torch.float64, device=self.device)
+        ops.ppo_adv_stats_all(adv_flat, total_local, kf, self.perm_seed, 1000 * self.itr, self.update_epochs,
+                              rows_local_full, num_batch, self._adv_all)
+        if self.world_size > 1:
+            self._allreduce(self._adv_all)
         k = 0
         stop = False
         for update_epoch in range(self.update_epochs):
@@ -238,12 +247,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 if rows <= 0:
                     break
                 global_rows = rows * self.world_size
-                stats = None
-                if self.world_size > 1:
-                    ops.ppo_adv_stats(adv_flat, total_local, kf, self.perm_seed, update_epoch + 1000 * self.itr,
-                                      start, rows, self.adv_stats)
-                    self._allreduce(self.adv_stats)
-                    stats = self.adv_stats
+                stats = self._adv_all[update_epoch * num_batch + batch]
                 if self.update_events is not None:
                     ev0 = torch.cuda.Event(enable_timing=True)
                     ev0.record(stream)

@@ -71,21 +71,28 @@ static inline uint8_t* P_out(void* p) { return (uint8_t*)p; }
 
 __global__ __launch_bounds__(128) void temb_table_kernel(const float* __restrict__ params, FlatOffsets F, int TD,
                                                          int stride, float* __restrict__ temb) {
+    // the sinusoid once per k (not once per (k, hidden unit)), weight loads unrolled so they issue
+    // together; the sums keep the oracle's order (k ascending, then h ascending)
+    __shared__ float te[64];
     __shared__ float ta1[128];
     const int row = blockIdx.x, t = row * stride, tid = threadIdx.x;   // row r holds t_emb(r * stride)
     const int half = TD / 2;
     const float lnf = logf(10000.f) / (float)(half - 1);
+    if (tid < TD) {
+        const float f = expf(-(float)(tid % half) * lnf) * (float)t;
+        te[tid] = tid < half ? sinf(f) : cosf(f);
+    }
+    __syncthreads();
     if (tid < 2 * TD) {
         float acc = params[F.time_b1 + tid];
-        for (int k = 0; k < TD; ++k) {
-            const float f = expf(-(float)(k % half) * lnf) * (float)t;
-            acc += (k < half ? sinf(f) : cosf(f)) * params[F.time_w1 + k * 2 * TD + tid];
-        }
+#pragma unroll 16
+        for (int k = 0; k < TD; ++k) acc += te[k] * params[F.time_w1 + k * 2 * TD + tid];
         ta1[tid] = mishf(acc);
     }
     __syncthreads();
     if (tid < TD) {
         float acc = params[F.time_b2 + tid];
+#pragma unroll 16
         for (int k = 0; k < 2 * TD; ++k) acc += ta1[k] * params[F.time_w2 + k * TD + tid];
         temb[(size_t)row * TD + tid] = acc;
     }

@@ -280,6 +280,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
     XPHASE(7);                                              // timing builds: phase 7 = prologue before the wait
     if (a.cond_tagged) {
         sampler_load_state_tagged<ST>(a, row0, st, c == 0, tid);
+        XPHASE(8);                                          // phase 8 = the wait for the tagged observation
         for (int i = tid; i < 16 * SD; i += ST) {
             const int r = i / SD, cc = i % SD, row = row0 + r;
             if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, st[i]);

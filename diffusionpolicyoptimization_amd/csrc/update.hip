@@ -356,6 +356,40 @@ __global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict_
     }
 }
 
+// the advantage moments of every minibatch of an update phase in one launch: blockIdx.y = minibatch
+// m = epoch * nbatch + batch; rows [batch * rows_full, min(+rows_full, total)) of epoch `epoch`'s
+// permutation (the per-minibatch adv_stats_kernel, batched)
+#define ADV_MAXE 64
+struct AdvStatsAll {
+    FeistelKey fk[ADV_MAXE];
+    int nbatch, KF;
+    int64_t rows_full, total;
+};
+__global__ __launch_bounds__(256) void adv_stats_all_kernel(const float* __restrict__ adv, AdvStatsAll a,
+                                                            double* __restrict__ stats) {
+    __shared__ double sh[3][4];
+    const int m = blockIdx.y, e = m / a.nbatch, b = m % a.nbatch;
+    const int64_t start = (int64_t)b * a.rows_full;
+    const int64_t end = start + a.rows_full < a.total ? start + a.rows_full : a.total;
+    const FeistelKey fk = a.fk[e];
+    double c = 0.0, s = 0.0, s2 = 0.0;
+    for (int64_t i = start + (int64_t)blockIdx.x * 256 + threadIdx.x; i < end; i += (int64_t)gridDim.x * 256) {
+        const uint64_t idx = minibatch_row(nullptr, (uint64_t)i, fk);
+        if (idx >= fk.n) continue;
+        const double v = adv[idx / a.KF];
+        c += 1.0; s += v; s2 += v * v;
+    }
+    c = wave_sumd(c); s = wave_sumd(s); s2 = wave_sumd(s2);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[0][w] = c; sh[1][w] = s; sh[2][w] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(stats + 3 * m + 0, sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3]);
+        atomicAdd(stats + 3 * m + 1, sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3]);
+        atomicAdd(stats + 3 * m + 2, sh[2][0] + sh[2][1] + sh[2][2] + sh[2][3]);
+    }
+}
+
 // zero up to 4 byte ranges (4-B aligned, sizes multiple of 4) in one launch
 struct ZeroArgs { void* p[4]; size_t n[4]; };
 __global__ __launch_bounds__(256) void zero_kernel(ZeroArgs z) {
@@ -440,6 +474,25 @@ extern "C" int dppo_ppo_adv_stats(const float* advantages, int64_t total, int K_
     const int blocks = dppo_cdiv(rows, 256) < 512 ? dppo_cdiv(rows, 256) : 512;
     hipLaunchKernelGGL(adv_stats_kernel, dim3(blocks), dim3(256), 0, s, advantages, fk, K_ft, start, rows, row_index,
                        adv_stats);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+extern "C" int dppo_ppo_adv_stats_all(const float* advantages, int64_t total, int K_ft, uint64_t perm_seed, int epoch0,
+                                      int n_epochs, int64_t rows_full, int n_batch, double* adv_stats, void* stream) {
+    DPPO_CHECK(advantages && adv_stats && total > 0 && K_ft > 0 && rows_full > 0 && n_batch > 0 && n_epochs > 0,
+               "dppo_ppo_adv_stats_all: bad args");
+    DPPO_CHECK(n_epochs <= ADV_MAXE, "dppo_ppo_adv_stats_all: at most %d epochs", ADV_MAXE);
+    DPPO_CHECK((uint64_t)total < ((uint64_t)1 << 32), "dppo_ppo_adv_stats_all: total exceeds 2^32");
+    hipStream_t s = (hipStream_t)stream;
+    const int nm = n_epochs * n_batch;
+    DPPO_HIP(hipMemsetAsync(adv_stats, 0, (size_t)3 * nm * sizeof(double), s));
+    AdvStatsAll a = {};
+    for (int e = 0; e < n_epochs; ++e) a.fk[e] = feistel_key((uint64_t)total, perm_seed, epoch0 + e);
+    a.nbatch = n_batch; a.KF = K_ft; a.rows_full = rows_full; a.total = total;
+    const int64_t bx = dppo_cdiv((int)(rows_full < total ? rows_full : total), 256);
+    const int blocks = bx < 64 ? (int)bx : 64;
+    hipLaunchKernelGGL(adv_stats_all_kernel, dim3(blocks, nm), dim3(256), 0, s, advantages, a, adv_stats);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }

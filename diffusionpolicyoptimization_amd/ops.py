@@ -434,6 +434,14 @@ def ppo_adv_stats(advantages, total, kf, perm_seed, epoch, start, rows, out, row
     return out
 
 
+def ppo_adv_stats_all(advantages, total, kf, perm_seed, epoch0, n_epochs, rows_full, n_batch, out):
+    """out fp64 [n_epochs * n_batch, 3]: every minibatch's advantage moments in one launch."""
+    _check(out, (n_epochs * n_batch, 3), torch.float64, "out")
+    _lib.call("dppo_ppo_adv_stats_all", ptr(advantages), int(total), int(kf), ctypes.c_uint64(perm_seed), int(epoch0),
+              int(n_epochs), int(rows_full), int(n_batch), ptr(out), stream_handle(advantages.device))
+    return out
+
+
 def ppo_hparams(gamma_denoising=0.99, clip_ploss_coef=0.01, clip_ploss_coef_base=0.01, clip_ploss_coef_rate=3.0,
                 min_logprob_std=0.1, vf_coef=0.5, norm_adv=True, reward_horizon=4, loss_scale=1.0, global_rows=1):
     return _lib.DppoPpoHparams(float(gamma_denoising), float(clip_ploss_coef), float(clip_ploss_coef_base),

@@ -211,6 +211,12 @@ typedef struct dppo_ppo_hparams {
 DPPO_API size_t dppo_ppo_workspace_bytes(const dppo_dims* d, int precision, int batch_rows);
 DPPO_API int dppo_ppo_adv_stats(const float* advantages, int64_t total, int K_ft, uint64_t perm_seed, int epoch,
                        int64_t start, int rows, const int64_t* row_index, double* adv_stats, void* stream);
+/* The adv_stats of every minibatch of an update phase in one launch: minibatch m = e * n_batch + b
+ * covers permutation positions [b * rows_full, min((b+1) * rows_full, total)) of epoch epoch0 + e;
+ * adv_stats receives fp64 [n_epochs * n_batch][3]. Same values as n_epochs * n_batch calls of
+ * dppo_ppo_adv_stats (row_index = NULL); a multi-GPU caller all-reduces the whole array once. */
+DPPO_API int dppo_ppo_adv_stats_all(const float* advantages, int64_t total, int K_ft, uint64_t perm_seed, int epoch0,
+                           int n_epochs, int64_t rows_full, int n_batch, double* adv_stats, void* stream);
 DPPO_API int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
                        const void* packed_ft, const void* packed_critic, const float* actor_params,
                        const float* sched, const float* obs, const float* chains, const float* lp_old_mean,

@@ -435,3 +435,24 @@ def test_pretrain_loss_grads(cuda, precision, rtol, dims):
     errs = {k: float(np.abs(ga[k] - ref).max() / (np.abs(ref).max() + 1e-12)) for k, ref in g_ref.items()}
     bad = {k: v for k, v in errs.items() if not v < rtol}
     assert not bad, (bad, errs)
+
+
+def test_adv_stats_all_matches_per_minibatch(cuda):
+    """dppo_ppo_adv_stats_all (every minibatch of an update phase in one launch) == one
+    dppo_ppo_adv_stats call per minibatch, ragged last minibatch included."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    rng = np.random.default_rng(4)
+    N, kf = 97, 10
+    total = N * kf
+    adv = torch.tensor(rng.normal(size=N).astype(np.float32), device=cuda)
+    rows_full, n_batch, n_ep, seed, ep0 = 200, 5, 3, 77, 3000
+    allst = torch.zeros(n_ep * n_batch, 3, dtype=torch.float64, device=cuda)
+    ops.ppo_adv_stats_all(adv, total, kf, seed, ep0, n_ep, rows_full, n_batch, allst)
+    one = torch.zeros(3, dtype=torch.float64, device=cuda)
+    for e in range(n_ep):
+        for b in range(n_batch):
+            start = b * rows_full
+            rows = min(rows_full, total - start)
+            ops.ppo_adv_stats(adv, total, kf, seed, ep0 + e, start, rows, one)
+            torch.testing.assert_close(allst[e * n_batch + b], one, rtol=1e-12, atol=1e-9)
