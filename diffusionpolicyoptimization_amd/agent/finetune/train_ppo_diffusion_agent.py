@@ -254,9 +254,11 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 m.minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, self.perm_seed,
                             update_epoch + 1000 * self.itr, start, rows, global_rows=global_rows,
                             reward_horizon=self.reward_horizon, adv_stats=stats)
-                if self.world_size > 1:
-                    self._allreduce(m.grads)
-                    self._allreduce(m.metrics)
+                if self.world_size > 1:                # one collective: gradients + metric sums
+                    ng = m.grads.numel()
+                    m.grads_ext[ng:ng + 5].copy_(m.metrics[:5])
+                    self._allreduce(m.grads_ext)
+                    m.metrics[:5].copy_(m.grads_ext[ng:ng + 5])
                 slot = k % 2
                 self._met_pin[slot].copy_(m.metrics[:5], non_blocking=True)
                 ev_m = torch.cuda.Event()

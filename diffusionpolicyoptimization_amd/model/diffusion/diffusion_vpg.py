@@ -64,7 +64,10 @@ class VPGDiffusion(DiffusionModel):
         self.train_params = torch.empty(self.n_actor + self.n_critic, dtype=torch.float32, device=dev)
         self.train_params[:self.n_actor].copy_(self.base_params)  # actor_ft = deepcopy(actor) (:95-97)
         self.train_params[self.n_actor:].copy_(torch.tensor(ops.flatten_params(self.critic_spec, critic_p)))
-        self.grads = torch.zeros_like(self.train_params)
+        # gradients + an 8-float tail: the data-parallel agent reduces the minibatch metrics in the
+        # same all-reduce as the gradients (one collective per minibatch)
+        self.grads_ext = torch.zeros(self.train_params.numel() + 8, dtype=torch.float32, device=dev)
+        self.grads = self.grads_ext[:self.train_params.numel()]
         self.packed_base = ops.pack_actor(self.dims, self.base_params, self.precision)
         self.packed_ft = torch.empty_like(self.packed_base)
         self.packed_critic = torch.empty(ops.critic_packed_bytes(self.dims, self.precision), dtype=torch.uint8,
