@@ -82,6 +82,8 @@ struct ActorArgs {
     const float* noise;    // [rows][XD]
     const float* qsched;   // [K][2] sqrt(alphas_cumprod), sqrt(1 - alphas_cumprod)
     float pre_scale;       // d loss / d eps = pre_scale * (eps - noise)
+    // tile range of one launch: image rows [row0, row_end); row_end = 0: all rows of the mode
+    int64_t row0, row_end;
 };
 
 struct CriticArgs {

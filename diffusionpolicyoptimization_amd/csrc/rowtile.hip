@@ -208,7 +208,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     float* rlpo = (float*)(smem + S.rlpo);   // per row: its old log-prob (train)
     float* nrm = (float*)(smem + S.nrm);     // advantage normalisation: mean, std + 1e-8
     float* part = (float*)(smem + S.tB);   // out-layer partials alias tB (u2 is dead by then)
-    const size_t grow0 = (size_t)blockIdx.x * ROWS;
+    const size_t grow0 = (size_t)a.row0 + (size_t)blockIdx.x * ROWS;
     const __amdgpu_buffer_rsrc_t wsr = packed_rsrc(a.ws.base);
     const uint32_t ldm32 = (uint32_t)a.ws.ldm, grow32 = (uint32_t)grow0;
 
@@ -803,9 +803,10 @@ static int launch_actor_t(const ActorArgs& a, hipStream_t s) {
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S.total));
     // TRAIN mode covers every row of the 64-padded feature-major images (padding rows get
     // finite activations and zero gradients), so the dW kernel never reads unwritten memory
-    const int64_t rows = (a.mode == ROWS_TRAIN || a.mode == ROWS_PRETRAIN) ? (int64_t)a.ws.ldm : a.nrows;
+    const int64_t all = (a.mode == ROWS_TRAIN || a.mode == ROWS_PRETRAIN) ? (int64_t)a.ws.ldm : a.nrows;
+    const int64_t rows = (a.row_end > 0 ? a.row_end : all) - a.row0;
     const int64_t grid = (rows + 16 * MT - 1) / (16 * MT);
-    if (grid == 0) return DPPO_OK;
+    if (grid <= 0) return DPPO_OK;
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * WAVES), S.total, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
@@ -836,13 +837,45 @@ static int dispatch_actor(const ActorArgs& a, hipStream_t s) {
     return dppo_set_error(DPPO_EUNSUPPORTED, "actor: hidden %d / chunk %d not instantiated", a.H, a.XD);
 }
 
+static int64_t actor_device_cus() {
+    static int n = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            c = 256;
+        return c > 0 ? c : 256;
+    }();
+    return n;
+}
+
 int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
     if (precision != DPPO_BF16) return dispatch_actor<PolicyF32, 2, 8>(a, s);
     const int v = row_tile_cfg().actor;
     // bf16, H = 512: 64-row tiles on 16 waves halve the weight stream per row of 32-row tiles; their
     // out-layer partials (16 waves x 64 rows x 16*NO) only fit the aliased LDS tile for XD <= 16
     // (walker2d / halfcheetah, XD = 24, run the 32-row tile)
-    if (a.H == 512 && v == 0 && a.XD <= 16) return dispatch_actor<PolicyBF16, 4, 16>(a, s);
+    if (a.H == 512 && v == 0 && a.XD <= 16) {
+        // The last round of 64-row tiles is short (minibatch 50,000 rows: 782 tiles = 3 rounds of
+        // 256 CUs + 14). Those tail tiles run as twice as many 32-row tiles (about 0.6 of a 64-row
+        // tile's time each) in a launch of their own, then the full rounds: the kernel's last
+        // round shrinks. DPPO_ACTOR_TAIL=0 disables it (measurement knob).
+        static const bool tail_on = [] { const char* e = getenv("DPPO_ACTOR_TAIL"); return !e || atoi(e) != 0; }();
+        const bool tr = a.mode == ROWS_TRAIN || a.mode == ROWS_PRETRAIN;
+        if (tail_on && tr && a.row0 == 0 && a.row_end == 0) {
+            const int64_t tiles = (int64_t)a.ws.ldm / 64, cus = actor_device_cus();
+            const int64_t rem = tiles - ((tiles - 1) / cus) * cus;   // tiles of the last round
+            if (tiles > cus && rem <= cus / 4) {
+                ActorArgs t = a;
+                t.row0 = (tiles - rem) * 64;
+                t.row_end = (int64_t)a.ws.ldm;
+                int rc = dispatch_actor<PolicyBF16, 2, 8>(t, s);
+                if (rc) return rc;
+                ActorArgs m = a;
+                m.row_end = (tiles - rem) * 64;
+                return dispatch_actor<PolicyBF16, 4, 16>(m, s);
+            }
+        }
+        return dispatch_actor<PolicyBF16, 4, 16>(a, s);
+    }
     if (a.H == 512 && v == 3 && a.XD <= 16) return dispatch_actor<PolicyBF16, 4, 8>(a, s);
     return v == 2 ? dispatch_actor<PolicyBF16, 2, 8, true>(a, s) : dispatch_actor<PolicyBF16, 2, 8>(a, s);
 }

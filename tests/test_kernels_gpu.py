@@ -3,6 +3,8 @@
 Tolerances: fp32 (f32-input MFMA) mode is checked tightly; bf16 mode (bf16 operands, fp32
 accumulate/epilogue) against a stated looser bound. Integer work (Feistel permutation) is bit-exact.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -11,6 +13,7 @@ from oracle import philox as PX
 from tests.helpers import HOPPER, HOPPER_DDIM, WALKER, make_models, to_f64
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _setup(dims, cuda, seed=0, eta=1.0):
@@ -456,3 +459,24 @@ def test_adv_stats_all_matches_per_minibatch(cuda):
             rows = min(rows_full, total - start)
             ops.ppo_adv_stats(adv, total, kf, seed, ep0 + e, start, rows, one)
             torch.testing.assert_close(allst[e * n_batch + b], one, rtol=1e-12, atol=1e-9)
+
+
+def test_actor_tail_split_matches_single_launch(tmp_path):
+    """A minibatch of 260 64-row tiles runs its short last round as 32-row tiles in a separate launch
+    (launch_actor_rowtile). Gradients and metrics must match the single-launch run
+    (DPPO_ACTOR_TAIL=0) up to the float-atomic order of the dW sums. Two child processes: the
+    switch is read once per process."""
+    import subprocess
+    import sys
+    outs = []
+    for flag in ("1", "0"):
+        out = str(tmp_path / f"tail{flag}.npz")
+        env = dict(os.environ, DPPO_ACTOR_TAIL=flag)
+        subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_tail_child.py"), out], env=env, check=True,
+                       timeout=120)
+        outs.append(np.load(out))
+    g1, g0 = outs[0]["grads"], outs[1]["grads"]
+    assert np.isfinite(g1).all()
+    np.testing.assert_allclose(g1, g0, rtol=2e-4, atol=1e-5 * np.abs(g0).max())
+    # the 32-row tiles sum the out-layer K in another order: log-prob ulps move ratio - 1 ~ 1e-8
+    np.testing.assert_allclose(outs[0]["metrics"][:5], outs[1]["metrics"][:5], rtol=1e-5, atol=1e-6)
