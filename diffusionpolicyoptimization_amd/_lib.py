@@ -74,6 +74,8 @@ _SIGNATURES = {
     "dppo_ppo_minibatch": (_I, [_DIMS, _I, ctypes.POINTER(DppoPpoHparams), _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                _I64, _U64, _I, _I64, _I, _P, _P, _P, _P, _P, _P]),
     "dppo_pretrain_minibatch": (_I, [_DIMS, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I64, _F, _P, _P, _P, _P]),
+    "dppo_ppo_minibatch_part": (_I, [_DIMS, _I, ctypes.POINTER(DppoPpoHparams), _P, _P, _P, _P, _P, _P, _P, _P,
+                                    _P, _I64, _U64, _I, _I64, _I, _P, _P, _P, _P, _P, _I, _P]),
     "dppo_feistel_permute": (_I, [_I64, _I64, _I64, _U64, _I, _P, _P]),
     "dppo_adamw": (_I, [_P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P]),
 }

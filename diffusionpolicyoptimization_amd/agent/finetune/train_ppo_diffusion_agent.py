@@ -238,6 +238,20 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                               rows_local_full, num_batch, self._adv_all)
         if self.world_size > 1:
             self._allreduce(self._adv_all)
+        # Split update (single GPU): the critic's half of each minibatch (row tiles, dW, its AdamW
+        # range, repack) runs on a side stream and the actor's on the main stream, so the critic of
+        # minibatch i+1 fills the CUs the actor leaves idle in its dW / small-kernel tail of i.
+        # Metrics alternate between two device buffers; the main stream joins the critic's half
+        # before copying a minibatch's metrics.
+        split = (self.world_size == 1 and self.max_grad_norm is None
+                 and os.environ.get("DPPO_SPLIT_UPDATE", "1") != "0")
+        if split:
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(device=self.device)
+                self._met_dev = [torch.zeros(16, dtype=torch.float64, device=self.device) for _ in range(2)]
+            side = self._side
+            side.wait_stream(stream)
+            na = m.n_actor
         k = 0
         stop = False
         for update_epoch in range(self.update_epochs):
@@ -251,16 +265,27 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 if self.update_events is not None:
                     ev0 = torch.cuda.Event(enable_timing=True)
                     ev0.record(stream)
-                m.minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, self.perm_seed,
-                            update_epoch + 1000 * self.itr, start, rows, global_rows=global_rows,
-                            reward_horizon=self.reward_horizon, adv_stats=stats)
+                mb_args = (obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, self.perm_seed,
+                           update_epoch + 1000 * self.itr, start, rows)
+                mb_kw = dict(global_rows=global_rows, reward_horizon=self.reward_horizon, adv_stats=stats)
+                met = m.metrics
+                if split:
+                    met = self._met_dev[k % 2]
+                    with torch.cuda.stream(side):
+                        m.minibatch(*mb_args, **mb_kw, part=2, metrics=met)
+                        ev_c = torch.cuda.Event()
+                        ev_c.record(side)
+                    m.minibatch(*mb_args, **mb_kw, part=1, metrics=met)
+                    stream.wait_event(ev_c)
+                else:
+                    m.minibatch(*mb_args, **mb_kw)
                 if self.world_size > 1:                # one collective: gradients + metric sums
                     ng = m.grads.numel()
                     m.grads_ext[ng:ng + 5].copy_(m.metrics[:5])
                     self._allreduce(m.grads_ext)
                     m.metrics[:5].copy_(m.grads_ext[ng:ng + 5])
                 slot = k % 2
-                self._met_pin[slot].copy_(m.metrics[:5], non_blocking=True)
+                self._met_pin[slot].copy_(met[:5], non_blocking=True)
                 ev_m = torch.cuda.Event()
                 ev_m.record(stream)
                 if pending is not None:
@@ -268,10 +293,17 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     if stop:                                                   # :366-370
                         break
                 if self.itr >= self.n_critic_warmup_itr:
-                    if self.max_grad_norm is not None:
-                        self._clip_by_norm_per_tensor()
-                    lr = self.actor_optimizer.apply_gradients(m.grads)
-                    m.repack()
+                    if split:
+                        self.actor_optimizer.apply_gradients_split(
+                            m.grads, [(0, na, stream), (na, m.grads.numel(), side)])
+                        m.repack(part=1)
+                        with torch.cuda.stream(side):
+                            m.repack(part=2)
+                    else:
+                        if self.max_grad_norm is not None:
+                            self._clip_by_norm_per_tensor()
+                        self.actor_optimizer.apply_gradients(m.grads)
+                        m.repack()
                 if self.update_events is not None:
                     ev1 = torch.cuda.Event(enable_timing=True)
                     ev1.record(stream)
@@ -282,6 +314,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 break
         if pending is not None and not stop:
             info, _ = finish(pending)
+        if split:
+            stream.wait_stream(side)
         # explained variance (:373-377)
         info["explained_var"] = explained_variance(self.values, ret_flat)
         info["clipfrac"] = float(np.mean(clipfracs)) if clipfracs else 0.0

@@ -555,12 +555,15 @@ static int launch_time_bwd(const Dims& D, const float* gseg, const float* actor_
     return DPPO_OK;
 }
 
-extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
-                                  const void* packed_ft, const void* packed_critic, const float* actor_params,
-                                  const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
-                                  const float* advantages, const float* returns, int64_t total, uint64_t perm_seed,
-                                  int epoch, int64_t start, int rows, const int64_t* row_index, const double* adv_stats,
-                                  void* workspace, float* grads, double* metrics, void* stream) {
+// parts: 3 = the whole minibatch (critic on the internal side stream); 1 = the actor's half only,
+// 2 = the critic's half only, each on the caller's stream (the caller overlaps them; see
+// dppo_ppo_minibatch_part in include/dppo.h)
+static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
+                              const void* packed_ft, const void* packed_critic, const float* actor_params,
+                              const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
+                              const float* advantages, const float* returns, int64_t total, uint64_t perm_seed,
+                              int epoch, int64_t start, int rows, const int64_t* row_index, const double* adv_stats,
+                              void* workspace, float* grads, double* metrics, void* stream, int parts) {
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
@@ -578,19 +581,32 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     const FlatOffsets FC = make_flat_offsets(D.SD, D.HC, 1, 0);
     float* ga = grads;
     float* gc = grads + FA.count;
-    // one launch zeroes the atomically accumulated outputs (gradients, metrics, bucket sums, stats)
+    DPPO_CHECK(parts >= 1 && parts <= 3, "dppo_ppo_minibatch: bad part %d", parts);
+    DPPO_CHECK(parts == 3 || adv_stats || parts == 2, "dppo_ppo_minibatch_part: the actor half needs adv_stats");
+    // one launch zeroes the atomically accumulated outputs of the half (or whole) being run:
+    // gradients, metrics (actor: 0, 2..15; critic: 1), bucket sums, stats
     ZeroArgs z = {};
-    z.p[0] = grads; z.n[0] = (FA.count + FC.count) * sizeof(float);
-    z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
-    z.p[2] = ws.gseg; z.n[2] = (size_t)16 * D.H * sizeof(float);
-    z.p[3] = ws.stats; z.n[3] = 4 * sizeof(double);
+    if (parts == 3) {
+        z.p[0] = grads; z.n[0] = (FA.count + FC.count) * sizeof(float);
+        z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
+        z.p[2] = ws.gseg; z.n[2] = (size_t)16 * D.H * sizeof(float);
+        z.p[3] = ws.stats; z.n[3] = 4 * sizeof(double);
+    } else if (parts == 1) {
+        z.p[0] = grads; z.n[0] = FA.count * sizeof(float);
+        z.p[1] = metrics; z.n[1] = sizeof(double);
+        z.p[2] = metrics + 2; z.n[2] = 14 * sizeof(double);
+        z.p[3] = ws.gseg; z.n[3] = (size_t)16 * D.H * sizeof(float);
+    } else {
+        z.p[0] = grads + FA.count; z.n[0] = FC.count * sizeof(float);
+        z.p[1] = metrics + 1; z.n[1] = sizeof(double);
+    }
     hipLaunchKernelGGL(zero_kernel, dim3(256), dim3(256), 0, s, z);
     DPPO_HIP(hipGetLastError());
     DPPO_CHECK((uint64_t)total < ((uint64_t)1 << 32), "dppo_ppo_minibatch: %lld samples x steps exceed 2^32",
                (long long)total);
     const FeistelKey fk = feistel_key((uint64_t)total, perm_seed, epoch);
     const double* stats = adv_stats;
-    if (!stats) {
+    if (!stats && parts != 2) {
         const int blocks = dppo_cdiv(rows, 256) < 512 ? dppo_cdiv(rows, 256) : 512;
         hipLaunchKernelGGL(adv_stats_kernel, dim3(blocks), dim3(256), 0, s, advantages, fk, D.KF, start, rows,
                            row_index, ws.stats);
@@ -657,6 +673,18 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     // side stream, filling the CUs the actor's row tiles leave idle (the actor's last partial round)
     // and overlapping the critic's HBM-bound dW with the actor's tiles. Joined before the
     // actor's dW completes the minibatch.
+    if (parts == 2) {                                  // the critic's half on the caller's stream
+        rc = launch_critic_rowtile(ca, precision, s);
+        if (rc) return rc;
+        return launch_grads(false, s);
+    }
+    if (parts == 1) {                                  // the actor's half on the caller's stream
+        rc = launch_actor_rowtile(aa, precision, s);
+        if (rc) return rc;
+        rc = launch_grads(true, s);
+        if (rc) return rc;
+        return launch_time_bwd(D, ws.gseg, actor_params, ga, D.KF, D.TS, s);
+    }
     SideStream* side = side_stream();
     if (side) {
         DPPO_HIP(hipEventRecord(side->fork, s));
@@ -680,6 +708,30 @@ extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_
     if (side) DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
 
     return launch_time_bwd(D, ws.gseg, actor_params, ga, D.KF, D.TS, s);
+}
+
+extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
+                                  const void* packed_ft, const void* packed_critic, const float* actor_params,
+                                  const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
+                                  const float* advantages, const float* returns, int64_t total, uint64_t perm_seed,
+                                  int epoch, int64_t start, int rows, const int64_t* row_index, const double* adv_stats,
+                                  void* workspace, float* grads, double* metrics, void* stream) {
+    return ppo_minibatch_impl(d, precision, hp, packed_ft, packed_critic, actor_params, sched, obs, chains, lp_old_mean,
+                              advantages, returns, total, perm_seed, epoch, start, rows, row_index, adv_stats, workspace,
+                              grads, metrics, stream, 3);
+}
+
+extern "C" int dppo_ppo_minibatch_part(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
+                                       const void* packed_ft, const void* packed_critic, const float* actor_params,
+                                       const float* sched, const float* obs, const float* chains,
+                                       const float* lp_old_mean, const float* advantages, const float* returns,
+                                       int64_t total, uint64_t perm_seed, int epoch, int64_t start, int rows,
+                                       const int64_t* row_index, const double* adv_stats, void* workspace,
+                                       float* grads, double* metrics, int part, void* stream) {
+    DPPO_CHECK(part == 1 || part == 2, "dppo_ppo_minibatch_part: part must be 1 (actor) or 2 (critic)");
+    return ppo_minibatch_impl(d, precision, hp, packed_ft, packed_critic, actor_params, sched, obs, chains, lp_old_mean,
+                              advantages, returns, total, perm_seed, epoch, start, rows, row_index, adv_stats, workspace,
+                              grads, metrics, stream, part);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -45,13 +45,17 @@ class PPODiffusion(VPGDiffusion):
         return ws
 
     def minibatch(self, obs, chains, lp_old_mean, advantages, returns, perm_seed, epoch, start, rows,
-                  global_rows=None, reward_horizon=4, loss_scale=1.0, adv_stats=None, row_index=None):
+                  global_rows=None, reward_horizon=4, loss_scale=1.0, adv_stats=None, row_index=None, part=None,
+                  metrics=None):
         """One fused PPO minibatch over HBM rollout buffers (obs [N,SD], chains [N,K'+1,XD],
-        lp_old_mean [N,K'], advantages/returns [N]); writes self.grads and self.metrics (sums)."""
+        lp_old_mean [N,K'], advantages/returns [N]); writes self.grads and self.metrics (sums).
+        part = 1 / 2 runs only the actor / critic half on the current stream (metrics: an
+        alternative fp64[16] buffer)."""
         hp = self.hparams(global_rows or rows, reward_horizon, loss_scale)
         ops.ppo_minibatch(self.dims, self.precision, hp, self.packed_ft, self.packed_critic, self.actor_ft_params,
                           self.sched, obs, chains, lp_old_mean, advantages, returns, perm_seed, epoch, start, rows,
-                          self.workspace(rows), self.grads, self.metrics, adv_stats=adv_stats, row_index=row_index)
+                          self.workspace(rows), self.grads, self.metrics if metrics is None else metrics,
+                          adv_stats=adv_stats, row_index=row_index, part=part)
 
     def c_loss(self, obs, chains_prev, chains_next, denoising_inds, returns, oldvalues, advantages, oldlogprobs,
                use_bc_loss=False, reward_horizon=4):

@@ -102,10 +102,13 @@ class VPGDiffusion(DiffusionModel):
     def trainable_variables(self):
         return [self.train_params]
 
-    def repack(self):
-        """Re-derive the packed fragment images of actor_ft and critic after an optimiser step."""
-        ops.pack_actor(self.dims, self.actor_ft_params, self.precision, out=self.packed_ft)
-        ops.pack_critic(self.dims, self.critic_params, self.precision, out=self.packed_critic)
+    def repack(self, part=None):
+        """Re-derive the packed fragment images of actor_ft (part 1) and/or critic (part 2) after an
+        optimiser step."""
+        if part in (None, 1):
+            ops.pack_actor(self.dims, self.actor_ft_params, self.precision, out=self.packed_ft)
+        if part in (None, 2):
+            ops.pack_critic(self.dims, self.critic_params, self.precision, out=self.packed_critic)
 
     def _load_actor(self, path, rng):
         if path is None or not os.path.exists(str(path)):

@@ -451,7 +451,7 @@ def ppo_hparams(gamma_denoising=0.99, clip_ploss_coef=0.01, clip_ploss_coef_base
 
 def ppo_minibatch(d: ModelDims, precision, hp, packed_ft, packed_critic, actor_params, sched, obs, chains, lp_old_mean,
                   advantages, returns, perm_seed, epoch, start, rows, workspace, grads, metrics, adv_stats=None,
-                  row_index=None):
+                  row_index=None, part=None):
     n = obs.shape[0]
     kf = d.ft_denoising_steps
     _check(obs, (n, d.sd), torch.float32, "obs")
@@ -470,10 +470,14 @@ def ppo_minibatch(d: ModelDims, precision, hp, packed_ft, packed_critic, actor_p
     need = int(_lib.query("dppo_ppo_workspace_bytes", ctypes.byref(d.c()), _prec(precision), int(rows)))
     if workspace.numel() < need:
         raise ValueError(f"workspace too small: {workspace.numel()} < {need}")
-    _lib.call("dppo_ppo_minibatch", ctypes.byref(d.c()), _prec(precision), ctypes.byref(hp), ptr(packed_ft),
-              ptr(packed_critic), ptr(actor_params), ptr(sched), ptr(obs), ptr(chains), ptr(lp_old_mean),
-              ptr(advantages), ptr(returns), int(n * kf), ctypes.c_uint64(perm_seed), int(epoch), int(start), int(rows),
-              ptr(row_index), ptr(adv_stats), ptr(workspace), ptr(grads), ptr(metrics), stream_handle(obs.device))
+    args = (ctypes.byref(d.c()), _prec(precision), ctypes.byref(hp), ptr(packed_ft), ptr(packed_critic),
+            ptr(actor_params), ptr(sched), ptr(obs), ptr(chains), ptr(lp_old_mean), ptr(advantages), ptr(returns),
+            int(n * kf), ctypes.c_uint64(perm_seed), int(epoch), int(start), int(rows), ptr(row_index), ptr(adv_stats),
+            ptr(workspace), ptr(grads), ptr(metrics))
+    if part is None:
+        _lib.call("dppo_ppo_minibatch", *args, stream_handle(obs.device))
+    else:   # 1 = actor half, 2 = critic half, on the current stream (dppo_ppo_minibatch_part)
+        _lib.call("dppo_ppo_minibatch_part", *args, int(part), stream_handle(obs.device))
 
 
 def q_sched_table(schedule):

@@ -31,6 +31,18 @@ class AdamW:
                   self.epsilon, self.mode)
         return lr
 
+    def apply_gradients_split(self, grads, ranges):
+        """One optimiser step over disjoint ranges of the flat buffer, each on its own stream:
+        ranges = [(lo, hi, stream), ...]. Elementwise, so it equals apply_gradients."""
+        import torch
+        lr = self.current_lr()
+        self.iterations += 1
+        for lo, hi, st in ranges:
+            with torch.cuda.stream(st):
+                ops.adamw(self.params[lo:hi], grads[lo:hi], self.m[lo:hi], self.v[lo:hi], self.iterations, lr,
+                          self.weight_decay, self.beta_1, self.beta_2, self.epsilon, self.mode)
+        return lr
+
     def state_dict(self):
         return {"m": self.m.detach().cpu().numpy(), "v": self.v.detach().cpu().numpy(), "iterations": self.iterations}
 

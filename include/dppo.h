@@ -241,6 +241,18 @@ DPPO_API int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const vo
                             const int32_t* t, const float* noise, int rows, int64_t global_rows, float loss_scale,
                             void* workspace, float* grads, double* metrics, void* stream);
 
+/* One half of dppo_ppo_minibatch on the caller's stream, so a caller can overlap the critic's half
+ * of minibatch i+1 with the actor's tail of minibatch i: part 1 = the actor (zeroes the actor
+ * gradients and metrics 0, 2..15; row tiles, dW, time-MLP backward; needs adv_stats), part 2 =
+ * the critic (zeroes the critic gradients and metric 1; row tiles, dW). Same arguments and results
+ * as dppo_ppo_minibatch, which runs both (the critic on an internal side stream). */
+DPPO_API int dppo_ppo_minibatch_part(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
+                            const void* packed_ft, const void* packed_critic, const float* actor_params,
+                            const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
+                            const float* advantages, const float* returns, int64_t total, uint64_t perm_seed,
+                            int epoch, int64_t start, int rows, const int64_t* row_index, const double* adv_stats,
+                            void* workspace, float* grads, double* metrics, int part, void* stream);
+
 /* Feistel permutation used above, exposed for tests: out[i] = perm(first + i), i < count. */
 DPPO_API int dppo_feistel_permute(int64_t first, int64_t count, int64_t n, uint64_t seed, int epoch, int64_t* out,
                          void* stream);
