@@ -68,6 +68,7 @@ class TrainAgent:
         self.save_full_observations = cfg.env.get("save_full_observations", False)
         self.furniture_sparse_reward = False
         self.batch_size = int(cfg.train.batch_size)
+        self.dp_scale_batch = bool(cfg.train.get("dp_scale_batch", True))
 
         self.model = instantiate(cfg.model, device=str(self.device), seed=self.seed)
         self.model.set_rng(self.seed, env_offset=self.env_offset)

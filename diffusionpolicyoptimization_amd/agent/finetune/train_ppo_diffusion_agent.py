@@ -205,8 +205,14 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
 
         total_local = N * kf
         total_global = total_local * self.world_size
-        num_batch = max(1, total_global // self.batch_size)                               # :288
-        rows_local_full = self.batch_size // self.world_size
+        # Data parallel (SURVEY §8(e), weak scaling): by default every rank runs the single-GPU
+        # minibatch of batch_size rows from its own shard and the gradients are averaged, i.e. the
+        # reference run with batch_size x world over world x n_envs envs (train.dp_scale_batch);
+        # with dp_scale_batch = false the global minibatch stays batch_size (batch_size / world
+        # rows per rank, world x more minibatches).
+        eff_batch = self.batch_size * (self.world_size if self.dp_scale_batch else 1)
+        num_batch = max(1, total_global // eff_batch)                                     # :288
+        rows_local_full = eff_batch // self.world_size
         clipfracs, info = [], {}
         stream = torch.cuda.current_stream(self.device)
         # The target_kl check (:366-370) reads each minibatch's approx_kl on the host. It runs one

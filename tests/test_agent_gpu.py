@@ -125,8 +125,10 @@ def test_pipelined_rollout_matches_model_call(cuda, protocol, precision, monkeyp
     pipe.close()
 
 
-def test_data_parallel_agent_two_ranks_share_one_gpu(tmp_path):
-    """2 ranks (gloo, both on cuda:0) run the DP agent; replicas must stay bit-identical."""
+@pytest.mark.parametrize("overrides", ["", "train.dp_scale_batch=false"], ids=["per-rank-batch", "global-batch"])
+def test_data_parallel_agent_two_ranks_share_one_gpu(tmp_path, overrides):
+    """2 ranks (gloo, both on cuda:0) run the DP agent; replicas must stay bit-identical, with the
+    minibatch per rank (default) or fixed globally."""
     import socket
     import subprocess
     import sys
@@ -136,7 +138,7 @@ def test_data_parallel_agent_two_ranks_share_one_gpu(tmp_path):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    env = dict(os.environ, DPPO_DIST_BACKEND="gloo", DPPO_SINGLE_DEVICE="1")
+    env = dict(os.environ, DPPO_DIST_BACKEND="gloo", DPPO_SINGLE_DEVICE="1", DPPO_SMOKE_OVERRIDES=overrides)
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                           "--master-addr", "127.0.0.1", "--master-port", str(port),
                           os.path.join(ROOT, "tools", "dist_smoke.py")],

@@ -19,7 +19,8 @@ def main():
     cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
                       [f"env.n_envs={4 * world}", "train.n_steps=20", "train.batch_size=200", "train.n_train_itr=3",
                        "train.val_freq=2", "train.save_checkpoints=False", "train.save_results=False",
-                       f"logdir=/tmp/dppo_dist_smoke_{os.environ.get('RANK', '0')}"])
+                       f"logdir=/tmp/dppo_dist_smoke_{os.environ.get('RANK', '0')}"]
+                      + os.environ.get("DPPO_SMOKE_OVERRIDES", "").split())
     agent = get_class(cfg._target_)(cfg)
     res = agent.run()
     p = agent.model.train_params.double()
