@@ -277,56 +277,58 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
     __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0): the resident set has landed
     permute_out();
     // pre-enqueued rollout step: wait for the host's observation (bounded, as sampler.hip)
+    // everything that does not need the observation is done before its wait: a0's x / temb /
+    // padding columns and the exchange-failure flag (xs, x_T, comes from the noise loop above)
+    __syncthreads();
+    const int k1w = KSI * 32;
+    for (int idx = tid; idx < 16 * k1w; idx += ST) {
+        const int r = idx / k1w, cc = idx % k1w;
+        if (cc >= XD + TD && cc < a.IN) continue;              // state columns: after the wait
+        const float v = cc < XD ? xs[r * XD + cc] : (cc < XD + TD ? temb[(K - 1) * TD + cc - XD] : 0.f);
+        a0[r * lda0 + cc] = Pol::cvt(v);
+    }
+    if (tid == 0) *xfail = 0;
     XPHASE(7);                                              // timing builds: phase 7 = prologue before the wait
+    // after the wait each thread writes the state columns of the entries it read itself (the tagged
+    // load and the go path map entry i to thread i mod ST), so one barrier ends the prologue
     if (a.cond_tagged) {
         sampler_load_state_tagged<ST>(a, row0, st, c == 0, tid);
         XPHASE(8);                                          // phase 8 = the wait for the tagged observation
         for (int i = tid; i < 16 * SD; i += ST) {
             const int r = i / SD, cc = i % SD, row = row0 + r;
+            a0[r * lda0 + XD + TD + cc] = Pol::cvt(st[i]);
             if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, st[i]);
         }
     } else {
-    if (a.go) {
-        if (tid == 0) {
-            const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;   // 100 MHz: 4 s
+        if (a.go) {
+            if (tid == 0) {
+                const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;   // 100 MHz: 4 s
 #if DPPO_SPLIT_SIGNAL >= 1
-            while (__hip_atomic_load(a.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
+                while (__hip_atomic_load(a.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
 #else
-            while (__hip_atomic_load(a.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
+                while (__hip_atomic_load(a.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
 #endif
-                __builtin_amdgcn_s_sleep(8);
-                if (__builtin_amdgcn_s_memrealtime() > t_end) {
-                    if (c == 0) __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
+                    __builtin_amdgcn_s_sleep(8);
+                    if (__builtin_amdgcn_s_memrealtime() > t_end) {
+                        if (c == 0) __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
                 }
-            }
 #if DPPO_SPLIT_SIGNAL >= 1
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");    // one system acquire after the match
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");    // one system acquire after the match
 #endif
+            }
+            __syncthreads();
         }
-        __syncthreads();
+        XPHASE(8);                                              // phase 8 = the wait for go
+        for (int i = tid; i < 16 * SD; i += ST) {
+            const int r = i / SD, cc = i % SD, row = row0 + r;
+            const float v = row < a.E ? a.cond[(size_t)row * SD + cc] : 0.f;
+            st[i] = v;
+            a0[r * lda0 + XD + TD + cc] = Pol::cvt(v);
+            if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, v);
+        }
     }
-    XPHASE(8);                                              // phase 8 = the wait for go
-    for (int i = tid; i < 16 * SD; i += ST) {
-        const int r = i / SD, cc = i % SD, row = row0 + r;
-        const float v = row < a.E ? a.cond[(size_t)row * SD + cc] : 0.f;
-        st[i] = v;
-        if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, v);
-    }
-    }
-    __syncthreads();
-    const int k1w = KSI * 32;
-    for (int idx = tid; idx < 16 * k1w; idx += ST) {
-        const int r = idx / k1w, cc = idx % k1w;
-        float v = 0.f;
-        if (cc < XD) v = xs[r * XD + cc];
-        else if (cc < XD + TD) v = temb[(K - 1) * TD + cc - XD];
-        else if (cc < a.IN) v = st[r * SD + cc - XD - TD];
-        a0[r * lda0 + cc] = Pol::cvt(v);
-    }
-    __syncthreads();
-
-    if (tid == 0) *xfail = 0;
     __syncthreads();
     const int env = lane & 15, jq = lane >> 4;
     XPHASE(0);
