@@ -222,6 +222,10 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     constexpr int QD = DPPO_ROWTILE_QD;   // weight k-steps in flight per wave
     WQueue<QD, NT> R;
     queue_prime(R, W(SEG_W_IN), KSI, NextLayers{W(SEG_W_L1), KSH, W(SEG_W_L2), KSH}, ntile0, lane);
+    // Phase 1 computes only the row map, so its barrier waits on no global load: the per-row
+    // advantage / old log-prob and the minibatch moments are loaded into registers here and
+    // reach LDS after L1 (first read in the epilogue); parameters and gathers share phase 2.
+    float pre_adv = 0.f, pre_lpo = 0.f, pre_m = 0.f, pre_s = 0.f;
     if (tid < ROWS) {
         const int64_t gr = (int64_t)grow0 + tid;
         int n = -1, j = 0;
@@ -242,16 +246,17 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         }
         rn[tid] = n; rj[tid] = j;
         if (train && !pre) {
-            radv[tid] = n >= 0 ? a.adv[n] : 0.f;
-            rlpo[tid] = n >= 0 ? a.lp_old[(size_t)n * KF + j] : 0.f;
+            pre_adv = n >= 0 ? a.adv[n] : 0.f;
+            pre_lpo = n >= 0 ? a.lp_old[(size_t)n * KF + j] : 0.f;
         }
     } else if (train && !pre && tid == ROWS) {   // population mean / std of the minibatch (diffusion_ppo.py:74-75)
         const double* S3 = a.adv_stats;
         const double mean = S3[1] / S3[0];
         const double var = fmax(S3[2] / S3[0] - mean * mean, 0.0);
-        nrm[0] = (float)mean;
-        nrm[1] = (float)(sqrt(var) + 1e-8);
+        pre_m = (float)mean;
+        pre_s = (float)(sqrt(var) + 1e-8);
     }
+    __syncthreads();
     for (int i = tid; i < KF * DPPO_SCHED_COLS; i += THREADS) sch[i] = a.sched[i];
     for (int i = tid; i < 3 * H + 16 * NO; i += THREADS) {
         const int seg = i < H ? SEG_B_IN : (i < 2 * H ? SEG_B_L1 : (i < 3 * H ? SEG_B_L2 : SEG_B_OUT));
@@ -262,7 +267,6 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         const float* tt = (const float*)(a.packed + L.off[SEG_TEMB]);
         for (int i = tid; i < KF * TD; i += THREADS) temb[i] = tt[i];
     }
-    __syncthreads();
     for (int i = tid; i < ROWS * XD; i += THREADS) {
         const int r = i / XD, q = i % XD, n = rn[r];
         float vp = 0.f, vn = 0.f;
@@ -334,6 +338,10 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.u1T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     PHASE(1);
+    if (train && !pre) {   // loaded in the prologue, read from the epilogue on (after later barriers)
+        if (tid < ROWS) { radv[tid] = pre_adv; rlpo[tid] = pre_lpo; }
+        else if (tid == ROWS) { nrm[0] = pre_m; nrm[1] = pre_s; }
+    }
     // ---- L2: h2 = relu(h1) W_l1 + b ----
     gemm_queue<P, MT, NT, KSH, QD>(tA, ldh, W(SEG_W_L1), ntile0, acc, lane, R,
                                    NextLayers{W(SEG_W_L2), KSH, W(SEG_W_IN), KSI});
