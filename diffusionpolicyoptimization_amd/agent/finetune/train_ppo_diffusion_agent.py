@@ -130,6 +130,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # step t+1's launch is enqueued before the envs of step t are stepped; it waits on
             # the device for the observation the host publishes after the env step
             pipe = self.pipe
+            pipe.begin()
             pipe.enqueue(0, eval_mode)
             pipe.publish()
             gated = getattr(self.venv, "native", None) is not None   # wait + step + publish in C
@@ -148,6 +149,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     if more:
                         pipe.publish()
                 bookkeeping(step, reward, terminated, truncated)
+            pipe.end()
             stream.synchronize()
         else:
             if self._stepper is None:

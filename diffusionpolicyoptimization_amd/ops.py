@@ -181,7 +181,15 @@ class SampleStepper:
         self._obs0, self._obs_step = obs_traj.data_ptr(), E * d.sd * 4
         self._ch0, self._ch_step = chains_traj.data_ptr(), E * (d.ft_denoising_steps + 1) * d.xd * 4
         self._fixed = (ptr(cond_host), ptr(actions), ptr(actions_host))
-        self._stream = stream_handle(obs_traj.device)
+        # consecutive launches alternate over DPPO_ROLLOUT_STREAMS streams (default 2): launch t+1 is
+        # dispatched, and runs its observation-independent prologue (resident weights, noise), while
+        # launch t still runs, instead of after it retires. begin() / end() order them against the
+        # caller's stream around a rollout.
+        nst = max(1, int(os.environ.get("DPPO_ROLLOUT_STREAMS", "2")))
+        dev = obs_traj.device
+        self._tstreams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(nst - 1)]
+        self._handles = [ctypes.c_void_p(st.cuda_stream) for st in self._tstreams]
+        self._stream = self._handles[0]
 
     def __call__(self, i, deterministic=False):
         if not 0 <= i < self.S:
@@ -247,7 +255,15 @@ class RolloutPipe:
         self._obs0, self._obs_step = obs_traj.data_ptr(), E * d.sd * 4
         self._ch0, self._ch_step = chains_traj.data_ptr(), E * (d.ft_denoising_steps + 1) * d.xd * 4
         self._actions = ptr(actions)
-        self._stream = stream_handle(obs_traj.device)
+        # consecutive launches alternate over DPPO_ROLLOUT_STREAMS streams (default 2): launch t+1 is
+        # dispatched, and runs its observation-independent prologue (resident weights, noise), while
+        # launch t still runs, instead of after it retires. begin() / end() order them against the
+        # caller's stream around a rollout.
+        nst = max(1, int(os.environ.get("DPPO_ROLLOUT_STREAMS", "2")))
+        dev = obs_traj.device
+        self._tstreams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(nst - 1)]
+        self._handles = [ctypes.c_void_p(st.cuda_stream) for st in self._tstreams]
+        self._stream = self._handles[0]
         self.nwg = (E + 15) // 16
         self.enqueued = 0      # steps launched so far (step s waits for go >= s + 1)
         self.published = 0
@@ -259,6 +275,7 @@ class RolloutPipe:
         m = self.model
         fc = m.final_action_clip_value
         p = self._p
+        self._stream = self._handles[self.enqueued % len(self._handles)]
         self.enqueued += 1
         common = (ctypes.byref(self._dims), _prec(m.precision), ptr(m.packed_base), ptr(m.packed_ft),
                   ptr(m.sched_for(deterministic)))
@@ -276,6 +293,16 @@ class RolloutPipe:
         if rc:
             raise _lib.DppoError(f"dppo_rollout_enqueue failed ({rc}): {self._lib.dppo_last_error().decode()}")
         m._call_id += 1
+
+    def begin(self):
+        """Before a rollout: the launch streams wait for the caller's stream (updated weights)."""
+        for st in self._tstreams[1:]:
+            st.wait_stream(self._tstreams[0])
+
+    def end(self):
+        """After a rollout: the caller's stream waits for every launch stream."""
+        for st in self._tstreams[1:]:
+            self._tstreams[0].wait_stream(st)
 
     def publish(self):
         self.published += 1
@@ -316,7 +343,8 @@ class RolloutPipe:
                 raise _lib.DppoError(f"rollout step {self.finished - 1} did not finish within {timeout_s} s")
 
     def close(self):
-        torch.cuda.current_stream(self._keep[0].device).synchronize()
+        for st in self._tstreams:
+            st.synchronize()
         for b in self._bufs:
             self._lib.dppo_host_free(ctypes.c_void_p(b))
         self._bufs = []

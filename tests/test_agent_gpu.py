@@ -103,6 +103,7 @@ def test_pipelined_rollout_matches_model_call(cuda, protocol, precision, monkeyp
     obs = [rng.uniform(-1, 1, (E, d.sd)).astype(np.float32) for _ in range(S)]
     cid0 = model._call_id
     pipe.obs.numpy()[:] = obs[0]
+    pipe.begin()
     pipe.enqueue(0)
     pipe.publish()
     got = []
@@ -114,6 +115,7 @@ def test_pipelined_rollout_matches_model_call(cuda, protocol, precision, monkeyp
         if i + 1 < S:
             pipe.obs.numpy()[:] = obs[i + 1]
             pipe.publish()
+    pipe.end()
     torch.cuda.synchronize()
     model._call_id = cid0
     for i in range(S):
