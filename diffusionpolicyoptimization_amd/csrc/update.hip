@@ -600,7 +600,10 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         z.p[0] = grads + FA.count; z.n[0] = FC.count * sizeof(float);
         z.p[1] = metrics + 1; z.n[1] = sizeof(double);
     }
-    hipLaunchKernelGGL(zero_kernel, dim3(256), dim3(256), 0, s, z);
+    // few workgroups: the split update runs this while the other stream's row tiles hold most CUs,
+    // and a 256-block grid waited ~25 us for slots (DPPO_ZERO_BLOCKS: measurement knob)
+    static const int zero_blocks = [] { const char* e = getenv("DPPO_ZERO_BLOCKS"); return e ? atoi(e) : 16; }();
+    hipLaunchKernelGGL(zero_kernel, dim3(zero_blocks > 0 ? zero_blocks : 16), dim3(256), 0, s, z);
     DPPO_HIP(hipGetLastError());
     DPPO_CHECK((uint64_t)total < ((uint64_t)1 << 32), "dppo_ppo_minibatch: %lld samples x steps exceed 2^32",
                (long long)total);
