@@ -240,7 +240,9 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
 // time-MLP backward (mlp_diffusion.py:40-45) from the per-t bucket sums of dh1:
 //   in_b' = sum_q G[q];  dtemb[q] = G[q] . W_in[XD:XD+TD]^T;  then Dense/mish/Dense backward.
 // ---------------------------------------------------------------------------------------------
+#ifndef TB_THREADS
 #define TB_THREADS 1024
+#endif
 // One workgroup; every parameter it reads (the TD temb rows of W_in and the time MLP) is staged into
 // LDS in one batch of coalesced loads at the start, so the dependent phases below run from LDS and
 // the kernel pays global-load latency about twice (staging, then G) instead of once per phase.
