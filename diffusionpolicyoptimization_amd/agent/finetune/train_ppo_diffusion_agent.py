@@ -133,7 +133,9 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             pipe.begin()
             pipe.enqueue(0, eval_mode)
             pipe.publish()
-            gated = getattr(self.venv, "native", None) is not None   # wait + step + publish in C
+            # wait + step + publish in C (the tagged stepper decodes the actions into act_view itself,
+            # so it needs the whole [E, horizon, Da] buffer: act_steps == horizon_steps)
+            gated = getattr(self.venv, "native", None) is not None and act_view.flags.c_contiguous
             for step in range(S):
                 more = step + 1 < S
                 if more:

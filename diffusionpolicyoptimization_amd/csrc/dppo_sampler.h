@@ -16,6 +16,7 @@ struct SampleArgs {
     float* chains;        // [E][KF+1][XD] or null
     float* cond_out;      // [E][SD] device copy of cond or null (cond may be mapped host memory)
     float* actions_host;  // [E][XD] mapped pinned host memory or null (zero-copy action hand-off)
+    uint64_t* actions_tagged;  // [E][XD] tagged granules {cond_tag, fp32} in mapped host memory, or null
     // pre-enqueued rollout steps (dppo_rollout_*): wait until *go >= go_value before reading cond,
     // and add 1 to *done per workgroup after the actions are visible to the host (both counters
     // live in fine-grained host memory); null = an ordinary launch

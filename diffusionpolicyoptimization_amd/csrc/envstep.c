@@ -167,20 +167,41 @@ DPPO_ENV_API void dppo_env_publish_tagged(int64_t count, const float* obs, uint6
     }
 }
 
-/* dppo_env_step_gated with the tagged protocol: after the step, when no episode ended (no reset
- * left for the host to apply), the observation is published as granules with `tag`. */
+/* dppo_env_step_gated with the tagged protocol both ways: spin until every action granule of
+ * act_tagged carries act_tag (the device's stores are the ready flag: no wait for the done counter,
+ * whose bit 31 still reports a device-side timeout), decode them into `actions` (the float buffer the
+ * caller keeps), step, and when no episode ended publish the observation as granules with `tag`. */
 DPPO_ENV_API int dppo_env_step_gated_tagged(int E, int Do, int Da, int act_steps, int Ta, int max_steps, int n_obs_steps,
                                             const double* AT, const double* B, const double* c, const double* goal,
-                                            double* state, int64_t* cnt, const float* actions, double* reward,
+                                            double* state, int64_t* cnt, float* actions, double* reward,
                                             uint8_t* terminated, uint8_t* truncated, float* obs_out,
-                                            const volatile uint32_t* done, uint32_t done_target, uint64_t* obs_tagged,
-                                            uint32_t tag, double timeout_s) {
-    const int rc = dppo_env_step_gated(E, Do, Da, act_steps, Ta, max_steps, n_obs_steps, AT, B, c, goal, state, cnt,
-                                       actions, reward, terminated, truncated, obs_out, done, done_target, NULL, 0,
-                                       timeout_s);
-    if (rc == 0 && obs_tagged) {
+                                            const volatile uint32_t* done, const uint64_t* act_tagged,
+                                            uint32_t act_tag, uint64_t* obs_tagged, uint32_t tag, double timeout_s) {
+    const int64_t na = (int64_t)E * Ta * Da;
+    double t_end = -1.0;
+    int64_t i = 0;   /* granules before i are known to carry act_tag */
+    for (uint32_t spins = 0;; ++spins) {
+        while (i < na) {
+            const uint64_t x = __atomic_load_n(act_tagged + i, __ATOMIC_ACQUIRE);
+            if ((uint32_t)(x >> 32) != act_tag) break;
+            const uint32_t bits = (uint32_t)x;
+            memcpy(actions + i, &bits, 4);
+            ++i;
+        }
+        if (i == na) break;
+        if (__atomic_load_n(done, __ATOMIC_ACQUIRE) & 0x80000000u) return -2;
+        _mm_pause();
+        if ((spins & 1023u) == 1023u) {
+            const double now = env_now_s();
+            if (t_end < 0.0) t_end = now + timeout_s;
+            else if (now > t_end) return -1;
+        }
+    }
+    const int n_done = dppo_env_step(E, Do, Da, act_steps, Ta, max_steps, n_obs_steps, AT, B, c, goal, state, cnt,
+                                     actions, reward, terminated, truncated, obs_out);
+    if (n_done == 0 && obs_tagged) {
         dppo_env_publish_tagged((int64_t)E * n_obs_steps * Do, obs_out, obs_tagged, tag);
         return DPPO_ENV_PUBLISHED;
     }
-    return rc;
+    return n_done;
 }

@@ -416,7 +416,11 @@ __global__ __launch_bounds__(SW * 64) void sample_kernel(SampleArgs a) {
                 if (a.chains && t <= KF) a.chains[((size_t)row * (KF + 1) + (KF - t)) * XD + q] = xn;
                 if (i == K - 1) {
                     a.actions[(size_t)row * XD + q] = xn;
-                    if (a.actions_host) a.actions_host[(size_t)row * XD + q] = xn;
+                    if (a.actions_tagged)   // the action is its own flag: one aligned 8-B store
+                        __hip_atomic_store(a.actions_tagged + (size_t)row * XD + q,
+                                           ((uint64_t)a.cond_tag << 32) | __float_as_uint(xn), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    else if (a.actions_host) a.actions_host[(size_t)row * XD + q] = xn;
                 }
             }
         } else if (t > 0) {                                     // the next step's time embedding
@@ -565,7 +569,8 @@ static int sample_impl(const dppo_dims* d, int precision, const void* packed_bas
                        float min_sampling_std, float randn_clip, float final_clip,
                        float* actions, float* chains, float* cond_out, float* actions_host, void* stream,
                        const uint32_t* go = nullptr, uint32_t go_value = 0, uint32_t* done = nullptr,
-                       const uint64_t* cond_tagged = nullptr, uint32_t cond_tag = 0) {
+                       const uint64_t* cond_tagged = nullptr, uint32_t cond_tag = 0,
+                       uint64_t* actions_tagged = nullptr) {
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
@@ -579,7 +584,7 @@ static int sample_impl(const dppo_dims* d, int precision, const void* packed_bas
     a.sched = sched; a.cond = cond; a.x_T = x_T; a.noise = noise; a.actions = actions; a.chains = chains;
     a.cond_out = cond_out; a.actions_host = actions_host;
     a.go = go; a.go_value = go_value; a.done = done;
-    a.cond_tagged = cond_tagged; a.cond_tag = cond_tag;
+    a.cond_tagged = cond_tagged; a.cond_tag = cond_tag; a.actions_tagged = actions_tagged;
     a.seed = seed; a.call_id = (uint32_t)call_id; a.E = n_envs; a.env_offset = env_offset;
     a.deterministic = deterministic; a.min_std = min_sampling_std; a.randn_clip = randn_clip; a.final_clip = final_clip;
     a.XD = D.XD; a.SD = D.SD; a.TD = D.TD; a.H = D.H; a.K = D.K; a.KF = D.KF; a.IN = D.IN;
@@ -700,16 +705,17 @@ extern "C" int dppo_rollout_enqueue_tagged(const dppo_dims* d, int precision, co
                                            const void* packed_ft, const float* sched, const uint64_t* obs_tagged,
                                            float* cond, int n_envs, uint64_t seed, uint64_t call_id, int env_offset,
                                            int deterministic, float min_sampling_std, float randn_clip,
-                                           float final_clip, float* actions, float* actions_host, float* chains,
+                                           float final_clip, float* actions, uint64_t* actions_tagged, float* chains,
                                            uint32_t tag, uint32_t* done, void* stream) {
-    DPPO_CHECK(obs_tagged && cond && actions && actions_host && done, "dppo_rollout_enqueue_tagged: null pointer argument");
+    DPPO_CHECK(obs_tagged && cond && actions && actions_tagged && done,
+               "dppo_rollout_enqueue_tagged: null pointer argument");
     DPPO_CHECK(tag != 0, "dppo_rollout_enqueue_tagged: tag 0 is the buffer's initial value");
     const uint64_t* obs_dev = (const uint64_t*)mapped_ptr(obs_tagged);
-    float* act_dev = (float*)mapped_ptr(actions_host);
+    uint64_t* act_dev = (uint64_t*)mapped_ptr(actions_tagged);
     uint32_t* done_dev = (uint32_t*)mapped_ptr(done);
     DPPO_CHECK(obs_dev && act_dev && done_dev,
                "dppo_rollout_enqueue_tagged: staging buffers must come from dppo_host_alloc (mapped, coherent)");
     return sample_impl(d, precision, packed_base, packed_ft, sched, nullptr, n_envs, nullptr, nullptr, seed, call_id,
                        env_offset, deterministic, min_sampling_std, randn_clip, final_clip, actions, chains, cond,
-                       act_dev, stream, nullptr, 0, done_dev, obs_dev, tag);
+                       nullptr, stream, nullptr, 0, done_dev, obs_dev, tag, act_dev);
 }

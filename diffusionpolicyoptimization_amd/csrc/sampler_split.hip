@@ -592,7 +592,11 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                     if (a.chains && t <= KF) store_out(a.chains + ((size_t)row * (KF + 1) + (KF - t)) * XD + q, y);
                     if (i == K - 1) {
                         store_out(a.actions + (size_t)row * XD + q, y);
-                        if (a.actions_host) a.actions_host[(size_t)row * XD + q] = y;
+                        if (a.actions_tagged)   // the action is its own flag: one aligned 8-B store
+                            __hip_atomic_store(a.actions_tagged + (size_t)row * XD + q,
+                                               ((uint64_t)a.cond_tag << 32) | __float_as_uint(y), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                        else if (a.actions_host) a.actions_host[(size_t)row * XD + q] = y;
                     }
                 }
             }

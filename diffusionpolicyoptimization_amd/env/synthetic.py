@@ -30,7 +30,8 @@ def _native():
         lib.dppo_env_step_gated.argtypes = [ctypes.c_int] * 7 + [P] * 11 + [P, ctypes.c_uint32, P, ctypes.c_uint32,
                                                                             ctypes.c_double]
         lib.dppo_env_step_gated.restype = ctypes.c_int
-        lib.dppo_env_step_gated_tagged.argtypes = [ctypes.c_int] * 7 + [P] * 11 + [P, ctypes.c_uint32, P,
+        # (..., done, act_tagged, act_tag, obs_tagged, tag, timeout)
+        lib.dppo_env_step_gated_tagged.argtypes = [ctypes.c_int] * 7 + [P] * 11 + [P, P, ctypes.c_uint32, P,
                                                                                    ctypes.c_uint32, ctypes.c_double]
         lib.dppo_env_step_gated_tagged.restype = ctypes.c_int
         lib.dppo_env_publish_tagged.argtypes = [ctypes.c_int64, P, P, ctypes.c_uint32]
@@ -97,7 +98,8 @@ class SyntheticLocomotionVecEnv:
 
     def step(self, actions, obs_out=None, gate=None):
         """actions [E, Ta, Da]; obs_out: optional float32 [E, To, Do] buffer (e.g. pinned staging).
-        gate: (protocol, done_addr, done_target, publish_addr, tag, timeout) of a pipelined rollout
+        gate: ("go", done_addr, done_target, go_addr, go_value, timeout) or
+        ("tagged", done_addr, act_tagged_addr, act_tag, obs_tagged_addr, obs_tag, timeout) of a pipelined rollout
         (ops.RolloutPipe.gate): the native stepper waits for the device's done counter, steps, and
         publishes the observation itself (go counter, or tagged granules) when no env needs a reset;
         self.published tells the caller whether it did."""
@@ -108,6 +110,10 @@ class SyntheticLocomotionVecEnv:
         if self.native is not None:
             a = actions if (isinstance(actions, np.ndarray) and actions.dtype == np.float32
                             and actions.flags.c_contiguous) else np.ascontiguousarray(actions, dtype=np.float32)
+            if gate is not None and gate[0] == "tagged" and a is not actions:
+                # the tagged stepper decodes the device's actions INTO this buffer: it must be the
+                # caller's own [E, Ta, Da] array, not a contiguous copy of a strided view
+                raise ValueError("tagged gated steps need C-contiguous float32 actions")
             ta = a.size // (E * self.action_dim)
             out = obs_out if obs_out is not None else np.empty((E, self.n_obs_steps, self.obs_dim), np.float32)
             if self._static_ptrs is None:

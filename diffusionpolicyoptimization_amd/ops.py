@@ -243,12 +243,14 @@ class RolloutPipe:
             raise ValueError(f"DPPO_ROLLOUT_PROTOCOL must be 'tagged' or 'go', got {self.protocol!r}")
         pt = alloc(8 * E * d.sd)
         self._obs_tag = np.ctypeslib.as_array((ctypes.c_uint64 * (E * d.sd)).from_address(pt))
+        pat = alloc(8 * E * d.xd)   # tagged actions (tagged protocol): the host polls the actions themselves
+        self._act_tag = np.ctypeslib.as_array((ctypes.c_uint64 * (E * d.xd)).from_address(pat))
         self.obs = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_float * (E * d.sd)).from_address(po))).view(E, d.sd)
         self.act = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_float * (E * d.xd)).from_address(pa))).view(E, d.xd)
         ctr = np.ctypeslib.as_array((ctypes.c_uint32 * 64).from_address(pc))
         self._go, self._done = ctr[0:1], ctr[16:17]          # separate 64-B lines
         self._p = dict(obs=ctypes.c_void_p(po), act=ctypes.c_void_p(pa), go=ctypes.c_void_p(pc),
-                       done=ctypes.c_void_p(pc + 64), obs_tag=ctypes.c_void_p(pt))
+                       done=ctypes.c_void_p(pc + 64), obs_tag=ctypes.c_void_p(pt), act_tag=ctypes.c_void_p(pat))
         self._fn = lib.dppo_rollout_enqueue_tagged if self.protocol == "tagged" else lib.dppo_rollout_enqueue
         self._dims = d.c()
         self._keep = (obs_traj, actions, chains_traj)
@@ -285,7 +287,8 @@ class RolloutPipe:
                 ctypes.c_void_p(self._ch0 + i * self._ch_step))
         obs_dev = ctypes.c_void_p(self._obs0 + i * self._obs_step)
         if self.protocol == "tagged":   # step s waits for granules tagged s + 1 (= its publish count)
-            rc = self._fn(*common, p["obs_tag"], obs_dev, *tail, ctypes.c_uint32(self.enqueued), p["done"],
+            tail_t = tail[:-2] + (p["act_tag"],) + tail[-1:]          # tagged actions replace actions_host
+            rc = self._fn(*common, p["obs_tag"], obs_dev, *tail_t, ctypes.c_uint32(self.enqueued), p["done"],
                           self._stream)
         else:
             rc = self._fn(*common, p["obs"], obs_dev, *tail, p["go"], ctypes.c_uint32(self.enqueued), p["done"],
@@ -317,9 +320,12 @@ class RolloutPipe:
         this step's done count itself and, if publish, releases the next launch. Call
         published() after a step that did publish, publish() after one that did not."""
         self.finished += 1
-        dst = self._p["obs_tag"] if self.protocol == "tagged" else self._p["go"]
-        pub = (dst, self.published + 1) if publish else (None, 0)
-        return (self.protocol, self._p["done"], ctypes.c_uint32(self.finished * self.nwg), pub[0],
+        if self.protocol == "tagged":   # the finished launch's actions carry its tag (= finished)
+            pub = (self._p["obs_tag"], self.published + 1) if publish else (None, 0)
+            return ("tagged", self._p["done"], self._p["act_tag"], ctypes.c_uint32(self.finished), pub[0],
+                    ctypes.c_uint32(pub[1]), ctypes.c_double(timeout_s))
+        pub = (self._p["go"], self.published + 1) if publish else (None, 0)
+        return ("go", self._p["done"], ctypes.c_uint32(self.finished * self.nwg), pub[0],
                 ctypes.c_uint32(pub[1]), ctypes.c_double(timeout_s))
 
     def published_by_gate(self):
@@ -330,12 +336,18 @@ class RolloutPipe:
         self.finished += 1
         target = self.finished * self.nwg
         done = self._done
+        tagged = self.protocol == "tagged"
         t0 = None
         while True:
             v = int(done[0])
             if v & 0x80000000:
-                raise _lib.DppoError("rollout step timed out waiting for its observation (go counter)")
-            if v >= target:
+                raise _lib.DppoError("rollout step timed out waiting for its observation")
+            if tagged:   # the launch stores its actions as {tag, bits} granules (no host float copy)
+                x = self._act_tag.copy()
+                if ((x >> np.uint64(32)) == np.uint64(self.finished)).all():
+                    self.act.numpy().reshape(-1).view(np.uint32)[:] = (x & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+                    return
+            elif v >= target:
                 return
             if t0 is None:
                 t0 = time.perf_counter()

@@ -145,13 +145,15 @@ DPPO_API int dppo_rollout_enqueue(const dppo_dims* d, int precision, const void*
  * obs_tagged ([n_envs][To*Do] uint64, from dppo_host_alloc), and the launch polls its envs'
  * granules until every tag equals `tag` (nonzero, unique among the tags the buffer may hold, e.g.
  * the step count). The observation carries its own ready flag: one PCIe round trip instead of a
- * flag poll followed by a read. done / timeout as dppo_rollout_enqueue; cond receives the device
- * copy of the observation. */
+ * flag poll followed by a read. The actions come back the same way: actions_tagged ([n_envs][Ta*Da]
+ * uint64, from dppo_host_alloc) receives {tag, fp32} granules, so the host can poll the actions
+ * themselves instead of waiting for *done (which still counts finished workgroups, and bit 31 still
+ * flags a timeout). cond receives the device copy of the observation. */
 DPPO_API int dppo_rollout_enqueue_tagged(const dppo_dims* d, int precision, const void* packed_base,
                 const void* packed_ft, const float* sched, const uint64_t* obs_tagged, float* cond,
                 int n_envs, uint64_t seed, uint64_t call_id, int env_offset, int deterministic,
                 float min_sampling_std, float randn_clip, float final_clip, float* actions,
-                float* actions_host, float* chains, uint32_t tag, uint32_t* done, void* stream);
+                uint64_t* actions_tagged, float* chains, uint32_t tag, uint32_t* done, void* stream);
 
 /* ---- a10: VPGDiffusion.get_logprobs (diffusion_vpg.py:343-425) + the clip/mean of c_loss
  * (diffusion_ppo.py:50-59) for the old-logprob pass (agent/finetune/train_ppo_diffusion_agent.py:214-229).

@@ -153,8 +153,11 @@ def test_gated_env_step_publishes_only_without_resets():
 
 
 def test_gated_env_step_tagged_publishes_granules():
-    """dppo_env_step_gated_tagged: like the go protocol, but the observation is published as tagged
-    granules {tag << 32 | fp32 bits} (what the sampler polls, dppo_rollout_enqueue_tagged)."""
+    """dppo_env_step_gated_tagged: the stepper polls the launch's actions as tagged granules
+    {tag << 32 | fp32 bits} (decoding them into the actions buffer), steps, and publishes the
+    observation as tagged granules (what the sampler polls, dppo_rollout_enqueue_tagged). A stale
+    action tag with the done counter's timeout bit set fails with -2; with no bit, the host timeout
+    fails with -1."""
     import ctypes
 
     from diffusionpolicyoptimization_amd.env.synthetic import SyntheticLocomotionVecEnv, _native
@@ -173,12 +176,16 @@ def test_gated_env_step_tagged_publishes_granules():
     obs = [np.zeros((E, 1, Do), np.float32) for _ in range(2)]
     rng = np.random.default_rng(1)
     pubs = []
+    act_t = np.zeros(E * 4 * Da, np.uint64)
+    act_p = ctypes.c_void_p(act_t.ctypes.data)
+    a = np.zeros((E, 4, Da), np.float32)
     for i in range(5):
-        a = rng.normal(0, 0.5, (E, 4, Da)).astype(np.float32)
-        ctr[0] = i + 1
-        g = envs[0].step(a, obs_out=obs[0], gate=("tagged", done_p, ctypes.c_uint32(i + 1), tag_p,
+        ref_a = rng.normal(0, 0.5, (E, 4, Da)).astype(np.float32)
+        act_t[:] = (np.uint64(i + 1) << np.uint64(32)) | ref_a.reshape(-1).view(np.uint32).astype(np.uint64)
+        g = envs[0].step(a, obs_out=obs[0], gate=("tagged", done_p, act_p, ctypes.c_uint32(i + 1), tag_p,
                                                   ctypes.c_uint32(i + 2), ctypes.c_double(1.0)))
-        r = envs[1].step(a, obs_out=obs[1])
+        np.testing.assert_array_equal(a, ref_a)
+        r = envs[1].step(ref_a, obs_out=obs[1])
         np.testing.assert_array_equal(obs[0], obs[1])
         np.testing.assert_array_equal(g[1], r[1])
         pubs.append(envs[0].published)
@@ -187,6 +194,13 @@ def test_gated_env_step_tagged_publishes_granules():
             np.testing.assert_array_equal((tagged & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.float32),
                                           obs[0].reshape(-1))
     assert pubs == [True, True, False, True, True]
+    gate = lambda: ("tagged", done_p, act_p, ctypes.c_uint32(7), tag_p, ctypes.c_uint32(8), ctypes.c_double(0.05))
+    ctr[0] = 0x80000000
+    with pytest.raises(RuntimeError, match="observation timed out"):
+        envs[0].step(a, obs_out=obs[0], gate=gate())
+    ctr[0] = 0
+    with pytest.raises(RuntimeError, match="did not finish"):
+        envs[0].step(a, obs_out=obs[0], gate=gate())
 
 
 def test_sampler_stream_bytes_per_geometry():
