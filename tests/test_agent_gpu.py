@@ -203,3 +203,32 @@ def test_split_update_matches_fused(cuda, tmp_path, monkeypatch):
     assert np.median(d) < 1e-6 and d.max() < 5e-3, (float(np.median(d)), float(d.max()))
     for k in ("pg_loss", "v_loss"):
         assert abs(r1[k] - r0[k]) <= 1e-3 * (abs(r0[k]) + 1e-3), (k, r1[k], r0[k])
+
+
+@pytest.mark.parametrize("protocol", ["tagged", "go"])
+def test_pipelined_rollout_unpublished_observation_times_out(cuda, protocol, monkeypatch):
+    """A launch whose observation never comes (the host died or stalled) gives up after its
+    bounded device-side wait (~4 s), flags bit 31 of the done counter and still finishes, so no
+    wave is left spinning; RolloutPipe.wait raises instead of returning stale actions."""
+    import torch
+
+    monkeypatch.setenv("DPPO_ROLLOUT_PROTOCOL", protocol)
+    from diffusionpolicyoptimization_amd import _lib, ops
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
+                      ["model.precision=bf16"])
+    model = instantiate(cfg.model, device=cuda, seed=5)
+    d = model.dims
+    E = 40
+    obs_traj = torch.zeros(1, E, d.sd, device=cuda)
+    chains = torch.zeros(1, E, d.ft_denoising_steps + 1, d.xd, device=cuda)
+    act = torch.empty(E, d.xd, device=cuda)
+    pipe = ops.RolloutPipe(model, obs_traj, act, chains)
+    pipe.begin()
+    pipe.enqueue(0)                      # never published
+    with pytest.raises(_lib.DppoError, match="timed out"):
+        pipe.wait(timeout_s=30.0)
+    pipe.end()
+    torch.cuda.synchronize()             # the launch drained
+    assert int(pipe._done[0]) & 0x80000000
+    pipe.close()
