@@ -64,49 +64,37 @@ def sampler_stream_bytes_per_tile(d, precision):
     return out.value
 
 
-def cpu_baseline(cfg, n_envs, S, bs, seconds=12.0):
-    """The oracle (float64 NumPy restatement) timed on a bounded sample on this host; extrapolated
-    to one iteration of the same workload. kind = "port"."""
-    import numpy as np
-    from threadpoolctl import threadpool_info
+def cpu_baseline(cfg, n_envs, S, bs):
+    """CPU baseline (kind "port"): oracle/cpu_reference.py, an fp32 torch-CPU restatement of the
+    whole iteration (rollout through the synthetic env, value / log-prob passes, reward scaling,
+    GAE, update_epochs x minibatches with autograd + Keras AdamW), timed for ONE FULL iteration of
+    this workload on torch's thread pool (the host's CPU share), plus a 1-thread figure from a
+    bounded sample (the rollout chunks one full minibatch needs, that minibatch, the passes over
+    those chunks) scaled to the iteration. TF-CPU itself cannot be installed (no network)."""
+    import torch
 
-    from oracle import dppo_oracle as O
-    rng = np.random.default_rng(0)
-    Do, Da, Ta, kf = cfg.obs_dim, cfg.action_dim, cfg.horizon_steps, cfg.ft_denoising_steps
-    base = O.init_actor(rng, Do, Da, Ta)
-    ft = {k: v.astype(np.float64) for k, v in base.items()}
-    critic = {k: v.astype(np.float64) for k, v in O.init_critic(rng, Do).items()}
-    sched = O.ddpm_schedule(cfg.denoising_steps)
-    # (1) rollout: sampler calls at E envs until ~40% of the budget
-    t0, steps = time.perf_counter(), 0
-    while time.perf_counter() - t0 < 0.4 * seconds or steps < 2:
-        st = rng.uniform(-1, 1, (n_envs, 1, Do))
-        z = rng.standard_normal((cfg.denoising_steps, n_envs, Ta, Da))
-        O.sample(ft, ft, sched, st, rng.standard_normal((n_envs, Ta, Da)), z, kf)
-        steps += 1
-    t_step = (time.perf_counter() - t0) / steps
-    # (2) one PPO minibatch (forward + gradient) on a row sample, scaled linearly to bs rows
-    rows = 2048
-    t1, mbs = time.perf_counter(), 0
-    while time.perf_counter() - t1 < 0.4 * seconds or mbs < 1:
-        j = rng.integers(0, kf, rows)
-        O.c_loss(ft, critic, sched, rng.uniform(-1, 1, (rows, 1, Do)), rng.normal(0, .5, (rows, Ta, Da)),
-                 rng.normal(0, .5, (rows, Ta, Da)), j, rng.normal(size=rows), None, rng.normal(size=rows),
-                 rng.normal(size=rows), kf)
-        mbs += 1
-    t_mb = (time.perf_counter() - t1) / mbs * (bs / rows)
-    # (3) old-logprob pass (forward only ~ 1/3 of fwd+bwd) over S*E*K' rows + value pass
-    total = S * n_envs * kf
-    n_mb = 5 * max(1, total // bs)
-    t_lp = t_mb / 3.0 * (total / bs)
-    t_iter = S * t_step + n_mb * t_mb + t_lp
-    cores = sum(p.get("num_threads", 1) for p in threadpool_info()) or 1
-    return {"value": n_envs * cfg.act_steps * S / t_iter, "unit": "env-steps/s", "cores": int(cores), "kind": "port",
-            "sample": (f"oracle (float64 NumPy) timed on {steps} sampler calls at {n_envs} envs "
-                       f"({t_step * 1e3:.1f} ms each) and {mbs} PPO minibatches of {rows} rows "
-                       f"({t_mb / (bs / rows):.2f} s each), extrapolated to one iteration: S={S} chunks, "
-                       f"{n_mb} minibatches of {bs} rows, logprob pass over {total} rows; est. {t_iter:.0f} s/iter"),
-            "ppo_updates_per_sec": 1.0 / t_mb}
+    from oracle import cpu_reference as C
+    threads = torch.get_num_threads()
+    kw = dict(obs_dim=cfg.obs_dim, action_dim=cfg.action_dim)
+    upd = int(cfg.train.update_epochs)
+    t_full, br = C.time_iteration(n_envs, S, bs, upd, **kw)
+    n_mb = br["minibatches"]
+    # 1 thread: enough chunks for one full minibatch of bs rows (S*E*K' >= bs) + that minibatch,
+    # scaled to the iteration
+    s1 = min(S, max(10, -(-bs // (n_envs * cfg.ft_denoising_steps))))
+    t1, b1 = C.time_iteration(n_envs, s1, bs, upd, threads=1, max_minibatches=1, **kw)
+    torch.set_num_threads(threads)
+    t1_iter = (b1["rollout_s"] + b1["passes_s"]) * S / s1 + b1["update_s"] / max(1, b1["minibatches"]) * n_mb
+    env_steps = n_envs * cfg.act_steps * S
+    return {"value": env_steps / t_full, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "threads": threads, "physical_cores": C.physical_cores(), "cpu_model": C.cpu_model(),
+            "value_1thread": env_steps / t1_iter,
+            "ppo_updates_per_sec": n_mb / br["update_s"] if br["update_s"] > 0 else None,
+            "seconds_per_iter": t_full, "breakdown_s": {k: br[k] for k in ("rollout_s", "passes_s", "update_s")},
+            "sample": (f"oracle/cpu_reference.py (fp32 torch-CPU, autograd) timed on ONE full iteration: {n_envs} "
+                       f"envs x {S} chunks, K={cfg.denoising_steps}, {n_mb} minibatches of {bs} rows, "
+                       f"{threads} threads, {t_full:.1f} s; value_1thread from {s1} chunks + 1 full minibatch "
+                       f"on 1 thread scaled to the iteration ({t1_iter:.0f} s/iter)")}
 
 
 def sampler_burst_ms(agent, n=30):
@@ -141,7 +129,6 @@ def main():
     ap.add_argument("--n-steps", type=int, default=None, help="override S (chunks per rollout)")
     ap.add_argument("--precision", default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -239,7 +226,7 @@ def main():
         "ppo_minibatch_avg_ms": upd_ms,
     }
     if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, agent.n_envs, cfg.train.n_steps, cfg.train.batch_size, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(cfg, agent.n_envs, cfg.train.n_steps, cfg.train.batch_size)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -105,13 +105,18 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
     # ------------------------------------------------------------------ rollout (agent :58-141)
     def rollout(self, eval_mode):
         S, E = self.n_steps, self.n_envs
+        # quirk 4: the reference assigns last_itr_eval = eval_mode right before it tests it (agent
+        # :70-74), so its "right after eval mode" clause never fires: envs are reset only when
+        # reset_at_iteration is set or on eval iterations, and the train iteration after an eval
+        # continues from the eval's env state with firsts[0] = done_venv. (The first iteration has
+        # no env state yet; the reference's itr 0 is always an eval, :68.)
+        self.last_itr_eval = eval_mode
         if self.reset_at_iteration or eval_mode or self.last_itr_eval or self.prev_obs_venv is None:
             obs = self.reset_env_all()
             self.obs_pin.numpy()[:] = obs["state"]
             self.firsts[0] = 1
         else:
             self.firsts[0] = self.done_venv  # envs that finished were already reset in-wrapper
-        self.last_itr_eval = eval_mode
         obs_np = self.obs_pin.numpy()
         act_view = self.act_pin.numpy().reshape(E, self.horizon_steps, self.action_dim)[:, :self.act_steps]
         stream = torch.cuda.current_stream(self.device)
@@ -222,14 +227,19 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         # The target_kl check (:366-370) reads each minibatch's approx_kl on the host. It runs one
         # minibatch behind: minibatch i's gradients are enqueued before the host waits for i-1's
         # metrics (an event right after i-1's kernels, the metrics copied to pinned memory), so the
-        # GPU never idles on that read. Only the AdamW step of i waits for the verdict: a stop
-        # leaves i's gradients unapplied, exactly as the reference never computes them.
+        # GPU never idles on that read. Only the AdamW step of i waits for the verdict. In the
+        # reference the minibatch that exceeds target_kl IS applied and its `break` leaves only the
+        # batch loop of that epoch (`if flag_break: break` sits inside the batch loop and is never
+        # reached; flag_break is reset per epoch, :284-286,366-370), so the next epoch still runs.
+        # Here: a stop by minibatch i-1 of the SAME epoch drops i's gradients (the reference never
+        # computes them) and ends the epoch; a stop by the previous epoch's last minibatch ended an
+        # epoch that was over anyway, so i (the new epoch's first) is applied.
         if not hasattr(self, "_met_pin"):
             self._met_pin = [torch.zeros(5, dtype=torch.float64).pin_memory() for _ in range(2)]
         pending = None
 
         def finish(p):
-            slot, ev, grows = p
+            slot, ev, grows, _ = p
             ev.synchronize()
             met = self._met_pin[slot].numpy() / grows
             self.timing["n_updates"] += 1
@@ -263,7 +273,6 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             side.wait_stream(stream)
             na = m.n_actor
         k = 0
-        stop = False
         for update_epoch in range(self.update_epochs):
             for batch in range(num_batch):
                 start = batch * rows_local_full
@@ -300,7 +309,9 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 ev_m.record(stream)
                 if pending is not None:
                     info, stop = finish(pending)
-                    if stop:                                                   # :366-370
+                    same_epoch = pending[3] == update_epoch
+                    pending = None
+                    if stop and same_epoch:                                    # :366-368
                         break
                 if self.itr >= self.n_critic_warmup_itr:
                     if split:
@@ -318,11 +329,9 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     ev1 = torch.cuda.Event(enable_timing=True)
                     ev1.record(stream)
                     self.update_events.append((ev0, ev1))
-                pending = (slot, ev_m, global_rows)
+                pending = (slot, ev_m, global_rows, update_epoch)
                 k += 1
-            if stop:
-                break
-        if pending is not None and not stop:
+        if pending is not None:
             info, _ = finish(pending)
         if split:
             stream.wait_stream(side)

@@ -89,3 +89,4 @@ int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s);
 bool sample_split_supported(int precision, int H, int XD, int ks_in, int E, int K);
 // workgroups (CUs) per 16-env group of the split sampler
 int split_sampler_members();
+int sampler_device_cus();   // CUs of the current device (0 if unknown)

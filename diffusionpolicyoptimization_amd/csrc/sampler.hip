@@ -608,6 +608,24 @@ extern "C" int dppo_sampler_layout(const dppo_dims* d, int precision, int n_envs
     return DPPO_OK;
 }
 
+// The split kernel's members wait on each other inside a launch, so every active workgroup of a
+// launch must be resident at once; a second launch in flight (the pipelined rollout's next step)
+// must not take the CUs the first one still needs. One workgroup per CU (register budget), G * P
+// active workgroups per launch. The streaming kernel has no inter-workgroup wait.
+extern "C" int dppo_sampler_max_in_flight(const dppo_dims* d, int precision, int n_envs, int* launches) {
+    int members = 0;
+    int rc = dppo_sampler_layout(d, precision, n_envs, &members);
+    if (rc) return rc;
+    DPPO_CHECK(launches, "dppo_sampler_max_in_flight: null output");
+    if (members == 0 || n_envs <= 0) {
+        *launches = 8;
+        return DPPO_OK;
+    }
+    const int active = dppo_cdiv(n_envs, 16) * members, cus = sampler_device_cus();
+    *launches = cus > 0 ? (cus / active > 0 ? cus / active : 1) : 1;
+    return DPPO_OK;
+}
+
 extern "C" int dppo_sample(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
                            const float* sched, const float* cond, int n_envs, const float* x_T, const float* noise,
                            uint64_t seed, uint64_t call_id, int env_offset, int deterministic,

@@ -15,11 +15,21 @@
 // the same fp32 DDPM epilogue on the same sum (fixed member order: bit-identical x on all eight).
 //
 // The exchange is in-launch (MI355X_MICROARCH.md "handoff-1to1"/R2 granules): each member stores
-// its partials as 8-byte {tag, value} granules with write-through agent-scope stores; wave 0 of
-// every member sweeps the group's granules with agent-scope loads until every tag matches. Tags
-// carry a per-launch sequence number and the step index, so nothing is zeroed between launches;
-// slots alternate by step parity (a member can be at most one step ahead of a peer). The wait is
+// its partials as 8-byte {tag, value} granules and every wave sweeps its slice of the group's
+// granules with agent-scope (sc1, L1-bypassing) loads until every tag matches. Tags carry a
+// per-launch sequence number and the step index, so nothing is zeroed between launches; slots
+// alternate by step parity (a member can be at most one step ahead of a peer). The wait is
 // bounded (100 ms): a launch that times out writes NaN actions and flags bit 31 of *done.
+// Store flavour, chosen per group at run time (never assumed from blockIdx):
+//   * every member reads its XCD from HW_REG_XCC_ID and announces it (sc1 granule) in the
+//     prologue; the members sweep the announcements and agree on the mode;
+//   * all on one XCD -> "L2-local": workgroup-scope (sc0) granule stores, which keep the line in
+//     that XCD's L2, where the peers' sc1 loads find it (tools/xchg_probe2.hip: 1.55 vs 2.21 us
+//     per exchange step; sc0 across XCDs never becomes visible: the probe's spread row times out).
+//     These granules live in a region owned by that XCD alone ([xcc][slot][G][P][NV], fixed
+//     stride), so no other XCD's L2 ever holds a copy of those lines;
+//   * otherwise -> write-through agent-scope (sc1) stores into the shared region, the
+//     placement-independent form.
 //
 // Layout per step (member c, 8 waves; all GEMMs computed TRANSPOSED, W^T x^T, so an MFMA result
 // lane holds 4 consecutive features of one env):
@@ -33,6 +43,7 @@
 // Block -> (group, member): members of a group share blockIdx % 8 (one XCD under the observed
 // round-robin placement: a speed choice only; correctness does not depend on placement).
 #include <mutex>
+#include <stdlib.h>
 #include <string.h>
 #include "dppo_common.cuh"
 #include "dppo_internal.h"
@@ -56,6 +67,16 @@ __device__ unsigned long long dppo_split_cycles[16 + 64 * 8];
     } while (0)
 #define XPHASE_START unsigned long long t_phase_ = __builtin_readcyclecounter(); int t_step_ = 0
 #define XSTEP(i) t_step_ = (i)
+// groups that ran the exchange L2-local ([1]) or shared ([0]), summed over launches
+__device__ unsigned dppo_split_xmode_groups[2];
+extern "C" DPPO_API int dppo_debug_split_xmode(unsigned* out, int reset) {
+    DPPO_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dppo_split_xmode_groups), sizeof(unsigned) * 2));
+    if (reset) {
+        unsigned z[2] = {};
+        DPPO_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dppo_split_xmode_groups), z, sizeof(z)));
+    }
+    return DPPO_OK;
+}
 extern "C" DPPO_API int dppo_debug_split_cycles(unsigned long long* out, int reset) {
     DPPO_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dppo_split_cycles), sizeof(unsigned long long) * (16 + 64 * 8)));
     if (reset) {
@@ -107,12 +128,22 @@ constexpr int SPLIT_H = 512;       // actor hidden width the split layout is bui
 constexpr int XMAX_NV = 16 * 32;   // granules per member per step at XD <= 32
 constexpr int XMAX_G = 32;         // groups per launch (512 envs): 8*P*G/8 = 256 workgroups
 
+constexpr size_t XREGION = (size_t)2 * XMAX_G * SPLIT_P * XMAX_NV;   // granules of one exchange region
+
 struct SplitArgs {
     SampleArgs a;
-    uint64_t* xbuf;   // granules [2 slots][G][P][NV]
+    uint64_t* xbuf;   // shared (sc1) region [2 slots][G][P][NV], then 8 XCD-owned (sc0) regions of
+                      // XREGION granules each, then the XCD announcements [XMAX_G][P]
     uint32_t seq;     // launch sequence number (tag high bits)
     int G;            // 16-env groups
+    int force_shared; // DPPO_SPLIT_XCHG=shared: always the placement-independent sc1 form (A/B knob)
 };
+
+__device__ inline int xcc_id() {
+    int x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x;
+}
 
 // one k-slot -> feature map of the transposed-result lane order: slot (j, e) of a 32-wide
 // k-step holds feature e < 4 ? 4j + e : 16 + 4j + (e - 4)
@@ -167,7 +198,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
     AT* u1 = (AT*)(smem + o); o += dppo_align16(2 * 16 * ldh);
     float* p1 = (float*)(smem + o); o += dppo_align16(4 * KP * 16 * ldp);
     float* part = (float*)(smem + o); o += dppo_align16(4 * SW * NV);      // [wave][16 x XD]
-    int* xfail = (int*)(smem + o); o += 16;
+    int* xfail = (int*)(smem + o); o += 16;                // [0] exchange failure, [1] exchange mode
     float* xs = (float*)(smem + o); o += dppo_align16(4 * 16 * XD);
     float* st = (float*)(smem + o); o += dppo_align16(4 * 16 * SD);
     float* temb = (float*)(smem + o); o += dppo_align16(4 * K * TD);
@@ -231,6 +262,12 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
 
+    // announce this member's XCD (sc1 granule, tag = seq << 6: step tags are seq << 6 | i + 1)
+    uint64_t* const xann = sa.xbuf + 9 * XREGION + (size_t)g * P;
+    const uint32_t ann_tag = sa.seq << 6;
+    if (tid == 0)
+        __hip_atomic_store(xann + c, ((uint64_t)ann_tag << 32) | (uint32_t)xcc_id(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     const int ft0 = __builtin_amdgcn_readfirstlane(K - 1 < KF ? 1 : 0);
     load_in(ft0); load_l1(ft0); load_l2(ft0); load_out(ft0);
     int cur = ft0;
@@ -276,6 +313,24 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0): the resident set has landed
     permute_out();
+    // the group's exchange mode from the members' announcements (bounded like the exchange): every
+    // member sees the same P words, so all agree; a timeout selects the placement-independent form
+    if (wave == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
+        uint64_t v = ((uint64_t)ann_tag << 32);
+        bool ok = false;
+        for (;;) {
+            if (lane < P) v = __hip_atomic_load(xann + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__all(lane >= P || (uint32_t)(v >> 32) == ann_tag)) { ok = true; break; }
+            if (__builtin_amdgcn_s_memrealtime() > t_end) break;
+        }
+        const int x0 = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        const bool one_xcd = ok && !sa.force_shared && __all(lane >= P || (int)(uint32_t)v == x0);
+        if (lane == 0) xfail[1] = one_xcd ? 1 + x0 : 0;
+#ifdef DPPO_SAMPLER_TIMING
+        if (lane == 0 && c == 0) atomicAdd(&dppo_split_xmode_groups[one_xcd ? 1 : 0], 1u);
+#endif
+    }
     // pre-enqueued rollout step: wait for the host's observation (bounded, as sampler.hip)
     // everything that does not need the observation is done before its wait: a0's x / temb /
     // padding columns and the exchange-failure flag (xs, x_T, comes from the noise loop above)
@@ -331,6 +386,9 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
     }
     __syncthreads();
     const int env = lane & 15, jq = lane >> 4;
+    // exchange region of this group: its XCD's own (L2-local, sc0 stores) or the shared one (sc1)
+    const int xmode = __builtin_amdgcn_readfirstlane(xfail[1]);
+    uint64_t* const xregion = sa.xbuf + (size_t)xmode * XREGION;
     XPHASE(0);
     for (int i = 0; i < K; ++i) {
         XSTEP(i);
@@ -480,14 +538,17 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
         //      (diffusion_vpg.py:198-243, 301-320) for them. No workgroup barrier in between.
         {
             const uint32_t tag = (sa.seq << 6) | (uint32_t)(i + 1);
-            uint64_t* xb = sa.xbuf + ((size_t)((i & 1) * sa.G + g) * P) * NV;
+            uint64_t* xb = xregion + ((size_t)((i & 1) * sa.G + g) * P) * NV;
             const int vw = wave * NVW;
             if (lane < NVW) {
                 float sum = part[vw + lane];
 #pragma unroll
                 for (int w = 1; w < SW; ++w) sum += part[w * NV + vw + lane];
-                __hip_atomic_store(xb + (size_t)c * NV + vw + lane, ((uint64_t)tag << 32) | __float_as_uint(sum),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t gr = ((uint64_t)tag << 32) | __float_as_uint(sum);
+                if (xmode)   // one XCD: the line stays in its L2, where the peers' sc1 loads read it
+                    __hip_atomic_store(xb + (size_t)c * NV + vw + lane, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    __hip_atomic_store(xb + (size_t)c * NV + vw + lane, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             XPHASE(15);
             // the next step's time embedding into a0 while the members arrive (a0 was last read by
@@ -635,6 +696,11 @@ size_t split_lds_bytes(int XD, int SD, int TD, int K, int KSI, int NO) {
     return o;
 }
 
+__global__ void xchg_zero_kernel(uint64_t* p, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        __hip_atomic_store(p + i, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // exchange buffers: one per stream (launches on one stream are ordered, so they can share one)
 struct XchgBuf {
     hipStream_t stream;
@@ -659,9 +725,11 @@ int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq) {
         }
     if (g_nxb == 16) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler: more than 16 streams");
     XchgBuf& x = g_xb[g_nxb];
-    const size_t bytes = sizeof(uint64_t) * 2 * XMAX_G * SPLIT_P * XMAX_NV;
-    DPPO_HIP(hipMalloc((void**)&x.buf, bytes));
-    DPPO_HIP(hipMemset(x.buf, 0, bytes));
+    const size_t n = 9 * XREGION + (size_t)XMAX_G * SPLIT_P;
+    DPPO_HIP(hipMalloc((void**)&x.buf, sizeof(uint64_t) * n));
+    // zeroed with write-through stores: no XCD's L2 is left holding a dirty copy of any line
+    hipLaunchKernelGGL(xchg_zero_kernel, dim3(1024), dim3(256), 0, s, x.buf, n);
+    DPPO_HIP(hipGetLastError());
     x.stream = s; x.device = dev; x.seq = 1;
     ++g_nxb;
     *buf = x.buf;
@@ -705,11 +773,18 @@ bool sample_split_supported(int precision, int H, int XD, int ks_in, int E, int 
 
 int split_sampler_members() { return SPLIT_P; }
 
+int sampler_device_cus() { return device_cus(); }
+
 int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s) {
     if (!sample_split_supported(precision, a.H, a.XD, a.L.ks_in, a.E, a.K)) return DPPO_EUNSUPPORTED;
     SplitArgs sa;
     sa.a = a;
     sa.G = dppo_cdiv(a.E, 16);
+    static const int force_shared = [] {
+        const char* e = getenv("DPPO_SPLIT_XCHG");
+        return e && !strcmp(e, "shared") ? 1 : 0;
+    }();
+    sa.force_shared = force_shared;
     int rc = xchg_for(s, &sa.xbuf, &sa.seq);
     if (rc) return rc;
     const bool inj = a.noise != nullptr;

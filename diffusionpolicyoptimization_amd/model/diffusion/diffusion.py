@@ -81,7 +81,9 @@ class DiffusionModel:
                                       denoising_steps=self.denoising_steps, ft_denoising_steps=1, time_stride=1)
         self.pre_spec = ops.actor_param_spec(self.pre_dims)
         path = self.network_path
-        if path is not None and str(path).endswith(".npz") and os.path.exists(str(path)):
+        if path is not None and not os.path.exists(str(path)):
+            raise FileNotFoundError(f"network_path {str(path)!r} does not exist (null = seeded synthetic weights)")
+        if path is not None and str(path).endswith(".npz"):
             with np.load(str(path), allow_pickle=False) as f:
                 pref = "network." if any(k.startswith("network.") for k in f.files) else ""
                 p = {n: np.asarray(f[pref + n], np.float32).reshape(s) for n, s in self.pre_spec}

@@ -111,11 +111,16 @@ class VPGDiffusion(DiffusionModel):
             ops.pack_critic(self.dims, self.critic_params, self.precision, out=self.packed_critic)
 
     def _load_actor(self, path, rng):
-        if path is None or not os.path.exists(str(path)):
-            if path is not None:
-                log.warning("base policy %s not found: using a seeded glorot_uniform actor (synthetic weights)", path)
+        # network_path: null is the only way to ask for synthetic weights; a path that does not
+        # exist fails here as the reference's load_weights does (diffusion_vpg.py:91-97), instead of
+        # silently fine-tuning a random actor
+        if path is None:
+            log.info("base policy: seeded glorot_uniform actor (synthetic weights, network_path: null)")
             return self.network.init_params(rng)
         path = str(path)
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"base policy checkpoint {path!r} does not exist (set network_path / "
+                                    "base_policy_path to null for seeded synthetic weights)")
         if path.endswith(".npz"):
             with np.load(path, allow_pickle=False) as f:
                 keys = [k for k in f.files]

@@ -160,6 +160,13 @@ def sampler_layout(d: ModelDims, precision, n_envs):
     return m.value
 
 
+def sampler_max_in_flight(d: ModelDims, precision, n_envs):
+    """Sampler launches of n_envs envs that may be in flight together (include/dppo.h)."""
+    m = ctypes.c_int()
+    _lib.call("dppo_sampler_max_in_flight", ctypes.byref(d.c()), _prec(precision), int(n_envs), ctypes.byref(m))
+    return m.value
+
+
 class SampleStepper:
     """dppo_sample_step with every argument but the step index, call counter and mode bound once
     (the rollout's buffers never move), so a rollout step costs one ctypes call."""
@@ -184,8 +191,10 @@ class SampleStepper:
         # consecutive launches alternate over DPPO_ROLLOUT_STREAMS streams (default 2): launch t+1 is
         # dispatched, and runs its observation-independent prologue (resident weights, noise), while
         # launch t still runs, instead of after it retires. begin() / end() order them against the
-        # caller's stream around a rollout.
+        # caller's stream around a rollout. Two launches in flight must both fit on the device (the
+        # split sampler's members wait for each other inside a launch): above that size, one stream.
         nst = max(1, int(os.environ.get("DPPO_ROLLOUT_STREAMS", "2")))
+        nst = min(nst, sampler_max_in_flight(d, model.precision, E))
         dev = obs_traj.device
         self._tstreams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(nst - 1)]
         self._handles = [ctypes.c_void_p(st.cuda_stream) for st in self._tstreams]
@@ -260,8 +269,10 @@ class RolloutPipe:
         # consecutive launches alternate over DPPO_ROLLOUT_STREAMS streams (default 2): launch t+1 is
         # dispatched, and runs its observation-independent prologue (resident weights, noise), while
         # launch t still runs, instead of after it retires. begin() / end() order them against the
-        # caller's stream around a rollout.
+        # caller's stream around a rollout. Two launches in flight must both fit on the device (the
+        # split sampler's members wait for each other inside a launch): above that size, one stream.
         nst = max(1, int(os.environ.get("DPPO_ROLLOUT_STREAMS", "2")))
+        nst = min(nst, sampler_max_in_flight(d, model.precision, E))
         dev = obs_traj.device
         self._tstreams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(nst - 1)]
         self._handles = [ctypes.c_void_p(st.cuda_stream) for st in self._tstreams]

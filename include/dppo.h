@@ -116,6 +116,12 @@ DPPO_API int dppo_sampler_stream_bytes(const dppo_dims* d, int precision, int64_
  * (the one allocation outside a caller workspace). */
 DPPO_API int dppo_sampler_layout(const dppo_dims* d, int precision, int n_envs, int* members);
 
+/* How many dppo_sample / dppo_rollout_enqueue* launches of n_envs envs may be in flight at once on
+ * the current device (on different streams) without one launch taking CUs another's split-kernel
+ * members wait for: floor(CUs / active workgroups) for the split kernel (>= 1), 8 for the
+ * weight-streaming kernel. The pipelined rollout (ops.RolloutPipe) uses at most this many streams. */
+DPPO_API int dppo_sampler_max_in_flight(const dppo_dims* d, int precision, int n_envs, int* launches);
+
 /* One rollout step (agent/finetune/train_ppo_diffusion_agent.py:106-122) in one call:
  * hipMemcpyAsync(cond <- cond_host [host, pinned]), dppo_sample with the Philox noise, hipMemcpyAsync
  * (actions_host [host, pinned] <- actions), then hipStreamSynchronize when synchronize != 0. */

@@ -28,21 +28,62 @@ def test_agent_iterations(cuda, precision, tmp_path):
     assert os.path.exists(os.path.join(tmp_path, "checkpoint", "state_0.npz"))
 
 
-def test_target_kl_stops_without_applying_the_next_minibatch(cuda, tmp_path):
-    """The target_kl early stop (agent :366-370) with the check one minibatch behind: at
-    target_kl = 0 the first minibatch whose approx_kl > 0 ends the update (it WAS applied); the
-    gradients already computed for the next minibatch are dropped. So every counted minibatch
-    had exactly one AdamW step, and the update stopped early."""
+def test_target_kl_stops_each_epoch_like_the_reference(cuda, tmp_path):
+    """The target_kl early stop (agent :366-370): the minibatch whose approx_kl exceeds target_kl
+    IS applied and its `break` leaves only that epoch's batch loop (the outer `if flag_break:
+    break` is never reached and flag_break is reset per epoch, :284-286), so every epoch still
+    applies its first minibatch. The check runs one minibatch behind here; a stop carried over from
+    the previous epoch's last minibatch must not drop the next epoch's first one. With
+    target_kl = -1 every approx_kl (>= 0) stops: exactly one AdamW step per epoch."""
     from diffusionpolicyoptimization_amd.util.config import get_class, load_config
     cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
                       ["model.precision=fp32", "train.n_steps=20", "train.batch_size=200", "train.n_train_itr=2",
-                       "train.val_freq=100", "train.target_kl=0.0", f"logdir={tmp_path}"])
+                       "train.val_freq=100", "train.target_kl=-1.0", f"logdir={tmp_path}"])
     a = get_class(cfg._target_)(cfg)
     a.run()
-    n = a.timing["n_updates"]
-    assert 1 <= n < 5 * ((20 * 4 * 10) // 200), n
-    assert a.actor_optimizer.iterations == n
+    assert a.timing["n_updates"] == a.update_epochs, a.timing["n_updates"]
+    assert a.actor_optimizer.iterations == a.update_epochs
     assert np.isfinite(a.model.train_params.cpu().numpy()).all()
+    # num_batch = 1: the stop (by the single minibatch of each epoch) is always carried into the
+    # next epoch, which must still apply its minibatch
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
+                      ["model.precision=fp32", "train.n_steps=20", "train.batch_size=800", "train.n_train_itr=2",
+                       "train.val_freq=100", "train.target_kl=-1.0", f"logdir={tmp_path}/b"])
+    a = get_class(cfg._target_)(cfg)
+    a.run()
+    assert a.timing["n_updates"] == a.update_epochs, a.timing["n_updates"]
+
+
+def test_envs_reset_only_on_eval_iterations(cuda, tmp_path):
+    """the reference assigns last_itr_eval = eval_mode just before testing it
+    (agent :70-74), so with reset_at_iteration False the envs are reset only on eval iterations:
+    the train iteration right after an eval continues from the eval's env state, with
+    firsts[0] = the eval's last done flags."""
+    from diffusionpolicyoptimization_amd.util.config import get_class, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
+                      ["model.precision=fp32", "train.n_steps=20", "train.batch_size=200", "train.n_train_itr=4",
+                       "train.val_freq=3", "env.reset_at_iteration=false", "env.max_episode_steps=44",
+                       f"logdir={tmp_path}"])
+    a = get_class(cfg._target_)(cfg)
+    resets = []
+    orig = a.reset_env_all
+
+    def counting(*args, **kw):
+        resets.append(a.itr)
+        return orig(*args, **kw)
+    a.reset_env_all = counting
+    firsts0, done_before = [], []
+    for _ in range(4):
+        done_before.append(a.done_venv.copy())
+        a.iteration()
+        firsts0.append(a.firsts[0].copy())
+    assert [r["eval"] for r in a.run_results] == [True, False, False, True]
+    assert resets == [0, 3], resets
+    # itr 1 and 2 continue: firsts[0] = the previous iteration's final done flags (episodes of
+    # 11 chunks end inside a 20-step rollout, so some envs are mid-episode and some just reset)
+    for i in (1, 2):
+        np.testing.assert_array_equal(firsts0[i], done_before[i].astype(np.float64))
+    np.testing.assert_array_equal(firsts0[3], np.ones(a.n_envs))
 
 
 def test_bound_rollout_step_matches_model_call(cuda):
@@ -79,11 +120,14 @@ def test_bound_rollout_step_matches_model_call(cuda):
         step(S)
 
 
-@pytest.mark.parametrize("protocol,precision", [("tagged", "bf16"), ("go", "bf16"), ("tagged", "fp32")])
-def test_pipelined_rollout_matches_model_call(cuda, protocol, precision, monkeypatch):
+@pytest.mark.parametrize("protocol,precision,E", [("tagged", "bf16", 40), ("go", "bf16", 40), ("tagged", "fp32", 40),
+                                                  ("tagged", "bf16", 512)])
+def test_pipelined_rollout_matches_model_call(cuda, protocol, precision, E, monkeypatch):
     """Pre-enqueued launches fed by the host == model(...), for both observation protocols:
     dppo_rollout_enqueue_tagged (the launch polls tagged observation granules) and
-    dppo_rollout_enqueue (a go counter, then the float buffer)."""
+    dppo_rollout_enqueue (a go counter, then the float buffer). At 512 envs the split sampler's
+    256 active workgroups fill the device, so the pipe must keep ONE launch in flight (two would
+    take CUs each other's members wait for): the co-residency guard of ops.RolloutPipe."""
     import torch
 
     monkeypatch.setenv("DPPO_ROLLOUT_PROTOCOL", protocol)
@@ -93,12 +137,16 @@ def test_pipelined_rollout_matches_model_call(cuda, protocol, precision, monkeyp
                       [f"model.precision={precision}"])
     model = instantiate(cfg.model, device=cuda, seed=5)
     d = model.dims
-    S, E = 4, 40
+    S = 4
     obs_traj = torch.zeros(S, E, d.sd, device=cuda)
     chains = torch.zeros(S, E, d.ft_denoising_steps + 1, d.xd, device=cuda)
     act = torch.empty(E, d.xd, device=cuda)
     pipe = ops.RolloutPipe(model, obs_traj, act, chains)
     assert pipe.protocol == protocol
+    members = ops.sampler_layout(d, precision, E)
+    if members:
+        cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+        assert len(pipe._tstreams) == min(2, max(1, cus // (members * ((E + 15) // 16))))
     rng = np.random.default_rng(2)
     obs = [rng.uniform(-1, 1, (E, d.sd)).astype(np.float32) for _ in range(S)]
     cid0 = model._call_id

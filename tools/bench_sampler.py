@@ -73,6 +73,13 @@ def main():
         for i, n in zip(range(11, 16), ["in_mm", "l1_mm", "l2_mm", "out_mm", "publish"]):
             phases[n] = round(buf[i] / wgs / d.denoising_steps)
         phases["wg0_steps"] = [[int(buf[16 + 8 * i + k]) for k in range(1, 7)] for i in range(d.denoising_steps)]
+        if hasattr(lib, "dppo_debug_split_xmode"):
+            xm = (ctypes.c_uint * 2)()
+            lib.dppo_debug_split_xmode(xm, 1)
+            m(cond)
+            torch.cuda.synchronize()
+            lib.dppo_debug_split_xmode(xm, 1)
+            phases["groups_shared_l2local"] = [int(xm[0]), int(xm[1])]
     print(json.dumps({"tag": args.tag, "envs": args.envs, "precision": args.precision, "ms_per_launch": ms,
                       "tflops": flops / (ms * 1e-3) / 1e12, "cycles_per_step": phases}), flush=True)
 

@@ -4,8 +4,9 @@
 set -o pipefail
 tag=${1:-chk}
 cd $GRAFT_REPO_ROOT
+export DPPO_PARITY_LOG=$GRAFT_REPO_ROOT/gpurun_out/parity_$tag.jsonl
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_$tag.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/gpu_tests_$tag.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_$tag.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/gpu_tests_$tag.log; exit 1; }
 tail -3 gpurun_out/gpu_tests_$tag.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_$tag.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench_$tag.log; exit 1; }
 tail -1 gpurun_out/bench_$tag.log
