@@ -210,7 +210,11 @@ def main():
                                 f"steps (K'={d.ft_denoising_steps}), {cfg.train.update_epochs} PPO epochs x "
                                 f"minibatch {cfg.train.batch_size}, {prec} denoiser, synthetic linear env"),
                    "global_envs": agent.n_envs_global, "chunks_per_rollout": cfg.train.n_steps,
-                   "parallelism": f"dp{world} (env shards + RCCL grad all-reduce)" if world > 1 else "single GPU"},
+                   "parallelism": f"dp{world} (env shards + RCCL grad all-reduce)" if world > 1 else "single GPU",
+                   "batch_semantics": (f"per-rank minibatch {cfg.train.batch_size} (global {cfg.train.batch_size * world}, "
+                                       "train.dp_scale_batch=true)" if agent.dp_scale_batch and world > 1 else
+                                       f"global minibatch {cfg.train.batch_size} rows = the reference's "
+                                       f"({cfg.train.batch_size // world} per rank)")},
         "ppo_updates_per_sec": n_updates / elapsed,
         "rollout_env_steps_per_sec": env_steps / t_roll if t_roll > 0 else None,
         "rollout_s_per_iter": t_roll / args.steps, "update_s_per_iter": t_upd / args.steps,

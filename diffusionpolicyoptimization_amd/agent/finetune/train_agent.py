@@ -68,7 +68,9 @@ class TrainAgent:
         self.save_full_observations = cfg.env.get("save_full_observations", False)
         self.furniture_sparse_reward = False
         self.batch_size = int(cfg.train.batch_size)
-        self.dp_scale_batch = bool(cfg.train.get("dp_scale_batch", True))
+        # data parallel: false (default) = the reference's PPO, global minibatch = batch_size rows
+        # (batch_size / world per rank); true = batch_size rows PER RANK (a batch_size x world PPO)
+        self.dp_scale_batch = bool(cfg.train.get("dp_scale_batch", False))
 
         self.model = instantiate(cfg.model, device=str(self.device), seed=self.seed)
         self.model.set_rng(self.seed, env_offset=self.env_offset)
@@ -103,16 +105,22 @@ class TrainAgent:
     def run(self):
         pass
 
+    def _ckpt_path(self, itr):
+        # train_agent.py:127-142: state_{itr}.weights.h5 (Keras-3 layout, util/keras_weights.py);
+        # train.checkpoint_format = npz keeps the .npz form
+        ext = ".npz" if self.cfg.train.get("checkpoint_format", "h5") == "npz" else ".weights.h5"
+        return os.path.join(self.checkpoint_dir, f"state_{itr}{ext}")
+
     def save_model(self):
-        """train_agent.py:127-133; .npz instead of Keras .weights.h5 (h5py absent)."""
+        """train_agent.py:127-133."""
         if self.rank != 0:
             return
-        path = os.path.join(self.checkpoint_dir, f"state_{self.itr}.npz")
+        path = self._ckpt_path(self.itr)
         self.model.save_weights(path)
         log.info("Saved model to %s", path)
 
     def load(self, itr):
-        path = os.path.join(self.checkpoint_dir, f"state_{itr}.npz")
+        path = self._ckpt_path(itr)
         self.model.load_weights(path)
         log.info("Loaded model from %s", path)
 

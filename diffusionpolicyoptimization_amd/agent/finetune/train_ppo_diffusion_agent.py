@@ -61,6 +61,9 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         self.timing = {"rollout_s": 0.0, "update_s": 0.0, "n_updates": 0, "env_steps": 0, "iters": 0}
         self.sampler_events = None    # optional list of (start, end) torch.cuda.Event pairs
         self.update_events = None
+        # test hook: called as minibatch_hook(epoch, batch, start, rows) after a minibatch's
+        # gradients (all-reduced under data parallelism) are in self.model.grads
+        self.minibatch_hook = None
         self._alloc_buffers()
         self.done_venv = np.zeros(self.n_envs, dtype=bool)
         self.last_itr_eval = False
@@ -214,11 +217,12 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
 
         total_local = N * kf
         total_global = total_local * self.world_size
-        # Data parallel (SURVEY §8(e), weak scaling): by default every rank runs the single-GPU
-        # minibatch of batch_size rows from its own shard and the gradients are averaged, i.e. the
-        # reference run with batch_size x world over world x n_envs envs (train.dp_scale_batch);
-        # with dp_scale_batch = false the global minibatch stays batch_size (batch_size / world
-        # rows per rank, world x more minibatches).
+        # Data parallel: by default the global minibatch is the reference's
+        # batch_size rows, batch_size / world drawn by each rank from its own shard (each rank's
+        # keyed permutation of its rows), so the update is the reference's PPO over the union of
+        # the shards (world x more minibatches than one rank over its own envs). With
+        # train.dp_scale_batch = true every rank runs a full batch_size minibatch of its own and
+        # the gradients are averaged: the reference run with batch_size x world.
         eff_batch = self.batch_size * (self.world_size if self.dp_scale_batch else 1)
         num_batch = max(1, total_global // eff_batch)                                     # :288
         rows_local_full = eff_batch // self.world_size
@@ -303,6 +307,10 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     m.grads_ext[ng:ng + 5].copy_(m.metrics[:5])
                     self._allreduce(m.grads_ext)
                     m.metrics[:5].copy_(m.grads_ext[ng:ng + 5])
+                if self.minibatch_hook is not None:
+                    if split:
+                        stream.wait_stream(side)
+                    self.minibatch_hook(update_epoch, batch, start, rows)
                 slot = k % 2
                 self._met_pin[slot].copy_(met[:5], non_blocking=True)
                 ev_m = torch.cuda.Event()

@@ -1,9 +1,9 @@
 """Pretraining agent (reference agent/pretrain/train_agent.py:61-187 and
 train_diffusion_agent.py:16-120): epochs over a StitchedSequenceDataset, the diffusion loss
 c_loss -> p_losses on the MI355X row-tile kernels (dppo_pretrain_minibatch), Keras-3 AdamW under
-CosineDecayRestarts, an EMA copy of the network, .npz checkpoints per save_model_freq.
+CosineDecayRestarts, an EMA copy of the network, Keras-3 .weights.h5 checkpoints per save_model_freq.
 
-Differences from the reference, by design: checkpoints are .npz (h5py is absent); t and noise come
+Differences from the reference, by design: t and noise come
 from a seeded device generator instead of tf.random; wandb logging is not built (out of scope)."""
 import logging
 import os
@@ -68,7 +68,8 @@ class TrainDiffusionAgent:
         self.ema.update_model_average(self.ema_params, self.model.params)
 
     def save_model(self, epoch):
-        path = os.path.join(self.checkpoint_dir, f"state_{epoch}.npz")
+        ext = ".npz" if self.cfg.train.get("checkpoint_format", "h5") == "npz" else ".weights.h5"
+        path = os.path.join(self.checkpoint_dir, f"state_{epoch}{ext}")   # agent/pretrain/train_agent.py:150-154
         self.model.save_network(path)
         saved = self.model.params.clone()
         self.model.params.copy_(self.ema_params)

@@ -9,6 +9,7 @@ import numpy as np
 import torch
 
 from ... import ops
+from ...util import keras_weights
 from .sampling import ddim_buffers, ddpm_buffers
 
 log = logging.getLogger(__name__)
@@ -87,9 +88,11 @@ class DiffusionModel:
             with np.load(str(path), allow_pickle=False) as f:
                 pref = "network." if any(k.startswith("network.") for k in f.files) else ""
                 p = {n: np.asarray(f[pref + n], np.float32).reshape(s) for n, s in self.pre_spec}
+        elif path is not None and str(path).endswith(".h5"):      # Keras-3 weights (util/keras_weights.py)
+            p = keras_weights.load_actor(str(path), self.pre_spec)
+        elif path is not None:
+            raise ValueError(f"network_path {path}: .weights.h5 or .npz checkpoints")
         else:
-            if path is not None:
-                log.warning("network_path %s not loaded (.npz checkpoints only): seeded glorot_uniform init", path)
             p = net.init_params(np.random.default_rng(self.seed))
         dev = self.device
         self.params = torch.tensor(ops.flatten_params(self.pre_spec, p), device=dev)
@@ -144,5 +147,10 @@ class DiffusionModel:
         return self.p_losses(actions, conditions, t, **kwargs)
 
     def save_network(self, path):
-        np.savez(path, **{"network." + n: v for n, v in
-                          ops.unflatten_params(self.pre_spec, self.params.detach().cpu().numpy()).items()})
+        """The network alone: a Keras-3 weights file for *.h5 (the reference's
+        self.model.network.save_weights, agent/pretrain/train_agent.py:150-154), else .npz."""
+        params = ops.unflatten_params(self.pre_spec, self.params.detach().cpu().numpy())
+        if str(path).endswith(".h5"):
+            keras_weights.save_actor(str(path), params)
+        else:
+            np.savez(path, **{"network." + n: v for n, v in params.items()})

@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from ... import ops
+from ...util import keras_weights
 from .diffusion import DiffusionModel, Sample
 
 log = logging.getLogger(__name__)
@@ -126,17 +127,19 @@ class VPGDiffusion(DiffusionModel):
                 keys = [k for k in f.files]
                 pref = "actor." if any(k.startswith("actor.") for k in keys) else ""
                 return {n: np.asarray(f[pref + n], np.float32).reshape(s) for n, s in self.actor_spec}
-        if path.endswith(".h5"):
-            try:
-                import h5py  # noqa: F401
-            except ImportError as e:
-                raise NotImplementedError(f"{path}: Keras .weights.h5 needs h5py, which is not installed; convert "
-                                          "the checkpoint to .npz (keys " + ", ".join(n for n, _ in self.actor_spec)
-                                          + ")") from e
-            raise NotImplementedError(".weights.h5 reader: SURVEY.md §8(f) rank 2")
+        if path.endswith(".h5"):          # Keras-3 weights of a DiffusionMLP (pretrain checkpoint)
+            return keras_weights.load_actor(path, self.actor_spec)
         raise ValueError(f"unsupported checkpoint format: {path}")
 
     def save_weights(self, path):
+        """PPODiffusion.save_weights: a Keras-3 weights file for *.h5 (actor/, actor_ft/, critic/;
+        agent/finetune/train_agent.py:127-133), else .npz with actor./actor_ft./critic. keys."""
+        if str(path).endswith(".h5"):
+            sp = lambda spec, flat: ops.unflatten_params(spec, flat.detach().cpu().numpy())
+            keras_weights.save_ppo_model(str(path), sp(self.actor_spec, self.base_params),
+                                         sp(self.actor_spec, self.actor_ft_params),
+                                         sp(self.critic_spec, self.critic_params))
+            return
         d = {}
         for prefix, flat, spec in (("actor.", self.base_params, self.actor_spec),
                                    ("actor_ft.", self.actor_ft_params, self.actor_spec),
@@ -146,6 +149,15 @@ class VPGDiffusion(DiffusionModel):
         np.savez(path, **d)
 
     def load_weights(self, path):
+        if str(path).endswith(".h5"):
+            w = keras_weights.load_ppo_model(str(path), self.actor_spec, self.critic_spec)
+            for key, flat, spec in (("actor", self.base_params, self.actor_spec),
+                                    ("actor_ft", self.actor_ft_params, self.actor_spec),
+                                    ("critic", self.critic_params, self.critic_spec)):
+                flat.copy_(torch.tensor(ops.flatten_params(spec, w[key])))
+            ops.pack_actor(self.dims, self.base_params, self.precision, out=self.packed_base)
+            self.repack()
+            return
         with np.load(path, allow_pickle=False) as f:
             for prefix, flat, spec in (("actor.", self.base_params, self.actor_spec),
                                        ("actor_ft.", self.actor_ft_params, self.actor_spec),

@@ -25,7 +25,12 @@ def test_agent_iterations(cuda, precision, tmp_path):
     assert agent.actor_optimizer.iterations == agent.timing["n_updates"]
     p = agent.model.train_params.cpu().numpy()
     assert np.isfinite(p).all()
-    assert os.path.exists(os.path.join(tmp_path, "checkpoint", "state_0.npz"))
+    # agent/finetune/train_agent.py:127-133: a Keras-3 weights file per save, readable back
+    ck = os.path.join(tmp_path, "checkpoint", "state_0.weights.h5")
+    assert os.path.exists(ck)
+    from diffusionpolicyoptimization_amd.util import keras_weights
+    w = keras_weights.load_ppo_model(ck, agent.model.actor_spec, agent.model.critic_spec)
+    assert set(w) == {"actor", "actor_ft", "critic"}
 
 
 def test_target_kl_stops_each_epoch_like_the_reference(cuda, tmp_path):
@@ -175,10 +180,10 @@ def test_pipelined_rollout_matches_model_call(cuda, protocol, precision, E, monk
     pipe.close()
 
 
-@pytest.mark.parametrize("overrides", ["", "train.dp_scale_batch=false"], ids=["per-rank-batch", "global-batch"])
+@pytest.mark.parametrize("overrides", ["", "train.dp_scale_batch=true"], ids=["reference-batch", "scaled-batch"])
 def test_data_parallel_agent_two_ranks_share_one_gpu(tmp_path, overrides):
     """2 ranks (gloo, both on cuda:0) run the DP agent; replicas must stay bit-identical, with the
-    minibatch per rank (default) or fixed globally."""
+    reference's global minibatch (default) or batch_size rows per rank (dp_scale_batch)."""
     import socket
     import subprocess
     import sys
@@ -195,6 +200,80 @@ def test_data_parallel_agent_two_ranks_share_one_gpu(tmp_path, overrides):
                          env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "replicas_identical=True" in out.stdout
+
+
+def test_data_parallel_update_equals_single_rank_on_the_union(cuda, tmp_path):
+    """SURVEY §8(e) on the HIP path: 2 ranks (gloo, both on cuda:0), reference batch semantics
+    (dp_scale_batch = false: the GLOBAL minibatch is batch_size rows, batch_size / 2 drawn by each
+    rank from its own shard). Against ONE rank running the same cfg over all 8 envs:
+      * the two rollout shards are exactly the single rank's rollout (per-global-env seeds and
+        Philox rows), and the advantages / returns (reward-RMS moments Chan-merged over ranks) match;
+      * the all-reduced gradient of minibatch 0 equals the single rank's gradient over the union of
+        the two ranks' rows (same global 1/batch_size scaling and global advantage moments), up to
+        fp summation order."""
+    import socket
+    import subprocess
+    import sys
+
+    import torch
+
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.config import get_class, load_config
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from dp_equiv import OVERRIDES
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, DPPO_DIST_BACKEND="gloo", DPPO_SINGLE_DEVICE="1", DPPO_EQUIV_DIR=str(tmp_path))
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(ROOT, "tools", "dp_equiv.py")], env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    r = [dict(np.load(tmp_path / f"rank{i}.npz")) for i in range(2)]
+    assert int(r[0]["world"]) == 2 and int(r[0]["rows"]) == 200 and int(r[1]["env_offset"]) == 4
+    np.testing.assert_array_equal(r[0]["grads"], r[1]["grads"])        # replicas see one gradient
+
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
+                      OVERRIDES + [f"logdir={tmp_path}/single"])
+    a = get_class(cfg._target_)(cfg)
+    m = a.model
+    np.testing.assert_array_equal(m.train_params.cpu().numpy(), r[0]["params"])
+    got = {}
+
+    def hook(epoch, batch, start, rows):
+        if (epoch, batch) != (0, 0):
+            return
+        S, E, kf = a.n_steps, a.n_envs, m.ft_denoising_steps
+        El = int(r[0]["n_envs"])
+        # the shards, side by side, are the single rank's rollout
+        for name, buf in (("obs", a.obs_traj), ("chains", a.chains_traj)):
+            np.testing.assert_array_equal(np.concatenate([r[0][name], r[1][name]], axis=1), buf.cpu().numpy())
+        adv = np.concatenate([r[0]["adv"], r[1]["adv"]], axis=1)
+        np.testing.assert_allclose(adv, a.adv.cpu().numpy(), rtol=0, atol=1e-5 * np.abs(adv).max())
+        # the union of the ranks' rows in the single rank's sample numbering
+        idx = []
+        for i in range(2):
+            loc = ops.feistel_permute(0, int(r[i]["rows"]), S * El * kf, int(r[i]["perm_seed"]), int(r[i]["epoch"]),
+                                      a.device).cpu().numpy()
+            n_loc, j = loc // kf, loc % kf
+            n_glob = (n_loc // El) * E + i * El + n_loc % El
+            idx.append(n_glob * kf + j)
+        idx = torch.tensor(np.concatenate(idx), device=a.device)
+        N = S * E
+        m.minibatch(a.obs_traj.view(N, -1), a.chains_traj.view(N, kf + 1, -1), a.lp_old, a.adv.view(-1),
+                    a.ret.view(-1), 0, 0, 0, idx.numel(), global_rows=a.batch_size, row_index=idx)
+        torch.cuda.synchronize()
+        got["grads"] = m.grads.cpu().numpy().copy()
+        got["metrics"] = m.metrics[:5].cpu().numpy().copy()
+        raise StopIteration
+    a.minibatch_hook = hook
+    with pytest.raises(StopIteration):
+        a.iteration(force_train=True)
+    g1, g2 = got["grads"], r[0]["grads"]
+    err = np.abs(g1 - g2).max() / np.abs(g1).max()
+    assert err < 1e-4, err
+    np.testing.assert_allclose(got["metrics"], r[0]["metrics"], rtol=1e-4, atol=1e-7)
 
 
 def test_pretrain_agent_trains(cuda, tmp_path):
@@ -218,7 +297,7 @@ def test_pretrain_agent_trains(cuda, tmp_path):
     last_epoch = agent.run()
     last = float(agent.model.p_losses(b["actions"], b["conditions"], t, z))
     assert np.isfinite(last_epoch) and np.isfinite(first) and last < 0.8 * first, (first, last)
-    ck = os.path.join(agent.checkpoint_dir, "state_4.npz")
+    ck = os.path.join(agent.checkpoint_dir, "state_4.weights.h5")   # network.save_weights layout
     assert os.path.exists(ck) and os.path.exists(ck.replace("state_", "ema_state_"))
     assert not torch.equal(agent.ema_params, agent.model.params)
     m2 = instantiate(cfg.model, network_path=ck)
@@ -280,3 +359,30 @@ def test_pipelined_rollout_unpublished_observation_times_out(cuda, protocol, mon
     torch.cuda.synchronize()             # the launch drained
     assert int(pipe._done[0]) & 0x80000000
     pipe.close()
+
+
+def test_keras_checkpoints_round_trip_through_the_model(cuda, tmp_path):
+    """§8(f) row 2 end to end: PPODiffusion.save_weights -> state_*.weights.h5 (actor/, actor_ft/,
+    critic/) -> load_weights into a fresh model; a pretrain-style network file (DiffusionMLP at the
+    root) as network_path loads into BOTH actors (diffusion_vpg.py:85-97); a missing path raises."""
+    import torch
+
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util import keras_weights
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp", ["model.precision=bf16"])
+    m = instantiate(cfg.model, device=cuda, seed=3)
+    m.train_params.add_(torch.randn_like(m.train_params) * 1e-3)
+    m.repack()
+    p = str(tmp_path / "state_7.weights.h5")
+    m.save_weights(p)
+    m2 = instantiate(cfg.model, device=cuda, seed=4)
+    m2.load_weights(p)
+    assert torch.equal(m2.base_params, m.base_params) and torch.equal(m2.train_params, m.train_params)
+    assert torch.equal(m2.packed_ft, m.packed_ft) and torch.equal(m2.packed_critic, m.packed_critic)
+    net = str(tmp_path / "state_785.weights.h5")
+    keras_weights.save_actor(net, ops.unflatten_params(m.actor_spec, m.actor_ft_params.cpu().numpy()))
+    m3 = instantiate(cfg.model, device=cuda, network_path=net)
+    assert torch.equal(m3.base_params, m.actor_ft_params) and torch.equal(m3.actor_ft_params, m.actor_ft_params)
+    with pytest.raises(FileNotFoundError):
+        instantiate(cfg.model, device=cuda, network_path=str(tmp_path / "missing.weights.h5"))

@@ -93,15 +93,20 @@ def test_sampler_philox_stream(cuda):
     assert np.abs(act.cpu().numpy().reshape(ref_a.shape) - ref_a).max() < 1e-3
 
 
-@pytest.mark.parametrize("E", [1, 16, 130, 512, 513])
-def test_sampler_bf16_sizes_philox(cuda, E):
-    """bf16 sampler with its own Philox noise at group boundaries (1, 16), a ragged multi-XCD size
-    (130 envs = 9 groups), the split kernel's maximum (512 envs = 256 workgroups) and one env past
-    it (513: the weight-streaming kernel). Checked against the oracle rounding at the kernel's
-    rounding points, given the same Philox draws."""
+@pytest.mark.parametrize("E,dims", [(1, HOPPER), (16, HOPPER), (64, HOPPER), (130, HOPPER), (256, WALKER),
+                                    (512, HOPPER), (513, HOPPER)],
+                         ids=["1", "16", "64-config2", "130", "256-walker-config3", "512", "513"])
+def test_sampler_bf16_sizes_philox(cuda, E, dims):
+    """bf16 sampler with its own Philox noise at group boundaries (1, 16), the BASELINE config-2
+    shape (hopper, 64 envs), a ragged multi-XCD size (130 envs = 9 groups), config 3's shape
+    (walker2d, XD = 24, 256 envs), the split kernel's maximum (512 envs = 256 workgroups) and one
+    env past it (513: the weight-streaming kernel). Checked against the oracle rounding at the
+    kernel's rounding points, given the same Philox draws: 99th percentile and mean tight; the
+    maximum bounded loosely (the t=19 x0 reconstruction multiplies eps by 406 before its clip, so a
+    single bf16 rounding-boundary flip can move one element)."""
     import torch
     from diffusionpolicyoptimization_amd import ops
-    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(dims, cuda)
     split = ops.sampler_layout(d, "bf16", E) > 0
     assert split == (E <= 512)
     seed, call = 987654321, 3
@@ -121,6 +126,7 @@ def test_sampler_bf16_sizes_philox(cuda, E):
     assert np.isfinite(act).all() and np.isfinite(ch).all()
     dev = np.abs(act - ref_a)
     assert np.quantile(dev, 0.99) < 2e-3 and np.abs(ch - ref_c).mean() < 2e-3, (dev.max(), np.quantile(dev, 0.99))
+    assert dev.max() < 0.1, dev.max()
 
 
 def test_sampler_split_repeatable(cuda):
@@ -480,3 +486,105 @@ def test_actor_tail_split_matches_single_launch(tmp_path):
     np.testing.assert_allclose(g1, g0, rtol=2e-4, atol=1e-5 * np.abs(g0).max())
     # the 32-row tiles sum the out-layer K in another order: log-prob ulps move ratio - 1 ~ 1e-8
     np.testing.assert_allclose(outs[0]["metrics"][:5], outs[1]["metrics"][:5], rtol=1e-5, atol=1e-6)
+
+
+def test_logprob_pass_full_size(cuda):
+    """The old-log-prob pass (a10 + c_loss:50-59, agent :209-229) at the bench's size: S*E =
+    500 x 64 = 32,000 samples (320,000 rows) in one launch, fp32; 256 random samples checked
+    against the oracle (element log-probs and the clipped per-row mean)."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    n, kf = 32000, d.ft_denoising_steps
+    g = torch.Generator(device=cuda).manual_seed(5)
+    obs = torch.rand(n, d.sd, device=cuda, generator=g) * 2 - 1
+    chains = torch.randn(n, kf + 1, d.xd, device=cuda, generator=g) * 0.5
+    packf = ops.pack_actor(d, pf, "fp32")
+    lpe, lpm = ops.logprob(d, "fp32", packf, tab, obs, chains, want_elem=True, want_mean=True)
+    torch.cuda.synchronize()
+    pick = np.random.default_rng(3).choice(n, 256, replace=False)
+    o, c = obs.cpu().numpy()[pick], chains.cpu().numpy()[pick]
+    ref = O.get_logprobs(to_f64(ft), sched, o.reshape(-1, 1, d.sd).astype(np.float64),
+                         c.reshape(-1, kf + 1, d.horizon_steps, d.action_dim).astype(np.float64), kf)
+    got = lpe.view(n, kf, d.xd).cpu().numpy()[pick].reshape(ref.shape)
+    assert np.abs(got - ref).max() < 1e-3, np.abs(got - ref).max()
+    ref_m = np.clip(ref, -5, 2).mean(axis=(1, 2)).reshape(-1, kf)
+    assert np.abs(lpm.cpu().numpy()[pick] - ref_m).max() < 1e-4
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_ppo_minibatch_full_size(cuda, precision):
+    """dppo_ppo_minibatch at the bench's minibatch, b = 50,000 rows (782 64-row actor tiles, the
+    32-row tail launch, split-K dW over all rows), over a 64,000-row rollout. The full-size launch is
+    checked through a size-independent property and the oracle:
+      * linearity: the loss is a mean over rows, so the gradient and metric sums of the full
+        launch equal the sum over 25 disjoint 2,000-row slices of the same rows (row_index), each
+        launched with global_rows = 50,000 and the full minibatch's advantage moments;
+      * one of those slices against the oracle (c_loss with denom = 50,000 and the full
+        minibatch's advantage mean / std)."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    N, kf, b, perm_seed, epoch = 6400, d.ft_denoising_steps, 50000, 77, 3
+    rng = np.random.default_rng(21)
+    obs = rng.uniform(-1, 1, (N, d.sd)).astype(np.float32)
+    chains = (rng.standard_normal((N, kf + 1, d.xd)) * 0.5).astype(np.float32)
+    adv = rng.normal(size=N).astype(np.float32)
+    ret = rng.normal(size=N).astype(np.float32)
+    T = lambda x: torch.tensor(x, device=cuda)
+    packf, packc = ops.pack_actor(d, pf, precision), ops.pack_critic(d, pc, precision)
+    _, lpm = ops.logprob(d, precision, packf, tab, T(obs), T(chains), want_elem=False)
+    # fp32: perturbed old log-probs (rows on both PPO clip branches); bf16: the policy's own (ratio 1),
+    # since bf16 rounding flips clip branches (see test_ppo_minibatch_grads)
+    noise = rng.normal(0, 0.01, (N, kf)) if precision == "fp32" else 0.0
+    lp_old = (lpm.cpu().numpy() + noise).astype(np.float32)
+    args = (T(obs), T(chains), T(lp_old), T(adv), T(ret))
+    na = ops.spec_count(ops.actor_param_spec(d))
+    nc = ops.spec_count(ops.critic_param_spec(d))
+    stats = torch.zeros(3, dtype=torch.float64, device=cuda)
+    ops.ppo_adv_stats(args[3], N * kf, kf, perm_seed, epoch, 0, b, stats)
+    hp = ops.ppo_hparams(global_rows=b)
+
+    def run(rows, row_index=None, start=0):
+        grads = torch.zeros(na + nc, dtype=torch.float32, device=cuda)
+        met = torch.zeros(16, dtype=torch.float64, device=cuda)
+        ops.ppo_minibatch(d, precision, hp, packf, packc, pf, tab, *args, perm_seed, epoch, start, rows,
+                          ops.ppo_workspace(d, precision, rows, cuda), grads, met, adv_stats=stats,
+                          row_index=row_index)
+        torch.cuda.synchronize()
+        return grads.cpu().numpy().astype(np.float64), met.cpu().numpy()[:5]
+
+    g_full, m_full = run(b)
+    assert np.isfinite(g_full).all()
+    perm = ops.feistel_permute(0, b, N * kf, perm_seed, epoch, cuda)
+    g_sum, m_sum = np.zeros_like(g_full), np.zeros(5)
+    g_slices = []
+    for k in range(25):
+        g, m = run(2000, row_index=perm, start=2000 * k)
+        g_sum += g
+        m_sum += m
+        g_slices.append(g)
+    rel = np.abs(g_sum - g_full).max() / np.abs(g_full).max()
+    assert rel < (1e-5 if precision == "fp32" else 1e-4), rel
+    # metric sums (pg, v, approx_kl, clipfrac, ratio) over 50,000 rows: fp32 accumulation order;
+    # approx_kl is ~0 at ratio 1 (bf16 case), so it gets an absolute bound
+    np.testing.assert_allclose(m_sum, m_full, rtol=1e-5, atol=1e-5)
+    # slice 7 against the oracle
+    rows = perm.cpu().numpy()[14000:16000]
+    bi, di = rows // kf, rows % kf
+    st = stats.cpu().numpy()
+    mean = st[1] / st[0]
+    std = np.sqrt(max(st[2] / st[0] - mean * mean, 0.0))
+    met_ref, ga, gc = O.c_loss(
+        to_f64(ft), to_f64(critic), sched, obs[bi].reshape(-1, 1, d.sd).astype(np.float64),
+        chains[bi, di].reshape(-1, d.horizon_steps, d.action_dim).astype(np.float64),
+        chains[bi, di + 1].reshape(-1, d.horizon_steps, d.action_dim).astype(np.float64), di,
+        ret[bi].astype(np.float64), None, adv[bi].astype(np.float64), lp_old[bi, di].astype(np.float64), kf,
+        rnd=_rnd(precision), adv_mean_std=(mean, std), denom=b)
+    g_ref = np.concatenate([ops.flatten_params(ops.actor_param_spec(d), ga).astype(np.float64),
+                            ops.flatten_params(ops.critic_param_spec(d), gc).astype(np.float64)])
+    g7 = g_slices[7]
+    tol = 5e-3 if precision == "fp32" else 1e-2
+    for lo, hi, name in ((0, na, "actor"), (na, na + nc, "critic")):
+        err = np.abs(g7[lo:hi] - g_ref[lo:hi]).max() / np.abs(g_ref[lo:hi]).max()
+        assert err < tol, (name, err)
