@@ -13,10 +13,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DPPO_LIB selects a tuning build (tools/variant_build.sh); it must exist like the default one
 LIB_PATH = os.environ.get("DPPO_LIB") or os.path.join(_HERE, "lib", "libdppo_hip.so")
 
-DPPO_F32, DPPO_BF16 = 0, 1
+DPPO_F32, DPPO_BF16, DPPO_F16 = 0, 1, 2
 DPPO_ADAMW_KERAS, DPPO_ADAMW_TORCH = 0, 1
 SCHED_COLS = 8
-PRECISION = {"fp32": DPPO_F32, "f32": DPPO_F32, "bf16": DPPO_BF16}
+PRECISION = {"fp32": DPPO_F32, "f32": DPPO_F32, "bf16": DPPO_BF16, "fp16": DPPO_F16, "f16": DPPO_F16}
 
 
 class DppoDims(ctypes.Structure):
@@ -86,7 +86,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class DppoError(RuntimeError):

@@ -67,7 +67,7 @@ extern "C" int dppo_pack_actor(const dppo_dims* d, int precision, const float* p
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
     DPPO_CHECK(params && packed, "dppo_pack_actor: null pointer");
-    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
     return dppo_pack_mlp(D.IN, D.H, D.XD, D.TD, precision, params, packed, (hipStream_t)stream, D.K, D.TS);
 }
 extern "C" int dppo_pack_critic(const dppo_dims* d, int precision, const float* params, void* packed, void* stream) {
@@ -75,6 +75,6 @@ extern "C" int dppo_pack_critic(const dppo_dims* d, int precision, const float* 
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
     DPPO_CHECK(params && packed, "dppo_pack_critic: null pointer");
-    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
     return dppo_pack_mlp(D.SD, D.HC, 1, 0, precision, params, packed, (hipStream_t)stream);
 }

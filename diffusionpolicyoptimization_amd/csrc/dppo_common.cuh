@@ -18,10 +18,17 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 typedef __attribute__((ext_vector_type(2))) float f32x2_t;
 
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
+
 // two floats -> packed bf16 pair (RNE) in ONE v_cvt_pk_bf16_f32; two scalar (__bf16) casts
 // compile to two conversions plus a shift and an or
 __device__ inline unsigned int dppo_pack_bf16x2(float lo, float hi) {
     return __builtin_bit_cast(unsigned int, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
+}
+// two floats -> packed fp16 pair (RNE, v_cvt_pk_f16_f32)
+__device__ inline unsigned int dppo_pack_f16x2(float lo, float hi) {
+    return __builtin_bit_cast(unsigned int, __builtin_convertvector((f32x2_t){lo, hi}, f16x2_t));
 }
 
 #define DPPO_WAVES 8
@@ -34,11 +41,40 @@ struct PolicyBF16 {
     using AT = __bf16;                 // activation element type in LDS
     static constexpr int KG = 32;      // k covered by one 16-B fragment
     static constexpr int EPL = 8;      // elements per lane per fragment
+    static constexpr float GRAD_SCALE = 1.f;   // backward seed scale (range of the 2-byte images)
     __device__ static inline AT cvt(float x) { return (__bf16)x; }
     __device__ static inline float tof(AT x) { return (float)x; }
+    __device__ static inline unsigned int pack2(float lo, float hi) { return dppo_pack_bf16x2(lo, hi); }
+    // the two halves of a packed pair back to fp32
+    __device__ static inline float lo2f(unsigned int w) { return __uint_as_float(w << 16); }
+    __device__ static inline float hi2f(unsigned int w) { return __uint_as_float(w & 0xffff0000u); }
     __device__ static inline f32x4 mma(u32x4 a, u32x4 b, f32x4 c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
                                                        __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+    }
+};
+
+// fp16 operands (BASELINE config 5): v_mfma_f32_16x16x32_f16, same fragment geometry as bf16.
+// fp16's 5-bit exponent does not hold the PPO gradients (~1e-5 per row at b = 50,000), so the
+// backward pass is seeded with GRAD_SCALE times the loss gradient and the weight-gradient outputs
+// (fp32) are multiplied by 1 / GRAD_SCALE (a power of two: exact).
+struct PolicyF16 {
+    using AT = _Float16;
+    static constexpr int KG = 32;
+    static constexpr int EPL = 8;
+    static constexpr float GRAD_SCALE = 4096.f;
+    __device__ static inline AT cvt(float x) { return (_Float16)x; }
+    __device__ static inline float tof(AT x) { return (float)x; }
+    __device__ static inline unsigned int pack2(float lo, float hi) { return dppo_pack_f16x2(lo, hi); }
+    __device__ static inline float lo2f(unsigned int w) {
+        return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu));
+    }
+    __device__ static inline float hi2f(unsigned int w) {
+        return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16));
+    }
+    __device__ static inline f32x4 mma(u32x4 a, u32x4 b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                      __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
     }
 };
 
@@ -46,6 +82,7 @@ struct PolicyF32 {
     using AT = float;
     static constexpr int KG = 16;
     static constexpr int EPL = 4;
+    static constexpr float GRAD_SCALE = 1.f;
     __device__ static inline AT cvt(float x) { return x; }
     __device__ static inline float tof(AT x) { return x; }
     // lane holds k = 4*(lane>>4) + q of the 16-k group for q = 0..3; MFMA q pairs A and B

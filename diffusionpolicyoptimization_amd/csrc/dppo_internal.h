@@ -17,5 +17,12 @@ struct Dims {
 };
 int dppo_check_dims(const dppo_dims* d, Dims* out);
 
+// precision enum values the library implements; the two 2-byte operand policies share layouts
+inline bool dppo_prec_ok(int p) { return p == DPPO_F32 || p == DPPO_BF16 || p == DPPO_F16; }
+inline bool dppo_prec_2b(int p) { return p == DPPO_BF16 || p == DPPO_F16; }
+// backward seed scale of a precision (PolicyF16::GRAD_SCALE): the row tiles seed the backward pass
+// with this times the loss gradient; the weight-gradient outputs multiply by its inverse
+inline float dppo_grad_scale(int p) { return p == DPPO_F16 ? 4096.f : 1.f; }
+
 #define DPPO_CHECK(cond, ...) do { if (!(cond)) return dppo_set_error(DPPO_EINVAL, __VA_ARGS__); } while (0)
 #define DPPO_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return dppo_hip_fail(e_, #x); } while (0)

@@ -51,7 +51,7 @@ DPPO_HD inline MlpLayout make_mlp_layout(int in_dim, int hidden, int out_dim, in
     MlpLayout L;
     L.in_dim = in_dim; L.hidden = hidden; L.out_dim = out_dim; L.time_dim = time_dim; L.precision = precision;
     L.temb_steps = time_dim > 0 ? temb_steps : 0;
-    L.KG = precision == 1 ? 32 : 16;
+    L.KG = (precision == 1 || precision == 2) ? 32 : 16;     // bf16 / fp16: 32; fp32: 16
     L.ks_in = packed_ksteps(in_dim, L.KG);
     L.ks_h = packed_ksteps(hidden, L.KG);
     L.ks_out_t = packed_ksteps(out_dim, L.KG);

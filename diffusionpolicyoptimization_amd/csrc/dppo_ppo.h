@@ -21,7 +21,7 @@ struct PpoWorkspace {
 inline PpoWorkspace make_ppo_workspace(const Dims& D, int precision, int rows, uint8_t* base) {
     PpoWorkspace w;
     w.base = base;
-    const size_t es = precision == DPPO_BF16 ? 2 : 4;
+    const size_t es = dppo_prec_2b(precision) ? 2 : 4;
     w.ldm = (size_t)dppo_cdiv(rows > 0 ? rows : 1, 64) * 64;
     size_t o = 0;
     auto take = [&](size_t feats) -> void* {

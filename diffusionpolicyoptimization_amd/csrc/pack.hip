@@ -22,7 +22,7 @@ struct PackArgs {
     uint8_t* out;
 };
 
-template <int KG, int EPL>
+template <int KG, int EPL, class ET = __bf16>
 __global__ void pack_all_kernel(PackArgs a) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.start[a.njobs]) return;
@@ -42,13 +42,13 @@ __global__ void pack_all_kernel(PackArgs a) {
     const int n = nt * 16 + (lane & 15);
     u32x4 v;
     if constexpr (EPL == 8) {
-        __bf16 e[8];
+        ET e[8];                 // __bf16 or _Float16 (RNE)
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int k = ks * KG + (lane >> 4) * EPL + q;
             float x = 0.f;
             if (k < J.K && n < J.N) x = J.transposed ? W[(size_t)n * J.K + k] : W[(size_t)k * J.N + n];
-            e[q] = (__bf16)x;
+            e[q] = (ET)x;
         }
         v = __builtin_bit_cast(u32x4, e);
     } else {
@@ -102,7 +102,7 @@ int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precisi
                   void* packed, hipStream_t s, int temb_steps, int time_stride) {
     const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision, temb_steps);
     const FlatOffsets F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
-    const int KG = precision == DPPO_BF16 ? 32 : 16;
+    const int KG = dppo_prec_2b(precision) ? 32 : 16;
     PackArgs a = {};
     auto mat = [&](size_t src, int K, int N, bool tr, int seg) {
         PackJob& J = a.j[a.njobs++];
@@ -131,7 +131,9 @@ int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precisi
     a.out = (uint8_t*)packed;
     const int blocks = dppo_cdiv(a.start[a.njobs], 256);
     if (precision == DPPO_BF16)
-        hipLaunchKernelGGL((pack_all_kernel<32, 8>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((pack_all_kernel<32, 8, __bf16>), dim3(blocks), dim3(256), 0, s, a);
+    else if (precision == DPPO_F16)
+        hipLaunchKernelGGL((pack_all_kernel<32, 8, _Float16>), dim3(blocks), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL((pack_all_kernel<16, 4>), dim3(blocks), dim3(256), 0, s, a);
     DPPO_HIP(hipGetLastError());

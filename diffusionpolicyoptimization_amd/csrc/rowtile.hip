@@ -79,8 +79,8 @@ __device__ inline void store_accT(__amdgpu_buffer_rsrc_t ws, uint32_t img_off, u
             const uint32_t so = so0 + ((uint32_t)n * 16u * ldm + (uint32_t)mp * 32u) * es;
             const f32x4 lo = v[2 * mp][n], hi = v[2 * mp + 1][n];
             if constexpr (es == 2) {
-                const u32x4 e = {dppo_pack_bf16x2(lo[0], lo[1]), dppo_pack_bf16x2(lo[2], lo[3]),
-                                 dppo_pack_bf16x2(hi[0], hi[1]), dppo_pack_bf16x2(hi[2], hi[3])};
+                const u32x4 e = {P::pack2(lo[0], lo[1]), P::pack2(lo[2], lo[3]),
+                                 P::pack2(hi[0], hi[1]), P::pack2(hi[2], hi[3])};
                 // soffset must be the literal 0: with an SGPR there, hipcc (ROCm 7.2) does not guard
                 // the >8-byte store-data hazard (a following VALU overwrote the 4th dword)
                 __builtin_amdgcn_raw_buffer_store_b128(e, ws, vo + so, 0, 0);
@@ -106,8 +106,8 @@ __device__ inline void store_img8(void* img, size_t ldm, size_t grow0, int c, in
     for (int k = 0; k < 8; ++k) e[k] = value(img_row(8 * g + k));
     AT* dst = (AT*)img + (size_t)c * ldm + grow0 + 8 * g;
     if constexpr (sizeof(AT) == 2) {
-        *(u32x4*)dst = u32x4{dppo_pack_bf16x2(e[0], e[1]), dppo_pack_bf16x2(e[2], e[3]),
-                             dppo_pack_bf16x2(e[4], e[5]), dppo_pack_bf16x2(e[6], e[7])};
+        *(u32x4*)dst = u32x4{P::pack2(e[0], e[1]), P::pack2(e[2], e[3]),
+                             P::pack2(e[4], e[5]), P::pack2(e[6], e[7])};
     } else {
 #pragma unroll
         for (int k = 0; k < 8; k += 2) *(u32x2*)(dst + k) = u32x2{__float_as_uint(e[k]), __float_as_uint(e[k + 1])};
@@ -855,8 +855,9 @@ static int64_t actor_device_cus() {
     return n;
 }
 
-int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
-    if (precision != DPPO_BF16) return dispatch_actor<PolicyF32, 2, 8>(a, s);
+// the 2-byte operand policies (bf16, fp16) share the tile configurations
+template <class P2>
+static int launch_actor_2b(const ActorArgs& a, hipStream_t s) {
     const int v = row_tile_cfg().actor;
     // bf16, H = 512: 64-row tiles on 16 waves halve the weight stream per row of 32-row tiles; their
     // out-layer partials (16 waves x 64 rows x 16*NO) only fit the aliased LDS tile for XD <= 16
@@ -875,17 +876,23 @@ int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
                 ActorArgs t = a;
                 t.row0 = (tiles - rem) * 64;
                 t.row_end = (int64_t)a.ws.ldm;
-                int rc = dispatch_actor<PolicyBF16, 2, 8>(t, s);
+                int rc = dispatch_actor<P2, 2, 8>(t, s);
                 if (rc) return rc;
                 ActorArgs m = a;
                 m.row_end = (tiles - rem) * 64;
-                return dispatch_actor<PolicyBF16, 4, 16>(m, s);
+                return dispatch_actor<P2, 4, 16>(m, s);
             }
         }
-        return dispatch_actor<PolicyBF16, 4, 16>(a, s);
+        return dispatch_actor<P2, 4, 16>(a, s);
     }
-    if (a.H == 512 && v == 3 && a.XD <= 16) return dispatch_actor<PolicyBF16, 4, 8>(a, s);
-    return v == 2 ? dispatch_actor<PolicyBF16, 2, 8, true>(a, s) : dispatch_actor<PolicyBF16, 2, 8>(a, s);
+    if (a.H == 512 && v == 3 && a.XD <= 16) return dispatch_actor<P2, 4, 8>(a, s);
+    return v == 2 ? dispatch_actor<P2, 2, 8, true>(a, s) : dispatch_actor<P2, 2, 8>(a, s);
+}
+
+int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
+    if (precision == DPPO_BF16) return launch_actor_2b<PolicyBF16>(a, s);
+    if (precision == DPPO_F16) return launch_actor_2b<PolicyF16>(a, s);
+    return dispatch_actor<PolicyF32, 2, 8>(a, s);
 }
 
 template <class P, int MT, int NT, bool TRAIN, int WAVES, bool O4>
@@ -918,8 +925,12 @@ static int dispatch_critic(const CriticArgs& a, hipStream_t s) {
 
 int launch_critic_rowtile(const CriticArgs& a, int precision, hipStream_t s) {
     if (row_tile_cfg().critic == 1)
-        return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8, true>(a, s) : dispatch_critic<PolicyF32, 2, 8, true>(a, s);
-    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8, false>(a, s) : dispatch_critic<PolicyF32, 2, 8, false>(a, s);
+        return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8, true>(a, s)
+             : precision == DPPO_F16  ? dispatch_critic<PolicyF16, 2, 8, true>(a, s)
+                                      : dispatch_critic<PolicyF32, 2, 8, true>(a, s);
+    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8, false>(a, s)
+         : precision == DPPO_F16  ? dispatch_critic<PolicyF16, 2, 8, false>(a, s)
+                                  : dispatch_critic<PolicyF32, 2, 8, false>(a, s);
 }
 
 // =============================================================================================
@@ -931,7 +942,7 @@ extern "C" int dppo_logprob(const dppo_dims* d, int precision, const void* packe
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
-    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
     DPPO_CHECK(n >= 0, "dppo_logprob: n < 0");
     if (n == 0) return DPPO_OK;
     DPPO_CHECK(packed_ft && sched && cond && chains && (lp_elem || lp_mean), "dppo_logprob: null pointer");
@@ -954,7 +965,7 @@ extern "C" int dppo_critic_forward(const dppo_dims* d, int precision, const void
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
-    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
     DPPO_CHECK(n >= 0, "dppo_critic_forward: n < 0");
     if (n == 0) return DPPO_OK;
     DPPO_CHECK(packed_critic && cond && values, "dppo_critic_forward: null pointer");

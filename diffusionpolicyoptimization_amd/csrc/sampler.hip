@@ -488,18 +488,22 @@ static char sampler_cfg() {
 
 template <class P, int NT16, int NO, int KSI, bool INJ>
 static int launch_sample_k(const SampleArgs& a, hipStream_t s) {
-    if constexpr (P::KG == 32 && NT16 == 2) {   // bf16, H = 512
-        const char c = sampler_cfg();
-        if (c == 'r' || c == 'x') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 0, 3>(a, s);
-        if (c == 'l') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 1, 3>(a, s);
-        if (c == 'm') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 1, 3>(a, s);
-        if (c == 'q') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 0, 3>(a, s);
-        if (c == 'i') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, 3>(a, s);
-        if (c == 'e') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, 0>(a, s);
+    if constexpr (P::KG == 32 && NT16 == 2 && P::GRAD_SCALE != 1.f) {   // fp16, H = 512: the default geometry only
+        return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 0, 3>(a, s);
+    } else {
+        if constexpr (P::KG == 32 && NT16 == 2) {   // bf16, H = 512
+            const char c = sampler_cfg();
+            if (c == 'r' || c == 'x') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 0, 3>(a, s);
+            if (c == 'l') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 1, 3>(a, s);
+            if (c == 'm') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 1, 3>(a, s);
+            if (c == 'q') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 0, 3>(a, s);
+            if (c == 'i') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, 3>(a, s);
+            if (c == 'e') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, 0>(a, s);
+        }
+        if (sampler_cfg() == 'I') return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 1>(a, s);
+        if (sampler_cfg() == 'O') return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 3>(a, s);
+        return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 0>(a, s);
     }
-    if (sampler_cfg() == 'I') return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 1>(a, s);
-    if (sampler_cfg() == 'O') return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 3>(a, s);
-    return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 0>(a, s);
 }
 
 template <class P, int NT, int NO, int KSI>
@@ -528,7 +532,7 @@ static int dispatch_sample(const SampleArgs& a, hipStream_t s) {
 // the geometry launch_sample_k picks, for dppo_sampler_stream_bytes
 struct SamplerGeom { int SW, RK, LK, RIO; };
 static SamplerGeom sampler_geom(int precision, int H) {
-    if (precision == DPPO_BF16 && H == 512) {
+    if (dppo_prec_2b(precision) && H == 512) {
         switch (sampler_cfg()) {
             case 'r': case 'x': return {8, 2, 0, 3};
             case 'l': return {8, 2, 1, 3};
@@ -549,7 +553,7 @@ extern "C" int dppo_sampler_stream_bytes(const dppo_dims* d, int precision, int6
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
     DPPO_CHECK(bytes_per_tile, "dppo_sampler_stream_bytes: null output");
-    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "dppo_sampler_stream_bytes: bad precision %d", precision);
+    DPPO_CHECK(dppo_prec_ok(precision), "dppo_sampler_stream_bytes: bad precision %d", precision);
     const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     const SamplerGeom g = sampler_geom(precision, D.H);
     const int64_t ntot = D.H / 16, no = dppo_cdiv(D.XD, 16);
@@ -575,7 +579,7 @@ static int sample_impl(const dppo_dims* d, int precision, const void* packed_bas
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
     DPPO_CHECK(n_envs >= 0, "dppo_sample: n_envs < 0");
-    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "dppo_sample: bad precision %d", precision);
+    DPPO_CHECK(dppo_prec_ok(precision), "dppo_sample: bad precision %d", precision);
     if (n_envs == 0) return DPPO_OK;
     DPPO_CHECK(packed_base && packed_ft && sched && (cond || cond_tagged) && actions, "dppo_sample: null pointer argument");
     SampleArgs a;
@@ -594,7 +598,8 @@ static int sample_impl(const dppo_dims* d, int precision, const void* packed_bas
         rc = launch_sample_split(a, precision, s);
         if (rc != DPPO_EUNSUPPORTED) return rc;
     }
-    return precision == DPPO_BF16 ? dispatch_sample<PolicyBF16>(a, s) : dispatch_sample<PolicyF32>(a, s);
+    return precision == DPPO_BF16 ? dispatch_sample<PolicyBF16>(a, s)
+         : precision == DPPO_F16  ? dispatch_sample<PolicyF16>(a, s) : dispatch_sample<PolicyF32>(a, s);
 }
 
 extern "C" int dppo_sampler_layout(const dppo_dims* d, int precision, int n_envs, int* members) {

@@ -149,7 +149,6 @@ __device__ inline int xcc_id() {
 // k-step holds feature e < 4 ? 4j + e : 16 + 4j + (e - 4)
 __device__ inline int slot_feature(int j, int e) { return e < 4 ? 4 * j + e : 16 + 4 * j + (e - 4); }
 
-__device__ inline uint32_t pack_bf16x2(float lo, float hi) { return dppo_pack_bf16x2(lo, hi); }
 
 template <int CTRL>
 __device__ inline float dpp_f32(float v) {
@@ -157,11 +156,12 @@ __device__ inline float dpp_f32(float v) {
 }
 
 // XQ = XD / 4 (compile time: the sweep's loads must all be in flight before the first wait)
-template <int P, int XQ, int KSI, bool INJ>
+// Pol: the 2-byte operand policy (PolicyBF16, or PolicyF16 for BASELINE config 5)
+template <class Pol, int P, int XQ, int KSI, bool INJ>
 __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
     constexpr int NO = (4 * XQ + 15) / 16;
-    using Pol = PolicyBF16;
-    using AT = __bf16;
+    using AT = typename Pol::AT;
+    auto pack_bf16x2 = [](float lo, float hi) { return Pol::pack2(lo, hi); };
     constexpr int H = SPLIT_H, NTH = H / 16, KSH = H / 32;
     constexpr int NT1 = NTH / P;           // l1 n-tiles per member
     constexpr int KP = SW / NT1;           // l1 K-parts (waves per l1 n-tile)
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 for (int e2 = 0; e2 < 4; ++e2) {
                     const float x0 = hv[2 * e2], x1 = hv[2 * e2 + 1];
                     hi[e2] = pack_bf16x2(x0, x1);
-                    const float r0 = __uint_as_float(hi[e2] << 16), r1 = __uint_as_float(hi[e2] & 0xffff0000u);
+                    const float r0 = Pol::lo2f(hi[e2]), r1 = Pol::hi2f(hi[e2]);
                     lo[e2] = pack_bf16x2(x0 - r0, x1 - r1);
                 }
 #pragma unroll
@@ -747,10 +747,10 @@ int device_cus() {
     return g_cus;
 }
 
-template <int XQ, int KSI, bool INJ>
+template <class Pol, int XQ, int KSI, bool INJ>
 int launch_split_k(const SplitArgs& sa, hipStream_t s) {
     constexpr int NO = (4 * XQ + 15) / 16;
-    auto k = sample_split_kernel<SPLIT_P, XQ, KSI, INJ>;
+    auto k = sample_split_kernel<Pol, SPLIT_P, XQ, KSI, INJ>;
     const SampleArgs& a = sa.a;
     const size_t lds = split_lds_bytes(a.XD, a.SD, a.TD, a.K, KSI, NO);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler needs %zu B of LDS", lds);
@@ -764,7 +764,7 @@ int launch_split_k(const SplitArgs& sa, hipStream_t s) {
 }  // namespace
 
 bool sample_split_supported(int precision, int H, int XD, int ks_in, int E, int K) {
-    if (precision != DPPO_BF16 || H != SPLIT_H || XD % 4 != 0 || XD > 32 || ks_in != 2 || K > 63) return false;
+    if (!dppo_prec_2b(precision) || H != SPLIT_H || XD % 4 != 0 || XD > 32 || ks_in != 2 || K > 63) return false;
     const int G = dppo_cdiv(E, 16);
     if (G < 1 || G > XMAX_G) return false;
     const int cus = device_cus();
@@ -788,9 +788,12 @@ int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s) {
     int rc = xchg_for(s, &sa.xbuf, &sa.seq);
     if (rc) return rc;
     const bool inj = a.noise != nullptr;
+    const bool f16 = precision == DPPO_F16;
     switch (a.XD / 4) {
-#define DPPO_SPLIT_CASE(xq) \
-    case xq: return inj ? launch_split_k<xq, 2, true>(sa, s) : launch_split_k<xq, 2, false>(sa, s);
+#define DPPO_SPLIT_CASE(xq)                                                                                 \
+    case xq:                                                                                                \
+        if (f16) return inj ? launch_split_k<PolicyF16, xq, 2, true>(sa, s) : launch_split_k<PolicyF16, xq, 2, false>(sa, s); \
+        return inj ? launch_split_k<PolicyBF16, xq, 2, true>(sa, s) : launch_split_k<PolicyBF16, xq, 2, false>(sa, s);
         DPPO_SPLIT_CASE(1) DPPO_SPLIT_CASE(2) DPPO_SPLIT_CASE(3) DPPO_SPLIT_CASE(4)
         DPPO_SPLIT_CASE(5) DPPO_SPLIT_CASE(6) DPPO_SPLIT_CASE(7) DPPO_SPLIT_CASE(8)
 #undef DPPO_SPLIT_CASE

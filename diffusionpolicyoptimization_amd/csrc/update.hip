@@ -5,11 +5,12 @@
 
 // ---------------------------------------------------------------------------------------------
 // grouped split-K weight-gradient GEMM:  G[k][n] += sum_m XT[k][m] * DT[n][m]
-// (dW = X^T dH in Keras [in,out] layout). A workgroup (4 waves, one per CU) owns a 128x128 output
-// tile and one m-chunk; each wave holds a 64x64 sub-tile (4x4 MFMA tiles, 64 accumulator VGPRs).
+// (dW = X^T dH in Keras [in,out] layout). A workgroup (one per CU) owns a WK x 128 output tile
+// (WK = 128: 4 waves, WK = 256: 8 waves; DWGeom) and one m-chunk; each wave holds a 64x64
+// sub-tile (4x4 MFMA tiles, 64 accumulator VGPRs).
 // Both operands are feature-major, so a stage of BK rows is one 128-B line per feature: the stage
 // is copied global -> LDS with 16-B global_load_lds (one 1 KiB wave-instruction = 8 features) into
-// a ring of DW_RING slots, DW_RING - 1 stages in flight: each wave waits with a counted vmcnt for
+// a ring of RING slots, RING - 1 stages in flight: each wave waits with a counted vmcnt for
 // its own copies of the oldest stage only, then one barrier (the kernel reads ~470 MB of images
 // per minibatch; one stage in flight behind a vmcnt(0) barrier left it latency bound at ~2.5 TB/s).
 // The LDS image is linear per wave-instruction; the bank swizzle (16-B slot = chunk ^ (feature & 7))
@@ -22,11 +23,24 @@
 // ---------------------------------------------------------------------------------------------
 enum { EXTRA_NONE = 0, EXTRA_ONES = 1, EXTRA_ONEHOT = 2 };
 #define DW_MAXP 8
-#define DW_T 128             // output tile edge
+#define DW_TN 128            // output tile edge along N (the gradient operand's features)
 #define DW_LINE 128          // bytes per feature per stage
-#define DW_OPB (DW_T * DW_LINE)   // 16 KiB: one operand's stage image
-#define DW_RING 4                 // ring slots (stages in flight: DW_RING - 1)
-#define DW_SLOT (2 * DW_OPB + 1024)   // A | B | the stage's seg bytes (padded)
+#define DW_BOPB (DW_TN * DW_LINE)   // 16 KiB: the B (gradient) operand's stage image
+
+// Output tile = DW_TK(WK) x 128: WK = 128 (4 waves, 2x2 of 64x64; ring of 4 slots, 3 stages in
+// flight) or WK = 256 (8 waves, 4x2 of 64x64; ring of 3 slots, 2 stages in flight). The kernel is
+// bound by the latency of its staged loads (Little's law over the LDS ring: about 96 KiB in flight
+// per CU either way), so the 256-row tile's 1.33x MFMAs per staged byte is what it buys; the
+// k-tile edge is chosen per launch (DPPO_DW_TK: measurement knob).
+template <int WK> struct DWGeom {
+    static constexpr int W = WK / 32;                    // waves: 4 or 8
+    static constexpr int AOPB = WK * DW_LINE;            // A (activation) operand's stage image
+    static constexpr int SLOT = AOPB + DW_BOPB + 1024;   // A | B | the stage's seg bytes (padded)
+    static constexpr int RING = WK == 256 ? 3 : 4;       // ring slots (stages in flight: RING - 1)
+    static constexpr int AI = WK / 8 / W;                // A wave-instructions per wave per stage (4)
+    static constexpr int BI = DW_TN / 8 / W;             // B wave-instructions per wave per stage (4 / 2)
+    static_assert(RING * SLOT <= 160 * 1024, "dW ring exceeds the CU's LDS");
+};
 
 struct DWProb {
     const void* XT; const void* DT; float* G; float* Gx;
@@ -36,6 +50,7 @@ struct DWArgs {
     DWProb p[DW_MAXP];
     int tile_start[DW_MAXP + 1];
     int nprob, nchunks, mchunk;
+    float out_scale;          // 1 / the backward seed scale (fp16 images), 1 otherwise
     size_t ldm;
     const int8_t* seg;
 };
@@ -60,7 +75,7 @@ __device__ inline u32x4 extra_frag(int extra, int q, const int8_t* seg_lds) {
     return __builtin_bit_cast(u32x4, e);
 }
 
-// fragment of a staged operand: feature f (0..127 within the tile), 16-B chunk c (0..7)
+// fragment of a staged operand: feature f (within the tile), 16-B chunk c (0..7)
 __device__ inline u32x4 dw_lds_frag(const uint8_t* img, int f, int c) {
     return *reinterpret_cast<const u32x4*>(img + f * DW_LINE + ((c ^ (f & 7)) << 4));
 }
@@ -76,46 +91,49 @@ __device__ inline void vm_wait() {
 // register allocator sees one uniform accumulator set per loop (a data-dependent MFMA inside
 // one loop made hipcc shuttle the accumulators between AGPRs and VGPRs every k-step).
 // SEGLD: this wave also copies the stage's seg bytes (ONEHOT extra rows).
-template <class P, bool EXTRA, bool SEGLD>
+template <class P, int WK, bool EXTRA, bool SEGLD>
 __device__ __forceinline__ void dw_loop(uint8_t* smem, const DWArgs& a, const DWProb& pr, int nst, size_t m_begin,
-                                        int k_base, int n_base, int wave, int lane,
-                                        const typename P::AT* const (&srcA)[4], const typename P::AT* const (&srcB)[4],
+                                        int wave, int lane, const typename P::AT* const (&srcA)[DWGeom<WK>::AI],
+                                        const typename P::AT* const (&srcB)[DWGeom<WK>::BI],
                                         f32x4 (&acc)[4][4], f32x4 (&acce)[4]) {
+    using G = DWGeom<WK>;
     constexpr int BK = DW_LINE / (int)sizeof(typename P::AT);
-    constexpr int OPS = 8 + (SEGLD ? 1 : 0);            // vector-memory ops per stage per wave
+    constexpr int OPS = G::AI + G::BI + (SEGLD ? 1 : 0);      // vector-memory ops per stage per wave
     const int wr = wave >> 1, wc = wave & 1;
     const int fr = lane & 15, cq = lane >> 4;
     auto issue = [&](int st) {
-        uint8_t* base = smem + (st % DW_RING) * DW_SLOT;
+        uint8_t* base = smem + (st % G::RING) * G::SLOT;
         const size_t off = (size_t)st * BK;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ins = wave + 4 * i;
-            __builtin_amdgcn_global_load_lds((void*)(srcA[i] + off), (lds_void_t*)(base + ins * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((void*)(srcB[i] + off), (lds_void_t*)(base + DW_OPB + ins * 1024), 16, 0, 0);
-        }
+        for (int i = 0; i < G::AI; ++i)
+            __builtin_amdgcn_global_load_lds((void*)(srcA[i] + off), (lds_void_t*)(base + (wave + G::W * i) * 1024), 16,
+                                             0, 0);
+#pragma unroll
+        for (int i = 0; i < G::BI; ++i)
+            __builtin_amdgcn_global_load_lds((void*)(srcB[i] + off),
+                                             (lds_void_t*)(base + G::AOPB + (wave + G::W * i) * 1024), 16, 0, 0);
         if constexpr (SEGLD) {   // BK seg bytes, 4 per lane (lanes past BK/4 fetch bytes nobody reads)
             const int8_t* sg = a.seg + m_begin + off + 4 * (lane < BK / 4 ? lane : 0);
-            __builtin_amdgcn_global_load_lds((void*)sg, (lds_void_t*)(base + 2 * DW_OPB), 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((void*)sg, (lds_void_t*)(base + G::AOPB + DW_BOPB), 4, 0, 0);
         }
     };
 #pragma unroll
-    for (int p = 0; p < DW_RING - 1; ++p)
+    for (int p = 0; p < G::RING - 1; ++p)
         if (p < nst) issue(p);
     for (int st = 0; st < nst; ++st) {
         // this wave's copies of stage st have landed once at most (stages issued after it) * OPS
         // operations are outstanding; the barrier then covers every wave's copies, and every wave
         // has finished reading stage st - 1, whose slot the next issue reuses
         const int ahead = nst - 1 - st;
-        if (ahead >= DW_RING - 2) vm_wait<(DW_RING - 2) * OPS>();
+        if (ahead >= G::RING - 2) vm_wait<(G::RING - 2) * OPS>();
         else if (ahead == 1) vm_wait<OPS>();
         else vm_wait<0>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (st + DW_RING - 1 < nst) issue(st + DW_RING - 1);
-        const uint8_t* imA = smem + (st % DW_RING) * DW_SLOT;
-        const uint8_t* imB = imA + DW_OPB;
-        const int8_t* seg_lds = (const int8_t*)(imA + 2 * DW_OPB);
+        if (st + G::RING - 1 < nst) issue(st + G::RING - 1);
+        const uint8_t* imA = smem + (st % G::RING) * G::SLOT;
+        const uint8_t* imB = imA + G::AOPB;
+        const int8_t* seg_lds = (const int8_t*)(imB + DW_BOPB);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             u32x4 A[4], B[4];
@@ -147,14 +165,15 @@ static int dw_device_cus() {
     return n;
 }
 
-template <class P>
-__global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
+template <class P, int WK>
+__global__ __launch_bounds__(DWGeom<WK>::W * 64) void dw_kernel(DWArgs a) {
     using AT = typename P::AT;
+    using G = DWGeom<WK>;
     constexpr int BK = DW_LINE / (int)sizeof(AT);     // rows per stage: 64 bf16 / 32 fp32
     constexpr int EPC = 16 / (int)sizeof(AT);         // elements per 16-B chunk
     // one LDS object (a second __shared__ array can make hipcc drain the glds queue at every
     // fragment read): the ring of [A | B | seg] stage slots
-    __shared__ __attribute__((aligned(1024))) uint8_t smem[DW_RING * DW_SLOT];
+    __shared__ __attribute__((aligned(1024))) uint8_t smem[G::RING * G::SLOT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // XCD-aware order: block b runs on XCD b % 8; XCD x takes the contiguous logical range
     // [x*per, (x+1)*per) of the chunk-major order, so the tiles that share one m-chunk's operand
@@ -171,7 +190,7 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
     const DWProb& pr = a.p[pi];
     const int lt = tile - a.tile_start[pi];
     const int kt = lt / pr.ntiles, nt = lt % pr.ntiles;
-    const int k_base = kt * DW_T, n_base = nt * DW_T;
+    const int k_base = kt * WK, n_base = nt * DW_TN;
     const int wr = wave >> 1, wc = wave & 1;
     const size_t m_begin = (size_t)chunk * a.mchunk;
     const size_t m_end = m_begin + a.mchunk < a.ldm ? m_begin + a.mchunk : a.ldm;
@@ -183,17 +202,21 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
     const bool do_extra = wg_extra && wr == 0;
     const bool seg_ld = do_extra && pr.extra == EXTRA_ONEHOT;
 
-    // per-lane glds sources for this wave's 4 A + 4 B wave-instructions (features ins*8 + lane/8)
-    const AT* srcA[4];
-    const AT* srcB[4];
+    // per-lane glds sources of this wave's A and B wave-instructions (features ins*8 + lane/8)
+    const AT* srcA[G::AI];
+    const AT* srcB[G::BI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int ins = wave + 4 * i;
-        const int f = ins * 8 + (lane >> 3);
+    for (int i = 0; i < G::AI; ++i) {
+        const int f = (wave + G::W * i) * 8 + (lane >> 3);
         const int c = (lane & 7) ^ (f & 7);
         int fa = k_base + f; fa = fa < pr.Kx ? fa : pr.Kx - 1;
-        int fb = n_base + f; fb = fb < pr.N ? fb : pr.N - 1;
         srcA[i] = XT + (size_t)fa * a.ldm + m_begin + c * EPC;
+    }
+#pragma unroll
+    for (int i = 0; i < G::BI; ++i) {
+        const int f = (wave + G::W * i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ (f & 7);
+        int fb = n_base + f; fb = fb < pr.N ? fb : pr.N - 1;
         srcB[i] = DT + (size_t)fb * a.ldm + m_begin + c * EPC;
     }
     f32x4 acc[4][4], acce[4];
@@ -203,10 +226,10 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) zero_acc(acc[i][j]);
     }
-    // waves 2,3 of an extra tile run the plain loop; the barrier count per stage is identical
-    if (seg_ld) dw_loop<P, true, true>(smem, a, pr, nst, m_begin, k_base, n_base, wave, lane, srcA, srcB, acc, acce);
-    else if (do_extra) dw_loop<P, true, false>(smem, a, pr, nst, m_begin, k_base, n_base, wave, lane, srcA, srcB, acc, acce);
-    else dw_loop<P, false, false>(smem, a, pr, nst, m_begin, k_base, n_base, wave, lane, srcA, srcB, acc, acce);
+    // the other waves of an extra tile run the plain loop; the barrier count per stage is identical
+    if (seg_ld) dw_loop<P, WK, true, true>(smem, a, pr, nst, m_begin, wave, lane, srcA, srcB, acc, acce);
+    else if (do_extra) dw_loop<P, WK, true, false>(smem, a, pr, nst, m_begin, wave, lane, srcA, srcB, acc, acce);
+    else dw_loop<P, WK, false, false>(smem, a, pr, nst, m_begin, wave, lane, srcA, srcB, acc, acce);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -215,7 +238,7 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int k = k_base + wr * 64 + i * 16 + crow(lane, r);
-                if (k < pr.Kx && n < pr.N) atomicAdd(pr.G + (size_t)k * pr.N + n, acc[i][j][r]);
+                if (k < pr.Kx && n < pr.N) atomicAdd(pr.G + (size_t)k * pr.N + n, acc[i][j][r] * a.out_scale);
             }
         }
     if (do_extra) {
@@ -227,9 +250,9 @@ __global__ __launch_bounds__(256) void dw_kernel(DWArgs a) {
             for (int r = 0; r < 4; ++r) {
                 const int q = crow(lane, r);
                 if (pr.extra == EXTRA_ONES) {
-                    if (q == 0) atomicAdd(pr.Gx + n, acce[j][r]);
+                    if (q == 0) atomicAdd(pr.Gx + n, acce[j][r] * a.out_scale);
                 } else {
-                    atomicAdd(pr.Gx + (size_t)q * pr.N + n, acce[j][r]);
+                    atomicAdd(pr.Gx + (size_t)q * pr.N + n, acce[j][r] * a.out_scale);
                 }
             }
         }
@@ -506,12 +529,21 @@ extern "C" size_t dppo_ppo_workspace_bytes(const dppo_dims* d, int precision, in
 }
 
 template <class P>
-static int launch_dw(const DWArgs& a, hipStream_t s) {
+static int launch_dw(const DWArgs& a, int wk, hipStream_t s) {
     const int tiles = a.tile_start[a.nprob];
     const int64_t blocks = 8 * (((int64_t)tiles * a.nchunks + 7) / 8);   // whole XCD rounds
-    hipLaunchKernelGGL(dw_kernel<P>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    if (wk == 256)
+        hipLaunchKernelGGL((dw_kernel<P, 256>), dim3((unsigned)blocks), dim3(DWGeom<256>::W * 64), 0, s, a);
+    else
+        hipLaunchKernelGGL((dw_kernel<P, 128>), dim3((unsigned)blocks), dim3(DWGeom<128>::W * 64), 0, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
+}
+
+// k-tile edge of the grouped dW launches (DPPO_DW_TK = 128 / 256: measurement knob)
+static int dw_tk() {
+    static const int tk = [] { const char* e = getenv("DPPO_DW_TK"); return e && atoi(e) == 128 ? 128 : 256; }();
+    return tk;
 }
 
 // one non-blocking side stream (+ fork/join events) per device and host thread, created on first use;
@@ -569,7 +601,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
-    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
     DPPO_CHECK(hp && packed_ft && packed_critic && actor_params && sched && obs && chains && lp_old_mean && advantages &&
                returns && workspace && grads && metrics, "dppo_ppo_minibatch: null pointer");
     DPPO_CHECK(total > 0 && total % D.KF == 0, "dppo_ppo_minibatch: total must be a positive multiple of K'");
@@ -623,7 +655,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     lh.clip_coef_base = hp->clip_ploss_coef_base; lh.clip_coef_rate = hp->clip_ploss_coef_rate;
     lh.min_lp_std = hp->min_logprob_std; lh.vf_coef = hp->vf_coef; lh.norm_adv = hp->norm_adv;
     lh.reward_horizon = hp->reward_horizon;
-    lh.grad_scale = hp->loss_scale / (float)hp->global_rows;
+    // fp16: the backward images carry GRAD_SCALE x the gradient (fp16 range); dW divides it out
+    lh.grad_scale = hp->loss_scale / (float)hp->global_rows * dppo_grad_scale(precision);
 
     ActorArgs aa = {};
     aa.packed = (const uint8_t*)packed_ft;
@@ -642,12 +675,13 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     // m-chunks: about one workgroup per CU (the ring takes 132 KB of LDS) in a single round.
     // DPPO_DW_CHUNKS overrides the chunk count (a measurement knob).
     static const int env_ch = [] { const char* e = getenv("DPPO_DW_CHUNKS"); return e ? atoi(e) : 0; }();
+    const int tk = dw_tk();
     auto launch_grads = [&](bool actor, hipStream_t st) -> int {
         DWArgs w = {};
         auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
             DWProb& p = w.p[w.nprob];
             p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
-            p.ktiles = dppo_cdiv(Kx, DW_T); p.ntiles = dppo_cdiv(N, DW_T);
+            p.ktiles = dppo_cdiv(Kx, tk); p.ntiles = dppo_cdiv(N, DW_TN);
             w.tile_start[w.nprob + 1] = w.tile_start[w.nprob] + p.ktiles * p.ntiles;
             w.nprob++;
         };
@@ -664,6 +698,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         }
         w.ldm = ws.ldm;
         w.seg = ws.seg;
+        w.out_scale = 1.f / dppo_grad_scale(precision);
         const int tiles = w.tile_start[w.nprob];
         int nch = env_ch > 0 ? env_ch : dw_device_cus() / tiles;
         const int max_ch = (int)(ws.ldm / 64);
@@ -671,7 +706,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (nch < 1) nch = 1;
         w.mchunk = (int)(dppo_cdiv((int)ws.ldm, nch * 64) * 64);
         w.nchunks = dppo_cdiv((int)ws.ldm, w.mchunk);
-        return precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, st) : launch_dw<PolicyF32>(w, st);
+        return precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, tk, st)
+             : precision == DPPO_F16  ? launch_dw<PolicyF16>(w, tk, st) : launch_dw<PolicyF32>(w, tk, st);
     };
 
     // The critic is independent of the actor: its row tiles and then its weight gradients run on a
@@ -747,7 +783,7 @@ extern "C" int dppo_ppo_minibatch_part(const dppo_dims* d, int precision, const 
 // are added in a fixed order (no global atomics: one writer per (q, n)).
 template <class AT>
 __global__ __launch_bounds__(256) void seg_reduce_kernel(const AT* __restrict__ dT, const int8_t* __restrict__ seg,
-                                                         size_t ldm, int nb, float* __restrict__ G, int H) {
+                                                         size_t ldm, int nb, float* __restrict__ G, int H, float scale) {
     __shared__ float bins[4][64];
     const int n = blockIdx.x, tid = threadIdx.x, wave = tid >> 6;
     for (int i = tid; i < 4 * 64; i += 256) (&bins[0][0])[i] = 0.f;
@@ -759,7 +795,7 @@ __global__ __launch_bounds__(256) void seg_reduce_kernel(const AT* __restrict__ 
         if (q >= 0 && q < nb) atomicAdd(&bins[wave][q], (float)row[r]);
     }
     __syncthreads();
-    if (tid < nb) G[(size_t)tid * H + n] = (bins[0][tid] + bins[1][tid]) + (bins[2][tid] + bins[3][tid]);
+    if (tid < nb) G[(size_t)tid * H + n] = ((bins[0][tid] + bins[1][tid]) + (bins[2][tid] + bins[3][tid])) * scale;
 }
 
 extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const void* packed_actor, const float* actor_params,
@@ -769,7 +805,7 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
-    DPPO_CHECK(precision == DPPO_F32 || precision == DPPO_BF16, "bad precision %d", precision);
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
     DPPO_CHECK(packed_actor && actor_params && sched && qsched && x_start && cond && t && noise && workspace && grads &&
                metrics, "dppo_pretrain_minibatch: null pointer");
     DPPO_CHECK(rows > 0 && global_rows >= rows, "dppo_pretrain_minibatch: bad rows / global_rows");
@@ -794,15 +830,16 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     aa.mode = ROWS_PRETRAIN; aa.nrows = rows; aa.ws = ws; aa.metrics = metrics;
     aa.tsteps = t; aa.noise = noise; aa.qsched = qsched;
     // loss = mean over global_rows * XD elements of (eps - noise)^2 (diffusion.py:192)
-    aa.pre_scale = 2.f * loss_scale / ((float)global_rows * (float)D.XD);
+    aa.pre_scale = 2.f * loss_scale / ((float)global_rows * (float)D.XD) * dppo_grad_scale(precision);
     rc = launch_actor_rowtile(aa, precision, s);
     if (rc) return rc;
 
+    const int tk = dw_tk();
     DWArgs w = {};
     auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
         DWProb& p = w.p[w.nprob];
         p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
-        p.ktiles = dppo_cdiv(Kx, DW_T); p.ntiles = dppo_cdiv(N, DW_T);
+        p.ktiles = dppo_cdiv(Kx, tk); p.ntiles = dppo_cdiv(N, DW_TN);
         w.tile_start[w.nprob + 1] = w.tile_start[w.nprob] + p.ktiles * p.ntiles;
         w.nprob++;
     };
@@ -813,6 +850,7 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
     w.ldm = ws.ldm;
     w.seg = ws.seg;
+    w.out_scale = 1.f / dppo_grad_scale(precision);
     const int tiles = w.tile_start[w.nprob];
     int nch = dw_device_cus() / tiles;
     const int max_ch = (int)(ws.ldm / 64);
@@ -820,14 +858,19 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     if (nch < 1) nch = 1;
     w.mchunk = (int)(dppo_cdiv((int)ws.ldm, nch * 64) * 64);
     w.nchunks = dppo_cdiv((int)ws.ldm, w.mchunk);
-    rc = precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, s) : launch_dw<PolicyF32>(w, s);
+    rc = precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, tk, s)
+       : precision == DPPO_F16  ? launch_dw<PolicyF16>(w, tk, s) : launch_dw<PolicyF32>(w, tk, s);
     if (rc) return rc;
+    const float inv = 1.f / dppo_grad_scale(precision);
     if (precision == DPPO_BF16)
         hipLaunchKernelGGL(seg_reduce_kernel<__bf16>, dim3(D.H), dim3(256), 0, s, (const __bf16*)ws.dh1T, ws.seg, ws.ldm,
-                           D.K, ws.gseg, D.H);
+                           D.K, ws.gseg, D.H, inv);
+    else if (precision == DPPO_F16)
+        hipLaunchKernelGGL(seg_reduce_kernel<_Float16>, dim3(D.H), dim3(256), 0, s, (const _Float16*)ws.dh1T, ws.seg,
+                           ws.ldm, D.K, ws.gseg, D.H, inv);
     else
         hipLaunchKernelGGL(seg_reduce_kernel<float>, dim3(D.H), dim3(256), 0, s, (const float*)ws.dh1T, ws.seg, ws.ldm,
-                           D.K, ws.gseg, D.H);
+                           D.K, ws.gseg, D.H, inv);
     DPPO_HIP(hipGetLastError());
     return launch_time_bwd(D, ws.gseg, actor_params, ga, D.K, 1, s);
 }

@@ -13,8 +13,10 @@
  *     nothing; scratch comes from a caller-owned workspace sized by the *_workspace_bytes query;
  *   - return 0 on success, a DPPO_E* code otherwise; dppo_last_error() gives the message
  *     (thread-local); no C++ exception crosses the ABI;
- *   - precision: DPPO_F32 = f32-input MFMA (exact fp32 products, the parity mode) or
- *     DPPO_BF16 = bf16 MFMA with fp32 accumulation and an fp32 DDPM/loss epilogue;
+ *   - precision: DPPO_F32 = f32-input MFMA (exact fp32 products, the parity mode),
+ *     DPPO_BF16 = bf16 MFMA with fp32 accumulation and an fp32 DDPM/loss epilogue, or
+ *     DPPO_F16 = the same with fp16 operands (BASELINE config 5; the backward images carry the
+ *     gradient times 4096 for fp16's range, removed exactly in the fp32 weight gradients);
  *   - flat parameter layout (fp32, Keras kernel [in,out] row-major, then bias [out]):
  *       actor : time_w1[TD,2TD] time_b1[2TD] time_w2[2TD,TD] time_b2[TD]
  *               in_w[XD+TD+SD, H] in_b[H] l1_w[H,H] l1_b[H] l2_w[H,H] l2_b[H] out_w[H,XD] out_b[XD]
@@ -31,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 2
+#define DPPO_ABI_VERSION 3
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -40,7 +42,7 @@ extern "C" {
 #endif
 
 enum { DPPO_OK = 0, DPPO_EINVAL = 1, DPPO_EHIP = 2, DPPO_EUNSUPPORTED = 3 };
-enum { DPPO_F32 = 0, DPPO_BF16 = 1 };
+enum { DPPO_F32 = 0, DPPO_BF16 = 1, DPPO_F16 = 2 };
 enum { DPPO_ADAMW_KERAS = 0, DPPO_ADAMW_TORCH = 1 };
 
 /* Model / schedule dimensions (cfg keys of cfg/gym/finetune/hopper-v2/ft_ppo_diffusion_mlp.yaml:18-25,78-110). */

@@ -150,6 +150,22 @@ def round_bf16(x):
     return u.astype(np.uint32).view(np.float32).astype(np.float64)
 
 
+def round_fp16(x):
+    """fp32 -> fp16 round-to-nearest-even -> back (v_cvt_pk_f16_f32; the fp16 operand policy)."""
+    return np.asarray(x, np.float32).astype(np.float16).astype(np.float64)
+
+
+FP16_GRAD_SCALE = 4096.0
+
+
+def _round_fp16_grad(x):
+    """The fp16 kernels store backward images as fp16(GRAD_SCALE * g) (PolicyF16, dppo_common.cuh)."""
+    return round_fp16(np.asarray(x, np.float64) * FP16_GRAD_SCALE) / FP16_GRAD_SCALE
+
+
+round_fp16.grad_round = _round_fp16_grad
+
+
 def _ident(x):
     return np.asarray(x, np.float64)
 
@@ -177,20 +193,21 @@ def residual_mlp_backward(p, cache, dy, act, prefix):
     from fp32 parameters)."""
     _, ag = ACT[act]
     R = cache.get("R", _ident)
+    Rg = getattr(R, "grad_round", R)        # rounding of the gradient images (fp16: scaled)
     g = {}
-    dyr = R(dy)
+    dyr = Rg(dy)
     g[prefix + "out_w"] = cache["h3"].T @ dyr
     g[prefix + "out_b"] = dyr.sum(0)
     dh3 = dyr @ R(p[prefix + "out_w"]).T
-    dh3r = R(dh3)
+    dh3r = Rg(dh3)
     g[prefix + "l2_w"] = cache["u2"].T @ dh3r
     g[prefix + "l2_b"] = dh3r.sum(0)
     du2 = dh3r @ R(p[prefix + "l2_w"]).T
-    dh2 = R(du2 * ag(cache["h2"]))
+    dh2 = Rg(du2 * ag(cache["h2"]))
     g[prefix + "l1_w"] = cache["u1"].T @ dh2
     g[prefix + "l1_b"] = dh2.sum(0)
     du1 = dh2 @ R(p[prefix + "l1_w"]).T
-    dh1 = R(dh3r + du1 * ag(cache["h1"]))   # the kernels re-read dh3 from its (rounded) LDS tile
+    dh1 = Rg(dh3r + du1 * ag(cache["h1"]))   # the kernels re-read dh3 from its (rounded) LDS tile
     g[prefix + "in_w"] = cache["x"].T @ dh1
     g[prefix + "in_b"] = dh1.sum(0)
     dx = dh1 @ np.asarray(p[prefix + "in_w"], np.float64).T

@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 def test_agent_iterations(cuda, precision, tmp_path):
     from diffusionpolicyoptimization_amd.util.config import get_class, load_config
     cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
@@ -379,7 +379,12 @@ def test_keras_checkpoints_round_trip_through_the_model(cuda, tmp_path):
     m2 = instantiate(cfg.model, device=cuda, seed=4)
     m2.load_weights(p)
     assert torch.equal(m2.base_params, m.base_params) and torch.equal(m2.train_params, m.train_params)
-    assert torch.equal(m2.packed_ft, m.packed_ft) and torch.equal(m2.packed_critic, m.packed_critic)
+    # the repacked images serve the same policy (image padding bytes are not compared)
+    cond = torch.rand(16, m.dims.sd, device=cuda) * 2 - 1
+    m._call_id = m2._call_id = 0
+    m2.seed = m.seed
+    assert torch.equal(m(cond).trajectories, m2(cond).trajectories)
+    assert torch.equal(m.critic_values(cond), m2.critic_values(cond))
     net = str(tmp_path / "state_785.weights.h5")
     keras_weights.save_actor(net, ops.unflatten_params(m.actor_spec, m.actor_ft_params.cpu().numpy()))
     m3 = instantiate(cfg.model, device=cuda, network_path=net)

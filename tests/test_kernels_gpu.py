@@ -37,10 +37,10 @@ def _setup(dims, cuda, seed=0, eta=1.0):
 
 
 def _rnd(precision):
-    return O.round_bf16 if precision == "bf16" else None
+    return {"bf16": O.round_bf16, "fp16": O.round_fp16}.get(precision)
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 2e-4), ("bf16", 2e-3)])
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-4), ("bf16", 2e-3), ("fp16", 1e-3)])
 @pytest.mark.parametrize("dims", [HOPPER, WALKER], ids=["hopper", "walker"])
 def test_sampler_injected_noise(cuda, precision, tol, dims):
     """fp32: vs the exact f64 oracle. bf16: vs the oracle rounding operands to bf16 at the
@@ -54,7 +54,7 @@ def test_sampler_injected_noise(cuda, precision, tol, dims):
     xT = rng.standard_normal((E, d.horizon_steps, d.action_dim)).astype(np.float32)
     z = rng.standard_normal((d.denoising_steps, E, d.horizon_steps, d.action_dim)).astype(np.float32)
     split = ops.sampler_layout(d, precision, E) > 0
-    assert split == (precision == "bf16"), "bf16 at 37 envs runs the split sampler by default"
+    assert split == (precision != "fp32"), "bf16 / fp16 at 37 envs run the split sampler by default"
     ref_a, ref_c = O.sample(to_f64(base), to_f64(ft), sched, state.astype(np.float64), xT, z, d.ft_denoising_steps,
                             rnd=_rnd(precision), round_h3=not split)
     packb, packf = ops.pack_actor(d, pb, precision), ops.pack_actor(d, pf, precision)
@@ -129,6 +129,35 @@ def test_sampler_bf16_sizes_philox(cuda, E, dims):
     assert dev.max() < 0.1, dev.max()
 
 
+def test_sampler_fp16_ddim_config5(cuda):
+    """BASELINE config 5's per-GPU workload: DDIM 10 rows over K = 20, 512 envs per GPU, fp16
+    operands, the split sampler at its maximum (256 workgroups), the kernel's own Philox noise;
+    against the oracle rounding operands to fp16 at the kernel's rounding points (parity-unpinned
+    like every DDIM result: the reference DDIM path cannot run)."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER_DDIM, cuda)
+    E, seed, call = 512, 424242, 9
+    assert ops.sampler_layout(d, "fp16", E) > 0
+    rng = np.random.default_rng(55)
+    state = rng.uniform(-1, 1, (E, 1, d.obs_dim)).astype(np.float32)
+    S = d.denoising_steps
+    xT = PX.sampler_normals(seed, call, 0, E, d.xd, S).reshape(E, d.horizon_steps, d.action_dim)
+    z = np.stack([PX.sampler_normals(seed, call, 0, E, d.xd, i) for i in range(S)])
+    z = z.reshape(S, E, d.horizon_steps, d.action_dim)
+    ref_a, ref_c = O.sample(to_f64(base), to_f64(ft), sched, state.astype(np.float64), xT, z, d.ft_denoising_steps,
+                            rnd=O.round_fp16, round_h3=False)
+    packb, packf = ops.pack_actor(d, pb, "fp16"), ops.pack_actor(d, pf, "fp16")
+    act, ch = ops.sample(d, "fp16", packb, packf, tab, torch.tensor(state.reshape(E, -1), device=cuda),
+                         seed=seed, call_id=call)
+    torch.cuda.synchronize()
+    dev = np.abs(act.cpu().numpy().reshape(ref_a.shape) - ref_a)
+    assert np.isfinite(dev).all()
+    assert np.quantile(dev, 0.99) < 1e-3 and np.abs(ch.cpu().numpy().reshape(ref_c.shape) - ref_c).mean() < 1e-3, \
+        (dev.max(), np.quantile(dev, 0.99))
+    assert dev.max() < 0.1, dev.max()
+
+
 def test_sampler_split_repeatable(cuda):
     """Back-to-back launches of the split sampler on the same stream reuse one exchange buffer with
     new tags: identical inputs give bit-identical outputs, launch after launch."""
@@ -146,7 +175,7 @@ def test_sampler_split_repeatable(cuda):
         assert torch.equal(o, outs[0])
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 2e-4), ("bf16", 3e-3)])
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-4), ("bf16", 3e-3), ("fp16", 2e-3)])
 def test_sampler_ddim(cuda, precision, tol):
     """BASELINE config 5's DDIM sampler (10 rows over K = 20, eta = 1) vs the oracle's DDIM
     restatement (parity-unpinned: the reference DDIM path cannot run)."""
@@ -232,7 +261,7 @@ def test_sampler_deterministic_and_empty(cuda):
     ops.sample(d, "fp32", packb, packf, tab, torch.zeros(0, d.sd, device=cuda))
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 2e-3)])
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 2e-3), ("fp16", 2e-3)])
 @pytest.mark.parametrize("dims", [HOPPER, WALKER], ids=["hopper", "walker"])
 def test_logprob(cuda, precision, tol, dims):
     import torch
@@ -255,7 +284,7 @@ def test_logprob(cuda, precision, tol, dims):
     assert np.abs(lpm.cpu().numpy() - ref_mean).max() < tol * 10
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("bf16", 1e-3)])
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("bf16", 1e-3), ("fp16", 1e-3)])
 def test_critic_forward(cuda, precision, tol):
     import torch
     from diffusionpolicyoptimization_amd import ops
@@ -339,7 +368,8 @@ def test_adamw(cuda, mode):
 @pytest.mark.parametrize("precision,case,rtol", [("fp32", "perturbed", 2e-3), ("fp32", "ratio1", 2e-3),
                                                   ("bf16", "ratio1", 1e-2), ("bf16", "perturbed", 2e-2),
                                                   ("fp32", "perturbed-ddim", 2e-3), ("fp32", "perturbed-walker", 2e-3),
-                                                  ("bf16", "ratio1-walker", 1e-2)])
+                                                  ("bf16", "ratio1-walker", 1e-2), ("fp16", "ratio1", 1e-2),
+                                                  ("fp16", "ratio1-ddim", 1e-2)])
 def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     """c_loss forward metrics and gradients of pg_loss + 0.5 v_loss vs the oracle.
 
@@ -410,7 +440,7 @@ def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     assert not bad, (bad, {k: float(v) for k, v in errs.items()})
 
 
-@pytest.mark.parametrize("precision,rtol", [("fp32", 2e-3), ("bf16", 1e-2)])
+@pytest.mark.parametrize("precision,rtol", [("fp32", 2e-3), ("bf16", 1e-2), ("fp16", 1e-2)])
 @pytest.mark.parametrize("dims", [HOPPER, WALKER], ids=["hopper", "walker"])
 def test_pretrain_loss_grads(cuda, precision, rtol, dims):
     """§8(f) row 3: p_losses / q_sample (diffusion.py:179-202) through the TRAIN row tile
@@ -512,7 +542,7 @@ def test_logprob_pass_full_size(cuda):
     assert np.abs(lpm.cpu().numpy()[pick] - ref_m).max() < 1e-4
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 def test_ppo_minibatch_full_size(cuda, precision):
     """dppo_ppo_minibatch at the bench's minibatch, b = 50,000 rows (782 64-row actor tiles, the
     32-row tail launch, split-K dW over all rows), over a 64,000-row rollout. The full-size launch is
