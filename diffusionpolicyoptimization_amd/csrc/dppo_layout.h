@@ -12,6 +12,13 @@
 //   T_L1   packed bwd  W_l1^T  as [K=H][N=H]
 //   TEMB   fp32 [K][TD] time embeddings t_emb(t) for t = 0..K-1 (actor only; derived from TIME at
 //          pack time, so no kernel re-evaluates the time MLP per launch)
+// and, for an actor, three segments derived for the split sampler (sampler_split.hip), whose
+// in-Dense then only multiplies the per-step inputs:
+//   W_XS   packed fwd  W_in rows [x ; state] (in-Dense input rows 0..XD-1 and XD+TD..in_dim-1)
+//   TIN    fp32 [K][H] b_in + W_in[temb rows]^T t_emb(t): the in-Dense's time part per t (2-byte
+//          precisions: operands rounded as the kernels round them, fp32 sums)
+//   B_OUT2 fp32 [16*ceil(out/16)] b_out + W_out^T b_l2: the l2 bias folded through the out-Dense
+//          (the residual block is linear from the l2 product to the out-Dense, mlp.py:186-206)
 // A packed matrix [K][N] is ceil(N/16) n-tiles x KS k-steps x 64 lanes x 16 B, with
 // KS = ceil(K / KG) rounded up to EVEN (the weight stream runs in k-step pairs), KG = 32 (bf16)
 // or 16 (fp32). Lane l of (ntile, ks) holds, for e < EPL,
@@ -27,7 +34,7 @@
 #endif
 
 enum MlpSeg { SEG_TIME = 0, SEG_W_IN, SEG_B_IN, SEG_W_L1, SEG_B_L1, SEG_W_L2, SEG_B_L2, SEG_W_OUT, SEG_B_OUT,
-              SEG_T_OUT, SEG_T_L2, SEG_T_L1, SEG_TEMB, SEG_COUNT };
+              SEG_T_OUT, SEG_T_L2, SEG_T_L1, SEG_TEMB, SEG_W_XS, SEG_TIN, SEG_B_OUT2, SEG_COUNT };
 
 struct MlpLayout {
     int in_dim, hidden, out_dim, time_dim, precision, temb_steps;
@@ -72,6 +79,10 @@ DPPO_HD inline MlpLayout make_mlp_layout(int in_dim, int hidden, int out_dim, in
     L.off[SEG_T_L2] = o; o = dppo_align256(o + packed_matrix_bytes(hidden, hidden, L.KG));
     L.off[SEG_T_L1] = o; o = dppo_align256(o + packed_matrix_bytes(hidden, hidden, L.KG));
     L.off[SEG_TEMB] = o; o = dppo_align256(o + (size_t)4 * L.temb_steps * time_dim);
+    const int xs_rows = time_dim > 0 ? in_dim - time_dim : 0;     // [x ; state]
+    L.off[SEG_W_XS] = o; o = dppo_align256(o + (xs_rows > 0 ? packed_matrix_bytes(xs_rows, hidden, L.KG) : 0));
+    L.off[SEG_TIN] = o; o = dppo_align256(o + (size_t)4 * L.temb_steps * hidden);
+    L.off[SEG_B_OUT2] = o; o = dppo_align256(o + (time_dim > 0 ? (size_t)4 * 16 * L.nt_out : 0));
     L.total = o;
     return L;
 }

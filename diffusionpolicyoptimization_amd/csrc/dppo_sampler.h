@@ -86,7 +86,7 @@ __device__ inline void sampler_load_state_tagged(const SampleArgs& a, int row0, 
 // touching the error message) when the shape is outside what it instantiates, or another error code.
 int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s);
 // whether the split sampler takes this shape (same test launch_sample_split applies)
-bool sample_split_supported(int precision, int H, int XD, int ks_in, int E, int K);
-// workgroups (CUs) per 16-env group of the split sampler
-int split_sampler_members();
+bool sample_split_supported(int precision, int H, int XD, int SD, int ks_in, int E, int K);
+// workgroups (CUs) per 16-env group of the split sampler for this shape (4 or 8), 0 = not taken
+int split_members_for(int precision, int H, int XD, int SD, int ks_in, int E, int K);
 int sampler_device_cus();   // CUs of the current device (0 if unknown)

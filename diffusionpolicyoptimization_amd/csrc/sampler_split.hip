@@ -150,6 +150,9 @@ __device__ inline int xcc_id() {
 __device__ inline int slot_feature(int j, int e) { return e < 4 ? 4 * j + e : 16 + 4 * j + (e - 4); }
 
 
+// relu as one v_med3_f32 (fmaxf(x, 0) canonicalises its MFMA-produced input first: two VALU ops)
+__device__ inline float relu_f(float x) { return __builtin_amdgcn_fmed3f(x, 0.f, __builtin_huge_valf()); }
+
 template <int CTRL>
 __device__ inline float dpp_f32(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
@@ -677,6 +680,493 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
     XPHASE(10);                                             // phase 10 = the done signal (member 0)
 }
 
+// ------------------------------------------------------------------------------------------------
+// P = 4 members per 16-env group (the default; DPPO_SPLIT_P=8 selects the kernel above). Halving
+// the members halves the exchange (tools/xchg_probe2.hip, sc0 one-XCD granules at 16 envs: P = 4
+// 0.98 us per step, P = 8 1.55 us) and the arrival skew it waits on, for 16 instead of 8 MFMAs per
+// wave in l1 and l2. Member c keeps 1/4 of the actor in registers (152 VGPRs at hopper's shape):
+//   in-Dense   W_in rows [x ; state] only (K = XD + SD <= 32 KX); the time part b_in + W_in^T
+//              t_emb(t) is the pack step's TIN table (dppo_layout.h), the MFMA accumulator's start
+//   l1         output columns [128c, 128c+128): wave w owns n-tile w over ALL 512 inputs, so its
+//              result is final (b_l1 is the accumulator's start) and leaves as bf16 relu(h2) for l2
+//   l2         input rows [128c, 128c+128), all outputs; member 0 starts the accumulator from the
+//              residual h1 (its own in-Dense registers: same features, same lane order), b_l2 is
+//              folded through the out-Dense into B_OUT2
+//   out-Dense  as above (hi/lo split of the member's partial h3 from registers)
+// so no wave adds a bias or a residual outside an MFMA, and no wave re-sums l1 partials.
+template <class Pol, int XQ, int KX, bool INJ>
+__global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
+    constexpr int P = 4;
+    constexpr int NO = (4 * XQ + 15) / 16;
+    using AT = typename Pol::AT;
+    auto pack_bf16x2 = [](float lo, float hi) { return Pol::pack2(lo, hi); };
+    constexpr int H = SPLIT_H, KSH = H / 32;
+    constexpr int HS = H / P;              // features per member slice (128)
+    constexpr int KS2 = HS / 32;           // l2 k-steps per member (4)
+    static_assert(HS / 16 == SW, "l1: one n-tile of the member slice per wave");
+    constexpr int NOC = 16 * NO;
+    constexpr int ST = SW * 64;
+    constexpr int pad = 16;
+    constexpr int ldh = H + pad;           // u1 row stride (2-byte elements)
+    constexpr int ldu2 = HS + pad;         // u2 row stride
+    constexpr int lda0 = KX * 32 + pad;    // a0 row stride
+    constexpr int XD = 4 * XQ;
+    constexpr int NV = 16 * XD;            // coordinates of a 16-env eps block
+    constexpr int NVW = NV / SW;           // per wave: 2 XD
+    constexpr int KW = (NVW + 15) / 16;    // sweep loads per lane (lane = 4 * slot + member)
+    constexpr int NB = H + NOC;            // per-actor bias floats: b_l1 | B_OUT2
+
+    const SampleArgs& a = sa.a;
+    const int b = blockIdx.x;
+    const int g = (b / (8 * P)) * 8 + b % 8, c = (b / 8) % P;
+    if (g >= sa.G) return;                 // whole workgroup: no barrier is skipped
+    XPHASE_START;
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int row0 = g * 16;
+    const MlpLayout& L = a.L;
+    const int SD = a.SD, K = a.K, KF = a.KF;
+    const int KSX = packed_ksteps(XD + SD, 32);   // k-step stride of the W_XS image
+
+    // ---- LDS carve (all offsets multiples of 16 B) ----
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    size_t o = 0;
+    AT* a0 = (AT*)(smem + o); o += dppo_align16(2 * 16 * lda0);
+    AT* u1 = (AT*)(smem + o); o += dppo_align16(2 * 16 * ldh);
+    AT* u2 = (AT*)(smem + o); o += dppo_align16(2 * 16 * ldu2);
+    float* part = (float*)(smem + o); o += dppo_align16(4 * SW * NV);      // [wave][16 x XD]
+    int* xfail = (int*)(smem + o); o += 16;                // [0] exchange failure, [1] exchange mode
+    float* xs = (float*)(smem + o); o += dppo_align16(4 * 16 * XD);
+    float* st = (float*)(smem + o); o += dppo_align16(4 * 16 * SD);
+    float* tin = (float*)(smem + o); o += dppo_align16(4 * K * H);
+    float* sch = (float*)(smem + o); o += dppo_align16(4 * K * DPPO_SCHED_COLS);
+    float* bias = (float*)(smem + o); o += dppo_align16(4 * 2 * NB);
+    float* zt = (float*)(smem + o); o += dppo_align16(4 * K * 16 * XD);
+    u32x4* wxs = (u32x4*)(smem + o); o += (size_t)SW * 4 * KX * 1024;     // [wave][n][ks] in-Dense fragments
+    u32x4* routl = (u32x4*)(smem + o); o += (size_t)SW * 2 * NO * 1024;   // [wave][s][n] out-Dense fragments
+
+    // ---- resident weight fragments (one actor at a time): l1 and l2 in registers; the in-Dense
+    //      and out-Dense fragments in this wave's own LDS (24 VGPRs the l1 pipeline needs) ----
+    const __amdgpu_buffer_rsrc_t rs_base = packed_rsrc(a.packed_base), rs_ft = packed_rsrc(a.packed_ft);
+    auto W = [&](int ft, int seg) { return wsrc(ft ? rs_ft : rs_base, L.off[seg]); };
+    u32x4 rl1[KSH], rl2[KS2][4];
+    // LDS-DMA of one 1 KiB fragment (lane l's 16 B land at dst + 16 l); wave-private destinations,
+    // consumed only after this wave's vmcnt(0)
+    auto dma_frag = [&](int ft, int seg, int KS, int ntile, int ks, u32x4* dst) {
+        const uint8_t* src = (ft ? a.packed_ft : a.packed_base) + L.off[seg] + ((size_t)(ntile * KS + ks) << 10) + 16 * lane;
+        __builtin_amdgcn_global_load_lds((void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    };
+    auto load_in = [&](int ft) {
+#pragma unroll
+        for (int ks = 0; ks < KX; ++ks)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) dma_frag(ft, SEG_W_XS, KSX, 4 * wave + n, ks, wxs + ((wave * 4 + n) * KX + ks) * 64);
+    };
+    auto load_l1 = [&](int ft) {
+#pragma unroll
+        for (int j = 0; j < KSH; ++j) rl1[j] = load_bfrag_c(W(ft, SEG_W_L1), KSH, (HS / 16) * c + wave, j, lane);
+    };
+    auto load_l2 = [&](int ft) {
+#pragma unroll
+        for (int s = 0; s < KS2; ++s)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) rl2[s][n] = load_bfrag_c(W(ft, SEG_W_L2), KSH, 4 * wave + n, c * KS2 + s, lane);
+    };
+    auto load_out = [&](int ft) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int n = 0; n < NO; ++n) dma_frag(ft, SEG_W_OUT, KSH, n, 2 * wave + s, routl + (wave * 2 * NO + s * NO + n) * 64);
+    };
+    // re-order the DMA'd out-Dense fragments in place to the transposed-result k-slot order
+    // (slot_feature), once per actor (one wave's LDS ops complete in order)
+    auto permute_out = [&]() {
+        u32x4* stg = routl + wave * 2 * NO * 64;
+        const int j = lane >> 4, q = lane & 15;
+        u32x4 pr[2][NO];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int n = 0; n < NO; ++n) {
+                const uint16_t* src = (const uint16_t*)(stg + (s * NO + n) * 64);
+                uint32_t w[4];
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2) {
+                    const int f0 = slot_feature(j, 2 * e2), f1 = slot_feature(j, 2 * e2 + 1);
+                    const uint32_t lo = src[(16 * (f0 >> 3) + q) * 8 + (f0 & 7)];
+                    const uint32_t hi = src[(16 * (f1 >> 3) + q) * 8 + (f1 & 7)];
+                    w[e2] = lo | (hi << 16);
+                }
+                pr[s][n] = u32x4{w[0], w[1], w[2], w[3]};
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int n = 0; n < NO; ++n) stg[(s * NO + n) * 64 + lane] = pr[s][n];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+
+    // announce this member's XCD (sc1 granule, tag = seq << 6: step tags are seq << 6 | i + 1)
+    uint64_t* const xann = sa.xbuf + 9 * XREGION + (size_t)g * P;
+    const uint32_t ann_tag = sa.seq << 6;
+    if (tid == 0)
+        __hip_atomic_store(xann + c, ((uint64_t)ann_tag << 32) | (uint32_t)xcc_id(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    const int ft0 = __builtin_amdgcn_readfirstlane(K - 1 < KF ? 1 : 0);
+    load_in(ft0); load_l1(ft0); load_l2(ft0); load_out(ft0);
+    int cur = ft0;
+
+    // ---- prologue: biases, in-Dense time tables, schedule, noise ----
+    for (int i4 = tid; i4 < 2 * NB / 4; i4 += ST) {
+        const int w = i4 / (NB / 4), j = 4 * (i4 % (NB / 4));
+        const uint8_t* PK = w ? a.packed_ft : a.packed_base;
+        ((float4*)bias)[i4] = j < H ? *((const float4*)(PK + L.off[SEG_B_L1]) + j / 4)
+                                    : *((const float4*)(PK + L.off[SEG_B_OUT2]) + (j - H) / 4);
+    }
+    // TIN row t of the actor that runs step t (base for t >= K', fine-tuned below)
+    for (int i4 = tid; i4 < K * H / 4; i4 += ST) {
+        const int t = 4 * i4 / H;
+        ((float4*)tin)[i4] = ((const float4*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIN]))[i4];
+    }
+    for (int i = tid; i < K * DPPO_SCHED_COLS; i += ST) sch[i] = a.sched[i];
+    const int XG = (XD + 3) / 4;
+    for (int it = tid; it < (K + 1) * 16 * XG; it += ST) {
+        const int step = it / (16 * XG), r = (it / XG) % 16, gq = it % XG, row = row0 + r;
+        float z[4];
+        if (step == K && a.x_T) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z[k] = (row < a.E && 4 * gq + k < XD) ? a.x_T[(size_t)row * XD + 4 * gq + k] : 0.f;
+        } else if (INJ && step < K) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                z[k] = (row < a.E && 4 * gq + k < XD) ? a.noise[((size_t)step * a.E + row) * XD + 4 * gq + k] : 0.f;
+        } else {
+            philox_normal4(a.seed, (uint32_t)gq, (uint32_t)(a.env_offset + row), (uint32_t)step, a.call_id, z);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = 4 * gq + k;
+            if (q >= XD) break;
+            if (step < K) {
+                zt[(step * 16 + r) * XD + q] = fminf(fmaxf(z[k], -a.randn_clip), a.randn_clip);
+            } else {
+                xs[r * XD + q] = z[k];
+                if (KF == K && c == 0 && a.chains && row < a.E) store_out(a.chains + ((size_t)row * (KF + 1) + 0) * XD + q, z[k]);
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0): the resident set has landed
+    permute_out();
+    // the group's exchange mode from the members' announcements (bounded like the exchange): every
+    // member sees the same P words, so all agree; a timeout selects the placement-independent form
+    if (wave == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
+        uint64_t v = ((uint64_t)ann_tag << 32);
+        bool ok = false;
+        for (;;) {
+            if (lane < P) v = __hip_atomic_load(xann + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__all(lane >= P || (uint32_t)(v >> 32) == ann_tag)) { ok = true; break; }
+            if (__builtin_amdgcn_s_memrealtime() > t_end) break;
+        }
+        const int x0 = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        const bool one_xcd = ok && !sa.force_shared && __all(lane >= P || (int)(uint32_t)v == x0);
+        if (lane == 0) xfail[1] = one_xcd ? 1 + x0 : 0;
+#ifdef DPPO_SAMPLER_TIMING
+        if (lane == 0 && c == 0) atomicAdd(&dppo_split_xmode_groups[one_xcd ? 1 : 0], 1u);
+#endif
+    }
+    __syncthreads();
+    // a0 = [x | state | 0]: everything but the state columns before the observation wait
+    constexpr int k1w = KX * 32;
+    for (int idx = tid; idx < 16 * k1w; idx += ST) {
+        const int r = idx / k1w, cc = idx % k1w;
+        if (cc >= XD && cc < XD + SD) continue;              // state columns: after the wait
+        a0[r * lda0 + cc] = Pol::cvt(cc < XD ? xs[r * XD + cc] : 0.f);
+    }
+    if (tid == 0) *xfail = 0;
+    XPHASE(7);
+    if (a.cond_tagged) {
+        sampler_load_state_tagged<ST>(a, row0, st, c == 0, tid);
+        XPHASE(8);
+        for (int i = tid; i < 16 * SD; i += ST) {
+            const int r = i / SD, cc = i % SD, row = row0 + r;
+            a0[r * lda0 + XD + cc] = Pol::cvt(st[i]);
+            if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, st[i]);
+        }
+    } else {
+        if (a.go) {
+            if (tid == 0) {
+                const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;   // 100 MHz: 4 s
+                while (__hip_atomic_load(a.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
+                    __builtin_amdgcn_s_sleep(8);
+                    if (__builtin_amdgcn_s_memrealtime() > t_end) {
+                        if (c == 0) __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");    // one system acquire after the match
+            }
+            __syncthreads();
+        }
+        XPHASE(8);
+        for (int i = tid; i < 16 * SD; i += ST) {
+            const int r = i / SD, cc = i % SD, row = row0 + r;
+            const float v = row < a.E ? a.cond[(size_t)row * SD + cc] : 0.f;
+            st[i] = v;
+            a0[r * lda0 + XD + cc] = Pol::cvt(v);
+            if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, v);
+        }
+    }
+    __syncthreads();
+    const int env = lane & 15, jq = lane >> 4;
+    const int xmode = __builtin_amdgcn_readfirstlane(xfail[1]);
+    uint64_t* const xregion = sa.xbuf + (size_t)xmode * XREGION;
+    XPHASE(0);
+    for (int i = 0; i < K; ++i) {
+        XSTEP(i);
+        const int t = K - 1 - i;
+        const int PK = __builtin_amdgcn_readfirstlane(t < KF ? 1 : 0);
+        const int PKn = __builtin_amdgcn_readfirstlane(t >= 1 && t - 1 < KF ? 1 : 0);
+        const bool pre = t >= 1 && PKn != PK;             // this step is the last of its actor
+        if (PK != cur) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            permute_out();
+            cur = PK;
+        }
+        XPHASE(1);
+        const float* bb = bias + PK * NB;
+        // ---- in-Dense (transposed): h1 = TIN[t] + W_xs^T [x; state]; no activation (mlp.py:144)
+        f32x4 h1[4];
+        {
+            u32x4 af[KX];
+#pragma unroll
+            for (int ks = 0; ks < KX; ++ks) af[ks] = lds_afrag<Pol>(a0, lda0, 0, ks, lane);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) h1[n] = *(const f32x4*)(tin + t * H + 16 * (4 * wave + n) + 4 * jq);
+#pragma unroll
+            for (int ks = 0; ks < KX; ++ks)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) h1[n] = Pol::mma(wxs[((wave * 4 + n) * KX + ks) * 64 + lane], af[ks], h1[n]);
+            // every LDS read (a0, TIN rows, fragments) in flight before the first MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, KX + 4 + 4 * KX, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 4 * KX, 0);
+            if (pre) load_in(PKn);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const int f = 16 * (4 * wave + n) + 4 * jq;
+                u32x2 pk;
+                pk[0] = pack_bf16x2(relu_f(h1[n][0]), relu_f(h1[n][1]));
+                pk[1] = pack_bf16x2(relu_f(h1[n][2]), relu_f(h1[n][3]));
+                *(u32x2*)(u1 + env * ldh + f) = pk;
+            }
+        }
+        XPHASE(11);
+        lds_sync();
+        XPHASE(2);
+        // ---- l1 (transposed): n-tile `wave` of this member's output columns over all 512 inputs,
+        //      from b_l1; out as u2 = bf16 relu(h2) (mlp.py:202-206)
+        {
+            f32x4 acc = *(const f32x4*)(bb + HS * c + 16 * wave + 4 * jq);
+            u32x4 fb[KSH];
+#pragma unroll
+            for (int j = 0; j < KSH; ++j) fb[j] = lds_afrag<Pol>(u1, ldh, 0, j, lane);
+#pragma unroll
+            for (int j = 0; j < KSH; ++j) acc = Pol::mma(rl1[j], fb[j], acc);
+            // schedule: the bias and L1D fragment reads first, then one read per MFMA, so L1D reads
+            // stay in flight ahead of the chain (left alone, hipcc issued read -> wait -> MFMA)
+            constexpr int L1D = 4;
+            __builtin_amdgcn_sched_group_barrier(0x100, L1D + 1, 0);
+#pragma unroll
+            for (int j = 0; j < KSH - L1D; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, L1D, 0);
+            if (pre) load_l1(PKn);
+            u32x2 pk;
+            pk[0] = pack_bf16x2(relu_f(acc[0]), relu_f(acc[1]));
+            pk[1] = pack_bf16x2(relu_f(acc[2]), relu_f(acc[3]));
+            *(u32x2*)(u2 + env * ldu2 + 16 * wave + 4 * jq) = pk;
+        }
+        XPHASE(12);
+        lds_sync();
+        XPHASE(3);
+        // ---- l2 (transposed) over this member's K-slice; member 0 starts from the residual h1
+        f32x4 h3[4];
+        {
+            u32x4 bf[KS2];
+#pragma unroll
+            for (int s = 0; s < KS2; ++s) bf[s] = lds_afrag<Pol>(u2, ldu2, 0, s, lane);
+            if (c == 0) {
+#pragma unroll
+                for (int n = 0; n < 4; ++n) h3[n] = Pol::mma(rl2[0][n], bf[0], h1[n]);
+            } else {
+#pragma unroll
+                for (int n = 0; n < 4; ++n) h3[n] = Pol::mma(rl2[0][n], bf[0], f32x4{0.f, 0.f, 0.f, 0.f});
+            }
+#pragma unroll
+            for (int s = 1; s < KS2; ++s)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) h3[n] = Pol::mma(rl2[s][n], bf[s], h3[n]);
+            if (pre) load_l2(PKn);
+        }
+        XPHASE(13);
+        // ---- out-Dense partial (transposed) from this wave's own h3 registers (hi/lo split)
+        {
+            f32x4 po[NO], pl[NO];
+#pragma unroll
+            for (int n = 0; n < NO; ++n) { zero_acc(po[n]); zero_acc(pl[n]); }
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                float hv[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { hv[e] = h3[2 * s][e]; hv[4 + e] = h3[2 * s + 1][e]; }
+                u32x4 hi, lo;
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2) {
+                    const float x0 = hv[2 * e2], x1 = hv[2 * e2 + 1];
+                    hi[e2] = pack_bf16x2(x0, x1);
+                    const float r0 = Pol::lo2f(hi[e2]), r1 = Pol::hi2f(hi[e2]);
+                    lo[e2] = pack_bf16x2(x0 - r0, x1 - r1);
+                }
+#pragma unroll
+                for (int n = 0; n < NO; ++n) {
+                    const u32x4 wo = routl[(wave * 2 * NO + s * NO + n) * 64 + lane];
+                    po[n] = Pol::mma(wo, hi, po[n]);
+                    pl[n] = Pol::mma(wo, lo, pl[n]);
+                }
+            }
+#pragma unroll
+            for (int n = 0; n < NO; ++n) po[n] += pl[n];
+            if (pre) load_out(PKn);
+#pragma unroll
+            for (int n = 0; n < NO; ++n)
+                if (16 * n + 4 * jq < XD) *(f32x4*)(part + wave * NV + env * XD + 16 * n + 4 * jq) = po[n];
+        }
+        XPHASE(14);
+        lds_sync();
+        XPHASE(4);
+        // ---- exchange + DDPM epilogue (as the P = 8 kernel; lane = 4 * slot + member, the member
+        //      sum is two DPP levels inside the quad)
+        {
+            const uint32_t tag = (sa.seq << 6) | (uint32_t)(i + 1);
+            uint64_t* xb = xregion + ((size_t)((i & 1) * sa.G + g) * P) * NV;
+            const int vw = wave * NVW;
+            if (lane < NVW) {
+                float sum = part[vw + lane];
+#pragma unroll
+                for (int w = 1; w < SW; ++w) sum += part[w * NV + vw + lane];
+                const uint64_t gr = ((uint64_t)tag << 32) | __float_as_uint(sum);
+                if (xmode)   // one XCD: the line stays in its L2, where the peers' sc1 loads read it
+                    __hip_atomic_store(xb + (size_t)c * NV + vw + lane, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    __hip_atomic_store(xb + (size_t)c * NV + vw + lane, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            XPHASE(15);
+            const int m = lane & 3, sl = lane >> 2;
+            // lane (slot sl, member m) finishes coordinate sl + 16 m of this wave's slice
+            const bool fin = m < KW && sl + 16 * m < NVW;
+            const int ve = vw + (fin ? sl + 16 * m : 0), re = ve / XD, qe = ve % XD;
+            const float* sc = sch + t * DPPO_SCHED_COLS;
+            const float c0 = sc[0], c1 = sc[1], c2 = sc[2], c3 = sc[3];
+            float sd = expf(0.5f * sc[4]);
+            if (a.deterministic && sc[6] != 0.f) sd = 0.f;
+            else if (a.deterministic) sd = fminf(fmaxf(sd, sc[5]), 1e6f);
+            else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
+            const float xe = xs[ve], ze = zt[i * 16 * XD + ve], be = bb[H + qe];
+            const uint64_t* src = xb + (size_t)m * NV + vw;
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
+            float val[KW];
+            bool failed = false;
+            uint64_t xa[KW];
+            for (;;) {
+#pragma unroll
+                for (int k = 0; k < KW; ++k) {
+                    const int v = sl + 16 * k < NVW ? sl + 16 * k : NVW - 1;   // clamped lanes re-read a valid granule
+                    xa[k] = __hip_atomic_load(src + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < KW; ++k) ok &= (uint32_t)(xa[k] >> 32) == tag;
+                if (__all(ok)) break;
+                if (__builtin_amdgcn_s_memrealtime() > t_end) {
+                    failed = true;
+                    if (lane == 0) *xfail = 1;
+                    break;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < KW; ++k) val[k] = __uint_as_float((uint32_t)xa[k]);
+            XPHASE(5);
+            // member sum: xor 1 then xor 2 inside the quad; every lane adds the same two partial
+            // sums, so all four hold the same bits
+#pragma unroll
+            for (int k = 0; k < KW; ++k) {
+                val[k] += dpp_f32<0xB1>(val[k]);     // quad_perm [1,0,3,2]
+                val[k] += dpp_f32<0x4E>(val[k]);     // quad_perm [2,3,0,1]
+            }
+            if (fin) {
+                float ep = val[0];
+#pragma unroll
+                for (int k = 1; k < KW; ++k) ep = m == k ? val[k] : ep;
+                const int v = ve, r = re, q = qe, row = row0 + r;
+                ep += be;
+                const float x = xe;
+                float xr = c0 * x - c1 * ep;                         // x0 reconstruction (:198-201)
+                xr = fminf(fmaxf(xr, -1.f), 1.f);                    // denoised_clip_value = 1 (diffusion.py:28)
+                const float mu = c2 * xr + c3 * x;                   // posterior mean (:239-242)
+                float y = mu + sd * ze;                              // (:301-320)
+                if (a.final_clip > 0.f && i == K - 1) y = fminf(fmaxf(y, -a.final_clip), a.final_clip);
+                if (failed) y = __builtin_nanf("");
+                xs[v] = y;
+                a0[r * lda0 + q] = Pol::cvt(y);
+                if (c == 0 && row < a.E) {
+                    if (a.chains && t <= KF) store_out(a.chains + ((size_t)row * (KF + 1) + (KF - t)) * XD + q, y);
+                    if (i == K - 1) {
+                        store_out(a.actions + (size_t)row * XD + q, y);
+                        if (a.actions_tagged)
+                            __hip_atomic_store(a.actions_tagged + (size_t)row * XD + q,
+                                               ((uint64_t)a.cond_tag << 32) | __float_as_uint(y), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                        else if (a.actions_host) a.actions_host[(size_t)row * XD + q] = y;
+                    }
+                }
+            }
+        }
+        lds_sync();
+        XPHASE(6);
+    }
+    XPHASE(9);
+    if (c == 0 && a.done) {
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) {
+            if (*xfail) __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    XPHASE(10);
+}
+
+size_t split4_lds_bytes(int XD, int SD, int K, int KX, int NO) {
+    const int pad = 16, ldh = SPLIT_H + pad, ldu2 = SPLIT_H / 4 + pad, lda0 = KX * 32 + pad;
+    size_t o = 0;
+    o += dppo_align16(2 * 16 * lda0);
+    o += dppo_align16(2 * 16 * ldh);
+    o += dppo_align16(2 * 16 * ldu2);
+    o += dppo_align16(4 * SW * 16 * XD);
+    o += 16;
+    o += dppo_align16(4 * 16 * XD);
+    o += dppo_align16(4 * 16 * SD);
+    o += dppo_align16(4 * K * SPLIT_H);
+    o += dppo_align16(4 * K * DPPO_SCHED_COLS);
+    o += dppo_align16(4 * 2 * (SPLIT_H + 16 * NO));
+    o += dppo_align16(4 * K * 16 * XD);
+    o += (size_t)SW * 4 * KX * 1024;
+    o += (size_t)SW * 2 * NO * 1024;
+    return o;
+}
+
 size_t split_lds_bytes(int XD, int SD, int TD, int K, int KSI, int NO) {
     const int pad = 16, ldh = SPLIT_H + pad, lda0 = KSI * 32 + pad, KP = SW / (SPLIT_H / 16 / SPLIT_P);
     const int ldp = SPLIT_H / SPLIT_P + 4;
@@ -761,22 +1251,54 @@ int launch_split_k(const SplitArgs& sa, hipStream_t s) {
     return DPPO_OK;
 }
 
-}  // namespace
-
-bool sample_split_supported(int precision, int H, int XD, int ks_in, int E, int K) {
-    if (!dppo_prec_2b(precision) || H != SPLIT_H || XD % 4 != 0 || XD > 32 || ks_in != 2 || K > 63) return false;
-    const int G = dppo_cdiv(E, 16);
-    if (G < 1 || G > XMAX_G) return false;
-    const int cus = device_cus();
-    return cus == 0 || 8 * SPLIT_P * ((G + 7) / 8) <= cus;   // every workgroup of the launch co-resident
+template <class Pol, int XQ, int KX, bool INJ>
+int launch_split4_k(const SplitArgs& sa, hipStream_t s) {
+    constexpr int NO = (4 * XQ + 15) / 16;
+    auto k = sample_split4_kernel<Pol, XQ, KX, INJ>;
+    const SampleArgs& a = sa.a;
+    const size_t lds = split4_lds_bytes(a.XD, a.SD, a.K, KX, NO);
+    if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler needs %zu B of LDS", lds);
+    DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int blocks = 8 * 4 * ((sa.G + 7) / 8);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(SW * 64), lds, s, sa);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
 }
 
-int split_sampler_members() { return SPLIT_P; }
+// DPPO_SPLIT_P: members per 16-env group, 4 (default) or 8 (the r01 kernel; A/B knob)
+int split_p_choice() {
+    static const int p = [] {
+        const char* e = getenv("DPPO_SPLIT_P");
+        return e && atoi(e) == 8 ? 8 : 4;
+    }();
+    return p;
+}
+
+}  // namespace
+
+int split_members_for(int precision, int H, int XD, int SD, int ks_in, int E, int K) {
+    if (!dppo_prec_2b(precision) || H != SPLIT_H || XD % 4 != 0 || XD > 32 || K > 63) return 0;
+    const int G = dppo_cdiv(E, 16);
+    if (G < 1 || G > XMAX_G) return 0;
+    const int cus = device_cus();
+    // every workgroup of the launch co-resident (one per CU: the register budget)
+    auto fits = [&](int P) { return cus == 0 || 8 * P * ((G + 7) / 8) <= cus; };
+    const int KX = dppo_cdiv(XD + SD, 32);
+    const bool p4 = KX <= 2 && split4_lds_bytes(XD, SD, K, KX, dppo_cdiv(XD, 16)) <= 160 * 1024 && fits(4);
+    const bool p8 = ks_in == 2 && fits(8);
+    if (split_p_choice() == 8) return p8 ? 8 : (p4 ? 4 : 0);
+    return p4 ? 4 : (p8 ? 8 : 0);
+}
+
+bool sample_split_supported(int precision, int H, int XD, int SD, int ks_in, int E, int K) {
+    return split_members_for(precision, H, XD, SD, ks_in, E, K) > 0;
+}
 
 int sampler_device_cus() { return device_cus(); }
 
 int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s) {
-    if (!sample_split_supported(precision, a.H, a.XD, a.L.ks_in, a.E, a.K)) return DPPO_EUNSUPPORTED;
+    const int P = split_members_for(precision, a.H, a.XD, a.SD, a.L.ks_in, a.E, a.K);
+    if (!P) return DPPO_EUNSUPPORTED;
     SplitArgs sa;
     sa.a = a;
     sa.G = dppo_cdiv(a.E, 16);
@@ -789,6 +1311,23 @@ int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s) {
     if (rc) return rc;
     const bool inj = a.noise != nullptr;
     const bool f16 = precision == DPPO_F16;
+    if (P == 4) {
+        const bool kx2 = a.XD + a.SD > 32;
+        switch (a.XD / 4) {
+#define DPPO_SPLIT4_CASE(xq)                                                                                 \
+    case xq:                                                                                                 \
+        if (kx2) {                                                                                           \
+            if (f16) return inj ? launch_split4_k<PolicyF16, xq, 2, true>(sa, s) : launch_split4_k<PolicyF16, xq, 2, false>(sa, s); \
+            return inj ? launch_split4_k<PolicyBF16, xq, 2, true>(sa, s) : launch_split4_k<PolicyBF16, xq, 2, false>(sa, s); \
+        }                                                                                                    \
+        if (f16) return inj ? launch_split4_k<PolicyF16, xq, 1, true>(sa, s) : launch_split4_k<PolicyF16, xq, 1, false>(sa, s); \
+        return inj ? launch_split4_k<PolicyBF16, xq, 1, true>(sa, s) : launch_split4_k<PolicyBF16, xq, 1, false>(sa, s);
+            DPPO_SPLIT4_CASE(1) DPPO_SPLIT4_CASE(2) DPPO_SPLIT4_CASE(3) DPPO_SPLIT4_CASE(4)
+            DPPO_SPLIT4_CASE(5) DPPO_SPLIT4_CASE(6) DPPO_SPLIT4_CASE(7) DPPO_SPLIT4_CASE(8)
+#undef DPPO_SPLIT4_CASE
+            default: return DPPO_EUNSUPPORTED;
+        }
+    }
     switch (a.XD / 4) {
 #define DPPO_SPLIT_CASE(xq)                                                                                 \
     case xq:                                                                                                \

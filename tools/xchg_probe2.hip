@@ -114,7 +114,10 @@ int main() {
     CHECK(hipMalloc(&fail, 4));
     CHECK(hipMalloc(&xcc, 64 * 16 * 4));
     uint32_t seq = 0;
-    for (int work : {0, 4}) {
+    for (int work : {0}) {
+        run<2, true, true>("sc0 stores, one XCD", 4, work, buf, out, fail, xcc, seq);
+        run<4, true, true>("sc0 stores, one XCD", 4, work, buf, out, fail, xcc, seq);
+        run<4, true, true>("sc0 stores, one XCD", 32, work, buf, out, fail, xcc, seq);
         run<8, false, true>("sc1 stores, one XCD", 4, work, buf, out, fail, xcc, seq);
         run<8, true, true>("sc0 stores, one XCD", 4, work, buf, out, fail, xcc, seq);
         run<16, false, true>("sc1 stores, one XCD", 4, work, buf, out, fail, xcc, seq);
