@@ -137,6 +137,8 @@ struct SplitArgs {
     uint32_t seq;     // launch sequence number (tag high bits)
     int G;            // 16-env groups
     int force_shared; // DPPO_SPLIT_XCHG=shared: always the placement-independent sc1 form (A/B knob)
+    uint32_t* xfail_host;  // mapped host word: set by a launch whose exchange timed out (lost
+                           // co-residency); the next launch on the stream reports it as an error
 };
 
 __device__ inline int xcc_id() {
@@ -150,8 +152,26 @@ __device__ inline int xcc_id() {
 __device__ inline int slot_feature(int j, int e) { return e < 4 ? 4 * j + e : 16 + 4 * j + (e - 4); }
 
 
-// relu as one v_med3_f32 (fmaxf(x, 0) canonicalises its MFMA-produced input first: two VALU ops)
-__device__ inline float relu_f(float x) { return __builtin_amdgcn_fmed3f(x, 0.f, __builtin_huge_valf()); }
+// tuning knobs of the P = 4 kernel (tools/split_variant.sh + tools/ab_variants.sh)
+#ifndef DPPO_S4_L1D
+#define DPPO_S4_L1D 4        // l1: u1 fragment reads kept in flight ahead of the MFMA chain
+#endif
+#ifndef DPPO_S4_INREADY
+#define DPPO_S4_INREADY 1    // in-Dense: all LDS operands in one round trip
+#endif
+#ifndef DPPO_S4_PUBREADY
+#define DPPO_S4_PUBREADY 1   // publish: the 8 wave partials in one round trip
+#endif
+#ifndef DPPO_S4_EPIEARLY
+#define DPPO_S4_EPIEARLY 1   // epilogue inputs read at the step start (else after the publish)
+#endif
+
+// relu as one v_max_i32 on the bits (fmaxf(x, 0) canonicalises its MFMA-produced input first: two
+// VALU ops per element); negative values and -0 map to +0, as fmaxf(x, 0) does up to the sign of 0
+__device__ inline float relu_f(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+// LDS_READY(...): an empty asm statement that "uses" its operands: every one of them is loaded
+// before it, so their loads issue together and pay one LDS round trip (left alone, hipcc sank each
+// read next to its use)
 
 template <int CTRL>
 __device__ inline float dpp_f32(float v) {
@@ -607,7 +627,10 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 if (got) break;
                 if (__builtin_amdgcn_s_memrealtime() > t_end) {
                     failed = true;
-                    if (lane == 0) *xfail = 1;
+                    if (lane == 0) {
+                        *xfail = 1;
+                        __hip_atomic_store(sa.xfail_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                     break;
                 }
             }
@@ -621,7 +644,10 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
 #endif
                 if (__builtin_amdgcn_s_memrealtime() > t_end) {
                     failed = true;
-                    if (lane == 0) *xfail = 1;
+                    if (lane == 0) {
+                        *xfail = 1;
+                        __hip_atomic_store(sa.xfail_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                     break;
                 }
             }
@@ -828,7 +854,18 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
         const int t = 4 * i4 / H;
         ((float4*)tin)[i4] = ((const float4*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIN]))[i4];
     }
-    for (int i = tid; i < K * DPPO_SCHED_COLS; i += ST) sch[i] = a.sched[i];
+    // per-step epilogue constants [i][c0 c1 c2 c3 sd]: schedule row t = K-1-i and the noise rule
+    // (include/dppo.h: eval DDPM t = 0 or any DDIM row -> 0; other DDPM rows clip at 1e-3; train:
+    // min_std; diffusion_vpg.py:303-315)
+    for (int i = tid; i < K; i += ST) {
+        const float* sc = a.sched + (K - 1 - i) * DPPO_SCHED_COLS;
+        float sd = expf(0.5f * sc[4]);
+        if (a.deterministic && sc[6] != 0.f) sd = 0.f;
+        else if (a.deterministic) sd = fminf(fmaxf(sd, sc[5]), 1e6f);
+        else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
+        float* e = sch + i * DPPO_SCHED_COLS;
+        e[0] = sc[0]; e[1] = sc[1]; e[2] = sc[2]; e[3] = sc[3]; e[4] = sd;
+    }
     const int XG = (XD + 3) / 4;
     for (int it = tid; it < (K + 1) * 16 * XG; it += ST) {
         const int step = it / (16 * XG), r = (it / XG) % 16, gq = it % XG, row = row0 + r;
@@ -921,6 +958,11 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
     const int env = lane & 15, jq = lane >> 4;
     const int xmode = __builtin_amdgcn_readfirstlane(xfail[1]);
     uint64_t* const xregion = sa.xbuf + (size_t)xmode * XREGION;
+    // this lane's exchange/epilogue coordinate (launch-constant): lane (slot sl, member m) finishes
+    // coordinate sl + 16 m of its wave's slice
+    const int xm = lane & 3, xsl = lane >> 2;
+    const bool fin = xm < KW && xsl + 16 * xm < NVW;
+    const int ve = wave * NVW + (fin ? xsl + 16 * xm : 0), re = ve / XD, qe = ve % XD;
     XPHASE(0);
     for (int i = 0; i < K; ++i) {
         XSTEP(i);
@@ -935,10 +977,14 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
         }
         XPHASE(1);
         const float* bb = bias + PK * NB;
+        // this step's epilogue inputs, read with the in-Dense operands (none depends on this step)
+        const f32x4 ec = *(const f32x4*)(sch + i * DPPO_SCHED_COLS);      // c0 c1 c2 c3
+        const float esd = sch[i * DPPO_SCHED_COLS + 4];
+        const float xe = xs[ve], ze = zt[i * 16 * XD + ve], be = bb[H + qe];
         // ---- in-Dense (transposed): h1 = TIN[t] + W_xs^T [x; state]; no activation (mlp.py:144)
         f32x4 h1[4];
         {
-            u32x4 af[KX];
+            u32x4 af[KX], wf[KX][4];
 #pragma unroll
             for (int ks = 0; ks < KX; ++ks) af[ks] = lds_afrag<Pol>(a0, lda0, 0, ks, lane);
 #pragma unroll
@@ -946,10 +992,21 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
 #pragma unroll
             for (int ks = 0; ks < KX; ++ks)
 #pragma unroll
-                for (int n = 0; n < 4; ++n) h1[n] = Pol::mma(wxs[((wave * 4 + n) * KX + ks) * 64 + lane], af[ks], h1[n]);
-            // every LDS read (a0, TIN rows, fragments) in flight before the first MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, KX + 4 + 4 * KX, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 4 * KX, 0);
+                for (int n = 0; n < 4; ++n) wf[ks][n] = wxs[((wave * 4 + n) * KX + ks) * 64 + lane];
+            // one LDS round trip for all of them
+#if DPPO_S4_INREADY
+            asm volatile("" ::"v"(af[0]), "v"(h1[0]), "v"(h1[1]), "v"(h1[2]), "v"(h1[3]), "v"(wf[0][0]), "v"(wf[0][1]),
+                         "v"(wf[0][2]), "v"(wf[0][3]));
+            if constexpr (KX == 2)
+                asm volatile("" ::"v"(af[KX - 1]), "v"(wf[KX - 1][0]), "v"(wf[KX - 1][1]), "v"(wf[KX - 1][2]), "v"(wf[KX - 1][3]));
+#endif
+#if DPPO_S4_EPIEARLY
+            asm volatile("" ::"v"(ec), "v"(esd), "v"(xe), "v"(ze), "v"(be));
+#endif
+#pragma unroll
+            for (int ks = 0; ks < KX; ++ks)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) h1[n] = Pol::mma(wf[ks][n], af[ks], h1[n]);
             if (pre) load_in(PKn);
 #pragma unroll
             for (int n = 0; n < 4; ++n) {
@@ -974,7 +1031,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
             for (int j = 0; j < KSH; ++j) acc = Pol::mma(rl1[j], fb[j], acc);
             // schedule: the bias and L1D fragment reads first, then one read per MFMA, so L1D reads
             // stay in flight ahead of the chain (left alone, hipcc issued read -> wait -> MFMA)
-            constexpr int L1D = 4;
+            constexpr int L1D = DPPO_S4_L1D;
             __builtin_amdgcn_sched_group_barrier(0x100, L1D + 1, 0);
 #pragma unroll
             for (int j = 0; j < KSH - L1D; ++j) {
@@ -1053,9 +1110,15 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
             uint64_t* xb = xregion + ((size_t)((i & 1) * sa.G + g) * P) * NV;
             const int vw = wave * NVW;
             if (lane < NVW) {
-                float sum = part[vw + lane];
+                float pp[SW];
 #pragma unroll
-                for (int w = 1; w < SW; ++w) sum += part[w * NV + vw + lane];
+                for (int w = 0; w < SW; ++w) pp[w] = part[w * NV + vw + lane];
+#if DPPO_S4_PUBREADY
+                asm volatile("" ::"v"(pp[0]), "v"(pp[1]), "v"(pp[2]), "v"(pp[3]), "v"(pp[4]), "v"(pp[5]), "v"(pp[6]), "v"(pp[7]));
+#endif
+                float sum = pp[0];
+#pragma unroll
+                for (int w = 1; w < SW; ++w) sum += pp[w];
                 const uint64_t gr = ((uint64_t)tag << 32) | __float_as_uint(sum);
                 if (xmode)   // one XCD: the line stays in its L2, where the peers' sc1 loads read it
                     __hip_atomic_store(xb + (size_t)c * NV + vw + lane, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1063,17 +1126,8 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
                     __hip_atomic_store(xb + (size_t)c * NV + vw + lane, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             XPHASE(15);
-            const int m = lane & 3, sl = lane >> 2;
-            // lane (slot sl, member m) finishes coordinate sl + 16 m of this wave's slice
-            const bool fin = m < KW && sl + 16 * m < NVW;
-            const int ve = vw + (fin ? sl + 16 * m : 0), re = ve / XD, qe = ve % XD;
-            const float* sc = sch + t * DPPO_SCHED_COLS;
-            const float c0 = sc[0], c1 = sc[1], c2 = sc[2], c3 = sc[3];
-            float sd = expf(0.5f * sc[4]);
-            if (a.deterministic && sc[6] != 0.f) sd = 0.f;
-            else if (a.deterministic) sd = fminf(fmaxf(sd, sc[5]), 1e6f);
-            else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
-            const float xe = xs[ve], ze = zt[i * 16 * XD + ve], be = bb[H + qe];
+            const int m = xm, sl = xsl;
+            const float c0 = ec[0], c1 = ec[1], c2 = ec[2], c3 = ec[3], sd = esd;
             const uint64_t* src = xb + (size_t)m * NV + vw;
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
             float val[KW];
@@ -1088,10 +1142,16 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
                 bool ok = true;
 #pragma unroll
                 for (int k = 0; k < KW; ++k) ok &= (uint32_t)(xa[k] >> 32) == tag;
+#ifdef DPPO_SPLIT_NOXCHG
+                ok = true;   // timing probe only: one sweep, no wait for the peers (wrong actions)
+#endif
                 if (__all(ok)) break;
                 if (__builtin_amdgcn_s_memrealtime() > t_end) {
                     failed = true;
-                    if (lane == 0) *xfail = 1;
+                    if (lane == 0) {
+                        *xfail = 1;
+                        __hip_atomic_store(sa.xfail_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                     break;
                 }
             }
@@ -1197,26 +1257,39 @@ struct XchgBuf {
     int device;
     uint64_t* buf;
     uint32_t seq;
+    uint32_t* fail_host;   // mapped pinned word (SplitArgs::xfail_host)
+    uint32_t* fail_dev;
 };
 std::mutex g_xmu;
 XchgBuf g_xb[16];
 int g_nxb = 0;
 int g_cus = 0;
 
-int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq) {
+int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq, uint32_t** fail_dev) {
     int dev = 0;
     DPPO_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(g_xmu);
     for (int i = 0; i < g_nxb; ++i)
         if (g_xb[i].stream == s && g_xb[i].device == dev) {
+            // an earlier launch on this stream lost its members' co-residency (another tenant took
+            // the CUs it waited for) and wrote NaN actions: report it instead of sampling on
+            if (__hip_atomic_load(g_xb[i].fail_host, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                __hip_atomic_store(g_xb[i].fail_host, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return dppo_set_error(DPPO_EHIP, "split sampler: a launch's partial-sum exchange timed out "
+                                      "(its workgroups were not all resident at once); its actions are NaN");
+            }
             *buf = g_xb[i].buf;
             *seq = g_xb[i].seq = (g_xb[i].seq + 1) & 0x03FFFFFFu;
+            *fail_dev = g_xb[i].fail_dev;
             return DPPO_OK;
         }
     if (g_nxb == 16) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler: more than 16 streams");
     XchgBuf& x = g_xb[g_nxb];
     const size_t n = 9 * XREGION + (size_t)XMAX_G * SPLIT_P;
     DPPO_HIP(hipMalloc((void**)&x.buf, sizeof(uint64_t) * n));
+    DPPO_HIP(hipHostMalloc((void**)&x.fail_host, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+    *x.fail_host = 0;
+    DPPO_HIP(hipHostGetDevicePointer((void**)&x.fail_dev, x.fail_host, 0));
     // zeroed with write-through stores: no XCD's L2 is left holding a dirty copy of any line
     hipLaunchKernelGGL(xchg_zero_kernel, dim3(1024), dim3(256), 0, s, x.buf, n);
     DPPO_HIP(hipGetLastError());
@@ -1224,6 +1297,7 @@ int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq) {
     ++g_nxb;
     *buf = x.buf;
     *seq = x.seq;
+    *fail_dev = x.fail_dev;
     return DPPO_OK;
 }
 
@@ -1307,7 +1381,7 @@ int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s) {
         return e && !strcmp(e, "shared") ? 1 : 0;
     }();
     sa.force_shared = force_shared;
-    int rc = xchg_for(s, &sa.xbuf, &sa.seq);
+    int rc = xchg_for(s, &sa.xbuf, &sa.seq, &sa.xfail_host);
     if (rc) return rc;
     const bool inj = a.noise != nullptr;
     const bool f16 = precision == DPPO_F16;
