@@ -86,7 +86,8 @@ __device__ inline void sampler_load_state_tagged(const SampleArgs& a, int row0, 
 // touching the error message) when the shape is outside what it instantiates, or another error code.
 int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s);
 // whether the split sampler takes this shape (same test launch_sample_split applies)
-bool sample_split_supported(int precision, int H, int XD, int SD, int ks_in, int E, int K);
-// workgroups (CUs) per 16-env group of the split sampler for this shape (4 or 8), 0 = not taken
-int split_members_for(int precision, int H, int XD, int SD, int ks_in, int E, int K);
+bool sample_split_supported(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF);
+// workgroups (CUs) per 16-env group of the split sampler for this shape (4, or 8: the P = 8 kernel
+// or the P = 4 kernel's two member sets), 0 = not taken
+int split_members_for(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF);
 int sampler_device_cus();   // CUs of the current device (0 if unknown)

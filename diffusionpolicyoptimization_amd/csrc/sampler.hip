@@ -608,7 +608,7 @@ extern "C" int dppo_sampler_layout(const dppo_dims* d, int precision, int n_envs
     if (rc) return rc;
     DPPO_CHECK(members, "dppo_sampler_layout: null output");
     const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
-    *members = sampler_cfg() == 'x' ? split_members_for(precision, D.H, D.XD, D.SD, L.ks_in, n_envs, D.K) : 0;
+    *members = sampler_cfg() == 'x' ? split_members_for(precision, D.H, D.XD, D.SD, L.ks_in, n_envs, D.K, D.KF) : 0;
     return DPPO_OK;
 }
 

@@ -129,6 +129,11 @@ constexpr int XMAX_NV = 16 * 32;   // granules per member per step at XD <= 32
 constexpr int XMAX_G = 32;         // groups per launch (512 envs): 8*P*G/8 = 256 workgroups
 
 constexpr size_t XREGION = (size_t)2 * XMAX_G * SPLIT_P * XMAX_NV;   // granules of one exchange region
+// after the 9 exchange regions: the XCD announcements [XMAX_G * SPLIT_P], then the dual-set x
+// hand-off [XMAX_G][XMAX_NV]
+constexpr size_t XANN = 9 * XREGION;
+constexpr size_t XHOFF = XANN + (size_t)XMAX_G * SPLIT_P;
+constexpr size_t XTOTAL = XHOFF + (size_t)XMAX_G * XMAX_NV;
 
 struct SplitArgs {
     SampleArgs a;
@@ -139,6 +144,8 @@ struct SplitArgs {
     int force_shared; // DPPO_SPLIT_XCHG=shared: always the placement-independent sc1 form (A/B knob)
     uint32_t* xfail_host;  // mapped host word: set by a launch whose exchange timed out (lost
                            // co-residency); the next launch on the stream reports it as an error
+    int dual;         // P = 4 kernel: the base actor's steps and the fine-tuned actor's steps run on
+                      // two member sets, each with its actor resident for the whole launch
 };
 
 __device__ inline int xcc_id() {
@@ -286,7 +293,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
     };
 
     // announce this member's XCD (sc1 granule, tag = seq << 6: step tags are seq << 6 | i + 1)
-    uint64_t* const xann = sa.xbuf + 9 * XREGION + (size_t)g * P;
+    uint64_t* const xann = sa.xbuf + XANN + (size_t)g * P;
     const uint32_t ann_tag = sa.seq << 6;
     if (tid == 0)
         __hip_atomic_store(xann + c, ((uint64_t)ann_tag << 32) | (uint32_t)xcc_id(), __ATOMIC_RELAXED,
@@ -743,15 +750,22 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
     constexpr int NB = H + NOC;            // per-actor bias floats: b_l1 | B_OUT2
 
     const SampleArgs& a = sa.a;
-    const int b = blockIdx.x;
+    // dual: set 0 runs the base actor's steps (t >= K'), set 1 the fine-tuned actor's (t < K'), each
+    // with its actor resident for the whole launch; set 0 hands x to set 1 once. Without it, one
+    // set runs every step and reloads the resident fragments at the switch (~5 us per launch)
+    const int per_set = 8 * P * ((sa.G + 7) / 8);
+    const int set = sa.dual ? (int)blockIdx.x / per_set : 0;
+    const int b = (int)blockIdx.x - set * per_set;
     const int g = (b / (8 * P)) * 8 + b % 8, c = (b / 8) % P;
     if (g >= sa.G) return;                 // whole workgroup: no barrier is skipped
+    const int gx = g + set * sa.G, GX = sa.G * (sa.dual ? 2 : 1);   // group index in the exchange regions
     XPHASE_START;
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int row0 = g * 16;
     const MlpLayout& L = a.L;
     const int SD = a.SD, K = a.K, KF = a.KF;
     const int KSX = packed_ksteps(XD + SD, 32);   // k-step stride of the W_XS image
+    const int i0 = sa.dual && set == 1 ? K - KF : 0, i1 = sa.dual && set == 0 ? K - KF : K;   // steps of this set
 
     // ---- LDS carve (all offsets multiples of 16 B) ----
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -833,12 +847,12 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
     };
 
     // announce this member's XCD (sc1 granule, tag = seq << 6: step tags are seq << 6 | i + 1)
-    uint64_t* const xann = sa.xbuf + 9 * XREGION + (size_t)g * P;
+    uint64_t* const xann = sa.xbuf + XANN + (size_t)gx * P;
     const uint32_t ann_tag = sa.seq << 6;
     if (tid == 0)
         __hip_atomic_store(xann + c, ((uint64_t)ann_tag << 32) | (uint32_t)xcc_id(), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-    const int ft0 = __builtin_amdgcn_readfirstlane(K - 1 < KF ? 1 : 0);
+    const int ft0 = __builtin_amdgcn_readfirstlane(sa.dual ? set : (K - 1 < KF ? 1 : 0));
     load_in(ft0); load_l1(ft0); load_l2(ft0); load_out(ft0);
     int cur = ft0;
 
@@ -955,6 +969,31 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
         }
     }
     __syncthreads();
+    uint64_t* const xh = sa.xbuf + XHOFF + (size_t)g * XMAX_NV;     // dual: x after the base actor's steps
+    const uint32_t htag = (sa.seq << 6) | 63u;
+    if (sa.dual && set == 1) {
+        // the base set waits for the observation first, so this wait is bounded like that one (4 s)
+        // plus margin; a timeout leaves x NaN and is flagged like an exchange failure
+        if (tid < NV) {
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 500000000ull;   // 5 s
+            uint64_t v;
+            bool ok = true;
+            for (;;) {
+                v = __hip_atomic_load(xh + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)(v >> 32) == htag) break;
+                if (__builtin_amdgcn_s_memrealtime() > t_end) { ok = false; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            xs[tid] = ok ? __uint_as_float((uint32_t)v) : __builtin_nanf("");
+            if (!ok) {
+                *xfail = 1;
+                __hip_atomic_store(sa.xfail_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        __syncthreads();
+        for (int idx = tid; idx < NV; idx += ST) a0[(idx / XD) * lda0 + idx % XD] = Pol::cvt(xs[idx]);
+        __syncthreads();
+    }
     const int env = lane & 15, jq = lane >> 4;
     const int xmode = __builtin_amdgcn_readfirstlane(xfail[1]);
     uint64_t* const xregion = sa.xbuf + (size_t)xmode * XREGION;
@@ -964,12 +1003,12 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
     const bool fin = xm < KW && xsl + 16 * xm < NVW;
     const int ve = wave * NVW + (fin ? xsl + 16 * xm : 0), re = ve / XD, qe = ve % XD;
     XPHASE(0);
-    for (int i = 0; i < K; ++i) {
+    for (int i = i0; i < i1; ++i) {
         XSTEP(i);
         const int t = K - 1 - i;
-        const int PK = __builtin_amdgcn_readfirstlane(t < KF ? 1 : 0);
+        const int PK = __builtin_amdgcn_readfirstlane(sa.dual ? cur : (t < KF ? 1 : 0));
         const int PKn = __builtin_amdgcn_readfirstlane(t >= 1 && t - 1 < KF ? 1 : 0);
-        const bool pre = t >= 1 && PKn != PK;             // this step is the last of its actor
+        const bool pre = !sa.dual && t >= 1 && PKn != PK;   // this step is the last of its actor
         if (PK != cur) {
             __builtin_amdgcn_s_waitcnt(0x0F70);
             permute_out();
@@ -1107,7 +1146,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
         //      sum is two DPP levels inside the quad)
         {
             const uint32_t tag = (sa.seq << 6) | (uint32_t)(i + 1);
-            uint64_t* xb = xregion + ((size_t)((i & 1) * sa.G + g) * P) * NV;
+            uint64_t* xb = xregion + ((size_t)((i & 1) * GX + gx) * P) * NV;
             const int vw = wave * NVW;
             if (lane < NVW) {
                 float pp[SW];
@@ -1197,6 +1236,15 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
         XPHASE(6);
     }
     XPHASE(9);
+    if (sa.dual && set == 0) {
+        // hand x to the fine-tuned set (member 0 of the group: every member holds the same bits)
+        if (c == 0 && tid < NV)
+            __hip_atomic_store(xh + tid, ((uint64_t)htag << 32) | __float_as_uint(xs[tid]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (c == 0 && tid == 0 && a.done && *xfail)
+            __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     if (c == 0 && a.done) {
         __threadfence_system();
         __syncthreads();
@@ -1285,7 +1333,7 @@ int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq, uint32_t** fail_dev) 
         }
     if (g_nxb == 16) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler: more than 16 streams");
     XchgBuf& x = g_xb[g_nxb];
-    const size_t n = 9 * XREGION + (size_t)XMAX_G * SPLIT_P;
+    const size_t n = XTOTAL;
     DPPO_HIP(hipMalloc((void**)&x.buf, sizeof(uint64_t) * n));
     DPPO_HIP(hipHostMalloc((void**)&x.fail_host, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
     *x.fail_host = 0;
@@ -1333,7 +1381,7 @@ int launch_split4_k(const SplitArgs& sa, hipStream_t s) {
     const size_t lds = split4_lds_bytes(a.XD, a.SD, a.K, KX, NO);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler needs %zu B of LDS", lds);
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const int blocks = 8 * 4 * ((sa.G + 7) / 8);
+    const int blocks = 8 * 4 * ((sa.G + 7) / 8) * (sa.dual ? 2 : 1);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(SW * 64), lds, s, sa);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
@@ -1348,33 +1396,49 @@ int split_p_choice() {
     return p;
 }
 
-}  // namespace
 
-int split_members_for(int precision, int H, int XD, int SD, int ks_in, int E, int K) {
-    if (!dppo_prec_2b(precision) || H != SPLIT_H || XD % 4 != 0 || XD > 32 || K > 63) return 0;
+// the split sampler's plan for a shape: P members per 16-env group (4 or 8; 0 = not taken) and
+// whether the P = 4 kernel runs its two actors on two member sets (dual)
+struct SplitPlan { int P; bool dual; };
+
+SplitPlan split_plan(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF) {
+    if (!dppo_prec_2b(precision) || H != SPLIT_H || XD % 4 != 0 || XD > 32 || K > 62) return {0, false};
     const int G = dppo_cdiv(E, 16);
-    if (G < 1 || G > XMAX_G) return 0;
+    if (G < 1 || G > XMAX_G) return {0, false};
     const int cus = device_cus();
     // every workgroup of the launch co-resident (one per CU: the register budget)
-    auto fits = [&](int P) { return cus == 0 || 8 * P * ((G + 7) / 8) <= cus; };
+    auto fits = [&](int P, int sets) { return cus == 0 || sets * 8 * P * ((G + 7) / 8) <= cus; };
     const int KX = dppo_cdiv(XD + SD, 32);
-    const bool p4 = KX <= 2 && split4_lds_bytes(XD, SD, K, KX, dppo_cdiv(XD, 16)) <= 160 * 1024 && fits(4);
-    const bool p8 = ks_in == 2 && fits(8);
-    if (split_p_choice() == 8) return p8 ? 8 : (p4 ? 4 : 0);
-    return p4 ? 4 : (p8 ? 8 : 0);
+    const bool p4 = KX <= 2 && split4_lds_bytes(XD, SD, K, KX, dppo_cdiv(XD, 16)) <= 160 * 1024 && fits(4, 1);
+    const bool p8 = ks_in == 2 && fits(8, 1);
+    static const bool dual_on = [] { const char* e = getenv("DPPO_SPLIT_DUAL"); return !e || atoi(e) != 0; }();
+    // two sets only while two launches of them still fit side by side (the pipelined rollout keeps
+    // the next step's launch resident while this one runs)
+    const bool dual = dual_on && KF > 0 && KF < K && (cus == 0 || 2 * 2 * 8 * 4 * ((G + 7) / 8) <= cus);
+    if (split_p_choice() == 8) return p8 ? SplitPlan{8, false} : (p4 ? SplitPlan{4, dual} : SplitPlan{0, false});
+    return p4 ? SplitPlan{4, dual} : (p8 ? SplitPlan{8, false} : SplitPlan{0, false});
 }
 
-bool sample_split_supported(int precision, int H, int XD, int SD, int ks_in, int E, int K) {
-    return split_members_for(precision, H, XD, SD, ks_in, E, K) > 0;
+}  // namespace
+
+int split_members_for(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF) {
+    const SplitPlan p = split_plan(precision, H, XD, SD, ks_in, E, K, KF);
+    return p.P * (p.dual ? 2 : 1);
+}
+
+bool sample_split_supported(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF) {
+    return split_members_for(precision, H, XD, SD, ks_in, E, K, KF) > 0;
 }
 
 int sampler_device_cus() { return device_cus(); }
 
 int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s) {
-    const int P = split_members_for(precision, a.H, a.XD, a.SD, a.L.ks_in, a.E, a.K);
+    const SplitPlan plan = split_plan(precision, a.H, a.XD, a.SD, a.L.ks_in, a.E, a.K, a.KF);
+    const int P = plan.P;
     if (!P) return DPPO_EUNSUPPORTED;
     SplitArgs sa;
     sa.a = a;
+    sa.dual = plan.dual ? 1 : 0;
     sa.G = dppo_cdiv(a.E, 16);
     static const int force_shared = [] {
         const char* e = getenv("DPPO_SPLIT_XCHG");
