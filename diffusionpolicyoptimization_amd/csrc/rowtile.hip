@@ -864,10 +864,11 @@ static int launch_actor_2b(const ActorArgs& a, hipStream_t s) {
     // (walker2d / halfcheetah, XD = 24, run the 32-row tile)
     if (a.H == 512 && v == 0 && a.XD <= 16) {
         // The last round of 64-row tiles is short (minibatch 50,000 rows: 782 tiles = 3 rounds of
-        // 256 CUs + 14). Those tail tiles run as twice as many 32-row tiles (about 0.6 of a 64-row
-        // tile's time each) in a launch of their own, then the full rounds: the kernel's last
-        // round shrinks. DPPO_ACTOR_TAIL=0 disables it (measurement knob).
-        static const bool tail_on = [] { const char* e = getenv("DPPO_ACTOR_TAIL"); return !e || atoi(e) != 0; }();
+        // 256 CUs + 14). DPPO_ACTOR_TAIL=1 runs those tail tiles as twice as many 32-row tiles in a
+        // launch of their own before the full rounds. Off by default: with the critic's half on the
+        // side stream filling the CUs the short last round leaves idle, the separate launch cost
+        // more than it saved (update 16.5 -> 15.5 ms per iteration without it, same box).
+        static const bool tail_on = [] { const char* e = getenv("DPPO_ACTOR_TAIL"); return e && atoi(e) != 0; }();
         const bool tr = a.mode == ROWS_TRAIN || a.mode == ROWS_PRETRAIN;
         if (tail_on && tr && a.row0 == 0 && a.row_end == 0) {
             const int64_t tiles = (int64_t)a.ws.ldm / 64, cus = actor_device_cus();

@@ -498,8 +498,8 @@ def test_adv_stats_all_matches_per_minibatch(cuda):
 
 
 def test_actor_tail_split_matches_single_launch(tmp_path):
-    """A minibatch of 260 64-row tiles runs its short last round as 32-row tiles in a separate launch
-    (launch_actor_rowtile). Gradients and metrics must match the single-launch run
+    """With DPPO_ACTOR_TAIL=1 (off by default) a minibatch of 260 64-row tiles runs its short last
+    round as 32-row tiles in a separate launch (launch_actor_rowtile). Gradients and metrics must match the single-launch run
     (DPPO_ACTOR_TAIL=0) up to the float-atomic order of the dW sums. Two child processes: the
     switch is read once per process."""
     import subprocess
