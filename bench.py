@@ -35,14 +35,15 @@ def sampler_flops_per_env(d):
 
 CU_LOAD_PEAK_GBS = 64 * 2.4   # per-CU vector-memory (TA) path: 64 B/clk at the 2.4 GHz max clock
 
-# Latency floor of one denoising step of the split sampler (csrc/sampler_split.hip), the figure
-# its per-step time is compared with: one in-launch exchange of partial sums between the 8
-# workgroups of a 16-env group (tools/xchg_probe.hip measured 1.10 us per step with the members on
-# one XCD, 1.68 us spread) + the step's MFMA issue on one SIMD (2 waves x 28
-# v_mfma_f32_16x16x32_bf16 x 16 cycles at 2.4 GHz = 0.37 us). Everything else in a step (LDS
-# round trips, barriers, the DDPM epilogue) is latency this floor does not count.
-SPLIT_XCHG_US = 1.10
-SPLIT_MFMA_US = 2 * 28 * 16 / 2.4e3
+# Latency floor of one denoising step of the split sampler (csrc/sampler_split.hip, P = 4 members
+# per 16-env group, the default), the figure its per-step time is compared with: one in-launch
+# exchange of partial sums between the 4 workgroups of a group (tools/xchg_probe2.hip: 0.98 us per
+# step with the members on one XCD, sc0 granules, nothing else in the step) + the step's MFMA issue
+# on one SIMD (2 waves x 40 v_mfma_f32_16x16x32_bf16 x 16 cycles at 2.4 GHz = 0.53 us: in-Dense
+# 4, l1 16, l2 16, out-Dense 4 per wave). Everything else in a step (LDS round trips, barriers,
+# VALU epilogues, the DDPM update) is latency this floor does not count.
+SPLIT_XCHG_US = {4: 0.98, 8: 1.55}
+SPLIT_MFMA_US = {4: 2 * 40 * 16 / 2.4e3, 8: 2 * 28 * 16 / 2.4e3}
 
 
 def sampler_layout(d, precision, envs):
@@ -178,7 +179,8 @@ def main():
     flops = sampler_flops_per_env(d) * agent.n_envs
     prec = agent.model.precision
     members = sampler_layout(d, prec, agent.n_envs)
-    kname = "sample_split_kernel" if members else "sample_kernel"
+    p8 = os.environ.get("DPPO_SPLIT_P") == "8"
+    kname = ("sample_split_kernel" if p8 else "sample_split4_kernel") if members else "sample_kernel"
     achieved = flops / (samp_ms * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -187,14 +189,17 @@ def main():
         if kname + "<" in tj.get("kernel", "") and tj.get("precision") == prec and tj.get("envs") == agent.n_envs:
             traffic = tj.get("hbm_bytes_per_launch")
     if members:
+        P = 8 if p8 else 4
         step_us = samp_ms * 1e3 / d.denoising_steps
-        floor_us = SPLIT_XCHG_US + SPLIT_MFMA_US
-        bound = {"kind": "latency", "kernel": kname, "workgroups_per_16_envs": members,
+        floor_us = SPLIT_XCHG_US[P] + SPLIT_MFMA_US[P]
+        bound = {"kind": "latency", "kernel": kname, "workgroups_per_16_envs": members, "members_per_set": P,
                  "us_per_denoising_step": step_us, "floor_us_per_step": floor_us, "frac": floor_us / step_us,
-                 "note": ("each 16-env group runs on 8 CUs with 1/8 of the actor resident in registers; a "
-                          "denoising step is a dependent chain of 4 GEMMs (M = 16 envs) and one cross-CU "
-                          "partial-sum exchange, so its floor is that exchange (tools/xchg_probe.hip) plus "
-                          "the step's MFMA issue, not bytes or FLOPs; see DESIGN.md")}
+                 "note": (f"each 16-env group runs on {P} CUs with 1/{P} of an actor resident in registers and "
+                          "LDS (the base and fine-tuned actors' steps on two such member sets when "
+                          "workgroups_per_16_envs is twice members_per_set); a denoising step is a dependent "
+                          "chain of 4 GEMMs (M = 16 envs) and one cross-CU partial-sum exchange, so its floor "
+                          "is that exchange (tools/xchg_probe2.hip) plus the step's MFMA issue, not bytes or "
+                          "FLOPs; see DESIGN.md")}
     else:
         stream_b = sampler_stream_bytes_per_tile(d, prec)
         bound = {"kind": "load_path", "kernel": kname, "bytes_per_cu_per_launch": stream_b,
