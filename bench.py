@@ -129,6 +129,7 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=64)
     ap.add_argument("--n-steps", type=int, default=None, help="override S (chunks per rollout)")
     ap.add_argument("--precision", default=None)
+    ap.add_argument("--batch-size", type=int, default=None, help="override train.batch_size (measurement)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
@@ -144,6 +145,8 @@ def main():
         over.append(f"train.n_steps={args.n_steps}")
     if args.precision:
         over.append(f"model.precision={args.precision}")
+    if args.batch_size:
+        over.append(f"train.batch_size={args.batch_size}")
     cfg = load_config(args.config_dir, args.config_name, over)
     agent = get_class(cfg._target_)(cfg)
     rank = agent.rank

@@ -79,6 +79,9 @@ _SIGNATURES = {
                                     _P, _I64, _U64, _I, _I64, _I, _P, _P, _P, _P, _P, _I, _P]),
     "dppo_feistel_permute": (_I, [_I64, _I64, _I64, _U64, _I, _P, _P]),
     "dppo_adamw": (_I, [_P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P]),
+    "dppo_pack_all": (_I, [_DIMS, _I, _P, _P, _P, _P, _P]),
+    "dppo_optimizer_step": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P, _P,
+                                 _P, _I, _P]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -86,7 +89,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class DppoError(RuntimeError):

@@ -238,14 +238,18 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         # Here: a stop by minibatch i-1 of the SAME epoch drops i's gradients (the reference never
         # computes them) and ends the epoch; a stop by the previous epoch's last minibatch ended an
         # epoch that was over anyway, so i (the new epoch's first) is applied.
-        if not hasattr(self, "_met_pin"):
-            self._met_pin = [torch.zeros(5, dtype=torch.float64).pin_memory() for _ in range(2)]
+        # Each minibatch's metric sums land in mapped host memory, copied by its optimiser-step
+        # launch (dppo_optimizer_step) or, before the critic warm-up ends, by a plain copy; one event
+        # per slot marks them readable.
+        if not hasattr(self, "_met_map"):
+            self._met_map = [ops.MappedDoubles(8) for _ in range(2)]
+            self._ev_m = [torch.cuda.Event() for _ in range(2)]
         pending = None
 
         def finish(p):
             slot, ev, grows, _ = p
             ev.synchronize()
-            met = self._met_pin[slot].numpy() / grows
+            met = self._met_map[slot].array[:5] / grows
             self.timing["n_updates"] += 1
             inf = dict(pg_loss=float(met[0]), v_loss=float(met[1]), approx_kl=float(met[2]),
                        clipfrac=float(met[3]), ratio=float(met[4]), bc_loss=0.0, eta=1.0,
@@ -312,31 +316,41 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         stream.wait_stream(side)
                     self.minibatch_hook(update_epoch, batch, start, rows)
                 slot = k % 2
-                self._met_pin[slot].copy_(met[:5], non_blocking=True)
-                ev_m = torch.cuda.Event()
-                ev_m.record(stream)
                 if pending is not None:
                     info, stop = finish(pending)
                     same_epoch = pending[3] == update_epoch
                     pending = None
                     if stop and same_epoch:                                    # :366-368
                         break
+                # the optimiser step (agent :346): AdamW, the metric sums to the host and the weight
+                # images re-derived, one dppo_optimizer_step per stream (two launches each)
+                ng = m.grads.numel()
+                met_out = self._met_map[slot]
                 if self.itr >= self.n_critic_warmup_itr:
+                    opt = self.actor_optimizer
+                    lr = opt.begin_step()
                     if split:
-                        self.actor_optimizer.apply_gradients_split(
-                            m.grads, [(0, na, stream), (na, m.grads.numel(), side)])
-                        m.repack(part=1)
+                        opt.apply_range(m.grads, 0, na, lr, m.dims, m.precision,
+                                        packs={"actor": (m.actor_ft_params, m.packed_ft)},
+                                        metrics=met, metrics_out=met_out.address, n_metrics=5)
                         with torch.cuda.stream(side):
-                            m.repack(part=2)
+                            opt.apply_range(m.grads, na, ng, lr, m.dims, m.precision,
+                                            packs={"critic": (m.critic_params, m.packed_critic)})
                     else:
                         if self.max_grad_norm is not None:
                             self._clip_by_norm_per_tensor()
-                        self.actor_optimizer.apply_gradients(m.grads)
-                        m.repack()
+                        opt.apply_range(m.grads, 0, ng, lr, m.dims, m.precision,
+                                        packs={"actor": (m.actor_ft_params, m.packed_ft),
+                                               "critic": (m.critic_params, m.packed_critic)},
+                                        metrics=met, metrics_out=met_out.address, n_metrics=5)
+                else:
+                    torch.from_numpy(met_out.array[:5]).copy_(met[:5])
                 if self.update_events is not None:
                     ev1 = torch.cuda.Event(enable_timing=True)
                     ev1.record(stream)
                     self.update_events.append((ev0, ev1))
+                ev_m = self._ev_m[slot]
+                ev_m.record(stream)
                 pending = (slot, ev_m, global_rows, update_epoch)
                 k += 1
         if pending is not None:

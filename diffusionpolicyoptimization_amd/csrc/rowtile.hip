@@ -884,6 +884,12 @@ static int launch_actor_2b(const ActorArgs& a, hipStream_t s) {
                 return dispatch_actor<P2, 4, 16>(m, s);
             }
         }
+        // a minibatch of less than one round of 64-row tiles (the per-rank share of an 8-GPU run
+        // under the reference's global minibatch: 6,250 rows = 98 tiles) finishes in one tile's
+        // latency either way, and a 32-row tile's is about 0.6 of a 64-row tile's (update 50.1 ->
+        // 47.1 ms per iteration at 6,250-row minibatches, tools/ab_small_mb.sh)
+        const int64_t rows = (a.mode == ROWS_TRAIN || a.mode == ROWS_PRETRAIN) ? (int64_t)a.ws.ldm : a.nrows;
+        if ((rows + 63) / 64 < actor_device_cus()) return dispatch_actor<P2, 2, 8>(a, s);
         return dispatch_actor<P2, 4, 16>(a, s);
     }
     if (a.H == 512 && v == 3 && a.XD <= 16) return dispatch_actor<P2, 4, 8>(a, s);

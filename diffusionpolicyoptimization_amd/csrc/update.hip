@@ -440,7 +440,11 @@ __global__ void feistel_kernel(int64_t first, int64_t count, FeistelKey fk, int6
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, int64_t n, float lr, float wd, float b1, float b2,
-                                                    float eps, float alpha, float bc1, float bc2, int mode) {
+                                                    float eps, float alpha, float bc1, float bc2, int mode,
+                                                    const double* __restrict__ met, double* __restrict__ met_out, int nmet) {
+    // the minibatch's metric sums ride along (dppo_optimizer_step): one launch fewer on the
+    // minibatch's critical path than a separate copy
+    if (blockIdx.x == 0 && (int)threadIdx.x < nmet) met_out[threadIdx.x] = met[threadIdx.x];
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         float pi = p[i], gi = g[i], mi = m[i], vi = v[i];
         if (mode == DPPO_ADAMW_KERAS) {
@@ -460,21 +464,66 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
     }
 }
 
-extern "C" int dppo_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
-                          float weight_decay, float beta1, float beta2, float eps, int mode, void* stream) {
+static int launch_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
+                        float weight_decay, float beta1, float beta2, float eps, int mode, const double* met,
+                        double* met_out, int nmet, hipStream_t s) {
     DPPO_CHECK(n >= 0 && step >= 1, "dppo_adamw: n < 0 or step < 1");
-    if (n == 0) return DPPO_OK;
-    DPPO_CHECK(params && grads && m && v, "dppo_adamw: null pointer");
     DPPO_CHECK(mode == DPPO_ADAMW_KERAS || mode == DPPO_ADAMW_TORCH, "dppo_adamw: bad mode");
+    DPPO_CHECK(nmet >= 0 && nmet <= 256 && (nmet == 0 || (met && met_out)), "dppo_optimizer_step: bad metrics copy");
+    if (n == 0 && nmet == 0) return DPPO_OK;
+    DPPO_CHECK(n == 0 || (params && grads && m && v), "dppo_adamw: null pointer");
     const double bc1 = 1.0 - pow((double)beta1, (double)step);
     const double bc2 = 1.0 - pow((double)beta2, (double)step);
     const float alpha = (float)((double)lr * sqrt(bc2) / bc1);
     const int64_t blocks64 = (n + 255) / 256;
-    const unsigned blocks = (unsigned)(blocks64 < 4096 ? blocks64 : 4096);
-    hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads, m, v, n, lr,
-                       weight_decay, beta1, beta2, eps, alpha, (float)bc1, (float)bc2, mode);
+    const unsigned blocks = (unsigned)(blocks64 < 1 ? 1 : (blocks64 < 4096 ? blocks64 : 4096));
+    hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, params, grads, m, v, n, lr,
+                       weight_decay, beta1, beta2, eps, alpha, (float)bc1, (float)bc2, mode, met, met_out, nmet);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
+}
+
+extern "C" int dppo_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
+                          float weight_decay, float beta1, float beta2, float eps, int mode, void* stream) {
+    return launch_adamw(params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode, nullptr, nullptr, 0,
+                        (hipStream_t)stream);
+}
+
+extern "C" int dppo_optimizer_step(const dppo_dims* d, int precision, float* params, const float* grads, float* m,
+                                   float* v, int64_t n, int64_t step, float lr, float weight_decay, float beta1,
+                                   float beta2, float eps, int mode, const float* actor_params, void* packed_actor,
+                                   const float* critic_params, void* packed_critic, const double* metrics,
+                                   double* metrics_out, int n_metrics, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
+    DPPO_CHECK(!packed_actor == !actor_params && !packed_critic == !critic_params,
+               "dppo_optimizer_step: a packed image needs its parameters");
+    hipStream_t s = (hipStream_t)stream;
+    // metrics_out may be mapped host memory (dppo_host_alloc): the kernel stores through its
+    // device address
+    double* mout = metrics_out;
+    if (mout) {
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, metrics_out, 0) == hipSuccess && dp) mout = (double*)dp;
+        else (void)hipGetLastError();
+    }
+    rc = launch_adamw(params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode, metrics, mout,
+                      n_metrics, s);
+    if (rc) return rc;
+    return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s);
+}
+
+extern "C" int dppo_pack_all(const dppo_dims* d, int precision, const float* actor_params, void* packed_actor,
+                             const float* critic_params, void* packed_critic, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
+    DPPO_CHECK(!packed_actor == !actor_params && !packed_critic == !critic_params,
+               "dppo_pack_all: a packed image needs its parameters");
+    return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, (hipStream_t)stream);
 }
 
 extern "C" int dppo_feistel_permute(int64_t first, int64_t count, int64_t n, uint64_t seed, int epoch, int64_t* out,

@@ -106,9 +106,12 @@ class VPGDiffusion(DiffusionModel):
     def repack(self, part=None):
         """Re-derive the packed fragment images of actor_ft (part 1) and/or critic (part 2) after an
         optimiser step."""
-        if part in (None, 1):
+        if part is None:               # both images in one launch
+            ops.pack_all(self.dims, self.precision, self.actor_ft_params, self.packed_ft, self.critic_params,
+                         self.packed_critic)
+        elif part == 1:
             ops.pack_actor(self.dims, self.actor_ft_params, self.precision, out=self.packed_ft)
-        if part in (None, 2):
+        elif part == 2:
             ops.pack_critic(self.dims, self.critic_params, self.precision, out=self.packed_critic)
 
     def _load_actor(self, path, rng):

@@ -5,6 +5,7 @@ stream of the tensor's device. Shapes/dtypes are checked here before any launch 
 call can never reach a kernel with mismatched extents.
 """
 import ctypes
+import functools
 import os
 import math
 from dataclasses import dataclass
@@ -65,6 +66,30 @@ def spec_count(spec):
     return int(sum(int(np.prod(s)) for _, s in spec))
 
 
+# Per-dims constants of the hot host paths, computed once: the update loop calls the minibatch,
+# optimiser and repack wrappers ~10x per PPO minibatch, and at the per-rank minibatch of an 8-GPU
+# run (6,250 rows) their Python cost, not the GPU, set the pace.
+@functools.lru_cache(maxsize=None)
+def _dims_c(d):
+    return d.c()
+
+
+@functools.lru_cache(maxsize=None)
+def _n_params(d):
+    return spec_count(actor_param_spec(d)), spec_count(critic_param_spec(d))
+
+
+@functools.lru_cache(maxsize=None)
+def _packed_bytes(d, prec):
+    return (int(_lib.query("dppo_actor_packed_bytes", ctypes.byref(_dims_c(d)), prec)),
+            int(_lib.query("dppo_critic_packed_bytes", ctypes.byref(_dims_c(d)), prec)))
+
+
+@functools.lru_cache(maxsize=None)
+def _workspace_bytes(d, prec, rows):
+    return int(_lib.query("dppo_ppo_workspace_bytes", ctypes.byref(_dims_c(d)), prec, int(rows)))
+
+
 def flatten_params(spec, params):
     return np.concatenate([np.asarray(params[n], np.float32).reshape(-1) for n, _ in spec])
 
@@ -103,24 +128,79 @@ def actor_packed_bytes(d: ModelDims, precision):
     return int(_lib.query("dppo_actor_packed_bytes", ctypes.byref(d.c()), _prec(precision)))
 
 
+def pack_all(d: ModelDims, precision, actor_params=None, packed_actor=None, critic_params=None, packed_critic=None):
+    """Both images (either pair may be None) in one launch (dppo_pack_all)."""
+    p = _prec(precision)
+    na, nc = _n_params(d)
+    ab, cb = _packed_bytes(d, p)
+    _check(actor_params, (na,), torch.float32, "actor params")
+    _check(packed_actor, (ab,), torch.uint8, "packed actor")
+    _check(critic_params, (nc,), torch.float32, "critic params")
+    _check(packed_critic, (cb,), torch.uint8, "packed critic")
+    t = actor_params if actor_params is not None else critic_params
+    _lib.call("dppo_pack_all", ctypes.byref(_dims_c(d)), p, ptr(actor_params), ptr(packed_actor), ptr(critic_params),
+              ptr(packed_critic), stream_handle(t.device))
+
+
+def optimizer_step(d: ModelDims, precision, params, grads, m, v, step, lr, weight_decay, beta1, beta2, eps, mode,
+                   actor_params=None, packed_actor=None, critic_params=None, packed_critic=None, metrics=None,
+                   metrics_out=None, n_metrics=0):
+    """AdamW over params/grads/m/v (equal-length flat ranges), the metric sums copied to
+    metrics_out (a device tensor or a dppo_host_alloc address), then the given images re-derived:
+    two launches on the current stream (dppo_optimizer_step)."""
+    n = params.numel()
+    for t, nm in ((grads, "grads"), (m, "m"), (v, "v")):
+        if t.numel() != n:
+            raise ValueError(f"{nm}: expected {n} elements")
+    p = _prec(precision)
+    mo = metrics_out if isinstance(metrics_out, int) else (metrics_out.data_ptr() if metrics_out is not None else None)
+    _lib.call("dppo_optimizer_step", ctypes.byref(_dims_c(d)), p, ptr(params), ptr(grads), ptr(m), ptr(v), int(n),
+              int(step), float(lr), float(weight_decay), float(beta1), float(beta2), float(eps),
+              _lib.DPPO_ADAMW_KERAS if mode == "keras" else _lib.DPPO_ADAMW_TORCH, ptr(actor_params), ptr(packed_actor),
+              ptr(critic_params), ptr(packed_critic), ptr(metrics), ctypes.c_void_p(mo) if mo else None,
+              int(n_metrics), stream_handle(params.device))
+
+
+class MappedDoubles:
+    """n doubles of coherent mapped pinned memory (dppo_host_alloc) the device stores into and the
+    host reads as a numpy array (the PPO metric sums of dppo_optimizer_step)."""
+
+    def __init__(self, n):
+        p = ctypes.c_void_p()
+        _lib.call("dppo_host_alloc", ctypes.c_size_t(8 * n), ctypes.byref(p))
+        self.address = p.value
+        self.array = np.ctypeslib.as_array((ctypes.c_double * n).from_address(self.address))
+
+    def __del__(self):
+        if getattr(self, "address", None) and _lib._lib is not None:
+            _lib.query("dppo_host_free", ctypes.c_void_p(self.address))
+            self.address = None
+
+
 def critic_packed_bytes(d: ModelDims, precision):
     return int(_lib.query("dppo_critic_packed_bytes", ctypes.byref(d.c()), _prec(precision)))
 
 
 def pack_actor(d: ModelDims, params_flat, precision, out=None):
-    _check(params_flat, (spec_count(actor_param_spec(d)),), torch.float32, "actor params")
+    p = _prec(precision)
+    _check(params_flat, (_n_params(d)[0],), torch.float32, "actor params")
     if out is None:
-        out = torch.empty(actor_packed_bytes(d, precision), dtype=torch.uint8, device=params_flat.device)
-    _lib.call("dppo_pack_actor", ctypes.byref(d.c()), _prec(precision), ptr(params_flat), ptr(out),
+        out = torch.empty(_packed_bytes(d, p)[0], dtype=torch.uint8, device=params_flat.device)
+    else:
+        _check(out, (_packed_bytes(d, p)[0],), torch.uint8, "packed actor")
+    _lib.call("dppo_pack_actor", ctypes.byref(_dims_c(d)), p, ptr(params_flat), ptr(out),
               stream_handle(params_flat.device))
     return out
 
 
 def pack_critic(d: ModelDims, params_flat, precision, out=None):
-    _check(params_flat, (spec_count(critic_param_spec(d)),), torch.float32, "critic params")
+    p = _prec(precision)
+    _check(params_flat, (_n_params(d)[1],), torch.float32, "critic params")
     if out is None:
-        out = torch.empty(critic_packed_bytes(d, precision), dtype=torch.uint8, device=params_flat.device)
-    _lib.call("dppo_pack_critic", ctypes.byref(d.c()), _prec(precision), ptr(params_flat), ptr(out),
+        out = torch.empty(_packed_bytes(d, p)[1], dtype=torch.uint8, device=params_flat.device)
+    else:
+        _check(out, (_packed_bytes(d, p)[1],), torch.uint8, "packed critic")
+    _lib.call("dppo_pack_critic", ctypes.byref(_dims_c(d)), p, ptr(params_flat), ptr(out),
               stream_handle(params_flat.device))
     return out
 
@@ -510,7 +590,7 @@ def ppo_minibatch(d: ModelDims, precision, hp, packed_ft, packed_critic, actor_p
     _check(lp_old_mean, (n, kf), torch.float32, "lp_old_mean")
     _check(advantages, (n,), torch.float32, "advantages")
     _check(returns, (n,), torch.float32, "returns")
-    na, nc = spec_count(actor_param_spec(d)), spec_count(critic_param_spec(d))
+    na, nc = _n_params(d)
     _check(actor_params, (na,), torch.float32, "actor_params")
     _check(grads, (na + nc,), torch.float32, "grads")
     _check(metrics, (16,), torch.float64, "metrics")
@@ -518,10 +598,10 @@ def ppo_minibatch(d: ModelDims, precision, hp, packed_ft, packed_critic, actor_p
         _check(row_index, (row_index.numel(),), torch.int64, "row_index")
         if row_index.numel() < start + rows:
             raise ValueError("row_index shorter than start + rows")
-    need = int(_lib.query("dppo_ppo_workspace_bytes", ctypes.byref(d.c()), _prec(precision), int(rows)))
+    need = _workspace_bytes(d, _prec(precision), int(rows))
     if workspace.numel() < need:
         raise ValueError(f"workspace too small: {workspace.numel()} < {need}")
-    args = (ctypes.byref(d.c()), _prec(precision), ctypes.byref(hp), ptr(packed_ft), ptr(packed_critic),
+    args = (ctypes.byref(_dims_c(d)), _prec(precision), ctypes.byref(hp), ptr(packed_ft), ptr(packed_critic),
             ptr(actor_params), ptr(sched), ptr(obs), ptr(chains), ptr(lp_old_mean), ptr(advantages), ptr(returns),
             int(n * kf), ctypes.c_uint64(perm_seed), int(epoch), int(start), int(rows), ptr(row_index), ptr(adv_stats),
             ptr(workspace), ptr(grads), ptr(metrics))

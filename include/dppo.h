@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 3
+#define DPPO_ABI_VERSION 4
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -271,6 +271,23 @@ DPPO_API int dppo_feistel_permute(int64_t first, int64_t count, int64_t n, uint6
  * train_ppo_agent.py:45-49). step is 1-based. ---- */
 DPPO_API int dppo_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
                float weight_decay, float beta1, float beta2, float eps, int mode, void* stream);
+
+/* Re-derive the packed images of the actor and/or the critic (either pair may be null) in ONE
+ * launch; the actor's includes its time tables. = dppo_pack_actor + dppo_pack_critic. */
+DPPO_API int dppo_pack_all(const dppo_dims* d, int precision, const float* actor_params, void* packed_actor,
+                  const float* critic_params, void* packed_critic, void* stream);
+
+/* One optimiser step after a PPO minibatch as two launches on `stream`
+ * (train_ppo_diffusion_agent.py:346 apply_gradients, then the weight images every kernel reads):
+ * dppo_adamw over the n elements at params/grads/m/v (a range of the flat [actor | critic]
+ * buffer), which also copies n_metrics (<= 256) doubles of `metrics` to `metrics_out` (device or
+ * host-mapped memory; the minibatch's metric sums for the host's target_kl check), then
+ * dppo_pack_all of the given networks. */
+DPPO_API int dppo_optimizer_step(const dppo_dims* d, int precision, float* params, const float* grads, float* m,
+                        float* v, int64_t n, int64_t step, float lr, float weight_decay, float beta1,
+                        float beta2, float eps, int mode, const float* actor_params, void* packed_actor,
+                        const float* critic_params, void* packed_critic, const double* metrics,
+                        double* metrics_out, int n_metrics, void* stream);
 
 #ifdef __cplusplus
 }

@@ -544,8 +544,8 @@ def test_logprob_pass_full_size(cuda):
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 def test_ppo_minibatch_full_size(cuda, precision):
-    """dppo_ppo_minibatch at the bench's minibatch, b = 50,000 rows (782 64-row actor tiles, the
-    32-row tail launch, split-K dW over all rows), over a 64,000-row rollout. The full-size launch is
+    """dppo_ppo_minibatch at the bench's minibatch, b = 50,000 rows (782 64-row actor tiles,
+    split-K dW over all rows), over a 64,000-row rollout. The full-size launch is
     checked through a size-independent property and the oracle:
       * linearity: the loss is a mean over rows, so the gradient and metric sums of the full
         launch equal the sum over 25 disjoint 2,000-row slices of the same rows (row_index), each
@@ -597,8 +597,11 @@ def test_ppo_minibatch_full_size(cuda, precision):
     rel = np.abs(g_sum - g_full).max() / np.abs(g_full).max()
     assert rel < (1e-5 if precision == "fp32" else 1e-4), rel
     # metric sums (pg, v, approx_kl, clipfrac, ratio) over 50,000 rows: fp32 accumulation order;
-    # approx_kl is ~0 at ratio 1 (bf16 case), so it gets an absolute bound
-    np.testing.assert_allclose(m_sum, m_full, rtol=1e-5, atol=1e-5)
+    # approx_kl is ~0 at ratio 1 (bf16 case), so it gets an absolute bound. The 2,000-row slices run
+    # 32-row actor tiles (a sub-round minibatch), whose out-layer sums in another order: with 2-byte
+    # operands that moves log-prob ulps, and the pg sum over 50,000 rows by ~6e-5 relative
+    tol = 1e-5 if precision == "fp32" else 2e-4
+    np.testing.assert_allclose(m_sum, m_full, rtol=tol, atol=tol)
     # slice 7 against the oracle
     rows = perm.cpu().numpy()[14000:16000]
     bi, di = rows // kf, rows % kf
