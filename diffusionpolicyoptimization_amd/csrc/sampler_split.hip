@@ -727,8 +727,8 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
 //              folded through the out-Dense into B_OUT2
 //   out-Dense  as above (hi/lo split of the member's partial h3 from registers)
 // so no wave adds a bias or a residual outside an MFMA, and no wave re-sums l1 partials.
-template <class Pol, int XQ, int KX, bool INJ>
-__global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
+template <class Pol, int XQ, int KX, bool INJ, int SWV>
+__global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     constexpr int P = 4;
     constexpr int NO = (4 * XQ + 15) / 16;
     using AT = typename Pol::AT;
@@ -736,7 +736,11 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
     constexpr int H = SPLIT_H, KSH = H / 32;
     constexpr int HS = H / P;              // features per member slice (128)
     constexpr int KS2 = HS / 32;           // l2 k-steps per member (4)
-    static_assert(HS / 16 == SW, "l1: one n-tile of the member slice per wave");
+    constexpr int SW = SWV;                // waves per member: 8 (2 per SIMD) or 4 (1 per SIMD)
+    constexpr int NTI = 32 / SW;           // in-Dense / l2 n-tiles per wave (the same h1 / h3 features)
+    constexpr int NL1 = (HS / 16) / SW;    // l1 n-tiles of the member slice per wave
+    constexpr int KO = NTI / 2;            // out-Dense k-steps per wave (its own h3 features)
+    static_assert(NL1 * SW == HS / 16 && NTI * SW == 32 && NTI % 2 == 0, "split geometry");
     constexpr int NOC = 16 * NO;
     constexpr int ST = SW * 64;
     constexpr int pad = 16;
@@ -781,14 +785,14 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
     float* sch = (float*)(smem + o); o += dppo_align16(4 * K * DPPO_SCHED_COLS);
     float* bias = (float*)(smem + o); o += dppo_align16(4 * 2 * NB);
     float* zt = (float*)(smem + o); o += dppo_align16(4 * K * 16 * XD);
-    u32x4* wxs = (u32x4*)(smem + o); o += (size_t)SW * 4 * KX * 1024;     // [wave][n][ks] in-Dense fragments
-    u32x4* routl = (u32x4*)(smem + o); o += (size_t)SW * 2 * NO * 1024;   // [wave][s][n] out-Dense fragments
+    u32x4* wxs = (u32x4*)(smem + o); o += (size_t)SW * NTI * KX * 1024;   // [wave][n][ks] in-Dense fragments
+    u32x4* routl = (u32x4*)(smem + o); o += (size_t)SW * KO * NO * 1024;  // [wave][s][n] out-Dense fragments
 
     // ---- resident weight fragments (one actor at a time): l1 and l2 in registers; the in-Dense
     //      and out-Dense fragments in this wave's own LDS (24 VGPRs the l1 pipeline needs) ----
     const __amdgpu_buffer_rsrc_t rs_base = packed_rsrc(a.packed_base), rs_ft = packed_rsrc(a.packed_ft);
     auto W = [&](int ft, int seg) { return wsrc(ft ? rs_ft : rs_base, L.off[seg]); };
-    u32x4 rl1[KSH], rl2[KS2][4];
+    u32x4 rl1[NL1][KSH], rl2[KS2][NTI];
     // LDS-DMA of one 1 KiB fragment (lane l's 16 B land at dst + 16 l); wave-private destinations,
     // consumed only after this wave's vmcnt(0)
     auto dma_frag = [&](int ft, int seg, int KS, int ntile, int ks, u32x4* dst) {
@@ -799,32 +803,34 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
 #pragma unroll
         for (int ks = 0; ks < KX; ++ks)
 #pragma unroll
-            for (int n = 0; n < 4; ++n) dma_frag(ft, SEG_W_XS, KSX, 4 * wave + n, ks, wxs + ((wave * 4 + n) * KX + ks) * 64);
+            for (int n = 0; n < NTI; ++n) dma_frag(ft, SEG_W_XS, KSX, NTI * wave + n, ks, wxs + ((wave * NTI + n) * KX + ks) * 64);
     };
     auto load_l1 = [&](int ft) {
 #pragma unroll
-        for (int j = 0; j < KSH; ++j) rl1[j] = load_bfrag_c(W(ft, SEG_W_L1), KSH, (HS / 16) * c + wave, j, lane);
+        for (int t = 0; t < NL1; ++t)
+#pragma unroll
+            for (int j = 0; j < KSH; ++j) rl1[t][j] = load_bfrag_c(W(ft, SEG_W_L1), KSH, (HS / 16) * c + NL1 * wave + t, j, lane);
     };
     auto load_l2 = [&](int ft) {
 #pragma unroll
         for (int s = 0; s < KS2; ++s)
 #pragma unroll
-            for (int n = 0; n < 4; ++n) rl2[s][n] = load_bfrag_c(W(ft, SEG_W_L2), KSH, 4 * wave + n, c * KS2 + s, lane);
+            for (int n = 0; n < NTI; ++n) rl2[s][n] = load_bfrag_c(W(ft, SEG_W_L2), KSH, NTI * wave + n, c * KS2 + s, lane);
     };
     auto load_out = [&](int ft) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < KO; ++s)
 #pragma unroll
-            for (int n = 0; n < NO; ++n) dma_frag(ft, SEG_W_OUT, KSH, n, 2 * wave + s, routl + (wave * 2 * NO + s * NO + n) * 64);
+            for (int n = 0; n < NO; ++n) dma_frag(ft, SEG_W_OUT, KSH, n, KO * wave + s, routl + (wave * KO * NO + s * NO + n) * 64);
     };
     // re-order the DMA'd out-Dense fragments in place to the transposed-result k-slot order
     // (slot_feature), once per actor (one wave's LDS ops complete in order)
     auto permute_out = [&]() {
-        u32x4* stg = routl + wave * 2 * NO * 64;
+        u32x4* stg = routl + wave * KO * NO * 64;
         const int j = lane >> 4, q = lane & 15;
-        u32x4 pr[2][NO];
+        u32x4 pr[KO][NO];
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < KO; ++s)
 #pragma unroll
             for (int n = 0; n < NO; ++n) {
                 const uint16_t* src = (const uint16_t*)(stg + (s * NO + n) * 64);
@@ -840,7 +846,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
             }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < KO; ++s)
 #pragma unroll
             for (int n = 0; n < NO; ++n) stg[(s * NO + n) * 64 + lane] = pr[s][n];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1021,23 +1027,29 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
         const float esd = sch[i * DPPO_SCHED_COLS + 4];
         const float xe = xs[ve], ze = zt[i * 16 * XD + ve], be = bb[H + qe];
         // ---- in-Dense (transposed): h1 = TIN[t] + W_xs^T [x; state]; no activation (mlp.py:144)
-        f32x4 h1[4];
+        f32x4 h1[NTI];
         {
-            u32x4 af[KX], wf[KX][4];
+            u32x4 af[KX], wf[KX][NTI];
 #pragma unroll
             for (int ks = 0; ks < KX; ++ks) af[ks] = lds_afrag<Pol>(a0, lda0, 0, ks, lane);
 #pragma unroll
-            for (int n = 0; n < 4; ++n) h1[n] = *(const f32x4*)(tin + t * H + 16 * (4 * wave + n) + 4 * jq);
+            for (int n = 0; n < NTI; ++n) h1[n] = *(const f32x4*)(tin + t * H + 16 * (NTI * wave + n) + 4 * jq);
 #pragma unroll
             for (int ks = 0; ks < KX; ++ks)
 #pragma unroll
-                for (int n = 0; n < 4; ++n) wf[ks][n] = wxs[((wave * 4 + n) * KX + ks) * 64 + lane];
+                for (int n = 0; n < NTI; ++n) wf[ks][n] = wxs[((wave * NTI + n) * KX + ks) * 64 + lane];
             // one LDS round trip for all of them
 #if DPPO_S4_INREADY
             asm volatile("" ::"v"(af[0]), "v"(h1[0]), "v"(h1[1]), "v"(h1[2]), "v"(h1[3]), "v"(wf[0][0]), "v"(wf[0][1]),
                          "v"(wf[0][2]), "v"(wf[0][3]));
+            if constexpr (NTI == 8)
+                asm volatile("" ::"v"(h1[NTI - 4]), "v"(h1[NTI - 3]), "v"(h1[NTI - 2]), "v"(h1[NTI - 1]), "v"(wf[0][NTI - 4]),
+                             "v"(wf[0][NTI - 3]), "v"(wf[0][NTI - 2]), "v"(wf[0][NTI - 1]));
             if constexpr (KX == 2)
                 asm volatile("" ::"v"(af[KX - 1]), "v"(wf[KX - 1][0]), "v"(wf[KX - 1][1]), "v"(wf[KX - 1][2]), "v"(wf[KX - 1][3]));
+            if constexpr (KX == 2 && NTI == 8)
+                asm volatile("" ::"v"(wf[KX - 1][NTI - 4]), "v"(wf[KX - 1][NTI - 3]), "v"(wf[KX - 1][NTI - 2]),
+                             "v"(wf[KX - 1][NTI - 1]));
 #endif
 #if DPPO_S4_EPIEARLY
             asm volatile("" ::"v"(ec), "v"(esd), "v"(xe), "v"(ze), "v"(be));
@@ -1045,11 +1057,11 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
 #pragma unroll
             for (int ks = 0; ks < KX; ++ks)
 #pragma unroll
-                for (int n = 0; n < 4; ++n) h1[n] = Pol::mma(wf[ks][n], af[ks], h1[n]);
+                for (int n = 0; n < NTI; ++n) h1[n] = Pol::mma(wf[ks][n], af[ks], h1[n]);
             if (pre) load_in(PKn);
 #pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                const int f = 16 * (4 * wave + n) + 4 * jq;
+            for (int n = 0; n < NTI; ++n) {
+                const int f = 16 * (NTI * wave + n) + 4 * jq;
                 u32x2 pk;
                 pk[0] = pack_bf16x2(relu_f(h1[n][0]), relu_f(h1[n][1]));
                 pk[1] = pack_bf16x2(relu_f(h1[n][2]), relu_f(h1[n][3]));
@@ -1062,48 +1074,55 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
         // ---- l1 (transposed): n-tile `wave` of this member's output columns over all 512 inputs,
         //      from b_l1; out as u2 = bf16 relu(h2) (mlp.py:202-206)
         {
-            f32x4 acc = *(const f32x4*)(bb + HS * c + 16 * wave + 4 * jq);
+            f32x4 acc[NL1];
+#pragma unroll
+            for (int tt = 0; tt < NL1; ++tt) acc[tt] = *(const f32x4*)(bb + HS * c + 16 * (NL1 * wave + tt) + 4 * jq);
             u32x4 fb[KSH];
 #pragma unroll
             for (int j = 0; j < KSH; ++j) fb[j] = lds_afrag<Pol>(u1, ldh, 0, j, lane);
 #pragma unroll
-            for (int j = 0; j < KSH; ++j) acc = Pol::mma(rl1[j], fb[j], acc);
+            for (int j = 0; j < KSH; ++j)
+#pragma unroll
+                for (int tt = 0; tt < NL1; ++tt) acc[tt] = Pol::mma(rl1[tt][j], fb[j], acc[tt]);
             // schedule: the bias and L1D fragment reads first, then one read per MFMA, so L1D reads
             // stay in flight ahead of the chain (left alone, hipcc issued read -> wait -> MFMA)
             constexpr int L1D = DPPO_S4_L1D;
-            __builtin_amdgcn_sched_group_barrier(0x100, L1D + 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, L1D + NL1, 0);
 #pragma unroll
             for (int j = 0; j < KSH - L1D; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, NL1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
-            __builtin_amdgcn_sched_group_barrier(0x008, L1D, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NL1 * L1D, 0);
             if (pre) load_l1(PKn);
-            u32x2 pk;
-            pk[0] = pack_bf16x2(relu_f(acc[0]), relu_f(acc[1]));
-            pk[1] = pack_bf16x2(relu_f(acc[2]), relu_f(acc[3]));
-            *(u32x2*)(u2 + env * ldu2 + 16 * wave + 4 * jq) = pk;
+#pragma unroll
+            for (int tt = 0; tt < NL1; ++tt) {
+                u32x2 pk;
+                pk[0] = pack_bf16x2(relu_f(acc[tt][0]), relu_f(acc[tt][1]));
+                pk[1] = pack_bf16x2(relu_f(acc[tt][2]), relu_f(acc[tt][3]));
+                *(u32x2*)(u2 + env * ldu2 + 16 * (NL1 * wave + tt) + 4 * jq) = pk;
+            }
         }
         XPHASE(12);
         lds_sync();
         XPHASE(3);
         // ---- l2 (transposed) over this member's K-slice; member 0 starts from the residual h1
-        f32x4 h3[4];
+        f32x4 h3[NTI];
         {
             u32x4 bf[KS2];
 #pragma unroll
             for (int s = 0; s < KS2; ++s) bf[s] = lds_afrag<Pol>(u2, ldu2, 0, s, lane);
             if (c == 0) {
 #pragma unroll
-                for (int n = 0; n < 4; ++n) h3[n] = Pol::mma(rl2[0][n], bf[0], h1[n]);
+                for (int n = 0; n < NTI; ++n) h3[n] = Pol::mma(rl2[0][n], bf[0], h1[n]);
             } else {
 #pragma unroll
-                for (int n = 0; n < 4; ++n) h3[n] = Pol::mma(rl2[0][n], bf[0], f32x4{0.f, 0.f, 0.f, 0.f});
+                for (int n = 0; n < NTI; ++n) h3[n] = Pol::mma(rl2[0][n], bf[0], f32x4{0.f, 0.f, 0.f, 0.f});
             }
 #pragma unroll
             for (int s = 1; s < KS2; ++s)
 #pragma unroll
-                for (int n = 0; n < 4; ++n) h3[n] = Pol::mma(rl2[s][n], bf[s], h3[n]);
+                for (int n = 0; n < NTI; ++n) h3[n] = Pol::mma(rl2[s][n], bf[s], h3[n]);
             if (pre) load_l2(PKn);
         }
         XPHASE(13);
@@ -1113,7 +1132,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
 #pragma unroll
             for (int n = 0; n < NO; ++n) { zero_acc(po[n]); zero_acc(pl[n]); }
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
+            for (int s = 0; s < KO; ++s) {
                 float hv[8];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) { hv[e] = h3[2 * s][e]; hv[4 + e] = h3[2 * s + 1][e]; }
@@ -1127,7 +1146,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
                 }
 #pragma unroll
                 for (int n = 0; n < NO; ++n) {
-                    const u32x4 wo = routl[(wave * 2 * NO + s * NO + n) * 64 + lane];
+                    const u32x4 wo = routl[(wave * KO * NO + s * NO + n) * 64 + lane];
                     po[n] = Pol::mma(wo, hi, po[n]);
                     pl[n] = Pol::mma(wo, lo, pl[n]);
                 }
@@ -1153,7 +1172,8 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
 #pragma unroll
                 for (int w = 0; w < SW; ++w) pp[w] = part[w * NV + vw + lane];
 #if DPPO_S4_PUBREADY
-                asm volatile("" ::"v"(pp[0]), "v"(pp[1]), "v"(pp[2]), "v"(pp[3]), "v"(pp[4]), "v"(pp[5]), "v"(pp[6]), "v"(pp[7]));
+                asm volatile("" ::"v"(pp[0]), "v"(pp[1]), "v"(pp[2]), "v"(pp[3]));
+                if constexpr (SW == 8) asm volatile("" ::"v"(pp[SW - 4]), "v"(pp[SW - 3]), "v"(pp[SW - 2]), "v"(pp[SW - 1]));
 #endif
                 float sum = pp[0];
 #pragma unroll
@@ -1256,13 +1276,13 @@ __global__ __launch_bounds__(SW * 64) void sample_split4_kernel(SplitArgs sa) {
     XPHASE(10);
 }
 
-size_t split4_lds_bytes(int XD, int SD, int K, int KX, int NO) {
+size_t split4_lds_bytes(int XD, int SD, int K, int KX, int NO, int sw) {
     const int pad = 16, ldh = SPLIT_H + pad, ldu2 = SPLIT_H / 4 + pad, lda0 = KX * 32 + pad;
     size_t o = 0;
     o += dppo_align16(2 * 16 * lda0);
     o += dppo_align16(2 * 16 * ldh);
     o += dppo_align16(2 * 16 * ldu2);
-    o += dppo_align16(4 * SW * 16 * XD);
+    o += dppo_align16(4 * sw * 16 * XD);
     o += 16;
     o += dppo_align16(4 * 16 * XD);
     o += dppo_align16(4 * 16 * SD);
@@ -1270,8 +1290,8 @@ size_t split4_lds_bytes(int XD, int SD, int K, int KX, int NO) {
     o += dppo_align16(4 * K * DPPO_SCHED_COLS);
     o += dppo_align16(4 * 2 * (SPLIT_H + 16 * NO));
     o += dppo_align16(4 * K * 16 * XD);
-    o += (size_t)SW * 4 * KX * 1024;
-    o += (size_t)SW * 2 * NO * 1024;
+    o += (size_t)32 * KX * 1024;                  // sw waves x 32/sw n-tiles x KX k-steps
+    o += (size_t)16 * NO * 1024;                  // sw waves x 16/sw k-steps x NO n-tiles
     return o;
 }
 
@@ -1373,18 +1393,30 @@ int launch_split_k(const SplitArgs& sa, hipStream_t s) {
     return DPPO_OK;
 }
 
-template <class Pol, int XQ, int KX, bool INJ>
-int launch_split4_k(const SplitArgs& sa, hipStream_t s) {
+// waves per member of the P = 4 kernel. The kernel also builds with 4 (one wave per SIMD, 512
+// registers: the l1 / l2 fragments partly in AGPRs, each wave two l1 n-tiles and eight in-Dense /
+// l2 n-tiles): measured 63.7 vs 59.3 us per launch at 8 (no second wave to hide its latencies), so
+// only 8 is instantiated
+constexpr int SPLIT4_WAVES = 8;
+int split_waves() { return SPLIT4_WAVES; }
+
+template <class Pol, int XQ, int KX, bool INJ, int SWV>
+int launch_split4_kw(const SplitArgs& sa, hipStream_t s) {
     constexpr int NO = (4 * XQ + 15) / 16;
-    auto k = sample_split4_kernel<Pol, XQ, KX, INJ>;
+    auto k = sample_split4_kernel<Pol, XQ, KX, INJ, SWV>;
     const SampleArgs& a = sa.a;
-    const size_t lds = split4_lds_bytes(a.XD, a.SD, a.K, KX, NO);
+    const size_t lds = split4_lds_bytes(a.XD, a.SD, a.K, KX, NO, SWV);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler needs %zu B of LDS", lds);
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int blocks = 8 * 4 * ((sa.G + 7) / 8) * (sa.dual ? 2 : 1);
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(SW * 64), lds, s, sa);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(SWV * 64), lds, s, sa);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
+}
+
+template <class Pol, int XQ, int KX, bool INJ>
+int launch_split4_k(const SplitArgs& sa, hipStream_t s) {
+    return launch_split4_kw<Pol, XQ, KX, INJ, SPLIT4_WAVES>(sa, s);
 }
 
 // DPPO_SPLIT_P: members per 16-env group, 4 (default) or 8 (the r01 kernel; A/B knob)
@@ -1409,7 +1441,8 @@ SplitPlan split_plan(int precision, int H, int XD, int SD, int ks_in, int E, int
     // every workgroup of the launch co-resident (one per CU: the register budget)
     auto fits = [&](int P, int sets) { return cus == 0 || sets * 8 * P * ((G + 7) / 8) <= cus; };
     const int KX = dppo_cdiv(XD + SD, 32);
-    const bool p4 = KX <= 2 && split4_lds_bytes(XD, SD, K, KX, dppo_cdiv(XD, 16)) <= 160 * 1024 && fits(4, 1);
+    const bool p4 = KX <= 2 && split4_lds_bytes(XD, SD, K, KX, dppo_cdiv(XD, 16), split_waves()) <= 160 * 1024 &&
+                    fits(4, 1);
     const bool p8 = ks_in == 2 && fits(8, 1);
     static const bool dual_on = [] { const char* e = getenv("DPPO_SPLIT_DUAL"); return !e || atoi(e) != 0; }();
     // two sets only while two launches of them still fit side by side (the pipelined rollout keeps
