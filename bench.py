@@ -155,7 +155,9 @@ def main():
 
     for _ in range(args.warmup):
         agent.iteration(force_train=True)
-    agent.sampler_events, agent.update_events = [], []
+    # the timed region carries no per-minibatch HIP timing events (their records sit on the
+    # minibatch chain); ppo_minibatch_avg_ms comes from one instrumented iteration after it
+    agent.sampler_events, agent.update_events = None, None
     agent.timing.update(rollout_s=0.0, update_s=0.0, n_updates=0, env_steps=0, iters=0)
 
     def barrier():
@@ -173,12 +175,18 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, t_roll, t_upd = t.tolist()
+    n_updates = agent.timing["n_updates"]
 
+    agent.sampler_events, agent.update_events = [], []   # instrumented, untimed
+    agent.host_profile = {}
+    agent.iteration(force_train=True)
+    barrier()
+    hp = agent.host_profile
+    host_us = {k: 1e6 * v / max(1, hp.get("minibatches", 0)) for k, v in hp.items() if k != "minibatches"}
     loop_samp_ms = sum(a.elapsed_time(b) for a, b in agent.sampler_events) / max(1, len(agent.sampler_events))
     samp_ms, n_burst = sampler_burst_ms(agent)
     upd_ms = sum(a.elapsed_time(b) for a, b in agent.update_events) / max(1, len(agent.update_events))
     env_steps = agent.n_envs_global * cfg.act_steps * cfg.train.n_steps * args.steps
-    n_updates = agent.timing["n_updates"]
     flops = sampler_flops_per_env(d) * agent.n_envs
     prec = agent.model.precision
     members = sampler_layout(d, prec, agent.n_envs)
@@ -236,6 +244,7 @@ def main():
                               "K x 4 small GEMMs, far below MFMA peak by construction; sampler_bound gives "
                               "the figure that bounds it")},
         "ppo_minibatch_avg_ms": upd_ms,
+        "host_us_per_minibatch": host_us,
     }
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, agent.n_envs, cfg.train.n_steps, cfg.train.batch_size)

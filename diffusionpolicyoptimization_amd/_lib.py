@@ -81,7 +81,8 @@ _SIGNATURES = {
     "dppo_adamw": (_I, [_P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P]),
     "dppo_pack_all": (_I, [_DIMS, _I, _P, _P, _P, _P, _P]),
     "dppo_optimizer_step": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P, _P,
-                                 _P, _I, _P]),
+                                 _P, _I, _U64, _P]),
+    "dppo_value_moments": (_I, [_P, _P, _I64, _P, _P]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -89,7 +90,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class DppoError(RuntimeError):

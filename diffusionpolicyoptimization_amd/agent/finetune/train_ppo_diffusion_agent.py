@@ -10,16 +10,18 @@ the PPO epochs. Differences from the reference are only where data lives and wha
     the metrics are summed with torch.distributed (RCCL) so all replicas take identical steps.
 Semantics kept on purpose: eval at itr % val_freq == 0 with env reset only
 then (4), population-std advantage normalisation per minibatch (3), one optimiser (2)."""
+import contextlib
 import logging
 import os
 import pickle
+import time
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
 from ... import ops
-from ...util.dist import allreduce_sum_, explained_variance
+from ...util.dist import allreduce_sum_, explained_variance_from_moments
 from ...util.timer import Timer
 from .train_ppo_agent import TrainPPOAgent
 
@@ -61,6 +63,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         self.timing = {"rollout_s": 0.0, "update_s": 0.0, "n_updates": 0, "env_steps": 0, "iters": 0}
         self.sampler_events = None    # optional list of (start, end) torch.cuda.Event pairs
         self.update_events = None
+        self.host_profile = None      # optional dict: host seconds per update-loop phase (tools)
+        self._passes_enqueued = False
         # test hook: called as minibatch_hook(epoch, batch, start, rows) after a minibatch's
         # gradients (all-reduced under data parallelism) are in self.model.grads
         self.minibatch_hook = None
@@ -91,6 +95,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             self.act_pin = torch.empty(E, d.xd, dtype=torch.float32).pin_memory()
         self.reward_pin = torch.empty(S, E, dtype=torch.float64).pin_memory()
         self.term_pin = torch.empty(S, E, dtype=torch.uint8).pin_memory()
+        self.first_pin = torch.empty(S, E, dtype=torch.uint8).pin_memory()
         self.firsts = np.zeros((S + 1, E))
         self.reward_dev = torch.empty(S, E, dtype=torch.float64, device=dev)
         self.first_dev = torch.empty(S, E, dtype=torch.uint8, device=dev)
@@ -102,12 +107,35 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         self.ret = torch.empty(S, E, dtype=torch.float32, device=dev)
         self.adv_stats = torch.zeros(3, dtype=torch.float64, device=dev)
 
+    def _enqueue_passes(self):
+        """The value and old-log-prob passes over the rollout (:191-229): one fused launch each,
+        no num_split needed."""
+        S, E, m = self.n_steps, self.n_envs, self.model
+        kf = m.ft_denoising_steps
+        N = S * E
+        ops.critic_forward(m.dims, m.precision, m.packed_critic, self.obs_traj.view(N, -1), values=self.values)
+        ops.logprob(m.dims, m.precision, m.packed_ft, m.sched, self.obs_traj.view(N, -1),
+                    self.chains_traj.view(N, kf + 1, -1), min_logprob_std=m.min_logprob_denoising_std,
+                    reward_horizon=self.reward_horizon, want_elem=False, lp_mean=self.lp_old)
+        self._passes_enqueued = True
+
+    def _update_stream(self):
+        if os.environ.get("DPPO_UPDATE_PRIO", "1") == "0":
+            return None
+        if getattr(self, "_hp_stream", None) is None:
+            _, greatest = torch.cuda.Stream.priority_range()
+            self._hp_stream = torch.cuda.Stream(device=self.device, priority=greatest)
+        return self._hp_stream
+
     def _allreduce(self, t):
         return allreduce_sum_(t)
 
     # ------------------------------------------------------------------ rollout (agent :58-141)
-    def rollout(self, eval_mode):
+    def rollout(self, eval_mode, defer_stats=False):
+        """One rollout of S chunks; returns the episode statistics, or None with defer_stats (the
+        train iteration computes them on the host while the update's first kernels run)."""
         S, E = self.n_steps, self.n_envs
+        self._ep_local = None
         # quirk 4: the reference assigns last_itr_eval = eval_mode right before it tests it (agent
         # :70-74), so its "right after eval mode" clause never fires: envs are reset only when
         # reset_at_iteration is set or on eval iterations, and the train iteration after an eval
@@ -138,8 +166,18 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # step t+1's launch is enqueued before the envs of step t are stepped; it waits on
             # the device for the observation the host publishes after the env step
             pipe = self.pipe
+            early = defer_stats      # a train iteration: its value / old-log-prob passes follow the rollout
+
+            def last_enqueued():
+                # right behind the last sampler launch, so the GPU runs the passes while the host
+                # does the last env step and the rollout's bookkeeping (they read only obs / chains)
+                pipe.end()
+                self._enqueue_passes()
+
             pipe.begin()
             pipe.enqueue(0, eval_mode)
+            if early and S == 1:
+                last_enqueued()
             pipe.publish()
             # wait + step + publish in C (the tagged stepper decodes the actions into act_view itself,
             # so it needs the whole [E, horizon, Da] buffer: act_steps == horizon_steps)
@@ -148,6 +186,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 more = step + 1 < S
                 if more:
                     pipe.enqueue(step + 1, eval_mode)
+                    if early and step + 2 == S:
+                        last_enqueued()
                 if gated:
                     _, reward, terminated, truncated, _ = self.venv.step(act_view, obs_out=obs_np,
                                                                          gate=pipe.gate(publish=more))
@@ -159,8 +199,10 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     if more:
                         pipe.publish()
                 bookkeeping(step, reward, terminated, truncated)
-            pipe.end()
-            stream.synchronize()
+            if not early:
+                pipe.end()
+                stream.synchronize()
+            # (a train iteration goes on enqueueing its update behind the passes: no host sync here)
         else:
             if self._stepper is None:
                 self._stepper = self.model.bind_rollout(self.obs_pin, self.obs_traj, self.act_dev, self.act_pin,
@@ -179,12 +221,17 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 _, reward, terminated, truncated, _ = self.venv.step(act_view, obs_out=obs_np)
                 bookkeeping(step, reward, terminated, truncated)
         self.prev_obs_venv = {"state": obs_np}
-        return self.episode_stats()
+        return None if defer_stats else self.episode_stats()
+
+    def _episode_sums_local(self):
+        if getattr(self, "_ep_local", None) is None:
+            self._ep_local = episode_sums(self.firsts, self.reward_pin.numpy(), self.act_steps,
+                                          self.best_reward_threshold_for_success)
+        return self._ep_local
 
     def episode_stats(self):
         """agent :144-183; sums over ranks so every rank logs the global statistics."""
-        sums = episode_sums(self.firsts, self.reward_pin.numpy(), self.act_steps,
-                            self.best_reward_threshold_for_success)
+        sums = list(self._episode_sums_local())
         if self.world_size > 1:
             t = torch.tensor(sums, dtype=torch.float64, device=self.device)
             self._allreduce(t)
@@ -198,14 +245,14 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         N = S * E
         obs_flat = self.obs_traj.view(N, -1)
         chains_flat = self.chains_traj.view(N, kf + 1, -1)
-        # values and old log-probs (:191-229) — one fused pass each, no num_split needed
-        ops.critic_forward(m.dims, m.precision, m.packed_critic, obs_flat, values=self.values)
-        ops.logprob(m.dims, m.precision, m.packed_ft, m.sched, obs_flat, chains_flat,
-                    min_logprob_std=m.min_logprob_denoising_std, reward_horizon=self.reward_horizon,
-                    want_elem=False, lp_mean=self.lp_old)
+        if not self._passes_enqueued:
+            self._enqueue_passes()
+        self._passes_enqueued = False
         self.reward_dev.copy_(self.reward_pin, non_blocking=True)
         self.term_dev.copy_(self.term_pin, non_blocking=True)
-        self.first_dev.copy_(torch.from_numpy(self.firsts[:-1].astype(np.uint8)), non_blocking=True)
+        # through pinned memory: a pageable source would block the host until the stream reaches it
+        np.copyto(self.first_pin.numpy(), self.firsts[:-1], casting="unsafe")
+        self.first_dev.copy_(self.first_pin, non_blocking=True)
         if self.reward_scale_running:                                                  # :232-236
             self.running_reward_scaler.scale_(self.reward_dev, self.first_dev,
                                               group=dist.group.WORLD if self.world_size > 1 else None)
@@ -214,6 +261,11 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         ops.gae(self.reward_dev, self.values.view(S, E), self.last_values, self.term_dev, self.gamma, self.gae_lambda,
                 self.reward_scale_const, adv=self.adv, ret=self.ret)                       # :239-263
         adv_flat, ret_flat = self.adv.view(-1), self.ret.view(-1)
+        # explained-variance moments of the pre-update values and returns (:373-377), read after the
+        # epochs from host-mapped memory (no torch reductions or host syncs at the end of the update)
+        if getattr(self, "_ev_map", None) is None:
+            self._ev_map = ops.MappedDoubles(5)
+        ops.value_moments(self.values, ret_flat, self._ev_map.address)
 
         total_local = N * kf
         total_global = total_local * self.world_size
@@ -227,138 +279,192 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         num_batch = max(1, total_global // eff_batch)                                     # :288
         rows_local_full = eff_batch // self.world_size
         clipfracs, info = [], {}
-        stream = torch.cuda.current_stream(self.device)
-        # The target_kl check (:366-370) reads each minibatch's approx_kl on the host. It runs one
-        # minibatch behind: minibatch i's gradients are enqueued before the host waits for i-1's
-        # metrics (an event right after i-1's kernels, the metrics copied to pinned memory), so the
-        # GPU never idles on that read. Only the AdamW step of i waits for the verdict. In the
-        # reference the minibatch that exceeds target_kl IS applied and its `break` leaves only the
-        # batch loop of that epoch (`if flag_break: break` sits inside the batch loop and is never
-        # reached; flag_break is reset per epoch, :284-286,366-370), so the next epoch still runs.
-        # Here: a stop by minibatch i-1 of the SAME epoch drops i's gradients (the reference never
-        # computes them) and ends the epoch; a stop by the previous epoch's last minibatch ended an
-        # epoch that was over anyway, so i (the new epoch's first) is applied.
-        # Each minibatch's metric sums land in mapped host memory, copied by its optimiser-step
-        # launch (dppo_optimizer_step) or, before the critic warm-up ends, by a plain copy; one event
-        # per slot marks them readable.
-        if not hasattr(self, "_met_map"):
-            self._met_map = [ops.MappedDoubles(8) for _ in range(2)]
-            self._ev_m = [torch.cuda.Event() for _ in range(2)]
-        pending = None
+        caller = torch.cuda.current_stream(self.device)
+        # the epochs run on a high-priority stream (DPPO_UPDATE_PRIO, default on): the actor half of
+        # a minibatch is the critical path, and the dispatcher then hands freed CUs to its workgroups
+        # before the critic half's (side stream, default priority), which has slack
+        hp = self._update_stream()
+        if hp is not None:
+            hp.wait_stream(caller)
+        with (torch.cuda.stream(hp) if hp is not None else contextlib.nullcontext()):
+            stream = torch.cuda.current_stream(self.device)
+            # The target_kl check (:366-370) reads each minibatch's approx_kl on the host. It runs one
+            # minibatch behind: minibatch i's gradients are enqueued before the host waits for i-1's
+            # metrics (an event right after i-1's kernels, the metrics copied to pinned memory), so the
+            # GPU never idles on that read. Only the AdamW step of i waits for the verdict. In the
+            # reference the minibatch that exceeds target_kl IS applied and its `break` leaves only the
+            # batch loop of that epoch (`if flag_break: break` sits inside the batch loop and is never
+            # reached; flag_break is reset per epoch, :284-286,366-370), so the next epoch still runs.
+            # Here: a stop by minibatch i-1 of the SAME epoch drops i's gradients (the reference never
+            # computes them) and ends the epoch; a stop by the previous epoch's last minibatch ended an
+            # epoch that was over anyway, so i (the new epoch's first) is applied.
+            # Each minibatch's metric sums land in mapped host memory, copied by its optimiser-step
+            # launch (dppo_optimizer_step) or, before the critic warm-up ends, by a plain copy; one event
+            # per slot marks them readable.
+            # With the optimiser step applied (after the critic warm-up) the launch stores a tag after the
+            # sums and the host polls it (ABI 5): no event record or cross-stream wait on the minibatch
+            # chain. In the split update the critic's step copies its own v_loss (metric 1) with the
+            # same tag, so the main stream never waits for the side stream inside the epochs.
+            if not hasattr(self, "_met_map"):
+                self._met_map = [ops.MappedDoubles(8) for _ in range(2)]
+                self._cmet_map = [ops.MappedDoubles(8) for _ in range(2)]
+                self._ev_m = [torch.cuda.Event() for _ in range(2)]
+                self._mb_tag = 0
+            pending = None
 
-        def finish(p):
-            slot, ev, grows, _ = p
-            ev.synchronize()
-            met = self._met_map[slot].array[:5] / grows
-            self.timing["n_updates"] += 1
-            inf = dict(pg_loss=float(met[0]), v_loss=float(met[1]), approx_kl=float(met[2]),
-                       clipfrac=float(met[3]), ratio=float(met[4]), bc_loss=0.0, eta=1.0,
-                       entropy_loss=-1.0, loss=float(met[0] + self.vf_coef * met[1]))
-            clipfracs.append(inf["clipfrac"])
-            return inf, self.target_kl is not None and inf["approx_kl"] > self.target_kl
-
-        # every minibatch's advantage moments (norm_adv, diffusion_ppo.py:74-75) in one launch, and
-        # on several GPUs one all-reduce of the whole table instead of one per minibatch
-        n_mb = self.update_epochs * num_batch
-        if getattr(self, "_adv_all", None) is None or self._adv_all.shape[0] != n_mb:
-            self._adv_all = torch.zeros(n_mb, 3, dtype=torch.float64, device=self.device)
-        ops.ppo_adv_stats_all(adv_flat, total_local, kf, self.perm_seed, 1000 * self.itr, self.update_epochs,
-                              rows_local_full, num_batch, self._adv_all)
-        if self.world_size > 1:
-            self._allreduce(self._adv_all)
-        # Split update (single GPU): the critic's half of each minibatch (row tiles, dW, its AdamW
-        # range, repack) runs on a side stream and the actor's on the main stream, so the critic of
-        # minibatch i+1 fills the CUs the actor leaves idle in its dW / small-kernel tail of i.
-        # Metrics alternate between two device buffers; the main stream joins the critic's half
-        # before copying a minibatch's metrics.
-        split = (self.world_size == 1 and self.max_grad_norm is None
-                 and os.environ.get("DPPO_SPLIT_UPDATE", "1") != "0")
-        if split:
-            if getattr(self, "_side", None) is None:
-                self._side = torch.cuda.Stream(device=self.device)
-                self._met_dev = [torch.zeros(16, dtype=torch.float64, device=self.device) for _ in range(2)]
-            side = self._side
-            side.wait_stream(stream)
-            na = m.n_actor
-        k = 0
-        for update_epoch in range(self.update_epochs):
-            for batch in range(num_batch):
-                start = batch * rows_local_full
-                rows = min(rows_local_full, total_local - start)
-                if rows <= 0:
-                    break
-                global_rows = rows * self.world_size
-                stats = self._adv_all[update_epoch * num_batch + batch]
-                if self.update_events is not None:
-                    ev0 = torch.cuda.Event(enable_timing=True)
-                    ev0.record(stream)
-                mb_args = (obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, self.perm_seed,
-                           update_epoch + 1000 * self.itr, start, rows)
-                mb_kw = dict(global_rows=global_rows, reward_horizon=self.reward_horizon, adv_stats=stats)
-                met = m.metrics
-                if split:
-                    met = self._met_dev[k % 2]
-                    with torch.cuda.stream(side):
-                        m.minibatch(*mb_args, **mb_kw, part=2, metrics=met)
-                        ev_c = torch.cuda.Event()
-                        ev_c.record(side)
-                    m.minibatch(*mb_args, **mb_kw, part=1, metrics=met)
-                    stream.wait_event(ev_c)
+            def finish(p):
+                slot, ev, grows, _, tag, ctag = p
+                if tag:
+                    self._met_map[slot].wait_tag(5, tag)
+                    met = self._met_map[slot].array[:5].copy()
+                    if ctag:
+                        self._cmet_map[slot].wait_tag(1, ctag)
+                        met[1] = self._cmet_map[slot].array[0]
+                    met /= grows
                 else:
-                    m.minibatch(*mb_args, **mb_kw)
-                if self.world_size > 1:                # one collective: gradients + metric sums
-                    ng = m.grads.numel()
-                    m.grads_ext[ng:ng + 5].copy_(m.metrics[:5])
-                    self._allreduce(m.grads_ext)
-                    m.metrics[:5].copy_(m.grads_ext[ng:ng + 5])
-                if self.minibatch_hook is not None:
-                    if split:
-                        stream.wait_stream(side)
-                    self.minibatch_hook(update_epoch, batch, start, rows)
-                slot = k % 2
-                if pending is not None:
-                    info, stop = finish(pending)
-                    same_epoch = pending[3] == update_epoch
-                    pending = None
-                    if stop and same_epoch:                                    # :366-368
+                    ev.synchronize()
+                    met = self._met_map[slot].array[:5] / grows
+                self.timing["n_updates"] += 1
+                inf = dict(pg_loss=float(met[0]), v_loss=float(met[1]), approx_kl=float(met[2]),
+                           clipfrac=float(met[3]), ratio=float(met[4]), bc_loss=0.0, eta=1.0,
+                           entropy_loss=-1.0, loss=float(met[0] + self.vf_coef * met[1]))
+                clipfracs.append(inf["clipfrac"])
+                return inf, self.target_kl is not None and inf["approx_kl"] > self.target_kl
+
+            # every minibatch's advantage moments (norm_adv, diffusion_ppo.py:74-75) in one launch, and
+            # on several GPUs one all-reduce of the whole table instead of one per minibatch
+            n_mb = self.update_epochs * num_batch
+            if getattr(self, "_adv_all", None) is None or self._adv_all.shape[0] != n_mb:
+                self._adv_all = torch.zeros(n_mb, 3, dtype=torch.float64, device=self.device)
+            ops.ppo_adv_stats_all(adv_flat, total_local, kf, self.perm_seed, 1000 * self.itr, self.update_epochs,
+                                  rows_local_full, num_batch, self._adv_all)
+            if self.world_size > 1:
+                self._allreduce(self._adv_all)
+            # Split update (single GPU): the critic's half of each minibatch (row tiles, dW, its AdamW
+            # range, repack) runs on a side stream and the actor's on the main stream, so the critic of
+            # minibatch i+1 fills the CUs the actor leaves idle in its dW / small-kernel tail of i.
+            # Metrics alternate between two device buffers; the main stream joins the critic's half
+            # before copying a minibatch's metrics.
+            split = (self.world_size == 1 and self.max_grad_norm is None
+                     and os.environ.get("DPPO_SPLIT_UPDATE", "1") != "0")
+            if split:
+                if getattr(self, "_side", None) is None:
+                    self._side = torch.cuda.Stream(device=self.device)
+                    self._met_dev = [torch.zeros(16, dtype=torch.float64, device=self.device) for _ in range(2)]
+                side = self._side
+                side.wait_stream(stream)
+                na = m.n_actor
+            k = 0
+            for update_epoch in range(self.update_epochs):
+                for batch in range(num_batch):
+                    start = batch * rows_local_full
+                    rows = min(rows_local_full, total_local - start)
+                    if rows <= 0:
                         break
-                # the optimiser step (agent :346): AdamW, the metric sums to the host and the weight
-                # images re-derived, one dppo_optimizer_step per stream (two launches each)
-                ng = m.grads.numel()
-                met_out = self._met_map[slot]
-                if self.itr >= self.n_critic_warmup_itr:
-                    opt = self.actor_optimizer
-                    lr = opt.begin_step()
+                    global_rows = rows * self.world_size
+                    stats = self._adv_all[update_epoch * num_batch + batch]
+                    hp_ = self.host_profile
+                    if hp_ is not None:
+                        t_h0 = time.perf_counter()
+                    if self.update_events is not None:
+                        ev0 = torch.cuda.Event(enable_timing=True)
+                        ev0.record(stream)
+                    mb_args = (obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, self.perm_seed,
+                               update_epoch + 1000 * self.itr, start, rows)
+                    mb_kw = dict(global_rows=global_rows, reward_horizon=self.reward_horizon, adv_stats=stats)
+                    met = m.metrics
+                    tagged = self.itr >= self.n_critic_warmup_itr
                     if split:
-                        opt.apply_range(m.grads, 0, na, lr, m.dims, m.precision,
-                                        packs={"actor": (m.actor_ft_params, m.packed_ft)},
-                                        metrics=met, metrics_out=met_out.address, n_metrics=5)
+                        met = self._met_dev[k % 2]
                         with torch.cuda.stream(side):
-                            opt.apply_range(m.grads, na, ng, lr, m.dims, m.precision,
-                                            packs={"critic": (m.critic_params, m.packed_critic)})
+                            m.minibatch(*mb_args, **mb_kw, part=2, metrics=met)
+                            if not tagged:
+                                ev_c = torch.cuda.Event()
+                                ev_c.record(side)
+                        m.minibatch(*mb_args, **mb_kw, part=1, metrics=met)
+                        if not tagged:
+                            stream.wait_event(ev_c)
                     else:
-                        if self.max_grad_norm is not None:
-                            self._clip_by_norm_per_tensor()
-                        opt.apply_range(m.grads, 0, ng, lr, m.dims, m.precision,
-                                        packs={"actor": (m.actor_ft_params, m.packed_ft),
-                                               "critic": (m.critic_params, m.packed_critic)},
-                                        metrics=met, metrics_out=met_out.address, n_metrics=5)
-                else:
-                    torch.from_numpy(met_out.array[:5]).copy_(met[:5])
-                if self.update_events is not None:
-                    ev1 = torch.cuda.Event(enable_timing=True)
-                    ev1.record(stream)
-                    self.update_events.append((ev0, ev1))
-                ev_m = self._ev_m[slot]
-                ev_m.record(stream)
-                pending = (slot, ev_m, global_rows, update_epoch)
-                k += 1
-        if pending is not None:
-            info, _ = finish(pending)
-        if split:
-            stream.wait_stream(side)
-        # explained variance (:373-377)
-        info["explained_var"] = explained_variance(self.values, ret_flat)
+                        m.minibatch(*mb_args, **mb_kw)
+                    if self.world_size > 1:                # one collective: gradients + metric sums
+                        ng = m.grads.numel()
+                        m.grads_ext[ng:ng + 5].copy_(m.metrics[:5])
+                        self._allreduce(m.grads_ext)
+                        m.metrics[:5].copy_(m.grads_ext[ng:ng + 5])
+                    if self.minibatch_hook is not None:
+                        if split:
+                            stream.wait_stream(side)
+                        self.minibatch_hook(update_epoch, batch, start, rows)
+                    if hp_ is not None:
+                        t_h1 = time.perf_counter()
+                    slot = k % 2
+                    if k == 1:
+                        self._episode_sums_local()   # host work while the GPU runs the first minibatches
+                    if pending is not None:
+                        info, stop = finish(pending)
+                        same_epoch = pending[3] == update_epoch
+                        pending = None
+                        if stop and same_epoch:                                    # :366-368
+                            break
+                    # the optimiser step (agent :346): AdamW, the metric sums to the host and the weight
+                    # images re-derived, one dppo_optimizer_step per stream (two launches each)
+                    if hp_ is not None:
+                        t_h2 = time.perf_counter()
+                    ng = m.grads.numel()
+                    met_out = self._met_map[slot]
+                    tag = ctag = 0
+                    if tagged:
+                        opt = self.actor_optimizer
+                        lr = opt.begin_step()
+                        self._mb_tag += 1
+                        tag = self._mb_tag
+                        if split:
+                            ctag = tag
+                            opt.apply_range(m.grads, 0, na, lr, m.dims, m.precision,
+                                            packs={"actor": (m.actor_ft_params, m.packed_ft)},
+                                            metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag)
+                            with torch.cuda.stream(side):
+                                opt.apply_range(m.grads, na, ng, lr, m.dims, m.precision,
+                                                packs={"critic": (m.critic_params, m.packed_critic)},
+                                                metrics=met[1:2], metrics_out=self._cmet_map[slot].address,
+                                                n_metrics=1, metrics_tag=ctag)
+                        else:
+                            if self.max_grad_norm is not None:
+                                self._clip_by_norm_per_tensor()
+                            opt.apply_range(m.grads, 0, ng, lr, m.dims, m.precision,
+                                            packs={"actor": (m.actor_ft_params, m.packed_ft),
+                                                   "critic": (m.critic_params, m.packed_critic)},
+                                            metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag)
+                    else:
+                        torch.from_numpy(met_out.array[:5]).copy_(met[:5])
+                    if self.update_events is not None:
+                        ev1 = torch.cuda.Event(enable_timing=True)
+                        ev1.record(stream)
+                        self.update_events.append((ev0, ev1))
+                    ev_m = None
+                    if not tag:
+                        ev_m = self._ev_m[slot]
+                        ev_m.record(stream)
+                    pending = (slot, ev_m, global_rows, update_epoch, tag, ctag)
+                    k += 1
+                    if hp_ is not None:   # host seconds: enqueue grads, wait for the previous metrics, enqueue step
+                        t_h3 = time.perf_counter()
+                        for key, dt in (("enqueue_grads", t_h1 - t_h0), ("wait_metrics", t_h2 - t_h1),
+                                        ("enqueue_step", t_h3 - t_h2)):
+                            hp_[key] = hp_.get(key, 0.0) + dt
+                        hp_["minibatches"] = hp_.get("minibatches", 0) + 1
+            self._episode_sums_local()
+            if pending is not None:
+                info, _ = finish(pending)
+            if split:
+                stream.wait_stream(side)
+        if hp is not None:
+            caller.wait_stream(hp)
+        stream = caller
+        # explained variance (:373-377) from the moments value_moments stored before the epochs
+        stream.synchronize()
+        info["explained_var"] = explained_variance_from_moments(
+            self._ev_map.array.copy(), self.device, group=dist.group.WORLD if self.world_size > 1 else None)
         info["clipfrac"] = float(np.mean(clipfracs)) if clipfracs else 0.0
         return info
 
@@ -381,13 +487,15 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         eval_mode = self.itr % self.val_freq == 0 and not ft
         torch.cuda.synchronize(self.device)
         t0 = Timer()
-        stats = self.rollout(eval_mode)
-        torch.cuda.synchronize(self.device)
-        t_roll = t0()
+        stats = self.rollout(eval_mode, defer_stats=not eval_mode)
+        if eval_mode:
+            torch.cuda.synchronize(self.device)
+        t_roll = t0()   # train iterations: host time to the last env step (the passes run behind it)
         info = {}
         if not eval_mode:
             info = self.update()
             torch.cuda.synchronize(self.device)
+            stats = self.episode_stats()
         t_upd = t0()
         self.timing["rollout_s"] += t_roll
         self.timing["update_s"] += t_upd

@@ -166,6 +166,42 @@ extern "C" int dppo_gae(const double* reward, const float* values, const float* 
     return DPPO_OK;
 }
 
+// explained-variance moments {sum y, sum y^2, sum d, sum d^2, n} of y = returns, d = y - values
+// (agent :373-377), fp64, one workgroup in a fixed summation order (deterministic); out may be
+// host-mapped memory (stored through its device address)
+#define VM_THREADS 1024
+__global__ __launch_bounds__(VM_THREADS) void value_moments_kernel(const float* __restrict__ val, const float* __restrict__ ret,
+                                                                   int64_t n, double* __restrict__ out) {
+    __shared__ double sh[4][VM_THREADS / 64];
+    double a = 0.0, b = 0.0, c = 0.0, e = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += VM_THREADS) {
+        const double y = ret[i], d = y - (double)val[i];
+        a += y; b += y * y; c += d; e += d * d;
+    }
+    a = wave_sumd(a); b = wave_sumd(b); c = wave_sumd(c); e = wave_sumd(e);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[0][w] = a; sh[1][w] = b; sh[2][w] = c; sh[3][w] = e; }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        double t = 0.0;
+        for (int k = 0; k < VM_THREADS / 64; ++k) t += sh[threadIdx.x][k];
+        out[threadIdx.x] = t;
+    } else if (threadIdx.x == 4) {
+        out[4] = (double)n;
+    }
+}
+
+extern "C" int dppo_value_moments(const float* values, const float* returns, int64_t n, double* moments, void* stream) {
+    DPPO_CHECK(n >= 0 && values && returns && moments, "dppo_value_moments: bad args");
+    double* out = moments;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, moments, 0) == hipSuccess && dp) out = (double*)dp;
+    else (void)hipGetLastError();
+    hipLaunchKernelGGL(value_moments_kernel, dim3(1), dim3(VM_THREADS), 0, (hipStream_t)stream, values, returns, n, out);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
 extern "C" int dppo_reward_scale_moments(const double* reward, const uint8_t* first, double* ret_state, double* workspace,
                                          double* moments, int S, int E, double gamma, void* stream) {
     DPPO_CHECK(S > 0 && E > 0, "dppo_reward_scale_moments: empty");

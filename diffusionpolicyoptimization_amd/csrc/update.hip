@@ -24,8 +24,18 @@
 enum { EXTRA_NONE = 0, EXTRA_ONES = 1, EXTRA_ONEHOT = 2 };
 #define DW_MAXP 8
 #define DW_TN 128            // output tile edge along N (the gradient operand's features)
-#define DW_LINE 128          // bytes per feature per stage
-#define DW_BOPB (DW_TN * DW_LINE)   // 16 KiB: the B (gradient) operand's stage image
+// bytes per feature per stage: 128 (two MFMA k-steps, 64 bf16 rows; the default) or 64 (one k-step).
+// 64-B stages halve the slot, so the same LDS holds twice the ring (6 slots of 25 KiB at WK = 256:
+// 5 stages, 120 KiB, in flight, against 3 of 49 KiB: 2 stages, 96 KiB), but pay a barrier per 32
+// rows: measured slower (fused minibatch 0.535 vs 0.515 ms, tools/ab_lib.sh), so 128 stays.
+#ifndef DPPO_DW_LINE
+#define DPPO_DW_LINE 128
+#endif
+#define DW_LINE DPPO_DW_LINE
+#define DW_CPL (DW_LINE / 16)       // 16-B chunks per feature line
+#define DW_FPI (64 / DW_CPL)        // features per 1 KiB wave-instruction
+#define DW_BOPB (DW_TN * DW_LINE)   // the B (gradient) operand's stage image
+static_assert(DW_LINE == 64 || DW_LINE == 128, "DPPO_DW_LINE must be 64 or 128");
 
 // Output tile = DW_TK(WK) x 128: WK = 128 (4 waves, 2x2 of 64x64; ring of 4 slots, 3 stages in
 // flight) or WK = 256 (8 waves, 4x2 of 64x64; ring of 3 slots, 2 stages in flight). The kernel is
@@ -36,9 +46,9 @@ template <int WK> struct DWGeom {
     static constexpr int W = WK / 32;                    // waves: 4 or 8
     static constexpr int AOPB = WK * DW_LINE;            // A (activation) operand's stage image
     static constexpr int SLOT = AOPB + DW_BOPB + 1024;   // A | B | the stage's seg bytes (padded)
-    static constexpr int RING = WK == 256 ? 3 : 4;       // ring slots (stages in flight: RING - 1)
-    static constexpr int AI = WK / 8 / W;                // A wave-instructions per wave per stage (4)
-    static constexpr int BI = DW_TN / 8 / W;             // B wave-instructions per wave per stage (4 / 2)
+    static constexpr int RING = 160 * 1024 / SLOT < 8 ? 160 * 1024 / SLOT : 8;   // ring slots (RING - 1 in flight)
+    static constexpr int AI = WK / DW_FPI / W;           // A wave-instructions per wave per stage
+    static constexpr int BI = DW_TN / DW_FPI / W;        // B wave-instructions per wave per stage
     static_assert(RING * SLOT <= 160 * 1024, "dW ring exceeds the CU's LDS");
 };
 
@@ -75,9 +85,18 @@ __device__ inline u32x4 extra_frag(int extra, int q, const int8_t* seg_lds) {
     return __builtin_bit_cast(u32x4, e);
 }
 
-// fragment of a staged operand: feature f (within the tile), 16-B chunk c (0..7)
+// 16-B slot of chunk c of feature f in a staged line: a bank swizzle that makes the fragment reads
+// (ds_read_b128: 16 features x 4 chunks per wave-instruction, serviced in 4 lane groups of 16)
+// conflict-free. 128-B lines: c ^ (f & 7). 64-B lines (4 slots, 4 features per 256-B bank row):
+// c ^ H[(f >> 2) & 3] with H = {0, 2, 3, 1} gives the 16 lanes of every ds_read_b128 lane group
+// ({0-3,12-15,20-27}, ...: MI355X_MICROARCH.md LDS table) 16 distinct banks.
+__device__ inline int dw_swz(int f, int c) {
+    if constexpr (DW_LINE == 128) return c ^ (f & 7);
+    else return c ^ ((0x78 >> (2 * ((f >> 2) & 3))) & 3);   // H packed 2 bits each: 0b01_11_10_00
+}
+// fragment of a staged operand: feature f (within the tile), 16-B chunk c
 __device__ inline u32x4 dw_lds_frag(const uint8_t* img, int f, int c) {
-    return *reinterpret_cast<const u32x4*>(img + f * DW_LINE + ((c ^ (f & 7)) << 4));
+    return *reinterpret_cast<const u32x4*>(img + f * DW_LINE + (dw_swz(f, c) << 4));
 }
 
 // wait until at most N of this wave's vector-memory operations are outstanding
@@ -135,7 +154,7 @@ __device__ __forceinline__ void dw_loop(uint8_t* smem, const DWArgs& a, const DW
         const uint8_t* imB = imA + G::AOPB;
         const int8_t* seg_lds = (const int8_t*)(imB + DW_BOPB);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < DW_LINE / 64; ++ks) {
             u32x4 A[4], B[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -169,7 +188,7 @@ template <class P, int WK>
 __global__ __launch_bounds__(DWGeom<WK>::W * 64) void dw_kernel(DWArgs a) {
     using AT = typename P::AT;
     using G = DWGeom<WK>;
-    constexpr int BK = DW_LINE / (int)sizeof(AT);     // rows per stage: 64 bf16 / 32 fp32
+    constexpr int BK = DW_LINE / (int)sizeof(AT);     // rows per stage: 32 bf16 / 16 fp32 (64-B lines)
     constexpr int EPC = 16 / (int)sizeof(AT);         // elements per 16-B chunk
     // one LDS object (a second __shared__ array can make hipcc drain the glds queue at every
     // fragment read): the ring of [A | B | seg] stage slots
@@ -207,15 +226,15 @@ __global__ __launch_bounds__(DWGeom<WK>::W * 64) void dw_kernel(DWArgs a) {
     const AT* srcB[G::BI];
 #pragma unroll
     for (int i = 0; i < G::AI; ++i) {
-        const int f = (wave + G::W * i) * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ (f & 7);
+        const int f = (wave + G::W * i) * DW_FPI + lane / DW_CPL;
+        const int c = dw_swz(f, lane % DW_CPL);
         int fa = k_base + f; fa = fa < pr.Kx ? fa : pr.Kx - 1;
         srcA[i] = XT + (size_t)fa * a.ldm + m_begin + c * EPC;
     }
 #pragma unroll
     for (int i = 0; i < G::BI; ++i) {
-        const int f = (wave + G::W * i) * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ (f & 7);
+        const int f = (wave + G::W * i) * DW_FPI + lane / DW_CPL;
+        const int c = dw_swz(f, lane % DW_CPL);
         int fb = n_base + f; fb = fb < pr.N ? fb : pr.N - 1;
         srcB[i] = DT + (size_t)fb * a.ldm + m_begin + c * EPC;
     }
@@ -441,10 +460,23 @@ __global__ void feistel_kernel(int64_t first, int64_t count, FeistelKey fk, int6
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, int64_t n, float lr, float wd, float b1, float b2,
                                                     float eps, float alpha, float bc1, float bc2, int mode,
-                                                    const double* __restrict__ met, double* __restrict__ met_out, int nmet) {
+                                                    const double* __restrict__ met, double* __restrict__ met_out, int nmet,
+                                                    uint64_t tag) {
     // the minibatch's metric sums ride along (dppo_optimizer_step): one launch fewer on the
-    // minibatch's critical path than a separate copy
-    if (blockIdx.x == 0 && (int)threadIdx.x < nmet) met_out[threadIdx.x] = met[threadIdx.x];
+    // minibatch's critical path than a separate copy. With a tag, met_out[nmet] receives it after
+    // the sums (system-scope release), so the host polls host-mapped memory instead of recording
+    // and waiting on an event (a marker packet on the minibatch chain).
+    if (blockIdx.x == 0) {
+        if ((int)threadIdx.x < nmet) met_out[threadIdx.x] = met[threadIdx.x];
+        if (tag) {
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(met_out + nmet), __builtin_bit_cast(uint64_t, (double)tag),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         float pi = p[i], gi = g[i], mi = m[i], vi = v[i];
         if (mode == DPPO_ADAMW_KERAS) {
@@ -466,11 +498,12 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 
 static int launch_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
                         float weight_decay, float beta1, float beta2, float eps, int mode, const double* met,
-                        double* met_out, int nmet, hipStream_t s) {
+                        double* met_out, int nmet, uint64_t tag, hipStream_t s) {
     DPPO_CHECK(n >= 0 && step >= 1, "dppo_adamw: n < 0 or step < 1");
     DPPO_CHECK(mode == DPPO_ADAMW_KERAS || mode == DPPO_ADAMW_TORCH, "dppo_adamw: bad mode");
     DPPO_CHECK(nmet >= 0 && nmet <= 256 && (nmet == 0 || (met && met_out)), "dppo_optimizer_step: bad metrics copy");
-    if (n == 0 && nmet == 0) return DPPO_OK;
+    DPPO_CHECK(tag == 0 || (met_out && tag < ((uint64_t)1 << 53)), "dppo_optimizer_step: a tag needs metrics_out and < 2^53");
+    if (n == 0 && nmet == 0 && tag == 0) return DPPO_OK;
     DPPO_CHECK(n == 0 || (params && grads && m && v), "dppo_adamw: null pointer");
     const double bc1 = 1.0 - pow((double)beta1, (double)step);
     const double bc2 = 1.0 - pow((double)beta2, (double)step);
@@ -478,14 +511,14 @@ static int launch_adamw(float* params, const float* grads, float* m, float* v, i
     const int64_t blocks64 = (n + 255) / 256;
     const unsigned blocks = (unsigned)(blocks64 < 1 ? 1 : (blocks64 < 4096 ? blocks64 : 4096));
     hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, params, grads, m, v, n, lr,
-                       weight_decay, beta1, beta2, eps, alpha, (float)bc1, (float)bc2, mode, met, met_out, nmet);
+                       weight_decay, beta1, beta2, eps, alpha, (float)bc1, (float)bc2, mode, met, met_out, nmet, tag);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
 
 extern "C" int dppo_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
                           float weight_decay, float beta1, float beta2, float eps, int mode, void* stream) {
-    return launch_adamw(params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode, nullptr, nullptr, 0,
+    return launch_adamw(params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode, nullptr, nullptr, 0, 0,
                         (hipStream_t)stream);
 }
 
@@ -493,7 +526,7 @@ extern "C" int dppo_optimizer_step(const dppo_dims* d, int precision, float* par
                                    float* v, int64_t n, int64_t step, float lr, float weight_decay, float beta1,
                                    float beta2, float eps, int mode, const float* actor_params, void* packed_actor,
                                    const float* critic_params, void* packed_critic, const double* metrics,
-                                   double* metrics_out, int n_metrics, void* stream) {
+                                   double* metrics_out, int n_metrics, uint64_t metrics_tag, void* stream) {
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
@@ -510,7 +543,7 @@ extern "C" int dppo_optimizer_step(const dppo_dims* d, int precision, float* par
         else (void)hipGetLastError();
     }
     rc = launch_adamw(params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode, metrics, mout,
-                      n_metrics, s);
+                      n_metrics, metrics_tag, s);
     if (rc) return rc;
     return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s);
 }

@@ -8,6 +8,7 @@ import ctypes
 import functools
 import os
 import math
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -144,10 +145,11 @@ def pack_all(d: ModelDims, precision, actor_params=None, packed_actor=None, crit
 
 def optimizer_step(d: ModelDims, precision, params, grads, m, v, step, lr, weight_decay, beta1, beta2, eps, mode,
                    actor_params=None, packed_actor=None, critic_params=None, packed_critic=None, metrics=None,
-                   metrics_out=None, n_metrics=0):
+                   metrics_out=None, n_metrics=0, metrics_tag=0):
     """AdamW over params/grads/m/v (equal-length flat ranges), the metric sums copied to
     metrics_out (a device tensor or a dppo_host_alloc address), then the given images re-derived:
-    two launches on the current stream (dppo_optimizer_step)."""
+    two launches on the current stream (dppo_optimizer_step). A nonzero metrics_tag is stored as
+    metrics_out[n_metrics] after the sums (the host polls it instead of an event)."""
     n = params.numel()
     for t, nm in ((grads, "grads"), (m, "m"), (v, "v")):
         if t.numel() != n:
@@ -158,7 +160,17 @@ def optimizer_step(d: ModelDims, precision, params, grads, m, v, step, lr, weigh
               int(step), float(lr), float(weight_decay), float(beta1), float(beta2), float(eps),
               _lib.DPPO_ADAMW_KERAS if mode == "keras" else _lib.DPPO_ADAMW_TORCH, ptr(actor_params), ptr(packed_actor),
               ptr(critic_params), ptr(packed_critic), ptr(metrics), ctypes.c_void_p(mo) if mo else None,
-              int(n_metrics), stream_handle(params.device))
+              int(n_metrics), ctypes.c_uint64(int(metrics_tag)), stream_handle(params.device))
+
+
+def value_moments(values, returns, out_address):
+    """{sum y, sum y^2, sum d, sum d^2, n} of y = returns, d = returns - values (fp64) into 5 doubles
+    at out_address (host-mapped, dppo_host_alloc) or a device tensor (dppo_value_moments)."""
+    n = values.numel()
+    if returns.numel() != n:
+        raise ValueError("values / returns: length mismatch")
+    out = out_address if isinstance(out_address, int) else out_address.data_ptr()
+    _lib.call("dppo_value_moments", ptr(values), ptr(returns), int(n), ctypes.c_void_p(out), stream_handle(values.device))
 
 
 class MappedDoubles:
@@ -170,6 +182,17 @@ class MappedDoubles:
         _lib.call("dppo_host_alloc", ctypes.c_size_t(8 * n), ctypes.byref(p))
         self.address = p.value
         self.array = np.ctypeslib.as_array((ctypes.c_double * n).from_address(self.address))
+        self.array[:] = 0.0
+
+    def wait_tag(self, index, tag, timeout_s=30.0):
+        """Spin until array[index] == tag (a tag the device stores after the data it guards)."""
+        a = self.array
+        if a[index] == tag:
+            return
+        t_end = time.perf_counter() + timeout_s
+        while a[index] != tag:
+            if time.perf_counter() > t_end:
+                raise _lib.DppoError(f"mapped tag {tag} not seen within {timeout_s} s (found {a[index]})")
 
     def __del__(self):
         if getattr(self, "address", None) and _lib._lib is not None:

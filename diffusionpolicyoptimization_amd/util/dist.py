@@ -109,3 +109,17 @@ def explained_variance(y_pred, y_true, group=None):
     var_y = float(mom[1] / n - (mom[0] / n) ** 2)
     var_d = float(mom[3] / n - (mom[2] / n) ** 2)
     return float("nan") if var_y == 0 else 1.0 - var_d / var_y
+
+
+def explained_variance_from_moments(mom, device, group=None):
+    """explained_variance from the per-rank moments {sum y, sum y^2, sum d, sum d^2, n} (fp64, as
+    dppo_value_moments stores them), summed over ranks when a group is given."""
+    import numpy as np
+    mom = np.asarray(mom, dtype=np.float64)
+    if group is not None:
+        t = allreduce_sum_(torch.tensor(mom, dtype=torch.float64, device=device), group)
+        mom = t.cpu().numpy()
+    n = mom[4]
+    var_y = float(mom[1] / n - (mom[0] / n) ** 2)
+    var_d = float(mom[3] / n - (mom[2] / n) ** 2)
+    return float("nan") if var_y == 0 else 1.0 - var_d / var_y

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 4
+#define DPPO_ABI_VERSION 5
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -196,6 +196,12 @@ DPPO_API int dppo_gae(const double* reward, const float* values, const float* la
              int S, int E, double gamma, double lam, double reward_scale_const,
              float* advantages, float* returns, void* stream);
 
+/* ---- a22: explained-variance moments (train_ppo_diffusion_agent.py:373-377) of y = returns and
+ * d = returns - values over n rows: moments fp64[5] = {sum y, sum y^2, sum d, sum d^2, n}, one
+ * deterministic workgroup; moments may be device or host-mapped memory (dppo_host_alloc). Summed
+ * over ranks they give explained_var = 1 - Var(d) / Var(y). (ABI 5) */
+DPPO_API int dppo_value_moments(const float* values, const float* returns, int64_t n, double* moments, void* stream);
+
 /* ---- a12/a13/a20: one PPO minibatch: gather by permutation, PPODiffusion.c_loss forward + gradient
  * of pg_loss + vf_coef*v_loss w.r.t. actor_ft and critic (diffusion_ppo.py:32-132,
  * train_ppo_diffusion_agent.py:287-346).
@@ -282,12 +288,15 @@ DPPO_API int dppo_pack_all(const dppo_dims* d, int precision, const float* actor
  * dppo_adamw over the n elements at params/grads/m/v (a range of the flat [actor | critic]
  * buffer), which also copies n_metrics (<= 256) doubles of `metrics` to `metrics_out` (device or
  * host-mapped memory; the minibatch's metric sums for the host's target_kl check), then
- * dppo_pack_all of the given networks. */
+ * dppo_pack_all of the given networks. ABI 5: a nonzero metrics_tag (< 2^53) is stored as the
+ * double metrics_out[n_metrics] AFTER the n_metrics sums (system-scope release), so a host polling
+ * host-mapped metrics_out for the tag reads complete sums without recording or waiting on an event
+ * (metrics_out then holds n_metrics + 1 doubles; pass 0 for no tag). */
 DPPO_API int dppo_optimizer_step(const dppo_dims* d, int precision, float* params, const float* grads, float* m,
                         float* v, int64_t n, int64_t step, float lr, float weight_decay, float beta1,
                         float beta2, float eps, int mode, const float* actor_params, void* packed_actor,
                         const float* critic_params, void* packed_critic, const double* metrics,
-                        double* metrics_out, int n_metrics, void* stream);
+                        double* metrics_out, int n_metrics, uint64_t metrics_tag, void* stream);
 
 #ifdef __cplusplus
 }

@@ -117,4 +117,9 @@ def episodes_and_ev(rank, world, port):
     ev = D.explained_variance(torch.tensor(vals[:, off:off + n_loc]).reshape(-1),
                               torch.tensor(rets[:, off:off + n_loc]).reshape(-1))
     np.testing.assert_allclose(ev, O.explained_variance(vals.ravel(), rets.ravel()), rtol=1e-10)
+    # the agent's path: per-rank moments (what dppo_value_moments stores) summed over ranks
+    y, d = rets[:, off:off + n_loc].ravel(), (rets - vals)[:, off:off + n_loc].ravel()
+    mom = [y.sum(), (y * y).sum(), d.sum(), (d * d).sum(), float(y.size)]
+    ev2 = D.explained_variance_from_moments(mom, torch.device("cpu"), group=dist.group.WORLD)
+    np.testing.assert_allclose(ev2, O.explained_variance(vals.ravel(), rets.ravel()), rtol=1e-10)
     dist.destroy_process_group()

@@ -365,6 +365,49 @@ def test_adamw(cuda, mode):
     np.testing.assert_allclose(P.cpu().numpy(), ref, rtol=1e-5, atol=1e-6)
 
 
+def test_optimizer_step_metrics_tag(cuda):
+    """ABI 5: dppo_optimizer_step stores the tag after the metric sums in host-mapped memory; the
+    AdamW step equals dppo_adamw's."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp_64env", [])
+    m = instantiate(cfg.model, device=cuda, seed=0)
+    n = m.n_actor
+    g = torch.randn(n, device=cuda)
+    P0 = m.actor_ft_params.clone()
+    M, V = torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    met = torch.arange(16, dtype=torch.float64, device=cuda) * 0.5 + 0.25
+    out = ops.MappedDoubles(8)
+    for tag in (7, 8):
+        ops.optimizer_step(m.dims, m.precision, m.actor_ft_params, g, M, V, 1, 1e-3, 0.004, 0.9, 0.999, 1e-7, "keras",
+                           m.actor_ft_params, m.packed_ft, metrics=met, metrics_out=out.address, n_metrics=5,
+                           metrics_tag=tag)
+        out.wait_tag(5, tag, timeout_s=10.0)
+        np.testing.assert_array_equal(out.array[:5], met[:5].cpu().numpy())
+        met += 1.0
+    torch.cuda.synchronize()
+    P1, M1, V1 = P0.clone(), torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    for _ in range(2):
+        ops.adamw(P1, g, M1, V1, 1, 1e-3, 0.004, 0.9, 0.999, 1e-7, "keras")
+    torch.cuda.synchronize()
+    assert torch.equal(P1, m.actor_ft_params)
+
+
+def test_value_moments(cuda):
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    rng = np.random.default_rng(5)
+    for n in (1, 777, 32000):
+        v = rng.normal(size=n).astype(np.float32)
+        r = (v + rng.normal(0, 0.3, n)).astype(np.float32)
+        out = ops.MappedDoubles(5)
+        ops.value_moments(torch.tensor(v, device=cuda), torch.tensor(r, device=cuda), out.address)
+        torch.cuda.synchronize()
+        y, d = r.astype(np.float64), r.astype(np.float64) - v.astype(np.float64)
+        np.testing.assert_allclose(out.array, [y.sum(), (y * y).sum(), d.sum(), (d * d).sum(), n], rtol=1e-12, atol=1e-9)
+
+
 @pytest.mark.parametrize("precision,case,rtol", [("fp32", "perturbed", 2e-3), ("fp32", "ratio1", 2e-3),
                                                   ("bf16", "ratio1", 1e-2), ("bf16", "perturbed", 2e-2),
                                                   ("fp32", "perturbed-ddim", 2e-3), ("fp32", "perturbed-walker", 2e-3),
