@@ -120,7 +120,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         self._passes_enqueued = True
 
     def _update_stream(self):
-        if os.environ.get("DPPO_UPDATE_PRIO", "1") == "0":
+        if os.environ.get("DPPO_UPDATE_PRIO", "0") == "0":
             return None
         if getattr(self, "_hp_stream", None) is None:
             _, greatest = torch.cuda.Stream.priority_range()
@@ -280,9 +280,9 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         rows_local_full = eff_batch // self.world_size
         clipfracs, info = [], {}
         caller = torch.cuda.current_stream(self.device)
-        # the epochs run on a high-priority stream (DPPO_UPDATE_PRIO, default on): the actor half of
-        # a minibatch is the critical path, and the dispatcher then hands freed CUs to its workgroups
-        # before the critic half's (side stream, default priority), which has slack
+        # DPPO_UPDATE_PRIO=1 runs the epochs on a high-priority stream (the actor half of a minibatch
+        # is the critical path; the critic half on the side stream has slack). Measured slower
+        # (update 15.0 vs 14.8 ms per iteration, tools/ab_env.sh), so off by default.
         hp = self._update_stream()
         if hp is not None:
             hp.wait_stream(caller)
