@@ -15,6 +15,11 @@ struct PpoWorkspace {
     int8_t* seg;      // [ldm] t of each row (bucket id for the one-hot bias/temb sums), -1 invalid
     float* gseg;      // [64][H] per-t sums of dh1 (actor in-layer; 16 buckets in PPO, K in pretraining)
     double* stats;    // [4] adv {count, sum, sumsq}
+    // the critic's distinct samples of a minibatch (sample-weighted value loss, ppo_minibatch_impl):
+    // crow_n [ldm] sample index, crow_w [ldm] its multiplicity, crow_cnt [1] how many
+    int* crow_n;
+    float* crow_w;
+    int* crow_cnt;
     size_t total;
 };
 
@@ -36,6 +41,9 @@ inline PpoWorkspace make_ppo_workspace(const Dims& D, int precision, int rows, u
     w.seg = base ? (int8_t*)(base + o) : nullptr; o = dppo_align256(o + w.ldm);
     w.gseg = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * 64 * (size_t)D.H);
     w.stats = base ? (double*)(base + o) : nullptr; o = dppo_align256(o + 8 * 4);
+    w.crow_n = base ? (int*)(base + o) : nullptr; o = dppo_align256(o + 4 * w.ldm);
+    w.crow_w = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * w.ldm);
+    w.crow_cnt = base ? (int*)(base + o) : nullptr; o = dppo_align256(o + 4);
     w.total = o;
     return w;
 }
@@ -100,6 +108,12 @@ struct CriticArgs {
     LossHP hp;
     PpoWorkspace ws;
     double* metrics;
+    // TRAIN with crow_n != null: row r is distinct sample crow_n[r] with weight crow_w[r] (its
+    // multiplicity in the minibatch), *crow_cnt rows (device-side count); the value loss and its
+    // gradient are the per-row ones summed over the copies
+    const int* crow_n;
+    const float* crow_w;
+    const int* crow_cnt;
 };
 
 int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s);

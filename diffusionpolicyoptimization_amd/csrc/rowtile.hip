@@ -613,20 +613,29 @@ __device__ __forceinline__ void critic_rowtile_body(const CriticArgs& a) {
     int* rn = (int*)(smem + S.rn);
     float* bias = (float*)(smem + S.bias);
     float* part = (float*)(smem + S.tB);
+    const size_t grow0 = (size_t)blockIdx.x * ROWS;
+    int64_t nrows = a.nrows;
+    if (train && a.crow_n) {
+        // sample-weighted rows: the count is known on the device only; tiles past the 64-row
+        // padded count exit (the dW launch reads images only that far, DWArgs::rows_dev)
+        nrows = __builtin_amdgcn_readfirstlane(*a.crow_cnt);
+        if ((int64_t)grow0 >= (nrows + 63) / 64 * 64) return;
+    }
     for (int i = tid; i < 3 * HC + 16; i += THREADS) {
         const int seg = i < HC ? SEG_B_IN : (i < 2 * HC ? SEG_B_L1 : (i < 3 * HC ? SEG_B_L2 : SEG_B_OUT));
         const int j = i < 3 * HC ? i % HC : i - 3 * HC;
         bias[i] = ((const float*)(a.packed + L.off[seg]))[j];
     }
-    const size_t grow0 = (size_t)blockIdx.x * ROWS;
     const __amdgpu_buffer_rsrc_t wsr = packed_rsrc(a.ws.base);
     const uint32_t ldm32 = (uint32_t)a.ws.ldm, grow32 = (uint32_t)grow0;
 
     if (tid < ROWS) {
         const int64_t gr = (int64_t)grow0 + tid;
         int n = -1;
-        if (gr < a.nrows) {
-            if (train) {
+        if (gr < nrows) {
+            if (train && a.crow_n) {
+                n = a.crow_n[gr];
+            } else if (train) {
                 const uint64_t idx = minibatch_row(a.row_index, (uint64_t)(a.start + gr), a.fk);
                 if (idx < a.fk.n) n = (int)(idx / a.KF);
             } else {
@@ -713,9 +722,10 @@ __device__ __forceinline__ void critic_rowtile_body(const CriticArgs& a) {
         } else {
             float vl = 0.f, dv = 0.f;
             if (n >= 0) {
+                const float w = a.crow_w ? a.crow_w[grow0 + r] : 1.f;   // copies of the sample in the minibatch
                 const float diff = V - a.returns[n];
-                vl = 0.5f * diff * diff;                         // v_loss = 0.5 mean((V-R)^2), diffusion_ppo.py:118
-                dv = a.hp.vf_coef * diff * a.hp.grad_scale;      // loss = pg + vf_coef * v_loss (agent :340)
+                vl = 0.5f * diff * diff * w;                     // v_loss = 0.5 mean((V-R)^2), diffusion_ppo.py:118
+                dv = a.hp.vf_coef * diff * a.hp.grad_scale * w;  // loss = pg + vf_coef * v_loss (agent :340)
             }
             for (int q = 0; q < ktw; ++q) a0[r * lda0 + q] = P::cvt(q == 0 ? dv : 0.f);
             ((AT*)a.ws.cdvT)[grow0 + img_pos(r)] = P::cvt(dv);

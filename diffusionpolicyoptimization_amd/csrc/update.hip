@@ -63,6 +63,8 @@ struct DWArgs {
     float out_scale;          // 1 / the backward seed scale (fp16 images), 1 otherwise
     size_t ldm;
     const int8_t* seg;
+    const int* rows_dev;      // non-null: only the first ceil64(*rows_dev) rows are summed (the chunk
+                              // edge is recomputed on the device from that count)
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -211,8 +213,14 @@ __global__ __launch_bounds__(DWGeom<WK>::W * 64) void dw_kernel(DWArgs a) {
     const int kt = lt / pr.ntiles, nt = lt % pr.ntiles;
     const int k_base = kt * WK, n_base = nt * DW_TN;
     const int wr = wave >> 1, wc = wave & 1;
-    const size_t m_begin = (size_t)chunk * a.mchunk;
-    const size_t m_end = m_begin + a.mchunk < a.ldm ? m_begin + a.mchunk : a.ldm;
+    size_t lim = a.ldm, mchunk = (size_t)a.mchunk;
+    if (a.rows_dev) {
+        const size_t d64 = (size_t)(__builtin_amdgcn_readfirstlane(*a.rows_dev) + 63) / 64 * 64;
+        lim = d64 < lim ? d64 : lim;
+        mchunk = (lim + (size_t)a.nchunks * 64 - 1) / ((size_t)a.nchunks * 64) * 64;
+    }
+    const size_t m_begin = (size_t)chunk * mchunk;
+    const size_t m_end = m_begin + mchunk < lim ? m_begin + mchunk : lim;
     if (m_begin >= m_end) return;
     const int nst = (int)((m_end - m_begin) / BK);
     const AT* XT = (const AT*)pr.XT;
@@ -444,6 +452,99 @@ __global__ __launch_bounds__(256) void zero_kernel(ZeroArgs z) {
         const size_t n = z.n[r] / 4;
         for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) q[i] = 0u;
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The critic's distinct samples of a minibatch. The value loss depends on the sample only (obs,
+// returns: diffusion_ppo.py:108-118), and a minibatch of b rows drawn from S*E*K' (sample, step)
+// pairs holds each sample ~b/(S*E) times (1.56x at the bench shape: 50,000 rows, 26k distinct
+// samples), so the critic runs once per distinct sample with the multiplicity as the row weight:
+// the same loss and gradient sums, ~half the critic row tiles and dW rows.
+// crit_count_kernel: cnt[sample] += 1 per row (integer atomics: order-independent);
+// crit_compact_kernel: one workgroup lists the nonzero counts in sample order (deterministic) and
+// zeroes them for the next minibatch.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void crit_count_kernel(const int64_t* __restrict__ row_index, int64_t start, int rows,
+                                                         FeistelKey fk, int KF, uint32_t* __restrict__ cnt) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < rows; i += (int64_t)gridDim.x * 256) {
+        const uint64_t idx = minibatch_row(row_index, (uint64_t)(start + i), fk);
+        if (idx < fk.n) atomicAdd(cnt + idx / KF, 1u);
+    }
+}
+
+#define CC_THREADS 1024
+__global__ __launch_bounds__(CC_THREADS) void crit_compact_kernel(uint32_t* __restrict__ cnt, int nsamp,
+                                                                  int* __restrict__ crow_n, float* __restrict__ crow_w,
+                                                                  int* __restrict__ crow_cnt) {
+    __shared__ int wtot[CC_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int base = 0;
+    for (int t0 = 0; t0 < nsamp; t0 += 4 * CC_THREADS) {
+        const int i0 = t0 + 4 * tid;
+        uint32_t c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] = i0 + k < nsamp ? cnt[i0 + k] : 0u;
+        const int nz = (c[0] != 0) + (c[1] != 0) + (c[2] != 0) + (c[3] != 0);
+        int inc = nz;                                   // inclusive scan over the wave
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += o;
+        }
+        if (lane == 63) wtot[wave] = inc;
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < CC_THREADS / 64; ++w) {
+            const int v = wtot[w];
+            before += w < wave ? v : 0;
+            total += v;
+        }
+        int o = base + before + inc - nz;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (c[k]) {
+                crow_n[o] = i0 + k;
+                crow_w[o] = (float)c[k];
+                cnt[i0 + k] = 0u;
+                ++o;
+            }
+        base += total;
+        __syncthreads();                                // wtot is rewritten by the next tile
+    }
+    if (tid == 0) *crow_cnt = base;
+}
+
+// per-(device, stream) sample-count scratch of the compaction (zero between uses), grown on demand
+static uint32_t* crit_count_scratch(int64_t nsamp, hipStream_t s) {
+    struct Ent { int dev; hipStream_t s; uint32_t* p; int64_t cap; };
+    thread_local Ent ents[16] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    Ent* e = nullptr;
+    for (auto& x : ents)
+        if (x.p && x.dev == dev && x.s == s) { e = &x; break; }
+    if (!e)
+        for (auto& x : ents)
+            if (!x.p) { e = &x; break; }
+    if (!e) return nullptr;
+    if (e->p && e->cap >= nsamp) return e->p;
+    if (e->p) {
+        if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+        (void)hipFree(e->p);
+        e->p = nullptr;
+    }
+    const int64_t cap = nsamp > 65536 ? nsamp : 65536;
+    if (hipMalloc((void**)&e->p, (size_t)cap * 4) != hipSuccess) { (void)hipGetLastError(); e->p = nullptr; return nullptr; }
+    if (hipMemsetAsync(e->p, 0, (size_t)cap * 4, s) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+    e->dev = dev; e->s = s; e->cap = cap;
+    return e->p;
+}
+
+// DPPO_CRITIC_DEDUP=0 runs the critic per minibatch row (measurement knob)
+static bool crit_dedup() {
+    static const bool on = [] { const char* e = getenv("DPPO_CRITIC_DEDUP"); return !e || atoi(e) != 0; }();
+    return on;
 }
 
 __global__ void feistel_kernel(int64_t first, int64_t count, FeistelKey fk, int64_t* out) {
@@ -758,8 +859,10 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     // DPPO_DW_CHUNKS overrides the chunk count (a measurement knob).
     static const int env_ch = [] { const char* e = getenv("DPPO_DW_CHUNKS"); return e ? atoi(e) : 0; }();
     const int tk = dw_tk();
+    const int* crit_rows_dev = nullptr;
     auto launch_grads = [&](bool actor, hipStream_t st) -> int {
         DWArgs w = {};
+        if (!actor) w.rows_dev = crit_rows_dev;
         auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
             DWProb& p = w.p[w.nprob];
             p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
@@ -796,11 +899,31 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
              : precision == DPPO_F16  ? launch_dw<PolicyF16>(w, tk, st) : launch_dw<PolicyF32>(w, tk, st);
     };
 
+    // the critic's distinct samples (sample-weighted value loss, crit_compact_kernel), on the stream
+    // the critic's half runs on
+    auto critic_rows = [&](hipStream_t st) -> int {
+        if (!crit_dedup()) return DPPO_OK;
+        const int64_t nsamp = total / D.KF;
+        uint32_t* cnt = crit_count_scratch(nsamp, st);
+        DPPO_CHECK(cnt, "dppo_ppo_minibatch: sample-count scratch allocation failed");
+        const int blocks = dppo_cdiv(rows, 256) < 512 ? dppo_cdiv(rows, 256) : 512;
+        hipLaunchKernelGGL(crit_count_kernel, dim3(blocks), dim3(256), 0, st, row_index, start, rows, fk, D.KF, cnt);
+        DPPO_HIP(hipGetLastError());
+        hipLaunchKernelGGL(crit_compact_kernel, dim3(1), dim3(CC_THREADS), 0, st, cnt, (int)nsamp, ws.crow_n, ws.crow_w,
+                           ws.crow_cnt);
+        DPPO_HIP(hipGetLastError());
+        ca.crow_n = ws.crow_n; ca.crow_w = ws.crow_w; ca.crow_cnt = ws.crow_cnt;
+        crit_rows_dev = ws.crow_cnt;
+        return DPPO_OK;
+    };
+
     // The critic is independent of the actor: its row tiles and then its weight gradients run on a
     // side stream, filling the CUs the actor's row tiles leave idle (the actor's last partial round)
     // and overlapping the critic's HBM-bound dW with the actor's tiles. Joined before the
     // actor's dW completes the minibatch.
     if (parts == 2) {                                  // the critic's half on the caller's stream
+        rc = critic_rows(s);
+        if (rc) return rc;
         rc = launch_critic_rowtile(ca, precision, s);
         if (rc) return rc;
         return launch_grads(false, s);
@@ -816,6 +939,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     if (side) {
         DPPO_HIP(hipEventRecord(side->fork, s));
         DPPO_HIP(hipStreamWaitEvent(side->stream, side->fork, 0));
+        rc = critic_rows(side->stream);
+        if (rc) return rc;
         rc = launch_critic_rowtile(ca, precision, side->stream);
         if (rc) return rc;
         rc = launch_grads(false, side->stream);
@@ -825,6 +950,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     rc = launch_actor_rowtile(aa, precision, s);
     if (rc) return rc;
     if (!side) {
+        rc = critic_rows(s);
+        if (rc) return rc;
         rc = launch_critic_rowtile(ca, precision, s);
         if (rc) return rc;
         rc = launch_grads(false, s);

@@ -345,7 +345,7 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
            advantages, oldlogprobs, ft_steps, gamma_denoising=0.99, clip_ploss_coef=0.01,
            clip_ploss_coef_base=0.01, clip_ploss_coef_rate=3.0, clip_vloss_coef=None,
            norm_adv=True, min_logprob_std=0.1, vf_coef=0.5, with_grad=True, reward_horizon=4, rnd=None,
-           adv_mean_std=None, denom=None):
+           adv_mean_std=None, denom=None, critic_dedup=None):
     """Returns (metrics dict, grads_actor dict, grads_critic dict).
 
     Data-parallel restatement hooks: adv_mean_std overrides the minibatch
@@ -388,9 +388,22 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
     rclip = np.clip(ratio, 1 - cc, 1 + cc)
     pg2 = -adv * rclip
     pg_loss = np.maximum(pg1, pg2).sum() / D                      # :104-106
+    cw = None
+    if critic_dedup is not None:
+        # the value loss depends on the sample only: evaluate each distinct sample once with its
+        # multiplicity as the weight (the same sums; with rnd, the kernels' rounding points of
+        # their sample-weighted critic rows, csrc/update.hip crit_compact_kernel)
+        first, mult = critic_dedup
+        first = np.asarray(first)
+        cw = np.asarray(mult, np.float64)
+        obs, returns = obs[first], np.asarray(returns, np.float64)[first]
     v, ccache = critic_forward(pc, obs, rnd=rnd)
     v = v[:, 0]                                                   # :109
-    if clip_vloss_coef is not None:                               # :110-116
+    if cw is not None:
+        if clip_vloss_coef is not None:
+            raise NotImplementedError("critic_dedup with clip_vloss_coef")
+        v_loss = 0.5 * (cw * (v - returns) ** 2).sum() / D
+    elif clip_vloss_coef is not None:                             # :110-116
         vl_un = (v - returns) ** 2
         v_cl = oldvalues + np.clip(v - oldvalues, -clip_vloss_coef, clip_vloss_coef)
         vl_cl = (v_cl - returns) ** 2
@@ -421,6 +434,8 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
     if clip_vloss_coef is not None:
         raise NotImplementedError("clip_vloss_coef gradient (cfg default None)")
     dv = vf_coef * (v - returns) / D
+    if cw is not None:
+        dv = dv * cw
     gc, _ = residual_mlp_backward(pc, ccache, dv[:, None], "Mish", "")
     return metrics, ga, gc
 

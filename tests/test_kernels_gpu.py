@@ -408,6 +408,12 @@ def test_value_moments(cuda):
         np.testing.assert_allclose(out.array, [y.sum(), (y * y).sum(), d.sum(), (d * d).sum(), n], rtol=1e-12, atol=1e-9)
 
 
+def _dedup(bi):
+    """(first row, multiplicity) of each distinct sample: the critic's sample-weighted rows."""
+    _, first, mult = np.unique(bi, return_index=True, return_counts=True)
+    return first, mult
+
+
 @pytest.mark.parametrize("precision,case,rtol", [("fp32", "perturbed", 2e-3), ("fp32", "ratio1", 2e-3),
                                                   ("bf16", "ratio1", 1e-2), ("bf16", "perturbed", 2e-2),
                                                   ("fp32", "perturbed-ddim", 2e-3), ("fp32", "perturbed-walker", 2e-3),
@@ -456,7 +462,7 @@ def test_ppo_minibatch_grads(cuda, precision, case, rtol):
         to_f64(ft), to_f64(critic), sched, obs[bi].reshape(rows, 1, -1).astype(np.float64),
         chains[bi, di].reshape(rows, d.horizon_steps, d.action_dim).astype(np.float64), chains[bi, di + 1].reshape(rows, d.horizon_steps, d.action_dim).astype(np.float64),
         di, ret[bi].astype(np.float64), None, adv[bi].astype(np.float64), lp_old_ref[bi, di], kf,
-        rnd=_rnd(precision))
+        rnd=_rnd(precision), critic_dedup=_dedup(bi))
     na = ops.spec_count(ops.actor_param_spec(d))
     nc = ops.spec_count(ops.critic_param_spec(d))
     grads = torch.zeros(na + nc, dtype=torch.float32, device=cuda)
@@ -637,8 +643,14 @@ def test_ppo_minibatch_full_size(cuda, precision):
         g_sum += g
         m_sum += m
         g_slices.append(g)
-    rel = np.abs(g_sum - g_full).max() / np.abs(g_full).max()
-    assert rel < (1e-5 if precision == "fp32" else 1e-4), rel
+    # the critic runs once per distinct sample with its multiplicity as the row weight; a sample's
+    # multiplicity in a 2,000-row slice differs from the full minibatch's, and with 2-byte operands
+    # the weighted gradient seed is rounded once per sample (bf16(w dv) vs a sum of smaller ones):
+    # rounding-level differences, so the critic half gets its own bound there
+    for lo, hi, tol_g in ((0, na, 1e-5 if precision == "fp32" else 1e-4),
+                          (na, na + nc, 1e-5 if precision == "fp32" else 1e-3)):
+        rel = np.abs(g_sum[lo:hi] - g_full[lo:hi]).max() / np.abs(g_full[lo:hi]).max()
+        assert rel < tol_g, (lo, rel)
     # metric sums (pg, v, approx_kl, clipfrac, ratio) over 50,000 rows: fp32 accumulation order;
     # approx_kl is ~0 at ratio 1 (bf16 case), so it gets an absolute bound. The 2,000-row slices run
     # 32-row actor tiles (a sub-round minibatch), whose out-layer sums in another order: with 2-byte
@@ -656,7 +668,7 @@ def test_ppo_minibatch_full_size(cuda, precision):
         chains[bi, di].reshape(-1, d.horizon_steps, d.action_dim).astype(np.float64),
         chains[bi, di + 1].reshape(-1, d.horizon_steps, d.action_dim).astype(np.float64), di,
         ret[bi].astype(np.float64), None, adv[bi].astype(np.float64), lp_old[bi, di].astype(np.float64), kf,
-        rnd=_rnd(precision), adv_mean_std=(mean, std), denom=b)
+        rnd=_rnd(precision), adv_mean_std=(mean, std), denom=b, critic_dedup=_dedup(bi))
     g_ref = np.concatenate([ops.flatten_params(ops.actor_param_spec(d), ga).astype(np.float64),
                             ops.flatten_params(ops.critic_param_spec(d), gc).astype(np.float64)])
     g7 = g_slices[7]
