@@ -35,15 +35,18 @@ def sampler_flops_per_env(d):
 
 CU_LOAD_PEAK_GBS = 64 * 2.4   # per-CU vector-memory (TA) path: 64 B/clk at the 2.4 GHz max clock
 
-# Latency floor of one denoising step of the split sampler (csrc/sampler_split.hip, P = 4 members
-# per 16-env group, the default), the figure its per-step time is compared with: one in-launch
-# exchange of partial sums between the 4 workgroups of a group (tools/xchg_probe2.hip: 0.98 us per
-# step with the members on one XCD, sc0 granules, nothing else in the step) + the step's MFMA issue
-# on one SIMD (2 waves x 40 v_mfma_f32_16x16x32_bf16 x 16 cycles at 2.4 GHz = 0.53 us: in-Dense
-# 4, l1 16, l2 16, out-Dense 4 per wave). Everything else in a step (LDS round trips, barriers,
-# VALU epilogues, the DDPM update) is latency this floor does not count.
-SPLIT_XCHG_US = {4: 0.98, 8: 1.55}
-SPLIT_MFMA_US = {4: 2 * 40 * 16 / 2.4e3, 8: 2 * 28 * 16 / 2.4e3}
+# Latency floor of one denoising step of the split sampler (csrc/sampler_split.hip, P = 2 members
+# per 16-env group, the default; l2 folded into the out-Dense), the figure its per-step time is
+# compared with: one in-launch exchange of partial sums between the P workgroups of a group
+# (tools/xchg_probe2.hip: 0.59 us per step at P = 2, 0.98 at 4, with the members on one XCD, sc0
+# granules, nothing else in the step) + the step's MFMA issue on one SIMD (2 waves x n
+# v_mfma_f32_16x16x32_bf16 x 16 cycles at 2.4 GHz; n per wave = in-Dense 4 + residual 4/P + l1
+# 64/P + fold 4/P: P = 2: 4 + 2 + 32 + 2 = 40, P = 4: 4 + 1 + 16 + 1 = 22; r01 8-member kernel 28).
+# Everything else in a step (LDS round trips, barriers, VALU epilogues, the DDPM update) is latency
+# this floor does not count.
+SPLIT_DEFAULT_P = 2
+SPLIT_XCHG_US = {2: 0.59, 4: 0.98, 8: 1.55}
+SPLIT_MFMA_US = {2: 2 * 40 * 16 / 2.4e3, 4: 2 * 22 * 16 / 2.4e3, 8: 2 * 28 * 16 / 2.4e3}
 
 
 def sampler_layout(d, precision, envs):
@@ -200,7 +203,7 @@ def main():
         if kname + "<" in tj.get("kernel", "") and tj.get("precision") == prec and tj.get("envs") == agent.n_envs:
             traffic = tj.get("hbm_bytes_per_launch")
     if members:
-        P = 8 if p8 else 4
+        P = 8 if p8 else SPLIT_DEFAULT_P
         step_us = samp_ms * 1e3 / d.denoising_steps
         floor_us = SPLIT_XCHG_US[P] + SPLIT_MFMA_US[P]
         bound = {"kind": "latency", "kernel": kname, "workgroups_per_16_envs": members, "members_per_set": P,
@@ -208,7 +211,8 @@ def main():
                  "note": (f"each 16-env group runs on {P} CUs with 1/{P} of an actor resident in registers and "
                           "LDS (the base and fine-tuned actors' steps on two such member sets when "
                           "workgroups_per_16_envs is twice members_per_set); a denoising step is a dependent "
-                          "chain of 4 GEMMs (M = 16 envs) and one cross-CU partial-sum exchange, so its floor "
+                          "chain of small GEMMs (M = 16 envs; l2 folded into the out-Dense) and one cross-CU "
+                          "partial-sum exchange, so its floor "
                           "is that exchange (tools/xchg_probe2.hip) plus the step's MFMA issue, not bytes or "
                           "FLOPs; see DESIGN.md")}
     else:

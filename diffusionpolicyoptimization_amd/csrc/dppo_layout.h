@@ -19,6 +19,14 @@
 //          precisions: operands rounded as the kernels round them, fp32 sums)
 //   B_OUT2 fp32 [16*ceil(out/16)] b_out + W_out^T b_l2: the l2 bias folded through the out-Dense
 //          (the residual block is linear from the l2 product to the out-Dense, mlp.py:186-206)
+//   FOLD   [nt_h][nt_out] 1 KiB fragments of M = rnd(W_l2) rnd(W_out) (fp32 product, [H][out]): the
+//          l2 layer folded into the out-Dense for the same reason, so the sampler's eps is
+//          W_out^T h1 + M^T relu(h2) + B_OUT2 and l2 never runs as a GEMM. Lane l of fragment
+//          (T, n) holds, for out o = 16n + (l&15) and features f = 16T + 4(l>>4) + e, e < 4:
+//          k-slots 0-3 = hi(M[f][o]), 4-7 = lo(M[f][o]) (2-byte hi/lo pair: the product's fp32
+//          value to ~16 bits), for a B operand that repeats the 4 activations in both halves
+//   ROUT   the same geometry with both halves = rnd(W_out[f][o]) (the residual h1 term, whose B
+//          operand is h1's hi/lo pair)
 // A packed matrix [K][N] is ceil(N/16) n-tiles x KS k-steps x 64 lanes x 16 B, with
 // KS = ceil(K / KG) rounded up to EVEN (the weight stream runs in k-step pairs), KG = 32 (bf16)
 // or 16 (fp32). Lane l of (ntile, ks) holds, for e < EPL,
@@ -34,7 +42,8 @@
 #endif
 
 enum MlpSeg { SEG_TIME = 0, SEG_W_IN, SEG_B_IN, SEG_W_L1, SEG_B_L1, SEG_W_L2, SEG_B_L2, SEG_W_OUT, SEG_B_OUT,
-              SEG_T_OUT, SEG_T_L2, SEG_T_L1, SEG_TEMB, SEG_W_XS, SEG_TIN, SEG_B_OUT2, SEG_COUNT };
+              SEG_T_OUT, SEG_T_L2, SEG_T_L1, SEG_TEMB, SEG_W_XS, SEG_TIN, SEG_B_OUT2,
+              SEG_FOLD, SEG_ROUT, SEG_COUNT };
 
 struct MlpLayout {
     int in_dim, hidden, out_dim, time_dim, precision, temb_steps;
@@ -83,6 +92,9 @@ DPPO_HD inline MlpLayout make_mlp_layout(int in_dim, int hidden, int out_dim, in
     L.off[SEG_W_XS] = o; o = dppo_align256(o + (xs_rows > 0 ? packed_matrix_bytes(xs_rows, hidden, L.KG) : 0));
     L.off[SEG_TIN] = o; o = dppo_align256(o + (size_t)4 * L.temb_steps * hidden);
     L.off[SEG_B_OUT2] = o; o = dppo_align256(o + (time_dim > 0 ? (size_t)4 * 16 * L.nt_out : 0));
+    const size_t fold_bytes = time_dim > 0 ? (size_t)L.nt_h * L.nt_out * 1024 : 0;
+    L.off[SEG_FOLD] = o; o = dppo_align256(o + fold_bytes);
+    L.off[SEG_ROUT] = o; o = dppo_align256(o + fold_bytes);
     L.total = o;
     return L;
 }

@@ -19,12 +19,14 @@ struct PackJob {
     int threads;         // work items of this job
 };
 // the actor's time tables: blocks [0, R) TEMB rows; with 2-byte operands also blocks [R, 2R) TIN
-// rows and block 2R B_OUT2 (tables = 2R + 1, else R)
+// rows, block 2R B_OUT2 and blocks [2R + 1, 2R + 1 + nfold) the FOLD / ROUT fragments of one
+// 16-feature tile each (tables = 2R + 1 + nfold, else R)
 struct TembArgs {
     const float* params;
     FlatOffsets F;
-    int TD, stride, R, XD, H, nout, tables;
+    int TD, stride, R, XD, H, nout, tables, nfold;
     float *temb, *tin, *bout2;
+    uint8_t *fold, *rout;
 };
 struct PackArgs {
     PackJob j[PACK_MAXJ];
@@ -106,10 +108,69 @@ __device__ void time_table_block(const TembArgs& b, int blk) {
     }
 }
 
+// FOLD / ROUT fragments of feature tile T (dppo_layout.h): M[f][o] = sum_j rnd(W_l2[f][j])
+// rnd(W_out[j][o]) in fp32 (j ascending, 128-row chunks of both staged in LDS), then split into its
+// 2-byte hi/lo pair; ROUT is rnd(W_out) rows 16T.. in the same fragment geometry. One thread per
+// (feature, out) of the tile: 16 x 16 threads, two out tiles each (out_dim <= 32).
+template <class ET>
+__device__ void fold_block(const TembArgs& b, int T) {
+    __shared__ float fw2[16][129];
+    __shared__ float fwo[128][33];
+    __shared__ float mv[16][33];
+    const int tid = threadIdx.x, H = b.H, XD = b.XD, nt_out = b.nout / 16;
+    const float* params = b.params;
+    const FlatOffsets& F = b.F;
+    const int fr = tid >> 4, oc = tid & 15;
+    float acc0 = 0.f, acc1 = 0.f;
+    for (int j0 = 0; j0 < H; j0 += 128) {
+        const int nj = min(128, H - j0);
+        __syncthreads();
+        for (int i = tid; i < 16 * 128; i += PACK_THREADS) {
+            const int r = i >> 7, jj = i & 127, f = 16 * T + r;
+            fw2[r][jj] = (jj < nj && f < H) ? (float)(ET)params[F.l2_w + (size_t)f * H + j0 + jj] : 0.f;
+        }
+        for (int i = tid; i < 128 * 32; i += PACK_THREADS) {
+            const int jj = i >> 5, o = i & 31;
+            fwo[jj][o] = (jj < nj && o < XD) ? (float)(ET)params[F.out_w + (size_t)(j0 + jj) * XD + o] : 0.f;
+        }
+        __syncthreads();
+        for (int jj = 0; jj < nj; ++jj) {
+            const float w = fw2[fr][jj];
+            acc0 = fmaf(w, fwo[jj][oc], acc0);
+            acc1 = fmaf(w, fwo[jj][16 + oc], acc1);
+        }
+    }
+    mv[fr][oc] = acc0;
+    mv[fr][16 + oc] = acc1;
+    __syncthreads();
+    if constexpr (sizeof(ET) == 2) {
+        if (tid < 64 * nt_out) {
+            const int lane = tid & 63, n = tid >> 6, o = 16 * n + (lane & 15), jq = lane >> 4;
+            ET e[8], w[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int fl = 4 * jq + q, f = 16 * T + fl;
+                const float m = o < XD ? mv[fl][o] : 0.f;
+                const ET hi = (ET)m;
+                e[q] = hi;
+                e[4 + q] = (ET)(m - (float)hi);
+                const ET wo = (ET)((o < XD && f < H) ? params[F.out_w + (size_t)f * XD + o] : 0.f);
+                w[q] = wo;
+                w[4 + q] = wo;
+            }
+            const size_t idx = ((size_t)T * nt_out + n) * 64 + lane;
+            reinterpret_cast<u32x4*>(b.fold)[idx] = __builtin_bit_cast(u32x4, e);
+            reinterpret_cast<u32x4*>(b.rout)[idx] = __builtin_bit_cast(u32x4, w);
+        }
+    }
+}
+
 template <int KG, int EPL, class ET = __bf16>
 __global__ __launch_bounds__(PACK_THREADS) void pack_all_kernel(PackArgs a) {
     if ((int)blockIdx.x >= a.pack_blocks) {          // whole block: no barrier is skipped
-        time_table_block<ET>(a.tb, (int)blockIdx.x - a.pack_blocks);
+        const int tb = (int)blockIdx.x - a.pack_blocks;
+        if (a.tb.nfold > 0 && tb > 2 * a.tb.R) fold_block<ET>(a.tb, tb - 2 * a.tb.R - 1);
+        else time_table_block<ET>(a.tb, tb);
         return;
     }
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -204,7 +265,10 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
         b.temb = (float*)(P_out(packed) + L.off[SEG_TEMB]);
         b.tin = (float*)(P_out(packed) + L.off[SEG_TIN]);
         b.bout2 = (float*)(P_out(packed) + L.off[SEG_B_OUT2]);
-        b.tables = split_tables ? 2 * L.temb_steps + 1 : L.temb_steps;
+        b.fold = P_out(packed) + L.off[SEG_FOLD];
+        b.rout = P_out(packed) + L.off[SEG_ROUT];
+        b.nfold = split_tables ? L.nt_h : 0;
+        b.tables = split_tables ? 2 * L.temb_steps + 1 + b.nfold : L.temb_steps;
     }
     return DPPO_OK;
 }

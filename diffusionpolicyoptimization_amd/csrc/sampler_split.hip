@@ -714,43 +714,50 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// P = 4 members per 16-env group (the default; DPPO_SPLIT_P=8 selects the kernel above). Halving
-// the members halves the exchange (tools/xchg_probe2.hip, sc0 one-XCD granules at 16 envs: P = 4
-// 0.98 us per step, P = 8 1.55 us) and the arrival skew it waits on, for 16 instead of 8 MFMAs per
-// wave in l1 and l2. Member c keeps 1/4 of the actor in registers (152 VGPRs at hopper's shape):
+// P = 2 (default) or 4 members per 16-env group (DPPO_SPLIT_P=8 selects the kernel above). Fewer
+// members mean a cheaper exchange (tools/xchg_probe2.hip, sc0 one-XCD granules at 16 envs: P = 2
+// 0.59 us per step, 4 0.98, 8 1.55) and less arrival skew, for more l1 MFMAs per wave. Member c
+// keeps 1/P of l1 in registers (P = 2: 128 of 228 VGPRs), written below for P = 4:
 //   in-Dense   W_in rows [x ; state] only (K = XD + SD <= 32 KX); the time part b_in + W_in^T
 //              t_emb(t) is the pack step's TIN table (dppo_layout.h), the MFMA accumulator's start
 //   l1         output columns [128c, 128c+128): wave w owns n-tile w over ALL 512 inputs, so its
-//              result is final (b_l1 is the accumulator's start) and leaves as bf16 relu(h2) for l2
-//   l2         input rows [128c, 128c+128), all outputs; member 0 starts the accumulator from the
-//              residual h1 (its own in-Dense registers: same features, same lane order), b_l2 is
-//              folded through the out-Dense into B_OUT2
-//   out-Dense  as above (hi/lo split of the member's partial h3 from registers)
+//              result is final (b_l1 is the accumulator's start): a = relu(h2), rounded as the
+//              reference's l2 input
+//   l2 + out   folded (mlp.py:186-206: the residual block is linear from the l2 product to the
+//              out-Dense): eps = W_out^T h1 + M^T a + B_OUT2 with M = W_l2 W_out, packed per actor
+//              (SEG_FOLD, hi/lo pairs). The member's partial eps is one MFMA per out tile on the l1
+//              result straight from registers (its 4 features per lane are the MFMA's k-slots,
+//              repeated against M's hi and lo halves), plus its share of the residual term: the
+//              in-Dense tiles w*NTI + r*P + c (h1 hi/lo against SEG_ROUT). No l2 GEMM, no l2
+//              weights resident, no LDS round trip or barrier between l1 and the exchange.
 // so no wave adds a bias or a residual outside an MFMA, and no wave re-sums l1 partials.
-template <class Pol, int XQ, int KX, bool INJ, int SWV>
+// PM = members per group: 2 (the default, DPPO_S4_P: 1/2 of l1 per member, 2 l1 n-tiles per wave,
+// a 2-member exchange; possible once l2 is folded away) or 4
+template <class Pol, int XQ, int KX, bool INJ, int SWV, int PM = 4>
 __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
-    constexpr int P = 4;
+    constexpr int P = PM;
+    static_assert(P == 2 || P == 4, "members per group");
     constexpr int NO = (4 * XQ + 15) / 16;
     using AT = typename Pol::AT;
     auto pack_bf16x2 = [](float lo, float hi) { return Pol::pack2(lo, hi); };
     constexpr int H = SPLIT_H, KSH = H / 32;
     constexpr int HS = H / P;              // features per member slice (128)
-    constexpr int KS2 = HS / 32;           // l2 k-steps per member (4)
     constexpr int SW = SWV;                // waves per member: 8 (2 per SIMD) or 4 (1 per SIMD)
-    constexpr int NTI = 32 / SW;           // in-Dense / l2 n-tiles per wave (the same h1 / h3 features)
+    constexpr int NTI = 32 / SW;           // in-Dense n-tiles per wave
     constexpr int NL1 = (HS / 16) / SW;    // l1 n-tiles of the member slice per wave
-    constexpr int KO = NTI / 2;            // out-Dense k-steps per wave (its own h3 features)
-    static_assert(NL1 * SW == HS / 16 && NTI * SW == 32 && NTI % 2 == 0, "split geometry");
+    constexpr int NR = NTI / P;            // in-Dense tiles per wave whose residual term this member adds
+    static_assert(NL1 * SW == HS / 16 && NTI * SW == 32 && NTI % P == 0, "split geometry");
     constexpr int NOC = 16 * NO;
     constexpr int ST = SW * 64;
     constexpr int pad = 16;
     constexpr int ldh = H + pad;           // u1 row stride (2-byte elements)
-    constexpr int ldu2 = HS + pad;         // u2 row stride
     constexpr int lda0 = KX * 32 + pad;    // a0 row stride
     constexpr int XD = 4 * XQ;
     constexpr int NV = 16 * XD;            // coordinates of a 16-env eps block
     constexpr int NVW = NV / SW;           // per wave: 2 XD
-    constexpr int KW = (NVW + 15) / 16;    // sweep loads per lane (lane = 4 * slot + member)
+    constexpr int SL = 64 / P;             // sweep slots per wave (lane = P * slot + member)
+    constexpr int KW = (NVW + SL - 1) / SL;  // sweep loads per lane
+    static_assert(KW <= P, "the finishing lanes are the members' lanes");
     constexpr int NB = H + NOC;            // per-actor bias floats: b_l1 | B_OUT2
 
     const SampleArgs& a = sa.a;
@@ -776,7 +783,6 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     size_t o = 0;
     AT* a0 = (AT*)(smem + o); o += dppo_align16(2 * 16 * lda0);
     AT* u1 = (AT*)(smem + o); o += dppo_align16(2 * 16 * ldh);
-    AT* u2 = (AT*)(smem + o); o += dppo_align16(2 * 16 * ldu2);
     float* part = (float*)(smem + o); o += dppo_align16(4 * SW * NV);      // [wave][16 x XD]
     int* xfail = (int*)(smem + o); o += 16;                // [0] exchange failure, [1] exchange mode
     float* xs = (float*)(smem + o); o += dppo_align16(4 * 16 * XD);
@@ -786,13 +792,12 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     float* bias = (float*)(smem + o); o += dppo_align16(4 * 2 * NB);
     float* zt = (float*)(smem + o); o += dppo_align16(4 * K * 16 * XD);
     u32x4* wxs = (u32x4*)(smem + o); o += (size_t)SW * NTI * KX * 1024;   // [wave][n][ks] in-Dense fragments
-    u32x4* routl = (u32x4*)(smem + o); o += (size_t)SW * KO * NO * 1024;  // [wave][s][n] out-Dense fragments
 
-    // ---- resident weight fragments (one actor at a time): l1 and l2 in registers; the in-Dense
-    //      and out-Dense fragments in this wave's own LDS (24 VGPRs the l1 pipeline needs) ----
+    // ---- resident weight fragments (one actor at a time): l1 and the folded out-Dense in
+    //      registers; the in-Dense fragments in this wave's own LDS ----
     const __amdgpu_buffer_rsrc_t rs_base = packed_rsrc(a.packed_base), rs_ft = packed_rsrc(a.packed_ft);
     auto W = [&](int ft, int seg) { return wsrc(ft ? rs_ft : rs_base, L.off[seg]); };
-    u32x4 rl1[NL1][KSH], rl2[KS2][NTI];
+    u32x4 rl1[NL1][KSH], rfold[NL1][NO], rres[NR][NO];
     // LDS-DMA of one 1 KiB fragment (lane l's 16 B land at dst + 16 l); wave-private destinations,
     // consumed only after this wave's vmcnt(0)
     auto dma_frag = [&](int ft, int seg, int KS, int ntile, int ks, u32x4* dst) {
@@ -811,45 +816,15 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
 #pragma unroll
             for (int j = 0; j < KSH; ++j) rl1[t][j] = load_bfrag_c(W(ft, SEG_W_L1), KSH, (HS / 16) * c + NL1 * wave + t, j, lane);
     };
-    auto load_l2 = [&](int ft) {
+    auto load_fold = [&](int ft) {
 #pragma unroll
-        for (int s = 0; s < KS2; ++s)
+        for (int tt = 0; tt < NL1; ++tt)
 #pragma unroll
-            for (int n = 0; n < NTI; ++n) rl2[s][n] = load_bfrag_c(W(ft, SEG_W_L2), KSH, NTI * wave + n, c * KS2 + s, lane);
-    };
-    auto load_out = [&](int ft) {
+            for (int n = 0; n < NO; ++n) rfold[tt][n] = load_bfrag_c(W(ft, SEG_FOLD), NO, (HS / 16) * c + NL1 * wave + tt, n, lane);
 #pragma unroll
-        for (int s = 0; s < KO; ++s)
+        for (int r = 0; r < NR; ++r)
 #pragma unroll
-            for (int n = 0; n < NO; ++n) dma_frag(ft, SEG_W_OUT, KSH, n, KO * wave + s, routl + (wave * KO * NO + s * NO + n) * 64);
-    };
-    // re-order the DMA'd out-Dense fragments in place to the transposed-result k-slot order
-    // (slot_feature), once per actor (one wave's LDS ops complete in order)
-    auto permute_out = [&]() {
-        u32x4* stg = routl + wave * KO * NO * 64;
-        const int j = lane >> 4, q = lane & 15;
-        u32x4 pr[KO][NO];
-#pragma unroll
-        for (int s = 0; s < KO; ++s)
-#pragma unroll
-            for (int n = 0; n < NO; ++n) {
-                const uint16_t* src = (const uint16_t*)(stg + (s * NO + n) * 64);
-                uint32_t w[4];
-#pragma unroll
-                for (int e2 = 0; e2 < 4; ++e2) {
-                    const int f0 = slot_feature(j, 2 * e2), f1 = slot_feature(j, 2 * e2 + 1);
-                    const uint32_t lo = src[(16 * (f0 >> 3) + q) * 8 + (f0 & 7)];
-                    const uint32_t hi = src[(16 * (f1 >> 3) + q) * 8 + (f1 & 7)];
-                    w[e2] = lo | (hi << 16);
-                }
-                pr[s][n] = u32x4{w[0], w[1], w[2], w[3]};
-            }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int s = 0; s < KO; ++s)
-#pragma unroll
-            for (int n = 0; n < NO; ++n) stg[(s * NO + n) * 64 + lane] = pr[s][n];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int n = 0; n < NO; ++n) rres[r][n] = load_bfrag_c(W(ft, SEG_ROUT), NO, NTI * wave + r * P + c, n, lane);
     };
 
     // announce this member's XCD (sc1 granule, tag = seq << 6: step tags are seq << 6 | i + 1)
@@ -859,7 +834,7 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
         __hip_atomic_store(xann + c, ((uint64_t)ann_tag << 32) | (uint32_t)xcc_id(), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     const int ft0 = __builtin_amdgcn_readfirstlane(sa.dual ? set : (K - 1 < KF ? 1 : 0));
-    load_in(ft0); load_l1(ft0); load_l2(ft0); load_out(ft0);
+    load_in(ft0); load_l1(ft0); load_fold(ft0);
     int cur = ft0;
 
     // ---- prologue: biases, in-Dense time tables, schedule, noise ----
@@ -913,7 +888,6 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
         }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0): the resident set has landed
-    permute_out();
     // the group's exchange mode from the members' announcements (bounded like the exchange): every
     // member sees the same P words, so all agree; a timeout selects the placement-independent form
     if (wave == 0) {
@@ -1004,10 +978,10 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     const int xmode = __builtin_amdgcn_readfirstlane(xfail[1]);
     uint64_t* const xregion = sa.xbuf + (size_t)xmode * XREGION;
     // this lane's exchange/epilogue coordinate (launch-constant): lane (slot sl, member m) finishes
-    // coordinate sl + 16 m of its wave's slice
-    const int xm = lane & 3, xsl = lane >> 2;
-    const bool fin = xm < KW && xsl + 16 * xm < NVW;
-    const int ve = wave * NVW + (fin ? xsl + 16 * xm : 0), re = ve / XD, qe = ve % XD;
+    // coordinate sl + SL m of its wave's slice
+    const int xm = lane & (P - 1), xsl = lane / P;
+    const bool fin = xm < KW && xsl + SL * xm < NVW;
+    const int ve = wave * NVW + (fin ? xsl + SL * xm : 0), re = ve / XD, qe = ve % XD;
     XPHASE(0);
     for (int i = i0; i < i1; ++i) {
         XSTEP(i);
@@ -1017,7 +991,6 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
         const bool pre = !sa.dual && t >= 1 && PKn != PK;   // this step is the last of its actor
         if (PK != cur) {
             __builtin_amdgcn_s_waitcnt(0x0F70);
-            permute_out();
             cur = PK;
         }
         XPHASE(1);
@@ -1068,11 +1041,30 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
                 *(u32x2*)(u1 + env * ldh + f) = pk;
             }
         }
+        // the residual term W_out^T h1 of this member's in-Dense tiles (h1 as a hi/lo pair against
+        // ROUT's repeated W_out), issued under the barrier
+        f32x4 po[NO];
+#pragma unroll
+        for (int n = 0; n < NO; ++n) zero_acc(po[n]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            f32x4 hv = h1[r * P];
+#pragma unroll
+            for (int q = 1; q < P; ++q)
+                if (c == q) hv = h1[r * P + q];
+            u32x4 bh;
+            bh[0] = pack_bf16x2(hv[0], hv[1]);
+            bh[1] = pack_bf16x2(hv[2], hv[3]);
+            bh[2] = pack_bf16x2(hv[0] - Pol::lo2f(bh[0]), hv[1] - Pol::hi2f(bh[0]));
+            bh[3] = pack_bf16x2(hv[2] - Pol::lo2f(bh[1]), hv[3] - Pol::hi2f(bh[1]));
+#pragma unroll
+            for (int n = 0; n < NO; ++n) po[n] = Pol::mma(rres[r][n], bh, po[n]);
+        }
         XPHASE(11);
         lds_sync();
         XPHASE(2);
         // ---- l1 (transposed): n-tile `wave` of this member's output columns over all 512 inputs,
-        //      from b_l1; out as u2 = bf16 relu(h2) (mlp.py:202-206)
+        //      from b_l1; a = relu(h2) feeds the folded l2 + out-Dense (mlp.py:202-206)
         {
             f32x4 acc[NL1];
 #pragma unroll
@@ -1095,65 +1087,19 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
             }
             __builtin_amdgcn_sched_group_barrier(0x008, NL1 * L1D, 0);
             if (pre) load_l1(PKn);
+            // folded l2 + out-Dense: a = relu(h2) rounded once, its 4 features per lane as k-slots
+            // 0-3 and again as 4-7, against M's hi and lo halves
 #pragma unroll
             for (int tt = 0; tt < NL1; ++tt) {
-                u32x2 pk;
-                pk[0] = pack_bf16x2(relu_f(acc[tt][0]), relu_f(acc[tt][1]));
-                pk[1] = pack_bf16x2(relu_f(acc[tt][2]), relu_f(acc[tt][3]));
-                *(u32x2*)(u2 + env * ldu2 + 16 * (NL1 * wave + tt) + 4 * jq) = pk;
+                u32x4 ba;
+                ba[0] = pack_bf16x2(relu_f(acc[tt][0]), relu_f(acc[tt][1]));
+                ba[1] = pack_bf16x2(relu_f(acc[tt][2]), relu_f(acc[tt][3]));
+                ba[2] = ba[0];
+                ba[3] = ba[1];
+#pragma unroll
+                for (int n = 0; n < NO; ++n) po[n] = Pol::mma(rfold[tt][n], ba, po[n]);
             }
-        }
-        XPHASE(12);
-        lds_sync();
-        XPHASE(3);
-        // ---- l2 (transposed) over this member's K-slice; member 0 starts from the residual h1
-        f32x4 h3[NTI];
-        {
-            u32x4 bf[KS2];
-#pragma unroll
-            for (int s = 0; s < KS2; ++s) bf[s] = lds_afrag<Pol>(u2, ldu2, 0, s, lane);
-            if (c == 0) {
-#pragma unroll
-                for (int n = 0; n < NTI; ++n) h3[n] = Pol::mma(rl2[0][n], bf[0], h1[n]);
-            } else {
-#pragma unroll
-                for (int n = 0; n < NTI; ++n) h3[n] = Pol::mma(rl2[0][n], bf[0], f32x4{0.f, 0.f, 0.f, 0.f});
-            }
-#pragma unroll
-            for (int s = 1; s < KS2; ++s)
-#pragma unroll
-                for (int n = 0; n < NTI; ++n) h3[n] = Pol::mma(rl2[s][n], bf[s], h3[n]);
-            if (pre) load_l2(PKn);
-        }
-        XPHASE(13);
-        // ---- out-Dense partial (transposed) from this wave's own h3 registers (hi/lo split)
-        {
-            f32x4 po[NO], pl[NO];
-#pragma unroll
-            for (int n = 0; n < NO; ++n) { zero_acc(po[n]); zero_acc(pl[n]); }
-#pragma unroll
-            for (int s = 0; s < KO; ++s) {
-                float hv[8];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) { hv[e] = h3[2 * s][e]; hv[4 + e] = h3[2 * s + 1][e]; }
-                u32x4 hi, lo;
-#pragma unroll
-                for (int e2 = 0; e2 < 4; ++e2) {
-                    const float x0 = hv[2 * e2], x1 = hv[2 * e2 + 1];
-                    hi[e2] = pack_bf16x2(x0, x1);
-                    const float r0 = Pol::lo2f(hi[e2]), r1 = Pol::hi2f(hi[e2]);
-                    lo[e2] = pack_bf16x2(x0 - r0, x1 - r1);
-                }
-#pragma unroll
-                for (int n = 0; n < NO; ++n) {
-                    const u32x4 wo = routl[(wave * KO * NO + s * NO + n) * 64 + lane];
-                    po[n] = Pol::mma(wo, hi, po[n]);
-                    pl[n] = Pol::mma(wo, lo, pl[n]);
-                }
-            }
-#pragma unroll
-            for (int n = 0; n < NO; ++n) po[n] += pl[n];
-            if (pre) load_out(PKn);
+            if (pre) load_fold(PKn);
 #pragma unroll
             for (int n = 0; n < NO; ++n)
                 if (16 * n + 4 * jq < XD) *(f32x4*)(part + wave * NV + env * XD + 16 * n + 4 * jq) = po[n];
@@ -1161,8 +1107,8 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
         XPHASE(14);
         lds_sync();
         XPHASE(4);
-        // ---- exchange + DDPM epilogue (as the P = 8 kernel; lane = 4 * slot + member, the member
-        //      sum is two DPP levels inside the quad)
+        // ---- exchange + DDPM epilogue (as the P = 8 kernel; lane = P * slot + member, the member
+        //      sum is log2 P DPP levels inside the quad)
         {
             const uint32_t tag = (sa.seq << 6) | (uint32_t)(i + 1);
             uint64_t* xb = xregion + ((size_t)((i & 1) * GX + gx) * P) * NV;
@@ -1195,7 +1141,7 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
             for (;;) {
 #pragma unroll
                 for (int k = 0; k < KW; ++k) {
-                    const int v = sl + 16 * k < NVW ? sl + 16 * k : NVW - 1;   // clamped lanes re-read a valid granule
+                    const int v = sl + SL * k < NVW ? sl + SL * k : NVW - 1;   // clamped lanes re-read a valid granule
                     xa[k] = __hip_atomic_load(src + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 bool ok = true;
@@ -1217,12 +1163,12 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
 #pragma unroll
             for (int k = 0; k < KW; ++k) val[k] = __uint_as_float((uint32_t)xa[k]);
             XPHASE(5);
-            // member sum: xor 1 then xor 2 inside the quad; every lane adds the same two partial
-            // sums, so all four hold the same bits
+            // member sum: xor 1 (then xor 2) inside the quad; every lane adds the same two partial
+            // sums, so all P hold the same bits
 #pragma unroll
             for (int k = 0; k < KW; ++k) {
                 val[k] += dpp_f32<0xB1>(val[k]);     // quad_perm [1,0,3,2]
-                val[k] += dpp_f32<0x4E>(val[k]);     // quad_perm [2,3,0,1]
+                if constexpr (P == 4) val[k] += dpp_f32<0x4E>(val[k]);     // quad_perm [2,3,0,1]
             }
             if (fin) {
                 float ep = val[0];
@@ -1277,11 +1223,10 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
 }
 
 size_t split4_lds_bytes(int XD, int SD, int K, int KX, int NO, int sw) {
-    const int pad = 16, ldh = SPLIT_H + pad, ldu2 = SPLIT_H / 4 + pad, lda0 = KX * 32 + pad;
+    const int pad = 16, ldh = SPLIT_H + pad, lda0 = KX * 32 + pad;
     size_t o = 0;
     o += dppo_align16(2 * 16 * lda0);
     o += dppo_align16(2 * 16 * ldh);
-    o += dppo_align16(2 * 16 * ldu2);
     o += dppo_align16(4 * sw * 16 * XD);
     o += 16;
     o += dppo_align16(4 * 16 * XD);
@@ -1291,7 +1236,7 @@ size_t split4_lds_bytes(int XD, int SD, int K, int KX, int NO, int sw) {
     o += dppo_align16(4 * 2 * (SPLIT_H + 16 * NO));
     o += dppo_align16(4 * K * 16 * XD);
     o += (size_t)32 * KX * 1024;                  // sw waves x 32/sw n-tiles x KX k-steps
-    o += (size_t)16 * NO * 1024;                  // sw waves x 16/sw k-steps x NO n-tiles
+    (void)NO; (void)sw;
     return o;
 }
 
@@ -1400,30 +1345,37 @@ int launch_split_k(const SplitArgs& sa, hipStream_t s) {
 constexpr int SPLIT4_WAVES = 8;
 int split_waves() { return SPLIT4_WAVES; }
 
-template <class Pol, int XQ, int KX, bool INJ, int SWV>
+template <class Pol, int XQ, int KX, bool INJ, int SWV, int PM>
 int launch_split4_kw(const SplitArgs& sa, hipStream_t s) {
     constexpr int NO = (4 * XQ + 15) / 16;
-    auto k = sample_split4_kernel<Pol, XQ, KX, INJ, SWV>;
+    auto k = sample_split4_kernel<Pol, XQ, KX, INJ, SWV, PM>;
     const SampleArgs& a = sa.a;
     const size_t lds = split4_lds_bytes(a.XD, a.SD, a.K, KX, NO, SWV);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler needs %zu B of LDS", lds);
     DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const int blocks = 8 * 4 * ((sa.G + 7) / 8) * (sa.dual ? 2 : 1);
+    const int blocks = 8 * PM * ((sa.G + 7) / 8) * (sa.dual ? 2 : 1);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(SWV * 64), lds, s, sa);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
 
+// members per group of the folded kernel: 2 (default: 47.2 us per bench launch), or 4 with
+// -DDPPO_S4_P=4 (50.4 us; same box, tools/ab_variants.sh) — a build-time A/B knob
+#ifndef DPPO_S4_P
+#define DPPO_S4_P 2
+#endif
+constexpr int S4P = DPPO_S4_P;
+
 template <class Pol, int XQ, int KX, bool INJ>
 int launch_split4_k(const SplitArgs& sa, hipStream_t s) {
-    return launch_split4_kw<Pol, XQ, KX, INJ, SPLIT4_WAVES>(sa, s);
+    return launch_split4_kw<Pol, XQ, KX, INJ, SPLIT4_WAVES, S4P>(sa, s);
 }
 
-// DPPO_SPLIT_P: members per 16-env group, 4 (default) or 8 (the r01 kernel; A/B knob)
+// DPPO_SPLIT_P: members per 16-env group, the folded kernel (default) or 8 (the r01 kernel; A/B knob)
 int split_p_choice() {
     static const int p = [] {
         const char* e = getenv("DPPO_SPLIT_P");
-        return e && atoi(e) == 8 ? 8 : 4;
+        return e && atoi(e) == 8 ? 8 : S4P;
     }();
     return p;
 }
@@ -1442,14 +1394,14 @@ SplitPlan split_plan(int precision, int H, int XD, int SD, int ks_in, int E, int
     auto fits = [&](int P, int sets) { return cus == 0 || sets * 8 * P * ((G + 7) / 8) <= cus; };
     const int KX = dppo_cdiv(XD + SD, 32);
     const bool p4 = KX <= 2 && split4_lds_bytes(XD, SD, K, KX, dppo_cdiv(XD, 16), split_waves()) <= 160 * 1024 &&
-                    fits(4, 1);
+                    fits(S4P, 1);
     const bool p8 = ks_in == 2 && fits(8, 1);
     static const bool dual_on = [] { const char* e = getenv("DPPO_SPLIT_DUAL"); return !e || atoi(e) != 0; }();
     // two sets only while two launches of them still fit side by side (the pipelined rollout keeps
     // the next step's launch resident while this one runs)
-    const bool dual = dual_on && KF > 0 && KF < K && (cus == 0 || 2 * 2 * 8 * 4 * ((G + 7) / 8) <= cus);
-    if (split_p_choice() == 8) return p8 ? SplitPlan{8, false} : (p4 ? SplitPlan{4, dual} : SplitPlan{0, false});
-    return p4 ? SplitPlan{4, dual} : (p8 ? SplitPlan{8, false} : SplitPlan{0, false});
+    const bool dual = dual_on && KF > 0 && KF < K && (cus == 0 || 2 * 2 * 8 * S4P * ((G + 7) / 8) <= cus);
+    if (split_p_choice() == 8) return p8 ? SplitPlan{8, false} : (p4 ? SplitPlan{S4P, dual} : SplitPlan{0, false});
+    return p4 ? SplitPlan{S4P, dual} : (p8 ? SplitPlan{8, false} : SplitPlan{0, false});
 }
 
 }  // namespace
@@ -1482,7 +1434,7 @@ int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s) {
     if (rc) return rc;
     const bool inj = a.noise != nullptr;
     const bool f16 = precision == DPPO_F16;
-    if (P == 4) {
+    if (P == S4P) {
         const bool kx2 = a.XD + a.SD > 32;
         switch (a.XD / 4) {
 #define DPPO_SPLIT4_CASE(xq)                                                                                 \
