@@ -19,8 +19,8 @@ struct PackJob {
     int threads;         // work items of this job
 };
 // the actor's time tables: blocks [0, R) TEMB rows; with 2-byte operands also blocks [R, 2R) TIN
-// rows, block 2R B_OUT2 and blocks [2R + 1, 2R + 1 + nfold) the FOLD / ROUT fragments of one
-// 16-feature tile each (tables = 2R + 1 + nfold, else R)
+// rows and block 2R B_OUT2 (tables = 2R + 1, else R); and nfold blocks of FOLD / ROUT fragments (one
+// 16-feature tile each), which the launch runs first
 struct TembArgs {
     const float* params;
     FlatOffsets F;
@@ -109,35 +109,39 @@ __device__ void time_table_block(const TembArgs& b, int blk) {
 }
 
 // FOLD / ROUT fragments of feature tile T (dppo_layout.h): M[f][o] = sum_j rnd(W_l2[f][j])
-// rnd(W_out[j][o]) in fp32 (j ascending, 128-row chunks of both staged in LDS), then split into its
-// 2-byte hi/lo pair; ROUT is rnd(W_out) rows 16T.. in the same fragment geometry. One thread per
-// (feature, out) of the tile: 16 x 16 threads, two out tiles each (out_dim <= 32).
+// rnd(W_out[j][o]) in fp32 (j ascending), then split into its 2-byte hi/lo pair; ROUT is rnd(W_out)
+// rows 16T.. in the same fragment geometry. The tile's 16 rows of W_l2 are staged in LDS in one
+// round trip; each thread then runs its (feature, out) dot products over j with W_out read from
+// L2 (24 KB shared by every fold block). These blocks come first in the launch: they are its
+// longest, so they start while the copy jobs run (the pack is on every minibatch's critical path).
 template <class ET>
 __device__ void fold_block(const TembArgs& b, int T) {
-    __shared__ float fw2[16][129];
-    __shared__ float fwo[128][33];
+    constexpr int MAXH = 512;
+    __shared__ float fw2[16][MAXH + 4];
     __shared__ float mv[16][33];
     const int tid = threadIdx.x, H = b.H, XD = b.XD, nt_out = b.nout / 16;
     const float* params = b.params;
     const FlatOffsets& F = b.F;
+    if (H > MAXH) return;   // the split sampler (the only reader) needs H = 512
+    for (int i = tid; i < 16 * H; i += PACK_THREADS) {
+        const int r = i / H, j = i % H, f = 16 * T + r;
+        fw2[r][j] = f < H ? (float)(ET)params[F.l2_w + (size_t)f * H + j] : 0.f;
+    }
+    __syncthreads();
     const int fr = tid >> 4, oc = tid & 15;
+    const float* wo = params + F.out_w;
     float acc0 = 0.f, acc1 = 0.f;
-    for (int j0 = 0; j0 < H; j0 += 128) {
-        const int nj = min(128, H - j0);
-        __syncthreads();
-        for (int i = tid; i < 16 * 128; i += PACK_THREADS) {
-            const int r = i >> 7, jj = i & 127, f = 16 * T + r;
-            fw2[r][jj] = (jj < nj && f < H) ? (float)(ET)params[F.l2_w + (size_t)f * H + j0 + jj] : 0.f;
-        }
-        for (int i = tid; i < 128 * 32; i += PACK_THREADS) {
-            const int jj = i >> 5, o = i & 31;
-            fwo[jj][o] = (jj < nj && o < XD) ? (float)(ET)params[F.out_w + (size_t)(j0 + jj) * XD + o] : 0.f;
-        }
-        __syncthreads();
-        for (int jj = 0; jj < nj; ++jj) {
-            const float w = fw2[fr][jj];
-            acc0 = fmaf(w, fwo[jj][oc], acc0);
-            acc1 = fmaf(w, fwo[jj][16 + oc], acc1);
+    if (oc < XD) {
+        if (16 + oc < XD) {
+#pragma unroll 8
+            for (int j = 0; j < H; ++j) {
+                const float w = fw2[fr][j];
+                acc0 = fmaf(w, (float)(ET)wo[(size_t)j * XD + oc], acc0);
+                acc1 = fmaf(w, (float)(ET)wo[(size_t)j * XD + 16 + oc], acc1);
+            }
+        } else {
+#pragma unroll 16
+            for (int j = 0; j < H; ++j) acc0 = fmaf(fw2[fr][j], (float)(ET)wo[(size_t)j * XD + oc], acc0);
         }
     }
     mv[fr][oc] = acc0;
@@ -154,9 +158,9 @@ __device__ void fold_block(const TembArgs& b, int T) {
                 const ET hi = (ET)m;
                 e[q] = hi;
                 e[4 + q] = (ET)(m - (float)hi);
-                const ET wo = (ET)((o < XD && f < H) ? params[F.out_w + (size_t)f * XD + o] : 0.f);
-                w[q] = wo;
-                w[4 + q] = wo;
+                const ET wq = (ET)((o < XD && f < H) ? wo[(size_t)f * XD + o] : 0.f);
+                w[q] = wq;
+                w[4 + q] = wq;
             }
             const size_t idx = ((size_t)T * nt_out + n) * 64 + lane;
             reinterpret_cast<u32x4*>(b.fold)[idx] = __builtin_bit_cast(u32x4, e);
@@ -167,13 +171,17 @@ __device__ void fold_block(const TembArgs& b, int T) {
 
 template <int KG, int EPL, class ET = __bf16>
 __global__ __launch_bounds__(PACK_THREADS) void pack_all_kernel(PackArgs a) {
-    if ((int)blockIdx.x >= a.pack_blocks) {          // whole block: no barrier is skipped
-        const int tb = (int)blockIdx.x - a.pack_blocks;
-        if (a.tb.nfold > 0 && tb > 2 * a.tb.R) fold_block<ET>(a.tb, tb - 2 * a.tb.R - 1);
-        else time_table_block<ET>(a.tb, tb);
+    int blk = (int)blockIdx.x;                       // whole blocks take a branch: no barrier is skipped
+    if (blk < a.tb.nfold) {
+        fold_block<ET>(a.tb, blk);
         return;
     }
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    blk -= a.tb.nfold;
+    if (blk >= a.pack_blocks) {
+        time_table_block<ET>(a.tb, blk - a.pack_blocks);
+        return;
+    }
+    const int gid = blk * blockDim.x + threadIdx.x;
     if (gid >= a.start[a.njobs]) return;
     int ji = 0;
     while (ji + 1 < a.njobs && gid >= a.start[ji + 1]) ++ji;
@@ -268,7 +276,7 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
         b.fold = P_out(packed) + L.off[SEG_FOLD];
         b.rout = P_out(packed) + L.off[SEG_ROUT];
         b.nfold = split_tables ? L.nt_h : 0;
-        b.tables = split_tables ? 2 * L.temb_steps + 1 + b.nfold : L.temb_steps;
+        b.tables = split_tables ? 2 * L.temb_steps + 1 : L.temb_steps;
     }
     return DPPO_OK;
 }
@@ -277,7 +285,7 @@ static int launch_pack(PackArgs& a, int precision, hipStream_t s) {
     a.start[0] = 0;
     for (int i = 0; i < a.njobs; ++i) a.start[i + 1] = a.start[i] + a.j[i].threads;
     a.pack_blocks = dppo_cdiv(a.start[a.njobs], PACK_THREADS);
-    const int blocks = a.pack_blocks + a.tb.tables;
+    const int blocks = a.tb.nfold + a.pack_blocks + a.tb.tables;
     if (blocks == 0) return DPPO_OK;
     if (precision == DPPO_BF16)
         hipLaunchKernelGGL((pack_all_kernel<32, 8, __bf16>), dim3(blocks), dim3(PACK_THREADS), 0, s, a);
