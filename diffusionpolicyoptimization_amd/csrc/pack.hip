@@ -110,38 +110,45 @@ __device__ void time_table_block(const TembArgs& b, int blk) {
 
 // FOLD / ROUT fragments of feature tile T (dppo_layout.h): M[f][o] = sum_j rnd(W_l2[f][j])
 // rnd(W_out[j][o]) in fp32 (j ascending), then split into its 2-byte hi/lo pair; ROUT is rnd(W_out)
-// rows 16T.. in the same fragment geometry. The tile's 16 rows of W_l2 are staged in LDS in one
-// round trip; each thread then runs its (feature, out) dot products over j with W_out read from
-// L2 (24 KB shared by every fold block). These blocks come first in the launch: they are its
-// longest, so they start while the copy jobs run (the pack is on every minibatch's critical path).
+// rows 16T.. in the same fragment geometry. The j range runs in chunks (256 rows at out_dim <= 16,
+// 128 above) whose W_l2 rows and W_out rows are staged in LDS in one round trip each, so the dot
+// products read LDS only. These blocks come first in the launch: they are its longest, and the
+// pack is on every minibatch's critical path.
 template <class ET>
 __device__ void fold_block(const TembArgs& b, int T) {
-    constexpr int MAXH = 512;
-    __shared__ float fw2[16][MAXH + 4];
+    constexpr int JMAX = 256;
+    __shared__ float fw2[16][JMAX + 4];
+    __shared__ float wos[JMAX * 16];       // [jc][XDP]: XDP = 16 (jc < 256) or 32 (jc < 128)
     __shared__ float mv[16][33];
     const int tid = threadIdx.x, H = b.H, XD = b.XD, nt_out = b.nout / 16;
     const float* params = b.params;
     const FlatOffsets& F = b.F;
-    if (H > MAXH) return;   // the split sampler (the only reader) needs H = 512
-    for (int i = tid; i < 16 * H; i += PACK_THREADS) {
-        const int r = i / H, j = i % H, f = 16 * T + r;
-        fw2[r][j] = f < H ? (float)(ET)params[F.l2_w + (size_t)f * H + j] : 0.f;
-    }
-    __syncthreads();
-    const int fr = tid >> 4, oc = tid & 15;
     const float* wo = params + F.out_w;
+    const int XDP = XD <= 16 ? 16 : 32, JC = XD <= 16 ? JMAX : JMAX / 2;
+    const int fr = tid >> 4, oc = tid & 15;
     float acc0 = 0.f, acc1 = 0.f;
-    if (oc < XD) {
-        if (16 + oc < XD) {
+    for (int j0 = 0; j0 < H; j0 += JC) {
+        const int nj = min(JC, H - j0);
+        __syncthreads();
+        for (int i = tid; i < 16 * JC; i += PACK_THREADS) {
+            const int r = i / JC, jj = i % JC, f = 16 * T + r;
+            fw2[r][jj] = (jj < nj && f < H) ? (float)(ET)params[F.l2_w + (size_t)f * H + j0 + jj] : 0.f;
+        }
+        for (int i = tid; i < JC * XDP; i += PACK_THREADS) {
+            const int jj = i / XDP, o = i % XDP;
+            wos[i] = (jj < nj && o < XD) ? (float)(ET)wo[(size_t)(j0 + jj) * XD + o] : 0.f;
+        }
+        __syncthreads();
+        if (XDP == 32) {
 #pragma unroll 8
-            for (int j = 0; j < H; ++j) {
-                const float w = fw2[fr][j];
-                acc0 = fmaf(w, (float)(ET)wo[(size_t)j * XD + oc], acc0);
-                acc1 = fmaf(w, (float)(ET)wo[(size_t)j * XD + 16 + oc], acc1);
+            for (int jj = 0; jj < nj; ++jj) {
+                const float w = fw2[fr][jj];
+                acc0 = fmaf(w, wos[jj * 32 + oc], acc0);
+                acc1 = fmaf(w, wos[jj * 32 + 16 + oc], acc1);
             }
         } else {
 #pragma unroll 16
-            for (int j = 0; j < H; ++j) acc0 = fmaf(fw2[fr][j], (float)(ET)wo[(size_t)j * XD + oc], acc0);
+            for (int jj = 0; jj < nj; ++jj) acc0 = fmaf(fw2[fr][jj], wos[jj * 16 + oc], acc0);
         }
     }
     mv[fr][oc] = acc0;
