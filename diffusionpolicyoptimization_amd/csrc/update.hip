@@ -444,13 +444,20 @@ __global__ __launch_bounds__(256) void adv_stats_all_kernel(const float* __restr
 
 // zero up to 4 byte ranges (4-B aligned, sizes multiple of 4) in one launch
 struct ZeroArgs { void* p[4]; size_t n[4]; };
+// 16-B stores over the 16-B aligned body of each range, 4-B stores over its head and tail (the
+// grid is small: it runs while the other stream's row tiles hold most CUs)
 __global__ __launch_bounds__(256) void zero_kernel(ZeroArgs z) {
-    const size_t stride = (size_t)gridDim.x * 256;
+    const size_t stride = (size_t)gridDim.x * 256, t0 = (size_t)blockIdx.x * 256 + threadIdx.x;
     for (int r = 0; r < 4; ++r) {
         if (!z.p[r]) continue;
         uint32_t* q = (uint32_t*)z.p[r];
         const size_t n = z.n[r] / 4;
-        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) q[i] = 0u;
+        const size_t head = ((16 - ((uintptr_t)q & 15)) & 15) / 4 < n ? ((16 - ((uintptr_t)q & 15)) & 15) / 4 : n;
+        const size_t n4 = (n - head) / 4;
+        uint4* q4 = (uint4*)(q + head);
+        for (size_t i = t0; i < n4; i += stride) q4[i] = uint4{0u, 0u, 0u, 0u};
+        for (size_t i = t0; i < head; i += stride) q[i] = 0u;
+        for (size_t i = head + 4 * n4 + t0; i < n; i += stride) q[i] = 0u;
     }
 }
 
