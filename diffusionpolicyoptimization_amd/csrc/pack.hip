@@ -109,52 +109,86 @@ __device__ void time_table_block(const TembArgs& b, int blk) {
 }
 
 // FOLD / ROUT fragments of feature tile T (dppo_layout.h): M[f][o] = sum_j rnd(W_l2[f][j])
-// rnd(W_out[j][o]) in fp32 (j ascending), then split into its 2-byte hi/lo pair; ROUT is rnd(W_out)
-// rows 16T.. in the same fragment geometry. The j range runs in chunks (256 rows at out_dim <= 16,
-// 128 above) whose W_l2 rows and W_out rows are staged in LDS in one round trip each, so the dot
-// products read LDS only. These blocks come first in the launch: they are its longest, and the
-// pack is on every minibatch's critical path.
+// rnd(W_out[j][o]) in fp32, then split into its 2-byte hi/lo pair; ROUT is rnd(W_out) rows 16T.. in
+// the same fragment geometry. The tile's W_l2 rows and W_out are staged in LDS as the rounded 2-byte
+// values (exact) in one round trip at hopper's out_dim <= 16 (chunks of 256 rows above);
+// thread (g, f, oq) sums j-quarter g of each chunk for feature f and outs 4 oq.. (+16), so one
+// broadcast read of W_l2 and one 8-B read of W_out feed 4 FMAs; the quarters are added in a fixed
+// order at the end. These blocks come first in the launch: the pack is on every minibatch's
+// critical path.
 template <class ET>
 __device__ void fold_block(const TembArgs& b, int T) {
-    constexpr int JMAX = 256;
-    __shared__ float fw2[16][JMAX + 4];
-    __shared__ float wos[JMAX * 16];       // [jc][XDP]: XDP = 16 (jc < 256) or 32 (jc < 128)
-    __shared__ float mv[16][33];
-    const int tid = threadIdx.x, H = b.H, XD = b.XD, nt_out = b.nout / 16;
-    const float* params = b.params;
-    const FlatOffsets& F = b.F;
-    const float* wo = params + F.out_w;
-    const int XDP = XD <= 16 ? 16 : 32, JC = XD <= 16 ? JMAX : JMAX / 2;
-    const int fr = tid >> 4, oc = tid & 15;
-    float acc0 = 0.f, acc1 = 0.f;
-    for (int j0 = 0; j0 < H; j0 += JC) {
-        const int nj = min(JC, H - j0);
-        __syncthreads();
-        for (int i = tid; i < 16 * JC; i += PACK_THREADS) {
-            const int r = i / JC, jj = i % JC, f = 16 * T + r;
-            fw2[r][jj] = (jj < nj && f < H) ? (float)(ET)params[F.l2_w + (size_t)f * H + j0 + jj] : 0.f;
-        }
-        for (int i = tid; i < JC * XDP; i += PACK_THREADS) {
-            const int jj = i / XDP, o = i % XDP;
-            wos[i] = (jj < nj && o < XD) ? (float)(ET)wo[(size_t)(j0 + jj) * XD + o] : 0.f;
-        }
-        __syncthreads();
-        if (XDP == 32) {
-#pragma unroll 8
-            for (int jj = 0; jj < nj; ++jj) {
-                const float w = fw2[fr][jj];
-                acc0 = fmaf(w, wos[jj * 32 + oc], acc0);
-                acc1 = fmaf(w, wos[jj * 32 + 16 + oc], acc1);
-            }
-        } else {
-#pragma unroll 16
-            for (int jj = 0; jj < nj; ++jj) acc0 = fmaf(fw2[fr][jj], wos[jj * 16 + oc], acc0);
-        }
-    }
-    mv[fr][oc] = acc0;
-    mv[fr][16 + oc] = acc1;
-    __syncthreads();
     if constexpr (sizeof(ET) == 2) {
+        constexpr int JMAX = 512;
+        __shared__ ET fw2[16][JMAX + 8];
+        __shared__ __attribute__((aligned(16))) ET wos[JMAX * 16];   // [jc][XDP]
+        __shared__ float red[4][16][33];
+        __shared__ float mv[16][33];
+        const int tid = threadIdx.x, H = b.H, XD = b.XD, nt_out = b.nout / 16;
+        const float* params = b.params;
+        const FlatOffsets& F = b.F;
+        const float* wo = params + F.out_w;
+        const int XDP = XD <= 16 ? 16 : 32, JC = XD <= 16 ? JMAX : JMAX / 2;
+        const int g = tid >> 6, fr = (tid & 63) >> 2, oq = tid & 3;
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        auto ld4 = [&](int off) {                      // 4 staged W_out values as fp32
+            const u32x2 w = *(const u32x2*)(wos + off);
+            return f32x4{(float)__builtin_bit_cast(ET, (uint16_t)(w[0] & 0xffffu)),
+                         (float)__builtin_bit_cast(ET, (uint16_t)(w[0] >> 16)),
+                         (float)__builtin_bit_cast(ET, (uint16_t)(w[1] & 0xffffu)),
+                         (float)__builtin_bit_cast(ET, (uint16_t)(w[1] >> 16))};
+        };
+        bool whole = false;                            // W_out fully staged (one chunk)
+        for (int j0 = 0; j0 < H; j0 += JC) {
+            const int nj = min(JC, H - j0);
+            whole = j0 == 0 && nj == H;
+            __syncthreads();
+            // unrolled so that 16 loads per thread are in flight (a rolled loop pays one L2
+            // round trip per element)
+#pragma unroll 16
+            for (int i = tid; i < 16 * JC; i += PACK_THREADS) {
+                const int r = i / JC, jj = i % JC, f = 16 * T + r;
+                fw2[r][jj] = (ET)((jj < nj && f < H) ? params[F.l2_w + (size_t)f * H + j0 + jj] : 0.f);
+            }
+#pragma unroll 16
+            for (int i = tid; i < JC * XDP; i += PACK_THREADS) {
+                const int jj = i / XDP, o = i % XDP;
+                wos[i] = (ET)((jj < nj && o < XD) ? wo[(size_t)(j0 + jj) * XD + o] : 0.f);
+            }
+            __syncthreads();
+            const int q = JC / 4, ja = g * q;           // rows past nj are zero in both operands
+            if (XDP == 32) {
+#pragma unroll 4
+                for (int jj = ja; jj < ja + q; ++jj) {
+                    const float w = (float)fw2[fr][jj];
+                    const f32x4 u = ld4(jj * 32 + 4 * oq), v = ld4(jj * 32 + 16 + 4 * oq);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        acc0[e] = fmaf(w, u[e], acc0[e]);
+                        acc1[e] = fmaf(w, v[e], acc1[e]);
+                    }
+                }
+            } else {
+#pragma unroll 8
+                for (int jj = ja; jj < ja + q; ++jj) {
+                    const float w = (float)fw2[fr][jj];
+                    const f32x4 u = ld4(jj * 16 + 4 * oq);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc0[e] = fmaf(w, u[e], acc0[e]);
+                }
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            red[g][fr][4 * oq + e] = acc0[e];
+            red[g][fr][16 + 4 * oq + e] = acc1[e];
+        }
+        __syncthreads();
+        for (int i = tid; i < 16 * 32; i += PACK_THREADS) {
+            const int f = i >> 5, o = i & 31;
+            mv[f][o] = ((red[0][f][o] + red[1][f][o]) + red[2][f][o]) + red[3][f][o];
+        }
+        __syncthreads();
         if (tid < 64 * nt_out) {
             const int lane = tid & 63, n = tid >> 6, o = 16 * n + (lane & 15), jq = lane >> 4;
             ET e[8], w[8];
@@ -165,7 +199,7 @@ __device__ void fold_block(const TembArgs& b, int T) {
                 const ET hi = (ET)m;
                 e[q] = hi;
                 e[4 + q] = (ET)(m - (float)hi);
-                const ET wq = (ET)((o < XD && f < H) ? wo[(size_t)f * XD + o] : 0.f);
+                const ET wq = whole ? wos[f * XDP + o] : (ET)((o < XD && f < H) ? wo[(size_t)f * XD + o] : 0.f);
                 w[q] = wq;
                 w[4 + q] = wq;
             }
