@@ -103,6 +103,7 @@ __device__ void time_table_block(const TembArgs& b, int blk) {
     __syncthreads();
     for (int h = tid; h < H; h += PACK_THREADS) {
         float acc = params[F.in_b + h];
+#pragma unroll 16                                  // the loads in flight together, not one round trip each
         for (int j = 0; j < TD; ++j) acc += tr[j] * (float)(ET)params[F.in_w + (size_t)(XD + j) * H + h];
         b.tin[(size_t)row * H + h] = acc;
     }
