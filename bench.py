@@ -245,7 +245,8 @@ def main():
                      "avg_launch_ms": samp_ms, "flops_per_launch": flops, "burst_launches": n_burst,
                      "in_loop_event_ms": loop_samp_ms if agent.sampler_events else None,
                      "note": ("M = envs/GPU rows per GEMM: at 64 envs the sampler is a dependent chain of "
-                              "K x 4 small GEMMs, far below MFMA peak by construction; sampler_bound gives "
+                              "K x 3 small GEMMs (in-Dense, l1, the folded l2 + out-Dense), far below MFMA peak by "
+                              "construction; sampler_bound gives "
                               "the figure that bounds it")},
         "ppo_minibatch_avg_ms": upd_ms,
         "host_us_per_minibatch": host_us,
