@@ -81,6 +81,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
     def _alloc_buffers(self):
         S, E, d = self.n_steps, self.n_envs, self.model.dims
         dev = self.device
+        self._buf_kf = d.ft_denoising_steps
         self.obs_traj = torch.empty(S, E, d.sd, dtype=torch.float32, device=dev)
         self.chains_traj = torch.empty(S, E, d.ft_denoising_steps + 1, d.xd, dtype=torch.float32, device=dev)
         self.act_dev = torch.empty(E, d.xd, dtype=torch.float32, device=dev)
@@ -106,6 +107,29 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         self.adv = torch.empty(S, E, dtype=torch.float32, device=dev)
         self.ret = torch.empty(S, E, dtype=torch.float32, device=dev)
         self.adv_stats = torch.zeros(3, dtype=torch.float64, device=dev)
+
+    def _fit_buffers_to_model(self):
+        """The K'-shaped buffers (chains_traj [S,E,K'+1,XD], lp_old [S*E,K'], the rollout pipe bound
+        to them) follow model.ft_denoising_steps, which annealing (model.step(), diffusion_vpg.py:
+        114-142, ft_denoising_steps_d / _t) lowers between iterations. The reference allocates its
+        chains_trajs from model.ft_denoising_steps every iteration (agent :87-95); here they are
+        re-sized only when K' changed. The env state (the last observation in the staging buffer)
+        carries over."""
+        kf = self.model.ft_denoising_steps
+        if kf == self._buf_kf:
+            return
+        if kf < 1:
+            raise ValueError("ft_denoising_steps annealed to 0: no fine-tuned denoising step is left to update")
+        obs = self.obs_pin.numpy().copy()
+        if self.pipe is not None:
+            self.pipe.close()
+        self._alloc_buffers()
+        self.obs_pin.numpy()[:] = obs
+        if self.prev_obs_venv is not None:
+            self.prev_obs_venv = {"state": self.obs_pin.numpy()}
+        self._stepper = None
+        self._passes_enqueued = False
+        log.info("rollout buffers re-sized for ft_denoising_steps = %d", kf)
 
     def _enqueue_passes(self):
         """The value and old-log-prob passes over the rollout (:191-229): one fused launch each,
@@ -486,6 +510,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         ft = self.force_train if force_train is None else force_train
         eval_mode = self.itr % self.val_freq == 0 and not ft
         torch.cuda.synchronize(self.device)
+        self._fit_buffers_to_model()
         t0 = Timer()
         stats = self.rollout(eval_mode, defer_stats=not eval_mode)
         if eval_mode:

@@ -39,6 +39,7 @@ class DiffusionModel:
         self.predict_epsilon = predict_epsilon
         self.use_ddim = use_ddim
         self.ddim_steps = ddim_steps
+        self.ddim_eta = float(ddim_eta)
         self.denoised_clip_value = denoised_clip_value
         self.final_action_clip_value = final_action_clip_value
         self.randn_clip_value = randn_clip_value

@@ -181,6 +181,10 @@ class VPGDiffusion(DiffusionModel):
             self.base_params.copy_(self.actor_ft_params)
             self.dims = ops.ModelDims(**{**self.dims.__dict__, "ft_denoising_steps": self.ft_denoising_steps})
             ops.pack_actor(self.dims, self.base_params, self.precision, out=self.packed_base)
+            if hasattr(self, "_ws"):
+                self._ws.clear()     # PPO workspaces are sized for the old K'
+            # the agent re-sizes its K'-shaped rollout buffers before the next iteration
+            # (TrainPPODiffusionAgent._fit_buffers_to_model; reference agent :87-95)
             log.info("Finished annealing fine-tuning denoising steps to %d", self.ft_denoising_steps)
 
     def get_min_sampling_denoising_std(self):

@@ -111,7 +111,7 @@ class PPODiffusionLoopOracle:
                  weight_decay=0.004, min_sampling_std=0.1, randn_clip=3.0, min_logprob_std=0.1,
                  gamma_denoising=0.99, clip_ploss_coef=0.01, clip_ploss_coef_base=0.01,
                  clip_ploss_coef_rate=3.0, vf_coef=0.5, success_threshold=3.0, env_offset=0,
-                 n_critic_warmup_itr=0):
+                 n_critic_warmup_itr=0, ft_denoising_steps_d=0, ft_denoising_steps_t=0):
         self.base = {k: np.asarray(v, np.float64) for k, v in base.items()}
         self.actor_spec, self.critic_spec = actor_spec, critic_spec
         self.theta = np.concatenate([_flat(actor_spec, ft), _flat(critic_spec, critic)])
@@ -134,6 +134,7 @@ class PPODiffusionLoopOracle:
                              min_logprob_std=min_logprob_std, vf_coef=vf_coef, reward_horizon=act_steps)
         self.success_threshold = success_threshold
         self.n_critic_warmup_itr = n_critic_warmup_itr
+        self.ft_steps_d, self.ft_steps_t, self.ft_steps_cnt = ft_denoising_steps_d, ft_denoising_steps_t, 0
         self.call_id = 0
         self.itr = 0
         self.prev_obs = None
@@ -192,8 +193,19 @@ class PPODiffusionLoopOracle:
                    episodes=O.episode_stats(firsts, rewards, self.act_steps, self.success_threshold))  # :144-183
         if not eval_mode:
             out.update(self._update(obs_traj, chains, rewards, terms, firsts))
+        self._anneal()                                                               # :399
         self.itr += 1
         return out
+
+    def _anneal(self):
+        """VPGDiffusion.step (diffusion_vpg.py:114-142): every ft_denoising_steps_t calls, K' drops by
+        ft_denoising_steps_d (floor 0) and the frozen base actor becomes a copy of actor_ft
+        (`self.actor = self.actor_ft; self.actor_ft = deepcopy(self.actor)`); actor_ft and its
+        optimiser state carry on."""
+        self.ft_steps_cnt += 1
+        if self.ft_steps_d > 0 and self.ft_steps_t > 0 and self.ft_steps_cnt % self.ft_steps_t == 0:
+            self.kf = max(0, self.kf - self.ft_steps_d)
+            self.base = self.ft
 
     def _update(self, obs_traj, chains, rewards, terms, firsts):
         S, E, kf = self.S, self.env.E, self.kf

@@ -58,7 +58,8 @@ def _agent_and_oracle(seed, tmp_path, extra=(), precision="fp32"):
         min_logprob_std=m.min_logprob_denoising_std, gamma_denoising=m.gamma_denoising,
         clip_ploss_coef=m.clip_ploss_coef, clip_ploss_coef_base=m.clip_ploss_coef_base,
         clip_ploss_coef_rate=m.clip_ploss_coef_rate, vf_coef=a.vf_coef,
-        success_threshold=a.best_reward_threshold_for_success, env_offset=a.env_offset)
+        success_threshold=a.best_reward_threshold_for_success, env_offset=a.env_offset,
+        ft_denoising_steps_d=m.ft_denoising_steps_d, ft_denoising_steps_t=m.ft_denoising_steps_t)
     return a, orc
 
 
@@ -140,6 +141,8 @@ def _run_and_compare(a, orc, n_itr=3):
             e["param_delta_l2_rel"] = float(np.linalg.norm(dg - dr) / np.linalg.norm(dr))
             e["param_delta_median_rel"] = float(np.median(diff) / scale)
             e["explained_var"] = (float(res["explained_var"]), float(ref["explained_var"]))
+            # explained variance (agent :373-377) of the pre-update values and the returns
+            assert abs(e["explained_var"][0] - e["explained_var"][1]) <= 1e-3 * max(1.0, abs(e["explained_var"][1])), e
             assert e["values_abs"] <= 1e-4 and e["lp_old_abs"] <= 1e-4, e
             assert e["adv_rel"] <= 1e-4 and e["ret_rel"] <= 1e-4, e
             # Adam divides each gradient by its own running norm: where a gradient element is near
@@ -184,3 +187,19 @@ def test_iterations_match_oracle_kl_stop(cuda, tmp_path):
     errs = _run_and_compare(a, orc)
     _record("kl_stop", errs)
     assert orc.n_updates == 2 * a.update_epochs
+
+
+def test_iterations_match_oracle_with_annealing(cuda, tmp_path):
+    """ft_denoising_steps annealing (model.step(), diffusion_vpg.py:114-142) with d = t = 1: K'
+    drops 10 -> 9 -> 8 over the three iterations and the base actor becomes a copy of actor_ft
+    each time; the rollout buffers follow K' (the reference re-sizes chains_trajs every
+    iteration, agent :87-95). Compared with the oracle loop extended by the same anneal."""
+    a, orc = _agent_and_oracle(42, tmp_path, ["model.ft_denoising_steps_d=1", "model.ft_denoising_steps_t=1"])
+    kfs = []
+    errs = []
+    for _ in range(3):
+        kfs.append(a.model.ft_denoising_steps)
+        errs += _run_and_compare(a, orc, n_itr=1)
+        assert a.model.ft_denoising_steps == orc.kf
+    _record("anneal", errs)
+    assert kfs == [10, 9, 8] and a.chains_traj.shape[2] == 9 and a.lp_old.shape[1] == 8

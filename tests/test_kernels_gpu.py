@@ -591,10 +591,15 @@ def test_logprob_pass_full_size(cuda):
     assert np.abs(lpm.cpu().numpy()[pick] - ref_m).max() < 1e-4
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
-def test_ppo_minibatch_full_size(cuda, precision):
-    """dppo_ppo_minibatch at the bench's minibatch, b = 50,000 rows (782 64-row actor tiles,
-    split-K dW over all rows), over a 64,000-row rollout. The full-size launch is
+@pytest.mark.parametrize("precision,dims", [("fp32", HOPPER), ("bf16", HOPPER), ("fp16", HOPPER),
+                                            ("bf16", WALKER), ("fp32", WALKER), ("fp16", HOPPER_DDIM)],
+                         ids=["fp32-hopper", "bf16-hopper-config2", "fp16-hopper", "bf16-walker-config3-4",
+                              "fp32-walker", "fp16-ddim-config5"])
+def test_ppo_minibatch_full_size(cuda, precision, dims):
+    """dppo_ppo_minibatch at the bench's minibatch, b = 50,000 rows (782 64-row actor tiles at
+    hopper dims; at walker2d / halfcheetah dims, XD = 24, the actor runs 32-row tiles: 1,563 of
+    them; split-K dW over all rows), over a 64,000-row rollout, for every per-GPU shard shape of
+    BASELINE configs 2-5 (config 5: DDIM, 10 rows over K = 20, fp16). The full-size launch is
     checked through a size-independent property and the oracle:
       * linearity: the loss is a mean over rows, so the gradient and metric sums of the full
         launch equal the sum over 25 disjoint 2,000-row slices of the same rows (row_index), each
@@ -603,7 +608,7 @@ def test_ppo_minibatch_full_size(cuda, precision):
         minibatch's advantage mean / std)."""
     import torch
     from diffusionpolicyoptimization_amd import ops
-    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(dims, cuda)
     N, kf, b, perm_seed, epoch = 6400, d.ft_denoising_steps, 50000, 77, 3
     rng = np.random.default_rng(21)
     obs = rng.uniform(-1, 1, (N, d.sd)).astype(np.float32)
