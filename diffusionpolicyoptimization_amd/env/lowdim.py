@@ -1,0 +1,293 @@
+"""The reference's gym locomotion env stack on a batched simulator (csrc/envwrap.c):
+
+    AsyncVectorEnv (env/gym_utils/async_vector_env.py:356-456, one worker process per env)
+      -> MultiStep (wrapper/multi_step.py:113-192: act_steps sub-steps, reward sum, termination /
+         truncation at max_episode_steps, reset within the step, n_obs_steps stacking)
+        -> MujocoLocomotionLowdimWrapper (wrapper/mujoco_locomotion_lowdim.py:57-70: obs normalised to
+           [-1, 1] by normalization.npz, actions unnormalised)
+          -> the simulator
+
+Here the whole stack for all envs is one C call per action chunk (dppo_lowdim_step) that drives a
+simulator through a callback table: one batched `step` call per sub-step for the envs still
+running, one batched `reset` for the envs whose chunk ended. A simulator is any object with
+`step_fn`, `reset_fn` (C function pointers of the dppo_sim types in csrc/envwrap.c) and `ctx`:
+
+  * LinearSimulator — a C simulator (seeded linear dynamics in raw coordinates with a terminal set)
+    that fills the table exactly as a MuJoCo C-API stepper would (mj_step per env, the task's
+    reward and termination); it runs the stack end to end on hosts without MuJoCo;
+  * CallbackSimulator — Python step / reset functions behind ctypes callbacks (test doubles, or a
+    simulator with only a Python API);
+  * GymSimulator — the reference's own simulator, gym + d4rl + mujoco_py envs, one per env, behind
+    a CallbackSimulator (needs those packages: absent on the MI355X hosts).
+
+The wire format is the reference's: reset_arg() -> {"state": [E, To, Do]}; step(actions [E, Ta, Da])
+-> ({"state": [E, To, Do]}, reward [E], terminated [E], truncated [E], infos)."""
+import ctypes
+
+import numpy as np
+
+from .synthetic import _ENV_LIB
+
+_lib = None
+_P = ctypes.c_void_p
+STEP_FN = ctypes.CFUNCTYPE(ctypes.c_int, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P)
+RESET_FN = ctypes.CFUNCTYPE(ctypes.c_int, _P, ctypes.c_int, _P, _P)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = ctypes.CDLL(_ENV_LIB)
+        L.dppo_lowdim_create.restype = _P
+        L.dppo_lowdim_create.argtypes = [ctypes.c_int] * 7 + [_P, _P, _P, _P, _P, _P, _P]
+        L.dppo_lowdim_destroy.argtypes = [_P]
+        L.dppo_lowdim_reset_all.argtypes = [_P, _P]
+        L.dppo_lowdim_reset_one.argtypes = [_P, ctypes.c_int, _P]
+        L.dppo_lowdim_step.argtypes = [_P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P]
+        L.dppo_lowdim_normalize_obs.argtypes = [ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P]
+        L.dppo_lowdim_normalize_obs.restype = None
+        L.dppo_lowdim_unnormalize_action.argtypes = [ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P]
+        L.dppo_lowdim_unnormalize_action.restype = None
+        L.dppo_lowdim_counters.restype = ctypes.POINTER(ctypes.c_int64)
+        L.dppo_lowdim_counters.argtypes = [_P]
+        L.dppo_sim_linear_create.restype = _P
+        L.dppo_sim_linear_create.argtypes = [ctypes.c_int] * 3 + [_P] * 8
+        L.dppo_sim_linear_destroy.argtypes = [_P]
+        L.dppo_sim_linear_seed.argtypes = [_P, _P]
+        L.dppo_sim_linear_seed.restype = None
+        L.dppo_sim_linear_step_fn.restype = _P
+        L.dppo_sim_linear_reset_fn.restype = _P
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def normalize_obs(raw, obs_min, obs_max):
+    """MujocoLocomotionLowdimWrapper.normalize_obs (:57-58) in the native library; raw float64 [..., Do]."""
+    raw = np.ascontiguousarray(raw, np.float64)
+    mn, mx = (np.ascontiguousarray(x, np.float32) for x in (obs_min, obs_max))
+    out = np.empty_like(raw)
+    lib().dppo_lowdim_normalize_obs(raw.size // mn.size, mn.size, _p(raw), _p(mn), _p(mx), _p(out))
+    return out
+
+
+def unnormalize_action(a, action_min, action_max):
+    """MujocoLocomotionLowdimWrapper.unnormalize_action (:60-62) in the native library; a float32 [..., Da]."""
+    a = np.ascontiguousarray(a, np.float32)
+    mn, mx = (np.ascontiguousarray(x, np.float32) for x in (action_min, action_max))
+    out = np.empty_like(a)
+    lib().dppo_lowdim_unnormalize_action(a.size // mn.size, mn.size, _p(a), _p(mn), _p(mx), _p(out))
+    return out
+
+
+def load_normalization(path):
+    """normalization.npz (the reference's data/gym/<task>/normalization.npz): obs_min/obs_max [Do],
+    action_min/action_max [Da], float32; loaded without pickle."""
+    with np.load(path, allow_pickle=False) as f:
+        return {k: np.ascontiguousarray(f[k], np.float32) for k in ("obs_min", "obs_max", "action_min", "action_max")}
+
+
+class LinearSimulator:
+    """dppo_sim_linear (csrc/envwrap.c): raw state s' = A s + B a + c, reward 1 - mean((s' - goal)^2)
+    - 1e-3 |a|^2, terminal when any |s'_j - center_j| > bound_j; reset = a seeded hash around `center`. Built
+    from a family seed (the dynamics) and the normalisation ranges (the raw coordinate box), so its
+    raw observations land in the box the normalisation maps to [-1, 1]."""
+
+    def __init__(self, num_envs, obs_dim, action_dim, family_seed=0, norm=None, bound_frac=0.9):
+        rng = np.random.default_rng(20_000 + family_seed)
+        if norm is not None:
+            lo, hi = norm["obs_min"].astype(np.float64), norm["obs_max"].astype(np.float64)
+            alo, ahi = norm["action_min"].astype(np.float64), norm["action_max"].astype(np.float64)
+        else:
+            lo, hi, alo, ahi = -np.ones(obs_dim), np.ones(obs_dim), -np.ones(action_dim), np.ones(action_dim)
+        center, half = (lo + hi) / 2, (hi - lo) / 2
+        q, _ = np.linalg.qr(rng.normal(size=(obs_dim, obs_dim)))
+        A = (0.95 * q) * half[:, None] / half[None, :]     # a rotation in the normalised coordinates
+        # s' - center = A (s - center) + B a + c0: a contraction around center driven by the action
+        self.A = np.ascontiguousarray(A)
+        self.B = np.ascontiguousarray(rng.normal(0, 0.04, (action_dim, obs_dim)) * half[None, :]
+                                      / np.maximum((ahi - alo) / 2, 1e-6)[:, None])
+        c0 = rng.normal(0, 0.02, obs_dim) * half
+        self.c = np.ascontiguousarray(center - A @ center + c0 - self.B.T @ ((alo + ahi) / 2))
+        self.goal = np.ascontiguousarray(center + rng.uniform(-0.3, 0.3, obs_dim) * half)
+        self.center, self.scale = np.ascontiguousarray(center), np.ascontiguousarray(0.1 * half)
+        # terminal set: leaving the box center +- bound_frac * half (like hopper's healthy-range check)
+        self.bound = np.ascontiguousarray(bound_frac * half)
+        self.num_envs, self.obs_dim, self.action_dim = num_envs, obs_dim, action_dim
+        L = lib()
+        seeds = np.arange(num_envs, dtype=np.int64)
+        self.ctx = L.dppo_sim_linear_create(num_envs, obs_dim, action_dim, _p(self.A), _p(self.B), _p(self.c),
+                                            _p(self.goal), _p(self.center), _p(self.scale), _p(self.bound), _p(seeds))
+        if not self.ctx:
+            raise MemoryError("dppo_sim_linear_create failed")
+        self.step_fn = L.dppo_sim_linear_step_fn()
+        self.reset_fn = L.dppo_sim_linear_reset_fn()
+
+    def seed(self, seeds):
+        s = np.ascontiguousarray(np.asarray(list(seeds), np.int64))
+        assert s.size == self.num_envs
+        lib().dppo_sim_linear_seed(self.ctx, _p(s))
+
+    def __del__(self):
+        if getattr(self, "ctx", None) and _lib is not None:
+            _lib.dppo_sim_linear_destroy(self.ctx)
+            self.ctx = None
+
+
+class CallbackSimulator:
+    """Python simulator behind the callback table. step(idx [n], act [n, Da] f64) -> (obs [n, Do],
+    reward [n], done [n] bool, time_limit [n] int: -1 absent, else 0 / 1); reset(idx) -> obs [n, Do]."""
+
+    def __init__(self, obs_dim, action_dim, step, reset, seed=None):
+        self.obs_dim, self.action_dim = obs_dim, action_dim
+        self._step, self._reset, self._seed = step, reset, seed
+        self.ctx = None
+        self.error = None
+
+        def c_step(ctx, n, idx, act, obs, rew, done, tl):
+            try:
+                ix = np.ctypeslib.as_array(ctypes.cast(idx, ctypes.POINTER(ctypes.c_int32)), (n,)).copy()
+                a = np.ctypeslib.as_array(ctypes.cast(act, ctypes.POINTER(ctypes.c_double)), (n, action_dim)).copy()
+                o, r, d, t = self._step(ix, a)
+                np.ctypeslib.as_array(ctypes.cast(obs, ctypes.POINTER(ctypes.c_double)), (n, obs_dim))[:] = o
+                np.ctypeslib.as_array(ctypes.cast(rew, ctypes.POINTER(ctypes.c_double)), (n,))[:] = r
+                np.ctypeslib.as_array(ctypes.cast(done, ctypes.POINTER(ctypes.c_uint8)), (n,))[:] = d
+                np.ctypeslib.as_array(ctypes.cast(tl, ctypes.POINTER(ctypes.c_int8)), (n,))[:] = t
+                return 0
+            except Exception as exc:   # reported by LowdimVecEnv.step, never across the C frame
+                self.error = exc
+                return 1
+
+        def c_reset(ctx, n, idx, obs):
+            try:
+                ix = np.ctypeslib.as_array(ctypes.cast(idx, ctypes.POINTER(ctypes.c_int32)), (n,)).copy()
+                np.ctypeslib.as_array(ctypes.cast(obs, ctypes.POINTER(ctypes.c_double)), (n, obs_dim))[:] = self._reset(ix)
+                return 0
+            except Exception as exc:
+                self.error = exc
+                return 1
+
+        self._c_step, self._c_reset = STEP_FN(c_step), RESET_FN(c_reset)   # kept alive with the object
+        self.step_fn = ctypes.cast(self._c_step, _P).value
+        self.reset_fn = ctypes.cast(self._c_reset, _P).value
+
+    def seed(self, seeds):
+        if self._seed is not None:
+            self._seed(list(seeds))
+
+
+class GymSimulator(CallbackSimulator):
+    """The reference's simulator: gym.make(id) per env with d4rl's locomotion registrations
+    (env/gym_utils/__init__.py:125-174), stepped through the callback table. Needs gym, d4rl and
+    mujoco_py; raises ImportError when they are missing."""
+
+    def __init__(self, env_id, num_envs, obs_dim, action_dim):
+        import gym
+        import d4rl.gym_mujoco  # noqa: F401  (registers the *-medium-v2 ids, as the reference does)
+        self.envs = [gym.make(env_id) for _ in range(num_envs)]
+
+        def step(idx, act):
+            obs = np.empty((len(idx), obs_dim))
+            rew, done, tl = np.empty(len(idx)), np.empty(len(idx), bool), np.empty(len(idx), np.int8)
+            for r, i in enumerate(idx):
+                o, rw, d, info = self.envs[i].step(act[r])
+                obs[r], rew[r], done[r] = o, rw, d
+                tl[r] = -1 if "TimeLimit.truncated" not in info else int(bool(info["TimeLimit.truncated"]))
+            return obs, rew, done, tl
+
+        def reset(idx):
+            return np.stack([np.asarray(self.envs[i].reset(), np.float64) for i in idx])
+
+        def seed(seeds):
+            # MujocoLocomotionLowdimWrapper.seed (:39-43) seeds the worker's global NumPy RNG; the
+            # simulator's own RNG is seeded too so every env's resets are reproducible
+            for e, s in zip(self.envs, seeds):
+                np.random.seed(int(s))
+                e.seed(int(s))
+
+        super().__init__(obs_dim, action_dim, step, reset, seed)
+
+
+class LowdimVecEnv:
+    """The vector env over a batched simulator (see the module docstring)."""
+
+    native = None     # the agent's gated tagged-protocol path is the synthetic stepper's alone
+
+    def __init__(self, sim, num_envs, obs_dim, action_dim, act_steps=4, n_obs_steps=1, max_episode_steps=1000,
+                 reset_within_step=True, normalization=None):
+        self.sim, self.num_envs, self.obs_dim, self.action_dim = sim, num_envs, obs_dim, action_dim
+        self.act_steps, self.n_obs_steps = act_steps, n_obs_steps
+        self.max_episode_steps = max_episode_steps
+        self.norm = normalization
+        self._h = None
+        self._make(reset_within_step)
+        E, To, Do = num_envs, n_obs_steps, obs_dim
+        self._reward = np.empty(E)
+        self._term = np.empty(E, np.uint8)
+        self._trunc = np.empty(E, np.uint8)
+        self._final = np.empty((E, To, Do), np.float32)
+        self._has_final = np.empty(E, np.uint8)
+        self.published = False
+
+    def _make(self, reset_within_step):
+        L = lib()
+        nm = self.norm
+        ptrs = [None] * 4 if nm is None else [_p(nm[k]) for k in ("obs_min", "obs_max", "action_min", "action_max")]
+        if nm is not None:
+            assert nm["obs_min"].size == self.obs_dim and nm["action_min"].size == self.action_dim, "normalization dims"
+        self._h = L.dppo_lowdim_create(self.num_envs, self.obs_dim, self.action_dim, self.n_obs_steps, self.act_steps,
+                                       int(self.max_episode_steps or 0), int(bool(reset_within_step)),
+                                       self.sim.step_fn, self.sim.reset_fn, self.sim.ctx, *ptrs)
+        if not self._h:
+            raise ValueError("dppo_lowdim_create rejected the env shape")
+
+    def _check(self, rc, what):
+        if rc < 0:
+            err = getattr(self.sim, "error", None)
+            raise RuntimeError(f"simulator {what} failed" + (f": {err!r}" if err is not None else "")) from err
+
+    # ---- reference VectorEnv API ----
+    def seed(self, seeds):
+        self.sim.seed(seeds)
+
+    def reset_arg(self, options_list=None):
+        out = np.empty((self.num_envs, self.n_obs_steps, self.obs_dim), np.float32)
+        self._check(lib().dppo_lowdim_reset_all(self._h, _p(out)), "reset")
+        return {"state": out}
+
+    def reset_one_arg(self, env_ind, options=None):
+        out = np.empty((self.num_envs, self.n_obs_steps, self.obs_dim), np.float32)
+        self._check(lib().dppo_lowdim_reset_one(self._h, int(env_ind), _p(out)), "reset")
+        return {"state": out[env_ind]}
+
+    @property
+    def counters(self):
+        return np.ctypeslib.as_array(lib().dppo_lowdim_counters(self._h), (self.num_envs,)).copy()
+
+    def step(self, actions, obs_out=None, gate=None):
+        if gate is not None:
+            raise RuntimeError("gated env steps need the synthetic native stepper")
+        E = self.num_envs
+        a = np.ascontiguousarray(actions, np.float32).reshape(E, -1, self.action_dim)
+        out = obs_out if obs_out is not None else np.empty((E, self.n_obs_steps, self.obs_dim), np.float32)
+        assert out.dtype == np.float32 and out.flags.c_contiguous and out.size == E * self.n_obs_steps * self.obs_dim
+        rc = lib().dppo_lowdim_step(self._h, _p(a), a.shape[1], _p(self._reward), _p(self._term), _p(self._trunc),
+                                    _p(out), _p(self._final), _p(self._has_final))
+        self._check(rc, "step")
+        infos = None
+        if self._has_final.any():
+            infos = {int(i): {"final_obs": self._final[i].copy()} for i in np.nonzero(self._has_final)[0]}
+        return ({"state": out}, self._reward.copy(), self._term.astype(bool), self._trunc.astype(bool), infos)
+
+    def close(self):
+        if self._h:
+            lib().dppo_lowdim_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.dppo_lowdim_destroy(self._h)
+            self._h = None

@@ -1,0 +1,168 @@
+"""The host env boundary: the reference's MultiStep +
+MujocoLocomotionLowdimWrapper stack batched in C (csrc/envwrap.c, env/lowdim.py) against a
+per-env NumPy restatement of the reference's wrapper code (oracle/envstack.py).
+
+  * the wrapper arithmetic (mujoco_locomotion_lowdim.py:57-62) on the reference's own
+    normalization.npz (tests/golden/hopper_medium_v2_normalization.npz): bit-exact;
+  * MultiStep (multi_step.py:113-192): reward sums, termination / truncation (incl. a truncation
+    in the middle of a chunk and the `cnt += 1` before the `break`), reset within the step and
+    final_obs, n_obs_steps stacking with padding, the TimeLimit.truncated branch: bit-exact over
+    40 chunks with the C reference simulator and with a Python simulator behind the callbacks;
+  * make_async: a gym id without env.synthetic needs MuJoCo and fails loudly; the synthetic
+    choices are explicit."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle.envstack import LinearSimOracle, LowdimWrapperOracle, MultiStepOracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NORM = os.path.join(ROOT, "tests", "golden", "hopper_medium_v2_normalization.npz")
+
+
+def _norm():
+    from diffusionpolicyoptimization_amd.env.lowdim import load_normalization
+    return load_normalization(NORM)
+
+
+def test_wrapper_maps_bit_exact_on_reference_normalization():
+    from diffusionpolicyoptimization_amd.env import lowdim
+    nm = _norm()
+    assert nm["obs_min"].shape == (11,) and nm["action_min"].shape == (3,)
+    rng = np.random.default_rng(0)
+    lo, hi = nm["obs_min"].astype(np.float64), nm["obs_max"].astype(np.float64)
+    raw = lo + (hi - lo) * rng.uniform(-0.2, 1.2, (1000, 11))
+    orc = LowdimWrapperOracle(None, nm)
+    np.testing.assert_array_equal(lowdim.normalize_obs(raw, nm["obs_min"], nm["obs_max"]), orc.normalize_obs(raw))
+    a = rng.uniform(-1.5, 1.5, (1000, 3)).astype(np.float32)
+    ref = orc.unnormalize_action(a)
+    assert ref.dtype == np.float32
+    np.testing.assert_array_equal(lowdim.unnormalize_action(a, nm["action_min"], nm["action_max"]), ref)
+
+
+def _linear_pair(E, seeds, norm, bound_frac):
+    from diffusionpolicyoptimization_amd.env.lowdim import LinearSimulator
+    sim = LinearSimulator(E, 11, 3, family_seed=3, norm=norm, bound_frac=bound_frac)
+    sim.seed(seeds)
+    orcs = [LinearSimOracle(sim.A, sim.B, sim.c, sim.goal, sim.center, sim.scale, sim.bound, s) for s in seeds]
+    return sim, orcs
+
+
+def _compare(venv, oracle_envs, E, Ta, n_chunks, rng, amp=1.2):
+    obs0 = venv.reset_arg()["state"]
+    ref0 = np.stack([o.reset()["state"] for o in oracle_envs]).astype(np.float32)
+    np.testing.assert_array_equal(obs0, ref0)
+    n_term = n_trunc = n_final = 0
+    for _ in range(n_chunks):
+        a = rng.uniform(-amp, amp, (E, Ta, venv.action_dim)).astype(np.float32)
+        obs, r, term, trunc, infos = venv.step(a)
+        for i, o in enumerate(oracle_envs):
+            ro, rr, rt, rtr, rinfo = o.step(a[i, :venv.act_steps])
+            np.testing.assert_array_equal(obs["state"][i], ro["state"].astype(np.float32))
+            assert r[i] == rr and term[i] == rt and trunc[i] == rtr, (i, r[i], rr, term[i], rt, trunc[i], rtr)
+            if "final_obs" in rinfo:
+                np.testing.assert_array_equal(infos[i]["final_obs"], rinfo["final_obs"]["state"].astype(np.float32))
+                n_final += 1
+            else:
+                assert infos is None or i not in infos
+        n_term += int(term.sum())
+        n_trunc += int(trunc.sum())
+    return n_term, n_trunc, n_final
+
+
+@pytest.mark.parametrize("To,rws", [(1, True), (2, True), (1, False), (3, True)])
+def test_multistep_lowdim_stack_matches_reference_restatement(To, rws):
+    from diffusionpolicyoptimization_amd.env.lowdim import LowdimVecEnv
+    E, Ta = 7, 4
+    nm = _norm()
+    seeds = [42 + i for i in range(E)]
+    sim, orcs = _linear_pair(E, seeds, nm, bound_frac=0.5)
+    venv = LowdimVecEnv(sim, E, 11, 3, act_steps=Ta, n_obs_steps=To, max_episode_steps=10, reset_within_step=rws,
+                        normalization=nm)
+    oracle_envs = [MultiStepOracle(LowdimWrapperOracle(o, nm), n_obs_steps=To, n_action_steps=Ta,
+                                   max_episode_steps=10, reset_within_step=rws) for o in orcs]
+    n_term, n_trunc, n_final = _compare(venv, oracle_envs, E, Ta, 40, np.random.default_rng(To))
+    assert n_term > 0 and n_trunc > 0, (n_term, n_trunc)        # both ending kinds exercised
+    assert (n_final > 0) == rws
+
+
+class _PySim:
+    """A Python simulator reporting TimeLimit.truncated itself (gym's TimeLimit wrapper)."""
+
+    def __init__(self, seed, limit=7):
+        self.rng = np.random.default_rng(seed)
+        self.limit, self.t, self.s = limit, 0, np.zeros(5)
+
+    def reset(self):
+        self.t = 0
+        self.s = self.rng.normal(size=5)
+        return self.s.copy()
+
+    def step(self, a):
+        a = np.asarray(a, np.float64)      # the simulator's control buffer is float64 (mujoco ctrl)
+        self.t += 1
+        self.s = 0.9 * self.s + 0.1 * np.concatenate([a, a])[:5]
+        done = bool(abs(self.s[0]) > 1.2)
+        info = {}
+        if self.t >= self.limit:
+            info["TimeLimit.truncated"] = not done
+            done = True
+        return self.s.copy(), float(self.s.sum()), done, info
+
+
+def test_multistep_timelimit_branch_through_python_callbacks():
+    from diffusionpolicyoptimization_amd.env.lowdim import CallbackSimulator, LowdimVecEnv
+    E, Ta = 5, 4
+    sims = [_PySim(10 + i) for i in range(E)]
+    orcs = [_PySim(10 + i) for i in range(E)]
+
+    def step(idx, act):
+        outs = [sims[i].step(act[r]) for r, i in enumerate(idx)]
+        tl = [(-1 if "TimeLimit.truncated" not in o[3] else int(o[3]["TimeLimit.truncated"])) for o in outs]
+        return np.stack([o[0] for o in outs]), [o[1] for o in outs], [o[2] for o in outs], tl
+
+    def reset(idx):
+        return np.stack([sims[i].reset() for i in idx])
+
+    norm = {"obs_min": -np.ones(5, np.float32), "obs_max": np.ones(5, np.float32),
+            "action_min": -2 * np.ones(3, np.float32), "action_max": 2 * np.ones(3, np.float32)}
+    venv = LowdimVecEnv(CallbackSimulator(5, 3, step, reset), E, 5, 3, act_steps=Ta, n_obs_steps=2,
+                        max_episode_steps=1000, reset_within_step=True, normalization=norm)
+    oracle_envs = [MultiStepOracle(LowdimWrapperOracle(o, norm), n_obs_steps=2, n_action_steps=Ta,
+                                   max_episode_steps=1000, reset_within_step=True) for o in orcs]
+    n_term, n_trunc, _ = _compare(venv, oracle_envs, E, Ta, 25, np.random.default_rng(5))
+    assert n_trunc > 0 and n_term > 0
+
+
+def test_callback_errors_surface():
+    from diffusionpolicyoptimization_amd.env.lowdim import CallbackSimulator, LowdimVecEnv
+
+    def step(idx, act):
+        raise ValueError("simulator exploded")
+
+    venv = LowdimVecEnv(CallbackSimulator(2, 1, step, lambda idx: np.zeros((len(idx), 2))), 3, 2, 1)
+    venv.reset_arg()
+    with pytest.raises(RuntimeError, match="simulator exploded"):
+        venv.step(np.zeros((3, 4, 1), np.float32))
+
+
+def test_make_async_is_explicit_about_the_stepper(tmp_path):
+    from diffusionpolicyoptimization_amd.env.gym_utils import make_async
+    from diffusionpolicyoptimization_amd.env.lowdim import LowdimVecEnv
+    from diffusionpolicyoptimization_amd.env.synthetic import SyntheticLocomotionVecEnv
+    wr = {"mujoco_locomotion_lowdim": {"normalization_path": NORM},
+          "multi_step": {"n_obs_steps": 1, "n_action_steps": 4, "max_episode_steps": 1000, "reset_within_step": True}}
+    with pytest.raises(RuntimeError, match="MuJoCo"):
+        make_async("hopper-medium-v2", num_envs=2, wrappers=wr, obs_dim=11, action_dim=3)
+    with pytest.raises(FileNotFoundError):
+        make_async("hopper-medium-v2", num_envs=2, obs_dim=11, action_dim=3,
+                   wrappers={"mujoco_locomotion_lowdim": {"normalization_path": str(tmp_path / "missing.npz")}})
+    assert isinstance(make_async("hopper-medium-v2", num_envs=2, wrappers=wr, obs_dim=11, action_dim=3,
+                                 synthetic=True), SyntheticLocomotionVecEnv)
+    v = make_async("hopper-medium-v2", num_envs=2, wrappers=wr, obs_dim=11, action_dim=3, synthetic="lowdim")
+    assert isinstance(v, LowdimVecEnv) and v.norm is not None
+    o = v.reset_arg()["state"]
+    assert o.shape == (2, 1, 11) and np.isfinite(o).all()
+    with pytest.raises(ValueError):
+        make_async("hopper-medium-v2", num_envs=2, obs_dim=11, action_dim=3, synthetic="mujoco")

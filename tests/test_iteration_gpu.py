@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _agent_and_oracle(seed, tmp_path, extra=(), precision="fp32"):
+def _agent_and_oracle(seed, tmp_path, extra=(), precision="fp32", env_oracle=None):
     from diffusionpolicyoptimization_amd import ops
     from diffusionpolicyoptimization_amd.util.config import get_class, load_config
     cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
@@ -43,8 +43,12 @@ def _agent_and_oracle(seed, tmp_path, extra=(), precision="fp32"):
     tp = m.train_params.cpu().numpy()
     ft = ops.unflatten_params(m.actor_spec, tp[:na])
     critic = ops.unflatten_params(m.critic_spec, tp[na:])
-    env = SyntheticVecEnvOracle([a.seed + a.env_offset + i for i in range(a.n_envs)], cfg.obs_dim, cfg.action_dim,
-                                cfg.act_steps, cfg.env.max_episode_steps, cfg.env.get("family_seed", 0))
+    seeds = [a.seed + a.env_offset + i for i in range(a.n_envs)]
+    if env_oracle is not None:
+        env = env_oracle(a, cfg, seeds)
+    else:
+        env = SyntheticVecEnvOracle(seeds, cfg.obs_dim, cfg.action_dim, cfg.act_steps, cfg.env.max_episode_steps,
+                                    cfg.env.get("family_seed", 0))
     assert a.actor_lr_scheduler(1) == a.actor_lr_scheduler(50) == cfg.train.actor_lr   # constant at this cfg
     orc = PPODiffusionLoopOracle(
         base, ft, critic, m.actor_spec, m.critic_spec, O.ddpm_schedule(cfg.denoising_steps), env,
@@ -203,3 +207,27 @@ def test_iterations_match_oracle_with_annealing(cuda, tmp_path):
         assert a.model.ft_denoising_steps == orc.kf
     _record("anneal", errs)
     assert kfs == [10, 9, 8] and a.chains_traj.shape[2] == 9 and a.lp_old.shape[1] == 8
+
+
+def test_iterations_match_oracle_lowdim_env(cuda, tmp_path):
+    """The agent on the reference's wrapper stack (env.synthetic = lowdim: MultiStep +
+    MujocoLocomotionLowdimWrapper batched in C over the C reference simulator, normalised by the
+    reference's own hopper normalization.npz; env/lowdim.py) against the loop oracle over the
+    per-env NumPy restatement of the same wrappers (oracle/envstack.py): the unpipelined host
+    path (pipe.wait + step + publish) with terminal states as well as truncations."""
+    from oracle.envstack import LinearSimOracle, LowdimVecEnvOracle
+    norm_path = os.path.join(ROOT, "tests", "golden", "hopper_medium_v2_normalization.npz")
+
+    def env_oracle(a, cfg, seeds):
+        sim = a.venv.sim
+        nm = a.venv.norm
+        sims = [LinearSimOracle(sim.A, sim.B, sim.c, sim.goal, sim.center, sim.scale, sim.bound, s) for s in seeds]
+        return LowdimVecEnvOracle(sims, nm, cfg.obs_dim, cfg.action_dim, cfg.act_steps, cfg.env.max_episode_steps)
+
+    a, orc = _agent_and_oracle(42, tmp_path, ["env.synthetic=lowdim",
+                                              f"+env.wrappers.mujoco_locomotion_lowdim.normalization_path={norm_path}"],
+                               env_oracle=env_oracle)
+    from diffusionpolicyoptimization_amd.env.lowdim import LowdimVecEnv
+    assert isinstance(a.venv, LowdimVecEnv) and a.venv.norm is not None
+    errs = _run_and_compare(a, orc)
+    _record("lowdim_env", errs)
