@@ -101,6 +101,92 @@ def cpu_baseline(cfg, n_envs, S, bs):
                        f"on 1 thread scaled to the iteration ({t1_iter:.0f} s/iter)")}
 
 
+# per-kernel figures (north_star: "achieved HBM GB/s on the DDPM/GAE kernels and MFMA utilisation
+# on the denoiser GEMMs"), computed from ALGORITHMIC bytes / FLOPs (with the dtypes
+# the kernels actually move) over the rocprofv3 --kernel-trace --stats averages of a committed
+# whole-iteration profile of this workload, so each figure reproduces from that CSV
+KERNEL_STATS_CSV = os.path.join(ROOT, "profiles", "r03_iteration_kernel_stats.csv")
+
+
+def kernel_figures(d, S, E, batch, n_mb, precision, path=KERNEL_STATS_CSV):
+    import csv
+    if not os.path.exists(path):
+        return None
+    stats = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            stats[r["Name"]] = (int(r["Calls"]), float(r["TotalDurationNs"]), float(r["AverageNs"]))
+
+    def base(k):   # "void dw_kernel<PolicyBF16, 256>(DWArgs)" -> "dw_kernel"
+        k = k[5:] if k.startswith("void ") else k
+        k = k.split("<")[0].split("(")[0]
+        return k.split("::")[-1]
+
+    def find(name, must=""):
+        ks = [k for k in stats if base(k) == name and must in k]
+        return max(ks, key=lambda k: stats[k][0]) if ks else None
+
+    out = {"source": os.path.relpath(path, ROOT), "hbm_peak_GBs": HBM_PEAK_GBS}
+    # minibatches the profile covers: one actor TRAIN row-tile launch each
+    kt = find("actor_rowtile_kernel", "true")
+    n_mb = stats[kt][0] if kt else n_mb
+    N = S * E
+    na = d.actor_in * d.actor_hidden + 2 * d.actor_hidden ** 2 + d.actor_hidden * d.xd  # actor weights (MACs/row)
+    n_par = None
+    try:
+        from diffusionpolicyoptimization_amd import ops
+        n_par = ops.spec_count(ops.actor_param_spec(d)) + ops.spec_count(ops.critic_param_spec(d))
+    except Exception:
+        pass
+    hbm = {
+        # reward f64 + values f32 + terminated u8 in, advantages + returns f32 out; + last values
+        "gae_kernel": (21 * N + 4 * E, "21 B per (t, e): r f64, V f32, term u8 in; A, R f32 out"),
+        # forward scan: r f64 + first u8 in, rets f64 out; moments: rets f64 in; apply: r f64 in + out
+        "rets_kernel": (17 * N, "17 B per (t, e)"),
+        "moments_kernel": (8 * N, "8 B per (t, e)"),
+        "scale_apply_kernel": (16 * N, "16 B per (t, e)"),
+    }
+    for name, (nbytes, note) in hbm.items():
+        k = find(name)
+        if k:
+            calls, tot, avg = stats[k]
+            out[name] = {"bytes_per_launch": nbytes, "avg_us": avg / 1e3, "achieved_GBs": nbytes / avg,
+                         "frac": nbytes / avg / HBM_PEAK_GBS, "note": note}
+    k = find("adamw_kernel")
+    if k and n_par:
+        calls, tot, avg = stats[k]
+        per_mb = 28 * n_par            # p, g, m, v in; p, m, v out (fp32) over actor_ft + critic
+        out["adamw_kernel"] = {"bytes_per_minibatch": per_mb, "launches_per_minibatch": calls / n_mb,
+                               "us_per_minibatch": tot / n_mb / 1e3, "achieved_GBs": per_mb / (tot / n_mb),
+                               "frac": per_mb / (tot / n_mb) / HBM_PEAK_GBS,
+                               "note": "28 B per parameter, actor and critic ranges summed (two launches under "
+                                       "the split update); durations include sharing the CUs with the other stream"}
+    peak = PEAK["bf16" if precision in ("bf16", "fp16") else "fp32"]
+    k = find("actor_rowtile_kernel", "true")
+    if k:
+        calls, tot, avg = stats[k]
+        fl = 2 * 2 * na * batch            # forward + backward-dX of the actor, per minibatch
+        out["actor_rowtile_train"] = {"flops_per_launch": fl, "avg_us": avg / 1e3, "achieved_TFLOPs": fl / avg / 1e3,
+                                      "frac": fl / avg / 1e3 / peak}
+    k = find("dw_kernel")
+    if k:
+        calls, tot, avg = stats[k]
+        hc = d.critic_hidden
+        nc = d.sd * hc + 2 * hc * hc + hc
+        fl = 2 * (na + nc) * batch         # actor + critic weight gradients over the minibatch rows
+        out["dw_kernel"] = {"flops_per_minibatch": fl, "us_per_minibatch": tot / n_mb / 1e3,
+                            "achieved_TFLOPs": fl / (tot / n_mb) / 1e3, "frac": fl / (tot / n_mb) / 1e3 / peak,
+                            "note": "actor + critic launches summed (the critic runs on distinct samples only, "
+                                    "its algorithmic FLOPs count every row as the reference computes them)"}
+    k = find("actor_rowtile_kernel", "false")
+    if k:
+        calls, tot, avg = stats[k]
+        fl = 2 * na * N * d.ft_denoising_steps   # the old-log-prob pass over S*E*K' rows
+        out["actor_rowtile_logprob"] = {"flops_per_launch": fl, "avg_us": avg / 1e3,
+                                        "achieved_TFLOPs": fl / avg / 1e3, "frac": fl / avg / 1e3 / peak}
+    return out
+
+
 def sampler_burst_ms(agent, n=30):
     """Average sampler launch duration with HIP events on the launch stream, over n launches
     enqueued back to back on the rollout's own buffers (same workload as the timed region). The
@@ -135,6 +221,11 @@ def main():
     ap.add_argument("--batch-size", type=int, default=None, help="override train.batch_size (measurement)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--emulate-ranks", type=int, default=1,
+                    help="measurement mode: run ONE rank's share of an N-rank job on this GPU (the reference's "
+                         "global minibatch split N ways: N x the minibatches of batch_size / N rows), every "
+                         "collective skipped; value = N x this rank's env steps / its time (a bound on the "
+                         "N-GPU number without collective time)")
     args = ap.parse_args()
 
     import torch
@@ -150,6 +241,11 @@ def main():
         over.append(f"model.precision={args.precision}")
     if args.batch_size:
         over.append(f"train.batch_size={args.batch_size}")
+    emu = max(1, args.emulate_ranks)
+    if emu > 1:
+        if world > 1:
+            raise SystemExit("--emulate-ranks runs one process")
+        over.append(f"train.emulate_world={emu}")
     cfg = load_config(args.config_dir, args.config_name, over)
     agent = get_class(cfg._target_)(cfg)
     rank = agent.rank
@@ -189,12 +285,15 @@ def main():
     loop_samp_ms = sum(a.elapsed_time(b) for a, b in agent.sampler_events) / max(1, len(agent.sampler_events))
     samp_ms, n_burst = sampler_burst_ms(agent)
     upd_ms = sum(a.elapsed_time(b) for a, b in agent.update_events) / max(1, len(agent.update_events))
-    env_steps = agent.n_envs_global * cfg.act_steps * cfg.train.n_steps * args.steps
+    env_steps = agent.n_envs_global * cfg.act_steps * cfg.train.n_steps * args.steps * emu
     flops = sampler_flops_per_env(d) * agent.n_envs
     prec = agent.model.precision
     members = sampler_layout(d, prec, agent.n_envs)
-    p8 = os.environ.get("DPPO_SPLIT_P") == "8"
-    kname = ("sample_split_kernel" if p8 else "sample_split4_kernel") if members else "sample_kernel"
+    from diffusionpolicyoptimization_amd import ops as _ops
+    plan = _ops.sampler_plan(d, prec, agent.n_envs)
+    p8 = plan["kernel"] == 1
+    kname = {0: "sample_kernel", 1: "sample_split_kernel", 2: "sample_split4_kernel",
+             3: "sample_pair_kernel"}[plan["kernel"]]
     achieved = flops / (samp_ms * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -207,6 +306,7 @@ def main():
         step_us = samp_ms * 1e3 / d.denoising_steps
         floor_us = SPLIT_XCHG_US[P] + SPLIT_MFMA_US[P]
         bound = {"kind": "latency", "kernel": kname, "workgroups_per_16_envs": members, "members_per_set": P,
+                 "sampler_plan": plan,
                  "us_per_denoising_step": step_us, "floor_us_per_step": floor_us, "frac": floor_us / step_us,
                  "note": (f"each 16-env group runs on {P} CUs with 1/{P} of an actor resident in registers and "
                           "LDS (the base and fine-tuned actors' steps on two such member sets when "
@@ -215,6 +315,17 @@ def main():
                           "partial-sum exchange, so its floor "
                           "is that exchange (tools/xchg_probe2.hip) plus the step's MFMA issue, not bytes or "
                           "FLOPs; see DESIGN.md")}
+        if plan["kernel"] == 3:
+            # the pair kernel hides the exchange behind the other tile's l1: its own floor is the MFMA
+            # issue of BOTH tiles' steps on one SIMD (2 tiles x 2 waves x 40 MFMAs x 16 cycles)
+            pf = 2 * SPLIT_MFMA_US[2]
+            bound["pair_mfma_floor_us_per_step"] = pf
+            bound["pair_frac"] = pf / step_us
+            bound["note"] = ("the pair kernel: each member pair (P = 2 CUs, 1/2 of an actor resident each) runs TWO "
+                             "16-env tiles half a denoising step apart, so one tile's cross-CU exchange overlaps the "
+                             "other tile's l1 MFMAs; floor_us_per_step is the r02 one-tile floor (exchange + MFMA "
+                             "issue), pair_mfma_floor_us_per_step the pair kernel's own (MFMA issue of both tiles); "
+                             "see DESIGN.md")
     else:
         stream_b = sampler_stream_bytes_per_tile(d, prec)
         bound = {"kind": "load_path", "kernel": kname, "bytes_per_cu_per_launch": stream_b,
@@ -251,6 +362,19 @@ def main():
         "ppo_minibatch_avg_ms": upd_ms,
         "host_us_per_minibatch": host_us,
     }
+    n_mb_iter = n_updates / max(1, args.steps)
+    figs = kernel_figures(d, cfg.train.n_steps, agent.n_envs, cfg.train.batch_size // emu, n_mb_iter or 1, prec)
+    if figs is not None and emu == 1:
+        out["kernels"] = figs
+    if emu > 1:
+        out["emulated_ranks"] = emu
+        out["scaling"] = "weak (emulated)"
+        out["config"]["parallelism"] = f"ONE rank of dp{emu} emulated on 1 GPU (collectives skipped)"
+        out["config"]["batch_semantics"] = (f"global minibatch {cfg.train.batch_size} rows = the reference's "
+                                            f"({cfg.train.batch_size // emu} per rank, {int(n_mb_iter)} minibatches "
+                                            "per rank per iteration)")
+        out["note"] = (f"value = {emu} x this rank's env steps / its wall time: the {emu}-GPU throughput this "
+                       "rank's compute allows, all-reduce time excluded (an upper bound on the real run)")
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, agent.n_envs, cfg.train.n_steps, cfg.train.batch_size)
     if rank == 0:

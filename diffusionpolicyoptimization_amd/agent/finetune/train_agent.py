@@ -120,7 +120,15 @@ class TrainAgent:
         log.info("Saved model to %s", path)
 
     def load(self, itr):
+        """train_agent.py:135-142. The file of train.checkpoint_format (default .weights.h5); a run saved
+        in the other format is found too (npz was the default before round 2)."""
         path = self._ckpt_path(itr)
+        if not os.path.exists(path):
+            other = os.path.join(self.checkpoint_dir, f"state_{itr}" + (".weights.h5" if path.endswith(".npz") else ".npz"))
+            if not os.path.exists(other):
+                raise FileNotFoundError(f"no checkpoint for itr {itr}: neither {path} nor {other} exists "
+                                        "(train.checkpoint_format selects h5 or npz for saving)")
+            path = other
         self.model.load_weights(path)
         log.info("Loaded model from %s", path)
 

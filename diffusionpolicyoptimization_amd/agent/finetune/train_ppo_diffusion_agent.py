@@ -61,6 +61,9 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         self.learn_eta = self.model.learn_eta
         self.perm_seed = int(cfg.train.get("perm_seed", self.seed * 1_000_003 + 17)) + 7919 * self.rank
         self.timing = {"rollout_s": 0.0, "update_s": 0.0, "n_updates": 0, "env_steps": 0, "iters": 0}
+        self.emulate_world = max(1, int(cfg.train.get("emulate_world", 1)))
+        if self.emulate_world > 1 and self.world_size > 1:
+            raise ValueError("train.emulate_world is a single-process measurement mode")
         self.sampler_events = None    # optional list of (start, end) torch.cuda.Event pairs
         self.update_events = None
         self.host_profile = None      # optional dict: host seconds per update-loop phase (tools)
@@ -131,16 +134,26 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         self._passes_enqueued = False
         log.info("rollout buffers re-sized for ft_denoising_steps = %d", kf)
 
-    def _enqueue_passes(self):
-        """The value and old-log-prob passes over the rollout (:191-229): one fused launch each,
-        no num_split needed."""
-        S, E, m = self.n_steps, self.n_envs, self.model
+    def _logprob_range(self, s0, s1):
+        """The old-log-prob pass (:209-229) over rollout steps [s0, s1) on the current stream."""
+        E, m = self.n_envs, self.model
         kf = m.ft_denoising_steps
+        a, b = s0 * E, s1 * E
+        ops.logprob(m.dims, m.precision, m.packed_ft, m.sched, self.obs_traj.view(-1, m.dims.sd)[a:b],
+                    self.chains_traj.view(-1, kf + 1, m.dims.xd)[a:b], min_logprob_std=m.min_logprob_denoising_std,
+                    reward_horizon=self.reward_horizon, want_elem=False, lp_mean=self.lp_old[a:b])
+
+    def _enqueue_passes(self, from_step=0):
+        """The value and old-log-prob passes over the rollout (:191-229): one fused launch each,
+        no num_split needed. Steps before from_step already had their log-probs computed during
+        the rollout (pass stream, see rollout())."""
+        S, E, m = self.n_steps, self.n_envs, self.model
         N = S * E
         ops.critic_forward(m.dims, m.precision, m.packed_critic, self.obs_traj.view(N, -1), values=self.values)
-        ops.logprob(m.dims, m.precision, m.packed_ft, m.sched, self.obs_traj.view(N, -1),
-                    self.chains_traj.view(N, kf + 1, -1), min_logprob_std=m.min_logprob_denoising_std,
-                    reward_horizon=self.reward_horizon, want_elem=False, lp_mean=self.lp_old)
+        if from_step < S:
+            self._logprob_range(from_step, S)
+        if getattr(self, "_pass_stream", None) is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._pass_stream)
         self._passes_enqueued = True
 
     def _update_stream(self):
@@ -191,15 +204,41 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # the device for the observation the host publishes after the env step
             pipe = self.pipe
             early = defer_stats      # a train iteration: its value / old-log-prob passes follow the rollout
+            # The old-log-prob pass of finished chunks runs DURING the rollout: actor_ft is frozen
+            # until the update, chunk t's chains and observation are final once launch t is done, and
+            # the sampler holds a few CUs only. Every G steps one log-prob launch over the last G
+            # chunks (G x E x K' rows) goes to a pass stream behind the events of the two latest
+            # launches, onto the idle CUs (DPPO_PASS_CHUNK = G; 0 = after the rollout).
+            G = int(os.environ.get("DPPO_PASS_CHUNK", "10")) if early else 0
+            if G > 0 and getattr(self, "_pass_stream", None) is None:
+                self._pass_stream = torch.cuda.Stream(device=self.device)
+            done_lp = 0
+            evs = []
+
+            def overlap_passes(last):
+                # launches 0..last are enqueued: log-probs of steps [done_lp, last] once they finish
+                nonlocal done_lp
+                if G <= 0 or last + 1 - done_lp < G:
+                    return
+                ps = self._pass_stream
+                for ev in evs[max(0, last - 1):last + 1]:   # the two streams' latest launches <= last
+                    ps.wait_event(ev)
+                with torch.cuda.stream(ps):
+                    self._logprob_range(done_lp, last + 1)
+                done_lp = last + 1
 
             def last_enqueued():
                 # right behind the last sampler launch, so the GPU runs the passes while the host
                 # does the last env step and the rollout's bookkeeping (they read only obs / chains)
                 pipe.end()
-                self._enqueue_passes()
+                self._enqueue_passes(done_lp)
 
             pipe.begin()
+            if G > 0:
+                self._pass_stream.wait_stream(stream)       # the weights the log-probs read
             pipe.enqueue(0, eval_mode)
+            if G > 0:
+                evs.append(pipe.launch_event())
             if early and S == 1:
                 last_enqueued()
             pipe.publish()
@@ -210,6 +249,10 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 more = step + 1 < S
                 if more:
                     pipe.enqueue(step + 1, eval_mode)
+                    if G > 0:
+                        evs.append(pipe.launch_event())
+                        if step + 2 < S:
+                            overlap_passes(step)           # launch `step` finished before launch step+1 can
                     if early and step + 2 == S:
                         last_enqueued()
                 if gated:
@@ -292,16 +335,21 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         ops.value_moments(self.values, ret_flat, self._ev_map.address)
 
         total_local = N * kf
-        total_global = total_local * self.world_size
+        # W: the data-parallel width the minibatch arithmetic follows. train.emulate_world = W' > 1
+        # on ONE process is a measurement mode (bench.py --emulate-ranks): this rank runs exactly one
+        # rank's share of the W'-rank update (W' x the minibatches, batch_size / W' rows each, the
+        # gradient scaled by 1 / batch_size) with every collective skipped
+        W = self.world_size if self.world_size > 1 else self.emulate_world
+        total_global = total_local * W
         # Data parallel: by default the global minibatch is the reference's
         # batch_size rows, batch_size / world drawn by each rank from its own shard (each rank's
         # keyed permutation of its rows), so the update is the reference's PPO over the union of
         # the shards (world x more minibatches than one rank over its own envs). With
         # train.dp_scale_batch = true every rank runs a full batch_size minibatch of its own and
         # the gradients are averaged: the reference run with batch_size x world.
-        eff_batch = self.batch_size * (self.world_size if self.dp_scale_batch else 1)
+        eff_batch = self.batch_size * (W if self.dp_scale_batch else 1)
         num_batch = max(1, total_global // eff_batch)                                     # :288
-        rows_local_full = eff_batch // self.world_size
+        rows_local_full = eff_batch // W
         clipfracs, info = [], {}
         caller = torch.cuda.current_stream(self.device)
         # DPPO_UPDATE_PRIO=1 runs the epochs on a high-priority stream (the actor half of a minibatch
@@ -355,6 +403,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 clipfracs.append(inf["clipfrac"])
                 return inf, self.target_kl is not None and inf["approx_kl"] > self.target_kl
 
+            dp = self.world_size > 1
             # every minibatch's advantage moments (norm_adv, diffusion_ppo.py:74-75) in one launch, and
             # on several GPUs one all-reduce of the whole table instead of one per minibatch
             n_mb = self.update_epochs * num_batch
@@ -362,19 +411,24 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 self._adv_all = torch.zeros(n_mb, 3, dtype=torch.float64, device=self.device)
             ops.ppo_adv_stats_all(adv_flat, total_local, kf, self.perm_seed, 1000 * self.itr, self.update_epochs,
                                   rows_local_full, num_batch, self._adv_all)
-            if self.world_size > 1:
+            if dp:
                 self._allreduce(self._adv_all)
-            # Split update (single GPU): the critic's half of each minibatch (row tiles, dW, its AdamW
-            # range, repack) runs on a side stream and the actor's on the main stream, so the critic of
+            # Split update: the critic's half of each minibatch (row tiles, dW, its AdamW range,
+            # repack) runs on a side stream and the actor's on the main stream, so the critic of
             # minibatch i+1 fills the CUs the actor leaves idle in its dW / small-kernel tail of i.
             # Metrics alternate between two device buffers; the main stream joins the critic's half
             # before copying a minibatch's metrics.
-            split = (self.world_size == 1 and self.max_grad_norm is None
-                     and os.environ.get("DPPO_SPLIT_UPDATE", "1") != "0")
+            # Under data parallelism the gradients go out in two buckets, each as soon as it is final:
+            # the critic's gradients + the minibatch's metric sums on the side stream once the actor's
+            # row tiles have produced their loss metrics (overlapping the actor's dW), then the actor's
+            # gradients on the main stream (overlapping the critic's optimiser step and repack).
+            split = self.max_grad_norm is None and os.environ.get("DPPO_SPLIT_UPDATE", "1") != "0"
             if split:
                 if getattr(self, "_side", None) is None:
                     self._side = torch.cuda.Stream(device=self.device)
                     self._met_dev = [torch.zeros(16, dtype=torch.float64, device=self.device) for _ in range(2)]
+                    self._ev_rows = torch.cuda.Event()
+                    self._ev_met = torch.cuda.Event()
                 side = self._side
                 side.wait_stream(stream)
                 na = m.n_actor
@@ -385,7 +439,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     rows = min(rows_local_full, total_local - start)
                     if rows <= 0:
                         break
-                    global_rows = rows * self.world_size
+                    global_rows = rows * W
                     stats = self._adv_all[update_epoch * num_batch + batch]
                     hp_ = self.host_profile
                     if hp_ is not None:
@@ -402,22 +456,37 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         met = self._met_dev[k % 2]
                         with torch.cuda.stream(side):
                             m.minibatch(*mb_args, **mb_kw, part=2, metrics=met)
-                            if not tagged:
+                            if not tagged and not dp:
                                 ev_c = torch.cuda.Event()
                                 ev_c.record(side)
-                        m.minibatch(*mb_args, **mb_kw, part=1, metrics=met)
-                        if not tagged:
-                            stream.wait_event(ev_c)
+                        if dp:
+                            ng = m.grads.numel()
+                            m.minibatch(*mb_args, **mb_kw, part=4, metrics=met)   # actor row tiles
+                            self._ev_rows.record(stream)
+                            with torch.cuda.stream(side):          # bucket 1: critic gradients + metrics
+                                side.wait_event(self._ev_rows)
+                                m.grads_ext[ng:ng + 5].copy_(met[:5])
+                                self._allreduce(m.grads_ext[na:])
+                                met[:5].copy_(m.grads_ext[ng:ng + 5])
+                                self._ev_met.record(side)
+                            m.minibatch(*mb_args, **mb_kw, part=5, metrics=met)   # actor dW + time MLP
+                            self._allreduce(m.grads_ext[:na])      # bucket 2: actor gradients
+                            stream.wait_event(self._ev_met)
+                        else:
+                            m.minibatch(*mb_args, **mb_kw, part=1, metrics=met)
+                            if not tagged:
+                                stream.wait_event(ev_c)
                     else:
                         m.minibatch(*mb_args, **mb_kw)
-                    if self.world_size > 1:                # one collective: gradients + metric sums
-                        ng = m.grads.numel()
-                        m.grads_ext[ng:ng + 5].copy_(m.metrics[:5])
-                        self._allreduce(m.grads_ext)
-                        m.metrics[:5].copy_(m.grads_ext[ng:ng + 5])
+                        if dp:                             # one collective: gradients + metric sums
+                            ng = m.grads.numel()
+                            m.grads_ext[ng:ng + 5].copy_(m.metrics[:5])
+                            self._allreduce(m.grads_ext)
+                            m.metrics[:5].copy_(m.grads_ext[ng:ng + 5])
                     if self.minibatch_hook is not None:
                         if split:
                             stream.wait_stream(side)
+                            m.metrics[:5].copy_(met[:5])   # the hook reads model.metrics
                         self.minibatch_hook(update_epoch, batch, start, rows)
                     if hp_ is not None:
                         t_h1 = time.perf_counter()

@@ -26,6 +26,17 @@ inline bool dppo_prec_2b(int p) { return p == DPPO_BF16 || p == DPPO_F16; }
 // backward seed scale of a precision (PolicyF16::GRAD_SCALE): the row tiles seed the backward pass
 // with this times the loss gradient; the weight-gradient outputs multiply by its inverse
 inline float dppo_grad_scale(int p) { return p == DPPO_F16 ? 4096.f : 1.f; }
+// the fp16 backward seed scale of a minibatch of global_rows rows: the largest power of two <=
+// min(4096, global_rows). The seed is scale / global_rows x the per-row loss gradient, so it never
+// exceeds the unscaled per-row gradient (a small minibatch with large value errors cannot overflow
+// fp16), and at the bench's 50,000 rows it is the full 4096 that keeps the per-row gradients
+// above fp16's subnormal range. A power of two: dividing it out of the fp32 dW is exact.
+inline float dppo_grad_scale_rows(int p, int64_t global_rows) {
+    if (p != DPPO_F16) return 1.f;
+    float s = 1.f;
+    while (s < 4096.f && (int64_t)(2.f * s) <= global_rows) s *= 2.f;
+    return s;
+}
 
 #define DPPO_CHECK(cond, ...) do { if (!(cond)) return dppo_set_error(DPPO_EINVAL, __VA_ARGS__); } while (0)
 #define DPPO_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return dppo_hip_fail(e_, #x); } while (0)

@@ -35,14 +35,14 @@ struct SampleArgs {
     MlpLayout L;          // same layout for base and ft
 };
 
-// This workgroup's 16 env rows of a TAGGED observation into st[16][SD]: every thread polls its
-// granules (system-scope relaxed loads of mapped host memory) until each carries a.cond_tag — the
+// This workgroup's R (16 or 32) env rows of a TAGGED observation into st[R][SD]: every thread polls
+// its granules (system-scope relaxed loads of mapped host memory) until each carries a.cond_tag — the
 // value arrives with its own ready flag, so there is no separate flag round trip. Bounded (4 s):
 // on timeout the step runs on what it read and (flag_timeout) sets bit 31 of *done.
-template <int ST>
+template <int ST, int R = 16>
 __device__ inline void sampler_load_state_tagged(const SampleArgs& a, int row0, float* st, bool flag_timeout, int tid) {
-    const int SD = a.SD, n = 16 * SD;
-    constexpr int NG = (16 * 64 + ST - 1) / ST;     // SD <= 64 (dppo_check_dims)
+    const int SD = a.SD, n = R * SD;
+    constexpr int NG = (R * 64 + ST - 1) / ST;      // SD <= 64 (dppo_check_dims)
     float v[NG];
     bool ok[NG];
 #pragma unroll
@@ -91,3 +91,5 @@ bool sample_split_supported(int precision, int H, int XD, int SD, int ks_in, int
 // or the P = 4 kernel's two member sets), 0 = not taken
 int split_members_for(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF);
 int sampler_device_cus();   // CUs of the current device (0 if unknown)
+// the split sampler's plan (dppo_sampler_plan): out[4] = kernel, members per set, sets, workgroups
+void split_plan_query(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF, int* out);

@@ -625,8 +625,29 @@ extern "C" int dppo_sampler_max_in_flight(const dppo_dims* d, int precision, int
         *launches = 8;
         return DPPO_OK;
     }
-    const int active = dppo_cdiv(n_envs, 16) * members, cus = sampler_device_cus();
+    Dims D;
+    dppo_check_dims(d, &D);
+    const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+    int plan[4];
+    split_plan_query(precision, D.H, D.XD, D.SD, L.ks_in, n_envs, D.K, D.KF, plan);
+    // the launch's own workgroup count (rounded as the launch rounds it), one per CU
+    const int active = plan[3] > 0 ? plan[3] : dppo_cdiv(n_envs, 16) * members, cus = sampler_device_cus();
     *launches = cus > 0 ? (cus / active > 0 ? cus / active : 1) : 1;
+    return DPPO_OK;
+}
+
+extern "C" int dppo_sampler_plan(const dppo_dims* d, int precision, int n_envs, int* plan) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(plan, "dppo_sampler_plan: null output");
+    const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+    if (sampler_cfg() == 'x') {
+        split_plan_query(precision, D.H, D.XD, D.SD, L.ks_in, n_envs, D.K, D.KF, plan);
+    } else {
+        plan[0] = plan[1] = plan[2] = plan[3] = 0;
+    }
+    if (plan[0] == 0) plan[3] = dppo_cdiv(n_envs, 16);
     return DPPO_OK;
 }
 

@@ -43,6 +43,7 @@
 // Block -> (group, member): members of a group share blockIdx % 8 (one XCD under the observed
 // round-robin placement: a speed choice only; correctness does not depend on placement).
 #include <mutex>
+#include <type_traits>
 #include <stdlib.h>
 #include <string.h>
 #include "dppo_common.cuh"
@@ -1222,6 +1223,496 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     XPHASE(10);
 }
 
+// =================================================================================================
+// The PAIR kernel (default at >= 32 envs for 2-byte operands when one member set holds one actor):
+// the folded 2-member split of sample_split4_kernel, with every member pair running TWO 16-env tiles
+// (A, B) half a denoising step apart. Per tile a step is a dependent chain
+//     in-Dense -> barrier -> l1 + fold -> barrier -> publish -> [cross-CU exchange] -> epilogue
+// whose exchange (an L2 round trip between the 2 CUs, ~0.6 us) left the MFMA pipes idle in the
+// one-tile kernel. Here one tile's exchange is in flight while the other tile's l1 runs on the
+// same resident weights, in four barrier intervals per step of both tiles:
+//     1: publish A(i)  ; in-Dense B(i)
+//     2: l1 B(i)       [first poll of A(i) issued half-way through its MFMAs] ; sweep + epilogue A(i)
+//     3: publish B(i)  ; in-Dense A(i+1)
+//     4: l1 A(i+1)     [first poll of B(i) half-way] ; sweep + epilogue B(i)
+// so each exchange overlaps (the other tile's in-Dense + a barrier + its l1). Twice the MFMAs per CU
+// per step against no exposed exchange: at 64 envs 8 CUs instead of 16 (4 pairs x 2 members, two
+// member sets). Numerics are the one-tile kernel's, operation for operation (same fragments, same
+// accumulation order, same fixed member order in the exchange sum): the actions are bit-identical.
+// Each member set holds one actor for the whole launch (dual sets, or K' = K / K' = 0).
+template <class Pol, int XQ, int KX, bool INJ>
+__global__ __launch_bounds__(512) void sample_pair_kernel(SplitArgs sa) {
+    constexpr int P = 2, SW = 8;
+    constexpr int NO = (4 * XQ + 15) / 16;
+    using AT = typename Pol::AT;
+    auto pack2 = [](float lo, float hi) { return Pol::pack2(lo, hi); };
+    constexpr int H = SPLIT_H, KSH = H / 32, HS = H / P;
+    constexpr int NTI = 32 / SW;           // in-Dense n-tiles per wave
+    constexpr int NL1 = (HS / 16) / SW;    // l1 n-tiles of the member slice per wave
+    constexpr int NR = NTI / P;            // in-Dense tiles per wave whose residual term this member adds
+    constexpr int NOC = 16 * NO, ST = SW * 64, pad = 16, ldh = H + pad, lda0 = KX * 32 + pad;
+    constexpr int XD = 4 * XQ, NV = 16 * XD, NVW = NV / SW, SL = 64 / P, KW = (NVW + SL - 1) / SL;
+    static_assert(KW <= P && NL1 * SW == HS / 16 && NTI % P == 0, "pair geometry");
+    constexpr int NB = H + NOC;
+    constexpr int L1D = DPPO_S4_L1D;
+
+    const SampleArgs& a = sa.a;
+    const int G2 = (sa.G + 1) >> 1;                       // member pairs (two 16-env tiles each)
+    const int per_set = 8 * P * ((G2 + 7) / 8);
+    const int set = sa.dual ? (int)blockIdx.x / per_set : 0;
+    const int b = (int)blockIdx.x - set * per_set;
+    const int g2 = (b / (8 * P)) * 8 + b % 8, c = (b / 8) % P;
+    if (g2 >= G2) return;                                 // whole workgroup: no barrier is skipped
+    const int GT = 2 * G2, GX = GT * (sa.dual ? 2 : 1);   // tile slots of the exchange regions
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const MlpLayout& L = a.L;
+    const int SD = a.SD, K = a.K, KF = a.KF;
+    const int KSX = packed_ksteps(XD + SD, 32);
+    const int i0 = sa.dual && set == 1 ? K - KF : 0, i1 = sa.dual && set == 0 ? K - KF : K;
+    const int NS = i1 - i0;
+    // the one actor of this set: dual -> set; otherwise K' = K (all fine-tuned) or K' = 0
+    const int FT = __builtin_amdgcn_readfirstlane(sa.dual ? set : (KF > 0 ? 1 : 0));
+    const int row00 = 32 * g2;
+
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    size_t o = 0;
+    AT* a0 = (AT*)(smem + o); o += dppo_align16(2 * 2 * 16 * lda0);        // [tile][16][lda0]
+    AT* u1 = (AT*)(smem + o); o += dppo_align16(2 * 2 * 16 * ldh);         // [tile][16][ldh]
+    float* part = (float*)(smem + o); o += dppo_align16(4 * 2 * SW * NV);  // [tile][wave][16 x XD]
+    int* xfail = (int*)(smem + o); o += 16;
+    float* xs = (float*)(smem + o); o += dppo_align16(4 * 2 * NV);         // [tile][16 x XD]
+    float* st = (float*)(smem + o); o += dppo_align16(4 * 32 * SD);
+    float* tin = (float*)(smem + o); o += dppo_align16((size_t)4 * NS * H); // this set's step rows
+    float* sch = (float*)(smem + o); o += dppo_align16(4 * K * DPPO_SCHED_COLS);
+    float* bias = (float*)(smem + o); o += dppo_align16(4 * NB);
+    float* zt = (float*)(smem + o); o += dppo_align16((size_t)4 * 2 * NS * NV);   // [tile][i - i0][NV]
+    u32x4* wxs = (u32x4*)(smem + o); o += (size_t)SW * NTI * KX * 1024;
+
+    // ---- the resident set of this set's actor ----
+    const __amdgpu_buffer_rsrc_t rs = packed_rsrc(FT ? a.packed_ft : a.packed_base);
+    const uint8_t* const PKD = FT ? a.packed_ft : a.packed_base;
+    auto W = [&](int seg) { return wsrc(rs, L.off[seg]); };
+    u32x4 rl1[NL1][KSH], rfold[NL1][NO], rres[NR][NO];
+#pragma unroll
+    for (int ks = 0; ks < KX; ++ks)
+#pragma unroll
+        for (int n = 0; n < NTI; ++n) {
+            const uint8_t* src = PKD + L.off[SEG_W_XS] + ((size_t)((NTI * wave + n) * KSX + ks) << 10) + 16 * lane;
+            __builtin_amdgcn_global_load_lds((void*)src, (__attribute__((address_space(3))) void*)(wxs + ((wave * NTI + n) * KX + ks) * 64),
+                                             16, 0, 0);
+        }
+#pragma unroll
+    for (int t = 0; t < NL1; ++t)
+#pragma unroll
+        for (int j = 0; j < KSH; ++j) rl1[t][j] = load_bfrag_c(W(SEG_W_L1), KSH, (HS / 16) * c + NL1 * wave + t, j, lane);
+#pragma unroll
+    for (int tt = 0; tt < NL1; ++tt)
+#pragma unroll
+        for (int n = 0; n < NO; ++n) rfold[tt][n] = load_bfrag_c(W(SEG_FOLD), NO, (HS / 16) * c + NL1 * wave + tt, n, lane);
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int n = 0; n < NO; ++n) rres[r][n] = load_bfrag_c(W(SEG_ROUT), NO, NTI * wave + r * P + c, n, lane);
+
+    // announce this member's XCD (one announcement per member pair)
+    uint64_t* const xann = sa.xbuf + XANN + (size_t)(g2 + set * G2) * P;
+    const uint32_t ann_tag = sa.seq << 6;
+    if (tid == 0)
+        __hip_atomic_store(xann + c, ((uint64_t)ann_tag << 32) | (uint32_t)xcc_id(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+
+    // ---- prologue: biases, this set's time rows, schedule, noise ----
+    for (int i4 = tid; i4 < NB / 4; i4 += ST) {
+        const int j = 4 * i4;
+        ((float4*)bias)[i4] = j < H ? *((const float4*)(PKD + L.off[SEG_B_L1]) + j / 4)
+                                    : *((const float4*)(PKD + L.off[SEG_B_OUT2]) + (j - H) / 4);
+    }
+    for (int i4 = tid; i4 < NS * H / 4; i4 += ST) {
+        const int r = 4 * i4 / H, t = K - 1 - (i0 + r);
+        ((float4*)tin)[i4] = ((const float4*)(PKD + L.off[SEG_TIN]))[t * (H / 4) + i4 % (H / 4)];
+    }
+    for (int i = tid; i < K; i += ST) {
+        const float* sc = a.sched + (K - 1 - i) * DPPO_SCHED_COLS;
+        float sd = expf(0.5f * sc[4]);
+        if (a.deterministic && sc[6] != 0.f) sd = 0.f;
+        else if (a.deterministic) sd = fminf(fmaxf(sd, sc[5]), 1e6f);
+        else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
+        float* e = sch + i * DPPO_SCHED_COLS;
+        e[0] = sc[0]; e[1] = sc[1]; e[2] = sc[2]; e[3] = sc[3]; e[4] = sd;
+    }
+    const int XG = (XD + 3) / 4;
+    const bool need_xT = !(sa.dual && set == 1);
+    for (int it = tid; it < (NS + 1) * 32 * XG; it += ST) {
+        const int si = it / (32 * XG), rr = (it / XG) % 32, gq = it % XG, row = row00 + rr;
+        const int step = si < NS ? i0 + si : K;          // si == NS: x_T (slot K)
+        if (step == K && !need_xT) continue;
+        float z[4];
+        if (step == K && a.x_T) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z[k] = (row < a.E && 4 * gq + k < XD) ? a.x_T[(size_t)row * XD + 4 * gq + k] : 0.f;
+        } else if (INJ && step < K) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                z[k] = (row < a.E && 4 * gq + k < XD) ? a.noise[((size_t)step * a.E + row) * XD + 4 * gq + k] : 0.f;
+        } else {
+            philox_normal4(a.seed, (uint32_t)gq, (uint32_t)(a.env_offset + row), (uint32_t)step, a.call_id, z);
+        }
+        const int tau = rr >> 4, r = rr & 15;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = 4 * gq + k;
+            if (q >= XD) break;
+            if (step < K) {
+                zt[(tau * NS + si) * NV + r * XD + q] = fminf(fmaxf(z[k], -a.randn_clip), a.randn_clip);
+            } else {
+                xs[tau * NV + r * XD + q] = z[k];
+                if (KF == K && c == 0 && a.chains && row < a.E) store_out(a.chains + ((size_t)row * (KF + 1) + 0) * XD + q, z[k]);
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);                     // vmcnt(0): the resident set has landed
+    if (wave == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
+        uint64_t v = ((uint64_t)ann_tag << 32);
+        bool ok = false;
+        for (;;) {
+            if (lane < P) v = __hip_atomic_load(xann + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__all(lane >= P || (uint32_t)(v >> 32) == ann_tag)) { ok = true; break; }
+            if (__builtin_amdgcn_s_memrealtime() > t_end) break;
+        }
+        const int x0 = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        const bool one_xcd = ok && !sa.force_shared && __all(lane >= P || (int)(uint32_t)v == x0);
+        if (lane == 0) xfail[1] = one_xcd ? 1 + x0 : 0;
+    }
+    __syncthreads();
+    constexpr int k1w = KX * 32;
+    for (int idx = tid; idx < 2 * 16 * k1w; idx += ST) {
+        const int rr = idx / k1w, cc = idx % k1w, tau = rr >> 4, r = rr & 15;
+        if (cc >= XD && cc < XD + SD) continue;              // state columns: after the wait
+        a0[(tau * 16 + r) * lda0 + cc] = Pol::cvt(cc < XD ? xs[tau * NV + r * XD + cc] : 0.f);
+    }
+    if (tid == 0) *xfail = 0;
+    if (a.cond_tagged) {
+        sampler_load_state_tagged<ST, 32>(a, row00, st, c == 0, tid);
+        for (int i = tid; i < 32 * SD; i += ST) {
+            const int rr = i / SD, cc = i % SD, row = row00 + rr;
+            a0[rr * lda0 + XD + cc] = Pol::cvt(st[i]);
+            if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, st[i]);
+        }
+    } else {
+        if (a.go) {
+            if (tid == 0) {
+                const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;   // 100 MHz: 4 s
+                while (__hip_atomic_load(a.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.go_value) {
+                    __builtin_amdgcn_s_sleep(8);
+                    if (__builtin_amdgcn_s_memrealtime() > t_end) {
+                        if (c == 0) __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            }
+            __syncthreads();
+        }
+        for (int i = tid; i < 32 * SD; i += ST) {
+            const int rr = i / SD, cc = i % SD, row = row00 + rr;
+            const float v = row < a.E ? a.cond[(size_t)row * SD + cc] : 0.f;
+            st[i] = v;
+            a0[rr * lda0 + XD + cc] = Pol::cvt(v);
+            if (a.cond_out && c == 0 && row < a.E) store_out(a.cond_out + (size_t)row * SD + cc, v);
+        }
+    }
+    __syncthreads();
+    const uint32_t htag = (sa.seq << 6) | 63u;
+    uint64_t* const xh = sa.xbuf + XHOFF + (size_t)(2 * g2) * XMAX_NV;   // [tile][XMAX_NV]
+    if (sa.dual && set == 1) {
+        if (tid < 2 * NV) {
+            const int tau = tid / NV, v0 = tid % NV;
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 500000000ull;   // 5 s
+            uint64_t v;
+            bool ok = true;
+            for (;;) {
+                v = __hip_atomic_load(xh + tau * XMAX_NV + v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)(v >> 32) == htag) break;
+                if (__builtin_amdgcn_s_memrealtime() > t_end) { ok = false; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            xs[tid] = ok ? __uint_as_float((uint32_t)v) : __builtin_nanf("");
+            if (!ok) {
+                *xfail = 1;
+                __hip_atomic_store(sa.xfail_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        __syncthreads();
+        for (int idx = tid; idx < 2 * NV; idx += ST) {
+            const int tau = idx / NV, v0 = idx % NV;
+            a0[(tau * 16 + v0 / XD) * lda0 + v0 % XD] = Pol::cvt(xs[idx]);
+        }
+        __syncthreads();
+    }
+
+    const int env = lane & 15, jq = lane >> 4;
+    const int xmode = __builtin_amdgcn_readfirstlane(xfail[1]);
+    uint64_t* const xregion = sa.xbuf + (size_t)xmode * XREGION;
+    const int xm = lane & (P - 1), xsl = lane / P;
+    const bool fin = xm < KW && xsl + SL * xm < NVW;
+    const int ve = wave * NVW + (fin ? xsl + SL * xm : 0), re = ve / XD, qe = ve % XD;
+    const int vw = wave * NVW;
+    const float be = bias[H + qe];
+    f32x4 po[2][NO];
+
+    // ---- the phases of one tile (tau compile-time: po[] stays in registers) ----
+    auto in_dense = [&](auto tauc, int i) {
+        constexpr int tau = decltype(tauc)::value;
+        const AT* A0 = a0 + tau * 16 * lda0;
+        AT* U1 = u1 + tau * 16 * ldh;
+        f32x4 h1[NTI];
+        u32x4 af[KX], wf[KX][NTI];
+#pragma unroll
+        for (int ks = 0; ks < KX; ++ks) af[ks] = lds_afrag<Pol>(A0, lda0, 0, ks, lane);
+#pragma unroll
+        for (int n = 0; n < NTI; ++n) h1[n] = *(const f32x4*)(tin + (i - i0) * H + 16 * (NTI * wave + n) + 4 * jq);
+#pragma unroll
+        for (int ks = 0; ks < KX; ++ks)
+#pragma unroll
+            for (int n = 0; n < NTI; ++n) wf[ks][n] = wxs[((wave * NTI + n) * KX + ks) * 64 + lane];
+        asm volatile("" ::"v"(af[0]), "v"(h1[0]), "v"(h1[1]), "v"(h1[2]), "v"(h1[3]), "v"(wf[0][0]), "v"(wf[0][1]),
+                     "v"(wf[0][2]), "v"(wf[0][3]));
+        if constexpr (KX == 2)
+            asm volatile("" ::"v"(af[KX - 1]), "v"(wf[KX - 1][0]), "v"(wf[KX - 1][1]), "v"(wf[KX - 1][2]), "v"(wf[KX - 1][3]));
+#pragma unroll
+        for (int ks = 0; ks < KX; ++ks)
+#pragma unroll
+            for (int n = 0; n < NTI; ++n) h1[n] = Pol::mma(wf[ks][n], af[ks], h1[n]);
+#pragma unroll
+        for (int n = 0; n < NTI; ++n) {
+            const int f = 16 * (NTI * wave + n) + 4 * jq;
+            u32x2 pk;
+            pk[0] = pack2(relu_f(h1[n][0]), relu_f(h1[n][1]));
+            pk[1] = pack2(relu_f(h1[n][2]), relu_f(h1[n][3]));
+            *(u32x2*)(U1 + env * ldh + f) = pk;
+        }
+#pragma unroll
+        for (int n = 0; n < NO; ++n) zero_acc(po[tau][n]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            f32x4 hv = h1[r * P];
+            if (c == 1) hv = h1[r * P + 1];
+            u32x4 bh;
+            bh[0] = pack2(hv[0], hv[1]);
+            bh[1] = pack2(hv[2], hv[3]);
+            bh[2] = pack2(hv[0] - Pol::lo2f(bh[0]), hv[1] - Pol::hi2f(bh[0]));
+            bh[3] = pack2(hv[2] - Pol::lo2f(bh[1]), hv[3] - Pol::hi2f(bh[1]));
+#pragma unroll
+            for (int n = 0; n < NO; ++n) po[tau][n] = Pol::mma(rres[r][n], bh, po[tau][n]);
+        }
+    };
+    // the tile's exchange granules of step i: [slot i & 1][tile][member][NV]
+    auto xslot = [&](int tau, int i) {
+        return xregion + ((size_t)((i & 1) * GX + set * GT + 2 * g2 + tau) * P) * NV;
+    };
+    // l1 + fold of tile tau; the first poll of tile pt's exchange (step pi) is issued half-way
+    // through the MFMA chain (pt < 0: none) and returned in xa
+    auto l1_fold = [&](auto tauc, auto ptc, int pi, uint64_t (&xa)[KW]) {
+        constexpr int tau = decltype(tauc)::value, pt = decltype(ptc)::value;
+        const AT* U1 = u1 + tau * 16 * ldh;
+        f32x4 acc[NL1];
+#pragma unroll
+        for (int tt = 0; tt < NL1; ++tt) acc[tt] = *(const f32x4*)(bias + HS * c + 16 * (NL1 * wave + tt) + 4 * jq);
+        u32x4 fb[KSH];
+#pragma unroll
+        for (int j = 0; j < KSH; ++j) fb[j] = lds_afrag<Pol>(U1, ldh, 0, j, lane);
+        if constexpr (pt >= 0) {
+            const uint64_t* src = xslot(pt, pi) + (size_t)xm * NV + vw;
+#pragma unroll
+            for (int k = 0; k < KW; ++k) {
+                const int v = xsl + SL * k < NVW ? xsl + SL * k : NVW - 1;
+                xa[k] = __hip_atomic_load(src + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < KSH; ++j)
+#pragma unroll
+            for (int tt = 0; tt < NL1; ++tt) acc[tt] = Pol::mma(rl1[tt][j], fb[j], acc[tt]);
+        __builtin_amdgcn_sched_group_barrier(0x100, L1D + NL1, 0);
+#pragma unroll
+        for (int j = 0; j < KSH - L1D; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, NL1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            if (pt >= 0 && j == (KSH - L1D) / 2) __builtin_amdgcn_sched_group_barrier(0x020, KW, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NL1 * L1D, 0);
+#pragma unroll
+        for (int tt = 0; tt < NL1; ++tt) {
+            u32x4 ba;
+            ba[0] = pack2(relu_f(acc[tt][0]), relu_f(acc[tt][1]));
+            ba[1] = pack2(relu_f(acc[tt][2]), relu_f(acc[tt][3]));
+            ba[2] = ba[0];
+            ba[3] = ba[1];
+#pragma unroll
+            for (int n = 0; n < NO; ++n) po[tau][n] = Pol::mma(rfold[tt][n], ba, po[tau][n]);
+        }
+        float* PT = part + tau * SW * NV;
+#pragma unroll
+        for (int n = 0; n < NO; ++n)
+            if (16 * n + 4 * jq < XD) *(f32x4*)(PT + wave * NV + env * XD + 16 * n + 4 * jq) = po[tau][n];
+    };
+    auto publish = [&](int tau, int i) {
+        const uint32_t tag = (sa.seq << 6) | (uint32_t)(i + 1);
+        uint64_t* xb = xslot(tau, i);
+        if (lane < NVW) {
+            const float* PT = part + tau * SW * NV;
+            float pp[SW];
+#pragma unroll
+            for (int w = 0; w < SW; ++w) pp[w] = PT[w * NV + vw + lane];
+            asm volatile("" ::"v"(pp[0]), "v"(pp[1]), "v"(pp[2]), "v"(pp[3]), "v"(pp[4]), "v"(pp[5]), "v"(pp[6]), "v"(pp[7]));
+            float sum = pp[0];
+#pragma unroll
+            for (int w = 1; w < SW; ++w) sum += pp[w];
+            const uint64_t gr = ((uint64_t)tag << 32) | __float_as_uint(sum);
+            if (xmode)
+                __hip_atomic_store(xb + (size_t)c * NV + vw + lane, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else
+                __hip_atomic_store(xb + (size_t)c * NV + vw + lane, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    // finish tile tau's exchange of step i (xa: the first poll, already issued) and run its epilogue
+    auto sweep_epilogue = [&](int tau, int i, uint64_t (&xa)[KW]) {
+        const uint32_t tag = (sa.seq << 6) | (uint32_t)(i + 1);
+        const uint64_t* src = xslot(tau, i) + (size_t)xm * NV + vw;
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
+        bool failed = false;
+        for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < KW; ++k) ok &= (uint32_t)(xa[k] >> 32) == tag;
+            if (__all(ok)) break;
+            if (__builtin_amdgcn_s_memrealtime() > t_end) {
+                failed = true;
+                if (lane == 0) {
+                    *xfail = 1;
+                    __hip_atomic_store(sa.xfail_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                break;
+            }
+#pragma unroll
+            for (int k = 0; k < KW; ++k) {
+                const int v = xsl + SL * k < NVW ? xsl + SL * k : NVW - 1;
+                xa[k] = __hip_atomic_load(src + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        float val[KW];
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            val[k] = __uint_as_float((uint32_t)xa[k]);
+            val[k] += dpp_f32<0xB1>(val[k]);                // member sum: quad_perm [1,0,3,2]
+        }
+        if (fin) {
+            const int t = K - 1 - i;
+            const f32x4 ec = *(const f32x4*)(sch + i * DPPO_SCHED_COLS);
+            const float sd = sch[i * DPPO_SCHED_COLS + 4];
+            float* XS = xs + tau * NV;
+            const float x = XS[ve], ze = zt[(tau * NS + (i - i0)) * NV + ve];
+            float ep = val[0];
+#pragma unroll
+            for (int k = 1; k < KW; ++k) ep = xm == k ? val[k] : ep;
+            ep += be;
+            float xr = ec[0] * x - ec[1] * ep;                   // x0 reconstruction (:198-201)
+            xr = fminf(fmaxf(xr, -1.f), 1.f);                    // denoised_clip_value = 1 (diffusion.py:28)
+            const float mu = ec[2] * xr + ec[3] * x;             // posterior mean (:239-242)
+            float y = mu + sd * ze;                              // (:301-320)
+            if (a.final_clip > 0.f && i == K - 1) y = fminf(fmaxf(y, -a.final_clip), a.final_clip);
+            if (failed) y = __builtin_nanf("");
+            XS[ve] = y;
+            a0[(tau * 16 + re) * lda0 + qe] = Pol::cvt(y);
+            // the row and its output addresses are rebuilt here every step: hoisted out of the step
+            // loop, eight 64-bit addresses stayed live across it and spilled to scratch
+            int row = row00 + 16 * tau + re;
+            asm volatile("" : "+v"(row));
+            if (c == 0 && row < a.E) {
+                if (a.chains && t <= KF) store_out(a.chains + ((size_t)row * (KF + 1) + (KF - t)) * XD + qe, y);
+                if (i == K - 1) {
+                    store_out(a.actions + (size_t)row * XD + qe, y);
+                    if (a.actions_tagged)
+                        __hip_atomic_store(a.actions_tagged + (size_t)row * XD + qe,
+                                           ((uint64_t)a.cond_tag << 32) | __float_as_uint(y), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    else if (a.actions_host) a.actions_host[(size_t)row * XD + qe] = y;
+                }
+            }
+        }
+    };
+    using T0 = std::integral_constant<int, 0>;
+    using T1 = std::integral_constant<int, 1>;
+    using TN = std::integral_constant<int, -1>;
+    uint64_t xaA[KW], xaB[KW];
+#pragma unroll
+    for (int k = 0; k < KW; ++k) xaA[k] = xaB[k] = 0;
+
+    in_dense(T0{}, i0);
+    lds_sync();
+    l1_fold(T0{}, TN{}, 0, xaB);
+    lds_sync();
+    for (int i = i0; i < i1; ++i) {
+        const bool more = i + 1 < i1;
+        publish(0, i);                       // 1: publish A(i) ; in-Dense B(i)
+        in_dense(T1{}, i);
+        lds_sync();
+        l1_fold(T1{}, T0{}, i, xaA);         // 2: l1 B(i) [poll A(i)] ; epilogue A(i)
+        sweep_epilogue(0, i, xaA);
+        lds_sync();
+        publish(1, i);                       // 3: publish B(i) ; in-Dense A(i+1)
+        if (more) in_dense(T0{}, i + 1);
+        lds_sync();
+        if (more) {                          // 4: l1 A(i+1) [poll B(i)] ; epilogue B(i)
+            l1_fold(T0{}, T1{}, i, xaB);
+        } else {
+            const uint64_t* src = xslot(1, i) + (size_t)xm * NV + vw;
+#pragma unroll
+            for (int k = 0; k < KW; ++k) {
+                const int v = xsl + SL * k < NVW ? xsl + SL * k : NVW - 1;
+                xaB[k] = __hip_atomic_load(src + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        sweep_epilogue(1, i, xaB);
+        lds_sync();
+    }
+    const int nreal = (row00 < a.E ? 1 : 0) + (row00 + 16 < a.E ? 1 : 0);   // 16-env tiles with envs
+    if (sa.dual && set == 0) {
+        if (c == 0 && tid < 2 * NV)
+            __hip_atomic_store(xh + (tid / NV) * XMAX_NV + tid % NV, ((uint64_t)htag << 32) | __float_as_uint(xs[tid]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c == 0 && tid == 0 && a.done && *xfail)
+            __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    if (c == 0 && a.done) {
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) {
+            if (*xfail) __hip_atomic_fetch_or(a.done, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_fetch_add(a.done, (uint32_t)nreal, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+size_t pair_lds_bytes(int XD, int SD, int K, int NS, int KX, int NO) {
+    const int pad = 16, ldh = SPLIT_H + pad, lda0 = KX * 32 + pad, NV = 16 * XD;
+    size_t o = 0;
+    o += dppo_align16(2 * 2 * 16 * lda0);
+    o += dppo_align16(2 * 2 * 16 * ldh);
+    o += dppo_align16(4 * 2 * 8 * NV);
+    o += 16;
+    o += dppo_align16(4 * 2 * NV);
+    o += dppo_align16(4 * 32 * SD);
+    o += dppo_align16((size_t)4 * NS * SPLIT_H);
+    o += dppo_align16(4 * K * DPPO_SCHED_COLS);
+    o += dppo_align16(4 * (SPLIT_H + 16 * NO));
+    o += dppo_align16((size_t)4 * 2 * NS * NV);
+    o += (size_t)32 * KX * 1024;
+    return o;
+}
+
 size_t split4_lds_bytes(int XD, int SD, int K, int KX, int NO, int sw) {
     const int pad = 16, ldh = SPLIT_H + pad, lda0 = KX * 32 + pad;
     size_t o = 0;
@@ -1296,8 +1787,18 @@ int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq, uint32_t** fail_dev) 
             *fail_dev = g_xb[i].fail_dev;
             return DPPO_OK;
         }
-    if (g_nxb == 16) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler: more than 16 streams");
-    XchgBuf& x = g_xb[g_nxb];
+    int slot = g_nxb;
+    if (g_nxb == 16) {
+        // every slot holds another stream (a process that made many rollout pipes): reuse the slots
+        // round robin once the device is idle; the evicted stream's next launch gets a fresh buffer
+        static int next_evict = 0;
+        slot = next_evict;
+        next_evict = (next_evict + 1) % 16;
+        DPPO_HIP(hipDeviceSynchronize());
+        DPPO_HIP(hipFree(g_xb[slot].buf));
+        DPPO_HIP(hipHostFree(g_xb[slot].fail_host));
+    }
+    XchgBuf& x = g_xb[slot];
     const size_t n = XTOTAL;
     DPPO_HIP(hipMalloc((void**)&x.buf, sizeof(uint64_t) * n));
     DPPO_HIP(hipHostMalloc((void**)&x.fail_host, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
@@ -1307,7 +1808,7 @@ int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq, uint32_t** fail_dev) 
     hipLaunchKernelGGL(xchg_zero_kernel, dim3(1024), dim3(256), 0, s, x.buf, n);
     DPPO_HIP(hipGetLastError());
     x.stream = s; x.device = dev; x.seq = 1;
-    ++g_nxb;
+    if (slot == g_nxb) ++g_nxb;
     *buf = x.buf;
     *seq = x.seq;
     *fail_dev = x.fail_dev;
@@ -1359,6 +1860,25 @@ int launch_split4_kw(const SplitArgs& sa, hipStream_t s) {
     return DPPO_OK;
 }
 
+// the pair kernel's instantiated shapes: hopper dims (XD = 12, XD + SD <= 32)
+constexpr bool pair_shape_ok(int XD, int KX) { return XD == 12 && KX == 1; }
+
+template <class Pol, int XQ, int KX, bool INJ>
+int launch_pair_k(const SplitArgs& sa, hipStream_t s) {
+    constexpr int NO = (4 * XQ + 15) / 16;
+    auto k = sample_pair_kernel<Pol, XQ, KX, INJ>;
+    const SampleArgs& a = sa.a;
+    const int NS = sa.dual ? (a.K - a.KF > a.KF ? a.K - a.KF : a.KF) : a.K;
+    const size_t lds = pair_lds_bytes(a.XD, a.SD, a.K, NS, KX, NO);
+    if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "pair sampler needs %zu B of LDS", lds);
+    DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int G2 = (sa.G + 1) / 2;
+    const int blocks = 8 * 2 * ((G2 + 7) / 8) * (sa.dual ? 2 : 1);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, s, sa);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
 // members per group of the folded kernel: 2 (default: 47.2 us per bench launch), or 4 with
 // -DDPPO_S4_P=4 (50.4 us; same box, tools/ab_variants.sh) — a build-time A/B knob
 #ifndef DPPO_S4_P
@@ -1381,27 +1901,42 @@ int split_p_choice() {
 }
 
 
-// the split sampler's plan for a shape: P members per 16-env group (4 or 8; 0 = not taken) and
-// whether the P = 4 kernel runs its two actors on two member sets (dual)
-struct SplitPlan { int P; bool dual; };
+// the split sampler's plan for a shape: P members per 16-env group (2, 4 or 8; 0 = not taken),
+// whether the two actors run on two member sets (dual), and whether each member pair runs two
+// 16-env tiles (the pair kernel); blocks = workgroups of one launch
+struct SplitPlan { int P; bool dual; bool pair; int blocks; };
 
 SplitPlan split_plan(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF) {
-    if (!dppo_prec_2b(precision) || H != SPLIT_H || XD % 4 != 0 || XD > 32 || K > 62) return {0, false};
+    if (!dppo_prec_2b(precision) || H != SPLIT_H || XD % 4 != 0 || XD > 32 || K > 62) return {0, false, false, 0};
     const int G = dppo_cdiv(E, 16);
-    if (G < 1 || G > XMAX_G) return {0, false};
+    if (G < 1 || G > XMAX_G) return {0, false, false, 0};
     const int cus = device_cus();
     // every workgroup of the launch co-resident (one per CU: the register budget)
-    auto fits = [&](int P, int sets) { return cus == 0 || sets * 8 * P * ((G + 7) / 8) <= cus; };
+    auto fits = [&](int P, int sets, int groups) { return cus == 0 || sets * 8 * P * ((groups + 7) / 8) <= cus; };
     const int KX = dppo_cdiv(XD + SD, 32);
     const bool p4 = KX <= 2 && split4_lds_bytes(XD, SD, K, KX, dppo_cdiv(XD, 16), split_waves()) <= 160 * 1024 &&
-                    fits(S4P, 1);
-    const bool p8 = ks_in == 2 && fits(8, 1);
+                    fits(S4P, 1, G);
+    const bool p8 = ks_in == 2 && fits(8, 1, G);
     static const bool dual_on = [] { const char* e = getenv("DPPO_SPLIT_DUAL"); return !e || atoi(e) != 0; }();
     // two sets only while two launches of them still fit side by side (the pipelined rollout keeps
     // the next step's launch resident while this one runs)
     const bool dual = dual_on && KF > 0 && KF < K && (cus == 0 || 2 * 2 * 8 * S4P * ((G + 7) / 8) <= cus);
-    if (split_p_choice() == 8) return p8 ? SplitPlan{8, false} : (p4 ? SplitPlan{S4P, dual} : SplitPlan{0, false});
-    return p4 ? SplitPlan{S4P, dual} : (p8 ? SplitPlan{8, false} : SplitPlan{0, false});
+    // the pair kernel: two tiles per member pair; each member set must hold one actor
+    // opt-in (DPPO_SPLIT_PAIR=1): bit-identical, but measured SLOWER at 64 envs (70.0 vs 47.4 us per
+    // launch, tools/r03_pair.sh): the exchange is hidden, everything else in a tile's step adds up
+    static const bool pair_on = [] { const char* e = getenv("DPPO_SPLIT_PAIR"); return e && atoi(e) != 0; }();
+    const int G2 = (G + 1) / 2;
+    const bool pdual = dual_on && KF > 0 && KF < K && (cus == 0 || 2 * 2 * 8 * 2 * ((G2 + 7) / 8) <= cus);
+    const int NS = pdual ? (K - KF > KF ? K - KF : KF) : K;
+    const bool pair = pair_on && S4P == 2 && G >= 2 && pair_shape_ok(XD, KX) && (pdual || KF == K || KF == 0) &&
+                      pair_lds_bytes(XD, SD, K, NS, KX, dppo_cdiv(XD, 16)) <= 160 * 1024 && fits(2, pdual ? 2 : 1, G2);
+    auto blocks = [&](int P, bool d2, int groups) { return 8 * P * ((groups + 7) / 8) * (d2 ? 2 : 1); };
+    if (split_p_choice() == 8)
+        return p8 ? SplitPlan{8, false, false, blocks(8, false, G)}
+                  : (p4 ? SplitPlan{S4P, dual, false, blocks(S4P, dual, G)} : SplitPlan{0, false, false, 0});
+    if (pair) return SplitPlan{2, pdual, true, blocks(2, pdual, G2)};
+    return p4 ? SplitPlan{S4P, dual, false, blocks(S4P, dual, G)}
+              : (p8 ? SplitPlan{8, false, false, blocks(8, false, G)} : SplitPlan{0, false, false, 0});
 }
 
 }  // namespace
@@ -1409,6 +1944,16 @@ SplitPlan split_plan(int precision, int H, int XD, int SD, int ks_in, int E, int
 int split_members_for(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF) {
     const SplitPlan p = split_plan(precision, H, XD, SD, ks_in, E, K, KF);
     return p.P * (p.dual ? 2 : 1);
+}
+
+// dppo_sampler_plan's fields: kernel (0 weight streaming, 1 split P = 8, 2 folded split, one tile per
+// group, 3 pair), members P per set, member sets, workgroups per launch
+void split_plan_query(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF, int* out) {
+    const SplitPlan p = split_plan(precision, H, XD, SD, ks_in, E, K, KF);
+    out[0] = p.P == 0 ? 0 : (p.pair ? 3 : (p.P == 8 ? 1 : 2));
+    out[1] = p.P;
+    out[2] = p.P ? (p.dual ? 2 : 1) : 0;
+    out[3] = p.blocks;
 }
 
 bool sample_split_supported(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF) {
@@ -1434,6 +1979,10 @@ int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s) {
     if (rc) return rc;
     const bool inj = a.noise != nullptr;
     const bool f16 = precision == DPPO_F16;
+    if (plan.pair) {
+        if (f16) return inj ? launch_pair_k<PolicyF16, 3, 1, true>(sa, s) : launch_pair_k<PolicyF16, 3, 1, false>(sa, s);
+        return inj ? launch_pair_k<PolicyBF16, 3, 1, true>(sa, s) : launch_pair_k<PolicyBF16, 3, 1, false>(sa, s);
+    }
     if (P == S4P) {
         const bool kx2 = a.XD + a.SD > 32;
         switch (a.XD / 4) {

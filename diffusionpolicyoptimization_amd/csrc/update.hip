@@ -534,7 +534,16 @@ static uint32_t* crit_count_scratch(int64_t nsamp, hipStream_t s) {
     if (!e)
         for (auto& x : ents)
             if (!x.p) { e = &x; break; }
-    if (!e) return nullptr;
+    if (!e) {
+        // every slot holds another (device, stream): a process that made many agents (one side stream
+        // each). Reuse the slots round robin; the evicted buffer is freed after the device is idle
+        thread_local int next = 0;
+        e = &ents[next];
+        next = (next + 1) % 16;
+        if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+        (void)hipFree(e->p);
+        e->p = nullptr;
+    }
     if (e->p && e->cap >= nsamp) return e->p;
     if (e->p) {
         if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
@@ -805,8 +814,9 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     const FlatOffsets FC = make_flat_offsets(D.SD, D.HC, 1, 0);
     float* ga = grads;
     float* gc = grads + FA.count;
-    DPPO_CHECK(parts >= 1 && parts <= 3, "dppo_ppo_minibatch: bad part %d", parts);
-    DPPO_CHECK(parts == 3 || adv_stats || parts == 2, "dppo_ppo_minibatch_part: the actor half needs adv_stats");
+    DPPO_CHECK(parts >= 1 && parts <= 5, "dppo_ppo_minibatch: bad part %d", parts);
+    DPPO_CHECK(parts == 3 || adv_stats || parts == 2 || parts == 5,
+               "dppo_ppo_minibatch_part: the actor half needs adv_stats");
     // one launch zeroes the atomically accumulated outputs of the half (or whole) being run:
     // gradients, metrics (actor: 0, 2..15; critic: 1), bucket sums, stats
     ZeroArgs z = {};
@@ -815,25 +825,27 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
         z.p[2] = ws.gseg; z.n[2] = (size_t)16 * D.H * sizeof(float);
         z.p[3] = ws.stats; z.n[3] = 4 * sizeof(double);
-    } else if (parts == 1) {
+    } else if (parts == 1 || parts == 4) {
         z.p[0] = grads; z.n[0] = FA.count * sizeof(float);
         z.p[1] = metrics; z.n[1] = sizeof(double);
         z.p[2] = metrics + 2; z.n[2] = 14 * sizeof(double);
         z.p[3] = ws.gseg; z.n[3] = (size_t)16 * D.H * sizeof(float);
-    } else {
+    } else if (parts == 2) {
         z.p[0] = grads + FA.count; z.n[0] = FC.count * sizeof(float);
         z.p[1] = metrics + 1; z.n[1] = sizeof(double);
     }
     // few workgroups: the split update runs this while the other stream's row tiles hold most CUs,
     // and a 256-block grid waited ~25 us for slots (DPPO_ZERO_BLOCKS: measurement knob)
     static const int zero_blocks = [] { const char* e = getenv("DPPO_ZERO_BLOCKS"); return e ? atoi(e) : 16; }();
-    hipLaunchKernelGGL(zero_kernel, dim3(zero_blocks > 0 ? zero_blocks : 16), dim3(256), 0, s, z);
-    DPPO_HIP(hipGetLastError());
+    if (parts != 5) {      // part 5 continues the actor half whose part 4 zeroed its outputs
+        hipLaunchKernelGGL(zero_kernel, dim3(zero_blocks > 0 ? zero_blocks : 16), dim3(256), 0, s, z);
+        DPPO_HIP(hipGetLastError());
+    }
     DPPO_CHECK((uint64_t)total < ((uint64_t)1 << 32), "dppo_ppo_minibatch: %lld samples x steps exceed 2^32",
                (long long)total);
     const FeistelKey fk = feistel_key((uint64_t)total, perm_seed, epoch);
     const double* stats = adv_stats;
-    if (!stats && parts != 2) {
+    if (!stats && parts != 2 && parts != 5) {
         const int blocks = dppo_cdiv(rows, 256) < 512 ? dppo_cdiv(rows, 256) : 512;
         hipLaunchKernelGGL(adv_stats_kernel, dim3(blocks), dim3(256), 0, s, advantages, fk, D.KF, start, rows,
                            row_index, ws.stats);
@@ -846,7 +858,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     lh.min_lp_std = hp->min_logprob_std; lh.vf_coef = hp->vf_coef; lh.norm_adv = hp->norm_adv;
     lh.reward_horizon = hp->reward_horizon;
     // fp16: the backward images carry GRAD_SCALE x the gradient (fp16 range); dW divides it out
-    lh.grad_scale = hp->loss_scale / (float)hp->global_rows * dppo_grad_scale(precision);
+    const float gscale = dppo_grad_scale_rows(precision, hp->global_rows);
+    lh.grad_scale = hp->loss_scale / (float)hp->global_rows * gscale;
 
     ActorArgs aa = {};
     aa.packed = (const uint8_t*)packed_ft;
@@ -890,7 +903,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         }
         w.ldm = ws.ldm;
         w.seg = ws.seg;
-        w.out_scale = 1.f / dppo_grad_scale(precision);
+        w.out_scale = 1.f / gscale;
         const int tiles = w.tile_start[w.nprob];
         // about one workgroup per CU, but no chunk under 768 rows: at small minibatches (6,250 rows,
         // an 8-GPU rank's share) thinner chunks cost more in partial-tile atomics than they gain
@@ -935,9 +948,12 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         return launch_grads(false, s);
     }
-    if (parts == 1) {                                  // the actor's half on the caller's stream
-        rc = launch_actor_rowtile(aa, precision, s);
-        if (rc) return rc;
+    if (parts == 1 || parts == 4 || parts == 5) {      // the actor's half (or its row tiles / its
+        if (parts != 5) {                              // weight gradients) on the caller's stream
+            rc = launch_actor_rowtile(aa, precision, s);
+            if (rc) return rc;
+        }
+        if (parts == 4) return DPPO_OK;
         rc = launch_grads(true, s);
         if (rc) return rc;
         return launch_time_bwd(D, ws.gseg, actor_params, ga, D.KF, D.TS, s);
@@ -989,7 +1005,8 @@ extern "C" int dppo_ppo_minibatch_part(const dppo_dims* d, int precision, const 
                                        int64_t total, uint64_t perm_seed, int epoch, int64_t start, int rows,
                                        const int64_t* row_index, const double* adv_stats, void* workspace,
                                        float* grads, double* metrics, int part, void* stream) {
-    DPPO_CHECK(part == 1 || part == 2, "dppo_ppo_minibatch_part: part must be 1 (actor) or 2 (critic)");
+    DPPO_CHECK(part == 1 || part == 2 || part == 4 || part == 5,
+               "dppo_ppo_minibatch_part: part must be 1 (actor), 2 (critic), 4 (actor row tiles) or 5 (actor dW)");
     return ppo_minibatch_impl(d, precision, hp, packed_ft, packed_critic, actor_params, sched, obs, chains, lp_old_mean,
                               advantages, returns, total, perm_seed, epoch, start, rows, row_index, adv_stats, workspace,
                               grads, metrics, stream, part);
@@ -1050,7 +1067,8 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     aa.mode = ROWS_PRETRAIN; aa.nrows = rows; aa.ws = ws; aa.metrics = metrics;
     aa.tsteps = t; aa.noise = noise; aa.qsched = qsched;
     // loss = mean over global_rows * XD elements of (eps - noise)^2 (diffusion.py:192)
-    aa.pre_scale = 2.f * loss_scale / ((float)global_rows * (float)D.XD) * dppo_grad_scale(precision);
+    const float gscale = dppo_grad_scale_rows(precision, global_rows);
+    aa.pre_scale = 2.f * loss_scale / ((float)global_rows * (float)D.XD) * gscale;
     rc = launch_actor_rowtile(aa, precision, s);
     if (rc) return rc;
 
@@ -1070,7 +1088,7 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
     w.ldm = ws.ldm;
     w.seg = ws.seg;
-    w.out_scale = 1.f / dppo_grad_scale(precision);
+    w.out_scale = 1.f / gscale;
     const int tiles = w.tile_start[w.nprob];
     int nch = dw_device_cus() / tiles;
     const int max_ch = (int)(ws.ldm / 64);
@@ -1081,7 +1099,7 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     rc = precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, tk, s)
        : precision == DPPO_F16  ? launch_dw<PolicyF16>(w, tk, s) : launch_dw<PolicyF32>(w, tk, s);
     if (rc) return rc;
-    const float inv = 1.f / dppo_grad_scale(precision);
+    const float inv = 1.f / gscale;
     if (precision == DPPO_BF16)
         hipLaunchKernelGGL(seg_reduce_kernel<__bf16>, dim3(D.H), dim3(256), 0, s, (const __bf16*)ws.dh1T, ws.seg, ws.ldm,
                            D.K, ws.gseg, D.H, inv);

@@ -264,10 +264,23 @@ def sampler_layout(d: ModelDims, precision, n_envs):
 
 
 def sampler_max_in_flight(d: ModelDims, precision, n_envs):
-    """Sampler launches of n_envs envs that may be in flight together (include/dppo.h)."""
+    """Sampler launches of n_envs envs that may be in flight together (include/dppo.h), divided
+    among the ranks that share this GPU (DPPO_SINGLE_DEVICE rehearsals: every rank's launches need
+    their co-resident workgroups at once)."""
     m = ctypes.c_int()
     _lib.call("dppo_sampler_max_in_flight", ctypes.byref(d.c()), _prec(precision), int(n_envs), ctypes.byref(m))
-    return m.value
+    sharing = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))) \
+        if os.environ.get("DPPO_SINGLE_DEVICE") else 1
+    return max(1, m.value // max(1, sharing))
+
+
+def sampler_plan(d: ModelDims, precision, n_envs):
+    """The sampler the library runs for n_envs envs (dppo_sampler_plan): dict(kernel, members,
+    sets, workgroups); kernel: 0 weight streaming, 1 split P = 8, 2 folded split (one 16-env tile
+    per member set), 3 pair (two tiles per member pair)."""
+    out = (ctypes.c_int * 4)()
+    _lib.call("dppo_sampler_plan", ctypes.byref(d.c()), _prec(precision), int(n_envs), out)
+    return dict(kernel=out[0], members=out[1], sets=out[2], workgroups=out[3])
 
 
 class SampleStepper:
@@ -410,6 +423,12 @@ class RolloutPipe:
         if rc:
             raise _lib.DppoError(f"dppo_rollout_enqueue failed ({rc}): {self._lib.dppo_last_error().decode()}")
         m._call_id += 1
+
+    def launch_event(self):
+        """An event recorded on the stream of the most recent launch (its completion)."""
+        ev = torch.cuda.Event()
+        ev.record(self._tstreams[(self.enqueued - 1) % len(self._tstreams)])
+        return ev
 
     def begin(self):
         """Before a rollout: the launch streams wait for the caller's stream (updated weights)."""

@@ -16,6 +16,7 @@ Keras's numbering) and checks every shape against the flat spec; what is missing
 error. Parity is pinned to this published layout, not to a file Keras wrote (TF/Keras cannot be
 installed here): the reader itself is pinned to files a real HDF5 library wrote.
 """
+import logging
 import re
 
 import numpy as np
@@ -54,13 +55,16 @@ def _keras_index(name):
     return (m.group(1), int(m.group(2) or 0))
 
 
-def _resolve(data, want):
+def _resolve(data, want, used=None):
     """want: name -> canonical path. Container-named levels (the residual block, the Sequential's
-    Dense layers) are matched by structure when the canonical name is absent."""
+    Dense layers) are matched by structure when the canonical name is absent. `used` collects the
+    dataset paths read."""
     got, missing = {}, []
+    used = set() if used is None else used
     for name, path in want.items():
         if path in data:
             got[name] = data[path]
+            used.add(path)
             continue
         alt = None
         if "/residual_blocks/" in path:                      # any single residual block name
@@ -80,9 +84,29 @@ def _resolve(data, want):
                 alt = f"{head}/layers/{layers[which]}/{tail.split('/', 1)[1]}"
         if alt is not None and alt in data:
             got[name] = data[alt]
+            used.add(alt)
         else:
             missing.append(path)
     return got, missing
+
+
+def _datasets(data, prefixes):
+    return sorted(k for k in data if k != "__groups__" and any(k.startswith(p) for p in prefixes))
+
+
+def _check_unused(path, data, used, model_prefixes, what):
+    """Every dataset inside the model's own subtrees must have been read: a Keras file whose layout
+    differs from the one this reader follows (renamed or extra variables) fails here, naming them,
+    instead of loading with variables silently skipped. Datasets outside those subtrees (e.g.
+    optimizer state) are listed in the log."""
+    unread = [k for k in _datasets(data, model_prefixes) if k not in used]
+    if unread:
+        raise ValueError(f"{path}: {what}: datasets inside the model that this reader does not map (layout "
+                         f"differs from the Keras-3 layout in util/keras_weights.py): {unread[:50]}")
+    other = [k for k in data if k != "__groups__" and not any(k.startswith(p) for p in model_prefixes)]
+    if other:
+        logging.getLogger(__name__).warning("%s: ignoring %d dataset(s) outside the %s: %s", path, len(other), what,
+                                            other[:20])
 
 
 def _find_prefix(data, candidates, probe):
@@ -111,9 +135,11 @@ def load_actor(path, spec, prefixes=("", "network/", "actor/", "actor_ft/")):
     if p is None:
         raise ValueError(f"{path}: no DiffusionMLP (mlp_mean/...) found; datasets: "
                          + ", ".join(sorted(k for k in data if k != "__groups__"))[:2000])
-    got, missing = _resolve(data, actor_paths(p))
+    used = set()
+    got, missing = _resolve(data, actor_paths(p), used)
     if missing:
         raise ValueError(f"{path}: missing DiffusionMLP variables: {missing}")
+    _check_unused(path, data, used, (p + "mlp_mean/", p + "time_embedding/"), "DiffusionMLP")
     return _checked(got, spec, "actor", path)
 
 
@@ -121,13 +147,15 @@ def load_ppo_model(path, actor_spec, critic_spec):
     """{"actor", "actor_ft", "critic"} dicts from a fine-tune checkpoint (PPODiffusion.save_weights)."""
     data = read_h5(path)
     out = {}
+    used = set()
     for key, paths, spec in (("actor", actor_paths("actor/"), actor_spec),
                              ("actor_ft", actor_paths("actor_ft/"), actor_spec),
                              ("critic", critic_paths("critic/"), critic_spec)):
-        got, missing = _resolve(data, paths)
+        got, missing = _resolve(data, paths, used)
         if missing:
             raise ValueError(f"{path}: missing {key} variables: {missing}")
         out[key] = _checked(got, spec, key, path)
+    _check_unused(path, data, used, ("actor/", "actor_ft/", "critic/"), "PPODiffusion model")
     return out
 
 

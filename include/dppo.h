@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 5
+#define DPPO_ABI_VERSION 6
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -123,6 +123,13 @@ DPPO_API int dppo_sampler_layout(const dppo_dims* d, int precision, int n_envs, 
  * members wait for: floor(CUs / active workgroups) for the split kernel (>= 1), 8 for the
  * weight-streaming kernel. The pipelined rollout (ops.RolloutPipe) uses at most this many streams. */
 DPPO_API int dppo_sampler_max_in_flight(const dppo_dims* d, int precision, int n_envs, int* launches);
+
+/* The sampler plan for n_envs envs (measurement aid, ABI 6): plan[0] = kernel (0 weight streaming,
+ * 1 split with 8 members per 16-env tile, 2 folded split with P members per tile, 3 the pair kernel:
+ * P = 2 members running two 16-env tiles half a denoising step apart), plan[1] = members per member
+ * set, plan[2] = member sets (2: the base actor's and the fine-tuned actor's steps on separate
+ * workgroups), plan[3] = workgroups per launch. */
+DPPO_API int dppo_sampler_plan(const dppo_dims* d, int precision, int n_envs, int* plan);
 
 /* One rollout step (agent/finetune/train_ppo_diffusion_agent.py:106-122) in one call:
  * hipMemcpyAsync(cond <- cond_host [host, pinned]), dppo_sample with the Philox noise, hipMemcpyAsync
@@ -260,8 +267,11 @@ DPPO_API int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const vo
 /* One half of dppo_ppo_minibatch on the caller's stream, so a caller can overlap the critic's half
  * of minibatch i+1 with the actor's tail of minibatch i: part 1 = the actor (zeroes the actor
  * gradients and metrics 0, 2..15; row tiles, dW, time-MLP backward; needs adv_stats), part 2 =
- * the critic (zeroes the critic gradients and metric 1; row tiles, dW). Same arguments and results
- * as dppo_ppo_minibatch, which runs both (the critic on an internal side stream). */
+ * the critic (zeroes the critic gradients and metric 1; row tiles, dW). Part 1 also splits in two
+ * (ABI 6): part 4 = the actor's zeroing + row tiles (its loss metrics are final after it), part 5 =
+ * the actor's dW + time-MLP backward, so a data-parallel caller can all-reduce the metrics with the
+ * critic's gradients while the actor's dW runs. Same arguments and results as dppo_ppo_minibatch,
+ * which runs both halves (the critic on an internal side stream). */
 DPPO_API int dppo_ppo_minibatch_part(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
                             const void* packed_ft, const void* packed_critic, const float* actor_params,
                             const float* sched, const float* obs, const float* chains, const float* lp_old_mean,

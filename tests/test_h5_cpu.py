@@ -128,3 +128,26 @@ def test_keras_layout_round_trip_and_errors(tmp_path):
     write_h5(r, ren)
     with pytest.raises(ValueError, match="output_layer"):
         KW.load_actor(r, a_spec)
+
+
+def test_keras_reader_fails_loudly_on_unmapped_variables(tmp_path):
+    """A Keras file with a variable inside the model that the layout does not map (a renamed or
+    extra layer) must not load with it silently skipped; state outside the model is only logged."""
+    a_spec, c_spec = _specs()
+    rng = np.random.default_rng(1)
+    mk = lambda spec: {n: rng.standard_normal(s).astype(np.float32) for n, s in spec}
+    p = str(tmp_path / "state_1.weights.h5")
+    KW.save_ppo_model(p, mk(a_spec), mk(a_spec), mk(c_spec))
+    d = read_h5(p)
+    d.pop("__groups__")
+    d["optimizer/vars/0"] = np.zeros(3, np.float32)          # outside the model: tolerated (logged)
+    q = str(tmp_path / "extra_ok.weights.h5")
+    write_h5(q, d)
+    KW.load_ppo_model(q, a_spec, c_spec)
+    d["actor_ft/mlp_mean/extra_layer/vars/0"] = np.zeros((4, 4), np.float32)   # inside: fails, named
+    r = str(tmp_path / "extra_bad.weights.h5")
+    write_h5(r, d)
+    with pytest.raises(ValueError, match="extra_layer"):
+        KW.load_ppo_model(r, a_spec, c_spec)
+    with pytest.raises(ValueError, match="extra_layer"):
+        KW.load_actor(r, a_spec, prefixes=("actor_ft/",))

@@ -681,3 +681,63 @@ def test_ppo_minibatch_full_size(cuda, precision, dims):
     for lo, hi, name in ((0, na, "actor"), (na, na + nc, "critic")):
         err = np.abs(g7[lo:hi] - g_ref[lo:hi]).max() / np.abs(g_ref[lo:hi]).max()
         assert err < tol, (name, err)
+
+
+def test_fp16_small_minibatch_large_returns_stays_finite(cuda):
+    """the fp16 backward seed is scale / global_rows x the per-row gradient; with a
+    fixed 4096 a 24-row minibatch with value errors ~1e3 overflowed fp16. The scale is now the
+    largest power of two <= min(4096, global_rows): finite gradients, matching the oracle."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER, cuda)
+    rng = np.random.default_rng(4)
+    N, kf, rows = 12, d.ft_denoising_steps, 24
+    obs = rng.uniform(-1, 1, (N, d.sd)).astype(np.float32)
+    chains = (rng.standard_normal((N, kf + 1, d.xd)) * 0.5).astype(np.float32)
+    adv = rng.normal(size=N).astype(np.float32)
+    ret = (rng.normal(size=N) * 1000.0).astype(np.float32)
+    T = lambda x: torch.tensor(x, device=cuda)
+    packf = ops.pack_actor(d, pf, "fp16")
+    _, lpm = ops.logprob(d, "fp16", packf, tab, T(obs), T(chains), want_elem=False)
+    lp_old = lpm.cpu().numpy()
+    na = ops.spec_count(ops.actor_param_spec(d))
+    nc = ops.spec_count(ops.critic_param_spec(d))
+    grads = torch.zeros(na + nc, dtype=torch.float32, device=cuda)
+    met = torch.zeros(16, dtype=torch.float64, device=cuda)
+    seed, epoch = 3, 0
+    ops.ppo_minibatch(d, "fp16", ops.ppo_hparams(global_rows=rows), packf, ops.pack_critic(d, pc, "fp16"), pf, tab,
+                      T(obs), T(chains), T(lp_old), T(adv), T(ret), seed, epoch, 0, rows,
+                      ops.ppo_workspace(d, "fp16", rows, cuda), grads, met)
+    torch.cuda.synchronize()
+    g = grads.cpu().numpy()
+    assert np.isfinite(g).all() and np.isfinite(met.cpu().numpy()).all()
+    perm = PX.feistel_permute(np.arange(rows), N * kf, seed, epoch)
+    bi, di = perm // kf, perm % kf
+    _, ga, gc = O.c_loss(to_f64(ft), to_f64(critic), sched, obs[bi].reshape(rows, 1, -1).astype(np.float64),
+                         chains[bi, di].reshape(rows, 4, 3).astype(np.float64),
+                         chains[bi, di + 1].reshape(rows, 4, 3).astype(np.float64), di, ret[bi].astype(np.float64),
+                         None, adv[bi].astype(np.float64), lp_old[bi, di].astype(np.float64), kf, rnd=O.round_fp16,
+                         critic_dedup=_dedup(bi))
+    gcrit = ops.unflatten_params(ops.critic_param_spec(d), g[na:])
+    for k in ("l1_w", "out_w", "in_w"):
+        rel = np.abs(gcrit[k] - gc[k]).max() / (np.abs(gc[k]).max() + 1e-12)
+        assert rel < 2e-2, (k, rel)
+
+
+@pytest.mark.parametrize("envs", [64, 37])
+def test_pair_sampler_bit_identical(tmp_path, envs):
+    """The opt-in pair kernel (DPPO_SPLIT_PAIR=1: two 16-env tiles per member pair, interleaved)
+    gives the one-tile kernel's actions and chains bit for bit (train and eval noise rules; 37
+    envs: a pair whose second tile has no env). Child processes: the switch is read once."""
+    import subprocess
+    import sys
+    res = {}
+    for flag in ("1", "0"):
+        out = str(tmp_path / f"pair{flag}.npz")
+        subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_pair_child.py"), out, str(envs)],
+                       env=dict(os.environ, DPPO_SPLIT_PAIR=flag), check=True, timeout=120)
+        res[flag] = np.load(out)
+    assert int(res["1"]["kernel"]) == 3 and int(res["0"]["kernel"]) == 2
+    for k in ("arr_0", "arr_1", "arr_2", "arr_3"):
+        assert np.isfinite(res["1"][k]).all()
+        np.testing.assert_array_equal(res["1"][k], res["0"][k])
