@@ -784,25 +784,12 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4)))
     critic_rowtile_body<P, MT, NT, TRAIN, WAVES>(a);
 }
 
-// Row-tile shape selection: DPPO_ROWTILE = "<actor>,<critic>" with actor in {64x16, 32x8, 32x8o4, 64x8}
-// and critic in {32x8, 32x8o4}; read once (a tuning knob for measurements, defaults below).
-// actor: 0 = 64x16, 1 = 32x8, 2 = 32x8o4, 3 = 64x8 (64 rows on 8 waves of 64x64); critic: 0 = 32x8, 1 = 32x8o4
+// Row-tile shapes: actor 64 rows on 16 waves (2-byte operands, H = 512, XD <= 16, at least one
+// round of tiles), else 32 rows on 8 waves; critic 32 rows on 8 waves at occupancy 4 (the _o4
+// kernel). r02 measured the alternatives (actor 32x8 at occupancy 4, 64x8; critic at occupancy 2)
+// slower or equal; r03 removed them with the binary's size in mind.
 struct RowTileCfg { int actor; int critic; };
-static RowTileCfg row_tile_cfg() {
-    static RowTileCfg c = [] {
-        RowTileCfg r{0, 1};
-        if (const char* e = getenv("DPPO_ROWTILE")) {
-            if (!strncmp(e, "64x8", 4)) r.actor = 3;
-            else if (!strncmp(e, "32x8o4", 6)) r.actor = 2;
-            else if (!strncmp(e, "32x8", 4)) r.actor = 1;
-            else if (!strncmp(e, "64x16", 5)) r.actor = 0;
-            const char* c2 = strchr(e, ',');
-            if (c2) r.critic = !strncmp(c2 + 1, "32x8o4", 6) ? 1 : 0;
-        }
-        return r;
-    }();
-    return c;
-}
+static RowTileCfg row_tile_cfg() { return RowTileCfg{0, 1}; }
 
 // =============================================================================================
 // launchers
@@ -902,8 +889,7 @@ static int launch_actor_2b(const ActorArgs& a, hipStream_t s) {
         if ((rows + 63) / 64 < actor_device_cus()) return dispatch_actor<P2, 2, 8>(a, s);
         return dispatch_actor<P2, 4, 16>(a, s);
     }
-    if (a.H == 512 && v == 3 && a.XD <= 16) return dispatch_actor<P2, 4, 8>(a, s);
-    return v == 2 ? dispatch_actor<P2, 2, 8, true>(a, s) : dispatch_actor<P2, 2, 8>(a, s);
+    return dispatch_actor<P2, 2, 8>(a, s);
 }
 
 int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
@@ -941,13 +927,9 @@ static int dispatch_critic(const CriticArgs& a, hipStream_t s) {
 }
 
 int launch_critic_rowtile(const CriticArgs& a, int precision, hipStream_t s) {
-    if (row_tile_cfg().critic == 1)
-        return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8, true>(a, s)
-             : precision == DPPO_F16  ? dispatch_critic<PolicyF16, 2, 8, true>(a, s)
-                                      : dispatch_critic<PolicyF32, 2, 8, true>(a, s);
-    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8, false>(a, s)
-         : precision == DPPO_F16  ? dispatch_critic<PolicyF16, 2, 8, false>(a, s)
-                                  : dispatch_critic<PolicyF32, 2, 8, false>(a, s);
+    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8, true>(a, s)
+         : precision == DPPO_F16  ? dispatch_critic<PolicyF16, 2, 8, true>(a, s)
+                                  : dispatch_critic<PolicyF32, 2, 8, true>(a, s);
 }
 
 // =============================================================================================

@@ -472,36 +472,26 @@ static int launch_sample_q(const SampleArgs& a, hipStream_t s) {
     return DPPO_OK;
 }
 
-// Sampler geometry (measurement knob DPPO_SAMPLER_CFG, default "x"):
-//   "x": the split register-resident kernel (sampler_split.hip) where it applies (bf16, H = 512,
-//        <= 512 envs), else "r"
-//   "s": 16 waves, nothing resident, QD 3 (the streaming-only layout)
-//   "r": 8 waves, in/out layers + 2 hidden k-steps resident, QD 3 (bf16 H = 512)
-//   "l": "r" + 1 more hidden k-step per layer in LDS; "m", "q", "i", "e": fewer resident
+// Sampler selection (DPPO_SAMPLER_CFG, default "x"):
+//   "x": the split register-resident kernel (sampler_split.hip) where it applies (2-byte operands,
+//        H = 512, <= 512 envs), else the weight-streaming kernel below;
+//   "r": the weight-streaming kernel always (8 waves, in/out layers + 2 hidden k-steps resident,
+//        QD 3, for 2-byte operands at H = 512; 16 waves with nothing resident otherwise).
+// (r01 measured five other resident-set geometries of the streaming kernel, "l", "m", "q", "i",
+// "e", and two 16-wave ones: all slower; they were removed in r03 with the binary's size in mind.)
 static char sampler_cfg() {
     static char c = [] {
         const char* e = getenv("DPPO_SAMPLER_CFG");
-        return e && e[0] ? e[0] : 'x';
+        return e && e[0] == 'r' ? 'r' : 'x';
     }();
     return c;
 }
 
 template <class P, int NT16, int NO, int KSI, bool INJ>
 static int launch_sample_k(const SampleArgs& a, hipStream_t s) {
-    if constexpr (P::KG == 32 && NT16 == 2 && P::GRAD_SCALE != 1.f) {   // fp16, H = 512: the default geometry only
+    if constexpr (P::KG == 32 && NT16 == 2) {   // 2-byte operands, H = 512
         return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 0, 3>(a, s);
     } else {
-        if constexpr (P::KG == 32 && NT16 == 2) {   // bf16, H = 512
-            const char c = sampler_cfg();
-            if (c == 'r' || c == 'x') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 0, 3>(a, s);
-            if (c == 'l') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 2, 1, 3>(a, s);
-            if (c == 'm') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 1, 3>(a, s);
-            if (c == 'q') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 1, 0, 3>(a, s);
-            if (c == 'i') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, 3>(a, s);
-            if (c == 'e') return launch_sample_q<P, 4, NO, KSI, INJ, 3, 8, 0, 0, 0>(a, s);
-        }
-        if (sampler_cfg() == 'I') return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 1>(a, s);
-        if (sampler_cfg() == 'O') return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 3>(a, s);
         return launch_sample_q<P, NT16, NO, KSI, INJ, 3, 16, 0, 0, 0>(a, s);
     }
 }
@@ -532,19 +522,7 @@ static int dispatch_sample(const SampleArgs& a, hipStream_t s) {
 // the geometry launch_sample_k picks, for dppo_sampler_stream_bytes
 struct SamplerGeom { int SW, RK, LK, RIO; };
 static SamplerGeom sampler_geom(int precision, int H) {
-    if (dppo_prec_2b(precision) && H == 512) {
-        switch (sampler_cfg()) {
-            case 'r': case 'x': return {8, 2, 0, 3};
-            case 'l': return {8, 2, 1, 3};
-            case 'm': return {8, 1, 1, 3};
-            case 'q': return {8, 1, 0, 3};
-            case 'i': return {8, 0, 0, 3};
-            case 'e': return {8, 0, 0, 0};
-            default: break;
-        }
-    }
-    if (sampler_cfg() == 'I') return {16, 0, 0, 1};
-    if (sampler_cfg() == 'O') return {16, 0, 0, 3};
+    if (dppo_prec_2b(precision) && H == 512) return {8, 2, 0, 3};
     return {16, 0, 0, 0};
 }
 

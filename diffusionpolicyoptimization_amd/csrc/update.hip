@@ -65,6 +65,7 @@ struct DWArgs {
     const int8_t* seg;
     const int* rows_dev;      // non-null: only the first ceil64(*rows_dev) rows are summed (the chunk
                               // edge is recomputed on the device from that count)
+    size_t m0, m1;            // the rows [m0, m1) summed (m1 = 0: [0, ldm)); m-chunks start at m0
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -213,13 +214,13 @@ __global__ __launch_bounds__(DWGeom<WK>::W * 64) void dw_kernel(DWArgs a) {
     const int kt = lt / pr.ntiles, nt = lt % pr.ntiles;
     const int k_base = kt * WK, n_base = nt * DW_TN;
     const int wr = wave >> 1, wc = wave & 1;
-    size_t lim = a.ldm, mchunk = (size_t)a.mchunk;
+    size_t lim = a.m1 ? a.m1 : a.ldm, mchunk = (size_t)a.mchunk;
     if (a.rows_dev) {
         const size_t d64 = (size_t)(__builtin_amdgcn_readfirstlane(*a.rows_dev) + 63) / 64 * 64;
         lim = d64 < lim ? d64 : lim;
         mchunk = (lim + (size_t)a.nchunks * 64 - 1) / ((size_t)a.nchunks * 64) * 64;
     }
-    const size_t m_begin = (size_t)chunk * mchunk;
+    const size_t m_begin = a.m0 + (size_t)chunk * mchunk;
     const size_t m_end = m_begin + mchunk < lim ? m_begin + mchunk : lim;
     if (m_begin >= m_end) return;
     const int nst = (int)((m_end - m_begin) / BK);
@@ -880,9 +881,13 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     static const int env_ch = [] { const char* e = getenv("DPPO_DW_CHUNKS"); return e ? atoi(e) : 0; }();
     const int tk = dw_tk();
     const int* crit_rows_dev = nullptr;
-    auto launch_grads = [&](bool actor, hipStream_t st) -> int {
+    // rows [m0, m1) of the images (m1 = 0: all of them)
+    auto launch_grads = [&](bool actor, hipStream_t st, size_t m0 = 0, size_t m1 = 0) -> int {
         DWArgs w = {};
         if (!actor) w.rows_dev = crit_rows_dev;
+        w.m0 = m0;
+        w.m1 = m1;
+        const size_t span = (m1 ? m1 : ws.ldm) - m0;
         auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
             DWProb& p = w.p[w.nprob];
             p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
@@ -909,12 +914,12 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         // an 8-GPU rank's share) thinner chunks cost more in partial-tile atomics than they gain
         // in parallelism (0.177 -> 0.154 ms per minibatch, tools/ab_small_mb2.sh)
         int nch = env_ch > 0 ? env_ch : dw_device_cus() / tiles;
-        if (env_ch <= 0 && nch > (int)(ws.ldm / 768)) nch = (int)(ws.ldm / 768);
-        const int max_ch = (int)(ws.ldm / 64);
+        if (env_ch <= 0 && nch > (int)(span / 768)) nch = (int)(span / 768);
+        const int max_ch = (int)(span / 64);
         if (nch > max_ch) nch = max_ch;
         if (nch < 1) nch = 1;
-        w.mchunk = (int)(dppo_cdiv((int)ws.ldm, nch * 64) * 64);
-        w.nchunks = dppo_cdiv((int)ws.ldm, w.mchunk);
+        w.mchunk = (int)(dppo_cdiv((int)span, nch * 64) * 64);
+        w.nchunks = dppo_cdiv((int)span, w.mchunk);
         return precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, tk, st)
              : precision == DPPO_F16  ? launch_dw<PolicyF16>(w, tk, st) : launch_dw<PolicyF32>(w, tk, st);
     };
@@ -948,13 +953,53 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         return launch_grads(false, s);
     }
+    // Early actor dW (parts 1, 4, 5). The last round of 64-row actor tiles is short (50,000 rows:
+    // 782 tiles = 3 rounds of 256 CUs + 14), and its 14 tiles took a whole round's time with the
+    // actor's dW waiting behind them. The row tiles run as two launches, the full rounds and then
+    // the short one, and the weight gradients over the full rounds' rows start on the internal side
+    // stream as soon as the first launch is done, on the CUs the short round leaves idle; the rest
+    // of the rows' dW follows the short round on the caller's stream, which then joins the side
+    // stream (the dW partials are fp32 atomic adds: two launches over disjoint rows sum exactly as
+    // one up to the order of those adds). DPPO_EARLY_DW=0 turns it off (A/B knob).
+    size_t split_row = 0;
+    SideStream* eside = nullptr;
+    if (parts == 1 || parts == 4 || parts == 5) {
+        static const bool early_on = [] { const char* e = getenv("DPPO_EARLY_DW"); return !e || atoi(e) != 0; }();
+        const int64_t tiles = (int64_t)ws.ldm / 64, cus = dw_device_cus();
+        const int64_t full = (tiles / cus) * cus, rem = tiles - full;
+        if (early_on && dppo_prec_2b(precision) && D.H == 512 && D.XD <= 16 && full > 0 && rem > 0 && rem <= cus / 2) {
+            eside = side_stream();
+            if (eside) split_row = (size_t)full * 64;
+        }
+    }
     if (parts == 1 || parts == 4 || parts == 5) {      // the actor's half (or its row tiles / its
         if (parts != 5) {                              // weight gradients) on the caller's stream
-            rc = launch_actor_rowtile(aa, precision, s);
+            if (split_row) {
+                ActorArgs a1 = aa;
+                a1.row_end = (int64_t)split_row;
+                rc = launch_actor_rowtile(a1, precision, s);
+                if (rc) return rc;
+                DPPO_HIP(hipEventRecord(eside->fork, s));
+                DPPO_HIP(hipStreamWaitEvent(eside->stream, eside->fork, 0));
+                rc = launch_grads(true, eside->stream, 0, split_row);
+                if (rc) return rc;
+                DPPO_HIP(hipEventRecord(eside->join, eside->stream));
+                ActorArgs a2 = aa;
+                a2.row0 = (int64_t)split_row;
+                rc = launch_actor_rowtile(a2, precision, s);
+            } else {
+                rc = launch_actor_rowtile(aa, precision, s);
+            }
             if (rc) return rc;
         }
         if (parts == 4) return DPPO_OK;
-        rc = launch_grads(true, s);
+        if (split_row) {
+            rc = launch_grads(true, s, split_row, 0);
+            if (rc) return rc;
+            DPPO_HIP(hipStreamWaitEvent(s, eside->join, 0));
+        } else {
+            rc = launch_grads(true, s);
+        }
         if (rc) return rc;
         return launch_time_bwd(D, ws.gseg, actor_params, ga, D.KF, D.TS, s);
     }

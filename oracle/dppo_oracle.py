@@ -158,6 +158,25 @@ def round_fp16(x):
 FP16_GRAD_SCALE = 4096.0
 
 
+def fp16_grad_scale(global_rows):
+    """dppo_grad_scale_rows (csrc/dppo_internal.h): the largest power of two <= min(4096, rows),
+    so a per-row gradient image (g / rows) times the scale stays <= |g| and cannot overflow."""
+    s = 1.0
+    while s < FP16_GRAD_SCALE and 2 * s <= global_rows:
+        s *= 2.0
+    return s
+
+
+def round_fp16_rows(global_rows):
+    """round_fp16 whose gradient images use the row-tied scale of a global_rows minibatch."""
+    sc = fp16_grad_scale(global_rows)
+
+    def rnd(x):
+        return round_fp16(x)
+    rnd.grad_round = lambda x: round_fp16(np.asarray(x, np.float64) * sc) / sc
+    return rnd
+
+
 def _round_fp16_grad(x):
     """The fp16 kernels store backward images as fp16(GRAD_SCALE * g) (PolicyF16, dppo_common.cuh)."""
     return round_fp16(np.asarray(x, np.float64) * FP16_GRAD_SCALE) / FP16_GRAD_SCALE
@@ -356,6 +375,8 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
     clipped per-row mean [b]."""
     b = obs.shape[0]
     j = np.asarray(denoising_inds)
+    if rnd is round_fp16:                    # the fp16 gradient images use the row-tied scale
+        rnd = round_fp16_rows(b if denom is None else denom)
     t = ft_steps - 1 - j                                          # :456-458
     eps, acache = diffusion_mlp_forward(p_ft, chains_prev, t * _tstride(sched), obs, rnd=rnd)
     mu, logvar, pm = p_mean_var(sched, eps, chains_prev, t)
@@ -458,6 +479,9 @@ def p_losses(p, sched, x_start, state, t, noise, with_grad=True, rnd=None, denom
     :182 and :187 are inputs here). denom overrides the element count of the mean (data-parallel
     shards: summing per-shard gradients with the global count gives the full-batch one)."""
     xn = q_sample(sched, x_start, np.asarray(t), noise)
+    if rnd is round_fp16:                    # the fp16 gradient images use the row-tied scale
+        xd = x_start.shape[1] * x_start.shape[2]
+        rnd = round_fp16_rows(x_start.shape[0] if denom is None else denom // xd)
     eps, cache = diffusion_mlp_forward(p, xn, np.asarray(t), state, rnd=rnd)
     e = eps - noise
     n = e.size if denom is None else denom
