@@ -8,12 +8,19 @@
 struct PpoWorkspace {
     uint8_t* base;    // start of the workspace (buffer-resource base of the image stores)
     size_t ldm;
-    // actor
-    void *a0T, *u1T, *u2T, *h3T, *dyT, *dh3T, *dh2T, *dh1T;
+    // actor (no dh3 image: l2's weight gradient is formed through the out layer, see pl2)
+    void *a0T, *u1T, *u2T, *h3T, *dyT, *dh2T, *dh1T;
     // critic
-    void *csT, *cu1T, *cu2T, *ch3T, *cdvT, *cdh3T, *cdh2T, *cdh1T;
+    void *csT, *cu1T, *cu2T, *ch3T, *cdvT, *cdh2T, *cdh1T;
     int8_t* seg;      // [ldm] t of each row (bucket id for the one-hot bias/temb sums), -1 invalid
+    // l2's weight gradient through the linear out layer: dh3 = dy W_out^T, so
+    //   dW_l2 = u2^T dh3 = (u2^T dy) W_out^T,  db_l2 = (1^T dy) W_out^T = db_out W_out^T
+    // pl2 = u2^T dy [H][XD] (actor) and cpl2 = cu2^T dv [HC] (critic) come from the dW GEMM (K = rows),
+    // the H x H products from l2_back_kernel. Each is followed by the buffer zeroed with it: pl2 |
+    // gseg, cpl2 | stats
+    float* pl2;
     float* gseg;      // [64][H] per-t sums of dh1 (actor in-layer; 16 buckets in PPO, K in pretraining)
+    float* cpl2;
     double* stats;    // [4] adv {count, sum, sumsq}
     // the critic's distinct samples of a minibatch (sample-weighted value loss, ppo_minibatch_impl):
     // crow_n [ldm] sample index, crow_w [ldm] its multiplicity, crow_cnt [1] how many
@@ -35,11 +42,13 @@ inline PpoWorkspace make_ppo_workspace(const Dims& D, int precision, int rows, u
         return p;
     };
     w.a0T = take(D.IN); w.u1T = take(D.H); w.u2T = take(D.H); w.h3T = take(D.H);
-    w.dyT = take(D.XD); w.dh3T = take(D.H); w.dh2T = take(D.H); w.dh1T = take(D.H);
+    w.dyT = take(D.XD); w.dh2T = take(D.H); w.dh1T = take(D.H);
     w.csT = take(D.SD); w.cu1T = take(D.HC); w.cu2T = take(D.HC); w.ch3T = take(D.HC);
-    w.cdvT = take(1); w.cdh3T = take(D.HC); w.cdh2T = take(D.HC); w.cdh1T = take(D.HC);
+    w.cdvT = take(1); w.cdh2T = take(D.HC); w.cdh1T = take(D.HC);
     w.seg = base ? (int8_t*)(base + o) : nullptr; o = dppo_align256(o + w.ldm);
+    w.pl2 = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * (size_t)D.H * D.XD);
     w.gseg = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * 64 * (size_t)D.H);
+    w.cpl2 = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * (size_t)D.HC);
     w.stats = base ? (double*)(base + o) : nullptr; o = dppo_align256(o + 8 * 4);
     w.crow_n = base ? (int*)(base + o) : nullptr; o = dppo_align256(o + 4 * w.ldm);
     w.crow_w = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * w.ldm);

@@ -526,11 +526,11 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     PHASE(7);
 
     // ---- backward dX chain (weights continue in the same stream) ----
-    // B4: dh3 = dy W_out^T (kept only in tB: B2 re-reads it from there, which frees 8*MT*NT VGPRs)
+    // B4: dh3 = dy W_out^T (kept only in tB: B2 re-reads it from there, which frees 8*MT*NT VGPRs;
+    // no image: l2's weight gradient is (u2^T dy) W_out^T, dppo_ppo.h pl2)
     gemm_queue<P, MT, NT, KSO, QD>(a0, lda0, W(SEG_T_OUT), ntile0, acc, lane, R,
                                    NextLayers{W(SEG_T_L2), KSH, W(SEG_T_L1), KSH});
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
-    store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.dh3T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     PHASE(8);
     // B3: dh2 = (dh3 W_l2^T) * relu'(h2)
@@ -735,10 +735,9 @@ __device__ __forceinline__ void critic_rowtile_body(const CriticArgs& a) {
     }
     if constexpr (!train) return;
     lds_sync();
-    // B4: dh3 = dV W_out^T (kept only in tB, re-read by B2)
+    // B4: dh3 = dV W_out^T (kept only in tB, re-read by B2; no image, as the actor's)
     gemm_stream<P, MT, NT, KSO>(a0, lda0, W(SEG_T_OUT), ntile0, acc, lane, R, NextLayer{W(SEG_T_L2), KSH, ntile0});
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
-    store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.cdh3T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     // B3: dh2 = (dh3 W_l2^T) * mish'(h2)
     gemm_stream<P, MT, NT, KSH>(tB, ldh, W(SEG_T_L2), ntile0, acc, lane, R, NextLayer{W(SEG_T_L1), KSH, ntile0});

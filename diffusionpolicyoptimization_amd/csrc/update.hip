@@ -65,7 +65,6 @@ struct DWArgs {
     const int8_t* seg;
     const int* rows_dev;      // non-null: only the first ceil64(*rows_dev) rows are summed (the chunk
                               // edge is recomputed on the device from that count)
-    size_t m0, m1;            // the rows [m0, m1) summed (m1 = 0: [0, ldm)); m-chunks start at m0
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -214,13 +213,13 @@ __global__ __launch_bounds__(DWGeom<WK>::W * 64) void dw_kernel(DWArgs a) {
     const int kt = lt / pr.ntiles, nt = lt % pr.ntiles;
     const int k_base = kt * WK, n_base = nt * DW_TN;
     const int wr = wave >> 1, wc = wave & 1;
-    size_t lim = a.m1 ? a.m1 : a.ldm, mchunk = (size_t)a.mchunk;
+    size_t lim = a.ldm, mchunk = (size_t)a.mchunk;
     if (a.rows_dev) {
         const size_t d64 = (size_t)(__builtin_amdgcn_readfirstlane(*a.rows_dev) + 63) / 64 * 64;
         lim = d64 < lim ? d64 : lim;
         mchunk = (lim + (size_t)a.nchunks * 64 - 1) / ((size_t)a.nchunks * 64) * 64;
     }
-    const size_t m_begin = a.m0 + (size_t)chunk * mchunk;
+    const size_t m_begin = (size_t)chunk * mchunk;
     const size_t m_end = m_begin + mchunk < lim ? m_begin + mchunk : lim;
     if (m_begin >= m_end) return;
     const int nst = (int)((m_end - m_begin) / BK);
@@ -294,12 +293,63 @@ __global__ __launch_bounds__(DWGeom<WK>::W * 64) void dw_kernel(DWArgs a) {
 #ifndef TB_THREADS
 #define TB_THREADS 1024
 #endif
-// One workgroup; every parameter it reads (the TD temb rows of W_in and the time MLP) is staged into
-// LDS in one batch of coalesced loads at the start, so the dependent phases below run from LDS and
-// the kernel pays global-load latency about twice (staging, then G) instead of once per phase.
+// l2's weight gradient through the linear out layer (mlp.py:186-206: h3 = l2(.) + h1 feeds
+// output_layer and nothing else, so dh3 = dy W_out^T with the out-Dense's rounded W_out, as B4 of
+// the row tile forms it): dW_l2[h][j] = sum_q pl2[h][q] rnd(W_out[j][q]) with pl2 = u2^T dy from the
+// dW GEMM, db_l2[j] = sum_q db_out[q] rnd(W_out[j][q]). Replaces an [H x rows] dh3 image (written by
+// the row tile, read back by the dW GEMM) and an H x H x rows GEMM by an H x N x rows one.
+struct L2Back {
+    const float* pl2;     // [H][N]
+    const float* gob;     // [N] db_out (final: the dW launch before this one produced it)
+    const uint8_t* wimg;  // the packed W_OUT image ([K = H][N] in fragment order, operands rounded)
+    float* gw;            // [H][H] dW_l2
+    float* gb;            // [H] db_l2
+    int H, N, prec;       // prec: DPPO_BF16 / DPPO_F16 (2-byte fragments) or fp32
+};
+constexpr int L2B_ROWS = 8;   // rows h of dW_l2 per workgroup
+// element (k, n) of a packed [K][N] weight image (dppo_layout.h; pack_all_kernel's slot order)
+__device__ inline float packed_elem(const uint8_t* img, int K, int k, int n, int prec) {
+    const bool two = prec == DPPO_BF16 || prec == DPPO_F16;
+    const int KG = two ? 32 : 16, EPL = two ? 8 : 4;
+    const int lane = (n & 15) + 16 * ((k % KG) / EPL);
+    const size_t slot = ((size_t)(n >> 4) * packed_ksteps(K, KG) + k / KG) * 64 + lane;
+    const uint8_t* e = img + slot * 16 + (size_t)(k % EPL) * (two ? 2 : 4);
+    if (prec == DPPO_BF16) return (float)*(const __bf16*)e;
+    if (prec == DPPO_F16) return (float)*(const _Float16*)e;
+    return *(const float*)e;
+}
+// workgroup b: rows [L2B_ROWS b, +L2B_ROWS) of dW_l2; workgroup 0 also db_l2
+__device__ void l2_back_rows(const L2Back& a, int b) {
+    const int H = a.H, N = a.N;
+    for (int e = threadIdx.x; e < L2B_ROWS * H; e += blockDim.x) {
+        const int h = L2B_ROWS * b + e / H, j = e % H;
+        if (h >= H) break;
+        const float* p = a.pl2 + (size_t)h * N;
+        float s = 0.f;
+        for (int q = 0; q < N; ++q) s += p[q] * packed_elem(a.wimg, H, j, q, a.prec);
+        a.gw[(size_t)h * H + j] = s;
+    }
+    if (b == 0)
+        for (int j = threadIdx.x; j < H; j += blockDim.x) {
+            float s = 0.f;
+            for (int q = 0; q < N; ++q) s += a.gob[q] * packed_elem(a.wimg, H, j, q, a.prec);
+            a.gb[j] = s;
+        }
+}
+__global__ __launch_bounds__(256) void l2_back_kernel(L2Back a) { l2_back_rows(a, (int)blockIdx.x); }
+
+// Workgroup 0 runs the time-MLP backward; workgroups 1.. run l2_back_rows for the actor (one launch
+// for the tail of the actor's gradient). Workgroup 0 stages every parameter it reads (the TD temb
+// rows of W_in and the time MLP) into LDS in one batch of coalesced loads at the start, so the
+// dependent phases below run from LDS and it pays global-load latency about twice (staging, then G)
+// instead of once per phase.
 __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __restrict__ gseg, const float* __restrict__ prm,
                                                        float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF,
-                                                       int TS, int stage_g) {
+                                                       int TS, int stage_g, L2Back l2b) {
+    if (blockIdx.x > 0) {      // whole workgroups branch: no barrier is skipped
+        l2_back_rows(l2b, (int)blockIdx.x - 1);
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* win = sm;                    // [TD][H]   W_in rows XD .. XD+TD-1
     float* w1 = win + TD * H;           // [TD][2TD]
@@ -767,10 +817,14 @@ static SideStream* side_stream() {
     return ss[dev].stream ? &ss[dev] : nullptr;
 }
 
-// time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg)
-static int launch_time_bwd(const Dims& D, const float* gseg, const float* actor_params, float* ga, int nb, int TS,
-                           hipStream_t s) {
+// time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg), and the actor's l2
+// weight gradient from pl2 (l2_back_rows) in the same launch
+static int launch_time_bwd(const Dims& D, int precision, const float* gseg, const float* pl2, const void* packed_actor,
+                           const float* actor_params, float* ga, int nb, int TS, hipStream_t s) {
     const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
+    const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+    L2Back l2b = {pl2, ga + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b, D.H,
+                  D.XD, precision};
     size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
                                   (size_t)nb * (2 * D.TD + 2 * 2 * D.TD));
     DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
@@ -783,8 +837,20 @@ static int launch_time_bwd(const Dims& D, const float* gseg, const float* actor_
             attr = true;
         }
     }
-    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD, D.TD, D.H, nb,
-                       TS, stage_g);
+    hipLaunchKernelGGL(time_bwd_kernel, dim3(1 + dppo_cdiv(D.H, L2B_ROWS)), dim3(TB_THREADS), tsm, s, gseg, actor_params,
+                       ga, FA, D.XD, D.TD, D.H, nb, TS, stage_g, l2b);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+// the critic's l2 weight gradient from cpl2 (N = 1)
+static int launch_critic_l2_back(const Dims& D, int precision, const float* cpl2, const void* packed_critic, float* gc,
+                                 hipStream_t s) {
+    const FlatOffsets FC = make_flat_offsets(D.SD, D.HC, 1, 0);
+    const MlpLayout L = make_mlp_layout(D.SD, D.HC, 1, 0, precision);
+    L2Back l2b = {cpl2, gc + FC.out_b, (const uint8_t*)packed_critic + L.off[SEG_W_OUT], gc + FC.l2_w, gc + FC.l2_b, D.HC, 1,
+                  precision};
+    hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.HC, L2B_ROWS)), dim3(256), 0, s, l2b);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -819,21 +885,24 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     DPPO_CHECK(parts == 3 || adv_stats || parts == 2 || parts == 5,
                "dppo_ppo_minibatch_part: the actor half needs adv_stats");
     // one launch zeroes the atomically accumulated outputs of the half (or whole) being run:
-    // gradients, metrics (actor: 0, 2..15; critic: 1), bucket sums, stats
+    // gradients, metrics (actor: 0, 2..15; critic: 1), pl2 | bucket sums, cpl2 | stats
     ZeroArgs z = {};
+    const size_t actor_acc = (size_t)((const uint8_t*)(ws.gseg + 16 * D.H) - (const uint8_t*)ws.pl2);
+    const size_t critic_acc = (size_t)((const uint8_t*)(ws.stats + 4) - (const uint8_t*)ws.cpl2);
     if (parts == 3) {
         z.p[0] = grads; z.n[0] = (FA.count + FC.count) * sizeof(float);
         z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
-        z.p[2] = ws.gseg; z.n[2] = (size_t)16 * D.H * sizeof(float);
-        z.p[3] = ws.stats; z.n[3] = 4 * sizeof(double);
+        z.p[2] = ws.pl2; z.n[2] = actor_acc;
+        z.p[3] = ws.cpl2; z.n[3] = critic_acc;
     } else if (parts == 1 || parts == 4) {
         z.p[0] = grads; z.n[0] = FA.count * sizeof(float);
         z.p[1] = metrics; z.n[1] = sizeof(double);
         z.p[2] = metrics + 2; z.n[2] = 14 * sizeof(double);
-        z.p[3] = ws.gseg; z.n[3] = (size_t)16 * D.H * sizeof(float);
+        z.p[3] = ws.pl2; z.n[3] = actor_acc;
     } else if (parts == 2) {
         z.p[0] = grads + FA.count; z.n[0] = FC.count * sizeof(float);
         z.p[1] = metrics + 1; z.n[1] = sizeof(double);
+        z.p[2] = ws.cpl2; z.n[2] = (size_t)D.HC * sizeof(float);
     }
     // few workgroups: the split update runs this while the other stream's row tiles hold most CUs,
     // and a 256-block grid waited ~25 us for slots (DPPO_ZERO_BLOCKS: measurement knob)
@@ -881,13 +950,10 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     static const int env_ch = [] { const char* e = getenv("DPPO_DW_CHUNKS"); return e ? atoi(e) : 0; }();
     const int tk = dw_tk();
     const int* crit_rows_dev = nullptr;
-    // rows [m0, m1) of the images (m1 = 0: all of them)
-    auto launch_grads = [&](bool actor, hipStream_t st, size_t m0 = 0, size_t m1 = 0) -> int {
+    auto launch_grads = [&](bool actor, hipStream_t st) -> int {
         DWArgs w = {};
         if (!actor) w.rows_dev = crit_rows_dev;
-        w.m0 = m0;
-        w.m1 = m1;
-        const size_t span = (m1 ? m1 : ws.ldm) - m0;
+        const size_t span = ws.ldm;
         auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
             DWProb& p = w.p[w.nprob];
             p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
@@ -898,12 +964,12 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (actor) {
             add(ws.a0T, D.IN, ws.dh1T, D.H, ga + FA.in_w, EXTRA_ONEHOT, ws.gseg);
             add(ws.u1T, D.H, ws.dh2T, D.H, ga + FA.l1_w, EXTRA_ONES, ga + FA.l1_b);
-            add(ws.u2T, D.H, ws.dh3T, D.H, ga + FA.l2_w, EXTRA_ONES, ga + FA.l2_b);
+            add(ws.u2T, D.H, ws.dyT, D.XD, ws.pl2, EXTRA_NONE, nullptr);   // l2 through the out layer
             add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
         } else {
             add(ws.csT, D.SD, ws.cdh1T, D.HC, gc + FC.in_w, EXTRA_ONES, gc + FC.in_b);
             add(ws.cu1T, D.HC, ws.cdh2T, D.HC, gc + FC.l1_w, EXTRA_ONES, gc + FC.l1_b);
-            add(ws.cu2T, D.HC, ws.cdh3T, D.HC, gc + FC.l2_w, EXTRA_ONES, gc + FC.l2_b);
+            add(ws.cu2T, D.HC, ws.cdvT, 1, ws.cpl2, EXTRA_NONE, nullptr);
             add(ws.ch3T, D.HC, ws.cdvT, 1, gc + FC.out_w, EXTRA_ONES, gc + FC.out_b);
         }
         w.ldm = ws.ldm;
@@ -951,57 +1017,19 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         rc = launch_critic_rowtile(ca, precision, s);
         if (rc) return rc;
-        return launch_grads(false, s);
-    }
-    // Early actor dW (parts 1, 4, 5). The last round of 64-row actor tiles is short (50,000 rows:
-    // 782 tiles = 3 rounds of 256 CUs + 14), and its 14 tiles took a whole round's time with the
-    // actor's dW waiting behind them. The row tiles run as two launches, the full rounds and then
-    // the short one, and the weight gradients over the full rounds' rows start on the internal side
-    // stream as soon as the first launch is done, on the CUs the short round leaves idle; the rest
-    // of the rows' dW follows the short round on the caller's stream, which then joins the side
-    // stream (the dW partials are fp32 atomic adds: two launches over disjoint rows sum exactly as
-    // one up to the order of those adds). DPPO_EARLY_DW=0 turns it off (A/B knob).
-    size_t split_row = 0;
-    SideStream* eside = nullptr;
-    if (parts == 1 || parts == 4 || parts == 5) {
-        static const bool early_on = [] { const char* e = getenv("DPPO_EARLY_DW"); return !e || atoi(e) != 0; }();
-        const int64_t tiles = (int64_t)ws.ldm / 64, cus = dw_device_cus();
-        const int64_t full = (tiles / cus) * cus, rem = tiles - full;
-        if (early_on && dppo_prec_2b(precision) && D.H == 512 && D.XD <= 16 && full > 0 && rem > 0 && rem <= cus / 2) {
-            eside = side_stream();
-            if (eside) split_row = (size_t)full * 64;
-        }
+        rc = launch_grads(false, s);
+        if (rc) return rc;
+        return launch_critic_l2_back(D, precision, ws.cpl2, packed_critic, gc, s);
     }
     if (parts == 1 || parts == 4 || parts == 5) {      // the actor's half (or its row tiles / its
         if (parts != 5) {                              // weight gradients) on the caller's stream
-            if (split_row) {
-                ActorArgs a1 = aa;
-                a1.row_end = (int64_t)split_row;
-                rc = launch_actor_rowtile(a1, precision, s);
-                if (rc) return rc;
-                DPPO_HIP(hipEventRecord(eside->fork, s));
-                DPPO_HIP(hipStreamWaitEvent(eside->stream, eside->fork, 0));
-                rc = launch_grads(true, eside->stream, 0, split_row);
-                if (rc) return rc;
-                DPPO_HIP(hipEventRecord(eside->join, eside->stream));
-                ActorArgs a2 = aa;
-                a2.row0 = (int64_t)split_row;
-                rc = launch_actor_rowtile(a2, precision, s);
-            } else {
-                rc = launch_actor_rowtile(aa, precision, s);
-            }
+            rc = launch_actor_rowtile(aa, precision, s);
             if (rc) return rc;
         }
         if (parts == 4) return DPPO_OK;
-        if (split_row) {
-            rc = launch_grads(true, s, split_row, 0);
-            if (rc) return rc;
-            DPPO_HIP(hipStreamWaitEvent(s, eside->join, 0));
-        } else {
-            rc = launch_grads(true, s);
-        }
+        rc = launch_grads(true, s);
         if (rc) return rc;
-        return launch_time_bwd(D, ws.gseg, actor_params, ga, D.KF, D.TS, s);
+        return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s);
     }
     SideStream* side = side_stream();
     if (side) {
@@ -1012,6 +1040,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         rc = launch_critic_rowtile(ca, precision, side->stream);
         if (rc) return rc;
         rc = launch_grads(false, side->stream);
+        if (rc) return rc;
+        rc = launch_critic_l2_back(D, precision, ws.cpl2, packed_critic, gc, side->stream);
         if (rc) return rc;
         DPPO_HIP(hipEventRecord(side->join, side->stream));
     }
@@ -1024,12 +1054,14 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         rc = launch_grads(false, s);
         if (rc) return rc;
+        rc = launch_critic_l2_back(D, precision, ws.cpl2, packed_critic, gc, s);
+        if (rc) return rc;
     }
     rc = launch_grads(true, s);
     if (rc) return rc;
     if (side) DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
 
-    return launch_time_bwd(D, ws.gseg, actor_params, ga, D.KF, D.TS, s);
+    return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s);
 }
 
 extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
@@ -1101,6 +1133,7 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     ZeroArgs z = {};
     z.p[0] = grads; z.n[0] = FA.count * sizeof(float);
     z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
+    z.p[2] = ws.pl2; z.n[2] = (size_t)D.H * D.XD * sizeof(float);
     hipLaunchKernelGGL(zero_kernel, dim3(256), dim3(256), 0, s, z);
     DPPO_HIP(hipGetLastError());
 
@@ -1129,7 +1162,7 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     // the in-layer's bias and time-MLP gradients come from K bucket sums (seg_reduce + time_bwd)
     add(ws.a0T, D.IN, ws.dh1T, D.H, ga + FA.in_w, EXTRA_NONE, nullptr);
     add(ws.u1T, D.H, ws.dh2T, D.H, ga + FA.l1_w, EXTRA_ONES, ga + FA.l1_b);
-    add(ws.u2T, D.H, ws.dh3T, D.H, ga + FA.l2_w, EXTRA_ONES, ga + FA.l2_b);
+    add(ws.u2T, D.H, ws.dyT, D.XD, ws.pl2, EXTRA_NONE, nullptr);   // l2 through the out layer
     add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
     w.ldm = ws.ldm;
     w.seg = ws.seg;
@@ -1155,5 +1188,5 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
         hipLaunchKernelGGL(seg_reduce_kernel<float>, dim3(D.H), dim3(256), 0, s, (const float*)ws.dh1T, ws.seg, ws.ldm,
                            D.K, ws.gseg, D.H, inv);
     DPPO_HIP(hipGetLastError());
-    return launch_time_bwd(D, ws.gseg, actor_params, ga, D.K, 1, s);
+    return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_actor, actor_params, ga, D.K, 1, s);
 }

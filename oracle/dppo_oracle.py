@@ -217,10 +217,13 @@ def residual_mlp_backward(p, cache, dy, act, prefix):
     dyr = Rg(dy)
     g[prefix + "out_w"] = cache["h3"].T @ dyr
     g[prefix + "out_b"] = dyr.sum(0)
-    dh3 = dyr @ R(p[prefix + "out_w"]).T
+    wo = R(p[prefix + "out_w"])
+    dh3 = dyr @ wo.T
     dh3r = Rg(dh3)
-    g[prefix + "l2_w"] = cache["u2"].T @ dh3r
-    g[prefix + "l2_b"] = dh3r.sum(0)
+    # l2's weight gradient through the linear out layer (the kernels form no dh3 image for it,
+    # csrc/update.hip l2_back_rows): u2^T (dy W_out^T) = (u2^T dy) W_out^T, unrounded dh3
+    g[prefix + "l2_w"] = (cache["u2"].T @ dyr) @ wo.T
+    g[prefix + "l2_b"] = g[prefix + "out_b"] @ wo.T
     du2 = dh3r @ R(p[prefix + "l2_w"]).T
     dh2 = Rg(du2 * ag(cache["h2"]))
     g[prefix + "l1_w"] = cache["u1"].T @ dh2
