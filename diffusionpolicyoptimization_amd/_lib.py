@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("DPPO_LIB") or os.path.join(_HERE, "lib", "libdppo_hip
 
 DPPO_F32, DPPO_BF16, DPPO_F16 = 0, 1, 2
 DPPO_ADAMW_KERAS, DPPO_ADAMW_TORCH = 0, 1
+DPPO_STEP_DEFER_SAMPLER_TABLES = 0x100   # OR'd into dppo_optimizer_step's mode (ABI 7)
 SCHED_COLS = 8
 PRECISION = {"fp32": DPPO_F32, "f32": DPPO_F32, "bf16": DPPO_BF16, "fp16": DPPO_F16, "f16": DPPO_F16}
 
@@ -84,6 +85,7 @@ _SIGNATURES = {
     "dppo_optimizer_step": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P, _P,
                                  _P, _I, _U64, _P]),
     "dppo_value_moments": (_I, [_P, _P, _I64, _P, _P]),
+    "dppo_refresh_sampler_tables": (_I, [_P, _P]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -91,7 +93,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class DppoError(RuntimeError):

@@ -423,6 +423,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # row tiles have produced their loss metrics (overlapping the actor's dW), then the actor's
             # gradients on the main stream (overlapping the critic's optimiser step and repack).
             split = self.max_grad_norm is None and os.environ.get("DPPO_SPLIT_UPDATE", "1") != "0"
+            defer = os.environ.get("DPPO_DEFER_TABLES", "1") != "0"   # A/B knob (measurement)
             if split:
                 if getattr(self, "_side", None) is None:
                     self._side = torch.cuda.Stream(device=self.device)
@@ -500,7 +501,10 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         if stop and same_epoch:                                    # :366-368
                             break
                     # the optimiser step (agent :346): AdamW, the metric sums to the host and the weight
-                    # images re-derived, one dppo_optimizer_step per stream (two launches each)
+                    # images re-derived, one dppo_optimizer_step per stream (two launches each). The actor
+                    # image skips the split sampler's tables (fold, TIN, W_XS, B_OUT2), which no PPO kernel
+                    # reads: the next rollout's first sampler launch re-derives them once
+                    # (DPPO_STEP_DEFER_SAMPLER_TABLES)
                     if hp_ is not None:
                         t_h2 = time.perf_counter()
                     ng = m.grads.numel()
@@ -515,7 +519,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             ctag = tag
                             opt.apply_range(m.grads, 0, na, lr, m.dims, m.precision,
                                             packs={"actor": (m.actor_ft_params, m.packed_ft)},
-                                            metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag)
+                                            metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
+                                            defer_sampler_tables=defer)
                             with torch.cuda.stream(side):
                                 opt.apply_range(m.grads, na, ng, lr, m.dims, m.precision,
                                                 packs={"critic": (m.critic_params, m.packed_critic)},
@@ -527,7 +532,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             opt.apply_range(m.grads, 0, ng, lr, m.dims, m.precision,
                                             packs={"actor": (m.actor_ft_params, m.packed_ft),
                                                    "critic": (m.critic_params, m.packed_critic)},
-                                            metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag)
+                                            metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
+                                            defer_sampler_tables=defer)
                     else:
                         torch.from_numpy(met_out.array[:5]).copy_(met[:5])
                     if self.update_events is not None:

@@ -16,9 +16,12 @@ struct Dims {
     int XD, SD, IN;   // XD = Ta*Da, SD = To*Do, IN = XD + TD + SD
 };
 int dppo_check_dims(const dppo_dims* d, Dims* out);
-// the images of the given networks (either may be null) and the actor's time tables, one launch
+// the images of the given networks (either may be null) and the actor's time tables, one launch;
+// defer_sampler_tables: the actor's split-sampler tables are left stale and re-derived by the
+// sampler before its next launch on that image (dppo_refresh_sampler_tables, pack.hip)
 int dppo_pack_models(const Dims& D, int precision, const float* actor_params, void* packed_actor,
-                     const float* critic_params, void* packed_critic, hipStream_t s);
+                     const float* critic_params, void* packed_critic, hipStream_t s, bool defer_sampler_tables = false);
+
 
 // precision enum values the library implements; the two 2-byte operand policies share layouts
 inline bool dppo_prec_ok(int p) { return p == DPPO_F32 || p == DPPO_BF16 || p == DPPO_F16; }

@@ -1,5 +1,6 @@
 // pack.hip — flat fp32 Keras parameters -> packed MFMA fragment images (dppo_layout.h).
 // Replaces the Keras variable storage of model/common/mlp.py:95-206 (kernels are [in,out]).
+#include <mutex>
 #include "dppo_common.cuh"
 #include "dppo_internal.h"
 
@@ -25,6 +26,7 @@ struct TembArgs {
     const float* params;
     FlatOffsets F;
     int TD, stride, R, XD, H, nout, tables, nfold;
+    int first_table;      // table block b runs time_table_block(first_table + b): R skips the TEMB rows
     float *temb, *tin, *bout2;
     uint8_t *fold, *rout;
 };
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(PACK_THREADS) void pack_all_kernel(PackArgs a) {
     }
     blk -= a.tb.nfold;
     if (blk >= a.pack_blocks) {
-        time_table_block<ET>(a.tb, blk - a.pack_blocks);
+        time_table_block<ET>(a.tb, a.tb.first_table + blk - a.pack_blocks);
         return;
     }
     const int gid = blk * blockDim.x + threadIdx.x;
@@ -268,14 +270,17 @@ __global__ __launch_bounds__(PACK_THREADS) void pack_all_kernel(PackArgs a) {
 static inline uint8_t* P_out(void* p) { return (uint8_t*)p; }
 
 // the jobs of one MLP image (and, for an actor, its time tables) appended to a
-// PackArgs; returns DPPO_OK or an error code
+// PackArgs; returns DPPO_OK or an error code. what: PACK_ALL, PACK_UPDATE (everything but the
+// split sampler's tables: W_XS, FOLD / ROUT, TIN, B_OUT2) or PACK_SAMPLER (those tables only)
+enum { PACK_ALL = 0, PACK_UPDATE = 1, PACK_SAMPLER = 2 };
 static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int time_dim, int precision,
-                        const float* params, void* packed, int temb_steps, int time_stride) {
+                        const float* params, void* packed, int temb_steps, int time_stride, int what = PACK_ALL) {
     const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision, temb_steps);
     const FlatOffsets F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
     const int KG = dppo_prec_2b(precision) ? 32 : 16;
     const bool split_tables = time_dim > 0 && L.temb_steps > 0 && dppo_prec_2b(precision);
-    const int jobs = 11 + (time_dim > 0 ? 1 : 0) + (split_tables ? 1 : 0);
+    const bool main_jobs = what != PACK_SAMPLER, sampler_tables = split_tables && what != PACK_UPDATE;
+    const int jobs = (main_jobs ? 11 + (time_dim > 0 ? 1 : 0) : 0) + (sampler_tables ? 1 : 0);
     if (a.njobs + jobs > PACK_MAXJ) return dppo_set_error(DPPO_EINVAL, "pack: too many images in one launch");
     auto mat = [&](size_t src, int K, int N, bool tr, int seg) {
         PackJob& J = a.j[a.njobs++];
@@ -287,20 +292,22 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
         PackJob& J = a.j[a.njobs++];
         J.kind = 1; J.n = n; J.npad = npad; J.src = params + src; J.dst = P_out(packed) + L.off[seg]; J.threads = npad;
     };
-    if (time_dim > 0) cpy(F.time_w1, (int)(F.in_w - F.time_w1), (int)(F.in_w - F.time_w1), SEG_TIME);
-    mat(F.in_w, in_dim, hidden, false, SEG_W_IN);
-    cpy(F.in_b, hidden, hidden, SEG_B_IN);
-    mat(F.l1_w, hidden, hidden, false, SEG_W_L1);
-    cpy(F.l1_b, hidden, hidden, SEG_B_L1);
-    mat(F.l2_w, hidden, hidden, false, SEG_W_L2);
-    cpy(F.l2_b, hidden, hidden, SEG_B_L2);
-    mat(F.out_w, hidden, out_dim, false, SEG_W_OUT);
-    cpy(F.out_b, out_dim, 16 * L.nt_out, SEG_B_OUT);
-    // transposed images: W^T viewed as a [K'=out][N'=in] weight, i.e. element (k', n') = W[n'][k']
-    mat(F.out_w, out_dim, hidden, true, SEG_T_OUT);
-    mat(F.l2_w, hidden, hidden, true, SEG_T_L2);
-    mat(F.l1_w, hidden, hidden, true, SEG_T_L1);
-    if (split_tables) {   // split sampler: W_in rows [x ; state] (skipping the TD time-embedding rows)
+    if (main_jobs) {
+        if (time_dim > 0) cpy(F.time_w1, (int)(F.in_w - F.time_w1), (int)(F.in_w - F.time_w1), SEG_TIME);
+        mat(F.in_w, in_dim, hidden, false, SEG_W_IN);
+        cpy(F.in_b, hidden, hidden, SEG_B_IN);
+        mat(F.l1_w, hidden, hidden, false, SEG_W_L1);
+        cpy(F.l1_b, hidden, hidden, SEG_B_L1);
+        mat(F.l2_w, hidden, hidden, false, SEG_W_L2);
+        cpy(F.l2_b, hidden, hidden, SEG_B_L2);
+        mat(F.out_w, hidden, out_dim, false, SEG_W_OUT);
+        cpy(F.out_b, out_dim, 16 * L.nt_out, SEG_B_OUT);
+        // transposed images: W^T viewed as a [K'=out][N'=in] weight, i.e. element (k', n') = W[n'][k']
+        mat(F.out_w, out_dim, hidden, true, SEG_T_OUT);
+        mat(F.l2_w, hidden, hidden, true, SEG_T_L2);
+        mat(F.l1_w, hidden, hidden, true, SEG_T_L1);
+    }
+    if (sampler_tables) {   // split sampler: W_in rows [x ; state] (skipping the TD time-embedding rows)
         mat(F.in_w, in_dim - time_dim, hidden, false, SEG_W_XS);
         a.j[a.njobs - 1].k_split = out_dim;
         a.j[a.njobs - 1].k_skip = time_dim;
@@ -317,8 +324,10 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
         b.bout2 = (float*)(P_out(packed) + L.off[SEG_B_OUT2]);
         b.fold = P_out(packed) + L.off[SEG_FOLD];
         b.rout = P_out(packed) + L.off[SEG_ROUT];
-        b.nfold = split_tables ? L.nt_h : 0;
-        b.tables = split_tables ? 2 * L.temb_steps + 1 : L.temb_steps;
+        // blocks: [0, R) TEMB rows, [R, 2R) TIN rows, 2R B_OUT2 (time_table_block)
+        b.nfold = sampler_tables ? L.nt_h : 0;
+        b.first_table = what == PACK_SAMPLER ? L.temb_steps : 0;
+        b.tables = sampler_tables ? 2 * L.temb_steps + 1 - b.first_table : L.temb_steps;
     }
     return DPPO_OK;
 }
@@ -339,20 +348,74 @@ static int launch_pack(PackArgs& a, int precision, hipStream_t s) {
     return DPPO_OK;
 }
 
+
+// Actor images whose split-sampler tables are stale (packed with PACK_UPDATE by an optimizer
+// step that deferred them): the sampler re-derives them on its own stream before its next launch
+// that reads the image (dppo_refresh_sampler_tables). The PPO row tiles never read those tables, so
+// a run of minibatches packs each actor image without them and the rollout after the update pays
+// for them once. Keyed by the image's address; stream order is the caller's, as for every launch.
+namespace {
+struct StaleTables { const void* packed; const float* params; Dims D; int precision; };
+constexpr int MAX_STALE = 32;
+std::mutex g_stale_mu;
+StaleTables g_stale[MAX_STALE];
+int g_nstale = 0;
+
+void clear_stale(const void* packed) {
+    std::lock_guard<std::mutex> lk(g_stale_mu);
+    for (int i = 0; i < g_nstale; ++i)
+        if (g_stale[i].packed == packed) { g_stale[i] = g_stale[--g_nstale]; return; }
+}
+
+int mark_stale(const Dims& D, int precision, const float* params, const void* packed) {
+    std::lock_guard<std::mutex> lk(g_stale_mu);
+    for (int i = 0; i < g_nstale; ++i)
+        if (g_stale[i].packed == packed) { g_stale[i] = {packed, params, D, precision}; return DPPO_OK; }
+    if (g_nstale == MAX_STALE) return dppo_set_error(DPPO_EINVAL, "deferred sampler tables: more than %d stale images", MAX_STALE);
+    g_stale[g_nstale++] = {packed, params, D, precision};
+    return DPPO_OK;
+}
+}  // namespace
+
 int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* params,
                   void* packed, hipStream_t s, int temb_steps, int time_stride) {
     PackArgs a = {};
     int rc = add_mlp_jobs(a, in_dim, hidden, out_dim, time_dim, precision, params, packed, temb_steps, time_stride);
     if (rc) return rc;
+    if (temb_steps > 0) clear_stale(packed);
     return launch_pack(a, precision, s);
 }
 
+extern "C" int dppo_refresh_sampler_tables(const void* packed, void* stream) {
+    if (!packed) return DPPO_OK;
+    hipStream_t s = (hipStream_t)stream;
+    StaleTables e;
+    {
+        std::lock_guard<std::mutex> lk(g_stale_mu);
+        int i = 0;
+        while (i < g_nstale && g_stale[i].packed != packed) ++i;
+        if (i == g_nstale) return DPPO_OK;
+        e = g_stale[i];
+        g_stale[i] = g_stale[--g_nstale];
+    }
+    PackArgs a = {};
+    int rc = add_mlp_jobs(a, e.D.IN, e.D.H, e.D.XD, e.D.TD, e.precision, e.params, (void*)e.packed, e.D.K, e.D.TS,
+                          PACK_SAMPLER);
+    if (rc) return rc;
+    return launch_pack(a, e.precision, s);
+}
+
 int dppo_pack_models(const Dims& D, int precision, const float* actor_params, void* packed_actor,
-                     const float* critic_params, void* packed_critic, hipStream_t s) {
+                     const float* critic_params, void* packed_critic, hipStream_t s, bool defer_sampler_tables) {
     PackArgs a = {};
     int rc;
     if (actor_params && packed_actor) {
-        rc = add_mlp_jobs(a, D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS);
+        const bool defer = defer_sampler_tables && D.TD > 0 && dppo_prec_2b(precision);
+        rc = add_mlp_jobs(a, D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS,
+                          defer ? PACK_UPDATE : PACK_ALL);
+        if (rc) return rc;
+        if (defer) rc = mark_stale(D, precision, actor_params, packed_actor);
+        else clear_stale(packed_actor);   // a full pack makes a pending refresh moot
         if (rc) return rc;
     }
     if (critic_params && packed_critic) {

@@ -560,6 +560,11 @@ static int sample_impl(const dppo_dims* d, int precision, const void* packed_bas
     DPPO_CHECK(dppo_prec_ok(precision), "dppo_sample: bad precision %d", precision);
     if (n_envs == 0) return DPPO_OK;
     DPPO_CHECK(packed_base && packed_ft && sched && (cond || cond_tagged) && actions, "dppo_sample: null pointer argument");
+    // tables an optimizer step deferred (DPPO_STEP_DEFER_SAMPLER_TABLES) are re-derived first, on this stream
+    rc = dppo_refresh_sampler_tables(packed_ft, stream);
+    if (rc) return rc;
+    rc = dppo_refresh_sampler_tables(packed_base, stream);
+    if (rc) return rc;
     SampleArgs a;
     a.packed_base = (const uint8_t*)packed_base;
     a.packed_ft = (const uint8_t*)packed_ft;

@@ -710,10 +710,12 @@ extern "C" int dppo_optimizer_step(const dppo_dims* d, int precision, float* par
         if (hipHostGetDevicePointer(&dp, metrics_out, 0) == hipSuccess && dp) mout = (double*)dp;
         else (void)hipGetLastError();
     }
+    const bool defer = (mode & DPPO_STEP_DEFER_SAMPLER_TABLES) != 0;
+    mode &= ~DPPO_STEP_DEFER_SAMPLER_TABLES;
     rc = launch_adamw(params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode, metrics, mout,
                       n_metrics, metrics_tag, s);
     if (rc) return rc;
-    return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s);
+    return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s, defer);
 }
 
 extern "C" int dppo_pack_all(const dppo_dims* d, int precision, const float* actor_params, void* packed_actor,

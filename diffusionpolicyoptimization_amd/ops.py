@@ -145,11 +145,13 @@ def pack_all(d: ModelDims, precision, actor_params=None, packed_actor=None, crit
 
 def optimizer_step(d: ModelDims, precision, params, grads, m, v, step, lr, weight_decay, beta1, beta2, eps, mode,
                    actor_params=None, packed_actor=None, critic_params=None, packed_critic=None, metrics=None,
-                   metrics_out=None, n_metrics=0, metrics_tag=0):
+                   metrics_out=None, n_metrics=0, metrics_tag=0, defer_sampler_tables=False):
     """AdamW over params/grads/m/v (equal-length flat ranges), the metric sums copied to
     metrics_out (a device tensor or a dppo_host_alloc address), then the given images re-derived:
     two launches on the current stream (dppo_optimizer_step). A nonzero metrics_tag is stored as
-    metrics_out[n_metrics] after the sums (the host polls it instead of an event)."""
+    metrics_out[n_metrics] after the sums (the host polls it instead of an event).
+    defer_sampler_tables: the actor image's split-sampler tables are left stale and re-derived by
+    the next sampler launch on it (DPPO_STEP_DEFER_SAMPLER_TABLES; the PPO kernels never read them)."""
     n = params.numel()
     for t, nm in ((grads, "grads"), (m, "m"), (v, "v")):
         if t.numel() != n:
@@ -158,9 +160,16 @@ def optimizer_step(d: ModelDims, precision, params, grads, m, v, step, lr, weigh
     mo = metrics_out if isinstance(metrics_out, int) else (metrics_out.data_ptr() if metrics_out is not None else None)
     _lib.call("dppo_optimizer_step", ctypes.byref(_dims_c(d)), p, ptr(params), ptr(grads), ptr(m), ptr(v), int(n),
               int(step), float(lr), float(weight_decay), float(beta1), float(beta2), float(eps),
-              _lib.DPPO_ADAMW_KERAS if mode == "keras" else _lib.DPPO_ADAMW_TORCH, ptr(actor_params), ptr(packed_actor),
+              (_lib.DPPO_ADAMW_KERAS if mode == "keras" else _lib.DPPO_ADAMW_TORCH) |
+              (_lib.DPPO_STEP_DEFER_SAMPLER_TABLES if defer_sampler_tables else 0), ptr(actor_params), ptr(packed_actor),
               ptr(critic_params), ptr(packed_critic), ptr(metrics), ctypes.c_void_p(mo) if mo else None,
               int(n_metrics), ctypes.c_uint64(int(metrics_tag)), stream_handle(params.device))
+
+
+def refresh_sampler_tables(packed_actor):
+    """Re-derive an actor image's split-sampler tables on the current stream if an optimizer step
+    deferred them (no-op otherwise); sampler launches do this themselves (dppo_refresh_sampler_tables)."""
+    _lib.call("dppo_refresh_sampler_tables", ptr(packed_actor), stream_handle(packed_actor.device))
 
 
 def value_moments(values, returns, out_address):
@@ -431,7 +440,13 @@ class RolloutPipe:
         return ev
 
     def begin(self):
-        """Before a rollout: the launch streams wait for the caller's stream (updated weights)."""
+        """Before a rollout: split-sampler tables an optimizer step deferred are re-derived on the
+        caller's stream, then the launch streams wait for it (updated weights and tables). A launch
+        reads its resident tables in its prologue, before its observation wait, so the refresh must
+        precede every stream, not only the first launch's."""
+        with torch.cuda.stream(self._tstreams[0]):
+            refresh_sampler_tables(self.model.packed_ft)
+            refresh_sampler_tables(self.model.packed_base)
         for st in self._tstreams[1:]:
             st.wait_stream(self._tstreams[0])
 

@@ -38,17 +38,19 @@ class AdamW:
         return lr
 
     def apply_range(self, grads, lo, hi, lr, dims=None, precision=None, packs=(), metrics=None, metrics_out=None,
-                    n_metrics=0, metrics_tag=0):
+                    n_metrics=0, metrics_tag=0, defer_sampler_tables=False):
         """The step begin_step() opened, over params[lo:hi], then the images in `packs`
         ((actor_params, packed_actor) and/or (critic_params, packed_critic), keyed "actor" /
         "critic") re-derived, with the minibatch's metric sums copied to metrics_out (followed by
-        metrics_tag when nonzero): one dppo_optimizer_step call (two launches) on the current stream."""
+        metrics_tag when nonzero): one dppo_optimizer_step call (two launches) on the current stream.
+        defer_sampler_tables: the actor's split-sampler tables wait for the next sampler launch."""
         pk = dict(packs)
         ap, pa = pk.get("actor", (None, None))
         cp, pc = pk.get("critic", (None, None))
         ops.optimizer_step(dims, precision, self.params[lo:hi], grads[lo:hi], self.m[lo:hi], self.v[lo:hi],
                            self.iterations, lr, self.weight_decay, self.beta_1, self.beta_2, self.epsilon, self.mode,
-                           ap, pa, cp, pc, metrics, metrics_out, n_metrics, metrics_tag)
+                           ap, pa, cp, pc, metrics, metrics_out, n_metrics, metrics_tag,
+                           defer_sampler_tables=defer_sampler_tables)
 
     def apply_gradients_split(self, grads, ranges):
         """One optimiser step over disjoint ranges of the flat buffer, each on its own stream:

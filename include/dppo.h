@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 6
+#define DPPO_ABI_VERSION 7
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -44,6 +44,12 @@ extern "C" {
 enum { DPPO_OK = 0, DPPO_EINVAL = 1, DPPO_EHIP = 2, DPPO_EUNSUPPORTED = 3 };
 enum { DPPO_F32 = 0, DPPO_BF16 = 1, DPPO_F16 = 2 };
 enum { DPPO_ADAMW_KERAS = 0, DPPO_ADAMW_TORCH = 1 };
+/* ABI 7: OR'd into dppo_optimizer_step's mode. The actor image is packed without the split
+ * sampler's tables (W_XS, FOLD/ROUT, TIN, B_OUT2: nothing the PPO row tiles read) and marked stale;
+ * the next sampler launch on that image (dppo_sample, dppo_sample_step, dppo_rollout_enqueue*)
+ * re-derives them on its own stream first, or dppo_refresh_sampler_tables does it explicitly. The
+ * actor parameters must stay allocated and unchanged until then (they are read at the refresh). */
+enum { DPPO_STEP_DEFER_SAMPLER_TABLES = 0x100 };
 
 /* Model / schedule dimensions (cfg keys of cfg/gym/finetune/hopper-v2/ft_ppo_diffusion_mlp.yaml:18-25,78-110). */
 typedef struct dppo_dims {
@@ -302,6 +308,10 @@ DPPO_API int dppo_pack_all(const dppo_dims* d, int precision, const float* actor
  * double metrics_out[n_metrics] AFTER the n_metrics sums (system-scope release), so a host polling
  * host-mapped metrics_out for the tag reads complete sums without recording or waiting on an event
  * (metrics_out then holds n_metrics + 1 doubles; pass 0 for no tag). */
+/* Enqueue the split-sampler tables of an actor image on `stream` if an optimizer step with
+ * DPPO_STEP_DEFER_SAMPLER_TABLES left them stale; a no-op otherwise (ABI 7). */
+DPPO_API int dppo_refresh_sampler_tables(const void* packed_actor, void* stream);
+
 DPPO_API int dppo_optimizer_step(const dppo_dims* d, int precision, float* params, const float* grads, float* m,
                         float* v, int64_t n, int64_t step, float lr, float weight_decay, float beta1,
                         float beta2, float eps, int mode, const float* actor_params, void* packed_actor,

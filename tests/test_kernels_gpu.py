@@ -394,6 +394,42 @@ def test_optimizer_step_metrics_tag(cuda):
     assert torch.equal(P1, m.actor_ft_params)
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_deferred_sampler_tables(cuda, precision):
+    """ABI 7: an optimizer step with DPPO_STEP_DEFER_SAMPLER_TABLES packs the actor image without the
+    split sampler's tables; the next sampler launch re-derives them on its stream, leaving the image
+    byte-identical to a full pack, and samples the same actions as after one. The refresh happens
+    once (a second launch finds nothing stale)."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp_64env",
+                      [f"model.precision={precision}"])
+    m = instantiate(cfg.model, device=cuda, seed=0)
+    n = m.n_actor
+    g = torch.randn(n, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3)) * 0.1
+    M, V = torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    before = m.packed_ft.clone()
+    ops.optimizer_step(m.dims, m.precision, m.actor_ft_params, g, M, V, 1, 1e-2, 0.004, 0.9, 0.999, 1e-7, "keras",
+                       m.actor_ft_params, m.packed_ft, defer_sampler_tables=True)
+    torch.cuda.synchronize()
+    stale = m.packed_ft.clone()
+    full = stale.clone()                 # the same bytes in the gaps between segments
+    ops.pack_actor(m.dims, m.actor_ft_params, m.precision, out=full)
+    torch.cuda.synchronize()
+    assert not torch.equal(stale, full) and not torch.equal(stale, before)   # tables stale, the rest repacked
+    cond = torch.rand(64, m.dims.sd, device=cuda, generator=torch.Generator(device=cuda).manual_seed(1)) * 2 - 1
+    m._call_id = 0
+    a_deferred = m(cond).trajectories.clone()          # refreshes the tables first
+    torch.cuda.synchronize()
+    assert torch.equal(m.packed_ft, full)
+    m.packed_ft.copy_(full)
+    m._call_id = 0
+    a_full = m(cond).trajectories.clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a_deferred, a_full)
+
+
 def test_value_moments(cuda):
     import torch
     from diffusionpolicyoptimization_amd import ops
