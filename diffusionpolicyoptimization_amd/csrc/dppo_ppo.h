@@ -23,9 +23,9 @@ struct PpoWorkspace {
     float* cpl2;
     double* stats;    // [4] adv {count, sum, sumsq}
     // the critic's distinct samples of a minibatch (sample-weighted value loss, ppo_minibatch_impl):
-    // crow_n [ldm] sample index, crow_w [ldm] its multiplicity, crow_cnt [1] how many
+    // crow_n [ldm] sample indices in arrival order, crow_cnt [1] how many (zeroed with cpl2 | stats;
+    // the multiplicities stay in the per-stream count scratch, crit_rows_kernel)
     int* crow_n;
-    float* crow_w;
     int* crow_cnt;
     size_t total;
 };
@@ -49,10 +49,9 @@ inline PpoWorkspace make_ppo_workspace(const Dims& D, int precision, int rows, u
     w.pl2 = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * (size_t)D.H * D.XD);
     w.gseg = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * 64 * (size_t)D.H);
     w.cpl2 = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * (size_t)D.HC);
-    w.stats = base ? (double*)(base + o) : nullptr; o = dppo_align256(o + 8 * 4);
-    w.crow_n = base ? (int*)(base + o) : nullptr; o = dppo_align256(o + 4 * w.ldm);
-    w.crow_w = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * w.ldm);
+    w.stats = base ? (double*)(base + o) : nullptr; o += 8 * 4;
     w.crow_cnt = base ? (int*)(base + o) : nullptr; o = dppo_align256(o + 4);
+    w.crow_n = base ? (int*)(base + o) : nullptr; o = dppo_align256(o + 4 * w.ldm);
     w.total = o;
     return w;
 }
@@ -117,11 +116,11 @@ struct CriticArgs {
     LossHP hp;
     PpoWorkspace ws;
     double* metrics;
-    // TRAIN with crow_n != null: row r is distinct sample crow_n[r] with weight crow_w[r] (its
+    // TRAIN with crow_n != null: row r is distinct sample n = crow_n[r] with weight crow_mult[n] (its
     // multiplicity in the minibatch), *crow_cnt rows (device-side count); the value loss and its
     // gradient are the per-row ones summed over the copies
     const int* crow_n;
-    const float* crow_w;
+    const uint32_t* crow_mult;
     const int* crow_cnt;
 };
 

@@ -722,7 +722,7 @@ __device__ __forceinline__ void critic_rowtile_body(const CriticArgs& a) {
         } else {
             float vl = 0.f, dv = 0.f;
             if (n >= 0) {
-                const float w = a.crow_w ? a.crow_w[grow0 + r] : 1.f;   // copies of the sample in the minibatch
+                const float w = a.crow_mult ? (float)a.crow_mult[n] : 1.f;   // copies of the sample in the minibatch
                 const float diff = V - a.returns[n];
                 vl = 0.5f * diff * diff * w;                     // v_loss = 0.5 mean((V-R)^2), diffusion_ppo.py:118
                 dv = a.hp.vf_coef * diff * a.hp.grad_scale * w;  // loss = pg + vf_coef * v_loss (agent :340)

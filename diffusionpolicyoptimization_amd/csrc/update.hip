@@ -305,8 +305,11 @@ struct L2Back {
     float* gw;            // [H][H] dW_l2
     float* gb;            // [H] db_l2
     int H, N, prec;       // prec: DPPO_BF16 / DPPO_F16 (2-byte fragments) or fp32
+    // critic: the minibatch's sample counts to zero afterwards (cnt[crow_n[r]], r < *crow_cnt), or null
+    uint32_t* zcnt;
+    const int* zlist;
+    const int* zn;
 };
-constexpr int L2B_ROWS = 8;   // rows h of dW_l2 per workgroup
 // element (k, n) of a packed [K][N] weight image (dppo_layout.h; pack_all_kernel's slot order)
 __device__ inline float packed_elem(const uint8_t* img, int K, int k, int n, int prec) {
     const bool two = prec == DPPO_BF16 || prec == DPPO_F16;
@@ -318,38 +321,71 @@ __device__ inline float packed_elem(const uint8_t* img, int K, int k, int n, int
     if (prec == DPPO_F16) return (float)*(const _Float16*)e;
     return *(const float*)e;
 }
-// workgroup b: rows [L2B_ROWS b, +L2B_ROWS) of dW_l2; workgroup 0 also db_l2
-__device__ void l2_back_rows(const L2Back& a, int b) {
-    const int H = a.H, N = a.N;
-    for (int e = threadIdx.x; e < L2B_ROWS * H; e += blockDim.x) {
-        const int h = L2B_ROWS * b + e / H, j = e % H;
-        if (h >= H) break;
-        const float* p = a.pl2 + (size_t)h * N;
-        float s = 0.f;
-        for (int q = 0; q < N; ++q) s += p[q] * packed_elem(a.wimg, H, j, q, a.prec);
-        a.gw[(size_t)h * H + j] = s;
-    }
-    if (b == 0)
-        for (int j = threadIdx.x; j < H; j += blockDim.x) {
-            float s = 0.f;
-            for (int q = 0; q < N; ++q) s += a.gob[q] * packed_elem(a.wimg, H, j, q, a.prec);
-            a.gb[j] = s;
+// Workgroup b forms rows [L2B_ROWS b, +L2B_ROWS) of dW_l2 (workgroup 0 also db_l2): thread t owns
+// columns j = t, t + 256, ... with rnd(W_out[j][:]) in registers; the workgroup's pl2 rows are
+// loaded up front (uniform addresses: one round trip for all of them, not one per row). No LDS and
+// a few hundred FMAs per thread, so the launch fits beside the other stream's row tiles. (Inside
+// time_bwd's single workgroup the H x H x N products took 210 us; as extra workgroups of that launch
+// they inherited its dynamic LDS and waited for CUs, 48 us; one row's loads at a time, 33 us.)
+constexpr int L2B_ROWS = 4;   // rows h of dW_l2 per workgroup
+constexpr int L2B_MAXN = 32;
+template <int NJ, int NQ>
+__device__ inline void l2_back_cols(const L2Back& a, int b) {
+    const int H = a.H;
+    const int h0 = L2B_ROWS * b;
+    float pv[L2B_ROWS + 1][NQ];   // the workgroup's pl2 rows, then (workgroup 0) db_out
+#pragma unroll
+    for (int r = 0; r < L2B_ROWS; ++r)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) pv[r][q] = (h0 + r < H && q < a.N) ? a.pl2[(size_t)(h0 + r) * a.N + q] : 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) pv[L2B_ROWS][q] = (b == 0 && q < a.N) ? a.gob[q] : 0.f;
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) {
+        const int j = threadIdx.x + c * (int)blockDim.x;
+        if (j >= H) continue;
+        float w[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) w[q] = q < a.N ? packed_elem(a.wimg, H, j, q, a.prec) : 0.f;
+#pragma unroll
+        for (int r = 0; r <= L2B_ROWS; ++r) {
+            float sum = 0.f;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) sum = fmaf(pv[r][q], w[q], sum);
+            if (r < L2B_ROWS) {
+                if (h0 + r < H) a.gw[(size_t)(h0 + r) * H + j] = sum;
+            } else if (b == 0) {
+                a.gb[j] = sum;
+            }
         }
+    }
 }
-__global__ __launch_bounds__(256) void l2_back_kernel(L2Back a) { l2_back_rows(a, (int)blockIdx.x); }
+template <int NQ>
+__device__ inline void l2_back_n(const L2Back& a, int b) {
+    if (a.H <= 256) l2_back_cols<1, NQ>(a, b);
+    else l2_back_cols<2, NQ>(a, b);
+}
+__global__ __launch_bounds__(256) void l2_back_kernel(L2Back a) {
+    const int b = (int)blockIdx.x;
+    switch (a.N) {     // the action-chunk widths of the cfgs (hopper 12; walker2d / halfcheetah 24), the critic's 1
+        case 1: l2_back_n<1>(a, b); break;
+        case 12: l2_back_n<12>(a, b); break;
+        case 24: l2_back_n<24>(a, b); break;
+        default: l2_back_n<L2B_MAXN>(a, b); break;   // any N <= 32, zero-padded
+    }
+    if (a.zcnt) {   // the critic's row tiles and dW (earlier on this stream) were the counts' last readers
+        const int nz = *a.zn;
+        for (int r = (int)(blockIdx.x * blockDim.x + threadIdx.x); r < nz; r += (int)(gridDim.x * blockDim.x))
+            a.zcnt[a.zlist[r]] = 0u;
+    }
+}
 
-// Workgroup 0 runs the time-MLP backward; workgroups 1.. run l2_back_rows for the actor (one launch
-// for the tail of the actor's gradient). Workgroup 0 stages every parameter it reads (the TD temb
-// rows of W_in and the time MLP) into LDS in one batch of coalesced loads at the start, so the
-// dependent phases below run from LDS and it pays global-load latency about twice (staging, then G)
-// instead of once per phase.
+// One workgroup; every parameter it reads (the TD temb rows of W_in and the time MLP) is staged into
+// LDS in one batch of coalesced loads at the start, so the dependent phases below run from LDS and
+// the kernel pays global-load latency about twice (staging, then G) instead of once per phase.
 __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __restrict__ gseg, const float* __restrict__ prm,
                                                        float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF,
-                                                       int TS, int stage_g, L2Back l2b) {
-    if (blockIdx.x > 0) {      // whole workgroups branch: no barrier is skipped
-        l2_back_rows(l2b, (int)blockIdx.x - 1);
-        return;
-    }
+                                                       int TS, int stage_g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* win = sm;                    // [TD][H]   W_in rows XD .. XD+TD-1
     float* w1 = win + TD * H;           // [TD][2TD]
@@ -518,62 +554,38 @@ __global__ __launch_bounds__(256) void zero_kernel(ZeroArgs z) {
 // pairs holds each sample ~b/(S*E) times (1.56x at the bench shape: 50,000 rows, 26k distinct
 // samples), so the critic runs once per distinct sample with the multiplicity as the row weight:
 // the same loss and gradient sums, ~half the critic row tiles and dW rows.
-// crit_count_kernel: cnt[sample] += 1 per row (integer atomics: order-independent);
-// crit_compact_kernel: one workgroup lists the nonzero counts in sample order (deterministic) and
-// zeroes them for the next minibatch.
+// crit_rows_kernel (one launch): cnt[sample] += 1 per row; the row that takes a count from 0 appends
+// the sample to crow_n (one atomic per wave on crow_cnt: the wave's first-touch lanes are ranked by
+// mbcnt). The list is in arrival order, so the critic's fp32 sums are accumulated in a run-dependent
+// order, as the dW's split-K atomics already are. The critic's row tile reads the weights from cnt;
+// the critic's last kernel (l2_back_kernel) zeroes the listed counts for the next minibatch.
+// (It replaced a count launch + a one-workgroup ordered compaction: 6 + 27 us alone, 85 + 90 us
+// beside the actor's row tiles.)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void crit_count_kernel(const int64_t* __restrict__ row_index, int64_t start, int rows,
-                                                         FeistelKey fk, int KF, uint32_t* __restrict__ cnt) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < rows; i += (int64_t)gridDim.x * 256) {
-        const uint64_t idx = minibatch_row(row_index, (uint64_t)(start + i), fk);
-        if (idx < fk.n) atomicAdd(cnt + idx / KF, 1u);
+__global__ __launch_bounds__(256) void crit_rows_kernel(const int64_t* __restrict__ row_index, int64_t start, int rows,
+                                                        FeistelKey fk, int KF, uint32_t* __restrict__ cnt,
+                                                        int* __restrict__ crow_n, int* __restrict__ crow_cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n_iter = ((int64_t)rows + (int64_t)gridDim.x * 256 - 1) / ((int64_t)gridDim.x * 256);
+    for (int64_t it = 0; it < n_iter; ++it) {   // uniform trip count: every lane reaches the ballot
+        const int64_t i = (it * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
+        int s = -1;
+        if (i < rows) {
+            const uint64_t idx = minibatch_row(row_index, (uint64_t)(start + i), fk);
+            if (idx < fk.n) s = (int)(idx / (uint64_t)KF);
+        }
+        const bool first = s >= 0 && atomicAdd(cnt + s, 1u) == 0u;
+        const uint64_t m = __ballot(first);
+        if (m == 0) continue;
+        const int leader = __builtin_ctzll(m);
+        int base = 0;
+        if (lane == leader) base = atomicAdd(crow_cnt, __popcll(m));
+        base = __shfl(base, leader, 64);
+        if (first) crow_n[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = s;
     }
 }
 
-#define CC_THREADS 1024
-__global__ __launch_bounds__(CC_THREADS) void crit_compact_kernel(uint32_t* __restrict__ cnt, int nsamp,
-                                                                  int* __restrict__ crow_n, float* __restrict__ crow_w,
-                                                                  int* __restrict__ crow_cnt) {
-    __shared__ int wtot[CC_THREADS / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int base = 0;
-    for (int t0 = 0; t0 < nsamp; t0 += 4 * CC_THREADS) {
-        const int i0 = t0 + 4 * tid;
-        uint32_t c[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] = i0 + k < nsamp ? cnt[i0 + k] : 0u;
-        const int nz = (c[0] != 0) + (c[1] != 0) + (c[2] != 0) + (c[3] != 0);
-        int inc = nz;                                   // inclusive scan over the wave
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int o = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += o;
-        }
-        if (lane == 63) wtot[wave] = inc;
-        __syncthreads();
-        int before = 0, total = 0;
-#pragma unroll
-        for (int w = 0; w < CC_THREADS / 64; ++w) {
-            const int v = wtot[w];
-            before += w < wave ? v : 0;
-            total += v;
-        }
-        int o = base + before + inc - nz;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (c[k]) {
-                crow_n[o] = i0 + k;
-                crow_w[o] = (float)c[k];
-                cnt[i0 + k] = 0u;
-                ++o;
-            }
-        base += total;
-        __syncthreads();                                // wtot is rewritten by the next tile
-    }
-    if (tid == 0) *crow_cnt = base;
-}
-
-// per-(device, stream) sample-count scratch of the compaction (zero between uses), grown on demand
+// per-(device, stream) sample-count scratch of crit_rows_kernel (zero between uses), grown on demand
 static uint32_t* crit_count_scratch(int64_t nsamp, hipStream_t s) {
     struct Ent { int dev; hipStream_t s; uint32_t* p; int64_t cap; };
     thread_local Ent ents[16] = {};
@@ -819,14 +831,17 @@ static SideStream* side_stream() {
     return ss[dev].stream ? &ss[dev] : nullptr;
 }
 
-// time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg), and the actor's l2
-// weight gradient from pl2 (l2_back_rows) in the same launch
+// the actor's l2 weight gradient from pl2 (l2_back_kernel: no LDS, so it starts on any CU with a
+// free wave slot), then the time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg)
 static int launch_time_bwd(const Dims& D, int precision, const float* gseg, const float* pl2, const void* packed_actor,
                            const float* actor_params, float* ga, int nb, int TS, hipStream_t s) {
     const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
     const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     L2Back l2b = {pl2, ga + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b, D.H,
-                  D.XD, precision};
+                  D.XD, precision, nullptr, nullptr, nullptr};
+    DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
+    hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
+    DPPO_HIP(hipGetLastError());
     size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
                                   (size_t)nb * (2 * D.TD + 2 * 2 * D.TD));
     DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
@@ -839,19 +854,19 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
             attr = true;
         }
     }
-    hipLaunchKernelGGL(time_bwd_kernel, dim3(1 + dppo_cdiv(D.H, L2B_ROWS)), dim3(TB_THREADS), tsm, s, gseg, actor_params,
-                       ga, FA, D.XD, D.TD, D.H, nb, TS, stage_g, l2b);
+    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD, D.TD, D.H,
+                       nb, TS, stage_g);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
 
 // the critic's l2 weight gradient from cpl2 (N = 1)
 static int launch_critic_l2_back(const Dims& D, int precision, const float* cpl2, const void* packed_critic, float* gc,
-                                 hipStream_t s) {
+                                 uint32_t* zcnt, const int* zlist, const int* zn, hipStream_t s) {
     const FlatOffsets FC = make_flat_offsets(D.SD, D.HC, 1, 0);
     const MlpLayout L = make_mlp_layout(D.SD, D.HC, 1, 0, precision);
     L2Back l2b = {cpl2, gc + FC.out_b, (const uint8_t*)packed_critic + L.off[SEG_W_OUT], gc + FC.l2_w, gc + FC.l2_b, D.HC, 1,
-                  precision};
+                  precision, zcnt, zlist, zn};
     hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.HC, L2B_ROWS)), dim3(256), 0, s, l2b);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
@@ -890,7 +905,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     // gradients, metrics (actor: 0, 2..15; critic: 1), pl2 | bucket sums, cpl2 | stats
     ZeroArgs z = {};
     const size_t actor_acc = (size_t)((const uint8_t*)(ws.gseg + 16 * D.H) - (const uint8_t*)ws.pl2);
-    const size_t critic_acc = (size_t)((const uint8_t*)(ws.stats + 4) - (const uint8_t*)ws.cpl2);
+    const size_t critic_acc = (size_t)((const uint8_t*)(ws.crow_cnt + 1) - (const uint8_t*)ws.cpl2);   // cpl2 | stats | crow_cnt
     if (parts == 3) {
         z.p[0] = grads; z.n[0] = (FA.count + FC.count) * sizeof(float);
         z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
@@ -904,7 +919,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     } else if (parts == 2) {
         z.p[0] = grads + FA.count; z.n[0] = FC.count * sizeof(float);
         z.p[1] = metrics + 1; z.n[1] = sizeof(double);
-        z.p[2] = ws.cpl2; z.n[2] = (size_t)D.HC * sizeof(float);
+        z.p[2] = ws.cpl2; z.n[2] = critic_acc;
     }
     // few workgroups: the split update runs this while the other stream's row tiles hold most CUs,
     // and a 256-block grid waited ~25 us for slots (DPPO_ZERO_BLOCKS: measurement knob)
@@ -992,22 +1007,24 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
              : precision == DPPO_F16  ? launch_dw<PolicyF16>(w, tk, st) : launch_dw<PolicyF32>(w, tk, st);
     };
 
-    // the critic's distinct samples (sample-weighted value loss, crit_compact_kernel), on the stream
+    // the critic's distinct samples (sample-weighted value loss, crit_rows_kernel), on the stream
     // the critic's half runs on
+    uint32_t* crit_cnt = nullptr;
     auto critic_rows = [&](hipStream_t st) -> int {
         if (!crit_dedup()) return DPPO_OK;
         const int64_t nsamp = total / D.KF;
-        uint32_t* cnt = crit_count_scratch(nsamp, st);
-        DPPO_CHECK(cnt, "dppo_ppo_minibatch: sample-count scratch allocation failed");
+        crit_cnt = crit_count_scratch(nsamp, st);
+        DPPO_CHECK(crit_cnt, "dppo_ppo_minibatch: sample-count scratch allocation failed");
         const int blocks = dppo_cdiv(rows, 256) < 512 ? dppo_cdiv(rows, 256) : 512;
-        hipLaunchKernelGGL(crit_count_kernel, dim3(blocks), dim3(256), 0, st, row_index, start, rows, fk, D.KF, cnt);
+        hipLaunchKernelGGL(crit_rows_kernel, dim3(blocks), dim3(256), 0, st, row_index, start, rows, fk, D.KF, crit_cnt,
+                           ws.crow_n, ws.crow_cnt);
         DPPO_HIP(hipGetLastError());
-        hipLaunchKernelGGL(crit_compact_kernel, dim3(1), dim3(CC_THREADS), 0, st, cnt, (int)nsamp, ws.crow_n, ws.crow_w,
-                           ws.crow_cnt);
-        DPPO_HIP(hipGetLastError());
-        ca.crow_n = ws.crow_n; ca.crow_w = ws.crow_w; ca.crow_cnt = ws.crow_cnt;
+        ca.crow_n = ws.crow_n; ca.crow_mult = crit_cnt; ca.crow_cnt = ws.crow_cnt;
         crit_rows_dev = ws.crow_cnt;
         return DPPO_OK;
+    };
+    auto critic_tail = [&](hipStream_t st) {
+        return launch_critic_l2_back(D, precision, ws.cpl2, packed_critic, gc, crit_cnt, ws.crow_n, ws.crow_cnt, st);
     };
 
     // The critic is independent of the actor: its row tiles and then its weight gradients run on a
@@ -1021,7 +1038,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         rc = launch_grads(false, s);
         if (rc) return rc;
-        return launch_critic_l2_back(D, precision, ws.cpl2, packed_critic, gc, s);
+        return critic_tail(s);
     }
     if (parts == 1 || parts == 4 || parts == 5) {      // the actor's half (or its row tiles / its
         if (parts != 5) {                              // weight gradients) on the caller's stream
@@ -1043,7 +1060,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         rc = launch_grads(false, side->stream);
         if (rc) return rc;
-        rc = launch_critic_l2_back(D, precision, ws.cpl2, packed_critic, gc, side->stream);
+        rc = critic_tail(side->stream);
         if (rc) return rc;
         DPPO_HIP(hipEventRecord(side->join, side->stream));
     }
@@ -1056,7 +1073,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         rc = launch_grads(false, s);
         if (rc) return rc;
-        rc = launch_critic_l2_back(D, precision, ws.cpl2, packed_critic, gc, s);
+        rc = critic_tail(s);
         if (rc) return rc;
     }
     rc = launch_grads(true, s);

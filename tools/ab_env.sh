@@ -1,9 +1,11 @@
 #!/bin/bash
-# A/B of an environment knob on bench.py (no CPU baseline), alternating A B A B.
-# usage: tools/ab_env.sh VAR valA valB [bench args]
+# same-box A/B of an environment knob on the bench: tools/ab_env.sh VAR "A B" [rounds]
 set -o pipefail
-var=$1; a=$2; b=$3; shift 3
-for v in $a $b $a $b; do
-  env $var=$v timeout -k 5 200 python bench.py --no-cpu-baseline "$@" > gpurun_out/ab_env_$v.json || exit 1
-  python3 -c "import json,sys; d=json.load(open('gpurun_out/ab_env_$v.json')); print('$var=$v', round(d['value']), 'roll', round(1e3*d['rollout_s_per_iter'],2), 'upd', round(1e3*d['update_s_per_iter'],2), 'mb', round(d['ppo_minibatch_avg_ms'],4))"
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+var=$1; vals=$2; n=${3:-2}
+for i in $(seq 1 $n); do
+  for v in $vals; do
+    env $var=$v timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/ab_${var}_${v}_$i.log 2>&1 || { tail -20 gpurun_out/ab_${var}_${v}_$i.log; exit 1; }
+    python3 -c "import json,sys; d=json.loads(open('gpurun_out/ab_${var}_${v}_$i.log').read().strip().splitlines()[-1]); print('$var=$v', round(d['value']), 'upd', round(d['update_s_per_iter']*1e3,2), 'mb', round(d['ppo_minibatch_avg_ms'],4), 'roll', round(d['rollout_s_per_iter']*1e3,2))"
+  done
 done
