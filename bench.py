@@ -129,7 +129,9 @@ def kernel_figures(d, S, E, batch, n_mb, precision, path=KERNEL_STATS_CSV):
     out = {"source": os.path.relpath(path, ROOT), "hbm_peak_GBs": HBM_PEAK_GBS}
     # minibatches the profile covers: one actor TRAIN row-tile launch each
     kt = find("actor_rowtile_kernel", "true")
-    n_mb = stats[kt][0] if kt else n_mb
+    n_mb_iter = n_mb                              # minibatches per iteration
+    n_mb = stats[kt][0] if kt else n_mb           # minibatches the profile covers
+    n_iter = max(1, round(n_mb / n_mb_iter)) if n_mb_iter else 1
     N = S * E
     na = d.actor_in * d.actor_hidden + 2 * d.actor_hidden ** 2 + d.actor_hidden * d.xd  # actor weights (MACs/row)
     n_par = None
@@ -176,14 +178,17 @@ def kernel_figures(d, S, E, batch, n_mb, precision, path=KERNEL_STATS_CSV):
         fl = 2 * (na + nc) * batch         # actor + critic weight gradients over the minibatch rows
         out["dw_kernel"] = {"flops_per_minibatch": fl, "us_per_minibatch": tot / n_mb / 1e3,
                             "achieved_TFLOPs": fl / (tot / n_mb) / 1e3, "frac": fl / (tot / n_mb) / 1e3 / peak,
-                            "note": "actor + critic launches summed (the critic runs on distinct samples only, "
-                                    "its algorithmic FLOPs count every row as the reference computes them)"}
+                            "note": "actor + critic launches summed; algorithmic FLOPs as the reference computes "
+                                    "them (every row for the critic, which runs on distinct samples only; l2's "
+                                    "H x H weight gradient, which the kernels form as (u2^T dy) W_out^T)"}
     k = find("actor_rowtile_kernel", "false")
     if k:
         calls, tot, avg = stats[k]
-        fl = 2 * na * N * d.ft_denoising_steps   # the old-log-prob pass over S*E*K' rows
-        out["actor_rowtile_logprob"] = {"flops_per_launch": fl, "avg_us": avg / 1e3,
-                                        "achieved_TFLOPs": fl / avg / 1e3, "frac": fl / avg / 1e3 / peak}
+        fl = 2 * na * N * d.ft_denoising_steps * n_iter   # the old-log-prob pass over S*E*K' rows per iteration
+        out["actor_rowtile_logprob"] = {"flops_per_launch": fl / calls, "launches": calls, "avg_us": avg / 1e3,
+                                        "achieved_TFLOPs": fl / tot / 1e3, "frac": fl / tot / 1e3 / peak,
+                                        "note": "launched in chunks during the rollout (every 10 env steps, beside "
+                                                "the sampler), so the FLOPs are summed over the profile's launches"}
     return out
 
 
