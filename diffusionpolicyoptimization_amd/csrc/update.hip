@@ -840,6 +840,8 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
     L2Back l2b = {pl2, ga + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b, D.H,
                   D.XD, precision, nullptr, nullptr, nullptr};
     DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
+    // (time_bwd forked onto a side stream beside l2_back measured slower: 0.428 vs 0.406 ms per
+    // minibatch, same box, tools/r03_ab2.sh)
     hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
     DPPO_HIP(hipGetLastError());
     size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
