@@ -213,6 +213,10 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     const uint32_t ldm32 = (uint32_t)a.ws.ldm, grow32 = (uint32_t)grow0;
 
     // ---- prologue: rows, gathers, schedule, biases, time embedding for t < K' (actor_ft) ----
+    // Its barriers are LDS-only (lds_sync): a __syncthreads() waits vmcnt(0), i.e. for the primed
+    // weight stream and every gather, at each of the three barriers. Each LDS write below takes its
+    // value from a global load the compiler waits for first, so lgkmcnt(0) + s_barrier publishes
+    // it; the image stores (a0T, seg) stay in flight (only later kernels read them).
     // The weight stream starts first (its latency overlaps everything below). One thread per row
     // maps it through the minibatch permutation (Feistel cycle-walk: done once per row) and
     // fetches the row's per-sample scalars; the chains / obs gathers follow one barrier later.
@@ -256,7 +260,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         pre_m = (float)mean;
         pre_s = (float)(sqrt(var) + 1e-8);
     }
-    __syncthreads();
+    lds_sync();
     for (int i = tid; i < KF * DPPO_SCHED_COLS; i += THREADS) sch[i] = a.sched[i];
     for (int i = tid; i < 3 * H + 16 * NO; i += THREADS) {
         const int seg = i < H ? SEG_B_IN : (i < 2 * H ? SEG_B_L1 : (i < 3 * H ? SEG_B_L2 : SEG_B_OUT));
@@ -286,7 +290,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         const int r = i / SD, c = i % SD, n = rn[r];
         st[i] = n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f;
     }
-    __syncthreads();
+    lds_sync();
     // a0 = [x_prev, temb(t), state] (mlp_diffusion.py:86), t = K'-1-j (diffusion_vpg.py:456-458)
     for (int i = tid; i < ROWS * k1w; i += THREADS) {
         const int r = i / k1w, c = i % k1w;
@@ -307,7 +311,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         }
         if (tid < ROWS) a.ws.seg[grow0 + img_pos(tid)] = rn[tid] >= 0 ? (int8_t)(KF - 1 - rj[tid]) : (int8_t)-1;
     }
-    __syncthreads();
+    lds_sync();
 
     PHASE(0);
     f32x4 acc[MT][NT];
@@ -644,12 +648,12 @@ __device__ __forceinline__ void critic_rowtile_body(const CriticArgs& a) {
         }
         rn[tid] = n;
     }
-    __syncthreads();
+    lds_sync();
     for (int i = tid; i < ROWS * k1w; i += THREADS) {
         const int r = i / k1w, c = i % k1w, n = rn[r];
         a0[r * lda0 + c] = P::cvt((n >= 0 && c < SD) ? a.obs[(size_t)n * SD + c] : 0.f);
     }
-    __syncthreads();
+    lds_sync();
     if (train) {   // csT image (permuted row order, img_pos) from the input tile
         for (int i = tid; i < (ROWS / 8) * SD; i += THREADS) {
             const int c = i / (ROWS / 8), g = i % (ROWS / 8);
