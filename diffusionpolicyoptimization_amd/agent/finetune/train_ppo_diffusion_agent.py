@@ -433,6 +433,22 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 side = self._side
                 side.wait_stream(stream)
                 na = m.n_actor
+            # the per-update arguments of the minibatch and optimizer calls, validated and marshalled
+            # once (host enqueue time per minibatch: an 8-GPU rank runs 255 small ones per iteration)
+            run_mb = m.bind_minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, self.perm_seed,
+                                      rows_local_full, reward_horizon=self.reward_horizon)
+            opt = self.actor_optimizer
+            ng_all = m.grads.numel()
+            if split:
+                step_actor = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
+                                            packs={"actor": (m.actor_ft_params, m.packed_ft)}, defer_sampler_tables=defer)
+                step_critic = opt.bind_range(m.grads, na, ng_all, m.dims, m.precision,
+                                             packs={"critic": (m.critic_params, m.packed_critic)})
+            elif self.max_grad_norm is None:
+                step_all = opt.bind_range(m.grads, 0, ng_all, m.dims, m.precision,
+                                          packs={"actor": (m.actor_ft_params, m.packed_ft),
+                                                 "critic": (m.critic_params, m.packed_critic)},
+                                          defer_sampler_tables=defer)
             k = 0
             for update_epoch in range(self.update_epochs):
                 for batch in range(num_batch):
@@ -448,21 +464,20 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     if self.update_events is not None:
                         ev0 = torch.cuda.Event(enable_timing=True)
                         ev0.record(stream)
-                    mb_args = (obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, self.perm_seed,
-                               update_epoch + 1000 * self.itr, start, rows)
-                    mb_kw = dict(global_rows=global_rows, reward_horizon=self.reward_horizon, adv_stats=stats)
+                    mb_args = (update_epoch + 1000 * self.itr, start, rows)
+                    mb_kw = dict(global_rows=global_rows, adv_stats=stats)
                     met = m.metrics
                     tagged = self.itr >= self.n_critic_warmup_itr
                     if split:
                         met = self._met_dev[k % 2]
                         with torch.cuda.stream(side):
-                            m.minibatch(*mb_args, **mb_kw, part=2, metrics=met)
+                            run_mb(*mb_args, **mb_kw, part=2, metrics=met)
                             if not tagged and not dp:
                                 ev_c = torch.cuda.Event()
                                 ev_c.record(side)
                         if dp:
                             ng = m.grads.numel()
-                            m.minibatch(*mb_args, **mb_kw, part=4, metrics=met)   # actor row tiles
+                            run_mb(*mb_args, **mb_kw, part=4, metrics=met)   # actor row tiles
                             self._ev_rows.record(stream)
                             with torch.cuda.stream(side):          # bucket 1: critic gradients + metrics
                                 side.wait_event(self._ev_rows)
@@ -470,15 +485,15 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                                 self._allreduce(m.grads_ext[na:])
                                 met[:5].copy_(m.grads_ext[ng:ng + 5])
                                 self._ev_met.record(side)
-                            m.minibatch(*mb_args, **mb_kw, part=5, metrics=met)   # actor dW + time MLP
+                            run_mb(*mb_args, **mb_kw, part=5, metrics=met)   # actor dW + time MLP
                             self._allreduce(m.grads_ext[:na])      # bucket 2: actor gradients
                             stream.wait_event(self._ev_met)
                         else:
-                            m.minibatch(*mb_args, **mb_kw, part=1, metrics=met)
+                            run_mb(*mb_args, **mb_kw, part=1, metrics=met)
                             if not tagged:
                                 stream.wait_event(ev_c)
                     else:
-                        m.minibatch(*mb_args, **mb_kw)
+                        run_mb(*mb_args, **mb_kw)
                         if dp:                             # one collective: gradients + metric sums
                             ng = m.grads.numel()
                             m.grads_ext[ng:ng + 5].copy_(m.metrics[:5])
@@ -511,29 +526,24 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     met_out = self._met_map[slot]
                     tag = ctag = 0
                     if tagged:
-                        opt = self.actor_optimizer
                         lr = opt.begin_step()
                         self._mb_tag += 1
                         tag = self._mb_tag
                         if split:
                             ctag = tag
-                            opt.apply_range(m.grads, 0, na, lr, m.dims, m.precision,
-                                            packs={"actor": (m.actor_ft_params, m.packed_ft)},
-                                            metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
-                                            defer_sampler_tables=defer)
+                            step_actor(lr, metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag)
                             with torch.cuda.stream(side):
-                                opt.apply_range(m.grads, na, ng, lr, m.dims, m.precision,
-                                                packs={"critic": (m.critic_params, m.packed_critic)},
-                                                metrics=met[1:2], metrics_out=self._cmet_map[slot].address,
-                                                n_metrics=1, metrics_tag=ctag)
-                        else:
-                            if self.max_grad_norm is not None:
-                                self._clip_by_norm_per_tensor()
+                                step_critic(lr, metrics=met[1:2], metrics_out=self._cmet_map[slot].address,
+                                            n_metrics=1, metrics_tag=ctag)
+                        elif self.max_grad_norm is not None:
+                            self._clip_by_norm_per_tensor()
                             opt.apply_range(m.grads, 0, ng, lr, m.dims, m.precision,
                                             packs={"actor": (m.actor_ft_params, m.packed_ft),
                                                    "critic": (m.critic_params, m.packed_critic)},
                                             metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
                                             defer_sampler_tables=defer)
+                        else:
+                            step_all(lr, metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag)
                     else:
                         torch.from_numpy(met_out.array[:5]).copy_(met[:5])
                     if self.update_events is not None:

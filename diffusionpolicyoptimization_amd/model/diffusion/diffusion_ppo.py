@@ -57,6 +57,24 @@ class PPODiffusion(VPGDiffusion):
                           self.workspace(rows), self.grads, self.metrics if metrics is None else metrics,
                           adv_stats=adv_stats, row_index=row_index, part=part)
 
+    def bind_minibatch(self, obs, chains, lp_old_mean, advantages, returns, perm_seed, max_rows, reward_horizon=4,
+                       loss_scale=1.0):
+        """minibatch() over fixed rollout buffers for a whole update phase, its arguments validated
+        and marshalled once (ops.BoundMinibatch): returns f(epoch, start, rows, global_rows=None,
+        adv_stats=None, part=None, metrics=None). Every minibatch uses the max_rows workspace."""
+        bound = ops.BoundMinibatch(self.dims, self.precision, self.packed_ft, self.packed_critic, self.actor_ft_params,
+                                   self.sched, obs, chains, lp_old_mean, advantages, returns, perm_seed,
+                                   self.workspace(max_rows), self.grads, max_rows)
+        hps = {}
+
+        def run(epoch, start, rows, global_rows=None, adv_stats=None, part=None, metrics=None):
+            g = int(global_rows or rows)
+            hp = hps.get(g)
+            if hp is None:
+                hp = hps[g] = self.hparams(g, reward_horizon, loss_scale)
+            bound(hp, epoch, start, rows, self.metrics if metrics is None else metrics, adv_stats=adv_stats, part=part)
+        return run
+
     def c_loss(self, obs, chains_prev, chains_next, denoising_inds, returns, oldvalues, advantages, oldlogprobs,
                use_bc_loss=False, reward_horizon=4):
         """diffusion_ppo.py:32-132 on an explicit batch. Returns (pg_loss, entropy_loss, v_loss, clipfrac,

@@ -668,6 +668,85 @@ def ppo_minibatch(d: ModelDims, precision, hp, packed_ft, packed_critic, actor_p
         _lib.call("dppo_ppo_minibatch_part", *args, int(part), stream_handle(obs.device))
 
 
+class BoundMinibatch:
+    """ppo_minibatch with the arguments that stay fixed over an update phase (rollout buffers,
+    weights and images, workspace, gradients) validated and marshalled once; a call passes what
+    changes per minibatch. The host's enqueue time per minibatch matters where minibatches are
+    small (an 8-GPU rank's 6,250 rows: ~0.13 ms of GPU time each)."""
+
+    def __init__(self, d: ModelDims, precision, packed_ft, packed_critic, actor_params, sched, obs, chains,
+                 lp_old_mean, advantages, returns, perm_seed, workspace, grads, max_rows):
+        n = obs.shape[0]
+        kf = d.ft_denoising_steps
+        _check(obs, (n, d.sd), torch.float32, "obs")
+        _check(chains, (n, kf + 1, d.xd), torch.float32, "chains")
+        _check(lp_old_mean, (n, kf), torch.float32, "lp_old_mean")
+        _check(advantages, (n,), torch.float32, "advantages")
+        _check(returns, (n,), torch.float32, "returns")
+        na, nc = _n_params(d)
+        _check(actor_params, (na,), torch.float32, "actor_params")
+        _check(grads, (na + nc,), torch.float32, "grads")
+        need = _workspace_bytes(d, _prec(precision), int(max_rows))
+        if workspace.numel() < need:
+            raise ValueError(f"workspace too small: {workspace.numel()} < {need}")
+        self.max_rows = int(max_rows)
+        self._lib = _lib.load()
+        self._dims = _dims_c(d)
+        self._prec = _prec(precision)
+        self._mid = (ptr(packed_ft), ptr(packed_critic), ptr(actor_params), ptr(sched), ptr(obs), ptr(chains),
+                     ptr(lp_old_mean), ptr(advantages), ptr(returns), int(n * kf), ctypes.c_uint64(int(perm_seed)))
+        self._tail = (ptr(workspace), ptr(grads))
+        self._dev = obs.device
+        self._keep = (packed_ft, packed_critic, actor_params, sched, obs, chains, lp_old_mean, advantages, returns,
+                      workspace, grads)   # the pointers above stay valid while this object lives
+
+    def __call__(self, hp, epoch, start, rows, metrics, adv_stats=None, part=None):
+        if not 0 < rows <= self.max_rows:
+            raise ValueError(f"rows {rows} outside (0, {self.max_rows}]")
+        if metrics.dtype != torch.float64 or metrics.numel() < 16:
+            raise ValueError("metrics: expected fp64[16]")
+        args = (ctypes.byref(self._dims), self._prec, ctypes.byref(hp)) + self._mid + (
+            int(epoch), int(start), int(rows), None, ptr(adv_stats)) + self._tail + (ptr(metrics),)
+        st = stream_handle(self._dev)
+        if part is None:
+            rc = self._lib.dppo_ppo_minibatch(*args, st)
+        else:
+            rc = self._lib.dppo_ppo_minibatch_part(*args, int(part), st)
+        if rc != 0:
+            raise _lib.DppoError(f"dppo_ppo_minibatch failed ({rc}): {self._lib.dppo_last_error().decode()}")
+
+
+class BoundOptimizerStep:
+    """optimizer_step over a fixed range and fixed images, validated and marshalled once; a call
+    passes the step, learning rate, metric source and tag (see BoundMinibatch)."""
+
+    def __init__(self, d: ModelDims, precision, params, grads, m, v, weight_decay, beta1, beta2, eps, mode,
+                 actor_params=None, packed_actor=None, critic_params=None, packed_critic=None,
+                 defer_sampler_tables=False):
+        n = params.numel()
+        for t, nm in ((grads, "grads"), (m, "m"), (v, "v")):
+            if t.numel() != n:
+                raise ValueError(f"{nm}: expected {n} elements")
+        self._lib = _lib.load()
+        self._dims = _dims_c(d)
+        mode_i = ((_lib.DPPO_ADAMW_KERAS if mode == "keras" else _lib.DPPO_ADAMW_TORCH) |
+                  (_lib.DPPO_STEP_DEFER_SAMPLER_TABLES if defer_sampler_tables else 0))
+        self._head = (ctypes.byref(self._dims), _prec(precision), ptr(params), ptr(grads), ptr(m), ptr(v), int(n))
+        self._hp = (float(weight_decay), float(beta1), float(beta2), float(eps), mode_i, ptr(actor_params),
+                    ptr(packed_actor), ptr(critic_params), ptr(packed_critic))
+        self._dev = params.device
+        self._keep = (params, grads, m, v, actor_params, packed_actor, critic_params, packed_critic)
+
+    def __call__(self, step, lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0):
+        """metrics_out: a device tensor or a dppo_host_alloc address (as optimizer_step)."""
+        mo = metrics_out if isinstance(metrics_out, int) else (metrics_out.data_ptr() if metrics_out is not None else None)
+        rc = self._lib.dppo_optimizer_step(*self._head, int(step), float(lr), *self._hp, ptr(metrics),
+                                           ctypes.c_void_p(mo) if mo else None, int(n_metrics),
+                                           ctypes.c_uint64(int(metrics_tag)), stream_handle(self._dev))
+        if rc != 0:
+            raise _lib.DppoError(f"dppo_optimizer_step failed ({rc}): {self._lib.dppo_last_error().decode()}")
+
+
 def q_sched_table(schedule):
     """[K][2] fp32 {sqrt(alphas_cumprod), sqrt(1 - alphas_cumprod)}: the q_sample buffers of
     diffusion.py:62-65 (computed in fp32 like the TF buffers)."""
