@@ -408,11 +408,14 @@ def test_deferred_sampler_tables(cuda, precision):
     m = instantiate(cfg.model, device=cuda, seed=0)
     n = m.n_actor
     g = torch.randn(n, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3)) * 0.1
-    M, V = torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    M, V = torch.rand(n, device=cuda) * 1e-3, torch.rand(n, device=cuda) * 1e-6
+    P1, M1, V1 = m.actor_ft_params.clone(), M.clone(), V.clone()
     before = m.packed_ft.clone()
-    ops.optimizer_step(m.dims, m.precision, m.actor_ft_params, g, M, V, 1, 1e-2, 0.004, 0.9, 0.999, 1e-7, "keras",
+    ops.optimizer_step(m.dims, m.precision, m.actor_ft_params, g, M, V, 3, 1e-2, 0.004, 0.9, 0.999, 1e-7, "keras",
                        m.actor_ft_params, m.packed_ft, defer_sampler_tables=True)
+    ops.adamw(P1, g, M1, V1, 3, 1e-2, 0.004, 0.9, 0.999, 1e-7, "keras")   # the step's AdamW is dppo_adamw's
     torch.cuda.synchronize()
+    assert torch.equal(P1, m.actor_ft_params) and torch.equal(M1, M) and torch.equal(V1, V)
     stale = m.packed_ft.clone()
     full = stale.clone()                 # the same bytes in the gaps between segments
     ops.pack_actor(m.dims, m.actor_ft_params, m.precision, out=full)
