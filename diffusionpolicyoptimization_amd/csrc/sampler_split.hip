@@ -108,6 +108,11 @@ extern "C" DPPO_API int dppo_debug_split_cycles(unsigned long long* out, int res
 #ifndef DPPO_SPLIT_POLL
 #define DPPO_SPLIT_POLL 1
 #endif
+// timing probes (tools/variant_build.sh ... -DDPPO_PROBE_NOSYNC=k, results wrong): drop barrier k of a
+// folded-kernel step (1 in-Dense, 2 partial sums, 3 step end)
+#ifndef DPPO_PROBE_NOSYNC
+#define DPPO_PROBE_NOSYNC 0
+#endif
 #ifndef DPPO_SPLIT_POLL_SLEEP
 #define DPPO_SPLIT_POLL_SLEEP 0
 #endif
@@ -1062,7 +1067,9 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
             for (int n = 0; n < NO; ++n) po[n] = Pol::mma(rres[r][n], bh, po[n]);
         }
         XPHASE(11);
+#if DPPO_PROBE_NOSYNC != 1   // timing probe only (wrong actions): drop the in-Dense barrier
         lds_sync();
+#endif
         XPHASE(2);
         // ---- l1 (transposed): n-tile `wave` of this member's output columns over all 512 inputs,
         //      from b_l1; a = relu(h2) feeds the folded l2 + out-Dense (mlp.py:202-206)
@@ -1106,7 +1113,9 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
                 if (16 * n + 4 * jq < XD) *(f32x4*)(part + wave * NV + env * XD + 16 * n + 4 * jq) = po[n];
         }
         XPHASE(14);
+#if DPPO_PROBE_NOSYNC != 2   // timing probe only (wrong actions): drop the partial-sum barrier
         lds_sync();
+#endif
         XPHASE(4);
         // ---- exchange + DDPM epilogue (as the P = 8 kernel; lane = P * slot + member, the member
         //      sum is log2 P DPP levels inside the quad)
@@ -1199,7 +1208,9 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
                 }
             }
         }
+#if DPPO_PROBE_NOSYNC != 3   // timing probe only (wrong actions): drop the step-end barrier
         lds_sync();
+#endif
         XPHASE(6);
     }
     XPHASE(9);
