@@ -16,6 +16,8 @@ LIB_PATH = os.environ.get("DPPO_LIB") or os.path.join(_HERE, "lib", "libdppo_hip
 DPPO_F32, DPPO_BF16, DPPO_F16 = 0, 1, 2
 DPPO_ADAMW_KERAS, DPPO_ADAMW_TORCH = 0, 1
 DPPO_STEP_DEFER_SAMPLER_TABLES = 0x100   # OR'd into dppo_optimizer_step's mode (ABI 7)
+DPPO_STEP_L2_FROM_PL2 = 0x200            # (ABI 8) the actor's l2 gradient arrives factored
+DPPO_PPO_L2_DEFERRED = 1                 # dppo_ppo_hparams.flags (ABI 8)
 SCHED_COLS = 8
 PRECISION = {"fp32": DPPO_F32, "f32": DPPO_F32, "bf16": DPPO_BF16, "fp16": DPPO_F16, "f16": DPPO_F16}
 
@@ -31,7 +33,8 @@ class DppoPpoHparams(ctypes.Structure):
     _fields_ = [("gamma_denoising", ctypes.c_float), ("clip_ploss_coef", ctypes.c_float),
                 ("clip_ploss_coef_base", ctypes.c_float), ("clip_ploss_coef_rate", ctypes.c_float),
                 ("min_logprob_std", ctypes.c_float), ("vf_coef", ctypes.c_float), ("norm_adv", ctypes.c_int32),
-                ("reward_horizon", ctypes.c_int32), ("loss_scale", ctypes.c_float), ("global_rows", ctypes.c_int32)]
+                ("reward_horizon", ctypes.c_int32), ("loss_scale", ctypes.c_float), ("global_rows", ctypes.c_int32),
+                ("flags", ctypes.c_int32)]
 
 
 _P = ctypes.c_void_p
@@ -86,6 +89,7 @@ _SIGNATURES = {
                                  _P, _I, _U64, _P]),
     "dppo_value_moments": (_I, [_P, _P, _I64, _P, _P]),
     "dppo_refresh_sampler_tables": (_I, [_P, _P]),
+    "dppo_materialize_l2": (_I, [_DIMS, _I, _P, _P, _P, _I, _P]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -93,7 +97,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class DppoError(RuntimeError):

@@ -435,20 +435,27 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 na = m.n_actor
             # the per-update arguments of the minibatch and optimizer calls, validated and marshalled
             # once (host enqueue time per minibatch: an 8-GPU rank runs 255 small ones per iteration)
+            # The actor's l2 gradient stays factored (u2^T dy in its own grads region) and the actor's
+            # AdamW launch forms it (DPPO_PPO_L2_DEFERRED + DPPO_STEP_L2_FROM_PL2): one launch fewer
+            # per minibatch. The factored form is linear, so the data-parallel all-reduce is unchanged.
+            # Not with per-tensor gradient clipping (it needs the tensor) or a test hook reading grads.
+            l2_def = (self.max_grad_norm is None and self.minibatch_hook is None
+                      and os.environ.get("DPPO_L2_DEFER", "1") != "0")
             run_mb = m.bind_minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, self.perm_seed,
-                                      rows_local_full, reward_horizon=self.reward_horizon)
+                                      rows_local_full, reward_horizon=self.reward_horizon, l2_deferred=l2_def)
             opt = self.actor_optimizer
             ng_all = m.grads.numel()
             if split:
                 step_actor = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
-                                            packs={"actor": (m.actor_ft_params, m.packed_ft)}, defer_sampler_tables=defer)
+                                            packs={"actor": (m.actor_ft_params, m.packed_ft)}, defer_sampler_tables=defer,
+                                            l2_from_pl2=l2_def)
                 step_critic = opt.bind_range(m.grads, na, ng_all, m.dims, m.precision,
                                              packs={"critic": (m.critic_params, m.packed_critic)})
             elif self.max_grad_norm is None:
                 step_all = opt.bind_range(m.grads, 0, ng_all, m.dims, m.precision,
                                           packs={"actor": (m.actor_ft_params, m.packed_ft),
                                                  "critic": (m.critic_params, m.packed_critic)},
-                                          defer_sampler_tables=defer)
+                                          defer_sampler_tables=defer, l2_from_pl2=l2_def)
             k = 0
             for update_epoch in range(self.update_epochs):
                 for batch in range(num_batch):

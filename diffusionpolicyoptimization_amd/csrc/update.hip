@@ -637,11 +637,37 @@ __global__ void feistel_kernel(int64_t first, int64_t count, FeistelKey fk, int6
 // ---------------------------------------------------------------------------------------------
 // AdamW over a flat fp32 buffer
 // ---------------------------------------------------------------------------------------------
+// DPPO_STEP_L2_FROM_PL2: the actor's l2 gradient in its factored form (DPPO_PPO_L2_DEFERRED): the
+// l2 weight region of g holds pl2 [H][XD]; AdamW forms dW_l2[h][j] = sum_q pl2[h][q] rnd(W_out[j][q])
+// and db_l2[j] = sum_q db_out[q] rnd(W_out[j][q]) itself, in l2_back_cols' order of operations
+struct L2Virt {
+    int on;
+    int64_t w_off, b_off, ob_off;   // l2_w, l2_b, out_b offsets in the optimizer range
+    int H, XD, prec;
+    const uint8_t* wimg;            // the actor image's W_OUT segment (not rewritten before the pack launch)
+};
+__device__ inline float l2_virtual_grad(const float* __restrict__ g, const L2Virt& vt, int64_t i) {
+    const float* pv;
+    int j;
+    if (i < vt.b_off) {        // weight: row h of pl2
+        const int64_t e = i - vt.w_off;
+        const int h = (int)(e / vt.H);
+        j = (int)(e - (int64_t)h * vt.H);
+        pv = g + vt.w_off + (int64_t)h * vt.XD;
+    } else {                   // bias: db_out
+        j = (int)(i - vt.b_off);
+        pv = g + vt.ob_off;
+    }
+    float sum = 0.f;
+    for (int q = 0; q < vt.XD; ++q) sum = fmaf(pv[q], packed_elem(vt.wimg, vt.H, j, q, vt.prec), sum);
+    return sum;
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, int64_t n, float lr, float wd, float b1, float b2,
                                                     float eps, float alpha, float bc1, float bc2, int mode,
                                                     const double* __restrict__ met, double* __restrict__ met_out, int nmet,
-                                                    uint64_t tag) {
+                                                    uint64_t tag, L2Virt vt) {
     // the minibatch's metric sums ride along (dppo_optimizer_step): one launch fewer on the
     // minibatch's critical path than a separate copy. With a tag, met_out[nmet] receives it after
     // the sums (system-scope release), so the host polls host-mapped memory instead of recording
@@ -658,7 +684,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
         }
     }
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        float pi = p[i], gi = g[i], mi = m[i], vi = v[i];
+        float pi = p[i], mi = m[i], vi = v[i];
+        const bool virt = vt.on && i >= vt.w_off && i < vt.b_off + vt.H;   // [l2_w | l2_b] are adjacent
+        const float gi = virt ? l2_virtual_grad(g, vt, i) : g[i];
         if (mode == DPPO_ADAMW_KERAS) {
             // Keras 3: decoupled decay first (variable -= variable*wd*lr), then Adam with
             // m += (g-m)(1-b1); v += (g^2-v)(1-b2); p -= m*alpha/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t)
@@ -678,7 +706,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 
 static int launch_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
                         float weight_decay, float beta1, float beta2, float eps, int mode, const double* met,
-                        double* met_out, int nmet, uint64_t tag, hipStream_t s) {
+                        double* met_out, int nmet, uint64_t tag, hipStream_t s, const L2Virt& vt = L2Virt{}) {
     DPPO_CHECK(n >= 0 && step >= 1, "dppo_adamw: n < 0 or step < 1");
     DPPO_CHECK(mode == DPPO_ADAMW_KERAS || mode == DPPO_ADAMW_TORCH, "dppo_adamw: bad mode");
     DPPO_CHECK(nmet >= 0 && nmet <= 256 && (nmet == 0 || (met && met_out)), "dppo_optimizer_step: bad metrics copy");
@@ -691,7 +719,7 @@ static int launch_adamw(float* params, const float* grads, float* m, float* v, i
     const int64_t blocks64 = (n + 255) / 256;
     const unsigned blocks = (unsigned)(blocks64 < 1 ? 1 : (blocks64 < 4096 ? blocks64 : 4096));
     hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, params, grads, m, v, n, lr,
-                       weight_decay, beta1, beta2, eps, alpha, (float)bc1, (float)bc2, mode, met, met_out, nmet, tag);
+                       weight_decay, beta1, beta2, eps, alpha, (float)bc1, (float)bc2, mode, met, met_out, nmet, tag, vt);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -723,9 +751,21 @@ extern "C" int dppo_optimizer_step(const dppo_dims* d, int precision, float* par
         else (void)hipGetLastError();
     }
     const bool defer = (mode & DPPO_STEP_DEFER_SAMPLER_TABLES) != 0;
-    mode &= ~DPPO_STEP_DEFER_SAMPLER_TABLES;
+    const bool l2v = (mode & DPPO_STEP_L2_FROM_PL2) != 0;
+    mode &= ~(DPPO_STEP_DEFER_SAMPLER_TABLES | DPPO_STEP_L2_FROM_PL2);
+    L2Virt vt = {};
+    if (l2v) {
+        DPPO_CHECK(packed_actor && actor_params == params,
+                   "dppo_optimizer_step: DPPO_STEP_L2_FROM_PL2 needs the actor's image and the actor range first");
+        const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
+        DPPO_CHECK(n >= (int64_t)FA.count, "dppo_optimizer_step: DPPO_STEP_L2_FROM_PL2 needs the whole actor range");
+        DPPO_CHECK(FA.l2_b == FA.l2_w + (size_t)D.H * D.H, "l2 layout");
+        const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+        vt = L2Virt{1, (int64_t)FA.l2_w, (int64_t)FA.l2_b, (int64_t)FA.out_b, D.H, D.XD, precision,
+                    (const uint8_t*)packed_actor + L.off[SEG_W_OUT]};
+    }
     rc = launch_adamw(params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode, metrics, mout,
-                      n_metrics, metrics_tag, s);
+                      n_metrics, metrics_tag, s, vt);
     if (rc) return rc;
     return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s, defer);
 }
@@ -834,7 +874,7 @@ static SideStream* side_stream() {
 // the actor's l2 weight gradient from pl2 (l2_back_kernel: no LDS, so it starts on any CU with a
 // free wave slot), then the time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg)
 static int launch_time_bwd(const Dims& D, int precision, const float* gseg, const float* pl2, const void* packed_actor,
-                           const float* actor_params, float* ga, int nb, int TS, hipStream_t s) {
+                           const float* actor_params, float* ga, int nb, int TS, hipStream_t s, bool l2_back = true) {
     const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
     const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     L2Back l2b = {pl2, ga + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b, D.H,
@@ -842,8 +882,10 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
     DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
     // (time_bwd forked onto a side stream beside l2_back measured slower: 0.428 vs 0.406 ms per
     // minibatch, same box, tools/r03_ab2.sh)
-    hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
-    DPPO_HIP(hipGetLastError());
+    if (l2_back) {
+        hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
+        DPPO_HIP(hipGetLastError());
+    }
     size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
                                   (size_t)nb * (2 * D.TD + 2 * 2 * D.TD));
     DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
@@ -949,6 +991,9 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     // fp16: the backward images carry GRAD_SCALE x the gradient (fp16 range); dW divides it out
     const float gscale = dppo_grad_scale_rows(precision, hp->global_rows);
     lh.grad_scale = hp->loss_scale / (float)hp->global_rows * gscale;
+    DPPO_CHECK((hp->flags & ~DPPO_PPO_L2_DEFERRED) == 0, "dppo_ppo_minibatch: unknown flags 0x%x", hp->flags);
+    // the actor's l2 gradient left factored in its own grads region (include/dppo.h)
+    const bool l2_def = (hp->flags & DPPO_PPO_L2_DEFERRED) != 0;
 
     ActorArgs aa = {};
     aa.packed = (const uint8_t*)packed_ft;
@@ -983,7 +1028,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (actor) {
             add(ws.a0T, D.IN, ws.dh1T, D.H, ga + FA.in_w, EXTRA_ONEHOT, ws.gseg);
             add(ws.u1T, D.H, ws.dh2T, D.H, ga + FA.l1_w, EXTRA_ONES, ga + FA.l1_b);
-            add(ws.u2T, D.H, ws.dyT, D.XD, ws.pl2, EXTRA_NONE, nullptr);   // l2 through the out layer
+            add(ws.u2T, D.H, ws.dyT, D.XD, l2_def ? ga + FA.l2_w : ws.pl2, EXTRA_NONE, nullptr);   // l2 through the out layer
             add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
         } else {
             add(ws.csT, D.SD, ws.cdh1T, D.HC, gc + FC.in_w, EXTRA_ONES, gc + FC.in_b);
@@ -1050,7 +1095,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (parts == 4) return DPPO_OK;
         rc = launch_grads(true, s);
         if (rc) return rc;
-        return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s);
+        return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def);
     }
     SideStream* side = side_stream();
     if (side) {
@@ -1082,7 +1127,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     if (rc) return rc;
     if (side) DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
 
-    return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s);
+    return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def);
 }
 
 extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
@@ -1108,6 +1153,26 @@ extern "C" int dppo_ppo_minibatch_part(const dppo_dims* d, int precision, const 
     return ppo_minibatch_impl(d, precision, hp, packed_ft, packed_critic, actor_params, sched, obs, chains, lp_old_mean,
                               advantages, returns, total, perm_seed, epoch, start, rows, row_index, adv_stats, workspace,
                               grads, metrics, stream, part);
+}
+
+extern "C" int dppo_materialize_l2(const dppo_dims* d, int precision, const void* packed_actor, float* grads,
+                                   void* workspace, int batch_rows, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
+    DPPO_CHECK(packed_actor && grads && workspace && batch_rows > 0, "dppo_materialize_l2: bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    const PpoWorkspace ws = make_ppo_workspace(D, precision, batch_rows, (uint8_t*)workspace);
+    const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
+    DPPO_HIP(hipMemcpyAsync(ws.pl2, grads + FA.l2_w, sizeof(float) * (size_t)D.H * D.XD, hipMemcpyDeviceToDevice, s));
+    const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+    L2Back l2b = {ws.pl2, grads + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], grads + FA.l2_w,
+                  grads + FA.l2_b, D.H, D.XD, precision, nullptr, nullptr, nullptr};
+    DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
+    hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
 }
 
 // ---------------------------------------------------------------------------------------------

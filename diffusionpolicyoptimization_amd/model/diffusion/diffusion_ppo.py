@@ -33,10 +33,10 @@ class PPODiffusion(VPGDiffusion):
         self.metrics = torch.zeros(16, dtype=torch.float64, device=self.device)
         self._ws = {}
 
-    def hparams(self, global_rows, reward_horizon=4, loss_scale=1.0):
+    def hparams(self, global_rows, reward_horizon=4, loss_scale=1.0, l2_deferred=False):
         return ops.ppo_hparams(self.gamma_denoising, self.clip_ploss_coef, self.clip_ploss_coef_base,
                                self.clip_ploss_coef_rate, self.min_logprob_denoising_std, self.vf_coef, self.norm_adv,
-                               reward_horizon, loss_scale, global_rows)
+                               reward_horizon, loss_scale, global_rows, l2_deferred=l2_deferred)
 
     def workspace(self, rows):
         ws = self._ws.get(rows)
@@ -58,10 +58,11 @@ class PPODiffusion(VPGDiffusion):
                           adv_stats=adv_stats, row_index=row_index, part=part)
 
     def bind_minibatch(self, obs, chains, lp_old_mean, advantages, returns, perm_seed, max_rows, reward_horizon=4,
-                       loss_scale=1.0):
+                       loss_scale=1.0, l2_deferred=False):
         """minibatch() over fixed rollout buffers for a whole update phase, its arguments validated
         and marshalled once (ops.BoundMinibatch): returns f(epoch, start, rows, global_rows=None,
-        adv_stats=None, part=None, metrics=None). Every minibatch uses the max_rows workspace."""
+        adv_stats=None, part=None, metrics=None). Every minibatch uses the max_rows workspace.
+        l2_deferred: the actor's l2 gradient stays factored for an optimizer step with l2_from_pl2."""
         bound = ops.BoundMinibatch(self.dims, self.precision, self.packed_ft, self.packed_critic, self.actor_ft_params,
                                    self.sched, obs, chains, lp_old_mean, advantages, returns, perm_seed,
                                    self.workspace(max_rows), self.grads, max_rows)
@@ -71,7 +72,7 @@ class PPODiffusion(VPGDiffusion):
             g = int(global_rows or rows)
             hp = hps.get(g)
             if hp is None:
-                hp = hps[g] = self.hparams(g, reward_horizon, loss_scale)
+                hp = hps[g] = self.hparams(g, reward_horizon, loss_scale, l2_deferred=l2_deferred)
             bound(hp, epoch, start, rows, self.metrics if metrics is None else metrics, adv_stats=adv_stats, part=part)
         return run
 

@@ -631,10 +631,20 @@ def ppo_adv_stats_all(advantages, total, kf, perm_seed, epoch0, n_epochs, rows_f
 
 
 def ppo_hparams(gamma_denoising=0.99, clip_ploss_coef=0.01, clip_ploss_coef_base=0.01, clip_ploss_coef_rate=3.0,
-                min_logprob_std=0.1, vf_coef=0.5, norm_adv=True, reward_horizon=4, loss_scale=1.0, global_rows=1):
+                min_logprob_std=0.1, vf_coef=0.5, norm_adv=True, reward_horizon=4, loss_scale=1.0, global_rows=1,
+                l2_deferred=False):
+    """l2_deferred (ABI 8, DPPO_PPO_L2_DEFERRED): the actor's l2 gradient is left factored in grads
+    for an optimizer step with l2_from_pl2 (or materialize_l2)."""
     return _lib.DppoPpoHparams(float(gamma_denoising), float(clip_ploss_coef), float(clip_ploss_coef_base),
                                float(clip_ploss_coef_rate), float(min_logprob_std), float(vf_coef), int(bool(norm_adv)),
-                               int(reward_horizon), float(loss_scale), int(global_rows))
+                               int(reward_horizon), float(loss_scale), int(global_rows),
+                               _lib.DPPO_PPO_L2_DEFERRED if l2_deferred else 0)
+
+
+def materialize_l2(d: ModelDims, precision, packed_actor, grads, workspace, batch_rows):
+    """The actor's l2 gradient of an l2_deferred minibatch formed in place (dppo_materialize_l2)."""
+    _lib.call("dppo_materialize_l2", ctypes.byref(_dims_c(d)), _prec(precision), ptr(packed_actor), ptr(grads),
+              ptr(workspace), int(batch_rows), stream_handle(grads.device))
 
 
 def ppo_minibatch(d: ModelDims, precision, hp, packed_ft, packed_critic, actor_params, sched, obs, chains, lp_old_mean,
@@ -722,7 +732,7 @@ class BoundOptimizerStep:
 
     def __init__(self, d: ModelDims, precision, params, grads, m, v, weight_decay, beta1, beta2, eps, mode,
                  actor_params=None, packed_actor=None, critic_params=None, packed_critic=None,
-                 defer_sampler_tables=False):
+                 defer_sampler_tables=False, l2_from_pl2=False):
         n = params.numel()
         for t, nm in ((grads, "grads"), (m, "m"), (v, "v")):
             if t.numel() != n:
@@ -730,7 +740,8 @@ class BoundOptimizerStep:
         self._lib = _lib.load()
         self._dims = _dims_c(d)
         mode_i = ((_lib.DPPO_ADAMW_KERAS if mode == "keras" else _lib.DPPO_ADAMW_TORCH) |
-                  (_lib.DPPO_STEP_DEFER_SAMPLER_TABLES if defer_sampler_tables else 0))
+                  (_lib.DPPO_STEP_DEFER_SAMPLER_TABLES if defer_sampler_tables else 0) |
+                  (_lib.DPPO_STEP_L2_FROM_PL2 if l2_from_pl2 else 0))
         self._head = (ctypes.byref(self._dims), _prec(precision), ptr(params), ptr(grads), ptr(m), ptr(v), int(n))
         self._hp = (float(weight_decay), float(beta1), float(beta2), float(eps), mode_i, ptr(actor_params),
                     ptr(packed_actor), ptr(critic_params), ptr(packed_critic))

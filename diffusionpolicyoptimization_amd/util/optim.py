@@ -52,7 +52,7 @@ class AdamW:
                            ap, pa, cp, pc, metrics, metrics_out, n_metrics, metrics_tag,
                            defer_sampler_tables=defer_sampler_tables)
 
-    def bind_range(self, grads, lo, hi, dims, precision, packs=(), defer_sampler_tables=False):
+    def bind_range(self, grads, lo, hi, dims, precision, packs=(), defer_sampler_tables=False, l2_from_pl2=False):
         """apply_range over a fixed range and fixed images, validated and marshalled once
         (ops.BoundOptimizerStep): returns f(lr, metrics=None, metrics_out=None, n_metrics=0,
         metrics_tag=0) for the step begin_step() opened."""
@@ -61,7 +61,7 @@ class AdamW:
         cp, pc = pk.get("critic", (None, None))
         b = ops.BoundOptimizerStep(dims, precision, self.params[lo:hi], grads[lo:hi], self.m[lo:hi], self.v[lo:hi],
                                    self.weight_decay, self.beta_1, self.beta_2, self.epsilon, self.mode, ap, pa, cp,
-                                   pc, defer_sampler_tables=defer_sampler_tables)
+                                   pc, defer_sampler_tables=defer_sampler_tables, l2_from_pl2=l2_from_pl2)
 
         def step(lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0):
             b(self.iterations, lr, metrics, metrics_out, n_metrics, metrics_tag)

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 7
+#define DPPO_ABI_VERSION 8
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -50,6 +50,10 @@ enum { DPPO_ADAMW_KERAS = 0, DPPO_ADAMW_TORCH = 1 };
  * re-derives them on its own stream first, or dppo_refresh_sampler_tables does it explicitly. The
  * actor parameters must stay allocated and unchanged until then (they are read at the refresh). */
 enum { DPPO_STEP_DEFER_SAMPLER_TABLES = 0x100 };
+/* ABI 8, OR'd into dppo_optimizer_step's mode: the actor's l2 gradient in grads is in the factored
+ * form of DPPO_PPO_L2_DEFERRED; AdamW forms it from pl2, db_out and the actor image's rnd(W_out)
+ * (needs actor_params == params and packed_actor). */
+enum { DPPO_STEP_L2_FROM_PL2 = 0x200 };
 
 /* Model / schedule dimensions (cfg keys of cfg/gym/finetune/hopper-v2/ft_ppo_diffusion_mlp.yaml:18-25,78-110). */
 typedef struct dppo_dims {
@@ -235,7 +239,17 @@ typedef struct dppo_ppo_hparams {
     int32_t norm_adv, reward_horizon;
     float loss_scale;       /* multiplies 1/b (= 1/world_size for a DP all-reduce-sum) */
     int32_t global_rows;    /* b used in the 1/b means (rows over all ranks) */
+    int32_t flags;          /* ABI 8: DPPO_PPO_* below (0: every gradient materialised) */
 } dppo_ppo_hparams;
+
+/* ABI 8, dppo_ppo_hparams.flags. DPPO_PPO_L2_DEFERRED: the actor's l2 gradient is left in its
+ * factored form. The l2 weight region of grads holds pl2 = u2^T dy as [H][XD] (row-major, the rest
+ * of the region zero) and the l2 bias region is zero; the true values are pl2 rnd(W_out)^T and
+ * db_out rnd(W_out)^T (the block's output feeds only the linear out layer). A following
+ * dppo_optimizer_step with DPPO_STEP_L2_FROM_PL2 forms them inside its AdamW launch (one launch
+ * fewer per minibatch); dppo_materialize_l2 forms them in place. The factored form is linear, so a
+ * data-parallel caller all-reduces it like the other gradients. */
+enum { DPPO_PPO_L2_DEFERRED = 1 };
 
 DPPO_API size_t dppo_ppo_workspace_bytes(const dppo_dims* d, int precision, int batch_rows);
 DPPO_API int dppo_ppo_adv_stats(const float* advantages, int64_t total, int K_ft, uint64_t perm_seed, int epoch,
@@ -308,6 +322,12 @@ DPPO_API int dppo_pack_all(const dppo_dims* d, int precision, const float* actor
  * double metrics_out[n_metrics] AFTER the n_metrics sums (system-scope release), so a host polling
  * host-mapped metrics_out for the tag reads complete sums without recording or waiting on an event
  * (metrics_out then holds n_metrics + 1 doubles; pass 0 for no tag). */
+/* ABI 8: the actor's l2 gradient of a DPPO_PPO_L2_DEFERRED minibatch, formed in place in grads (the
+ * actor range first) from the factored form; workspace = the minibatch's (its pl2 slot is the
+ * staging copy). */
+DPPO_API int dppo_materialize_l2(const dppo_dims* d, int precision, const void* packed_actor, float* grads,
+                                 void* workspace, int batch_rows, void* stream);
+
 /* Enqueue the split-sampler tables of an actor image on `stream` if an optimizer step with
  * DPPO_STEP_DEFER_SAMPLER_TABLES left them stale; a no-op otherwise (ABI 7). */
 DPPO_API int dppo_refresh_sampler_tables(const void* packed_actor, void* stream);

@@ -433,6 +433,56 @@ def test_deferred_sampler_tables(cuda, precision):
     assert torch.equal(a_deferred, a_full)
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_l2_deferred_minibatch_and_step(cuda, precision):
+    """ABI 8: a minibatch with DPPO_PPO_L2_DEFERRED leaves the actor's l2 gradient factored; formed in
+    place (dppo_materialize_l2) it equals the plain minibatch's gradient (up to the dW's float-atomic
+    order), and an optimizer step with DPPO_STEP_L2_FROM_PL2 on the factored gradient gives exactly
+    the parameters, moments and image of a plain step on the materialised one."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp_64env",
+                      [f"model.precision={precision}"])
+    m = instantiate(cfg.model, device=cuda, seed=0)
+    d = m.dims
+    N, kf, rows = 64 * 40, d.ft_denoising_steps, 3000
+    gen = torch.Generator(device=cuda).manual_seed(0)
+    obs = torch.rand(N, d.sd, device=cuda, generator=gen) * 2 - 1
+    chains = torch.randn(N, kf + 1, d.xd, device=cuda, generator=gen) * 0.5
+    adv = torch.randn(N, device=cuda, generator=gen)
+    ret = torch.randn(N, device=cuda, generator=gen)
+    lp_old = torch.empty(N, kf, device=cuda)
+    ops.logprob(d, m.precision, m.packed_ft, m.sched, obs, chains, want_elem=False, lp_mean=lp_old)
+    lp_old += 0.01 * torch.randn(N, kf, device=cuda, generator=gen)
+    run = {}
+    for deferred in (False, True):
+        f = m.bind_minibatch(obs, chains, lp_old, adv, ret, 11, rows, l2_deferred=deferred)
+        f(3, 0, rows)
+        torch.cuda.synchronize()
+        run[deferred] = m.grads.clone()
+    g_plain, g_def = run[False], run[True]
+    g_mat = g_def.clone()
+    ops.materialize_l2(d, m.precision, m.packed_ft, g_mat, m.workspace(rows), rows)
+    torch.cuda.synchronize()
+    scale = g_plain.abs().max()
+    assert (g_mat - g_plain).abs().max() <= 1e-5 * scale, float((g_mat - g_plain).abs().max() / scale)
+    na = m.n_actor
+    gen2 = torch.Generator(device=cuda).manual_seed(1)
+    M0 = torch.rand(na, device=cuda, generator=gen2) * 1e-4
+    V0 = torch.rand(na, device=cuda, generator=gen2) * 1e-7
+    out = {}
+    for virt, g in ((True, g_def), (False, g_mat)):
+        P, M, V, img = m.actor_ft_params.clone(), M0.clone(), V0.clone(), m.packed_ft.clone()
+        step = ops.BoundOptimizerStep(d, m.precision, P, g[:na], M, V, 0.004, 0.9, 0.999, 1e-7, "keras", P, img,
+                                      l2_from_pl2=virt)
+        step(2, 1e-3)
+        torch.cuda.synchronize()
+        out[virt] = (P, M, V, img)
+    for a, b in zip(out[True], out[False]):
+        assert torch.equal(a, b)
+
+
 def test_value_moments(cuda):
     import torch
     from diffusionpolicyoptimization_amd import ops
