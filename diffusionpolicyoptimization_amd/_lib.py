@@ -18,6 +18,7 @@ DPPO_ADAMW_KERAS, DPPO_ADAMW_TORCH = 0, 1
 DPPO_STEP_DEFER_SAMPLER_TABLES = 0x100   # OR'd into dppo_optimizer_step's mode (ABI 7)
 DPPO_STEP_L2_FROM_PL2 = 0x200            # (ABI 8) the actor's l2 gradient arrives factored
 DPPO_PPO_L2_DEFERRED = 1                 # dppo_ppo_hparams.flags (ABI 8)
+DPPO_PPO_LEARN_ETA = 2                   # (ABI 9) d loss / d eta into metrics[8]
 SCHED_COLS = 8
 PRECISION = {"fp32": DPPO_F32, "f32": DPPO_F32, "bf16": DPPO_BF16, "fp16": DPPO_F16, "f16": DPPO_F16}
 
@@ -84,6 +85,7 @@ _SIGNATURES = {
                                     _P, _I64, _U64, _I, _I64, _I, _P, _P, _P, _P, _P, _I, _P]),
     "dppo_feistel_permute": (_I, [_I64, _I64, _I64, _U64, _I, _P, _P]),
     "dppo_adamw": (_I, [_P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P]),
+    "dppo_eta_step": (_I, [_P, _P, _I64, _F, _F, _F, _F, _F, _I, _F, _F, _P, _P, _I, _P, _P]),
     "dppo_pack_all": (_I, [_DIMS, _I, _P, _P, _P, _P, _P]),
     "dppo_optimizer_step": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P, _P,
                                  _P, _I, _U64, _P]),
@@ -97,7 +99,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class DppoError(RuntimeError):

@@ -22,6 +22,7 @@ import torch.distributed as dist
 
 from ... import ops
 from ...util.dist import allreduce_sum_, explained_variance_from_moments
+from ...util.scheduler import CosineAnnealingWarmupRestarts
 from ...util.timer import Timer
 from .train_ppo_agent import TrainPPOAgent
 
@@ -59,6 +60,16 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         super().__init__(cfg)
         self.reward_horizon = cfg.get("reward_horizon", self.act_steps)
         self.learn_eta = self.model.learn_eta
+        if self.learn_eta:
+            # the eta AdamW of agent :28-45 (Keras defaults, its own cosine-warmup schedule evaluated at
+            # the eta optimizer's step count), stepped every eta_update_interval minibatches as the
+            # commented-out :358-359 (the original DPPO's schedule); PARITY UNPINNED
+            el = cfg.train.eta_lr_scheduler
+            self.eta_update_interval = int(cfg.train.eta_update_interval)
+            self.eta_lr_scheduler = CosineAnnealingWarmupRestarts(
+                first_cycle_steps=el.first_cycle_steps, cycle_mult=1.0, max_lr=cfg.train.eta_lr, min_lr=el.min_lr,
+                warmup_steps=el.warmup_steps, gamma=1.0)
+            self.eta_weight_decay = float(cfg.train.get("eta_weight_decay", 0.004))
         self.perm_seed = int(cfg.train.get("perm_seed", self.seed * 1_000_003 + 17)) + 7919 * self.rank
         self.timing = {"rollout_s": 0.0, "update_s": 0.0, "n_updates": 0, "env_steps": 0, "iters": 0}
         self.emulate_world = max(1, int(cfg.train.get("emulate_world", 1)))
@@ -383,6 +394,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 self._ev_m = [torch.cuda.Event() for _ in range(2)]
                 self._mb_tag = 0
             pending = None
+            eta_now = m.current_eta()   # c_loss's eta metric (diffusion_ppo.py:131), as of the update's start
 
             def finish(p):
                 slot, ev, grows, _, tag, ctag = p
@@ -398,8 +410,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     met = self._met_map[slot].array[:5] / grows
                 self.timing["n_updates"] += 1
                 inf = dict(pg_loss=float(met[0]), v_loss=float(met[1]), approx_kl=float(met[2]),
-                           clipfrac=float(met[3]), ratio=float(met[4]), bc_loss=0.0, eta=1.0,
-                           entropy_loss=-1.0, loss=float(met[0] + self.vf_coef * met[1]))
+                           clipfrac=float(met[3]), ratio=float(met[4]), bc_loss=0.0, eta=eta_now,
+                           entropy_loss=-eta_now, loss=float(met[0] + self.vf_coef * met[1]))
                 clipfracs.append(inf["clipfrac"])
                 return inf, self.target_kl is not None and inf["approx_kl"] > self.target_kl
 
@@ -489,8 +501,10 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             with torch.cuda.stream(side):          # bucket 1: critic gradients + metrics
                                 side.wait_event(self._ev_rows)
                                 m.grads_ext[ng:ng + 5].copy_(met[:5])
+                                m.grads_ext[ng + 5:ng + 6].copy_(met[8:9])   # learn_eta: d loss / d eta
                                 self._allreduce(m.grads_ext[na:])
                                 met[:5].copy_(m.grads_ext[ng:ng + 5])
+                                met[8:9].copy_(m.grads_ext[ng + 5:ng + 6])
                                 self._ev_met.record(side)
                             run_mb(*mb_args, **mb_kw, part=5, metrics=met)   # actor dW + time MLP
                             self._allreduce(m.grads_ext[:na])      # bucket 2: actor gradients
@@ -504,8 +518,10 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         if dp:                             # one collective: gradients + metric sums
                             ng = m.grads.numel()
                             m.grads_ext[ng:ng + 5].copy_(m.metrics[:5])
+                            m.grads_ext[ng + 5:ng + 6].copy_(m.metrics[8:9])
                             self._allreduce(m.grads_ext)
                             m.metrics[:5].copy_(m.grads_ext[ng:ng + 5])
+                            m.metrics[8:9].copy_(m.grads_ext[ng + 5:ng + 6])
                     if self.minibatch_hook is not None:
                         if split:
                             stream.wait_stream(side)
@@ -551,6 +567,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                                             defer_sampler_tables=defer)
                         else:
                             step_all(lr, metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag)
+                        if self.learn_eta and batch % self.eta_update_interval == 0:   # :358-359
+                            m.eta_optimizer_step(met, self.eta_lr_scheduler(m.eta_step_count), self.eta_weight_decay)
                     else:
                         torch.from_numpy(met_out.array[:5]).copy_(met[:5])
                     if self.update_events is not None:

@@ -70,6 +70,7 @@ struct LossHP {
     float gamma_denoising, clip_coef, clip_coef_base, clip_coef_rate, min_lp_std, vf_coef;
     int norm_adv, reward_horizon;
     float grad_scale;     // loss_scale / global_rows
+    float eta_unscale;    // learnable DDIM eta (DPPO_PPO_LEARN_ETA): 1 / the fp16 seed scale, else 0
 };
 
 struct ActorArgs {

@@ -494,6 +494,8 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     // fastest so the dyT image stores coalesce
     AT* dyt = a0;   // a0 tile is dead after L1; dy tile has row stride lda0
     float sq = 0.f;                      // pretrain: this thread's sum of (eps - noise)^2
+    float geta = 0.f;                    // learnable DDIM eta: this thread's share of d loss / d eta
+    const bool leta = a.hp.eta_unscale != 0.f;
     for (int idx = tid; idx < ROWS * ktw; idx += THREADS) {
         const int q = idx / ROWS, r = idx % ROWS;
         float d = 0.f;
@@ -513,14 +515,38 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
             const float sd = row_sd(r);
             const float* sc = sch + (KF - 1 - rj[r]) * DPPO_SCHED_COLS;
             const float dlp = (lp >= -5.f && lp <= 2.f) ? e_dn[r] / (float)nh : 0.f;
-            const float dmu = dlp * (xn[r * XD + q] - e_mu[e]) / (sd * sd);
+            const float res = xn[r * XD + q] - e_mu[e];
+            const float dmu = dlp * res / (sd * sd);
             d = e_uc[e] != 0.f ? -sc[1] * sc[2] * dmu : 0.f;
+            if (leta) {
+                // DDIM row (include/dppo.h): mu = sqrt(abar_prev) x0 + dd eps', sigma = max(eta s, 1e-10),
+                // dd = sqrt(clip(1 - abar_prev - sigma^2, 0, 1e6)); d mu / d eta = (d dd / d eta) eps' with
+                // eps' = (x - sqrt(abar) x0) / sqrt(1 - abar) = (x - x0 / c0) c0 / c1, dd = c3 c1 / c0;
+                // d std / d eta = s where sigma is neither clamped nor clipped (oracle ddim_eta_grad_terms)
+                const float s = sc[7];
+                const float sig = expf(0.5f * sc[4]);
+                const float x = xp[r * XD + q];
+                float eps = bo[q];   // the out-layer partials in tB are still live (as in the pretrain branch)
+#pragma unroll
+                for (int w = 0; w < WAVES; ++w) eps += part[(w * ROWS + r) * (16 * NO) + q];
+                const float x0 = fminf(fmaxf(sc[0] * x - sc[1] * eps, -1.f), 1.f);
+                const float ep2 = (x - x0 / sc[0]) * sc[0] / sc[1];
+                const float dd = sc[3] * sc[1] / sc[0];
+                const bool free_sig = sig > 1e-10f * 1.0001f;
+                const float ddd = (dd > 0.f && free_sig) ? -sig * s / dd : 0.f;
+                const float dstd = (free_sig && sig > a.hp.min_lp_std && sig < 1e6f) ? s : 0.f;
+                geta += dlp * (res / (sd * sd) * ddd * ep2 + (res * res / (sd * sd * sd) - 1.f / sd) * dstd);
+            }
         }
         dyt[r * lda0 + q] = P::cvt(d);
     }
     if (pre) {
         sq = wave_sum(sq);
         if (lane == 0) atomic_add_metric(a.metrics, 0, sq);
+    }
+    if (leta) {   // d loss / d eta (with the loss's 1/b and loss_scale; the fp16 seed scale divided out)
+        geta = wave_sum(geta);
+        if (lane == 0 && geta != 0.f) atomic_add_metric(a.metrics, 8, (double)geta * (double)a.hp.eta_unscale);
     }
     lds_sync();
     for (int i = tid; i < (ROWS / 8) * XD; i += THREADS) {   // dyT image from the dy tile

@@ -770,6 +770,77 @@ extern "C" int dppo_optimizer_step(const dppo_dims* d, int precision, float* par
     return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s, defer);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Learnable DDIM eta (§8(f) row 4; the original DPPO's EtaFixed, parity unpinned: the reference's
+// eta module is absent and its eta step is commented out, train_ppo_diffusion_agent.py:28-45,
+// 358-359). state = {logit, m, v}; eta = eta_min + (eta_max - eta_min) (tanh(logit) + 1) / 2.
+// One workgroup: thread 0 applies AdamW to the logit with d loss / d logit = metrics[8] d eta / d
+// logit (metrics[8] = d loss / d eta from the DPPO_PPO_LEARN_ETA row tiles), then one thread per
+// DDIM row rewrites the eta-dependent schedule columns c2, c3, logvar in ddim_buffers' fp32 order of
+// operations (model/diffusion/sampling.py), from the eta-independent base rows
+// {abar_prev, sqrt(abar_prev), sqrt(abar), sqrt(1 - abar), s}.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void eta_step_kernel(float* __restrict__ st, const double* __restrict__ met, int apply,
+                                                     float lr, float wd, float b1, float b2, float eps, float alpha,
+                                                     float bc1, float bc2, int mode, float emin, float emax,
+                                                     const float* __restrict__ base, float* __restrict__ sched, int S,
+                                                     float* __restrict__ eta_out) {
+    __shared__ float eta_s;
+    if (threadIdx.x == 0) {
+        float th = st[0];
+        if (apply) {
+            const float tn = tanhf(th);
+            const float gi = (float)met[8] * (0.5f * (emax - emin) * (1.f - tn * tn));
+            float mi = st[1], vi = st[2];
+            if (mode == DPPO_ADAMW_KERAS) {
+                th -= th * wd * lr;
+                mi += (gi - mi) * (1.f - b1);
+                vi += (gi * gi - vi) * (1.f - b2);
+                th -= (mi * alpha) / (sqrtf(vi) + eps);
+            } else {
+                th *= 1.f - lr * wd;
+                mi = b1 * mi + (1.f - b1) * gi;
+                vi = b2 * vi + (1.f - b2) * gi * gi;
+                th -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+            }
+            st[0] = th; st[1] = mi; st[2] = vi;
+        }
+        const float e = emin + (emax - emin) * (0.5f * (tanhf(th) + 1.f));
+        eta_s = e;
+        if (eta_out) *eta_out = e;
+    }
+    __syncthreads();
+    const int j = threadIdx.x;
+    if (j < S) {
+        const float* b = base + 5 * j;   // abar_prev, sqrt(abar_prev), sqrt(abar), sqrt(1 - abar), s
+        const float sig = fmaxf(__fmul_rn(eta_s, b[4]), 1e-10f);
+        const float in = __fsub_rn(__fsub_rn(1.f, b[0]), __fmul_rn(sig, sig));
+        const float dd = sqrtf(fminf(fmaxf(in, 0.f), 1e6f));
+        float* r = sched + (size_t)j * DPPO_SCHED_COLS;
+        r[2] = __fsub_rn(b[1], __fdiv_rn(__fmul_rn(dd, b[2]), b[3]));
+        r[3] = __fdiv_rn(dd, b[3]);
+        r[4] = logf(__fmul_rn(sig, sig));
+    }
+}
+
+extern "C" int dppo_eta_step(float* eta_state, const double* metrics, int64_t step, float lr, float weight_decay,
+                             float beta1, float beta2, float eps, int mode, float eta_min, float eta_max,
+                             const float* ddim_base, float* sched, int ddim_steps, float* eta_out, void* stream) {
+    DPPO_CHECK(eta_state && ddim_base && sched, "dppo_eta_step: null pointer");
+    DPPO_CHECK(ddim_steps >= 1 && ddim_steps <= 64, "dppo_eta_step: ddim_steps %d outside [1, 64]", ddim_steps);
+    DPPO_CHECK(eta_max > eta_min, "dppo_eta_step: eta_max must exceed eta_min");
+    DPPO_CHECK(mode == DPPO_ADAMW_KERAS || mode == DPPO_ADAMW_TORCH, "dppo_eta_step: bad mode");
+    const int apply = metrics != nullptr && step >= 1;
+    const double bc1 = apply ? 1.0 - pow((double)beta1, (double)step) : 1.0;
+    const double bc2 = apply ? 1.0 - pow((double)beta2, (double)step) : 1.0;
+    const float alpha = (float)((double)lr * sqrt(bc2) / bc1);
+    hipLaunchKernelGGL(eta_step_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, eta_state, metrics, apply, lr,
+                       weight_decay, beta1, beta2, eps, alpha, (float)bc1, (float)bc2, mode, eta_min, eta_max, ddim_base,
+                       sched, ddim_steps, eta_out);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
 extern "C" int dppo_pack_all(const dppo_dims* d, int precision, const float* actor_params, void* packed_actor,
                              const float* critic_params, void* packed_critic, void* stream) {
     Dims D;
@@ -991,7 +1062,9 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     // fp16: the backward images carry GRAD_SCALE x the gradient (fp16 range); dW divides it out
     const float gscale = dppo_grad_scale_rows(precision, hp->global_rows);
     lh.grad_scale = hp->loss_scale / (float)hp->global_rows * gscale;
-    DPPO_CHECK((hp->flags & ~DPPO_PPO_L2_DEFERRED) == 0, "dppo_ppo_minibatch: unknown flags 0x%x", hp->flags);
+    DPPO_CHECK((hp->flags & ~(DPPO_PPO_L2_DEFERRED | DPPO_PPO_LEARN_ETA)) == 0, "dppo_ppo_minibatch: unknown flags 0x%x",
+               hp->flags);
+    lh.eta_unscale = (hp->flags & DPPO_PPO_LEARN_ETA) ? 1.f / gscale : 0.f;
     // the actor's l2 gradient left factored in its own grads region (include/dppo.h)
     const bool l2_def = (hp->flags & DPPO_PPO_L2_DEFERRED) != 0;
 
@@ -1111,9 +1184,9 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         DPPO_HIP(hipEventRecord(side->join, side->stream));
     }
-    rc = launch_actor_rowtile(aa, precision, s);
-    if (rc) return rc;
     if (!side) {
+        rc = launch_actor_rowtile(aa, precision, s);
+        if (rc) return rc;
         rc = critic_rows(s);
         if (rc) return rc;
         rc = launch_critic_rowtile(ca, precision, s);
@@ -1122,10 +1195,15 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         rc = critic_tail(s);
         if (rc) return rc;
+        rc = launch_grads(true, s);
+        if (rc) return rc;
+    } else {
+        rc = launch_actor_rowtile(aa, precision, s);
+        if (rc) return rc;
+        rc = launch_grads(true, s);
+        if (rc) return rc;
+        DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
     }
-    rc = launch_grads(true, s);
-    if (rc) return rc;
-    if (side) DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
 
     return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def);
 }

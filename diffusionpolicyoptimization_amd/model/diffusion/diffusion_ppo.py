@@ -12,6 +12,7 @@ from .diffusion_vpg import VPGDiffusion, _as_state
 
 # metrics slots written by the kernels (sums over rows; see update.hip)
 M_PG, M_VLOSS, M_KL, M_CLIPFRAC, M_RATIO = 0, 1, 2, 3, 4
+M_DETA = 8   # learn_eta: d loss / d eta (DPPO_PPO_LEARN_ETA)
 
 
 class PPODiffusion(VPGDiffusion):
@@ -36,7 +37,8 @@ class PPODiffusion(VPGDiffusion):
     def hparams(self, global_rows, reward_horizon=4, loss_scale=1.0, l2_deferred=False):
         return ops.ppo_hparams(self.gamma_denoising, self.clip_ploss_coef, self.clip_ploss_coef_base,
                                self.clip_ploss_coef_rate, self.min_logprob_denoising_std, self.vf_coef, self.norm_adv,
-                               reward_horizon, loss_scale, global_rows, l2_deferred=l2_deferred)
+                               reward_horizon, loss_scale, global_rows, l2_deferred=l2_deferred,
+                               learn_eta=self.learn_eta)
 
     def workspace(self, rows):
         ws = self._ws.get(rows)
@@ -101,5 +103,8 @@ class PPODiffusion(VPGDiffusion):
         row_index = (r * kf + j).contiguous()
         self.minibatch(state, ch, lp_old, adv, ret, 0, 0, 0, b, reward_horizon=reward_horizon, row_index=row_index)
         m = (self.metrics[:5] / b).cpu().numpy()
-        return (float(m[M_PG]), -1.0, float(m[M_VLOSS]), float(m[M_CLIPFRAC]), float(m[M_KL]), float(m[M_RATIO]),
-                0.0, 1.0)
+        eta = self.current_eta()
+        # entropy_loss = -mean(eta), the last element mean(eta) (diffusion_ppo.py:49, 131); with
+        # learn_eta, d loss / d eta is left in self.metrics[M_DETA]
+        return (float(m[M_PG]), -eta, float(m[M_VLOSS]), float(m[M_CLIPFRAC]), float(m[M_KL]), float(m[M_RATIO]),
+                0.0, eta)

@@ -32,10 +32,10 @@ class VPGDiffusion(DiffusionModel):
     def __init__(self, actor, critic, ft_denoising_steps, ft_denoising_steps_d=0, ft_denoising_steps_t=0,
                  network_path=None, min_sampling_denoising_std=0.1, min_logprob_denoising_std=0.1, eta=None,
                  learn_eta=False, **kwargs):
-        if learn_eta:
-            raise NotImplementedError("learn_eta: the reference's eta module is absent from it (model/diffusion/"
-                                      "eta.py is not in the repository); a fixed eta (EtaFixed) is supported")
-        super().__init__(network=actor, network_path=network_path, ddim_eta=self._fixed_eta(eta), **kwargs)
+        eta_cfg = self._eta_config(eta)
+        super().__init__(network=actor, network_path=network_path, ddim_eta=eta_cfg["base_eta"], **kwargs)
+        # "Cannot learn eta with DDPM." (diffusion_vpg.py:52)
+        assert not (learn_eta and not self.use_ddim), "Cannot learn eta with DDPM."
         assert ft_denoising_steps <= self.sampling_steps
         self.ft_denoising_steps = int(ft_denoising_steps)
         self.ft_denoising_steps_d = ft_denoising_steps_d
@@ -43,7 +43,9 @@ class VPGDiffusion(DiffusionModel):
         self.ft_denoising_steps_cnt = 0
         self.min_sampling_denoising_std = min_sampling_denoising_std
         self.min_logprob_denoising_std = min_logprob_denoising_std
-        self.learn_eta = False
+        self.learn_eta = bool(learn_eta)
+        if self.learn_eta:
+            self._init_learnable_eta(eta_cfg)
         self.actor = actor
         self.critic = critic
         critic._owner = self
@@ -79,16 +81,55 @@ class VPGDiffusion(DiffusionModel):
         log.info("Number of finetuned parameters: %d (actor_ft) + %d (critic)", self.n_actor, self.n_critic)
 
     @staticmethod
-    def _fixed_eta(eta):
-        """eta of the DDIM mean/variance: a number, or an EtaFixed-style config {base_eta: x}
-        (the original DPPO's model.diffusion.eta.EtaFixed; default 1)."""
+    def _eta_config(eta):
+        """eta of the DDIM mean/variance: a number, or an EtaFixed-style config {base_eta, min_eta,
+        max_eta} (the original DPPO's model.diffusion.eta.EtaFixed; defaults 1 / 0.1 / 1)."""
         if eta is None:
-            return 1.0
+            return dict(base_eta=1.0, min_eta=0.1, max_eta=1.0)
         if isinstance(eta, (int, float)):
-            return float(eta)
+            return dict(base_eta=float(eta), min_eta=0.1, max_eta=1.0)
         if hasattr(eta, "get") and eta.get("base_eta") is not None:
-            return float(eta.get("base_eta"))
+            return dict(base_eta=float(eta.get("base_eta")), min_eta=float(eta.get("min_eta", 0.1)),
+                        max_eta=float(eta.get("max_eta", 1.0)))
         raise ValueError(f"eta must be a number or an EtaFixed config with base_eta, got {eta!r}")
+
+    def _init_learnable_eta(self, cfg):
+        """learn_eta (§8(f) row 4, PARITY UNPINNED: the reference's eta module, model/diffusion/eta.py
+        of the original DPPO, is absent and its eta step is commented out): EtaFixed's one scalar,
+        eta = min + (max - min) (tanh(logit) + 1) / 2, logit initialised at base_eta. The device state
+        {logit, m, v} is stepped by dppo_eta_step, which also re-derives the DDIM rows of self.sched
+        (train-mode sampling and every log-prob), so the table always holds the current eta."""
+        lo, hi, base = cfg["min_eta"], cfg["max_eta"], cfg["base_eta"]
+        if not lo < base < hi:
+            raise ValueError(f"learn_eta: base_eta {base} must lie strictly inside (min_eta {lo}, max_eta {hi})")
+        self.eta_min, self.eta_max = lo, hi
+        logit = float(np.arctanh(2.0 * (base - lo) / (hi - lo) - 1.0))
+        dev = self.device
+        self.eta_state = torch.tensor([logit, 0.0, 0.0], dtype=torch.float32, device=dev)
+        self.eta_value = torch.zeros(1, dtype=torch.float32, device=dev)
+        dd = {k: getattr(self, k) for k in ("ddim_alphas_prev", "ddim_sqrt_alphas_prev", "ddim_sqrt_alphas",
+                                            "ddim_sqrt_1m_alphas", "ddim_sfac")}
+        self.eta_base = torch.tensor(ops.ddim_eta_base(dd), device=dev)
+        self.eta_step_count = 0
+        self.refresh_eta()
+
+    def refresh_eta(self):
+        """Re-derive the eta columns of the train-mode DDIM table from the current logit (no step)."""
+        ops.eta_step(self.eta_state, None, 0, 0.0, 0.0, self.eta_min, self.eta_max, self.eta_base, self.sched,
+                     eta_out=self.eta_value)
+
+    def eta_optimizer_step(self, metrics, lr, weight_decay, beta1=0.9, beta2=0.999, eps=1e-7):
+        """One AdamW step of the eta logit from metrics[8] (d loss / d eta of a learn_eta minibatch,
+        the gradient the reference's eta_optimizer would apply, agent :358-359)."""
+        self.eta_step_count += 1
+        ops.eta_step(self.eta_state, metrics, self.eta_step_count, lr, weight_decay, self.eta_min, self.eta_max,
+                     self.eta_base, self.sched, eta_out=self.eta_value, beta1=beta1, beta2=beta2, eps=eps)
+
+    def current_eta(self):
+        """eta of the train-mode DDIM rows (c_loss's `eta` metric, diffusion_ppo.py:131)."""
+        if self.learn_eta:
+            return float(self.eta_value.item())
+        return self.ddim_eta if self.use_ddim else 1.0
 
     # ------------------------------------------------------------------ parameters
     @property

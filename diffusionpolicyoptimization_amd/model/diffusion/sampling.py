@@ -54,7 +54,8 @@ def ddim_buffers(denoising_steps, ddim_steps, eta=1.0):
     ddim_t = np.arange(ddim_steps) * ratio                           # uniform discretisation (:80-82)
     a = abar_all[ddim_t].astype(f)
     a_prev = np.concatenate([np.ones(1, f), a[:-1]]).astype(f)      # corrected: previous sub-sequence element
-    sig = (f(eta) * np.sqrt((one - a_prev) / (one - a) * (one - a / a_prev))).astype(f)
+    sfac = np.sqrt((one - a_prev) / (one - a) * (one - a / a_prev)).astype(f)   # sigma / eta, unclamped
+    sig = (f(eta) * sfac).astype(f)
     sig = np.maximum(sig, f(1e-10))                                   # .clamp_(min=1e-10) (:228)
     d = np.sqrt(np.clip(one - a_prev - sig * sig, f(0.0), f(1e6))).astype(f)
     sa, s1a = np.sqrt(a).astype(f), np.sqrt(one - a).astype(f)
@@ -65,6 +66,8 @@ def ddim_buffers(denoising_steps, ddim_steps, eta=1.0):
         "ddim_c2": (np.sqrt(a_prev) - d * sa / s1a).astype(f),
         "ddim_c3": (d / s1a).astype(f),
         "ddim_logvar": np.log(sig * sig).astype(f),
+        "ddim_sfac": sfac,
+        "ddim_sqrt_alphas_prev": np.sqrt(a_prev).astype(f), "ddim_sqrt_alphas": sa, "ddim_sqrt_1m_alphas": s1a,
         "time_stride": ratio,
     }
 

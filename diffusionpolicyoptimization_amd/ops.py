@@ -632,13 +632,35 @@ def ppo_adv_stats_all(advantages, total, kf, perm_seed, epoch0, n_epochs, rows_f
 
 def ppo_hparams(gamma_denoising=0.99, clip_ploss_coef=0.01, clip_ploss_coef_base=0.01, clip_ploss_coef_rate=3.0,
                 min_logprob_std=0.1, vf_coef=0.5, norm_adv=True, reward_horizon=4, loss_scale=1.0, global_rows=1,
-                l2_deferred=False):
+                l2_deferred=False, learn_eta=False):
     """l2_deferred (ABI 8, DPPO_PPO_L2_DEFERRED): the actor's l2 gradient is left factored in grads
-    for an optimizer step with l2_from_pl2 (or materialize_l2)."""
+    for an optimizer step with l2_from_pl2 (or materialize_l2). learn_eta (ABI 9,
+    DPPO_PPO_LEARN_ETA): the row tiles add d loss / d eta of a DDIM schedule into metrics[8]."""
+    flags = (_lib.DPPO_PPO_L2_DEFERRED if l2_deferred else 0) | (_lib.DPPO_PPO_LEARN_ETA if learn_eta else 0)
     return _lib.DppoPpoHparams(float(gamma_denoising), float(clip_ploss_coef), float(clip_ploss_coef_base),
                                float(clip_ploss_coef_rate), float(min_logprob_std), float(vf_coef), int(bool(norm_adv)),
-                               int(reward_horizon), float(loss_scale), int(global_rows),
-                               _lib.DPPO_PPO_L2_DEFERRED if l2_deferred else 0)
+                               int(reward_horizon), float(loss_scale), int(global_rows), flags)
+
+
+def ddim_eta_base(schedule):
+    """fp32 [S][5] eta-independent rows of a DDIM schedule (ddim_buffers) for dppo_eta_step:
+    {abar_prev, sqrt(abar_prev), sqrt(abar), sqrt(1 - abar), s = sigma / eta}."""
+    return np.stack([schedule["ddim_alphas_prev"], schedule["ddim_sqrt_alphas_prev"], schedule["ddim_sqrt_alphas"],
+                     schedule["ddim_sqrt_1m_alphas"], schedule["ddim_sfac"]], axis=1).astype(np.float32)
+
+
+def eta_step(eta_state, metrics, step, lr, weight_decay, eta_min, eta_max, ddim_base, sched, eta_out=None,
+             beta1=0.9, beta2=0.999, eps=1e-7, mode=0):
+    """dppo_eta_step on the current stream: AdamW on the eta logit from metrics[8] (metrics=None:
+    only re-derive the schedule's eta columns), then the DDIM rows of sched for the new eta."""
+    _check(eta_state, (3,), torch.float32, "eta_state")
+    _check(sched, (sched.shape[0], _lib.SCHED_COLS), torch.float32, "sched")
+    _check(ddim_base, (sched.shape[0], 5), torch.float32, "ddim_base")
+    if metrics is not None:
+        _check(metrics, (16,), torch.float64, "metrics")
+    _lib.call("dppo_eta_step", ptr(eta_state), ptr(metrics), int(step), float(lr), float(weight_decay), float(beta1),
+              float(beta2), float(eps), int(mode), float(eta_min), float(eta_max), ptr(ddim_base), ptr(sched),
+              int(sched.shape[0]), ptr(eta_out), stream_handle(eta_state.device))
 
 
 def materialize_l2(d: ModelDims, precision, packed_actor, grads, workspace, batch_rows):
@@ -808,6 +830,7 @@ def sched_table(schedule):
             tab[:, j] = schedule[k]
         tab[:, 5] = 0.0                      # eval: no noise on any DDIM row (diffusion_vpg.py:303-306)
         tab[:, 6] = 1.0
+        tab[:, 7] = schedule["ddim_sfac"]    # sigma / eta: the learnable-eta gradient's row factor
         return tab
     K = len(schedule["betas"])
     tab = np.zeros((K, _lib.SCHED_COLS), np.float32)

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 8
+#define DPPO_ABI_VERSION 9
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -82,7 +82,9 @@ typedef struct dppo_dims {
  *     mu = sqrt(abar_prev) x0 + d eps', d = sqrt(max(1 - abar_prev - sigma^2, 0)), which is the same
  *     affine form: c2 = sqrt(abar_prev) - d sqrt(abar) / sqrt(1 - abar), c3 = d / sqrt(1 - abar);
  *     c0 = 1 / sqrt(abar), c1 = sqrt(1/abar - 1); logvar = log(sigma^2), sigma = max(eta sqrt((1 - abar_prev)
- *     / (1 - abar) (1 - abar / abar_prev)), 1e-10); eval_floor 0, eval_zero 1. */
+ *     / (1 - abar) (1 - abar / abar_prev)), 1e-10); eval_floor 0, eval_zero 1; column 7 = s =
+ *     sqrt((1 - abar_prev) / (1 - abar) (1 - abar / abar_prev)) (sigma / eta: read only by the
+ *     learnable-eta gradient, DPPO_PPO_LEARN_ETA; ABI 9; 0 for DDPM rows). */
 #define DPPO_SCHED_COLS 8
 
 DPPO_API int         dppo_abi_version(void);
@@ -250,6 +252,24 @@ typedef struct dppo_ppo_hparams {
  * fewer per minibatch); dppo_materialize_l2 forms them in place. The factored form is linear, so a
  * data-parallel caller all-reduces it like the other gradients. */
 enum { DPPO_PPO_L2_DEFERRED = 1 };
+/* ABI 9, dppo_ppo_hparams.flags. DPPO_PPO_LEARN_ETA: a learnable DDIM eta (the original DPPO's
+ * EtaFixed; the reference's eta module is absent, so parity is unpinned): the actor's row tiles add
+ * d loss / d eta into metrics[8] (fp64), through sigma = eta s and d = sqrt(clip(1 - abar_prev -
+ * sigma^2, 0, 1e6)) of each row (schedule column 7 = s). dppo_eta_step applies it. */
+enum { DPPO_PPO_LEARN_ETA = 2 };
+
+/* ABI 9: the learnable DDIM eta's optimizer step (the original DPPO's EtaFixed trained by its own
+ * AdamW every eta_update_interval minibatches, train_ppo_diffusion_agent.py:28-45, 358-359 — the
+ * reference's step is commented out and its eta module absent: parity unpinned). eta_state (device
+ * fp32[3]) = {logit, m, v}, eta = eta_min + (eta_max - eta_min) (tanh(logit) + 1) / 2. With metrics
+ * (device fp64[16], metrics[8] = d loss / d eta of a DPPO_PPO_LEARN_ETA minibatch) and step >= 1 it
+ * applies AdamW (mode as dppo_adamw) to the logit; then (also with metrics == NULL: a refresh) it
+ * rewrites columns c2, c3, logvar of the ddim_steps rows of sched for the current eta from ddim_base
+ * (fp32 [ddim_steps][5] = {abar_prev, sqrt(abar_prev), sqrt(abar), sqrt(1 - abar), s}) and stores
+ * eta to eta_out (device or mapped, may be NULL). One launch on stream. */
+DPPO_API int dppo_eta_step(float* eta_state, const double* metrics, int64_t step, float lr, float weight_decay,
+                           float beta1, float beta2, float eps, int mode, float eta_min, float eta_max,
+                           const float* ddim_base, float* sched, int ddim_steps, float* eta_out, void* stream);
 
 DPPO_API size_t dppo_ppo_workspace_bytes(const dppo_dims* d, int precision, int batch_rows);
 DPPO_API int dppo_ppo_adv_stats(const float* advantages, int64_t total, int K_ft, uint64_t perm_seed, int epoch,

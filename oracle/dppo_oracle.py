@@ -54,26 +54,58 @@ def ddpm_schedule(K):
                 ddpm_var=var, ddpm_logvar_clipped=logvar, ddpm_mu_coef1=coef1, ddpm_mu_coef2=coef2)
 
 
-def ddim_schedule(K, S, eta=1.0):
+def ddim_schedule(K, S, eta=1.0, dtype=np.float32):
     """DDIM sub-sequence (diffusion.py:76-96; diffusion_vpg.py:184-234 documented formulas) with
     the corrections of SURVEY.md §8 quirk 6: walked from the largest t down, alpha_prev = the
     previous SUB-SEQUENCE element, fixed eta, eps recomputed from the clipped x0. PARITY
     UNPINNED: the reference DDIM path cannot run (quirk 6), so this restates the formulas.
     Returns the affine per-row coefficients under the DDPM keys p_mean_var reads (row j = DDIM
     index, diffusion time j*K/S), plus the raw sub-sequence arrays (p_mean_var_ddim_direct)."""
-    f = np.float32
+    f = dtype
     one = f(1.0)
     ratio = K // S
     ac = ddpm_schedule(K)["alphas_cumprod"]
     a = ac[np.arange(S) * ratio].astype(f)
     ap = np.concatenate([np.ones(1, f), a[:-1]]).astype(f)
-    sig = np.maximum((f(eta) * np.sqrt((one - ap) / (one - a) * (one - a / ap))).astype(f), f(1e-10))
+    sfac = np.sqrt((one - ap) / (one - a) * (one - a / ap)).astype(f)   # sigma / eta before the clamp
+    sig = np.maximum((f(eta) * sfac).astype(f), f(1e-10))
     d = np.sqrt(np.clip(one - ap - sig * sig, 0, 1e6)).astype(f)
     sa, s1a = np.sqrt(a).astype(f), np.sqrt(one - a).astype(f)
     return dict(sqrt_recip_alphas_cumprod=(one / sa).astype(f), sqrt_recipm1_alphas_cumprod=(s1a / sa).astype(f),
                 ddpm_mu_coef1=(np.sqrt(ap) - d * sa / s1a).astype(f), ddpm_mu_coef2=(d / s1a).astype(f),
                 ddpm_logvar_clipped=np.log(sig * sig).astype(f), time_stride=ratio, eval_floor=0.0,
-                eval_zero=np.ones(S, bool), ddim_alphas=a, ddim_alphas_prev=ap, ddim_sigmas=sig, ddim_dir=d)
+                eval_zero=np.ones(S, bool), ddim_alphas=a, ddim_alphas_prev=ap, ddim_sigmas=sig, ddim_dir=d,
+                ddim_sfac=sfac, ddim_eta=float(eta))
+
+
+# ----------------------------------------------------------------------------------------------
+# §8(f) row 4: a learnable DDIM eta. The reference builds VPGDiffusion(eta=..., learn_eta=...) and an
+# eta AdamW (train_ppo_diffusion_agent.py:28-45) but its eta module (model/diffusion/eta.py of the
+# original DPPO) is absent and the eta step is commented out (:358-359): PARITY UNPINNED. Restated
+# from the original DPPO's EtaFixed: eta = min + (max - min) (tanh(logit) + 1) / 2, one scalar for
+# every row, entering p_mean_var through sigma = eta s_t and the direction coefficient
+# d = sqrt(clip(1 - abar_prev - sigma^2, 0, 1e6)) (diffusion_vpg.py:219-234).
+# ----------------------------------------------------------------------------------------------
+def eta_from_logit(logit, eta_min, eta_max):
+    return eta_min + (eta_max - eta_min) * 0.5 * (math.tanh(logit) + 1.0)
+
+
+def eta_logit_init(base_eta, eta_min, eta_max):
+    """EtaFixed's initial logit: atanh(2 (base - min) / (max - min) - 1)."""
+    return math.atanh(2.0 * (base_eta - eta_min) / (eta_max - eta_min) - 1.0)
+
+
+def ddim_eta_grad_terms(sched, t, eta, min_logprob_std):
+    """Per-row derivatives of the DDIM row's direction coefficient d and log-prob std w.r.t. eta
+    (zero where a clamp or clip holds the value): dd/deta = -sigma s / d, dstd/deta = s."""
+    s = sched["ddim_sfac"].astype(np.float64)[t]
+    sig_raw = eta * s
+    sig = np.maximum(sig_raw, 1e-10)
+    inner = 1.0 - sched["ddim_alphas_prev"].astype(np.float64)[t] - sig ** 2
+    dd = np.where((inner > 0) & (inner < 1e6) & (sig_raw > 1e-10),
+                  -sig * s / np.sqrt(np.maximum(inner, 1e-300)), 0.0)
+    dstd = np.where((sig_raw > 1e-10) & (sig > min_logprob_std) & (sig < 1e6), s, 0.0)
+    return dd, dstd
 
 
 def p_mean_var_ddim_direct(sched, eps, x, j, denoised_clip=1.0):
@@ -300,7 +332,7 @@ def p_mean_var(sched, eps, x, t, denoised_clip=1.0):
     m2 = sched["ddpm_mu_coef2"].astype(np.float64)[t].reshape(sh)
     mu = m1 * xr + m2 * x                                        # :239-242
     logvar = sched["ddpm_logvar_clipped"].astype(np.float64)[t].reshape(sh)
-    return mu, logvar, dict(m1=m1, c2=c2, unclipped=unclipped)
+    return mu, logvar, dict(m1=m1, c1=c1, c2=c2, unclipped=unclipped)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -367,7 +399,7 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
            advantages, oldlogprobs, ft_steps, gamma_denoising=0.99, clip_ploss_coef=0.01,
            clip_ploss_coef_base=0.01, clip_ploss_coef_rate=3.0, clip_vloss_coef=None,
            norm_adv=True, min_logprob_std=0.1, vf_coef=0.5, with_grad=True, reward_horizon=4, rnd=None,
-           adv_mean_std=None, denom=None, critic_dedup=None):
+           adv_mean_std=None, denom=None, critic_dedup=None, eta_grad=False):
     """Returns (metrics dict, grads_actor dict, grads_critic dict).
 
     Data-parallel restatement hooks: adv_mean_std overrides the minibatch
@@ -461,6 +493,18 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
     if cw is not None:
         dv = dv * cw
     gc, _ = residual_mlp_backward(pc, ccache, dv[:, None], "Mish", "")
+    if eta_grad:
+        # d loss / d eta (learnable DDIM eta, parity unpinned): mu = c2 x0 + c3 x moves through
+        # d (dmu/deta = dd/deta * eps', eps' the noise recomputed from the clipped x0) and the
+        # Normal's std through sigma (diffusion_vpg.py:219-234, 417-422)
+        dd, dstd = ddim_eta_grad_terms(sched, t, sched["ddim_eta"], min_logprob_std)
+        sh = (-1,) + (1,) * (chains_prev.ndim - 1)
+        a = sched["ddim_alphas"].astype(np.float64)[t].reshape(sh)
+        x0 = np.clip(pm["c1"] * chains_prev - pm["c2"] * eps, -1.0, 1.0)
+        e2 = (chains_prev - np.sqrt(a) * x0) / np.sqrt(1.0 - a)
+        r = chains_next - mu
+        dlp_deta = r / std ** 2 * dd.reshape(sh) * e2 + (r ** 2 / std ** 3 - 1.0 / std) * dstd.reshape(sh)
+        metrics["d_eta"] = float((dlp_el * dlp_deta).sum())
     return metrics, ga, gc
 
 

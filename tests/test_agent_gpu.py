@@ -391,3 +391,35 @@ def test_keras_checkpoints_round_trip_through_the_model(cuda, tmp_path):
     assert torch.equal(m3.base_params, m.actor_ft_params) and torch.equal(m3.actor_ft_params, m.actor_ft_params)
     with pytest.raises(FileNotFoundError):
         instantiate(cfg.model, device=cuda, network_path=str(tmp_path / "missing.weights.h5"))
+
+
+def test_learn_eta_agent_iterations(cuda, tmp_path):
+    """§8(f) row 4 (parity unpinned): the DDIM agent with a learnable eta runs train iterations; the
+    eta logit moves by its AdamW (one step per minibatch, eta_update_interval 1), eta stays inside
+    (min_eta, max_eta), the train-mode DDIM table holds the current eta's rows (ddim_buffers at that
+    eta), the eval table keeps eta = 0, and c_loss's eta metric reports it."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.model.diffusion.sampling import ddim_buffers
+    from diffusionpolicyoptimization_amd.util.config import get_class, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp_ddim_learn_eta",
+                      ["model.precision=fp32", "env.n_envs=8", "train.n_steps=20", "train.batch_size=200",
+                       "train.n_train_itr=2", "train.val_freq=100", "train.n_critic_warmup_itr=0",
+                       "train.eta_lr=1e-2", f"logdir={tmp_path}"])
+    agent = get_class(cfg._target_)(cfg)
+    m = agent.model
+    assert m.learn_eta
+    logit0 = float(m.eta_state[0].item())
+    eta0 = m.current_eta()
+    assert abs(eta0 - 0.5) < 1e-6
+    res = agent.run()
+    n_mb = agent.timing["n_updates"]
+    assert n_mb > 0 and m.eta_step_count == n_mb
+    eta1 = m.current_eta()
+    assert float(m.eta_state[0].item()) != logit0 and 0.1 < eta1 < 1.0
+    assert all(math.isfinite(r["pg_loss"]) for r in res if not r["eval"])
+    ref = ops.sched_table(ddim_buffers(20, 10, np.float32(eta1)))
+    np.testing.assert_allclose(m.sched.cpu().numpy()[:, 2:5], ref[:, 2:5], rtol=3e-7, atol=1e-7)
+    ev = ops.sched_table(ddim_buffers(20, 10, 0.0))
+    np.testing.assert_array_equal(m.sched_eval.cpu().numpy(), ev)
+    assert np.isfinite(m.train_params.cpu().numpy()).all()

@@ -830,3 +830,103 @@ def test_pair_sampler_bit_identical(tmp_path, envs):
     for k in ("arr_0", "arr_1", "arr_2", "arr_3"):
         assert np.isfinite(res["1"][k]).all()
         np.testing.assert_array_equal(res["1"][k], res["0"][k])
+
+
+@pytest.mark.parametrize("precision,rtol", [("fp32", 2e-3), ("fp16", 3e-2)])
+def test_learn_eta_gradient_matches_oracle(cuda, precision, rtol):
+    """§8(f) row 4, learnable DDIM eta (PARITY UNPINNED: the reference's eta module is absent; the
+    oracle's derivative is pinned to central differences of its own loss, test_oracle.py): with
+    DPPO_PPO_LEARN_ETA the actor's row tiles add d loss / d eta into metrics[8]; checked against the
+    oracle at eta = 0.6 (rows on both the free and the min_logprob_std-clipped std branch), 'perturbed'
+    old log-probs (fp32) or ratio 1 (fp16). The other metrics and gradients are those of the
+    fixed-eta minibatch (test_ppo_minibatch_grads); the flag must not change them."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    eta = 0.6
+    d, base, ft, critic, sched, tab, pb, pf, pc = _setup(HOPPER_DDIM, cuda, eta=eta)
+    rng = np.random.default_rng(12)
+    N, kf = 40, d.ft_denoising_steps
+    total = N * kf
+    obs = rng.uniform(-1, 1, (N, d.sd)).astype(np.float32)
+    chains = (rng.standard_normal((N, kf + 1, d.xd)) * 0.5).astype(np.float32)
+    adv = rng.normal(size=N).astype(np.float32)
+    ret = rng.normal(size=N).astype(np.float32)
+    T = lambda x: torch.tensor(x, device=cuda)
+    packf = ops.pack_actor(d, pf, precision)
+    lp_ref = O.get_logprobs(to_f64(ft), sched, obs.reshape(N, 1, -1).astype(np.float64),
+                            chains.reshape(N, kf + 1, d.horizon_steps, d.action_dim).astype(np.float64), kf,
+                            rnd=_rnd(precision))
+    lp_ref_mean = np.clip(lp_ref, -5, 2).mean(axis=(1, 2)).reshape(N, kf)
+    if precision == "fp32":
+        lp_old_gpu = (lp_ref_mean + rng.normal(0, 0.02, (N, kf))).astype(np.float32)
+        lp_old_ref = lp_old_gpu.astype(np.float64)
+    else:
+        _, lpm = ops.logprob(d, precision, packf, tab, T(obs), T(chains), want_elem=False)
+        lp_old_gpu = lpm.cpu().numpy()
+        lp_old_ref = lp_ref_mean
+    seed, epoch, start, rows = 99, 1, 37, 150
+    perm = PX.feistel_permute(np.arange(start, start + rows), total, seed, epoch)
+    bi, di = perm // kf, perm % kf
+    mref, _, _ = O.c_loss(
+        to_f64(ft), to_f64(critic), sched, obs[bi].reshape(rows, 1, -1).astype(np.float64),
+        chains[bi, di].reshape(rows, d.horizon_steps, d.action_dim).astype(np.float64),
+        chains[bi, di + 1].reshape(rows, d.horizon_steps, d.action_dim).astype(np.float64),
+        di, ret[bi].astype(np.float64), None, adv[bi].astype(np.float64), lp_old_ref[bi, di], kf,
+        rnd=_rnd(precision), critic_dedup=_dedup(bi), eta_grad=True)
+    na, nc = ops.spec_count(ops.actor_param_spec(d)), ops.spec_count(ops.critic_param_spec(d))
+    packc = ops.pack_critic(d, pc, precision)
+    outs = []
+    for learn in (True, False):
+        grads = torch.zeros(na + nc, dtype=torch.float32, device=cuda)
+        metrics = torch.zeros(16, dtype=torch.float64, device=cuda)
+        ops.ppo_minibatch(d, precision, ops.ppo_hparams(global_rows=rows, learn_eta=learn), packf, packc, pf, tab,
+                          T(obs), T(chains), T(lp_old_gpu), T(adv), T(ret), seed, epoch, start, rows,
+                          ops.ppo_workspace(d, precision, rows, cuda), grads, metrics)
+        torch.cuda.synchronize()
+        outs.append((grads.cpu().numpy(), metrics.cpu().numpy()))
+    (g1, m1), (g0, m0) = outs
+    ref = mref["d_eta"]
+    assert abs(ref) > 1e-3
+    assert abs(m1[8] - ref) <= rtol * abs(ref), (m1[8], ref)
+    assert m0[8] == 0.0
+    np.testing.assert_allclose(m1[:5], m0[:5], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(g1, g0, rtol=1e-4, atol=1e-6 * np.abs(g0).max())
+
+
+def test_eta_step_matches_numpy(cuda):
+    """dppo_eta_step: Keras AdamW on the eta logit from metrics[8] x d eta / d logit, then the DDIM
+    table's eta columns (c2, c3, logvar) for the new eta equal ddim_buffers at that eta (fp32, the
+    same order of operations: within 2 ulp), the other columns untouched; a refresh (metrics None)
+    leaves the logit alone."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.model.diffusion.sampling import ddim_buffers
+    lo, hi, base = 0.1, 1.0, 0.5
+    logit = O.eta_logit_init(base, lo, hi)
+    dd = ddim_buffers(20, 10, base)
+    tab = torch.tensor(ops.sched_table(dd), device=cuda)
+    tab0 = tab.clone()
+    eb = torch.tensor(ops.ddim_eta_base(dd), device=cuda)
+    st = torch.tensor([logit, 0.0, 0.0], dtype=torch.float32, device=cuda)
+    met = torch.zeros(16, dtype=torch.float64, device=cuda)
+    out = torch.zeros(1, dtype=torch.float32, device=cuda)
+    p, m, v = np.float64(np.float32(logit)), 0.0, 0.0
+    for step, g_eta in enumerate((0.7, -0.3, 1.1), start=1):
+        met[8] = g_eta
+        ops.eta_step(st, met, step, 1e-2, 0.004, lo, hi, eb, tab, eta_out=out)
+        torch.cuda.synchronize()
+        g = g_eta * 0.5 * (hi - lo) * (1 - np.tanh(p) ** 2)
+        p, m, v = O.keras_adamw_step(np.array([p]), np.array([g]), np.array([m]), np.array([v]), step, lr=1e-2, wd=0.004)
+        p, m, v = float(p[0]), float(m[0]), float(v[0])
+        got = st.cpu().numpy()
+        np.testing.assert_allclose(got, [p, m, v], rtol=1e-5, atol=1e-7)
+        e = float(out.item())
+        assert abs(e - O.eta_from_logit(float(got[0]), lo, hi)) < 1e-6
+        ref = ops.sched_table(ddim_buffers(20, 10, np.float32(e)))
+        t = tab.cpu().numpy()
+        np.testing.assert_array_equal(t[:, [0, 1, 5, 6, 7]], tab0.cpu().numpy()[:, [0, 1, 5, 6, 7]])
+        np.testing.assert_allclose(t[:, 2:5], ref[:, 2:5], rtol=3e-7, atol=1e-7)
+    before = st.clone()
+    ops.eta_step(st, None, 0, 0.0, 0.0, lo, hi, eb, tab, eta_out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(before, st)

@@ -239,3 +239,33 @@ def test_oracle_pretrain_loss_gradient_matches_autograd():
     assert abs(loss - float(L)) < 1e-12
     for k, v in P.items():
         np.testing.assert_allclose(g[k], v.grad.numpy(), rtol=1e-8, atol=1e-12, err_msg=k)
+
+
+def test_oracle_eta_gradient_matches_finite_differences():
+    """d loss / d eta of the learnable DDIM eta (oracle c_loss eta_grad, parity unpinned: the
+    reference's eta module is absent) against central differences of the oracle's own pg_loss with
+    the DDIM schedule rebuilt in float64 at eta +- h, for etas whose rows hit both the std clip
+    (sigma < min_logprob_std) and the free branch."""
+    base, ft, critic = make_models(0, HOPPER)
+    rng = np.random.default_rng(7)
+    b, kf = 48, 10
+    obs = rng.uniform(-1, 1, (b, 1, 11))
+    prev = rng.normal(0, 0.5, (b, 4, 3))
+    nxt = prev + rng.normal(0, 0.2, (b, 4, 3))
+    j = rng.integers(0, kf, b)
+    ret, adv = rng.normal(size=b), rng.normal(size=b)
+    oldlp = rng.normal(0.0, 0.2, b)
+    for eta in (0.3, 0.7, 1.0):
+        sc = O.ddim_schedule(20, 10, eta, dtype=np.float64)
+        args = (to_f64(ft), to_f64(critic))
+        rest = (obs, prev, nxt, j, ret, None, adv, oldlp, kf)
+        m, _, _ = O.c_loss(*args, sc, *rest, eta_grad=True)
+        h = 1e-6
+        lp = O.c_loss(*args, O.ddim_schedule(20, 10, eta + h, dtype=np.float64), *rest, with_grad=False)[0]["pg_loss"]
+        lm = O.c_loss(*args, O.ddim_schedule(20, 10, eta - h, dtype=np.float64), *rest, with_grad=False)[0]["pg_loss"]
+        fd = (lp - lm) / (2 * h)
+        assert abs(m["d_eta"]) > 1e-4
+        assert abs(m["d_eta"] - fd) <= 1e-6 * max(1.0, abs(fd)), (eta, m["d_eta"], fd)
+    # the EtaFixed parametrisation round-trips
+    lg = O.eta_logit_init(0.5, 0.1, 1.0)
+    assert abs(O.eta_from_logit(lg, 0.1, 1.0) - 0.5) < 1e-12
