@@ -85,6 +85,7 @@ _SIGNATURES = {
                                     _P, _I64, _U64, _I, _I64, _I, _P, _P, _P, _P, _P, _I, _P]),
     "dppo_feistel_permute": (_I, [_I64, _I64, _I64, _U64, _I, _P, _P]),
     "dppo_adamw": (_I, [_P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P]),
+    "dppo_copy_from_host": (_I, [_I, _P, _P, _P, _P]),
     "dppo_eta_step": (_I, [_P, _P, _I64, _F, _F, _F, _F, _F, _I, _F, _F, _P, _P, _I, _P, _P]),
     "dppo_pack_all": (_I, [_DIMS, _I, _P, _P, _P, _P, _P]),
     "dppo_optimizer_step": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P, _P,

@@ -108,11 +108,17 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         else:
             self.obs_pin = torch.empty(E, self.n_cond_step, self.obs_dim, dtype=torch.float32).pin_memory()
             self.act_pin = torch.empty(E, d.xd, dtype=torch.float32).pin_memory()
-        self.reward_pin = torch.empty(S, E, dtype=torch.float64).pin_memory()
-        self.term_pin = torch.empty(S, E, dtype=torch.uint8).pin_memory()
-        self.first_pin = torch.empty(S, E, dtype=torch.uint8).pin_memory()
+        # per-step rewards and flags in coherent mapped memory: the host writes them during the rollout
+        # and the update moves all three to the device in one kernel (ops.copy_from_host)
+        self._reward_map = ops.MappedArray((S, E), np.float64)
+        self._term_map = ops.MappedArray((S, E), np.uint8)
+        self._first_map = ops.MappedArray((S, E), np.uint8)
+        self.reward_pin = self._reward_map.tensor
+        self.term_pin = self._term_map.tensor
+        self.first_pin = self._first_map.tensor
         self.firsts = np.zeros((S + 1, E))
         self.reward_dev = torch.empty(S, E, dtype=torch.float64, device=dev)
+        self.last_obs_dev = torch.empty(E, d.sd, dtype=torch.float32, device=dev)
         self.first_dev = torch.empty(S, E, dtype=torch.uint8, device=dev)
         self.term_dev = torch.empty(S, E, dtype=torch.uint8, device=dev)
         self.values = torch.empty(S * E, dtype=torch.float32, device=dev)
@@ -224,7 +230,11 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             if G > 0 and getattr(self, "_pass_stream", None) is None:
                 self._pass_stream = torch.cuda.Stream(device=self.device)
             done_lp = 0
-            evs = []
+            # completion events of the launches, a ring re-recorded per step (only the two latest
+            # launches <= last are ever waited on); created once per agent
+            if G > 0 and getattr(self, "_launch_evs", None) is None:
+                self._launch_evs = [torch.cuda.Event() for _ in range(4)]
+            evs = self._launch_evs if G > 0 else None
 
             def overlap_passes(last):
                 # launches 0..last are enqueued: log-probs of steps [done_lp, last] once they finish
@@ -232,8 +242,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 if G <= 0 or last + 1 - done_lp < G:
                     return
                 ps = self._pass_stream
-                for ev in evs[max(0, last - 1):last + 1]:   # the two streams' latest launches <= last
-                    ps.wait_event(ev)
+                for i in range(max(0, last - 1), last + 1):   # the two streams' latest launches <= last
+                    ps.wait_event(evs[i % 4])
                 with torch.cuda.stream(ps):
                     self._logprob_range(done_lp, last + 1)
                 done_lp = last + 1
@@ -249,7 +259,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 self._pass_stream.wait_stream(stream)       # the weights the log-probs read
             pipe.enqueue(0, eval_mode)
             if G > 0:
-                evs.append(pipe.launch_event())
+                pipe.launch_event(evs[0])
             if early and S == 1:
                 last_enqueued()
             pipe.publish()
@@ -261,7 +271,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 if more:
                     pipe.enqueue(step + 1, eval_mode)
                     if G > 0:
-                        evs.append(pipe.launch_event())
+                        pipe.launch_event(evs[(step + 1) % 4])
                         if step + 2 < S:
                             overlap_passes(step)           # launch `step` finished before launch step+1 can
                     if early and step + 2 == S:
@@ -326,15 +336,17 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         if not self._passes_enqueued:
             self._enqueue_passes()
         self._passes_enqueued = False
-        self.reward_dev.copy_(self.reward_pin, non_blocking=True)
-        self.term_dev.copy_(self.term_pin, non_blocking=True)
-        # through pinned memory: a pageable source would block the host until the stream reaches it
         np.copyto(self.first_pin.numpy(), self.firsts[:-1], casting="unsafe")
-        self.first_dev.copy_(self.first_pin, non_blocking=True)
+        copies = [(self.reward_dev, self._reward_map), (self.term_dev, self._term_map), (self.first_dev, self._first_map)]
+        if self.pipe is not None:           # the last observation, for the bootstrap values (:239-246)
+            last_obs = self.last_obs_dev
+            copies.append((last_obs, self.pipe.obs_mapped))
+        ops.copy_from_host(copies)
         if self.reward_scale_running:                                                  # :232-236
             self.running_reward_scaler.scale_(self.reward_dev, self.first_dev,
                                               group=dist.group.WORLD if self.world_size > 1 else None)
-        last_obs = self.obs_pin.view(E, -1).to(self.device, non_blocking=True)
+        if self.pipe is None:
+            last_obs = self.obs_pin.view(E, -1).to(self.device, non_blocking=True)
         ops.critic_forward(m.dims, m.precision, m.packed_critic, last_obs, values=self.last_values)
         ops.gae(self.reward_dev, self.values.view(S, E), self.last_values, self.term_dev, self.gamma, self.gae_lambda,
                 self.reward_scale_const, adv=self.adv, ret=self.ret)                       # :239-263
@@ -453,21 +465,34 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # Not with per-tensor gradient clipping (it needs the tensor) or a test hook reading grads.
             l2_def = (self.max_grad_norm is None and self.minibatch_hook is None
                       and os.environ.get("DPPO_L2_DEFER", "1") != "0")
-            run_mb = m.bind_minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, self.perm_seed,
-                                      rows_local_full, reward_horizon=self.reward_horizon, l2_deferred=l2_def)
             opt = self.actor_optimizer
             ng_all = m.grads.numel()
-            if split:
-                step_actor = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
-                                            packs={"actor": (m.actor_ft_params, m.packed_ft)}, defer_sampler_tables=defer,
-                                            l2_from_pl2=l2_def)
-                step_critic = opt.bind_range(m.grads, na, ng_all, m.dims, m.precision,
-                                             packs={"critic": (m.critic_params, m.packed_critic)})
-            elif self.max_grad_norm is None:
-                step_all = opt.bind_range(m.grads, 0, ng_all, m.dims, m.precision,
-                                          packs={"actor": (m.actor_ft_params, m.packed_ft),
-                                                 "critic": (m.critic_params, m.packed_critic)},
-                                          defer_sampler_tables=defer, l2_from_pl2=l2_def)
+            # the bound calls are reused across updates while every buffer they captured is the same
+            # (~0.2 ms of host marshalling per update, with the device idle behind it)
+            ptrs = lambda *ts: tuple((t.data_ptr(), tuple(t.shape)) for t in ts)
+            bkey = (ptrs(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, m.grads, m.train_params,
+                         m.packed_ft, m.packed_critic, m.sched, m.workspace(rows_local_full), opt.m, opt.v),
+                    self.perm_seed, rows_local_full, self.reward_horizon, l2_def, split, defer,
+                    self.max_grad_norm is None, m.dims.ft_denoising_steps, m.precision)
+            if getattr(self, "_bound_key", None) != bkey:
+                bound = {"run_mb": m.bind_minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat,
+                                                    self.perm_seed, rows_local_full, reward_horizon=self.reward_horizon,
+                                                    l2_deferred=l2_def)}
+                if split:
+                    bound["actor"] = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
+                                                    packs={"actor": (m.actor_ft_params, m.packed_ft)},
+                                                    defer_sampler_tables=defer, l2_from_pl2=l2_def)
+                    bound["critic"] = opt.bind_range(m.grads, na, ng_all, m.dims, m.precision,
+                                                     packs={"critic": (m.critic_params, m.packed_critic)})
+                elif self.max_grad_norm is None:
+                    bound["all"] = opt.bind_range(m.grads, 0, ng_all, m.dims, m.precision,
+                                                  packs={"actor": (m.actor_ft_params, m.packed_ft),
+                                                         "critic": (m.critic_params, m.packed_critic)},
+                                                  defer_sampler_tables=defer, l2_from_pl2=l2_def)
+                self._bound_key, self._bound = bkey, bound
+            run_mb = self._bound["run_mb"]
+            step_actor, step_critic = self._bound.get("actor"), self._bound.get("critic")
+            step_all = self._bound.get("all")
             k = 0
             for update_epoch in range(self.update_epochs):
                 for batch in range(num_batch):

@@ -705,6 +705,49 @@ extern "C" int dppo_host_alloc(size_t bytes, void** ptr) {
     return DPPO_OK;
 }
 
+// Up to 4 host-mapped -> device copies in ONE kernel launch (the rollout's reward / termination /
+// first flags into the update's device buffers). hipMemcpyAsync of the same pinned buffers went through
+// the SDMA path, where the second and third copies started ~0.9 ms after they were issued with the
+// device idle (r03 HIP trace: rollout -> update gap 1.2-2.1 ms per iteration); a kernel reading the
+// coherent mapped memory over the bus runs as soon as the stream reaches it.
+struct HostCopies { const uint8_t* src[4]; uint8_t* dst[4]; size_t n[4]; };
+__global__ __launch_bounds__(256) void copy_host_kernel(HostCopies c) {
+    const size_t stride = (size_t)gridDim.x * 256, t0 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    for (int r = 0; r < 4; ++r) {
+        if (!c.n[r]) continue;
+        const uint8_t* s = c.src[r];
+        uint8_t* d = c.dst[r];
+        const size_t n = c.n[r];
+        if ((((uintptr_t)s | (uintptr_t)d) & 15) == 0) {
+            const size_t n16 = n / 16;
+            for (size_t i = t0; i < n16; i += stride) ((uint4*)d)[i] = ((const uint4*)s)[i];
+            for (size_t i = 16 * n16 + t0; i < n; i += stride) d[i] = s[i];
+        } else {
+            for (size_t i = t0; i < n; i += stride) d[i] = s[i];
+        }
+    }
+}
+
+extern "C" int dppo_copy_from_host(int n, void* const* dst, const void* const* src_host, const size_t* bytes, void* stream) {
+    DPPO_CHECK(n >= 0 && n <= 4 && (n == 0 || (dst && src_host && bytes)), "dppo_copy_from_host: bad arguments");
+    HostCopies c = {};
+    size_t total = 0;
+    for (int i = 0; i < n; ++i) {
+        DPPO_CHECK(bytes[i] == 0 || (dst[i] && src_host[i]), "dppo_copy_from_host: null range %d", i);
+        c.src[i] = (const uint8_t*)mapped_ptr(src_host[i]);
+        DPPO_CHECK(bytes[i] == 0 || c.src[i], "dppo_copy_from_host: source %d is not mapped host memory (dppo_host_alloc)", i);
+        c.dst[i] = (uint8_t*)dst[i];
+        c.n[i] = bytes[i];
+        total += bytes[i];
+    }
+    if (total == 0) return DPPO_OK;
+    const size_t blocks = (total / 16 + 255) / 256;
+    hipLaunchKernelGGL(copy_host_kernel, dim3((unsigned)(blocks < 1 ? 1 : (blocks > 256 ? 256 : blocks))), dim3(256), 0,
+                       (hipStream_t)stream, c);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
 extern "C" int dppo_host_free(void* ptr) {
     if (ptr) DPPO_HIP(hipHostFree(ptr));
     return DPPO_OK;

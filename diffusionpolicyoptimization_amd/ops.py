@@ -182,6 +182,47 @@ def value_moments(values, returns, out_address):
     _lib.call("dppo_value_moments", ptr(values), ptr(returns), int(n), ctypes.c_void_p(out), stream_handle(values.device))
 
 
+class MappedArray:
+    """A NumPy array (and a torch CPU view of it) over coherent mapped pinned memory
+    (dppo_host_alloc): the host writes it, copy_from_host moves it to the device in one kernel."""
+
+    def __init__(self, shape, dtype):
+        self.array = np.zeros(shape, dtype)
+        n = max(1, self.array.nbytes)
+        p = ctypes.c_void_p()
+        _lib.call("dppo_host_alloc", ctypes.c_size_t(n), ctypes.byref(p))
+        self.address = p.value
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(self.address))[:self.array.nbytes] \
+            .view(dtype).reshape(shape)
+        self.tensor = torch.from_numpy(self.array)
+
+
+class MappedRef:
+    """address + size of a dppo_host_alloc buffer owned elsewhere (copy_from_host source)."""
+
+    def __init__(self, address, nbytes):
+        self.address, self.nbytes = address, nbytes
+
+
+def copy_from_host(pairs, stream=None):
+    """[(device tensor, MappedArray | MappedRef)] -> one dppo_copy_from_host launch on the current
+    stream."""
+    if not pairs:
+        return
+    if len(pairs) > 4:
+        raise ValueError("copy_from_host: at most 4 ranges per launch")
+    n = len(pairs)
+    dst = (ctypes.c_void_p * n)(*[t.data_ptr() for t, _ in pairs])
+    src = (ctypes.c_void_p * n)(*[m.address for _, m in pairs])
+    nb = (ctypes.c_size_t * n)()
+    for i, (t, m) in enumerate(pairs):
+        n_src = m.nbytes if isinstance(m, MappedRef) else m.array.nbytes
+        if not t.is_cuda or not t.is_contiguous() or t.numel() * t.element_size() != n_src:
+            raise ValueError("copy_from_host: destination must be a contiguous device tensor of the source's size")
+        nb[i] = n_src
+    _lib.call("dppo_copy_from_host", n, dst, src, nb, stream_handle(pairs[0][0].device) if stream is None else stream)
+
+
 class MappedDoubles:
     """n doubles of coherent mapped pinned memory (dppo_host_alloc) the device stores into and the
     host reads as a numpy array (the PPO metric sums of dppo_optimizer_step)."""
@@ -380,6 +421,7 @@ class RolloutPipe:
         pat = alloc(8 * E * d.xd)   # tagged actions (tagged protocol): the host polls the actions themselves
         self._act_tag = np.ctypeslib.as_array((ctypes.c_uint64 * (E * d.xd)).from_address(pat))
         self.obs = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_float * (E * d.sd)).from_address(po))).view(E, d.sd)
+        self.obs_mapped = MappedRef(po, 4 * E * d.sd)   # for copy_from_host
         self.act = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_float * (E * d.xd)).from_address(pa))).view(E, d.xd)
         ctr = np.ctypeslib.as_array((ctypes.c_uint32 * 64).from_address(pc))
         self._go, self._done = ctr[0:1], ctr[16:17]          # separate 64-B lines
@@ -433,9 +475,12 @@ class RolloutPipe:
             raise _lib.DppoError(f"dppo_rollout_enqueue failed ({rc}): {self._lib.dppo_last_error().decode()}")
         m._call_id += 1
 
-    def launch_event(self):
-        """An event recorded on the stream of the most recent launch (its completion)."""
-        ev = torch.cuda.Event()
+    def launch_event(self, ev=None):
+        """An event recorded on the stream of the most recent launch (its completion); ev: an
+        event to re-record (a caller's ring: creating and destroying one per step cost ~3 us of
+        host time each, ~1.5 ms per 500-step rollout when the list was freed)."""
+        if ev is None:
+            ev = torch.cuda.Event()
         ev.record(self._tstreams[(self.enqueued - 1) % len(self._tstreams)])
         return ev
 

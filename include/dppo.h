@@ -161,6 +161,11 @@ DPPO_API int dppo_sample_step(const dppo_dims* d, int precision, const void* pac
  * (~4 s): on timeout the step proceeds and sets bit 31 of *done. */
 DPPO_API int dppo_host_alloc(size_t bytes, void** ptr);
 DPPO_API int dppo_host_free(void* ptr);
+/* ABI 9: n <= 4 copies src_host[i] (dppo_host_alloc memory) -> dst[i] (device), bytes[i] each, in ONE
+ * kernel launch on stream that reads the mapped memory over the bus (no copy engine): the rollout's
+ * per-step rewards and flags into the update's device buffers (agent :232-263). */
+DPPO_API int dppo_copy_from_host(int n, void* const* dst, const void* const* src_host, const size_t* bytes,
+                                 void* stream);
 DPPO_API int dppo_rollout_enqueue(const dppo_dims* d, int precision, const void* packed_base, const void* packed_ft,
                 const float* sched, const float* cond_host, float* cond, int n_envs, uint64_t seed,
                 uint64_t call_id, int env_offset, int deterministic, float min_sampling_std,
