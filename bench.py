@@ -105,7 +105,7 @@ def cpu_baseline(cfg, n_envs, S, bs):
 # on the denoiser GEMMs"), computed from ALGORITHMIC bytes / FLOPs (with the dtypes
 # the kernels actually move) over the rocprofv3 --kernel-trace --stats averages of a committed
 # whole-iteration profile of this workload, so each figure reproduces from that CSV
-KERNEL_STATS_CSV = os.path.join(ROOT, "profiles", "r03_iteration_kernel_stats.csv")
+KERNEL_STATS_CSV = os.path.join(ROOT, "profiles", "r03x_iteration_kernel_stats.csv")
 
 
 def kernel_figures(d, S, E, batch, n_mb, precision, path=KERNEL_STATS_CSV):

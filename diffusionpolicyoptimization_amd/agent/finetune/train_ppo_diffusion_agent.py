@@ -493,6 +493,13 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             run_mb = self._bound["run_mb"]
             step_actor, step_critic = self._bound.get("actor"), self._bound.get("critic")
             step_all = self._bound.get("all")
+            # raw device addresses and stream handles, computed once: per minibatch the host passes
+            # ints instead of slicing tensors and entering stream contexts (~tens of us per minibatch,
+            # which an 8-GPU rank's 255 small minibatches per iteration wait on)
+            adv_base = self._adv_all.data_ptr()
+            st_main = stream.cuda_stream
+            st_side = side.cuda_stream if split else None
+            met_ptrs = [t.data_ptr() for t in self._met_dev] if split else None
             k = 0
             for update_epoch in range(self.update_epochs):
                 for batch in range(num_batch):
@@ -501,7 +508,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     if rows <= 0:
                         break
                     global_rows = rows * W
-                    stats = self._adv_all[update_epoch * num_batch + batch]
+                    stats = adv_base + 24 * (update_epoch * num_batch + batch)   # fp64[3] row
                     hp_ = self.host_profile
                     if hp_ is not None:
                         t_h0 = time.perf_counter()
@@ -514,11 +521,11 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     tagged = self.itr >= self.n_critic_warmup_itr
                     if split:
                         met = self._met_dev[k % 2]
-                        with torch.cuda.stream(side):
-                            run_mb(*mb_args, **mb_kw, part=2, metrics=met)
-                            if not tagged and not dp:
-                                ev_c = torch.cuda.Event()
-                                ev_c.record(side)
+                        met_p = met_ptrs[k % 2]
+                        run_mb(*mb_args, **mb_kw, part=2, metrics=met_p, stream=st_side)
+                        if not tagged and not dp:
+                            ev_c = torch.cuda.Event()
+                            ev_c.record(side)
                         if dp:
                             ng = m.grads.numel()
                             run_mb(*mb_args, **mb_kw, part=4, metrics=met)   # actor row tiles
@@ -535,7 +542,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             self._allreduce(m.grads_ext[:na])      # bucket 2: actor gradients
                             stream.wait_event(self._ev_met)
                         else:
-                            run_mb(*mb_args, **mb_kw, part=1, metrics=met)
+                            run_mb(*mb_args, **mb_kw, part=1, metrics=met_p, stream=st_main)
                             if not tagged:
                                 stream.wait_event(ev_c)
                     else:
@@ -579,10 +586,10 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         tag = self._mb_tag
                         if split:
                             ctag = tag
-                            step_actor(lr, metrics=met, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag)
-                            with torch.cuda.stream(side):
-                                step_critic(lr, metrics=met[1:2], metrics_out=self._cmet_map[slot].address,
-                                            n_metrics=1, metrics_tag=ctag)
+                            step_actor(lr, metrics=met_p, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
+                                       stream=st_main)
+                            step_critic(lr, metrics=met_p + 8, metrics_out=self._cmet_map[slot].address,   # met[1]
+                                        n_metrics=1, metrics_tag=ctag, stream=st_side)
                         elif self.max_grad_norm is not None:
                             self._clip_by_norm_per_tensor()
                             opt.apply_range(m.grads, 0, ng, lr, m.dims, m.precision,

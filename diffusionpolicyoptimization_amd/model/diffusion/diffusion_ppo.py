@@ -70,12 +70,13 @@ class PPODiffusion(VPGDiffusion):
                                    self.workspace(max_rows), self.grads, max_rows)
         hps = {}
 
-        def run(epoch, start, rows, global_rows=None, adv_stats=None, part=None, metrics=None):
+        def run(epoch, start, rows, global_rows=None, adv_stats=None, part=None, metrics=None, stream=None):
             g = int(global_rows or rows)
             hp = hps.get(g)
             if hp is None:
                 hp = hps[g] = self.hparams(g, reward_horizon, loss_scale, l2_deferred=l2_deferred)
-            bound(hp, epoch, start, rows, self.metrics if metrics is None else metrics, adv_stats=adv_stats, part=part)
+            bound(hp, epoch, start, rows, self.metrics if metrics is None else metrics, adv_stats=adv_stats, part=part,
+                  stream=stream)
         return run
 
     def c_loss(self, obs, chains_prev, chains_next, denoising_inds, returns, oldvalues, advantages, oldlogprobs,

@@ -777,14 +777,21 @@ class BoundMinibatch:
         self._keep = (packed_ft, packed_critic, actor_params, sched, obs, chains, lp_old_mean, advantages, returns,
                       workspace, grads)   # the pointers above stay valid while this object lives
 
-    def __call__(self, hp, epoch, start, rows, metrics, adv_stats=None, part=None):
+    def __call__(self, hp, epoch, start, rows, metrics, adv_stats=None, part=None, stream=None):
+        """metrics / adv_stats: device tensors, or device addresses (ints) of fp64[16] / fp64[3]
+        (the update loop passes precomputed addresses); stream: a raw stream handle (default: the
+        current stream)."""
         if not 0 < rows <= self.max_rows:
             raise ValueError(f"rows {rows} outside (0, {self.max_rows}]")
-        if metrics.dtype != torch.float64 or metrics.numel() < 16:
-            raise ValueError("metrics: expected fp64[16]")
+        if isinstance(metrics, torch.Tensor):
+            if metrics.dtype != torch.float64 or metrics.numel() < 16:
+                raise ValueError("metrics: expected fp64[16]")
+            metrics = metrics.data_ptr()
+        if isinstance(adv_stats, torch.Tensor):
+            adv_stats = adv_stats.data_ptr()
         args = (ctypes.byref(self._dims), self._prec, ctypes.byref(hp)) + self._mid + (
-            int(epoch), int(start), int(rows), None, ptr(adv_stats)) + self._tail + (ptr(metrics),)
-        st = stream_handle(self._dev)
+            int(epoch), int(start), int(rows), None, adv_stats) + self._tail + (metrics,)
+        st = stream_handle(self._dev) if stream is None else stream
         if part is None:
             rc = self._lib.dppo_ppo_minibatch(*args, st)
         else:
@@ -815,12 +822,15 @@ class BoundOptimizerStep:
         self._dev = params.device
         self._keep = (params, grads, m, v, actor_params, packed_actor, critic_params, packed_critic)
 
-    def __call__(self, step, lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0):
-        """metrics_out: a device tensor or a dppo_host_alloc address (as optimizer_step)."""
+    def __call__(self, step, lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0, stream=None):
+        """metrics_out: a device tensor or a dppo_host_alloc address (as optimizer_step); metrics: a
+        device tensor or address; stream: a raw stream handle (default: the current stream)."""
         mo = metrics_out if isinstance(metrics_out, int) else (metrics_out.data_ptr() if metrics_out is not None else None)
-        rc = self._lib.dppo_optimizer_step(*self._head, int(step), float(lr), *self._hp, ptr(metrics),
+        mi = metrics if isinstance(metrics, int) else ptr(metrics)
+        rc = self._lib.dppo_optimizer_step(*self._head, int(step), float(lr), *self._hp, mi,
                                            ctypes.c_void_p(mo) if mo else None, int(n_metrics),
-                                           ctypes.c_uint64(int(metrics_tag)), stream_handle(self._dev))
+                                           ctypes.c_uint64(int(metrics_tag)),
+                                           stream_handle(self._dev) if stream is None else stream)
         if rc != 0:
             raise _lib.DppoError(f"dppo_optimizer_step failed ({rc}): {self._lib.dppo_last_error().decode()}")
 

@@ -63,8 +63,8 @@ class AdamW:
                                    self.weight_decay, self.beta_1, self.beta_2, self.epsilon, self.mode, ap, pa, cp,
                                    pc, defer_sampler_tables=defer_sampler_tables, l2_from_pl2=l2_from_pl2)
 
-        def step(lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0):
-            b(self.iterations, lr, metrics, metrics_out, n_metrics, metrics_tag)
+        def step(lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0, stream=None):
+            b(self.iterations, lr, metrics, metrics_out, n_metrics, metrics_tag, stream=stream)
         return step
 
     def apply_gradients_split(self, grads, ranges):
