@@ -470,91 +470,6 @@ __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __res
     }
 }
 
-// The same backward over nb buckets as nb workgroups (one per bucket, TD <= 64): workgroup q forms
-// its bucket's dtemb = G[q] . W_in[XD:XD+TD]^T, the time-MLP forward at t = q TS and da1, and stores
-// {e, mish(a1), dtemb, da1} to a scratch row; the LAST workgroup to finish (an agent-scope counter
-// after a release fence) sums the buckets in fixed order into the time-MLP gradients and in_b, so the
-// result does not depend on the arrival order. scratch: nb * 6 TD floats; counter: zero on entry
-// (the rows of gseg after the buckets, cleared with gseg by the minibatch's zero kernel), reset by the
-// last workgroup. The one-workgroup kernel above spent ~15 us in serial phases per minibatch.
-constexpr int TBM_THREADS = 256;
-__global__ __launch_bounds__(TBM_THREADS) void time_bwd_multi_kernel(const float* __restrict__ gseg,
-                                                                     const float* __restrict__ prm,
-                                                                     float* __restrict__ grad, FlatOffsets F, int XD,
-                                                                     int TD, int H, int nb, int TS,
-                                                                     float* __restrict__ scratch,
-                                                                     unsigned* __restrict__ counter) {
-    __shared__ float e[64], a1[128], mz[128], dt[64], da1[128];
-    __shared__ int last;
-    const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int NW = TBM_THREADS / 64;
-    const float* G = gseg + (size_t)q * H;
-    const int half = TD / 2;
-    if (tid < TD) {
-        const float lnf = logf(10000.f) / (float)(half - 1);
-        const float f = expf(-(float)(tid % half) * lnf) * (float)(q * TS);
-        e[tid] = tid < half ? sinf(f) : cosf(f);
-    }
-    // dtemb[j] = G[q] . W_in[XD + j] (one wave per j, lanes over the hidden units)
-    for (int j = wave; j < TD; j += NW) {
-        const float* w = prm + F.in_w + (size_t)(XD + j) * H;
-        float sacc = 0.f;
-#pragma unroll 8
-        for (int n = lane; n < H; n += 64) sacc += G[n] * w[n];
-        sacc = wave_sum(sacc);
-        if (lane == 0) dt[j] = sacc;
-    }
-    __syncthreads();
-    for (int h = tid; h < 2 * TD; h += TBM_THREADS) {
-        float sacc = prm[F.time_b1 + h];
-        for (int k = 0; k < TD; ++k) sacc += e[k] * prm[F.time_w1 + k * 2 * TD + h];
-        a1[h] = sacc;
-        mz[h] = mishf(sacc);
-        float dm = 0.f;
-        for (int j = 0; j < TD; ++j) dm += dt[j] * prm[F.time_w2 + h * TD + j];
-        da1[h] = dm * mish_gradf(sacc);
-    }
-    __syncthreads();
-    float* row = scratch + (size_t)q * 6 * TD;   // e | mish(a1) | dtemb | da1
-    for (int i = tid; i < 6 * TD; i += TBM_THREADS)
-        row[i] = i < TD ? e[i] : (i < 3 * TD ? mz[i - TD] : (i < 4 * TD ? dt[i - 3 * TD] : da1[i - 4 * TD]));
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) last = atomicAdd(counter, 1u) == (unsigned)(nb - 1);
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    for (int i = tid; i < 2 * TD * TD; i += TBM_THREADS) {           // time_w2 [2TD][TD]
-        const int h = i / TD, j = i % TD;
-        float sacc = 0.f;
-        for (int b = 0; b < nb; ++b) sacc += ld(scratch + (size_t)b * 6 * TD + TD + h) * ld(scratch + (size_t)b * 6 * TD + 3 * TD + j);
-        grad[F.time_w2 + i] = sacc;
-    }
-    for (int i = tid; i < TD * 2 * TD; i += TBM_THREADS) {           // time_w1 [TD][2TD]
-        const int k = i / (2 * TD), h = i % (2 * TD);
-        float sacc = 0.f;
-        for (int b = 0; b < nb; ++b) sacc += ld(scratch + (size_t)b * 6 * TD + k) * ld(scratch + (size_t)b * 6 * TD + 4 * TD + h);
-        grad[F.time_w1 + i] = sacc;
-    }
-    for (int j = tid; j < TD; j += TBM_THREADS) {
-        float sacc = 0.f;
-        for (int b = 0; b < nb; ++b) sacc += ld(scratch + (size_t)b * 6 * TD + 3 * TD + j);
-        grad[F.time_b2 + j] = sacc;
-    }
-    for (int h = tid; h < 2 * TD; h += TBM_THREADS) {
-        float sacc = 0.f;
-        for (int b = 0; b < nb; ++b) sacc += ld(scratch + (size_t)b * 6 * TD + 4 * TD + h);
-        grad[F.time_b1 + h] = sacc;
-    }
-    for (int n = tid; n < H; n += TBM_THREADS) {                      // in_b' = sum_q G[q]
-        float sacc = 0.f;
-        for (int b = 0; b < nb; ++b) sacc += gseg[(size_t)b * H + n];
-        grad[F.in_b + n] = sacc;
-    }
-    if (tid == 0) *counter = 0u;
-}
-
 // ---------------------------------------------------------------------------------------------
 // minibatch advantage statistics {count, sum, sumsq} (for norm_adv, diffusion_ppo.py:74-75)
 // ---------------------------------------------------------------------------------------------
@@ -1029,16 +944,8 @@ static SideStream* side_stream() {
 
 // the actor's l2 weight gradient from pl2 (l2_back_kernel: no LDS, so it starts on any CU with a
 // free wave slot), then the time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg)
-static bool time_bwd_multi() {   // DPPO_TIME_BWD_MULTI=1: the bucket-parallel kernel (opt-in until GPU-measured)
-    static const bool on = [] { const char* e = getenv("DPPO_TIME_BWD_MULTI"); return e && atoi(e) != 0; }();
-    return on;
-}
-
-// multi = the bucket-parallel kernel (PPO minibatches: gseg rows [nb, 16) are cleared with the buckets
-// by the minibatch's zero kernel and hold its scratch and counter)
 static int launch_time_bwd(const Dims& D, int precision, const float* gseg, const float* pl2, const void* packed_actor,
-                           const float* actor_params, float* ga, int nb, int TS, hipStream_t s, bool l2_back = true,
-                           bool multi = false) {
+                           const float* actor_params, float* ga, int nb, int TS, hipStream_t s, bool l2_back = true) {
     const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
     const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     L2Back l2b = {pl2, ga + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b, D.H,
@@ -1049,14 +956,6 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
     if (l2_back) {
         hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
         DPPO_HIP(hipGetLastError());
-    }
-    if (multi && time_bwd_multi() && D.TD <= 64 && D.TD % 2 == 0 && (size_t)nb * 6 * D.TD + 64 <= (size_t)(16 - nb) * D.H) {
-        float* scratch = const_cast<float*>(gseg) + (size_t)nb * D.H;
-        unsigned* counter = (unsigned*)(const_cast<float*>(gseg) + (size_t)16 * D.H - 64);
-        hipLaunchKernelGGL(time_bwd_multi_kernel, dim3(nb), dim3(TBM_THREADS), 0, s, gseg, actor_params, ga, FA, D.XD,
-                           D.TD, D.H, nb, TS, scratch, counter);
-        DPPO_HIP(hipGetLastError());
-        return DPPO_OK;
     }
     size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
                                   (size_t)nb * (2 * D.TD + 2 * 2 * D.TD));
@@ -1269,7 +1168,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (parts == 4) return DPPO_OK;
         rc = launch_grads(true, s);
         if (rc) return rc;
-        return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def, true);
+        return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def);
     }
     SideStream* side = side_stream();
     if (side) {
@@ -1306,7 +1205,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
     }
 
-    return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def, true);
+    return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def);
 }
 
 extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
