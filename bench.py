@@ -231,6 +231,13 @@ def main():
                          "global minibatch split N ways: N x the minibatches of batch_size / N rows), every "
                          "collective skipped; value = N x this rank's env steps / its time (a bound on the "
                          "N-GPU number without collective time)")
+    ap.add_argument("--env", choices=["synthetic", "lowdim"], default="synthetic",
+                    help="synthetic: the AVX2 synthetic stepper (the headline workload); lowdim: the reference's "
+                         "MultiStep + lowdim wrapper stack (csrc/envwrap.c) on the hopper normalization.npz over the "
+                         "C linear simulator, pipelined through the gated thread-pool step")
+    ap.add_argument("--env-threads", type=int, default=None, help="lowdim: host threads stepping the envs")
+    ap.add_argument("--sim-cost-us", type=float, default=0.0,
+                    help="lowdim: emulated physics work per env sub-step of the C simulator (measurement knob)")
     args = ap.parse_args()
 
     import torch
@@ -246,6 +253,12 @@ def main():
         over.append(f"model.precision={args.precision}")
     if args.batch_size:
         over.append(f"train.batch_size={args.batch_size}")
+    if args.env == "lowdim":
+        npz = os.path.join(ROOT, "tests", "golden", "hopper_medium_v2_normalization.npz")
+        over += ["env.synthetic=lowdim", f"+env.wrappers.mujoco_locomotion_lowdim.normalization_path={npz}",
+                 f"+env.sim_cost_us={args.sim_cost_us}"]
+        if args.env_threads:
+            over.append(f"+env.num_threads={args.env_threads}")
     emu = max(1, args.emulate_ranks)
     if emu > 1:
         if world > 1:
@@ -344,7 +357,13 @@ def main():
         "config": {"workload": (f"{cfg.env_name} DPPO fine-tune iteration: {agent.n_envs} envs/GPU x "
                                 f"{cfg.train.n_steps} chunks (Ta={cfg.horizon_steps}), K={d.denoising_steps} DDPM "
                                 f"steps (K'={d.ft_denoising_steps}), {cfg.train.update_epochs} PPO epochs x "
-                                f"minibatch {cfg.train.batch_size}, {prec} denoiser, synthetic linear env"),
+                                f"minibatch {cfg.train.batch_size}, {prec} denoiser, " + (
+                                    "synthetic linear env" if args.env == "synthetic" else
+                                    f"reference wrapper stack (MultiStep + MujocoLocomotionLowdimWrapper in C, "
+                                    f"{agent.venv.num_threads} host threads) over the C linear simulator"
+                                    + (f" with {args.sim_cost_us} us emulated work per env sub-step"
+                                       if args.sim_cost_us else ""))),
+                   "env": args.env,
                    "global_envs": agent.n_envs_global, "chunks_per_rollout": cfg.train.n_steps,
                    "parallelism": f"dp{world} (env shards + RCCL grad all-reduce)" if world > 1 else "single GPU",
                    "batch_semantics": (f"per-rank minibatch {cfg.train.batch_size} (global {cfg.train.batch_size * world}, "

@@ -68,6 +68,7 @@ _SIGNATURES = {
     "dppo_sampler_layout": (_I, [_DIMS, _I, _I, ctypes.POINTER(ctypes.c_int)]),
     "dppo_sampler_max_in_flight": (_I, [_DIMS, _I, _I, ctypes.POINTER(ctypes.c_int)]),
     "dppo_sampler_plan": (_I, [_DIMS, _I, _I, ctypes.POINTER(ctypes.c_int)]),
+    "dppo_sampler_release_stream": (_I, [_P]),
     "dppo_logprob": (_I, [_DIMS, _I, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P]),
     "dppo_critic_forward": (_I, [_DIMS, _I, _P, _P, _I, _P, _P]),
     "dppo_reward_scale_workspace_doubles": (_SZ, [_I, _I]),
@@ -100,7 +101,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class DppoError(RuntimeError):

@@ -56,7 +56,9 @@ class TrainAgent:
                                asynchronous=True, max_episode_steps=cfg.env.max_episode_steps, wrappers=wrappers,
                                obs_dim=cfg.obs_dim, action_dim=cfg.action_dim, act_steps=cfg.act_steps,
                                obs_steps=cfg.cond_steps, family_seed=cfg.env.get("family_seed", 0),
-                               native=bool(cfg.env.get("native", True)), synthetic=cfg.env.get("synthetic", False))
+                               native=bool(cfg.env.get("native", True)), synthetic=cfg.env.get("synthetic", False),
+                               num_threads=cfg.env.get("num_threads", None),
+                               sim_cost_us=float(cfg.env.get("sim_cost_us", 0.0)))
         self.venv.seed([self.seed + self.env_offset + i for i in range(self.n_envs)])  # train_agent.py:53-56
         self.n_cond_step = cfg.cond_steps
         self.obs_dim = cfg.obs_dim

@@ -143,6 +143,9 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         obs = self.obs_pin.numpy().copy()
         if self.pipe is not None:
             self.pipe.close()
+        # the old mapped reward / flag buffers are freed with their last view (ops.MappedArray):
+        # no device copy from them may still be pending
+        torch.cuda.synchronize(self.device)
         self._alloc_buffers()
         self.obs_pin.numpy()[:] = obs
         if self.prev_obs_venv is not None:

@@ -11,6 +11,8 @@
 #include <string.h>
 #include <time.h>
 
+#include "dppo_env.h"
+
 #define DPPO_ENV_API __attribute__((visibility("default")))
 #define EB 16
 #define MAXD 64
@@ -127,7 +129,6 @@ static double env_now_s(void) {
  * pre-enqueued sampler launch of the next step. go == NULL: never publish (the last step).
  * Returns n_done, with DPPO_ENV_PUBLISHED or'ed in when go was published; -1 host timeout;
  * -2 the device flagged that its own wait for go timed out. */
-#define DPPO_ENV_PUBLISHED (1 << 30)
 DPPO_ENV_API int dppo_env_step_gated(int E, int Do, int Da, int act_steps, int Ta, int max_steps, int n_obs_steps,
                                      const double* AT, const double* B, const double* c, const double* goal,
                                      double* state, int64_t* cnt, const float* actions, double* reward,

@@ -1,39 +1,82 @@
 /* envwrap.c — the host env boundary of the reference's gym locomotion stack, batched in C over a
- * simulator callback table, so a real simulator (MuJoCo's C API, or gym envs behind a Python
- * callback) plugs in without the reference's one-process-per-env pipes:
+ * simulator callback table and fanned out over a pool of host threads, so a real simulator
+ * (MuJoCo's C API, or gym envs behind a Python callback) plugs in without the reference's
+ * one-process-per-env pipes:
  *
  *   AsyncVectorEnv.step (env/gym_utils/async_vector_env.py:356-456, worker :774-840)
  *     -> MultiStep.step (env/gym_utils/wrapper/multi_step.py:135-192)
  *       -> MujocoLocomotionLowdimWrapper.step (wrapper/mujoco_locomotion_lowdim.py:57-70)
  *         -> the simulator (mujoco_py in the reference; here the dppo_sim callback table)
  *
- * One dppo_lowdim_step call executes one action chunk for all E envs: sub-step k calls sim.step ONCE
- * for the batch of envs still running, with the unnormalised float32 actions (:60-62), normalises
- * the raw observations (:57-58), sums rewards, applies MultiStep's termination / truncation rules
- * and, with reset_within_step, resets the envs whose chunk ended (sim.reset, one batched call).
- * Observations leave as float32 [E][To][Do] straight into the caller's (pinned) staging buffer.
+ * One dppo_lowdim_step call executes one action chunk for all E envs. The envs are split into
+ * contiguous slices, one per pool thread (the reference's worker processes, async_vector_env.py:
+ * 189-214, become threads of this process; the caller's thread runs slice 0). Within a slice,
+ * sub-step k calls sim.step ONCE for the slice's envs still running, with the unnormalised float32
+ * actions (:60-62), normalises the raw observations (:57-58), sums rewards, applies MultiStep's
+ * termination / truncation rules and, with reset_within_step, resets the envs whose chunk ended
+ * (sim.reset, one batched call per slice). Observations leave as float32 [E][To][Do] straight into
+ * the caller's (pinned / mapped) staging buffer. Every env's arithmetic depends on that env alone,
+ * so the outputs are bit-identical for any thread count (tests/test_envstack_cpu.py).
+ *
+ * The gated entries (dppo_lowdim_step_gated_tagged / _gated) are the pipelined rollout's host
+ * step (ops.RolloutPipe): each slice thread polls ITS envs' action granules in mapped
+ * memory, steps them, and publishes ITS envs' observation granules as soon as they are final, so
+ * the sampler launch for the next chunk (already enqueued, polling per granule) starts on the
+ * observation the moment the last slice publishes.
  *
  * Arithmetic follows NumPy's on the reference's dtypes, bit for bit (compiled with
  * -ffp-contract=off): the action map is float32 ((a + 1) / 2 * (max - min) + min, every operand
  * float32); the observation map is float64 with the float32 range (max - min + 1e-6 in float32,
  * NumPy's weak-scalar rule) promoted. */
+#include <immintrin.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+
+#include "dppo_env.h"
 
 #define DPPO_ENV_API __attribute__((visibility("default")))
 
-/* The simulator: raw (unnormalised) coordinates, one batched call per sub-step. idx lists the n
- * env indices the call covers (ascending); rows of act / obs / reward / done / time_limit are in
- * idx order. step: act [n][Da] float64 (the float32 unnormalised actions, widened) -> obs [n][Do]
- * float64, reward [n], done [n] (gym's done), time_limit [n] (gym's info["TimeLimit.truncated"]:
- * -1 when the key is absent, else 0 / 1). reset: obs [n][Do]. Return 0, or nonzero to abort the
- * chunk (reported as -1 by dppo_lowdim_step). */
-typedef int (*dppo_sim_step_fn)(void* ctx, int n, const int32_t* idx, const double* act, double* obs,
-                                double* reward, uint8_t* done, int8_t* time_limit);
-typedef int (*dppo_sim_reset_fn)(void* ctx, int n, const int32_t* idx, double* obs);
+/* the simulator callback table (dppo_sim_step_fn / dppo_sim_reset_fn) and every entry point are
+ * declared in include/dppo_env.h */
+
+struct LowdimEnv;
+
+/* one chunk's arguments, shared by the slice threads */
+typedef struct {
+    float* actions;                /* [E][Ta][Da]; the gated tagged step decodes into it */
+    int Ta;
+    double* reward;
+    uint8_t *terminated, *truncated;
+    float *obs_out, *final_obs;
+    uint8_t* has_final;
+    /* gated tagged protocol (NULL act_tagged: plain step) */
+    const volatile uint32_t* done;
+    const uint64_t* act_tagged;
+    uint32_t act_tag;
+    uint64_t* obs_tagged;          /* NULL: do not publish */
+    uint32_t obs_tag;
+    double deadline;               /* monotonic seconds */
+} Chunk;
 
 typedef struct {
+    struct LowdimEnv* env;
+    int n;                         /* threads, the caller's included */
+    pthread_t* th;
+    int* rc;                       /* per-slice result */
+    volatile int gen;              /* job generation (bumped under mu) */
+    volatile int pending;          /* slices still running */
+    volatile int stop;
+    int sleepers;
+    double spin_s;                 /* how long an idle worker spins before it sleeps */
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+} Pool;
+
+typedef struct LowdimEnv {
     int E, Do, Da, To, act_steps, max_episode_steps, reset_within_step;
     dppo_sim_step_fn step;
     dppo_sim_reset_fn reset;
@@ -41,15 +84,23 @@ typedef struct {
     float *obs_min, *obs_max, *act_min, *act_max;   /* NULL: identity maps (no normalisation file) */
     int64_t* cnt;        /* MultiStep.cnt per env */
     double* hist;        /* [E][To][Do]: the last To normalised observations (MultiStep.obs deque) */
-    /* scratch */
+    /* scratch, [E]-sized; slice [lo, hi) uses rows [lo, hi) */
     int32_t* idx;
     double *act, *obs, *rew;
     uint8_t* done;
     int8_t* tl;
     uint8_t *term, *trunc, *alive, *last_done;
+    Pool* pool;          /* NULL: one thread */
+    Chunk chunk;         /* the chunk in flight */
 } LowdimEnv;
 
-DPPO_ENV_API int dppo_lowdim_abi(void) { return 1; }
+DPPO_ENV_API int dppo_lowdim_abi(void) { return 2; }
+
+static double mono_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 /* mujoco_locomotion_lowdim.py:57-58, n rows of Do: out = 2 * ((raw - min) / (max - min + 1e-6) - 0.5) */
 DPPO_ENV_API void dppo_lowdim_normalize_obs(int64_t n, int Do, const double* raw, const float* mn, const float* mx,
@@ -76,9 +127,12 @@ DPPO_ENV_API void dppo_lowdim_unnormalize_action(int64_t n, int Da, const float*
 
 static void* xcalloc(size_t n, size_t s) { return calloc(n ? n : 1, s); }
 
+static void pool_destroy(Pool* p);
+
 DPPO_ENV_API void dppo_lowdim_destroy(void* h) {
     LowdimEnv* e = (LowdimEnv*)h;
     if (!e) return;
+    pool_destroy(e->pool);
     free(e->obs_min); free(e->obs_max); free(e->act_min); free(e->act_max);
     free(e->cnt); free(e->hist); free(e->idx); free(e->act); free(e->obs); free(e->rew);
     free(e->done); free(e->tl); free(e->term); free(e->trunc); free(e->alive); free(e->last_done);
@@ -86,7 +140,8 @@ DPPO_ENV_API void dppo_lowdim_destroy(void* h) {
 }
 
 /* max_episode_steps <= 0: MultiStep(max_episode_steps=None). obs_min/obs_max [Do], act_min/act_max
- * [Da]: the normalization.npz arrays (float32), or NULL for identity maps. */
+ * [Da]: the normalization.npz arrays (float32), or NULL for identity maps. One thread until
+ * dppo_lowdim_set_threads. */
 DPPO_ENV_API void* dppo_lowdim_create(int E, int Do, int Da, int To, int act_steps, int max_episode_steps,
                                       int reset_within_step, dppo_sim_step_fn step, dppo_sim_reset_fn reset, void* ctx,
                                       const float* obs_min, const float* obs_max, const float* act_min,
@@ -126,14 +181,14 @@ DPPO_ENV_API void* dppo_lowdim_create(int E, int Do, int Da, int To, int act_ste
     return e;
 }
 
-/* the normalised raw observation of row r of e->obs into env i's history: reset fills every slot
+/* the normalised raw observation `raw` [Do] into env i's history: reset fills every slot
  * (stack_last_n_obs pads with the oldest entry, multi_step.py:68-78), a step shifts it in */
-static void hist_put(LowdimEnv* e, int i, int r, int fill) {
+static void hist_put(LowdimEnv* e, int i, const double* raw, int fill) {
     double* h = e->hist + (size_t)i * e->To * e->Do;
     double v[256];
     double* nv = e->Do <= 256 ? v : (double*)malloc(8 * (size_t)e->Do);
-    if (e->obs_min) dppo_lowdim_normalize_obs(1, e->Do, e->obs + (size_t)r * e->Do, e->obs_min, e->obs_max, nv);
-    else memcpy(nv, e->obs + (size_t)r * e->Do, 8 * (size_t)e->Do);
+    if (e->obs_min) dppo_lowdim_normalize_obs(1, e->Do, raw, e->obs_min, e->obs_max, nv);
+    else memcpy(nv, raw, 8 * (size_t)e->Do);
     if (fill) {
         for (int o = 0; o < e->To; ++o) memcpy(h + (size_t)o * e->Do, nv, 8 * (size_t)e->Do);
     } else {
@@ -150,22 +205,256 @@ static void hist_out(const LowdimEnv* e, int i, float* obs_out) {
 }
 
 /* reset the n envs idx[0..n) (MultiStep.reset, multi_step.py:113-133: cnt = 0, the deque holds the
- * reset observation only) */
-static int reset_envs(LowdimEnv* e, int n, const int32_t* idx) {
+ * reset observation only); obs: the n-row scratch the simulator writes */
+static int reset_envs(LowdimEnv* e, int n, const int32_t* idx, double* obs) {
     if (n == 0) return 0;
-    if (e->reset(e->ctx, n, idx, e->obs)) return -1;
+    if (e->reset(e->ctx, n, idx, obs)) return -1;
     for (int r = 0; r < n; ++r) {
         e->cnt[idx[r]] = 0;
-        hist_put(e, idx[r], r, 1);
+        hist_put(e, idx[r], obs + (size_t)r * e->Do, 1);
     }
     return 0;
+}
+
+/* ---- the pool: persistent threads, slice t of a chunk = envs [E t / n, E (t + 1) / n) ---- */
+static int slice_lo(const LowdimEnv* e, int n, int t) { return (int)((int64_t)e->E * t / n); }
+
+static int run_slice(LowdimEnv* e, int lo, int hi);
+
+typedef struct { Pool* p; int t; } WorkerArg;
+
+static void* worker(void* a) {
+    WorkerArg* wa = (WorkerArg*)a;
+    Pool* p = wa->p;
+    const int t = wa->t;
+    free(wa);
+    int seen = 0;   /* a new pool starts at generation 0: a chunk dispatched before this thread ran is still seen */
+    for (;;) {
+        /* spin for a while (a rollout steps every few tens of microseconds), then sleep */
+        double t_end = -1.0;
+        for (uint32_t spins = 0; __atomic_load_n(&p->gen, __ATOMIC_ACQUIRE) == seen && !p->stop; ++spins) {
+            _mm_pause();
+            if ((spins & 255u) == 255u) {
+                sched_yield();
+                const double now = mono_s();
+                if (t_end < 0.0) t_end = now + p->spin_s;
+                else if (now > t_end) break;
+            }
+        }
+        if (__atomic_load_n(&p->gen, __ATOMIC_ACQUIRE) == seen && !p->stop) {
+            pthread_mutex_lock(&p->mu);
+            p->sleepers++;
+            while (__atomic_load_n(&p->gen, __ATOMIC_ACQUIRE) == seen && !p->stop) pthread_cond_wait(&p->cv, &p->mu);
+            p->sleepers--;
+            pthread_mutex_unlock(&p->mu);
+        }
+        if (p->stop) break;
+        seen = __atomic_load_n(&p->gen, __ATOMIC_ACQUIRE);
+        LowdimEnv* e = p->env;
+        p->rc[t] = run_slice(e, slice_lo(e, p->n, t), slice_lo(e, p->n, t + 1));
+        __atomic_fetch_sub(&p->pending, 1, __ATOMIC_ACQ_REL);
+    }
+    return NULL;
+}
+
+static void pool_destroy(Pool* p) {
+    if (!p) return;
+    pthread_mutex_lock(&p->mu);
+    p->stop = 1;
+    pthread_cond_broadcast(&p->cv);
+    pthread_mutex_unlock(&p->mu);
+    for (int t = 1; t < p->n; ++t) pthread_join(p->th[t], NULL);
+    pthread_mutex_destroy(&p->mu);
+    pthread_cond_destroy(&p->cv);
+    free(p->th); free(p->rc); free(p);
+}
+
+/* Threads that step the envs (the caller's included): 1 = step on the caller's thread only;
+ * n > E is clamped to E. spin_us: how long an idle pool thread spins for the next chunk before it
+ * sleeps (<= 0: 2000 us). Returns the thread count in use, or -1. */
+DPPO_ENV_API int dppo_lowdim_set_threads(void* h, int n, double spin_us) {
+    LowdimEnv* e = (LowdimEnv*)h;
+    if (!e) return -1;
+    if (n < 1) n = 1;
+    if (n > e->E) n = e->E;
+    if (e->pool && e->pool->n == n) {
+        e->pool->spin_s = (spin_us > 0 ? spin_us : 2000.0) * 1e-6;
+        return n;
+    }
+    pool_destroy(e->pool);
+    e->pool = NULL;
+    if (n == 1) return 1;
+    Pool* p = (Pool*)xcalloc(1, sizeof(Pool));
+    if (!p) return -1;
+    p->env = e; p->n = n;
+    p->spin_s = (spin_us > 0 ? spin_us : 2000.0) * 1e-6;
+    p->th = (pthread_t*)xcalloc(n, sizeof(pthread_t));
+    p->rc = (int*)xcalloc(n, sizeof(int));
+    pthread_mutex_init(&p->mu, NULL);
+    pthread_cond_init(&p->cv, NULL);
+    for (int t = 1; t < n; ++t) {
+        WorkerArg* wa = (WorkerArg*)malloc(sizeof(WorkerArg));
+        wa->p = p; wa->t = t;
+        if (pthread_create(&p->th[t], NULL, worker, wa)) {
+            free(wa);
+            p->n = t;              /* join the ones that started */
+            pool_destroy(p);
+            return -1;
+        }
+    }
+    e->pool = p;
+    return n;
+}
+
+DPPO_ENV_API int dppo_lowdim_threads(void* h) {
+    LowdimEnv* e = (LowdimEnv*)h;
+    return e->pool ? e->pool->n : 1;
+}
+
+/* run e->chunk on every slice; the caller's thread takes slice 0. Returns the sum of the slices'
+ * results, or the most negative one. */
+static int run_chunk(LowdimEnv* e) {
+    Pool* p = e->pool;
+    if (!p) return run_slice(e, 0, e->E);
+    __atomic_store_n(&p->pending, p->n - 1, __ATOMIC_RELEASE);
+    pthread_mutex_lock(&p->mu);
+    __atomic_fetch_add(&p->gen, 1, __ATOMIC_ACQ_REL);
+    if (p->sleepers) pthread_cond_broadcast(&p->cv);
+    pthread_mutex_unlock(&p->mu);
+    p->rc[0] = run_slice(e, 0, slice_lo(e, p->n, 1));
+    /* yield now and then: a worker the scheduler placed on this CPU must get to run */
+    for (uint32_t spins = 1; __atomic_load_n(&p->pending, __ATOMIC_ACQUIRE) > 0; ++spins) {
+        _mm_pause();
+        if ((spins & 63u) == 0) sched_yield();
+    }
+    int sum = 0, worst = 0;
+    for (int t = 0; t < p->n; ++t) {
+        if (p->rc[t] < worst) worst = p->rc[t];
+        if (p->rc[t] > 0) sum += p->rc[t];
+    }
+    return worst < 0 ? worst : sum;
+}
+
+/* the gated tagged protocol, per slice: wait until env rows [lo, hi)'s action granules carry the
+ * tag, decoding them into the float actions. 0, -1 (host timeout), -2 (device flagged a timeout) */
+static int slice_wait_actions(LowdimEnv* e, int lo, int hi) {
+    const Chunk* c = &e->chunk;
+    const int64_t per = (int64_t)c->Ta * e->Da;
+    int64_t i = lo * per;
+    const int64_t end = hi * per;
+    for (uint32_t spins = 0;; ++spins) {
+        while (i < end) {
+            const uint64_t x = __atomic_load_n(c->act_tagged + i, __ATOMIC_ACQUIRE);
+            if ((uint32_t)(x >> 32) != c->act_tag) break;
+            const uint32_t bits = (uint32_t)x;
+            memcpy(c->actions + i, &bits, 4);
+            ++i;
+        }
+        if (i == end) return 0;
+        if (__atomic_load_n(c->done, __ATOMIC_ACQUIRE) & 0x80000000u) return -2;
+        _mm_pause();
+        if ((spins & 1023u) == 1023u) {
+            sched_yield();
+            if (mono_s() > c->deadline) return -1;
+        }
+    }
+}
+
+/* One chunk for envs [lo, hi) (multi_step.py:135-192); see dppo_lowdim_step. */
+static int run_slice(LowdimEnv* e, int lo, int hi) {
+    const Chunk* c = &e->chunk;
+    const int Do = e->Do, Da = e->Da, To = e->To, Ta = c->Ta;
+    if (lo >= hi) return 0;
+    if (c->act_tagged) {
+        const int w = slice_wait_actions(e, lo, hi);
+        if (w) return w;
+    }
+    int32_t* idx = e->idx + lo;
+    double* act = e->act + (size_t)lo * Da;
+    double* obs = e->obs + (size_t)lo * Do;
+    double* rew = e->rew + lo;
+    uint8_t* done = e->done + lo;
+    int8_t* tl = e->tl + lo;
+    const int nsub = e->act_steps < Ta ? e->act_steps : Ta;
+    for (int i = lo; i < hi; ++i) {
+        e->term[i] = e->trunc[i] = 0;
+        e->alive[i] = 1;
+        e->last_done[i] = 0;
+        c->reward[i] = 0.0;
+        if (c->has_final) c->has_final[i] = 0;
+    }
+    for (int k = 0; k < nsub; ++k) {
+        /* for act_step, act in enumerate(action): self.cnt += 1; if terminated or truncated: break */
+        int n = 0;
+        for (int i = lo; i < hi; ++i) {
+            if (!e->alive[i]) continue;
+            e->cnt[i] += 1;
+            if (e->term[i] || e->trunc[i]) {
+                e->alive[i] = 0;
+                continue;
+            }
+            idx[n] = i;
+            const float* a = c->actions + ((size_t)i * Ta + k) * Da;
+            float raw[64];
+            if (e->act_min) dppo_lowdim_unnormalize_action(1, Da, a, e->act_min, e->act_max, raw);
+            else memcpy(raw, a, 4 * (size_t)Da);
+            for (int j = 0; j < Da; ++j) act[(size_t)n * Da + j] = (double)raw[j];
+            ++n;
+        }
+        if (n == 0) break;
+        if (e->step(e->ctx, n, idx, act, obs, rew, done, tl)) return -1;
+        for (int r = 0; r < n; ++r) {
+            const int i = idx[r];
+            hist_put(e, i, obs + (size_t)r * Do, 0);
+            c->reward[i] += rew[r];                                /* reward_agg_method = "sum" */
+            if (tl[r] < 0) {                                       /* no "TimeLimit.truncated" in info */
+                if (done[r]) e->term[i] = 1;
+                else if (e->max_episode_steps > 0 && e->cnt[i] >= e->max_episode_steps) e->trunc[i] = 1;
+            } else {
+                e->trunc[i] = (uint8_t)(tl[r] != 0);
+                e->term[i] = done[r] ? 1 : 0;
+            }
+            e->last_done[i] = e->term[i] || e->trunc[i];          /* self.done[-1] */
+        }
+    }
+    /* the returned observation, then reset within the step where the chunk ended (:172-187) */
+    int n_done = 0, nr = 0;
+    for (int i = lo; i < hi; ++i) {
+        c->terminated[i] = e->term[i];
+        c->truncated[i] = e->trunc[i];
+        hist_out(e, i, c->obs_out);
+        if (e->last_done[i]) {
+            ++n_done;
+            if (e->reset_within_step) {
+                if (e->trunc[i] && c->final_obs) {
+                    memcpy(c->final_obs + (size_t)i * To * Do, c->obs_out + (size_t)i * To * Do, 4 * (size_t)To * Do);
+                    c->has_final[i] = 1;
+                }
+                idx[nr++] = i;
+            }
+        }
+    }
+    if (nr) {
+        if (reset_envs(e, nr, idx, obs)) return -1;
+        for (int r = 0; r < nr; ++r) hist_out(e, idx[r], c->obs_out);
+    }
+    if (c->obs_tagged) {   /* publish this slice's observation granules (one aligned 8-byte store each) */
+        const uint64_t hi_tag = (uint64_t)c->obs_tag << 32;
+        const int64_t per = (int64_t)To * Do;
+        for (int64_t q = lo * per; q < hi * per; ++q) {
+            uint32_t bits;
+            memcpy(&bits, c->obs_out + q, 4);
+            __atomic_store_n(c->obs_tagged + q, hi_tag | bits, __ATOMIC_RELEASE);
+        }
+    }
+    return n_done;
 }
 
 /* AsyncVectorEnv.reset_arg -> MultiStep.reset for every env; obs_out [E][To][Do] float32 */
 DPPO_ENV_API int dppo_lowdim_reset_all(void* h, float* obs_out) {
     LowdimEnv* e = (LowdimEnv*)h;
     for (int i = 0; i < e->E; ++i) e->idx[i] = i;
-    if (reset_envs(e, e->E, e->idx)) return -1;
+    if (reset_envs(e, e->E, e->idx, e->obs)) return -1;
     for (int i = 0; i < e->E; ++i) hist_out(e, i, obs_out);
     return 0;
 }
@@ -174,9 +463,17 @@ DPPO_ENV_API int dppo_lowdim_reset_one(void* h, int env, float* obs_out) {
     LowdimEnv* e = (LowdimEnv*)h;
     if (env < 0 || env >= e->E) return -1;
     int32_t one = env;
-    if (reset_envs(e, 1, &one)) return -1;
+    if (reset_envs(e, 1, &one, e->obs)) return -1;
     hist_out(e, env, obs_out);
     return 0;
+}
+
+static void set_chunk(LowdimEnv* e, float* actions, int Ta, double* reward, uint8_t* terminated, uint8_t* truncated,
+                      float* obs_out, float* final_obs, uint8_t* has_final) {
+    Chunk* c = &e->chunk;
+    memset(c, 0, sizeof(*c));
+    c->actions = actions; c->Ta = Ta; c->reward = reward; c->terminated = terminated; c->truncated = truncated;
+    c->obs_out = obs_out; c->final_obs = final_obs; c->has_final = final_obs ? has_final : NULL;
 }
 
 /* One chunk for all envs (multi_step.py:135-192). actions [E][Ta][Da] float32 (the first
@@ -189,71 +486,60 @@ DPPO_ENV_API int dppo_lowdim_reset_one(void* h, int env, float* obs_out) {
 DPPO_ENV_API int dppo_lowdim_step(void* h, const float* actions, int Ta, double* reward, uint8_t* terminated,
                                   uint8_t* truncated, float* obs_out, float* final_obs, uint8_t* has_final) {
     LowdimEnv* e = (LowdimEnv*)h;
-    const int E = e->E, Do = e->Do, Da = e->Da, To = e->To;
-    const int nsub = e->act_steps < Ta ? e->act_steps : Ta;
-    for (int i = 0; i < E; ++i) {
-        e->term[i] = e->trunc[i] = 0;
-        e->alive[i] = 1;
-        e->last_done[i] = 0;
-        reward[i] = 0.0;
-        if (has_final) has_final[i] = 0;
+    if (Ta < 1) return -1;
+    set_chunk(e, (float*)actions, Ta, reward, terminated, truncated, obs_out, final_obs, has_final);
+    return run_chunk(e);
+}
+
+/* dppo_lowdim_step as the pipelined rollout's host step with the tagged protocol both ways
+ * (the wrapper-stack counterpart of dppo_env_step_gated_tagged, csrc/envstep.c): every slice
+ * thread spins until its envs' action granules act_tagged [E][Ta][Da] carry act_tag (the device's
+ * stores are the ready flag; bit 31 of *done reports a device-side timeout), decodes them into
+ * `actions`, steps its envs, and — when obs_tagged is not NULL — publishes its envs' observation
+ * granules {tag : 32, fp32 bits : 32} of obs_out. The in-wrapper reset is already applied to
+ * obs_out, so the observation is always publishable. Returns n_done (| DPPO_ENV_PUBLISHED when
+ * published), -1 simulator error or host timeout, -2 the device flagged its own wait timed out. */
+DPPO_ENV_API int dppo_lowdim_step_gated_tagged(void* h, float* actions, int Ta, double* reward, uint8_t* terminated,
+                                               uint8_t* truncated, float* obs_out, float* final_obs,
+                                               uint8_t* has_final, const volatile uint32_t* done,
+                                               const uint64_t* act_tagged, uint32_t act_tag, uint64_t* obs_tagged,
+                                               uint32_t tag, double timeout_s) {
+    LowdimEnv* e = (LowdimEnv*)h;
+    if (Ta < 1 || !done || !act_tagged) return -1;
+    set_chunk(e, actions, Ta, reward, terminated, truncated, obs_out, final_obs, has_final);
+    Chunk* c = &e->chunk;
+    c->done = done; c->act_tagged = act_tagged; c->act_tag = act_tag;
+    c->obs_tagged = obs_tagged; c->obs_tag = tag;
+    c->deadline = mono_s() + timeout_s;
+    const int rc = run_chunk(e);
+    if (rc < 0) return rc;
+    return obs_tagged ? (rc | DPPO_ENV_PUBLISHED) : rc;
+}
+
+/* The "go" protocol (dppo_rollout_enqueue): spin until *done >= done_target, step, then store
+ * go_value to *go (go NULL: no publish). Same returns as the tagged entry. */
+DPPO_ENV_API int dppo_lowdim_step_gated(void* h, float* actions, int Ta, double* reward, uint8_t* terminated,
+                                        uint8_t* truncated, float* obs_out, float* final_obs, uint8_t* has_final,
+                                        const volatile uint32_t* done, uint32_t done_target, volatile uint32_t* go,
+                                        uint32_t go_value, double timeout_s) {
+    LowdimEnv* e = (LowdimEnv*)h;
+    if (Ta < 1 || !done) return -1;
+    const double deadline = mono_s() + timeout_s;
+    for (uint32_t spins = 0;; ++spins) {
+        const uint32_t v = __atomic_load_n(done, __ATOMIC_ACQUIRE);
+        if (v & 0x80000000u) return -2;
+        if (v >= done_target) break;
+        _mm_pause();
+        if ((spins & 1023u) == 1023u && mono_s() > deadline) return -1;
     }
-    for (int k = 0; k < nsub; ++k) {
-        /* for act_step, act in enumerate(action): self.cnt += 1; if terminated or truncated: break */
-        int n = 0;
-        for (int i = 0; i < E; ++i) {
-            if (!e->alive[i]) continue;
-            e->cnt[i] += 1;
-            if (e->term[i] || e->trunc[i]) {
-                e->alive[i] = 0;
-                continue;
-            }
-            e->idx[n] = i;
-            const float* a = actions + ((size_t)i * Ta + k) * Da;
-            float raw[64];
-            if (e->act_min) dppo_lowdim_unnormalize_action(1, Da, a, e->act_min, e->act_max, raw);
-            else memcpy(raw, a, 4 * (size_t)Da);
-            for (int j = 0; j < Da; ++j) e->act[(size_t)n * Da + j] = (double)raw[j];
-            ++n;
-        }
-        if (n == 0) break;
-        if (e->step(e->ctx, n, e->idx, e->act, e->obs, e->rew, e->done, e->tl)) return -1;
-        for (int r = 0; r < n; ++r) {
-            const int i = e->idx[r];
-            hist_put(e, i, r, 0);
-            reward[i] += e->rew[r];                                /* reward_agg_method = "sum" */
-            if (e->tl[r] < 0) {                                    /* no "TimeLimit.truncated" in info */
-                if (e->done[r]) e->term[i] = 1;
-                else if (e->max_episode_steps > 0 && e->cnt[i] >= e->max_episode_steps) e->trunc[i] = 1;
-            } else {
-                e->trunc[i] = (uint8_t)(e->tl[r] != 0);
-                e->term[i] = e->done[r] ? 1 : 0;
-            }
-            e->last_done[i] = e->term[i] || e->trunc[i];          /* self.done[-1] */
-        }
+    set_chunk(e, actions, Ta, reward, terminated, truncated, obs_out, final_obs, has_final);
+    const int rc = run_chunk(e);
+    if (rc < 0) return rc;
+    if (go) {
+        __atomic_store_n(go, go_value, __ATOMIC_RELEASE);   /* x86: the obs stores are visible first */
+        return rc | DPPO_ENV_PUBLISHED;
     }
-    /* the returned observation, then reset within the step where the chunk ended (:172-187) */
-    int n_done = 0, nr = 0;
-    for (int i = 0; i < E; ++i) {
-        terminated[i] = e->term[i];
-        truncated[i] = e->trunc[i];
-        hist_out(e, i, obs_out);
-        if (e->last_done[i]) {
-            ++n_done;
-            if (e->reset_within_step) {
-                if (e->trunc[i] && final_obs) {
-                    memcpy(final_obs + (size_t)i * To * Do, obs_out + (size_t)i * To * Do, 4 * (size_t)To * Do);
-                    has_final[i] = 1;
-                }
-                e->idx[nr++] = i;
-            }
-        }
-    }
-    if (nr) {
-        if (reset_envs(e, nr, e->idx)) return -1;
-        for (int r = 0; r < nr; ++r) hist_out(e, e->idx[r], obs_out);
-    }
-    return n_done;
+    return rc;
 }
 
 DPPO_ENV_API const int64_t* dppo_lowdim_counters(void* h) { return ((LowdimEnv*)h)->cnt; }
@@ -266,9 +552,10 @@ DPPO_ENV_API const int64_t* dppo_lowdim_counters(void* h) { return ((LowdimEnv*)
  * (env seed, episode index) around `center`. */
 typedef struct {
     int E, Do, Da;
-    double *A, *B, *c, *goal, *center, *scale, *bound;   /* A [Do][Do] row-major, B [Da][Do] */
+    double *A, *AT, *B, *c, *goal, *center, *scale, *bound;   /* A [Do][Do] row-major, AT = A^T, B [Da][Do] */
     double* s;          /* [E][Do] */
     int64_t *seed, *episode;
+    double cost_s;      /* emulated extra work per env sub-step (0: none), dppo_sim_linear_set_cost */
 } LinearSim;
 
 DPPO_ENV_API void* dppo_sim_linear_create(int E, int Do, int Da, const double* A, const double* B, const double* c,
@@ -285,6 +572,9 @@ DPPO_ENV_API void* dppo_sim_linear_create(int E, int Do, int Da, const double* A
     m->s = (double*)xcalloc((size_t)E * Do, 8);
     m->seed = (int64_t*)xcalloc(E, 8); m->episode = (int64_t*)xcalloc(E, 8);
     memcpy(m->A, A, 8 * (size_t)Do * Do); memcpy(m->B, B, 8 * (size_t)Da * Do);
+    m->AT = (double*)xcalloc((size_t)Do * Do, 8);
+    for (int j = 0; j < Do; ++j)
+        for (int q = 0; q < Do; ++q) m->AT[(size_t)q * Do + j] = A[(size_t)j * Do + q];
     memcpy(m->c, c, 8 * (size_t)Do); memcpy(m->goal, goal, 8 * (size_t)Do);
     memcpy(m->center, center, 8 * (size_t)Do); memcpy(m->scale, scale, 8 * (size_t)Do);
     memcpy(m->seed, seeds, 8 * (size_t)E);
@@ -299,10 +589,17 @@ DPPO_ENV_API void dppo_sim_linear_seed(void* p, const int64_t* seeds) {
     memset(m->episode, 0, 8 * (size_t)m->E);
 }
 
+/* Measurement knob: busy-wait cost_us per env sub-step inside step, standing in for the work of a
+ * physics step (a MuJoCo locomotion step with frame_skip is tens of microseconds on one core), so
+ * the pool's fan-out can be measured without a simulator; 0 (the default) turns it off. */
+DPPO_ENV_API void dppo_sim_linear_set_cost(void* p, double cost_us) {
+    ((LinearSim*)p)->cost_s = cost_us > 0 ? cost_us * 1e-6 : 0.0;
+}
+
 DPPO_ENV_API void dppo_sim_linear_destroy(void* p) {
     LinearSim* m = (LinearSim*)p;
     if (!m) return;
-    free(m->A); free(m->B); free(m->c); free(m->goal); free(m->center); free(m->scale); free(m->bound); free(m->s);
+    free(m->A); free(m->AT); free(m->B); free(m->c); free(m->goal); free(m->center); free(m->scale); free(m->bound); free(m->s);
     free(m->seed); free(m->episode); free(m);
 }
 
@@ -317,11 +614,22 @@ DPPO_ENV_API int dppo_sim_linear_step(void* ctx, int n, const int32_t* idx, cons
         const double* a = act + (size_t)r * Da;
         double err = 0.0, asq = 0.0;
         int out = 0;
+        /* sn[j] = c[j] + sum_q A[j][q] s[q] + sum_q B[q][j] a[q], each row's terms added in that
+         * order (the oracle's): the loops run over j innermost so they vectorise without
+         * reassociating any row's sum */
+        for (int j = 0; j < Do; ++j) sn[j] = m->c[j];
+        for (int q = 0; q < Do; ++q) {
+            const double sq = s[q];
+            const double* at = m->AT + (size_t)q * Do;
+            for (int j = 0; j < Do; ++j) sn[j] += at[j] * sq;
+        }
+        for (int q = 0; q < Da; ++q) {
+            const double aq = a[q];
+            const double* b = m->B + (size_t)q * Do;
+            for (int j = 0; j < Do; ++j) sn[j] += b[j] * aq;
+        }
         for (int j = 0; j < Do; ++j) {
-            double v = m->c[j];
-            for (int q = 0; q < Do; ++q) v += m->A[(size_t)j * Do + q] * s[q];
-            for (int q = 0; q < Da; ++q) v += m->B[(size_t)q * Do + j] * a[q];
-            sn[j] = v;
+            const double v = sn[j];
             const double d = v - m->goal[j];
             err += d * d;
             const double dc = v - m->center[j];
@@ -333,6 +641,10 @@ DPPO_ENV_API int dppo_sim_linear_step(void* ctx, int n, const int32_t* idx, cons
         reward[r] = 1.0 - err / Do - 1e-3 * asq;
         done[r] = (uint8_t)out;
         time_limit[r] = -1;
+        if (m->cost_s > 0) {
+            const double t_end = mono_s() + m->cost_s;
+            while (mono_s() < t_end) _mm_pause();
+        }
     }
     return 0;
 }

@@ -1766,10 +1766,16 @@ __global__ void xchg_zero_kernel(uint64_t* p, size_t n) {
         __hip_atomic_store(p + i, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// exchange buffers: one per stream (launches on one stream are ordered, so they can share one)
+// exchange buffers: one per stream (launches on one stream are ordered, so they can share one).
+// A slot is bound to one stream while `live`; dppo_sampler_release_stream unbinds it (the pipe that
+// owned the stream is closed), and a new stream takes an unbound slot of its device first. A buffer
+// is never freed: a rebound slot keeps its buffer and CONTINUES its launch sequence number, so no
+// granule left in it by the previous stream can carry a tag the next launch waits for, and no
+// zeroing (or device-wide synchronisation) is needed to hand it over.
 struct XchgBuf {
     hipStream_t stream;
     int device;
+    int live;
     uint64_t* buf;
     uint32_t seq;
     uint32_t* fail_host;   // mapped pinned word (SplitArgs::xfail_host)
@@ -1785,7 +1791,7 @@ int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq, uint32_t** fail_dev) 
     DPPO_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(g_xmu);
     for (int i = 0; i < g_nxb; ++i)
-        if (g_xb[i].stream == s && g_xb[i].device == dev) {
+        if (g_xb[i].live && g_xb[i].stream == s && g_xb[i].device == dev) {
             // an earlier launch on this stream lost its members' co-residency (another tenant took
             // the CUs it waited for) and wrote NaN actions: report it instead of sampling on
             if (__hip_atomic_load(g_xb[i].fail_host, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
@@ -1798,17 +1804,38 @@ int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq, uint32_t** fail_dev) 
             *fail_dev = g_xb[i].fail_dev;
             return DPPO_OK;
         }
-    int slot = g_nxb;
-    if (g_nxb == 16) {
-        // every slot holds another stream (a process that made many rollout pipes): reuse the slots
-        // round robin once the device is idle; the evicted stream's next launch gets a fresh buffer
-        static int next_evict = 0;
-        slot = next_evict;
-        next_evict = (next_evict + 1) % 16;
-        DPPO_HIP(hipDeviceSynchronize());
-        DPPO_HIP(hipFree(g_xb[slot].buf));
-        DPPO_HIP(hipHostFree(g_xb[slot].fail_host));
+    int slot = -1;
+    for (int i = 0; i < g_nxb && slot < 0; ++i)       // a released slot of this device
+        if (!g_xb[i].live && g_xb[i].device == dev) slot = i;
+    if (slot < 0 && g_nxb == 16) {
+        // every slot is bound to a live stream (a process with more than 16 sampling streams):
+        // rebind the slot of a stream with no work pending; only when every such stream is busy,
+        // wait for ONE of them (never the whole device: another stream may hold a pipelined launch
+        // that waits for an observation the host publishes only after this call returns)
+        for (int i = 0; i < 16 && slot < 0; ++i)
+            if (g_xb[i].device == dev && hipStreamQuery(g_xb[i].stream) == hipSuccess) slot = i;
+        if (slot < 0) {
+            static int next_evict = 0;
+            for (int k = 0; k < 16 && slot < 0; ++k) {
+                const int i = (next_evict + k) % 16;
+                if (g_xb[i].device == dev) slot = i;
+            }
+            if (slot < 0) return dppo_set_error(DPPO_EHIP, "split sampler: no exchange buffer slot for this device");
+            next_evict = (slot + 1) % 16;
+            DPPO_HIP(hipStreamSynchronize(g_xb[slot].stream));
+        }
     }
+    if (slot >= 0) {                                    // rebind: same buffer, sequence continues
+        XchgBuf& x = g_xb[slot];
+        __hip_atomic_store(x.fail_host, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        x.stream = s; x.live = 1;
+        x.seq = (x.seq + 1) & 0x03FFFFFFu;
+        *buf = x.buf;
+        *seq = x.seq;
+        *fail_dev = x.fail_dev;
+        return DPPO_OK;
+    }
+    slot = g_nxb;
     XchgBuf& x = g_xb[slot];
     const size_t n = XTOTAL;
     DPPO_HIP(hipMalloc((void**)&x.buf, sizeof(uint64_t) * n));
@@ -1818,13 +1845,30 @@ int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq, uint32_t** fail_dev) 
     // zeroed with write-through stores: no XCD's L2 is left holding a dirty copy of any line
     hipLaunchKernelGGL(xchg_zero_kernel, dim3(1024), dim3(256), 0, s, x.buf, n);
     DPPO_HIP(hipGetLastError());
-    x.stream = s; x.device = dev; x.seq = 1;
-    if (slot == g_nxb) ++g_nxb;
+    x.stream = s; x.device = dev; x.seq = 1; x.live = 1;
+    ++g_nxb;
     *buf = x.buf;
     *seq = x.seq;
     *fail_dev = x.fail_dev;
     return DPPO_OK;
 }
+
+}  // namespace
+
+// ABI 10: unbind the exchange buffer of `stream` (its owner is done sampling on it): waits for the
+// stream's work, then leaves the buffer to the next new stream of the device
+extern "C" DPPO_API int dppo_sampler_release_stream(void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(g_xmu);
+    for (int i = 0; i < g_nxb; ++i)
+        if (g_xb[i].live && g_xb[i].stream == s) {
+            DPPO_HIP(hipStreamSynchronize(s));
+            g_xb[i].live = 0;
+        }
+    return DPPO_OK;
+}
+
+namespace {
 
 int device_cus() {
     if (!g_cus) {

@@ -27,7 +27,9 @@ def _wrapper_args(wrappers):
 
 def make_async(id, num_envs=1, asynchronous=True, wrappers=None, render=False, obs_dim=23, action_dim=7,
                env_type=None, max_episode_steps=None, act_steps=4, obs_steps=1, family_seed=0, native=True,
-               synthetic=False, **kwargs):
+               synthetic=False, num_threads=None, sim_cost_us=0.0, **kwargs):
+    """num_threads: host threads stepping the wrapper stack (LowdimVecEnv; None: its default).
+    sim_cost_us: emulated work per env sub-step of the C reference simulator (measurement only)."""
     name = str(id).lower()
     if env_type not in (None, "gym") or not any(name.startswith(p) for p in _LOCOMOTION):
         raise NotImplementedError(f"env {id!r} (type {env_type}): only the gym locomotion tasks are in scope")
@@ -42,9 +44,10 @@ def make_async(id, num_envs=1, asynchronous=True, wrappers=None, render=False, o
     npath = lo.get("normalization_path")
     norm = load_normalization(npath) if npath and os.path.exists(str(npath)) else None
     if synthetic == "lowdim":
-        sim = LinearSimulator(num_envs, obs_dim, action_dim, family_seed=family_seed, norm=norm)
+        sim = LinearSimulator(num_envs, obs_dim, action_dim, family_seed=family_seed, norm=norm, cost_us=sim_cost_us)
         return LowdimVecEnv(sim, num_envs, obs_dim, action_dim, act_steps=n_act, n_obs_steps=n_obs,
-                            max_episode_steps=max_steps, reset_within_step=rws, normalization=norm)
+                            max_episode_steps=max_steps, reset_within_step=rws, normalization=norm,
+                            num_threads=num_threads)
     if synthetic not in (False, None):
         raise ValueError(f"env.synthetic must be true, 'lowdim' or false, got {synthetic!r}")
     # the reference's simulator (env/gym_utils/__init__.py:125-174: d4rl.gym_mujoco + gym.make per env)
@@ -61,4 +64,5 @@ def make_async(id, num_envs=1, asynchronous=True, wrappers=None, render=False, o
     if "mujoco_locomotion_lowdim" not in (wrappers or {}):
         norm = None
     return LowdimVecEnv(sim, num_envs, obs_dim, action_dim, act_steps=n_act, n_obs_steps=n_obs,
-                        max_episode_steps=max_steps, reset_within_step=rws, normalization=norm)
+                        max_episode_steps=max_steps, reset_within_step=rws, normalization=norm,
+                        num_threads=num_threads)

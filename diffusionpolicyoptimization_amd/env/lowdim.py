@@ -21,8 +21,21 @@ running, one batched `reset` for the envs whose chunk ended. A simulator is any 
     a CallbackSimulator (needs those packages: absent on the MI355X hosts).
 
 The wire format is the reference's: reset_arg() -> {"state": [E, To, Do]}; step(actions [E, Ta, Da])
--> ({"state": [E, To, Do]}, reward [E], terminated [E], truncated [E], infos)."""
+-> ({"state": [E, To, Do]}, reward [E], terminated [E], truncated [E], infos).
+
+Parallelism: the reference runs one worker process per env (async_vector_env.py:189-214). Here the
+envs are split into contiguous slices over a pool of host threads inside the C library
+(dppo_lowdim_set_threads; `num_threads`, default from the simulator's `thread_safe` flag and the
+env count). A C simulator with per-env state (LinearSimulator, a MuJoCo C-API stepper with one
+mjData per env) steps its slices concurrently; a Python simulator holds the GIL in every callback,
+so it gets one thread unless it says otherwise. Outputs are bit-identical for any thread count.
+
+Pipelined rollout: step(..., gate=("tagged", ...)) is the gated host step of ops.RolloutPipe over
+this stack (dppo_lowdim_step_gated_tagged): each slice thread polls its envs' action granules,
+steps them and publishes their observation granules, so the agent's next sampler launch overlaps
+the env step exactly as with the synthetic stepper."""
 import ctypes
+import os
 
 import numpy as np
 
@@ -44,6 +57,15 @@ def lib():
         L.dppo_lowdim_reset_all.argtypes = [_P, _P]
         L.dppo_lowdim_reset_one.argtypes = [_P, ctypes.c_int, _P]
         L.dppo_lowdim_step.argtypes = [_P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P]
+        # (h, actions, Ta, reward, term, trunc, obs_out, final_obs, has_final, done, act_tagged, act_tag,
+        #  obs_tagged, tag, timeout)
+        L.dppo_lowdim_step_gated_tagged.argtypes = [_P, _P, ctypes.c_int] + [_P] * 6 + [_P, _P, ctypes.c_uint32, _P,
+                                                                                      ctypes.c_uint32, ctypes.c_double]
+        # (h, actions, Ta, reward, term, trunc, obs_out, final_obs, has_final, done, done_target, go, go_value, timeout)
+        L.dppo_lowdim_step_gated.argtypes = [_P, _P, ctypes.c_int] + [_P] * 6 + [_P, ctypes.c_uint32, _P,
+                                                                               ctypes.c_uint32, ctypes.c_double]
+        L.dppo_lowdim_set_threads.argtypes = [_P, ctypes.c_int, ctypes.c_double]
+        L.dppo_lowdim_threads.argtypes = [_P]
         L.dppo_lowdim_normalize_obs.argtypes = [ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P]
         L.dppo_lowdim_normalize_obs.restype = None
         L.dppo_lowdim_unnormalize_action.argtypes = [ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P]
@@ -55,6 +77,8 @@ def lib():
         L.dppo_sim_linear_destroy.argtypes = [_P]
         L.dppo_sim_linear_seed.argtypes = [_P, _P]
         L.dppo_sim_linear_seed.restype = None
+        L.dppo_sim_linear_set_cost.argtypes = [_P, ctypes.c_double]
+        L.dppo_sim_linear_set_cost.restype = None
         L.dppo_sim_linear_step_fn.restype = _P
         L.dppo_sim_linear_reset_fn.restype = _P
         _lib = L
@@ -94,9 +118,13 @@ class LinearSimulator:
     """dppo_sim_linear (csrc/envwrap.c): raw state s' = A s + B a + c, reward 1 - mean((s' - goal)^2)
     - 1e-3 |a|^2, terminal when any |s'_j - center_j| > bound_j; reset = a seeded hash around `center`. Built
     from a family seed (the dynamics) and the normalisation ranges (the raw coordinate box), so its
-    raw observations land in the box the normalisation maps to [-1, 1]."""
+    raw observations land in the box the normalisation maps to [-1, 1]. Per-env state only, so the
+    pool's threads step disjoint env slices concurrently (thread_safe). cost_us > 0 adds that much
+    busy work per env sub-step (a stand-in for a physics step's cost when measuring the pool)."""
 
-    def __init__(self, num_envs, obs_dim, action_dim, family_seed=0, norm=None, bound_frac=0.9):
+    thread_safe = True
+
+    def __init__(self, num_envs, obs_dim, action_dim, family_seed=0, norm=None, bound_frac=0.9, cost_us=0.0):
         rng = np.random.default_rng(20_000 + family_seed)
         if norm is not None:
             lo, hi = norm["obs_min"].astype(np.float64), norm["obs_max"].astype(np.float64)
@@ -125,6 +153,17 @@ class LinearSimulator:
             raise MemoryError("dppo_sim_linear_create failed")
         self.step_fn = L.dppo_sim_linear_step_fn()
         self.reset_fn = L.dppo_sim_linear_reset_fn()
+        self.set_cost(cost_us)
+
+    def suggested_threads(self, num_envs):
+        """Pool size for this simulator: a step of the bare linear dynamics is ~0.1 us per env, below
+        the pool's hand-off cost (one thread); with emulated physics work, one thread per 16 envs, at
+        most 8."""
+        return 1 if self.cost_us < 1.0 else min(8, max(1, num_envs // 16))
+
+    def set_cost(self, cost_us):
+        self.cost_us = float(cost_us)
+        lib().dppo_sim_linear_set_cost(self.ctx, self.cost_us)
 
     def seed(self, seeds):
         s = np.ascontiguousarray(np.asarray(list(seeds), np.int64))
@@ -139,9 +178,12 @@ class LinearSimulator:
 
 class CallbackSimulator:
     """Python simulator behind the callback table. step(idx [n], act [n, Da] f64) -> (obs [n, Do],
-    reward [n], done [n] bool, time_limit [n] int: -1 absent, else 0 / 1); reset(idx) -> obs [n, Do]."""
+    reward [n], done [n] bool, time_limit [n] int: -1 absent, else 0 / 1); reset(idx) -> obs [n, Do].
+    The callbacks take the GIL, so the pool steps a Python simulator on one thread unless the
+    caller passes thread_safe=True (its step / reset keep per-env state only) and asks for more."""
 
-    def __init__(self, obs_dim, action_dim, step, reset, seed=None):
+    def __init__(self, obs_dim, action_dim, step, reset, seed=None, thread_safe=False):
+        self.thread_safe = bool(thread_safe)
         self.obs_dim, self.action_dim = obs_dim, action_dim
         self._step, self._reset, self._seed = step, reset, seed
         self.ctx = None
@@ -182,55 +224,99 @@ class CallbackSimulator:
 class GymSimulator(CallbackSimulator):
     """The reference's simulator: gym.make(id) per env with d4rl's locomotion registrations
     (env/gym_utils/__init__.py:125-174), stepped through the callback table. Needs gym, d4rl and
-    mujoco_py; raises ImportError when they are missing."""
+    mujoco_py; raises ImportError when they are missing (they are absent on the MI355X hosts, so
+    this class is written against their documented API and has not run). mujoco_py's step holds the
+    GIL, so these envs step serially on one thread; a MuJoCo C-API simulator filling the same
+    callback table (one mjData per env) is the intended multi-threaded filler.
+
+    RNG: the reference seeds the GLOBAL NumPy RNG of each worker process
+    (wrapper/mujoco_locomotion_lowdim.py:39-43), one process per env. In one process a loop of
+    np.random.seed calls would leave only the last env's seed, so each env keeps its own global-RNG
+    state: it is swapped in around that env's step / reset and saved after, which reproduces the
+    per-process streams."""
 
     def __init__(self, env_id, num_envs, obs_dim, action_dim):
         import gym
         import d4rl.gym_mujoco  # noqa: F401  (registers the *-medium-v2 ids, as the reference does)
         self.envs = [gym.make(env_id) for _ in range(num_envs)]
+        self._rng_states = [np.random.get_state() for _ in range(num_envs)]
+
+        def on_env(i, fn):
+            outer = np.random.get_state()
+            np.random.set_state(self._rng_states[i])
+            try:
+                return fn(self.envs[i])
+            finally:
+                self._rng_states[i] = np.random.get_state()
+                np.random.set_state(outer)
 
         def step(idx, act):
             obs = np.empty((len(idx), obs_dim))
             rew, done, tl = np.empty(len(idx)), np.empty(len(idx), bool), np.empty(len(idx), np.int8)
             for r, i in enumerate(idx):
-                o, rw, d, info = self.envs[i].step(act[r])
+                o, rw, d, info = on_env(i, lambda e: e.step(act[r]))
                 obs[r], rew[r], done[r] = o, rw, d
                 tl[r] = -1 if "TimeLimit.truncated" not in info else int(bool(info["TimeLimit.truncated"]))
             return obs, rew, done, tl
 
         def reset(idx):
-            return np.stack([np.asarray(self.envs[i].reset(), np.float64) for i in idx])
+            return np.stack([np.asarray(on_env(i, lambda e: e.reset()), np.float64) for i in idx])
 
         def seed(seeds):
-            # MujocoLocomotionLowdimWrapper.seed (:39-43) seeds the worker's global NumPy RNG; the
-            # simulator's own RNG is seeded too so every env's resets are reproducible
-            for e, s in zip(self.envs, seeds):
+            # MujocoLocomotionLowdimWrapper.seed (:39-43): np.random.seed(seed) in the env's own
+            # process, plus the simulator's RNG so resets are reproducible
+            for i, s in enumerate(seeds):
+                outer = np.random.get_state()
                 np.random.seed(int(s))
-                e.seed(int(s))
+                self._rng_states[i] = np.random.get_state()
+                np.random.set_state(outer)
+                self.envs[i].seed(int(s))
 
         super().__init__(obs_dim, action_dim, step, reset, seed)
 
 
 class LowdimVecEnv:
-    """The vector env over a batched simulator (see the module docstring)."""
+    """The vector env over a batched simulator (see the module docstring). num_threads: host
+    threads that step the envs (None: DPPO_ENV_THREADS, else the simulator's suggested_threads(E),
+    else 1)."""
 
-    native = None     # the agent's gated tagged-protocol path is the synthetic stepper's alone
+    _PUBLISHED = 1 << 30
 
     def __init__(self, sim, num_envs, obs_dim, action_dim, act_steps=4, n_obs_steps=1, max_episode_steps=1000,
-                 reset_within_step=True, normalization=None):
+                 reset_within_step=True, normalization=None, num_threads=None):
         self.sim, self.num_envs, self.obs_dim, self.action_dim = sim, num_envs, obs_dim, action_dim
         self.act_steps, self.n_obs_steps = act_steps, n_obs_steps
         self.max_episode_steps = max_episode_steps
         self.norm = normalization
         self._h = None
         self._make(reset_within_step)
+        self.native = lib()            # the agent's gated (pipelined) step runs through this library
+        if num_threads is None:
+            env_t = os.environ.get("DPPO_ENV_THREADS")
+            if env_t:
+                num_threads = int(env_t)
+            else:
+                num_threads = sim.suggested_threads(num_envs) if hasattr(sim, "suggested_threads") else 1
+        self.set_threads(num_threads)
         E, To, Do = num_envs, n_obs_steps, obs_dim
         self._reward = np.empty(E)
         self._term = np.empty(E, np.uint8)
         self._trunc = np.empty(E, np.uint8)
         self._final = np.empty((E, To, Do), np.float32)
         self._has_final = np.empty(E, np.uint8)
+        self._tail = [_p(x) for x in (self._reward, self._term, self._trunc)]
+        self._fin = [_p(self._final), _p(self._has_final)]
         self.published = False
+
+    def set_threads(self, n, spin_us=2000.0):
+        """Host threads stepping the envs (the caller's included); returns the count in use."""
+        if int(n) > 1 and not getattr(self.sim, "thread_safe", False):
+            raise ValueError(f"{type(self.sim).__name__} is not thread-safe: it steps on one thread")
+        got = lib().dppo_lowdim_set_threads(self._h, int(n), float(spin_us))
+        if got < 1:
+            raise RuntimeError("dppo_lowdim_set_threads failed")
+        self.num_threads = got
+        return got
 
     def _make(self, reset_within_step):
         L = lib()
@@ -268,15 +354,33 @@ class LowdimVecEnv:
         return np.ctypeslib.as_array(lib().dppo_lowdim_counters(self._h), (self.num_envs,)).copy()
 
     def step(self, actions, obs_out=None, gate=None):
-        if gate is not None:
-            raise RuntimeError("gated env steps need the synthetic native stepper")
+        """actions [E, Ta, Da] float32; obs_out: optional float32 [E, To, Do] buffer (pinned / mapped
+        staging). gate: the pipelined rollout's arguments (ops.RolloutPipe.gate): ("tagged", done,
+        act_tagged, act_tag, obs_tagged, obs_tag, timeout) — the slice threads wait for the device's
+        action granules, decode them INTO `actions` (so it must be the caller's own C-contiguous
+        float32 array), step, and publish the observation granules — or ("go", done, done_target,
+        go, go_value, timeout). self.published tells the caller whether the observation went out."""
         E = self.num_envs
-        a = np.ascontiguousarray(actions, np.float32).reshape(E, -1, self.action_dim)
+        self.published = False
+        a = actions if (isinstance(actions, np.ndarray) and actions.dtype == np.float32
+                        and actions.flags.c_contiguous) else np.ascontiguousarray(actions, np.float32)
+        if gate is not None and a is not actions:
+            raise ValueError("gated steps decode the device's actions into `actions`: pass a C-contiguous "
+                             "float32 array")
+        ta = a.size // (E * self.action_dim)
         out = obs_out if obs_out is not None else np.empty((E, self.n_obs_steps, self.obs_dim), np.float32)
         assert out.dtype == np.float32 and out.flags.c_contiguous and out.size == E * self.n_obs_steps * self.obs_dim
-        rc = lib().dppo_lowdim_step(self._h, _p(a), a.shape[1], _p(self._reward), _p(self._term), _p(self._trunc),
-                                    _p(out), _p(self._final), _p(self._has_final))
-        self._check(rc, "step")
+        L = lib()
+        if gate is None:
+            rc = L.dppo_lowdim_step(self._h, _p(a), ta, *self._tail, _p(out), *self._fin)
+            self._check(rc, "step")
+        else:
+            fn = L.dppo_lowdim_step_gated_tagged if gate[0] == "tagged" else L.dppo_lowdim_step_gated
+            rc = fn(self._h, _p(a), ta, *self._tail, _p(out), *self._fin, *gate[1:])
+            if rc == -2:
+                raise RuntimeError("pipelined rollout: the device's wait for the observation timed out")
+            self._check(rc, "gated step (simulator error or the sampler step did not finish)")
+            self.published = bool(rc & self._PUBLISHED)
         infos = None
         if self._has_final.any():
             infos = {int(i): {"final_obs": self._final[i].copy()} for i in np.nonzero(self._has_final)[0]}

@@ -175,14 +175,32 @@ class VPGDiffusion(DiffusionModel):
             return keras_weights.load_actor(path, self.actor_spec)
         raise ValueError(f"unsupported checkpoint format: {path}")
 
+    def _eta_checkpoint(self):
+        """The learnable eta's state for a checkpoint: {logit, m, v, step} (None without learn_eta).
+        The original DPPO saves the eta module's logit with the model; m, v and the step count make
+        a resumed run continue the eta optimizer exactly."""
+        if not self.learn_eta:
+            return None
+        logit, m, v = (float(x) for x in self.eta_state.detach().cpu().numpy())
+        return {"logit": logit, "m": m, "v": v, "step": int(self.eta_step_count)}
+
+    def _restore_eta(self, eta):
+        if eta is None or not self.learn_eta:
+            return
+        self.eta_state.copy_(torch.tensor([eta["logit"], eta["m"], eta["v"]], dtype=torch.float32))
+        self.eta_step_count = int(eta["step"])
+        self.refresh_eta()     # the train-mode DDIM table follows the restored logit
+
     def save_weights(self, path):
         """PPODiffusion.save_weights: a Keras-3 weights file for *.h5 (actor/, actor_ft/, critic/;
-        agent/finetune/train_agent.py:127-133), else .npz with actor./actor_ft./critic. keys."""
+        agent/finetune/train_agent.py:127-133), else .npz with actor./actor_ft./critic. keys. A
+        learn_eta model also saves its eta (eta/ group, or eta.state / eta.step keys)."""
+        eta = self._eta_checkpoint()
         if str(path).endswith(".h5"):
             sp = lambda spec, flat: ops.unflatten_params(spec, flat.detach().cpu().numpy())
             keras_weights.save_ppo_model(str(path), sp(self.actor_spec, self.base_params),
                                          sp(self.actor_spec, self.actor_ft_params),
-                                         sp(self.critic_spec, self.critic_params))
+                                         sp(self.critic_spec, self.critic_params), eta=eta)
             return
         d = {}
         for prefix, flat, spec in (("actor.", self.base_params, self.actor_spec),
@@ -190,6 +208,9 @@ class VPGDiffusion(DiffusionModel):
                                    ("critic.", self.critic_params, self.critic_spec)):
             for n, v in ops.unflatten_params(spec, flat.detach().cpu().numpy()).items():
                 d[prefix + n] = v
+        if eta is not None:
+            d["eta.state"] = np.array([eta["logit"], eta["m"], eta["v"]], np.float32)
+            d["eta.step"] = np.array(eta["step"], np.int64)
         np.savez(path, **d)
 
     def load_weights(self, path):
@@ -201,15 +222,22 @@ class VPGDiffusion(DiffusionModel):
                 flat.copy_(torch.tensor(ops.flatten_params(spec, w[key])))
             ops.pack_actor(self.dims, self.base_params, self.precision, out=self.packed_base)
             self.repack()
+            self._restore_eta(w.get("eta"))
             return
+        eta = None
         with np.load(path, allow_pickle=False) as f:
             for prefix, flat, spec in (("actor.", self.base_params, self.actor_spec),
                                        ("actor_ft.", self.actor_ft_params, self.actor_spec),
                                        ("critic.", self.critic_params, self.critic_spec)):
                 if all(prefix + n in f.files for n, _ in spec):
                     flat.copy_(torch.tensor(ops.flatten_params(spec, {n: f[prefix + n] for n, _ in spec})))
+            if "eta.state" in f.files:
+                st = f["eta.state"]
+                eta = {"logit": float(st[0]), "m": float(st[1]), "v": float(st[2]),
+                       "step": int(f["eta.step"]) if "eta.step" in f.files else 0}
         ops.pack_actor(self.dims, self.base_params, self.precision, out=self.packed_base)
         self.repack()
+        self._restore_eta(eta)
 
     # ------------------------------------------------------------------ annealing (diffusion_vpg.py:114-148)
     def step(self):

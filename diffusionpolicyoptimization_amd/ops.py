@@ -182,18 +182,38 @@ def value_moments(values, returns, out_address):
     _lib.call("dppo_value_moments", ptr(values), ptr(returns), int(n), ctypes.c_void_p(out), stream_handle(values.device))
 
 
+class _HostBlock:
+    """Owner of one dppo_host_alloc block: freed (dppo_host_free) when the last view of it is gone.
+    The ctypes array every NumPy / torch view is built on holds it, so no view outlives the memory."""
+
+    def __init__(self, nbytes):
+        p = ctypes.c_void_p()
+        _lib.call("dppo_host_alloc", ctypes.c_size_t(nbytes), ctypes.byref(p))
+        self.address, self.nbytes = p.value, nbytes
+
+    def view(self):
+        buf = (ctypes.c_uint8 * self.nbytes).from_address(self.address)
+        buf.owner = self
+        return np.ctypeslib.as_array(buf)
+
+    def __del__(self):
+        if getattr(self, "address", None) and _lib._lib is not None:
+            _lib.query("dppo_host_free", ctypes.c_void_p(self.address))
+            self.address = None
+
+
 class MappedArray:
     """A NumPy array (and a torch CPU view of it) over coherent mapped pinned memory
-    (dppo_host_alloc): the host writes it, copy_from_host moves it to the device in one kernel."""
+    (dppo_host_alloc): the host writes it, copy_from_host moves it to the device in one kernel.
+    The memory is freed when the MappedArray and every array / tensor view of it are gone; a
+    pending device copy from it must be complete by then (the owner synchronises first)."""
 
     def __init__(self, shape, dtype):
-        self.array = np.zeros(shape, dtype)
-        n = max(1, self.array.nbytes)
-        p = ctypes.c_void_p()
-        _lib.call("dppo_host_alloc", ctypes.c_size_t(n), ctypes.byref(p))
-        self.address = p.value
-        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(self.address))[:self.array.nbytes] \
-            .view(dtype).reshape(shape)
+        nbytes = int(np.prod(shape, dtype=np.int64)) * np.dtype(dtype).itemsize
+        block = _HostBlock(max(1, nbytes))
+        self.address = block.address
+        self.array = block.view()[:nbytes].view(dtype).reshape(shape)
+        self.array[...] = 0
         self.tensor = torch.from_numpy(self.array)
 
 
@@ -550,6 +570,8 @@ class RolloutPipe:
     def close(self):
         for st in self._tstreams:
             st.synchronize()
+        for h in self._handles:     # the split sampler's exchange buffers of these streams go back to the pool
+            _lib.call("dppo_sampler_release_stream", h)
         for b in self._bufs:
             self._lib.dppo_host_free(ctypes.c_void_p(b))
         self._bufs = []

@@ -103,7 +103,7 @@ def _check_unused(path, data, used, model_prefixes, what):
     if unread:
         raise ValueError(f"{path}: {what}: datasets inside the model that this reader does not map (layout "
                          f"differs from the Keras-3 layout in util/keras_weights.py): {unread[:50]}")
-    other = [k for k in data if k != "__groups__" and not any(k.startswith(p) for p in model_prefixes)]
+    other = [k for k in data if k != "__groups__" and k not in used and not any(k.startswith(p) for p in model_prefixes)]
     if other:
         logging.getLogger(__name__).warning("%s: ignoring %d dataset(s) outside the %s: %s", path, len(other), what,
                                             other[:20])
@@ -143,11 +143,21 @@ def load_actor(path, spec, prefixes=("", "network/", "actor/", "actor_ft/")):
     return _checked(got, spec, "actor", path)
 
 
+ETA_LOGIT = "eta/vars/0"                 # EtaFixed's one variable, where Keras 3 writes a sub-layer's weight
+ETA_OPT = "eta/optimizer_state"         # [m, v, step] of its AdamW (resume exactly)
+
+
 def load_ppo_model(path, actor_spec, critic_spec):
-    """{"actor", "actor_ft", "critic"} dicts from a fine-tune checkpoint (PPODiffusion.save_weights)."""
+    """{"actor", "actor_ft", "critic"} dicts from a fine-tune checkpoint (PPODiffusion.save_weights),
+    plus "eta" = {"logit", "m", "v", "step"} when the model learned eta."""
     data = read_h5(path)
     out = {}
     used = set()
+    if ETA_LOGIT in data:
+        opt = np.asarray(data.get(ETA_OPT, np.zeros(3)), np.float64).reshape(-1)
+        out["eta"] = {"logit": float(np.asarray(data[ETA_LOGIT]).reshape(-1)[0]), "m": float(opt[0]),
+                      "v": float(opt[1]), "step": int(opt[2])}
+        used.update(k for k in (ETA_LOGIT, ETA_OPT) if k in data)
     for key, paths, spec in (("actor", actor_paths("actor/"), actor_spec),
                              ("actor_ft", actor_paths("actor_ft/"), actor_spec),
                              ("critic", critic_paths("critic/"), critic_spec)):
@@ -176,14 +186,18 @@ def save_actor(path, params):
              groups=_empty_groups("", "actor"))
 
 
-def save_ppo_model(path, actor, actor_ft, critic):
-    """PPODiffusion.save_weights (agent/finetune/train_agent.py:127-133 layout)."""
+def save_ppo_model(path, actor, actor_ft, critic, eta=None):
+    """PPODiffusion.save_weights (agent/finetune/train_agent.py:127-133 layout); eta: the learnable
+    eta's {"logit", "m", "v", "step"} (learn_eta models), stored under eta/."""
     d = {}
+    if eta is not None:
+        d[ETA_LOGIT] = np.array([eta["logit"]], np.float32)
+        d[ETA_OPT] = np.array([eta["m"], eta["v"], eta["step"]], np.float64)
     for prefix, params, paths in (("actor/", actor, actor_paths("actor/")),
                                   ("actor_ft/", actor_ft, actor_paths("actor_ft/")),
                                   ("critic/", critic, critic_paths("critic/"))):
         for k, v in params.items():
             d[paths[k]] = np.asarray(v, np.float32)
     groups = ["vars"] + _empty_groups("actor/", "actor") + _empty_groups("actor_ft/", "actor") + \
-        _empty_groups("critic/", "critic")
+        _empty_groups("critic/", "critic") + (["eta"] if eta is not None else [])
     write_h5(path, d, groups=groups)

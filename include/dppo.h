@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 9
+#define DPPO_ABI_VERSION 10
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -135,6 +135,13 @@ DPPO_API int dppo_sampler_layout(const dppo_dims* d, int precision, int n_envs, 
  * members wait for: floor(CUs / active workgroups) for the split kernel (>= 1), 8 for the
  * weight-streaming kernel. The pipelined rollout (ops.RolloutPipe) uses at most this many streams. */
 DPPO_API int dppo_sampler_max_in_flight(const dppo_dims* d, int precision, int n_envs, int* launches);
+
+/* ABI 10: the caller is done sampling on `stream` (a closed rollout pipe): waits for the stream's
+ * pending work, then unbinds the exchange buffer the split kernel keeps for it, so a later stream
+ * reuses that buffer instead of a new allocation. Slots are also rebound, without a device-wide
+ * synchronisation, when more than 16 streams sample. (No reference counterpart: the reference's
+ * sampler is a TF call, diffusion_vpg.py:250-339.) */
+DPPO_API int dppo_sampler_release_stream(void* stream);
 
 /* The sampler plan for n_envs envs (measurement aid, ABI 6): plan[0] = kernel (0 weight streaming,
  * 1 split with 8 members per 16-env tile, 2 folded split with P members per tile, 3 the pair kernel:

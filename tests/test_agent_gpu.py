@@ -180,6 +180,75 @@ def test_pipelined_rollout_matches_model_call(cuda, protocol, precision, E, monk
     pipe.close()
 
 
+@pytest.mark.parametrize("protocol,threads", [("tagged", 1), ("tagged", 4), ("go", 3)])
+def test_pipelined_rollout_matches_model_call_lowdim(cuda, protocol, threads, monkeypatch):
+    """The pipelined rollout over the reference's wrapper stack (env/lowdim.py): the gated host step
+    dppo_lowdim_step_gated_tagged (slice threads poll their envs' action granules, step, publish
+    their observation granules) or dppo_lowdim_step_gated (go counter) drives pre-enqueued sampler
+    launches; actions, observations and rewards equal an unpipelined replay (model(obs) -> plain
+    one-thread env step) bit for bit, with terminal states and in-wrapper resets inside the run."""
+    import torch
+
+    monkeypatch.setenv("DPPO_ROLLOUT_PROTOCOL", protocol)
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.env.lowdim import LinearSimulator, LowdimVecEnv, load_normalization
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp", ["model.precision=bf16"])
+    model = instantiate(cfg.model, device=cuda, seed=9)
+    d = model.dims
+    S, E = 24, 40
+    norm = load_normalization(os.path.join(ROOT, "tests", "golden", "hopper_medium_v2_normalization.npz"))
+
+    def make(th):
+        sim = LinearSimulator(E, d.obs_dim, d.action_dim, family_seed=1, norm=norm, bound_frac=0.6)
+        sim.seed([100 + i for i in range(E)])
+        return LowdimVecEnv(sim, E, d.obs_dim, d.action_dim, act_steps=4, n_obs_steps=1, max_episode_steps=40,
+                            normalization=norm, num_threads=th)
+    venv, ref_env = make(threads), make(1)
+    assert venv.num_threads == threads
+    obs_traj = torch.zeros(S, E, d.sd, device=cuda)
+    chains = torch.zeros(S, E, d.ft_denoising_steps + 1, d.xd, device=cuda)
+    act = torch.empty(E, d.xd, device=cuda)
+    pipe = ops.RolloutPipe(model, obs_traj, act, chains)
+    obs_np = pipe.obs.numpy().reshape(E, 1, d.obs_dim)
+    act_view = pipe.act.numpy().reshape(E, 4, d.action_dim)
+    obs_np[:] = venv.reset_arg()["state"]
+    obs0 = obs_np.copy()
+    cid0 = model._call_id
+    got_a, got_o, got_r, n_done = [], [], [], 0
+    pipe.begin()
+    pipe.enqueue(0)
+    pipe.publish()
+    for i in range(S):
+        more = i + 1 < S
+        if more:
+            pipe.enqueue(i + 1)
+        _, r, term, trunc, _ = venv.step(act_view, obs_out=obs_np, gate=pipe.gate(publish=more))
+        assert venv.published == more
+        if more:
+            pipe.published_by_gate()
+        got_a.append(act_view.copy())
+        got_o.append(obs_np.copy())
+        got_r.append(r)
+        n_done += int((term | trunc).sum())
+    pipe.end()
+    torch.cuda.synchronize()
+    assert n_done > 0
+    model._call_id = cid0
+    o = ref_env.reset_arg()["state"]
+    np.testing.assert_array_equal(o, obs0)
+    for i in range(S):
+        np.testing.assert_array_equal(obs_traj[i].cpu().numpy(), o.reshape(E, -1))
+        ref = model(torch.tensor(o.reshape(E, -1), device=cuda), return_chain=True)
+        a = ref.trajectories.reshape(E, 4, d.action_dim).cpu().numpy()
+        np.testing.assert_array_equal(got_a[i], a)
+        ob, r, _, _, _ = ref_env.step(a)
+        o = ob["state"].copy()
+        np.testing.assert_array_equal(got_o[i], o)
+        np.testing.assert_array_equal(got_r[i], r)
+    pipe.close()
+
+
 @pytest.mark.parametrize("overrides", ["", "train.dp_scale_batch=true"], ids=["reference-batch", "scaled-batch"])
 def test_data_parallel_agent_two_ranks_share_one_gpu(tmp_path, overrides):
     """2 ranks (gloo, both on cuda:0) run the DP agent; replicas must stay bit-identical, with the
@@ -332,6 +401,52 @@ def test_split_update_matches_fused(cuda, tmp_path, monkeypatch):
         assert abs(r1[k] - r0[k]) <= 1e-3 * (abs(r0[k]) + 1e-3), (k, r1[k], r0[k])
 
 
+@pytest.mark.parametrize("cfg_name", ["ft_ppo_diffusion_mlp", "ft_ppo_diffusion_mlp_ddim_learn_eta"])
+def test_split_dp_update_matches_fused_dp(cuda, tmp_path, monkeypatch, cfg_name):
+    """the split update under data parallelism (parts 2 / 4 / 5, two gradient buckets
+    all-reduced from two streams: critic + metrics + d loss / d eta on the side stream during the
+    actor's dW, then the actor's) against the fused data-parallel path (one collective per
+    minibatch). One process plays rank 0 of W = 2 with an all-reduce that sums two identical
+    replicas (x 2, issued on the stream the agent calls it from), so both paths run every stream
+    ordering and bucket boundary of the real DP update; gradients, metrics, the KL / eta steps and
+    the parameters must agree up to the float-atomic order the single-GPU split test allows."""
+    import torch
+
+    from diffusionpolicyoptimization_amd.util.config import get_class, load_config
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DPPO_SPLIT_UPDATE", flag)
+        extra = ["env.n_envs=8", "train.n_critic_warmup_itr=0", "train.eta_lr=1e-2"] if "eta" in cfg_name else []
+        cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), cfg_name,
+                          ["model.precision=fp32", "train.n_steps=20", "train.batch_size=200", "train.n_train_itr=2",
+                           "train.val_freq=100", f"logdir={tmp_path}/{flag}"] + extra)
+        a = get_class(cfg._target_)(cfg)
+        a.world_size = 2                          # rank 0 of 2; every reduction goes through _allreduce
+        calls = []
+
+        def replica_sum(t, calls=calls):
+            calls.append(t.numel())
+            return t.mul_(2.0)
+        a._allreduce = replica_sum
+        res = a.run()
+        torch.cuda.synchronize()
+        m = a.model
+        out[flag] = (m.train_params.cpu().numpy().copy(), res[-1], a.timing["n_updates"], calls,
+                     m.current_eta(), getattr(m, "eta_step_count", 0))
+    p1, r1, n1, c1, e1, s1 = out["1"]
+    p0, r0, n0, c0, e0, s0 = out["0"]
+    assert n1 == n0 > 0 and s1 == s0
+    na = m.n_actor
+    # the split path all-reduces two buckets per minibatch (critic + metrics, then the actor), the
+    # fused one one bucket; both once for the advantage-moment table and the episode sums
+    assert sorted(set(c1)) != sorted(set(c0)) and na in c1 and m.grads_ext.numel() in c0
+    d = np.abs(p1 - p0)
+    assert np.median(d) < 1e-6 and d.max() < 5e-3, (float(np.median(d)), float(d.max()))
+    for k in ("pg_loss", "v_loss", "approx_kl", "clipfrac"):
+        assert abs(r1[k] - r0[k]) <= 1e-3 * (abs(r0[k]) + 1e-3), (k, r1[k], r0[k])
+    assert abs(e1 - e0) <= 1e-5 * abs(e0), (e1, e0)
+
+
 @pytest.mark.parametrize("protocol", ["tagged", "go"])
 def test_pipelined_rollout_unpublished_observation_times_out(cuda, protocol, monkeypatch):
     """A launch whose observation never comes (the host died or stalled) gives up after its
@@ -423,3 +538,16 @@ def test_learn_eta_agent_iterations(cuda, tmp_path):
     ev = ops.sched_table(ddim_buffers(20, 10, 0.0))
     np.testing.assert_array_equal(m.sched_eval.cpu().numpy(), ev)
     assert np.isfinite(m.train_params.cpu().numpy()).all()
+    # the eta state is part of the checkpoint (h5 and npz); a fresh model restores
+    # logit, moments and step count, and its train-mode DDIM table follows the restored eta
+    from diffusionpolicyoptimization_amd.util.config import instantiate
+    for ext in ("weights.h5", "npz"):
+        path = str(tmp_path / f"eta_ckpt.{ext}")
+        m.save_weights(path)
+        m2 = instantiate(cfg.model, device=cuda)
+        assert abs(m2.current_eta() - 0.5) < 1e-6
+        m2.load_weights(path)
+        assert torch.equal(m2.eta_state, m.eta_state) and m2.eta_step_count == m.eta_step_count
+        assert m2.current_eta() == m.current_eta()
+        np.testing.assert_array_equal(m2.sched.cpu().numpy(), m.sched.cpu().numpy())
+        assert torch.equal(m2.train_params, m.train_params)

@@ -166,3 +166,132 @@ def test_make_async_is_explicit_about_the_stepper(tmp_path):
     assert o.shape == (2, 1, 11) and np.isfinite(o).all()
     with pytest.raises(ValueError):
         make_async("hopper-medium-v2", num_envs=2, obs_dim=11, action_dim=3, synthetic="mujoco")
+
+
+# ---- the thread pool and the gated (pipelined) step (csrc/envwrap.c, dppo_lowdim_set_threads) ----
+def _lowdim(E, threads, To=2, cost_us=0.0, max_steps=10):
+    from diffusionpolicyoptimization_amd.env.lowdim import LinearSimulator, LowdimVecEnv
+    nm = _norm()
+    sim = LinearSimulator(E, 11, 3, family_seed=3, norm=nm, bound_frac=0.5, cost_us=cost_us)
+    sim.seed([42 + i for i in range(E)])
+    return LowdimVecEnv(sim, E, 11, 3, act_steps=4, n_obs_steps=To, max_episode_steps=max_steps,
+                        reset_within_step=True, normalization=nm, num_threads=threads)
+
+
+@pytest.mark.parametrize("threads", [2, 3, 8, 64])
+def test_thread_pool_is_bit_identical_to_one_thread(threads):
+    E = 37                                  # ragged slices
+    one, many = _lowdim(E, 1), _lowdim(E, threads)
+    assert one.num_threads == 1 and many.num_threads == min(threads, E)
+    np.testing.assert_array_equal(one.reset_arg()["state"], many.reset_arg()["state"])
+    rng = np.random.default_rng(7)
+    n_done = 0
+    for _ in range(60):
+        a = rng.uniform(-1.2, 1.2, (E, 4, 3)).astype(np.float32)
+        o1, r1, t1, u1, i1 = one.step(a)
+        o2, r2, t2, u2, i2 = many.step(a)
+        np.testing.assert_array_equal(o1["state"], o2["state"])
+        np.testing.assert_array_equal(r1, r2)
+        np.testing.assert_array_equal(t1, t2)
+        np.testing.assert_array_equal(u1, u2)
+        assert (i1 or {}).keys() == (i2 or {}).keys()
+        for k in i1 or {}:
+            np.testing.assert_array_equal(i1[k]["final_obs"], i2[k]["final_obs"])
+        n_done += int((t1 | u1).sum())
+    np.testing.assert_array_equal(one.counters, many.counters)
+    assert n_done > 0
+
+
+def test_thread_pool_survives_resize_and_idle_sleep():
+    import time
+    v = _lowdim(16, 4)
+    v.set_threads(4, spin_us=50.0)          # idle workers sleep after 50 us
+    v.reset_arg()
+    a = np.zeros((16, 4, 3), np.float32)
+    v.step(a)
+    time.sleep(0.05)                        # every worker is asleep on the condition variable now
+    v.step(a)
+    assert v.set_threads(2) == 2 and v.set_threads(1) == 1 and v.set_threads(5) == 5
+    v.step(a)
+    v.close()
+
+
+def test_python_simulator_refuses_threads():
+    from diffusionpolicyoptimization_amd.env.lowdim import CallbackSimulator, LowdimVecEnv
+    sim = CallbackSimulator(2, 1, lambda i, a: None, lambda idx: np.zeros((len(idx), 2)))
+    v = LowdimVecEnv(sim, 8, 2, 1)
+    assert v.num_threads == 1
+    with pytest.raises(ValueError, match="thread-safe"):
+        v.set_threads(4)
+
+
+class _Granules:
+    """The mapped-memory side of ops.RolloutPipe's tagged protocol, in plain host memory: the
+    device's done word, its action granules {tag : 32, fp32 bits : 32} and the observation
+    granules the host publishes."""
+
+    def __init__(self, E, xd, od):
+        self.done = np.zeros(16, np.uint32)
+        self.act = np.zeros(E * xd, np.uint64)
+        self.obs = np.zeros(E * od, np.uint64)
+
+    def put_actions(self, a, tag):
+        self.act[:] = (np.uint64(tag) << np.uint64(32)) | a.reshape(-1).view(np.uint32).astype(np.uint64)
+
+    def gate(self, act_tag, obs_tag, timeout=5.0, publish=True):
+        import ctypes
+        P = lambda x: ctypes.c_void_p(x.ctypes.data)
+        return ("tagged", P(self.done), P(self.act), ctypes.c_uint32(act_tag), P(self.obs) if publish else None,
+                ctypes.c_uint32(obs_tag), ctypes.c_double(timeout))
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_gated_tagged_step_matches_plain_step(threads):
+    """dppo_lowdim_step_gated_tagged: decode the action granules into the caller's buffer, step,
+    publish every observation granule with the tag — the same chunk as the plain step."""
+    import threading
+    import time
+    E, To = 24, 2
+    ref, gated = _lowdim(E, 1, To=To), _lowdim(E, threads, To=To)
+    np.testing.assert_array_equal(ref.reset_arg()["state"], gated.reset_arg()["state"])
+    g = _Granules(E, 12, To * 11)
+    act_buf = np.zeros((E, 4, 3), np.float32)
+    obs_buf = np.zeros((E, To, 11), np.float32)
+    rng = np.random.default_rng(3)
+    for step in range(1, 31):
+        a = rng.uniform(-1.2, 1.2, (E, 4, 3)).astype(np.float32)
+        if step % 3 == 0:   # the "device" stores its actions while the slices already spin
+            t = threading.Timer(0.002, g.put_actions, (a, step))
+            t.start()
+        else:
+            g.put_actions(a, step)
+        o2, r2, t2, u2, _ = gated.step(act_buf, obs_out=obs_buf, gate=g.gate(step, 100 + step))
+        if step % 3 == 0:
+            t.join()
+        assert gated.published
+        np.testing.assert_array_equal(act_buf, a)
+        o1, r1, t1, u1, _ = ref.step(a)
+        np.testing.assert_array_equal(o1["state"], obs_buf)
+        np.testing.assert_array_equal(r1, r2)
+        np.testing.assert_array_equal(t1 | u1, t2 | u2)
+        assert ((g.obs >> np.uint64(32)) == 100 + step).all()
+        np.testing.assert_array_equal((g.obs & np.uint64(0xFFFFFFFF)).astype(np.uint32),
+                                      obs_buf.reshape(-1).view(np.uint32))
+    time.sleep(0)
+
+
+def test_gated_step_timeouts_and_device_flag():
+    E = 8
+    v = _lowdim(E, 2)
+    v.reset_arg()
+    g = _Granules(E, 12, 22)
+    act_buf = np.zeros((E, 4, 3), np.float32)
+    g.put_actions(act_buf, 1)
+    with pytest.raises(RuntimeError, match="did not finish"):
+        v.step(act_buf, obs_out=np.zeros((E, 2, 11), np.float32), gate=g.gate(2, 5, timeout=0.05))
+    g.done[0] = np.uint32(0x80000000)
+    with pytest.raises(RuntimeError, match="device's wait"):
+        v.step(act_buf, obs_out=np.zeros((E, 2, 11), np.float32), gate=g.gate(2, 5, timeout=5.0))
+    g.done[0] = 0
+    with pytest.raises(ValueError, match="C-contiguous"):
+        v.step(act_buf[:, :2], gate=g.gate(1, 5))

@@ -151,3 +151,24 @@ def test_keras_reader_fails_loudly_on_unmapped_variables(tmp_path):
         KW.load_ppo_model(r, a_spec, c_spec)
     with pytest.raises(ValueError, match="extra_layer"):
         KW.load_actor(r, a_spec, prefixes=("actor_ft/",))
+
+
+def test_ppo_checkpoint_carries_learnable_eta(tmp_path):
+    """A learn_eta model's checkpoint holds the eta logit (eta/vars/0, where Keras 3 writes a
+    sub-layer's variable) and its optimizer state; a model without it has no eta group."""
+    import numpy as np
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util import keras_weights as K
+    d = ops.ModelDims()
+    a, c = ops.actor_param_spec(d), ops.critic_param_spec(d)
+    rng = np.random.default_rng(0)
+    A = {n: rng.normal(size=s).astype(np.float32) for n, s in a}
+    C = {n: rng.normal(size=s).astype(np.float32) for n, s in c}
+    p = str(tmp_path / "eta.weights.h5")
+    K.save_ppo_model(p, A, A, C, eta={"logit": 0.25, "m": 1e-3, "v": 2e-6, "step": 7})
+    w = K.load_ppo_model(p, a, c)
+    assert w["eta"] == {"logit": 0.25, "m": 1e-3, "v": 2e-6, "step": 7}
+    np.testing.assert_array_equal(w["critic"]["l1_w"], C["l1_w"])
+    q = str(tmp_path / "plain.weights.h5")
+    K.save_ppo_model(q, A, A, C)
+    assert "eta" not in K.load_ppo_model(q, a, c)

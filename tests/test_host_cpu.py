@@ -41,7 +41,24 @@ def test_library_exports_every_declared_symbol(lib):
     exported = set(re.findall(r"\bT (dppo_\w+)", nm))
     assert set(_declared()) <= exported
     assert exported <= set(_declared()), f"undeclared exports: {exported - set(_declared())}"
-    assert lib.dppo_abi_version() == 9
+    assert lib.dppo_abi_version() == 10
+
+
+def test_env_library_exports_exactly_its_header():
+    """libdppo_env.so (the wrapper stack, its thread pool, the synthetic stepper) exports exactly the
+    functions include/dppo_env.h declares."""
+    from diffusionpolicyoptimization_amd.env.synthetic import _ENV_LIB
+    if not os.path.exists(_ENV_LIB):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "diffusionpolicyoptimization_amd", "csrc"),
+                        "../lib/libdppo_env.so"], check=True)
+    src = open(os.path.join(ROOT, "include", "dppo_env.h")).read()
+    declared = set(re.findall(r"^[\w\s\*]+?\b(dppo_\w+)\s*\(", src, flags=re.M))
+    assert len(declared) >= 25
+    nm = subprocess.run(["nm", "-D", "--defined-only", _ENV_LIB], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (dppo_\w+)", nm))
+    assert declared == exported, (declared ^ exported)
+    L = ctypes.CDLL(_ENV_LIB)
+    assert L.dppo_lowdim_abi() == 2 and L.dppo_env_abi() == 3
 
 
 def test_host_queries_match_python_layout(lib):

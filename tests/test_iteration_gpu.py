@@ -209,12 +209,14 @@ def test_iterations_match_oracle_with_annealing(cuda, tmp_path):
     assert kfs == [10, 9, 8] and a.chains_traj.shape[2] == 9 and a.lp_old.shape[1] == 8
 
 
-def test_iterations_match_oracle_lowdim_env(cuda, tmp_path):
+@pytest.mark.parametrize("threads", [1, 4])
+def test_iterations_match_oracle_lowdim_env(cuda, tmp_path, threads):
     """The agent on the reference's wrapper stack (env.synthetic = lowdim: MultiStep +
     MujocoLocomotionLowdimWrapper batched in C over the C reference simulator, normalised by the
     reference's own hopper normalization.npz; env/lowdim.py) against the loop oracle over the
-    per-env NumPy restatement of the same wrappers (oracle/envstack.py): the unpipelined host
-    path (pipe.wait + step + publish) with terminal states as well as truncations."""
+    per-env NumPy restatement of the same wrappers (oracle/envstack.py): the pipelined host path
+    (the gated tagged step of csrc/envwrap.c on 1 or 4 host threads) with terminal states as well
+    as truncations."""
     from oracle.envstack import LinearSimOracle, LowdimVecEnvOracle
     norm_path = os.path.join(ROOT, "tests", "golden", "hopper_medium_v2_normalization.npz")
 
@@ -224,10 +226,11 @@ def test_iterations_match_oracle_lowdim_env(cuda, tmp_path):
         sims = [LinearSimOracle(sim.A, sim.B, sim.c, sim.goal, sim.center, sim.scale, sim.bound, s) for s in seeds]
         return LowdimVecEnvOracle(sims, nm, cfg.obs_dim, cfg.action_dim, cfg.act_steps, cfg.env.max_episode_steps)
 
-    a, orc = _agent_and_oracle(42, tmp_path, ["env.synthetic=lowdim",
+    a, orc = _agent_and_oracle(42, tmp_path, ["env.synthetic=lowdim", f"+env.num_threads={threads}",
                                               f"+env.wrappers.mujoco_locomotion_lowdim.normalization_path={norm_path}"],
                                env_oracle=env_oracle)
     from diffusionpolicyoptimization_amd.env.lowdim import LowdimVecEnv
-    assert isinstance(a.venv, LowdimVecEnv) and a.venv.norm is not None
+    assert isinstance(a.venv, LowdimVecEnv) and a.venv.norm is not None and a.venv.num_threads == threads
+    assert a.pipe is not None and a.venv.native is not None       # the gated (pipelined) host step runs
     errs = _run_and_compare(a, orc)
-    _record("lowdim_env", errs)
+    _record(f"lowdim_env_t{threads}", errs)

@@ -334,6 +334,48 @@ def test_reward_scale_multi_call(cuda):
         np.testing.assert_allclose(rms.cpu().numpy(), [orc.mean, orc.var, orc.count], rtol=1e-10)
 
 
+@pytest.mark.parametrize("entry", ["dppo_reward_scale", "RunningRewardScaler.scale_", "RunningRewardScaler.__call__"])
+def test_reward_scale_matches_reference_goldens(cuda, entry):
+    """a18 pinned on the GPU directly: tests/golden/reward_scaling.npz holds outputs of the
+    reference's own util/reward_scaling.py (RunningRewardScaler, :42-87, generated by
+    tests/golden/make_golden.py) over 4 shapes and 2-4 consecutive calls each. Every call of every
+    case goes through the fp64 kernels with the scaler state (ret, mean / var / count) carried
+    between calls, through the raw C-ABI entry, the agent's time-major scale_() and the
+    reference-signature __call__; outputs, ret and (mean, var, count) at rtol 1e-12."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.reward_scaling import RunningRewardScaler
+    g = np.load(os.path.join(ROOT, "tests", "golden", "reward_scaling.npz"))
+    ci = 0
+    while f"c{ci}_meta" in g:
+        E, S, n_calls = (int(x) for x in g[f"c{ci}_meta"])
+        ret = torch.zeros(E, dtype=torch.float64, device=cuda)
+        rms = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=cuda)
+        sc = RunningRewardScaler(E, device=cuda)
+        for k in range(n_calls):
+            p = f"c{ci}_k{k}_"
+            r, first = g[p + "reward"], g[p + "first"]          # [E, S], the reference's layout
+            if entry == "dppo_reward_scale":
+                rt = torch.tensor(np.ascontiguousarray(r.T), device=cuda)
+                ops.reward_scale(rt, torch.tensor(np.ascontiguousarray(first.T).astype(np.uint8), device=cuda), ret, rms)
+                out = rt.cpu().numpy().T
+                state = (ret, rms)
+            elif entry == "RunningRewardScaler.scale_":
+                rt = torch.tensor(np.ascontiguousarray(r.T), device=cuda)
+                sc.scale_(rt, torch.tensor(np.ascontiguousarray(first.T).astype(np.uint8), device=cuda))
+                out = rt.cpu().numpy().T
+                state = (sc.ret, sc.rms)
+            else:
+                out = sc(reward=r, first=first)
+                state = (sc.ret, sc.rms)
+            torch.cuda.synchronize()
+            np.testing.assert_allclose(out, g[p + "out"], rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(state[0].cpu().numpy(), g[p + "ret"], rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(state[1].cpu().numpy(), g[p + "rms"], rtol=1e-12)
+        ci += 1
+    assert ci == 4
+
+
 def test_feistel_bit_exact(cuda):
     from diffusionpolicyoptimization_amd import ops
     for n, seed, ep in [(320000, 42, 0), (1000, 7, 3), (13, 1, 1), (1, 5, 0)]:
