@@ -103,35 +103,65 @@ def cpu_baseline(cfg, n_envs, S, bs):
 
 # per-kernel figures (north_star: "achieved HBM GB/s on the DDPM/GAE kernels and MFMA utilisation
 # on the denoiser GEMMs"), computed from ALGORITHMIC bytes / FLOPs (with the dtypes
-# the kernels actually move) over the rocprofv3 --kernel-trace --stats averages of a committed
-# whole-iteration profile of this workload, so each figure reproduces from that CSV
+# the kernels actually move) over per-kernel launch times. The figures are measured LIVE in this
+# run: the library's kernel timer (dppo_kernel_timing, HIP events around each launch on its own
+# stream) over one instrumented iteration. The committed rocprofv3 whole-iteration trace of the
+# same workload is reported beside them as a cross-check.
 KERNEL_STATS_CSV = os.path.join(ROOT, "profiles", "r03x_iteration_kernel_stats.csv")
 
 
-def kernel_figures(d, S, E, batch, n_mb, precision, path=KERNEL_STATS_CSV):
+def kernel_times_live(agent):
+    """One untimed iteration with the library's kernel timer on: {kernel: (total_ms, launches)}."""
+    import ctypes
+
+    import numpy as np
+    from diffusionpolicyoptimization_amd import _lib
+    lib = _lib.load()
+    names = []
+    while True:
+        nm = lib.dppo_kernel_timing_name(len(names))
+        if not nm:
+            break
+        names.append(nm.decode())
+    _lib.call("dppo_kernel_timing", 1)
+    try:
+        agent.iteration(force_train=True)
+        tot = np.zeros(len(names))
+        cnt = np.zeros(len(names), np.int64)
+        _lib.call("dppo_kernel_timing_read", len(names), ctypes.c_void_p(tot.ctypes.data), ctypes.c_void_p(cnt.ctypes.data))
+    finally:
+        _lib.call("dppo_kernel_timing", 0)
+    return {n: (float(t), int(c)) for n, t, c in zip(names, tot, cnt) if c > 0}
+
+
+def kernel_stats_csv(path=KERNEL_STATS_CSV):
+    """{base kernel name: (total_ms, launches)} of a committed rocprofv3 --stats CSV (the cross-check)."""
     import csv
     if not os.path.exists(path):
         return None
-    stats = {}
+    out = {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            stats[r["Name"]] = (int(r["Calls"]), float(r["TotalDurationNs"]), float(r["AverageNs"]))
+            k = r["Name"]
+            k = k[5:] if k.startswith("void ") else k
+            base = k.split("<")[0].split("(")[0].split("::")[-1]
+            if "pack_all_kernel" in base:
+                base = "pack_all_kernel"
+            elif base.startswith("actor_rowtile_kernel"):
+                base = "actor_rowtile_train" if "true" in k else "actor_rowtile_logprob"
+            elif base.startswith("critic_rowtile_kernel"):
+                base = "critic_rowtile_train" if "true" in k else "critic_rowtile_forward"
+            elif base == "adv_stats_all_kernel":
+                base = "adv_stats_kernel"
+            tot, calls = float(r["TotalDurationNs"]) / 1e6, int(r["Calls"])
+            t0, c0 = out.get(base, (0.0, 0))
+            out[base] = (t0 + tot, c0 + calls)
+    return out
 
-    def base(k):   # "void dw_kernel<PolicyBF16, 256>(DWArgs)" -> "dw_kernel"
-        k = k[5:] if k.startswith("void ") else k
-        k = k.split("<")[0].split("(")[0]
-        return k.split("::")[-1]
 
-    def find(name, must=""):
-        ks = [k for k in stats if base(k) == name and must in k]
-        return max(ks, key=lambda k: stats[k][0]) if ks else None
-
-    out = {"source": os.path.relpath(path, ROOT), "hbm_peak_GBs": HBM_PEAK_GBS}
-    # minibatches the profile covers: one actor TRAIN row-tile launch each
-    kt = find("actor_rowtile_kernel", "true")
-    n_mb_iter = n_mb                              # minibatches per iteration
-    n_mb = stats[kt][0] if kt else n_mb           # minibatches the profile covers
-    n_iter = max(1, round(n_mb / n_mb_iter)) if n_mb_iter else 1
+def kernel_figures(d, S, E, batch, n_mb, precision, times, source, iters=1):
+    """times: {kernel: (total_ms, launches)} over `iters` iterations with n_mb minibatches of `batch` rows."""
+    out = {"source": source, "hbm_peak_GBs": HBM_PEAK_GBS, "minibatches": n_mb}
     N = S * E
     na = d.actor_in * d.actor_hidden + 2 * d.actor_hidden ** 2 + d.actor_hidden * d.xd  # actor weights (MACs/row)
     n_par = None
@@ -149,46 +179,57 @@ def kernel_figures(d, S, E, batch, n_mb, precision, path=KERNEL_STATS_CSV):
         "scale_apply_kernel": (16 * N, "16 B per (t, e)"),
     }
     for name, (nbytes, note) in hbm.items():
-        k = find(name)
-        if k:
-            calls, tot, avg = stats[k]
-            out[name] = {"bytes_per_launch": nbytes, "avg_us": avg / 1e3, "achieved_GBs": nbytes / avg,
-                         "frac": nbytes / avg / HBM_PEAK_GBS, "note": note}
-    k = find("adamw_kernel")
-    if k and n_par:
-        calls, tot, avg = stats[k]
+        if name in times:
+            tot, calls = times[name]
+            avg = tot / calls * 1e6          # ns
+            out[name] = {"bytes_per_launch": nbytes, "launches": calls, "avg_us": avg / 1e3,
+                         "achieved_GBs": nbytes / avg, "frac": nbytes / avg / HBM_PEAK_GBS, "note": note}
+    if "adamw_kernel" in times and n_par:
+        tot, calls = times["adamw_kernel"]
         per_mb = 28 * n_par            # p, g, m, v in; p, m, v out (fp32) over actor_ft + critic
+        ns = tot * 1e6 / n_mb
         out["adamw_kernel"] = {"bytes_per_minibatch": per_mb, "launches_per_minibatch": calls / n_mb,
-                               "us_per_minibatch": tot / n_mb / 1e3, "achieved_GBs": per_mb / (tot / n_mb),
-                               "frac": per_mb / (tot / n_mb) / HBM_PEAK_GBS,
+                               "us_per_minibatch": ns / 1e3, "achieved_GBs": per_mb / ns, "frac": per_mb / ns / HBM_PEAK_GBS,
                                "note": "28 B per parameter, actor and critic ranges summed (two launches under "
-                                       "the split update); durations include sharing the CUs with the other stream"}
+                                       "the split update, on two streams); durations include sharing the CUs"}
     peak = PEAK["bf16" if precision in ("bf16", "fp16") else "fp32"]
-    k = find("actor_rowtile_kernel", "true")
-    if k:
-        calls, tot, avg = stats[k]
+    if "actor_rowtile_train" in times:
+        tot, calls = times["actor_rowtile_train"]
         fl = 2 * 2 * na * batch            # forward + backward-dX of the actor, per minibatch
-        out["actor_rowtile_train"] = {"flops_per_launch": fl, "avg_us": avg / 1e3, "achieved_TFLOPs": fl / avg / 1e3,
-                                      "frac": fl / avg / 1e3 / peak}
-    k = find("dw_kernel")
-    if k:
-        calls, tot, avg = stats[k]
+        ns = tot * 1e6 / n_mb
+        out["actor_rowtile_train"] = {"flops_per_minibatch": fl, "launches": calls, "us_per_minibatch": ns / 1e3,
+                                      "achieved_TFLOPs": fl / ns / 1e3, "frac": fl / ns / 1e3 / peak}
+    dw = [times[k] for k in ("dw_kernel_actor", "dw_kernel_critic", "dw_kernel") if k in times]
+    if dw:
+        tot = sum(t for t, _ in dw)
         hc = d.critic_hidden
         nc = d.sd * hc + 2 * hc * hc + hc
         fl = 2 * (na + nc) * batch         # actor + critic weight gradients over the minibatch rows
-        out["dw_kernel"] = {"flops_per_minibatch": fl, "us_per_minibatch": tot / n_mb / 1e3,
-                            "achieved_TFLOPs": fl / (tot / n_mb) / 1e3, "frac": fl / (tot / n_mb) / 1e3 / peak,
+        ns = tot * 1e6 / n_mb
+        out["dw_kernel"] = {"flops_per_minibatch": fl, "us_per_minibatch": ns / 1e3,
+                            "achieved_TFLOPs": fl / ns / 1e3, "frac": fl / ns / 1e3 / peak,
                             "note": "actor + critic launches summed; algorithmic FLOPs as the reference computes "
                                     "them (every row for the critic, which runs on distinct samples only; l2's "
                                     "H x H weight gradient, which the kernels form as (u2^T dy) W_out^T)"}
-    k = find("actor_rowtile_kernel", "false")
-    if k:
-        calls, tot, avg = stats[k]
-        fl = 2 * na * N * d.ft_denoising_steps * n_iter   # the old-log-prob pass over S*E*K' rows per iteration
-        out["actor_rowtile_logprob"] = {"flops_per_launch": fl / calls, "launches": calls, "avg_us": avg / 1e3,
-                                        "achieved_TFLOPs": fl / tot / 1e3, "frac": fl / tot / 1e3 / peak,
+        for k in ("dw_kernel_actor", "dw_kernel_critic"):
+            if k in times:
+                out["dw_kernel"][k.replace("dw_kernel_", "") + "_us_per_minibatch"] = times[k][0] * 1e3 / n_mb
+    if "actor_rowtile_logprob" in times:
+        tot, calls = times["actor_rowtile_logprob"]
+        fl = 2 * na * N * d.ft_denoising_steps * iters   # the old-log-prob pass over S*E*K' rows per iteration
+        out["actor_rowtile_logprob"] = {"flops_per_iteration": fl, "launches": calls, "avg_us": tot * 1e3 / calls,
+                                        "achieved_TFLOPs": fl / (tot * 1e9), "frac": fl / (tot * 1e9) / peak,
                                         "note": "launched in chunks during the rollout (every 10 env steps, beside "
-                                                "the sampler), so the FLOPs are summed over the profile's launches"}
+                                                "the sampler), so the FLOPs are summed over the iteration's launches"}
+    for k in ("time_bwd_kernel", "l2_back_kernel", "pack_all_kernel", "zero_kernel", "crit_rows_kernel",
+              "critic_rowtile_train", "critic_rowtile_forward", "adv_stats_kernel"):
+        if k in times:
+            tot, calls = times[k]
+            out.setdefault("latency_kernels_us", {})[k] = {"launches": calls, "avg_us": tot * 1e3 / calls}
+    if "sampler" in times:
+        tot, calls = times["sampler"]
+        out["sampler_in_rollout"] = {"launches": calls, "avg_us": tot * 1e3 / calls,
+                                     "note": "pipelined launches: each includes its wait for the host's observation"}
     return out
 
 
@@ -387,8 +428,19 @@ def main():
         "host_us_per_minibatch": host_us,
     }
     n_mb_iter = n_updates / max(1, args.steps)
-    figs = kernel_figures(d, cfg.train.n_steps, agent.n_envs, cfg.train.batch_size // emu, n_mb_iter or 1, prec)
-    if figs is not None and emu == 1:
+    if emu == 1:
+        mb_before = agent.timing["n_updates"]
+        live = kernel_times_live(agent)
+        n_mb_live = agent.timing["n_updates"] - mb_before
+        figs = kernel_figures(d, cfg.train.n_steps, agent.n_envs, cfg.train.batch_size, n_mb_live or 1, prec, live,
+                              "live: dppo_kernel_timing (HIP events around each launch) over one untimed iteration")
+        prof = kernel_stats_csv()
+        if prof:
+            n_mb_prof = prof.get("actor_rowtile_train", (0, n_mb_live))[1] or n_mb_live
+            cross = kernel_figures(d, cfg.train.n_steps, agent.n_envs, cfg.train.batch_size, n_mb_prof, prec, prof,
+                                   os.path.relpath(KERNEL_STATS_CSV, ROOT),
+                                   iters=max(1, round(n_mb_prof / max(1, n_mb_live))))
+            figs["profile_crosscheck"] = {k: v for k, v in cross.items() if k != "hbm_peak_GBs"}
         out["kernels"] = figs
     if emu > 1:
         out["emulated_ranks"] = emu

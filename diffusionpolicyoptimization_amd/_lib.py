@@ -69,6 +69,9 @@ _SIGNATURES = {
     "dppo_sampler_max_in_flight": (_I, [_DIMS, _I, _I, ctypes.POINTER(ctypes.c_int)]),
     "dppo_sampler_plan": (_I, [_DIMS, _I, _I, ctypes.POINTER(ctypes.c_int)]),
     "dppo_sampler_release_stream": (_I, [_P]),
+    "dppo_kernel_timing": (_I, [_I]),
+    "dppo_kernel_timing_name": (ctypes.c_char_p, [_I]),
+    "dppo_kernel_timing_read": (_I, [_I, _P, _P]),
     "dppo_logprob": (_I, [_DIMS, _I, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P]),
     "dppo_critic_forward": (_I, [_DIMS, _I, _P, _P, _I, _P, _P]),
     "dppo_reward_scale_workspace_doubles": (_SZ, [_I, _I]),

@@ -1,6 +1,8 @@
 // api.hip — C-ABI plumbing of libdppo_hip.so: errors, dimension checks, sizes, packing entry points.
 #include <stdarg.h>
 #include <stdio.h>
+#include <mutex>
+#include <vector>
 #include "dppo_common.cuh"
 #include "dppo_internal.h"
 
@@ -77,4 +79,82 @@ extern "C" int dppo_pack_critic(const dppo_dims* d, int precision, const float* 
     DPPO_CHECK(params && packed, "dppo_pack_critic: null pointer");
     DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
     return dppo_pack_mlp(D.SD, D.HC, 1, 0, precision, params, packed, (hipStream_t)stream);
+}
+
+// ---- kernel timer: (start, end) event pairs per launch of a timed kernel, summed on read ----
+volatile int g_dppo_kt_on = 0;
+namespace {
+const char* const kKtNames[KT_COUNT] = {
+    "sampler", "actor_rowtile_train", "actor_rowtile_logprob", "critic_rowtile_train",
+    "critic_rowtile_forward", "dw_kernel_actor", "dw_kernel_critic", "l2_back_kernel", "time_bwd_kernel",
+    "adamw_kernel", "pack_all_kernel", "gae_kernel", "rets_kernel", "moments_kernel", "scale_apply_kernel",
+    "zero_kernel", "crit_rows_kernel", "adv_stats_kernel"};
+struct KtRec { int id; hipEvent_t e0, e1; };
+std::mutex g_kt_mu;
+std::vector<KtRec> g_kt;     // event pool; [0, g_kt_used) hold this window's launches
+size_t g_kt_used = 0;
+}
+
+int dppo_kt_begin(int id, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_kt_mu);
+    if (!g_dppo_kt_on || id < 0 || id >= KT_COUNT) return -1;
+    if (g_kt_used == g_kt.size()) {
+        KtRec r{id, nullptr, nullptr};
+        if (hipEventCreate(&r.e0) != hipSuccess || hipEventCreate(&r.e1) != hipSuccess) {
+            (void)hipGetLastError();
+            return -1;
+        }
+        g_kt.push_back(r);
+    }
+    KtRec& r = g_kt[g_kt_used];
+    r.id = id;
+    if (hipEventRecord(r.e0, s) != hipSuccess) { (void)hipGetLastError(); return -1; }
+    return (int)g_kt_used++;
+}
+
+void dppo_kt_end(int slot, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_kt_mu);
+    if (slot >= 0 && (size_t)slot < g_kt_used && hipEventRecord(g_kt[slot].e1, s) != hipSuccess) (void)hipGetLastError();
+}
+
+extern "C" int dppo_kernel_timing(int enable) {
+    std::lock_guard<std::mutex> lk(g_kt_mu);
+    g_dppo_kt_on = enable ? 1 : 0;
+    g_kt_used = 0;
+    return DPPO_OK;
+}
+
+extern "C" const char* dppo_kernel_timing_name(int id) { return id >= 0 && id < KT_COUNT ? kKtNames[id] : nullptr; }
+
+extern "C" int dppo_kernel_timing_read(int n, double* total_ms, int64_t* launches) {
+    DPPO_CHECK(n >= 0 && (n == 0 || (total_ms && launches)), "dppo_kernel_timing_read: bad arguments");
+    std::lock_guard<std::mutex> lk(g_kt_mu);
+    for (int i = 0; i < n; ++i) { total_ms[i] = 0.0; launches[i] = 0; }
+    for (size_t k = 0; k < g_kt_used; ++k) {
+        const KtRec& r = g_kt[k];
+        DPPO_HIP(hipEventSynchronize(r.e1));
+        float ms = 0.f;
+        DPPO_HIP(hipEventElapsedTime(&ms, r.e0, r.e1));
+        if (r.id < n) { total_ms[r.id] += ms; launches[r.id] += 1; }
+    }
+    g_kt_used = 0;
+    return DPPO_OK;
+}
+
+namespace {
+std::mutex g_lds_mu;
+std::vector<std::pair<const void*, size_t>> g_lds;
+}
+int dppo_func_lds(const void* k, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g_lds_mu);
+    for (auto& e : g_lds)
+        if (e.first == k) {
+            if (bytes <= e.second) return DPPO_OK;
+            DPPO_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+            e.second = bytes;
+            return DPPO_OK;
+        }
+    DPPO_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    g_lds.emplace_back(k, bytes);
+    return DPPO_OK;
 }

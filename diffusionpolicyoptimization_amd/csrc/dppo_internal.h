@@ -43,3 +43,23 @@ inline float dppo_grad_scale_rows(int p, int64_t global_rows) {
 
 #define DPPO_CHECK(cond, ...) do { if (!(cond)) return dppo_set_error(DPPO_EINVAL, __VA_ARGS__); } while (0)
 #define DPPO_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return dppo_hip_fail(e_, #x); } while (0)
+
+// ---- kernel timer (ABI 10, dppo_kernel_timing*): HIP events around the launches of the kernels
+// below, on the launch's own stream, while enabled (one relaxed flag test per launch otherwise) ----
+enum DppoKt {
+    KT_SAMPLER, KT_ACTOR_TRAIN, KT_ACTOR_LOGPROB, KT_CRITIC_TRAIN, KT_CRITIC_FWD, KT_DW_ACTOR, KT_DW_CRITIC,
+    KT_L2_BACK, KT_TIME_BWD, KT_ADAMW, KT_PACK_ALL, KT_GAE, KT_RETS, KT_MOMENTS, KT_SCALE_APPLY, KT_ZERO,
+    KT_CRIT_ROWS, KT_ADV_STATS, KT_COUNT
+};
+extern volatile int g_dppo_kt_on;
+int dppo_kt_begin(int id, hipStream_t s);   // -1 when disabled
+void dppo_kt_end(int slot, hipStream_t s);
+struct DppoKtScope {   // brackets the launches of one scope: { DppoKtScope kt(KT_GAE, s); launch; }
+    int slot; hipStream_t s;
+    DppoKtScope(int id, hipStream_t st) : slot(g_dppo_kt_on ? dppo_kt_begin(id, st) : -1), s(st) {}
+    ~DppoKtScope() { if (slot >= 0) dppo_kt_end(slot, s); }
+};
+
+// the opt-in to `bytes` of dynamic LDS for kernel k: hipFuncSetAttribute only the first time k asks
+// for that much (a host API call per launch otherwise)
+int dppo_func_lds(const void* k, size_t bytes);

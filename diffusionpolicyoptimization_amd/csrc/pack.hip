@@ -338,6 +338,7 @@ static int launch_pack(PackArgs& a, int precision, hipStream_t s) {
     a.pack_blocks = dppo_cdiv(a.start[a.njobs], PACK_THREADS);
     const int blocks = a.tb.nfold + a.pack_blocks + a.tb.tables;
     if (blocks == 0) return DPPO_OK;
+    DppoKtScope kt(KT_PACK_ALL, s);
     if (precision == DPPO_BF16)
         hipLaunchKernelGGL((pack_all_kernel<32, 8, __bf16>), dim3(blocks), dim3(PACK_THREADS), 0, s, a);
     else if (precision == DPPO_F16)

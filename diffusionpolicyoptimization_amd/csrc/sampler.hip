@@ -466,7 +466,8 @@ static int launch_sample_q(const SampleArgs& a, hipStream_t s) {
     const size_t lds = sample_lds_bytes<P>(a, NO, SW, LK);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "sampler needs %zu B of LDS", lds);
     auto k = sample_kernel<P, NT, NO, KSI, INJ, QD, SW, RK, LK, RIO>;
-    DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    { const int rc_ = dppo_func_lds((const void*)k, (size_t)lds); if (rc_) return rc_; }
+    DppoKtScope kt(KT_SAMPLER, s);
     hipLaunchKernelGGL(k, dim3(dppo_cdiv(a.E, 16)), dim3(SW * 64), lds, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;

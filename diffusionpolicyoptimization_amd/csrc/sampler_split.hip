@@ -1887,8 +1887,9 @@ int launch_split_k(const SplitArgs& sa, hipStream_t s) {
     const SampleArgs& a = sa.a;
     const size_t lds = split_lds_bytes(a.XD, a.SD, a.TD, a.K, KSI, NO);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler needs %zu B of LDS", lds);
-    DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    { const int rc_ = dppo_func_lds((const void*)k, (size_t)lds); if (rc_) return rc_; }
     const int blocks = 8 * SPLIT_P * ((sa.G + 7) / 8);
+    DppoKtScope kt(KT_SAMPLER, s);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(SW * 64), lds, s, sa);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
@@ -1908,8 +1909,9 @@ int launch_split4_kw(const SplitArgs& sa, hipStream_t s) {
     const SampleArgs& a = sa.a;
     const size_t lds = split4_lds_bytes(a.XD, a.SD, a.K, KX, NO, SWV);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler needs %zu B of LDS", lds);
-    DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    { const int rc_ = dppo_func_lds((const void*)k, (size_t)lds); if (rc_) return rc_; }
     const int blocks = 8 * PM * ((sa.G + 7) / 8) * (sa.dual ? 2 : 1);
+    DppoKtScope kt(KT_SAMPLER, s);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(SWV * 64), lds, s, sa);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
@@ -1926,9 +1928,10 @@ int launch_pair_k(const SplitArgs& sa, hipStream_t s) {
     const int NS = sa.dual ? (a.K - a.KF > a.KF ? a.K - a.KF : a.KF) : a.K;
     const size_t lds = pair_lds_bytes(a.XD, a.SD, a.K, NS, KX, NO);
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "pair sampler needs %zu B of LDS", lds);
-    DPPO_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    { const int rc_ = dppo_func_lds((const void*)k, (size_t)lds); if (rc_) return rc_; }
     const int G2 = (sa.G + 1) / 2;
     const int blocks = 8 * 2 * ((G2 + 7) / 8) * (sa.dual ? 2 : 1);
+    DppoKtScope kt(KT_SAMPLER, s);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, s, sa);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;

@@ -160,8 +160,10 @@ extern "C" int dppo_gae(const double* reward, const float* values, const float* 
     DPPO_CHECK(S >= 0 && E >= 0, "dppo_gae: negative size");
     if (S == 0 || E == 0) return DPPO_OK;
     DPPO_CHECK(reward && values && last_values && terminated && advantages && returns, "dppo_gae: null pointer");
-    hipLaunchKernelGGL(gae_kernel, dim3(dppo_cdiv(E, SCAN_WAVES)), dim3(64 * SCAN_WAVES), 0, (hipStream_t)stream,
-                       reward, values, last_values, terminated, S, E, gamma, lam, reward_scale_const, advantages, returns);
+    { DppoKtScope kt(KT_GAE, (hipStream_t)stream);
+        hipLaunchKernelGGL(gae_kernel, dim3(dppo_cdiv(E, SCAN_WAVES)), dim3(64 * SCAN_WAVES), 0, (hipStream_t)stream,
+                           reward, values, last_values, terminated, S, E, gamma, lam, reward_scale_const, advantages, returns);
+    }
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -209,10 +211,14 @@ extern "C" int dppo_reward_scale_moments(const double* reward, const uint8_t* fi
     hipStream_t s = (hipStream_t)stream;
     double* rets_ws = workspace;
     double* env_mom = rets_ws + (size_t)S * E;
-    hipLaunchKernelGGL(rets_kernel, dim3(dppo_cdiv(E, SCAN_WAVES)), dim3(64 * SCAN_WAVES), 0, s,
-                       reward, first, ret_state, rets_ws, env_mom, S, E, gamma);
+    { DppoKtScope kt(KT_RETS, (hipStream_t)stream);
+        hipLaunchKernelGGL(rets_kernel, dim3(dppo_cdiv(E, SCAN_WAVES)), dim3(64 * SCAN_WAVES), 0, s,
+                           reward, first, ret_state, rets_ws, env_mom, S, E, gamma);
+    }
     DPPO_HIP(hipGetLastError());
-    hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(64), 0, s, env_mom, E, moments, (double*)nullptr);
+    { DppoKtScope kt(KT_MOMENTS, (hipStream_t)stream);
+        hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(64), 0, s, env_mom, E, moments, (double*)nullptr);
+    }
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -222,8 +228,10 @@ extern "C" int dppo_reward_scale_apply(double* reward, const double* rms_state, 
     DPPO_CHECK(reward && rms_state, "dppo_reward_scale_apply: null pointer");
     const int64_t n = (int64_t)S * E;
     if (n == 0) return DPPO_OK;
-    hipLaunchKernelGGL(scale_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       reward, rms_state, n, cliprew, epsilon);
+    { DppoKtScope kt(KT_SCALE_APPLY, (hipStream_t)stream);
+        hipLaunchKernelGGL(scale_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           reward, rms_state, n, cliprew, epsilon);
+    }
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -241,13 +249,19 @@ extern "C" int dppo_reward_scale(double* reward, const uint8_t* first, double* r
     double* rets = workspace;
     double* env_mom = rets + (size_t)S * E;
     double* moments = env_mom + (size_t)3 * E;
-    hipLaunchKernelGGL(rets_kernel, dim3(dppo_cdiv(E, SCAN_WAVES)), dim3(64 * SCAN_WAVES), 0, s,
-                       reward, first, ret_state, rets, env_mom, S, E, gamma);
+    { DppoKtScope kt(KT_RETS, (hipStream_t)stream);
+        hipLaunchKernelGGL(rets_kernel, dim3(dppo_cdiv(E, SCAN_WAVES)), dim3(64 * SCAN_WAVES), 0, s,
+                           reward, first, ret_state, rets, env_mom, S, E, gamma);
+    }
     DPPO_HIP(hipGetLastError());
-    hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(64), 0, s, env_mom, E, moments, rms_state);
+    { DppoKtScope kt(KT_MOMENTS, (hipStream_t)stream);
+        hipLaunchKernelGGL(moments_kernel, dim3(1), dim3(64), 0, s, env_mom, E, moments, rms_state);
+    }
     DPPO_HIP(hipGetLastError());
-    hipLaunchKernelGGL(scale_apply_kernel, dim3(dppo_cdiv(S * E, 256)), dim3(256), 0, s, reward, rms_state,
-                       (int64_t)S * E, cliprew, epsilon);
+    { DppoKtScope kt(KT_SCALE_APPLY, (hipStream_t)stream);
+        hipLaunchKernelGGL(scale_apply_kernel, dim3(dppo_cdiv(S * E, 256)), dim3(256), 0, s, reward, rms_state,
+                           (int64_t)S * E, cliprew, epsilon);
+    }
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }

@@ -718,6 +718,7 @@ static int launch_adamw(float* params, const float* grads, float* m, float* v, i
     const float alpha = (float)((double)lr * sqrt(bc2) / bc1);
     const int64_t blocks64 = (n + 255) / 256;
     const unsigned blocks = (unsigned)(blocks64 < 1 ? 1 : (blocks64 < 4096 ? blocks64 : 4096));
+    DppoKtScope kt(KT_ADAMW, s);
     hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, params, grads, m, v, n, lr,
                        weight_decay, beta1, beta2, eps, alpha, (float)bc1, (float)bc2, mode, met, met_out, nmet, tag, vt);
     DPPO_HIP(hipGetLastError());
@@ -892,6 +893,7 @@ extern "C" int dppo_ppo_adv_stats_all(const float* advantages, int64_t total, in
     a.nbatch = n_batch; a.KF = K_ft; a.rows_full = rows_full; a.total = total;
     const int64_t bx = dppo_cdiv((int)(rows_full < total ? rows_full : total), 256);
     const int blocks = bx < 64 ? (int)bx : 64;
+    DppoKtScope kt(KT_ADV_STATS, s);
     hipLaunchKernelGGL(adv_stats_all_kernel, dim3(blocks, nm), dim3(256), 0, s, advantages, a, adv_stats);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
@@ -954,6 +956,7 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
     // (time_bwd forked onto a side stream beside l2_back measured slower: 0.428 vs 0.406 ms per
     // minibatch, same box, tools/r03_ab2.sh)
     if (l2_back) {
+        DppoKtScope kt(KT_L2_BACK, s);
         hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
         DPPO_HIP(hipGetLastError());
     }
@@ -969,6 +972,7 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
             attr = true;
         }
     }
+    DppoKtScope kt(KT_TIME_BWD, s);
     hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD, D.TD, D.H,
                        nb, TS, stage_g);
     DPPO_HIP(hipGetLastError());
@@ -982,6 +986,7 @@ static int launch_critic_l2_back(const Dims& D, int precision, const float* cpl2
     const MlpLayout L = make_mlp_layout(D.SD, D.HC, 1, 0, precision);
     L2Back l2b = {cpl2, gc + FC.out_b, (const uint8_t*)packed_critic + L.off[SEG_W_OUT], gc + FC.l2_w, gc + FC.l2_b, D.HC, 1,
                   precision, zcnt, zlist, zn};
+    DppoKtScope kt(KT_L2_BACK, s);
     hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.HC, L2B_ROWS)), dim3(256), 0, s, l2b);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
@@ -1040,6 +1045,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     // and a 256-block grid waited ~25 us for slots (DPPO_ZERO_BLOCKS: measurement knob)
     static const int zero_blocks = [] { const char* e = getenv("DPPO_ZERO_BLOCKS"); return e ? atoi(e) : 16; }();
     if (parts != 5) {      // part 5 continues the actor half whose part 4 zeroed its outputs
+        DppoKtScope kt(KT_ZERO, s);
         hipLaunchKernelGGL(zero_kernel, dim3(zero_blocks > 0 ? zero_blocks : 16), dim3(256), 0, s, z);
         DPPO_HIP(hipGetLastError());
     }
@@ -1123,6 +1129,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (nch < 1) nch = 1;
         w.mchunk = (int)(dppo_cdiv((int)span, nch * 64) * 64);
         w.nchunks = dppo_cdiv((int)span, w.mchunk);
+        DppoKtScope kt(actor ? KT_DW_ACTOR : KT_DW_CRITIC, st);
         return precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, tk, st)
              : precision == DPPO_F16  ? launch_dw<PolicyF16>(w, tk, st) : launch_dw<PolicyF32>(w, tk, st);
     };
@@ -1136,6 +1143,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         crit_cnt = crit_count_scratch(nsamp, st);
         DPPO_CHECK(crit_cnt, "dppo_ppo_minibatch: sample-count scratch allocation failed");
         const int blocks = dppo_cdiv(rows, 256) < 512 ? dppo_cdiv(rows, 256) : 512;
+        DppoKtScope kt(KT_CRIT_ROWS, st);
         hipLaunchKernelGGL(crit_rows_kernel, dim3(blocks), dim3(256), 0, st, row_index, start, rows, fk, D.KF, crit_cnt,
                            ws.crow_n, ws.crow_cnt);
         DPPO_HIP(hipGetLastError());

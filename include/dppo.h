@@ -143,6 +143,17 @@ DPPO_API int dppo_sampler_max_in_flight(const dppo_dims* d, int precision, int n
  * sampler is a TF call, diffusion_vpg.py:250-339.) */
 DPPO_API int dppo_sampler_release_stream(void* stream);
 
+/* Kernel timer (ABI 10, measurement): while enabled, the library brackets the launches of its
+ * timed kernels (the sampler, the row tiles, dW, l2_back, time_bwd, AdamW, pack, GAE, the reward
+ * scaler's three kernels, ...; dppo_kernel_timing_name(id) names id, NULL past the last) with HIP
+ * events on the launch's own stream. dppo_kernel_timing(enable) switches it and clears the window;
+ * dppo_kernel_timing_read(n, total_ms[n], launches[n]) waits for the window's launches, returns the
+ * summed event time and launch count per id, and clears the window. Off by default: a disabled timer
+ * is one flag test per launch. */
+DPPO_API int dppo_kernel_timing(int enable);
+DPPO_API const char* dppo_kernel_timing_name(int id);
+DPPO_API int dppo_kernel_timing_read(int n, double* total_ms, int64_t* launches);
+
 /* The sampler plan for n_envs envs (measurement aid, ABI 6): plan[0] = kernel (0 weight streaming,
  * 1 split with 8 members per 16-env tile, 2 folded split with P members per tile, 3 the pair kernel:
  * P = 2 members running two 16-env tiles half a denoising step apart), plan[1] = members per member

@@ -62,17 +62,38 @@ def main():
         phases = {f"s{i}": round(buf[i] / wgs / (d.denoising_steps if i else 1)) for i in range(7)}
     if hasattr(lib, "dppo_debug_split_cycles") and _split(m, args.envs):   # split kernel phases
         import ctypes
+        from diffusionpolicyoptimization_amd import ops
+        plan = ops.sampler_plan(d, m.precision, args.envs)
         buf = (ctypes.c_ulonglong * (16 + 64 * 8))()
         lib.dppo_debug_split_cycles(buf, 1)
-        m(cond)
-        torch.cuda.synchronize()
+        n_launch = 20
+        e0.record()
+        for _ in range(n_launch):
+            m(cond)
+        e1.record()
+        e1.synchronize()
+        ms_t = e0.elapsed_time(e1) / n_launch
         lib.dppo_debug_split_cycles(buf, 1)
-        wgs = 8 * ((args.envs + 15) // 16)
-        names = ["prologue", "switch", "in", "l1", "l2_out", "xchg", "epilogue"]
-        phases = {n: round(buf[i] / wgs / (1 if i < 2 else d.denoising_steps)) for i, n in enumerate(names)}
-        for i, n in zip(range(11, 16), ["in_mm", "l1_mm", "l2_mm", "out_mm", "publish"]):
-            phases[n] = round(buf[i] / wgs / d.denoising_steps)
-        phases["wg0_steps"] = [[int(buf[16 + 8 * i + k]) for k in range(1, 7)] for i in range(d.denoising_steps)]
+        G = (args.envs + 15) // 16
+        active = G * plan["members"] * plan["sets"]          # workgroups that run steps
+        steps = d.denoising_steps // plan["sets"] if plan["kernel"] == 2 else d.denoising_steps   # steps per workgroup
+        per = lambda k, n: buf[k] / (n_launch * active * n)
+        if plan["kernel"] == 2:   # sample_split4_kernel (folded, P = 2 / 4): XPHASE ids in step order
+            names = [(7, "prologue_before_obs_wait", 1), (8, "obs_wait", 1), (0, "prologue_after_obs", 1),
+                     (1, "step_head", steps), (11, "in_dense_mfma_u1_store_residual", steps),
+                     (2, "in_dense_barrier", steps), (14, "l1_fold_partial_store", steps),
+                     (4, "partial_barrier", steps), (15, "publish", steps), (5, "exchange_wait", steps),
+                     (6, "epilogue_step_barrier", steps), (9, "loop_end", 1), (10, "done_signal", 1)]
+        else:
+            names = [(i, f"phase{i}", steps) for i in range(16)]
+        phases = {"kernel_plan": plan, "active_workgroups": active, "steps_per_workgroup": steps,
+                  "ms_per_launch_timing_build": ms_t, "unit": "shader cycles (s_memtime) of wave 0, per step "
+                  "(per launch for the prologue / end phases), averaged over the active workgroups"}
+        phases.update({n: round(per(k, cnt), 1) for k, n, cnt in names})
+        step_sum = sum(per(k, steps) for k, _, cnt in names if cnt == steps)
+        phases["step_total"] = round(step_sum, 1)
+        # the shader clock the kernel ran at: the step loop's cycles over its share of the launch time
+        phases["wg0_steps_first8phases"] = [[int(buf[16 + 8 * i + k]) for k in range(8)] for i in range(d.denoising_steps)]
         if hasattr(lib, "dppo_debug_split_xmode"):
             xm = (ctypes.c_uint * 2)()
             lib.dppo_debug_split_xmode(xm, 1)

@@ -60,7 +60,8 @@ def main():
         lib.dppo_debug_phase_cycles(buf, 1)
         tiles = (args.rows + 63) // 64
         phases = {f"p{i}": round(buf[i] / tiles) for i in range(11)}
-    print(json.dumps({"rowtile": os.environ.get("DPPO_ROWTILE", "default"), "phase_cycles_per_tile": phases,
+    print(json.dumps({"rowtile": "default", "lib": os.path.basename(_lib.LIB_PATH),
+                      "phase_cycles_per_tile": phases,
                       "minibatch_ms": mb,
                       "logprob_pass_ms": lp, "value_pass_ms": cv,
                       "grad_finite": bool(torch.isfinite(m.grads).all())}), flush=True)

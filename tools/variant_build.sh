@@ -8,8 +8,9 @@ out=../lib/variants/libdppo_hip_$tag.so
 mkdir -p ../lib/variants build/$tag
 objs=""
 for f in api pack sampler sampler_split scan rowtile update; do
+    vf="-mllvm -amdgpu-mfma-vgpr-form"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -mcode-object-version=5 -fvisibility=hidden \
-        -I../../include -mllvm -amdgpu-mfma-vgpr-form $extra -c $f.hip -o build/$tag/$f.o &
+        -I../../include $vf $extra -c $f.hip -o build/$tag/$f.o &
     objs="$objs build/$tag/$f.o"
 done
 wait
