@@ -1,5 +1,5 @@
 #!/bin/bash
-# r03: update knobs on the emulated W = 8 rank (6,250-row minibatches), same box
+# update knobs on the emulated W = 8 rank (6,250-row minibatches), same box: tools/emu_knobs.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 run() {
