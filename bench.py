@@ -153,6 +153,8 @@ def kernel_stats_csv(path=KERNEL_STATS_CSV):
                 base = "critic_rowtile_train" if "true" in k else "critic_rowtile_forward"
             elif base == "adv_stats_all_kernel":
                 base = "adv_stats_kernel"
+            elif base == "adamw_fused_kernel":
+                base = "adamw_kernel"
             tot, calls = float(r["TotalDurationNs"]) / 1e6, int(r["Calls"])
             t0, c0 = out.get(base, (0.0, 0))
             out[base] = (t0 + tot, c0 + calls)
@@ -191,7 +193,9 @@ def kernel_figures(d, S, E, batch, n_mb, precision, times, source, iters=1):
         out["adamw_kernel"] = {"bytes_per_minibatch": per_mb, "launches_per_minibatch": calls / n_mb,
                                "us_per_minibatch": ns / 1e3, "achieved_GBs": per_mb / ns, "frac": per_mb / ns / HBM_PEAK_GBS,
                                "note": "28 B per parameter, actor and critic ranges summed (two launches under "
-                                       "the split update, on two streams); durations include sharing the CUs"}
+                                       "the split update, on two streams; since ABI 11 each also stores its "
+                                       "network's image slots and zeroes the next minibatch's accumulators, "
+                                       "replacing the pack and zero launches); durations include sharing the CUs"}
     peak = PEAK["bf16" if precision in ("bf16", "fp16") else "fp32"]
     if "actor_rowtile_train" in times:
         tot, calls = times["actor_rowtile_train"]

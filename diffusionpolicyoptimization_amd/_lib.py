@@ -19,6 +19,9 @@ DPPO_STEP_DEFER_SAMPLER_TABLES = 0x100   # OR'd into dppo_optimizer_step's mode 
 DPPO_STEP_L2_FROM_PL2 = 0x200            # (ABI 8) the actor's l2 gradient arrives factored
 DPPO_PPO_L2_DEFERRED = 1                 # dppo_ppo_hparams.flags (ABI 8)
 DPPO_PPO_LEARN_ETA = 2                   # (ABI 9) d loss / d eta into metrics[8]
+DPPO_STEP_FUSED_PACK = 0x400             # (ABI 11) AdamW + the image in one launch
+DPPO_STEP_CLEAR_GRADS = 0x800            # (ABI 11) the step zeroes the range's gradients after reading
+DPPO_PPO_PRECLEARED = 4                  # (ABI 11) the part's accumulators are already zero
 SCHED_COLS = 8
 PRECISION = {"fp32": DPPO_F32, "f32": DPPO_F32, "bf16": DPPO_BF16, "fp16": DPPO_F16, "f16": DPPO_F16}
 
@@ -94,6 +97,9 @@ _SIGNATURES = {
     "dppo_pack_all": (_I, [_DIMS, _I, _P, _P, _P, _P, _P]),
     "dppo_optimizer_step": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P, _P,
                                  _P, _I, _U64, _P]),
+    "dppo_optimizer_step_ex": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P,
+                                    _P, _P, _I, _U64, _P, _P, _I, _P]),
+    "dppo_ppo_clear_ranges": (_I, [_DIMS, _I, _I, _P, _P, _I, _P, _P, ctypes.POINTER(ctypes.c_int)]),
     "dppo_value_moments": (_I, [_P, _P, _I64, _P, _P]),
     "dppo_refresh_sampler_tables": (_I, [_P, _P]),
     "dppo_materialize_l2": (_I, [_DIMS, _I, _P, _P, _P, _I, _P]),
@@ -104,7 +110,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class DppoError(RuntimeError):

@@ -468,6 +468,16 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # Not with per-tensor gradient clipping (it needs the tensor) or a test hook reading grads.
             l2_def = (self.max_grad_norm is None and self.minibatch_hook is None
                       and os.environ.get("DPPO_L2_DEFER", "1") != "0")
+            # ABI 11: the critic's optimizer step is one launch (AdamW storing the image slots;
+            # DPPO_STEP_FUSED_PACK) that also zeroes what the critic's next half would zero first
+            # (its gradients, metric slot and workspace accumulators: DPPO_STEP_CLEAR_GRADS +
+            # ops.ClearRanges), which then runs with DPPO_PPO_PRECLEARED: two launches fewer per
+            # minibatch on the side stream. The actor's half the same way ("all") measured slower:
+            # with the virtual l2 gradient its last workgroup's W_out work is serial.
+            # Not with a test hook reading the gradients (they are zero after the step).
+            fuse_mode = os.environ.get("DPPO_FUSED_STEP", "critic")   # "0" | "critic" | "all" (A/B knob)
+            fuse = split and self.minibatch_hook is None and fuse_mode != "0"
+            fuse_actor = fuse and fuse_mode == "all"
             opt = self.actor_optimizer
             ng_all = m.grads.numel()
             # the bound calls are reused across updates while every buffer they captured is the same
@@ -476,7 +486,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             bkey = (ptrs(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, m.grads, m.train_params,
                          m.packed_ft, m.packed_critic, m.sched, m.workspace(rows_local_full), opt.m, opt.v),
                     self.perm_seed, rows_local_full, self.reward_horizon, l2_def, split, defer,
-                    self.max_grad_norm is None, m.dims.ft_denoising_steps, m.precision)
+                    self.max_grad_norm is None, m.dims.ft_denoising_steps, m.precision, fuse, fuse_actor)
             if getattr(self, "_bound_key", None) != bkey:
                 bound = {"run_mb": m.bind_minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat,
                                                     self.perm_seed, rows_local_full, reward_horizon=self.reward_horizon,
@@ -484,9 +494,16 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 if split:
                     bound["actor"] = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
                                                     packs={"actor": (m.actor_ft_params, m.packed_ft)},
-                                                    defer_sampler_tables=defer, l2_from_pl2=l2_def)
+                                                    defer_sampler_tables=defer, l2_from_pl2=l2_def,
+                                                    fused_pack=fuse_actor, clear_grads=fuse_actor)
                     bound["critic"] = opt.bind_range(m.grads, na, ng_all, m.dims, m.precision,
-                                                     packs={"critic": (m.critic_params, m.packed_critic)})
+                                                     packs={"critic": (m.critic_params, m.packed_critic)},
+                                                     fused_pack=fuse, clear_grads=fuse)
+                    if fuse:   # what each half of a full minibatch zeroes, per metrics buffer
+                        ws_full = m.workspace(rows_local_full)
+                        bound["clear"] = [(ops.ClearRanges(m.dims, m.precision, rows_local_full, ws_full, t, 1),
+                                           ops.ClearRanges(m.dims, m.precision, rows_local_full, ws_full, t, 2))
+                                          for t in self._met_dev] if fuse else None
                 elif self.max_grad_norm is None:
                     bound["all"] = opt.bind_range(m.grads, 0, ng_all, m.dims, m.precision,
                                                   packs={"actor": (m.actor_ft_params, m.packed_ft),
@@ -496,6 +513,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             run_mb = self._bound["run_mb"]
             step_actor, step_critic = self._bound.get("actor"), self._bound.get("critic")
             step_all = self._bound.get("all")
+            clear_next = self._bound.get("clear")
+            cleared = False   # the previous optimizer step zeroed this minibatch's accumulators
             # raw device addresses and stream handles, computed once: per minibatch the host passes
             # ints instead of slicing tensors and entering stream contexts (~tens of us per minibatch,
             # which an 8-GPU rank's 255 small minibatches per iteration wait on)
@@ -519,19 +538,21 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         ev0 = torch.cuda.Event(enable_timing=True)
                         ev0.record(stream)
                     mb_args = (update_epoch + 1000 * self.itr, start, rows)
+                    pre = cleared and rows == rows_local_full
                     mb_kw = dict(global_rows=global_rows, adv_stats=stats)
                     met = m.metrics
                     tagged = self.itr >= self.n_critic_warmup_itr
                     if split:
                         met = self._met_dev[k % 2]
                         met_p = met_ptrs[k % 2]
-                        run_mb(*mb_args, **mb_kw, part=2, metrics=met_p, stream=st_side)
+                        run_mb(*mb_args, **mb_kw, part=2, metrics=met_p, stream=st_side, precleared=pre)
                         if not tagged and not dp:
                             ev_c = torch.cuda.Event()
                             ev_c.record(side)
                         if dp:
                             ng = m.grads.numel()
-                            run_mb(*mb_args, **mb_kw, part=4, metrics=met)   # actor row tiles
+                            run_mb(*mb_args, **mb_kw, part=4, metrics=met,   # actor row tiles
+                                   precleared=pre and fuse_actor)
                             self._ev_rows.record(stream)
                             with torch.cuda.stream(side):          # bucket 1: critic gradients + metrics
                                 side.wait_event(self._ev_rows)
@@ -545,7 +566,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             self._allreduce(m.grads_ext[:na])      # bucket 2: actor gradients
                             stream.wait_event(self._ev_met)
                         else:
-                            run_mb(*mb_args, **mb_kw, part=1, metrics=met_p, stream=st_main)
+                            run_mb(*mb_args, **mb_kw, part=1, metrics=met_p, stream=st_main,
+                                   precleared=pre and fuse_actor)
                             if not tagged:
                                 stream.wait_event(ev_c)
                     else:
@@ -572,6 +594,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         same_epoch = pending[3] == update_epoch
                         pending = None
                         if stop and same_epoch:                                    # :366-368
+                            cleared = False   # this minibatch's sums stay; no step clears them
                             break
                     # the optimiser step (agent :346): AdamW, the metric sums to the host and the weight
                     # images re-derived, one dppo_optimizer_step per stream (two launches each). The actor
@@ -589,10 +612,13 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         tag = self._mb_tag
                         if split:
                             ctag = tag
+                            ca, cc = clear_next[(k + 1) % 2] if fuse else (None, None)
+                            ca = ca if fuse_actor else None
                             step_actor(lr, metrics=met_p, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
-                                       stream=st_main)
+                                       stream=st_main, clear=ca)
                             step_critic(lr, metrics=met_p + 8, metrics_out=self._cmet_map[slot].address,   # met[1]
-                                        n_metrics=1, metrics_tag=ctag, stream=st_side)
+                                        n_metrics=1, metrics_tag=ctag, stream=st_side, clear=cc)
+                            cleared = fuse
                         elif self.max_grad_norm is not None:
                             self._clip_by_norm_per_tensor()
                             opt.apply_range(m.grads, 0, ng, lr, m.dims, m.precision,
@@ -606,6 +632,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             m.eta_optimizer_step(met, self.eta_lr_scheduler(m.eta_step_count), self.eta_weight_decay)
                     else:
                         torch.from_numpy(met_out.array[:5]).copy_(met[:5])
+                        cleared = False
                     if self.update_events is not None:
                         ev1 = torch.cuda.Event(enable_timing=True)
                         ev1.record(stream)

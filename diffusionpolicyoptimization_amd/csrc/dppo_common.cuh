@@ -349,6 +349,46 @@ __device__ inline float mish_gradf(float x) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// t_emb(t) = Dense(2TD->TD)(mish(Dense(TD->2TD)(SinusoidalPosEmb(t)))) (mlp_diffusion.py:40-45,
+// modules.py:4-15), element by element. p: the actor's flat parameters (time_w1 [TD][2TD], time_b1,
+// time_w2 [2TD][TD], time_b2 at the given offsets). The dot products are explicit fmaf chains: the
+// pack's per-row blocks (pack.hip) and the fused optimizer step's last workgroup (update.hip) then
+// agree bit for bit whatever the compiler contracts in each kernel (left to it, the same source
+// compiled to different contractions in the two: last-ulp differences).
+// ------------------------------------------------------------------------------------------------
+__device__ inline float temb_sinusoid(int j, int t, int TD) {
+    const int half = TD / 2;
+    const float lnf = logf(10000.f) / (float)(half - 1);
+    const float f = expf(-(float)(j % half) * lnf) * (float)t;
+    return j < half ? sinf(f) : cosf(f);
+}
+__device__ inline float temb_hidden(const float* p, size_t w1, size_t b1, const float* te, int TD, int h) {
+    float acc = p[b1 + h];
+#pragma unroll 16
+    for (int k = 0; k < TD; ++k) acc = __builtin_fmaf(te[k], p[w1 + (size_t)k * 2 * TD + h], acc);
+    return mishf(acc);
+}
+__device__ inline float temb_output(const float* p, size_t w2, size_t b2, const float* a1, int TD, int j) {
+    float acc = p[b2 + j];
+#pragma unroll 16
+    for (int k = 0; k < 2 * TD; ++k) acc = __builtin_fmaf(a1[k], p[w2 + (size_t)k * TD + j], acc);
+    return acc;
+}
+// The R rows of the TEMB table (row r = t_emb(r TS)) by one workgroup; sm: 3 R TD floats of LDS
+__device__ inline void temb_rows_block(const float* p, int64_t w1, int64_t b1, int64_t w2,
+                                                                  int64_t b2, int TD, int TS, int R, float* out,
+                                                                  float* sm) {
+    const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
+    float* te = sm;              // [R][TD]
+    float* a1 = sm + R * TD;     // [R][2TD]
+    for (int i = tid; i < R * TD; i += nt) te[i] = temb_sinusoid(i % TD, (i / TD) * TS, TD);
+    __syncthreads();
+    for (int i = tid; i < R * 2 * TD; i += nt) a1[i] = temb_hidden(p, w1, b1, te + (i / (2 * TD)) * TD, TD, i % (2 * TD));
+    __syncthreads();
+    for (int i = tid; i < R * TD; i += nt) out[i] = temb_output(p, w2, b2, a1 + (i / TD) * 2 * TD, TD, i % TD);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Philox4x32-10 + Box-Muller (restated bit-for-bit by oracle/philox.py)
 // ------------------------------------------------------------------------------------------------
 struct u32x4s { uint32_t x, y, z, w; };

@@ -22,6 +22,22 @@ int dppo_check_dims(const dppo_dims* d, Dims* out);
 int dppo_pack_models(const Dims& D, int precision, const float* actor_params, void* packed_actor,
                      const float* critic_params, void* packed_critic, hipStream_t s, bool defer_sampler_tables = false);
 
+// The pack of one network as per-element stores (DPPO_STEP_FUSED_PACK, update.hip): each job maps
+// the elements [lo, hi) of the network's flat parameters to one image segment
+struct FuseJob {
+    int kind;          // 0 = packed [IK][IN] image from a row-major [IK][IN] tensor, 1 = packed [IK][IN]
+                       // image of the transpose of a row-major [IN][IK] tensor, 2 = fp32 copy
+    int IK, IN, KS;    // image rows / columns / k-steps
+    int64_t lo, hi;
+    uint8_t* dst;
+};
+constexpr int FUSE_MAXJ = 12;
+// the jobs of the update-mode pack (PACK_UPDATE: no split-sampler tables) of one network whose flat
+// parameters start at element 0 of the step's range; returns the job count (<= FUSE_MAXJ) or -1
+int dppo_fuse_jobs(int in_dim, int hidden, int out_dim, int time_dim, int precision, void* packed, int temb_steps,
+                   FuseJob* jobs);
+int dppo_mark_tables_stale(const Dims& D, int precision, const float* actor_params, const void* packed_actor);
+
 
 // precision enum values the library implements; the two 2-byte operand policies share layouts
 inline bool dppo_prec_ok(int p) { return p == DPPO_F32 || p == DPPO_BF16 || p == DPPO_F16; }

@@ -80,24 +80,12 @@ __device__ void time_table_block(const TembArgs& b, int blk) {
         return;
     }
     const int row = blk % R, t = row * b.stride;   // row r holds t_emb(r * stride)
-    const int half = TD / 2;
-    const float lnf = logf(10000.f) / (float)(half - 1);
-    if (tid < TD) {
-        const float f = expf(-(float)(tid % half) * lnf) * (float)t;
-        te[tid] = tid < half ? sinf(f) : cosf(f);
-    }
+    if (tid < TD) te[tid] = temb_sinusoid(tid, t, TD);
     __syncthreads();
-    if (tid < 2 * TD) {
-        float acc = params[F.time_b1 + tid];
-#pragma unroll 16
-        for (int k = 0; k < TD; ++k) acc += te[k] * params[F.time_w1 + k * 2 * TD + tid];
-        ta1[tid] = mishf(acc);
-    }
+    if (tid < 2 * TD) ta1[tid] = temb_hidden(params, F.time_w1, F.time_b1, te, TD, tid);
     __syncthreads();
     if (tid < TD) {
-        float acc = params[F.time_b2 + tid];
-#pragma unroll 16
-        for (int k = 0; k < 2 * TD; ++k) acc += ta1[k] * params[F.time_w2 + k * TD + tid];
+        const float acc = temb_output(params, F.time_w2, F.time_b2, ta1, TD, tid);
         if (blk < R) b.temb[(size_t)row * TD + tid] = acc;
         tr[tid] = (float)(ET)acc;
     }
@@ -332,6 +320,36 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
     return DPPO_OK;
 }
 
+// add_mlp_jobs' main jobs (PACK_UPDATE) as element ranges of the flat parameters, same segments and
+// geometry; the TEMB table is derived separately (the fused step's last workgroup)
+int dppo_fuse_jobs(int in_dim, int hidden, int out_dim, int time_dim, int precision, void* packed, int temb_steps,
+                   FuseJob* jobs) {
+    const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision, temb_steps);
+    const FlatOffsets F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
+    const int KG = dppo_prec_2b(precision) ? 32 : 16;
+    int n = 0;
+    auto job = [&](int kind, size_t src, size_t count, int IK, int IN, int seg) {
+        if (n >= FUSE_MAXJ) { n = FUSE_MAXJ + 1; return; }
+        FuseJob& J = jobs[n++];
+        J.kind = kind; J.IK = IK; J.IN = IN; J.KS = kind == 2 ? 0 : packed_ksteps(IK, KG);
+        J.lo = (int64_t)src; J.hi = (int64_t)(src + count); J.dst = P_out(packed) + L.off[seg];
+    };
+    const size_t hh = (size_t)hidden * hidden, ho = (size_t)hidden * out_dim;
+    if (time_dim > 0) job(2, F.time_w1, F.in_w - F.time_w1, 0, 0, SEG_TIME);
+    job(0, F.in_w, (size_t)in_dim * hidden, in_dim, hidden, SEG_W_IN);
+    job(2, F.in_b, hidden, 0, 0, SEG_B_IN);
+    job(0, F.l1_w, hh, hidden, hidden, SEG_W_L1);
+    job(1, F.l1_w, hh, hidden, hidden, SEG_T_L1);
+    job(2, F.l1_b, hidden, 0, 0, SEG_B_L1);
+    job(0, F.l2_w, hh, hidden, hidden, SEG_W_L2);
+    job(1, F.l2_w, hh, hidden, hidden, SEG_T_L2);
+    job(2, F.l2_b, hidden, 0, 0, SEG_B_L2);
+    job(0, F.out_w, ho, hidden, out_dim, SEG_W_OUT);
+    job(1, F.out_w, ho, out_dim, hidden, SEG_T_OUT);
+    job(2, F.out_b, out_dim, 0, 0, SEG_B_OUT);
+    return n <= FUSE_MAXJ ? n : -1;
+}
+
 static int launch_pack(PackArgs& a, int precision, hipStream_t s) {
     a.start[0] = 0;
     for (int i = 0; i < a.njobs; ++i) a.start[i + 1] = a.start[i] + a.j[i].threads;
@@ -377,6 +395,11 @@ int mark_stale(const Dims& D, int precision, const float* params, const void* pa
     return DPPO_OK;
 }
 }  // namespace
+
+// the fused step leaves the actor image's split-sampler tables stale like a PACK_UPDATE pack
+int dppo_mark_tables_stale(const Dims& D, int precision, const float* actor_params, const void* packed_actor) {
+    return mark_stale(D, precision, actor_params, packed_actor);
+}
 
 int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* params,
                   void* packed, hipStream_t s, int temb_steps, int time_stride) {

@@ -414,13 +414,23 @@ __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __res
         const float f = expf(-(float)(j % half) * lnf) * (float)(q * TS);   // bucket q = row q: t = q * TS
         e[i] = j < half ? sinf(f) : cosf(f);
     }
-    for (int n = tid; n < H; n += TB_THREADS) {       // in_b' = sum_q G[q]
-        float s = 0.f;
+    if (!gs) {
+        for (int n = tid; n < H; n += TB_THREADS) {   // in_b' = sum_q G[q]
+            float s = 0.f;
 #pragma unroll 8
-        for (int q = 0; q < KF; ++q) s += gseg[q * H + n];
-        grad[F.in_b + n] = s;
+            for (int q = 0; q < KF; ++q) s += gseg[q * H + n];
+            grad[F.in_b + n] = s;
+        }
     }
     __syncthreads();
+    if (gs) {   // from the staged copy: no second global round trip
+        for (int n = tid; n < H; n += TB_THREADS) {
+            float s = 0.f;
+#pragma unroll 8
+            for (int q = 0; q < KF; ++q) s += gs[q * H + n];
+            grad[F.in_b + n] = s;
+        }
+    }
     // dtemb[q][j] = G[q] . W_in[XD + j]: one wave per (q, j), lanes over the hidden units, G from
     // LDS when it was staged (gs != nullptr), W_in rows from LDS
     for (int i = wave; i < KF * TD; i += TB_THREADS / 64) {
@@ -663,45 +673,237 @@ __device__ inline float l2_virtual_grad(const float* __restrict__ g, const L2Vir
     return sum;
 }
 
+struct AdamHP { float lr, wd, b1, b2, eps, alpha, bc1, bc2; int mode; };
+__device__ inline void adamw_elem(float& pi, float& mi, float& vi, float gi, const AdamHP& h) {
+    if (h.mode == DPPO_ADAMW_KERAS) {
+        // Keras 3: decoupled decay first (variable -= variable*wd*lr), then Adam with
+        // m += (g-m)(1-b1); v += (g^2-v)(1-b2); p -= m*alpha/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t)
+        pi -= pi * h.wd * h.lr;
+        mi += (gi - mi) * (1.f - h.b1);
+        vi += (gi * gi - vi) * (1.f - h.b2);
+        pi -= (mi * h.alpha) / (sqrtf(vi) + h.eps);
+    } else {
+        pi *= 1.f - h.lr * h.wd;
+        mi = h.b1 * mi + (1.f - h.b1) * gi;
+        vi = h.b2 * vi + (1.f - h.b2) * gi * gi;
+        pi -= h.lr * (mi / h.bc1) / (sqrtf(vi / h.bc2) + h.eps);
+    }
+}
+// the minibatch's metric sums ride along (dppo_optimizer_step): one launch fewer on the
+// minibatch's critical path than a separate copy. With a tag, met_out[nmet] receives it after
+// the sums (system-scope release), so the host polls host-mapped memory instead of recording
+// and waiting on an event (a marker packet on the minibatch chain). Workgroup 0.
+__device__ inline void copy_metrics(const double* __restrict__ met, double* __restrict__ met_out, int nmet, uint64_t tag) {
+    if ((int)threadIdx.x < nmet) met_out[threadIdx.x] = met[threadIdx.x];
+    if (tag) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(met_out + nmet), __builtin_bit_cast(uint64_t, (double)tag),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, int64_t n, float lr, float wd, float b1, float b2,
                                                     float eps, float alpha, float bc1, float bc2, int mode,
                                                     const double* __restrict__ met, double* __restrict__ met_out, int nmet,
                                                     uint64_t tag, L2Virt vt) {
-    // the minibatch's metric sums ride along (dppo_optimizer_step): one launch fewer on the
-    // minibatch's critical path than a separate copy. With a tag, met_out[nmet] receives it after
-    // the sums (system-scope release), so the host polls host-mapped memory instead of recording
-    // and waiting on an event (a marker packet on the minibatch chain).
-    if (blockIdx.x == 0) {
-        if ((int)threadIdx.x < nmet) met_out[threadIdx.x] = met[threadIdx.x];
-        if (tag) {
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                __hip_atomic_store(reinterpret_cast<uint64_t*>(met_out + nmet), __builtin_bit_cast(uint64_t, (double)tag),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-    }
+    if (blockIdx.x == 0) copy_metrics(met, met_out, nmet, tag);
+    const AdamHP h = {lr, wd, b1, b2, eps, alpha, bc1, bc2, mode};
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         float pi = p[i], mi = m[i], vi = v[i];
         const bool virt = vt.on && i >= vt.w_off && i < vt.b_off + vt.H;   // [l2_w | l2_b] are adjacent
         const float gi = virt ? l2_virtual_grad(g, vt, i) : g[i];
-        if (mode == DPPO_ADAMW_KERAS) {
-            // Keras 3: decoupled decay first (variable -= variable*wd*lr), then Adam with
-            // m += (g-m)(1-b1); v += (g^2-v)(1-b2); p -= m*alpha/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t)
-            pi -= pi * wd * lr;
-            mi += (gi - mi) * (1.f - b1);
-            vi += (gi * gi - vi) * (1.f - b2);
-            pi -= (mi * alpha) / (sqrtf(vi) + eps);
-        } else {
-            pi *= 1.f - lr * wd;
-            mi = b1 * mi + (1.f - b1) * gi;
-            vi = b2 * vi + (1.f - b2) * gi * gi;
-            pi -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
-        }
+        adamw_elem(pi, mi, vi, gi, h);
         p[i] = pi; m[i] = mi; v[i] = vi;
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The fused optimizer step (ABI 11, DPPO_STEP_FUSED_PACK and/or DPPO_STEP_CLEAR_GRADS): one launch
+// for AdamW + the network's image + the next minibatch's zeroing, which otherwise take three
+// launches (adamw_kernel, pack_all_kernel, zero_kernel) on every minibatch's critical path:
+//  * each element's thread stores its updated parameter into its slots of the images (the pack's
+//    per-element values: the same RNE conversion, FuseJob in dppo_internal.h), and zeroes its
+//    gradient after the read (CLEAR_GRADS);
+//  * the launch's last workgroup (ticket counter) then writes what other threads read during the
+//    launch or what needs every element final: the actor's W_OUT / T_OUT images (the virtual l2
+//    gradient reads rnd(W_out)), the pl2 and db_out gradients (read by every l2 element), the TEMB
+//    table (temb_* in dppo_common.cuh, the pack's arithmetic) and the caller's byte ranges (the
+//    next minibatch's metrics and workspace accumulators, dppo_ppo_clear_ranges).
+// ---------------------------------------------------------------------------------------------
+struct StepFuse {
+    int njobs;
+    FuseJob j[FUSE_MAXJ];
+    // elements whose new values the last workgroup needs: [0] the actor's time MLP (it derives TEMB
+    // from them), [1] W_out (its image slots are written by the last workgroup: the virtual l2
+    // gradient reads the old image during the launch). Their threads also publish the new value as
+    // a tagged granule {tag, fp32 bits} with an agent-scope store (the split sampler's exchange form)
+    int64_t own[2][2];
+    uint64_t* gran;                 // [own[0] count + own[1] count] granules
+    uint32_t gtag;                  // this launch's tag (nonzero, new per launch on the stream)
+    int temb_rows, TD, TS;          // the actor's TEMB rows (0: none) and its time stride
+    int64_t b1, w2, b2;             // time-MLP offsets relative to own[0][0] (= time_w1)
+    float* temb;
+    int clear_grads;
+    int64_t keep[2][2];             // gradients other elements read: cleared by the last workgroup
+    void* clr[4];
+    uint32_t clr_words[4];
+    int use_last;                   // 0: no last-workgroup phase (block 0 clears, no ticket)
+    unsigned* ticket;               // zero between launches (the last workgroup resets it)
+};
+
+template <class ET, int KG, int EPL>
+__device__ inline void fuse_store(const FuseJob& J, int64_t e, float x) {
+    if (J.kind == 2) {
+        reinterpret_cast<float*>(J.dst)[e] = x;
+        return;
+    }
+    // e < 2^31 (one weight tensor): 32-bit division
+    int k, nn;
+    if (J.kind == 0) { k = (int)e / J.IN; nn = (int)e - k * J.IN; }
+    else { nn = (int)e / J.IK; k = (int)e - nn * J.IK; }
+    const size_t slot = ((size_t)(nn >> 4) * J.KS + k / KG) * 64 + (nn & 15) + 16 * ((k % KG) / EPL);
+    reinterpret_cast<ET*>(J.dst + slot * 16)[k % EPL] = (ET)x;
+}
+
+__device__ inline bool in_range(int64_t i, const int64_t* r) { return i >= r[0] && i < r[1]; }
+
+// No device-scope fences (a release fence per workgroup is an L2 write-back on gfx950: ~2,000 of
+// them per launch). What the last workgroup reads from other workgroups comes as tagged granules it
+// polls; what it overwrites — the W_OUT / T_OUT slots and the pl2 / db_out gradients the virtual l2
+// gradient reads — every other workgroup has finished reading when it takes its ticket. Tickets are
+// counted per XCD first (blockIdx % 8), so no single address takes more than ~1/8 of the atomics.
+// The job loops stay rolled: unrolled they made the kernel ~20k instructions long.
+constexpr int FUSE_BLOCKS = 1024;
+template <class ET, int KG, int EPL>
+__global__ __launch_bounds__(256) void adamw_fused_kernel(float* __restrict__ p, float* g, float* __restrict__ m,
+                                                          float* __restrict__ v, int64_t n, AdamHP h,
+                                                          const double* __restrict__ met, double* __restrict__ met_out,
+                                                          int nmet, uint64_t tag, L2Virt vt, StepFuse f) {
+    extern __shared__ __attribute__((aligned(16))) float fsm[];
+    const int tid = threadIdx.x;
+    const int64_t n0 = f.own[0][1] - f.own[0][0], n1 = f.own[1][1] - f.own[1][0];
+    if (blockIdx.x == 0) copy_metrics(met, met_out, nmet, tag);
+    auto clears = [&]() {
+        for (int r = 0; r < 4; ++r)
+            for (uint32_t i = tid; i < f.clr_words[r]; i += 256) reinterpret_cast<uint32_t*>(f.clr[r])[i] = 0u;
+    };
+    if (!f.use_last && blockIdx.x == 0) clears();
+    for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < n; i += (int64_t)gridDim.x * 256) {
+        float pi = p[i], mi = m[i], vi = v[i];
+        const bool virt = vt.on && i >= vt.w_off && i < vt.b_off + vt.H;
+        const float gi = virt ? l2_virtual_grad(g, vt, i) : g[i];
+        adamw_elem(pi, mi, vi, gi, h);
+        p[i] = pi; m[i] = mi; v[i] = vi;
+        if (f.clear_grads && !in_range(i, f.keep[0]) && !in_range(i, f.keep[1])) g[i] = 0.f;
+        const bool o0 = in_range(i, f.own[0]), o1 = in_range(i, f.own[1]);
+        if (o0 || o1)
+            __hip_atomic_store(f.gran + (o0 ? i - f.own[0][0] : n0 + i - f.own[1][0]),
+                               ((uint64_t)f.gtag << 32) | __float_as_uint(pi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (o1) continue;   // W_OUT / T_OUT: the last workgroup's
+#pragma unroll 1
+        for (int q = 0; q < f.njobs; ++q) {
+            const FuseJob& J = f.j[q];
+            if (i >= J.lo && i < J.hi) fuse_store<ET, KG, EPL>(J, i - J.lo, pi);
+        }
+    }
+    if (!f.use_last) return;
+    __syncthreads();
+    __shared__ int last;
+    if (tid == 0) {
+        const unsigned xcd = blockIdx.x & 7, per = (gridDim.x - xcd + 7) / 8;   // blocks counted on this XCD's ticket
+        int l = 0;
+        if (atomicAdd(f.ticket + 16 * xcd, 1u) == per - 1) {
+            f.ticket[16 * xcd] = 0u;
+            const unsigned nx = gridDim.x < 8 ? gridDim.x : 8;
+            l = atomicAdd(f.ticket + 128, 1u) == nx - 1;
+        }
+        last = l;
+    }
+    __syncthreads();
+    if (!last) return;
+    if (tid == 0) f.ticket[128] = 0u;
+    float* ov = fsm;   // [n0 + n1] the owned elements' new values, then TEMB scratch
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 100000000ull;   // 1 s (100 MHz)
+    constexpr int GB = 8;   // granule loads in flight per thread
+    for (int64_t base = 0; base < n0 + n1; base += 256 * GB) {
+        uint64_t w[GB];
+#pragma unroll
+        for (int u = 0; u < GB; ++u) {
+            const int64_t q = base + u * 256 + tid;
+            w[u] = q < n0 + n1 ? __hip_atomic_load(f.gran + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < GB; ++u) {
+            const int64_t q = base + u * 256 + tid;
+            if (q >= n0 + n1) continue;
+            uint64_t x = w[u];
+            while ((uint32_t)(x >> 32) != f.gtag) {   // published before its workgroup's ticket; bounded
+                if (__builtin_amdgcn_s_memrealtime() > t_end) { x = ((uint64_t)f.gtag << 32) | 0x7fc00000u; break; }
+                __builtin_amdgcn_s_sleep(1);
+                x = __hip_atomic_load(f.gran + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            ov[q] = __uint_as_float((uint32_t)x);
+        }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int jq = 0; jq < f.njobs; ++jq) {   // job-major: each job's fields are loaded once
+        const FuseJob& J = f.j[jq];
+        const int64_t lo = J.lo > f.own[1][0] ? J.lo : f.own[1][0], hi = J.hi < f.own[1][1] ? J.hi : f.own[1][1];
+        for (int64_t i = lo + tid; i < hi; i += 256) fuse_store<ET, KG, EPL>(J, i - J.lo, ov[n0 + i - f.own[1][0]]);
+    }
+    if (f.temb_rows > 0) temb_rows_block(ov, 0, f.b1, f.w2, f.b2, f.TD, f.TS, f.temb_rows, f.temb, ov + n0 + n1);
+    if (f.clear_grads)
+        for (int r = 0; r < 2; ++r)
+            for (int64_t i = f.keep[r][0] + tid; i < f.keep[r][1]; i += 256) g[i] = 0.f;
+    clears();
+}
+
+// per (device, stream): a zeroed ticket counter, the granule buffer of the fused step and its launch
+// tag, created on first use and grown on demand (launches on one stream are ordered, so they share
+// them; the critic's step on the side stream has its own)
+struct StepScratch { unsigned* ticket; uint64_t* gran; int64_t cap; uint32_t* tag; };
+static int step_scratch(hipStream_t s, int64_t ngran, StepScratch* out) {
+    struct Ent { int dev; hipStream_t s; unsigned* ticket; uint64_t* gran; int64_t cap; uint32_t tag; };
+    thread_local Ent ents[16] = {};
+    thread_local int next = 0;
+    int dev = 0;
+    DPPO_HIP(hipGetDevice(&dev));
+    Ent* e = nullptr;
+    for (auto& x : ents)
+        if (x.ticket && x.dev == dev && x.s == s) { e = &x; break; }
+    if (!e) {
+        for (auto& x : ents)
+            if (!x.ticket) { e = &x; break; }
+        if (!e) {   // every slot taken (many streams): evict round robin once the device is idle
+            e = &ents[next];
+            next = (next + 1) % 16;
+            DPPO_HIP(hipDeviceSynchronize());
+            (void)hipFree(e->ticket);
+            (void)hipFree(e->gran);
+            *e = Ent{};
+        }
+        DPPO_HIP(hipMalloc((void**)&e->ticket, 1024));   // 8 per-XCD counters 64 B apart, the total at 512 B
+        e->dev = dev; e->s = s;
+        DPPO_HIP(hipMemsetAsync(e->ticket, 0, 1024, s));
+    }
+    if (ngran > e->cap) {   // stale granules never match: the tag is new per launch
+        if (e->gran) {
+            DPPO_HIP(hipStreamSynchronize(s));
+            (void)hipFree(e->gran);
+            e->gran = nullptr; e->cap = 0;
+        }
+        const int64_t cap = ngran > 32768 ? ngran : 32768;
+        DPPO_HIP(hipMalloc((void**)&e->gran, (size_t)cap * 8));
+        DPPO_HIP(hipMemsetAsync(e->gran, 0, (size_t)cap * 8, s));
+        e->cap = cap;
+    }
+    out->ticket = e->ticket; out->gran = e->gran; out->cap = e->cap; out->tag = &e->tag;
+    return DPPO_OK;
 }
 
 static int launch_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
@@ -731,17 +933,23 @@ extern "C" int dppo_adamw(float* params, const float* grads, float* m, float* v,
                         (hipStream_t)stream);
 }
 
-extern "C" int dppo_optimizer_step(const dppo_dims* d, int precision, float* params, const float* grads, float* m,
-                                   float* v, int64_t n, int64_t step, float lr, float weight_decay, float beta1,
-                                   float beta2, float eps, int mode, const float* actor_params, void* packed_actor,
-                                   const float* critic_params, void* packed_critic, const double* metrics,
-                                   double* metrics_out, int n_metrics, uint64_t metrics_tag, void* stream) {
+static int optimizer_step_impl(const dppo_dims* d, int precision, float* params, float* grads, float* m, float* v,
+                               int64_t n, int64_t step, float lr, float weight_decay, float beta1, float beta2,
+                               float eps, int mode, const float* actor_params, void* packed_actor,
+                               const float* critic_params, void* packed_critic, const double* metrics,
+                               double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
+                               const size_t* clear_bytes, int n_clear, void* stream) {
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
     DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
     DPPO_CHECK(!packed_actor == !actor_params && !packed_critic == !critic_params,
                "dppo_optimizer_step: a packed image needs its parameters");
+    DPPO_CHECK(n_clear >= 0 && n_clear <= 4 && (n_clear == 0 || (clear_ptrs && clear_bytes)),
+               "dppo_optimizer_step_ex: at most 4 clear ranges");
+    for (int r = 0; r < n_clear; ++r)
+        DPPO_CHECK(clear_ptrs[r] && ((uintptr_t)clear_ptrs[r] & 3) == 0 && clear_bytes[r] % 4 == 0 &&
+                   clear_bytes[r] / 4 < ((size_t)1 << 32), "dppo_optimizer_step_ex: clear range %d must be 4-B aligned", r);
     hipStream_t s = (hipStream_t)stream;
     // metrics_out may be mapped host memory (dppo_host_alloc): the kernel stores through its
     // device address
@@ -753,22 +961,137 @@ extern "C" int dppo_optimizer_step(const dppo_dims* d, int precision, float* par
     }
     const bool defer = (mode & DPPO_STEP_DEFER_SAMPLER_TABLES) != 0;
     const bool l2v = (mode & DPPO_STEP_L2_FROM_PL2) != 0;
-    mode &= ~(DPPO_STEP_DEFER_SAMPLER_TABLES | DPPO_STEP_L2_FROM_PL2);
+    const bool fuse = (mode & DPPO_STEP_FUSED_PACK) != 0;
+    const bool clear_g = (mode & DPPO_STEP_CLEAR_GRADS) != 0;
+    mode &= ~(DPPO_STEP_DEFER_SAMPLER_TABLES | DPPO_STEP_L2_FROM_PL2 | DPPO_STEP_FUSED_PACK | DPPO_STEP_CLEAR_GRADS);
+    const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
+    const FlatOffsets FC = make_flat_offsets(D.SD, D.HC, 1, 0);
     L2Virt vt = {};
     if (l2v) {
         DPPO_CHECK(packed_actor && actor_params == params,
                    "dppo_optimizer_step: DPPO_STEP_L2_FROM_PL2 needs the actor's image and the actor range first");
-        const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
         DPPO_CHECK(n >= (int64_t)FA.count, "dppo_optimizer_step: DPPO_STEP_L2_FROM_PL2 needs the whole actor range");
         DPPO_CHECK(FA.l2_b == FA.l2_w + (size_t)D.H * D.H, "l2 layout");
         const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
         vt = L2Virt{1, (int64_t)FA.l2_w, (int64_t)FA.l2_b, (int64_t)FA.out_b, D.H, D.XD, precision,
                     (const uint8_t*)packed_actor + L.off[SEG_W_OUT]};
     }
+    // the one-launch form: a single network whose parameters are exactly the range, and (actor,
+    // 2-byte operands) its split-sampler tables deferred, as the pack would leave them
+    const bool one_actor = packed_actor && !packed_critic && actor_params == params && n == (int64_t)FA.count &&
+                           (!dppo_prec_2b(precision) || defer);
+    const bool one_critic = packed_critic && !packed_actor && critic_params == params && n == (int64_t)FC.count;
+    const int R = D.K;
+    const size_t lds_max = sizeof(float) * ((size_t)3 * R * D.TD + (FA.in_w - FA.time_w1) + (size_t)D.H * D.XD);
+    if ((fuse || clear_g) && (one_actor || one_critic) && (!one_actor || lds_max <= 64 * 1024) && n > 0) {
+        const bool two = dppo_prec_2b(precision);
+        StepFuse f = {};
+        for (int r = 0; r < 2; ++r) f.own[r][0] = f.own[r][1] = f.keep[r][0] = f.keep[r][1] = -1;
+        if (fuse) {
+            f.njobs = one_actor ? dppo_fuse_jobs(D.IN, D.H, D.XD, D.TD, precision, packed_actor, D.K, f.j)
+                                : dppo_fuse_jobs(D.SD, D.HC, 1, 0, precision, packed_critic, 0, f.j);
+            DPPO_CHECK(f.njobs >= 0, "dppo_optimizer_step: fused pack jobs");
+            if (one_actor) {
+                const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+                f.temb_rows = R; f.TD = D.TD; f.TS = D.TS;
+                f.own[0][0] = (int64_t)FA.time_w1; f.own[0][1] = (int64_t)FA.in_w;
+                f.b1 = (int64_t)(FA.time_b1 - FA.time_w1); f.w2 = (int64_t)(FA.time_w2 - FA.time_w1);
+                f.b2 = (int64_t)(FA.time_b2 - FA.time_w1);
+                f.temb = (float*)((uint8_t*)packed_actor + L.off[SEG_TEMB]);
+                if (l2v) { f.own[1][0] = (int64_t)FA.out_w; f.own[1][1] = (int64_t)(FA.out_w + (size_t)D.H * D.XD); }
+            }
+        }
+        f.clear_grads = clear_g ? 1 : 0;
+        if (l2v && clear_g) {   // read by every l2 element's virtual gradient
+            f.keep[0][0] = (int64_t)FA.l2_w; f.keep[0][1] = (int64_t)(FA.l2_w + (size_t)D.H * D.XD);
+            f.keep[1][0] = (int64_t)FA.out_b; f.keep[1][1] = (int64_t)(FA.out_b + D.XD);
+        }
+        for (int r = 0; r < n_clear; ++r) { f.clr[r] = clear_ptrs[r]; f.clr_words[r] = (uint32_t)(clear_bytes[r] / 4); }
+        f.use_last = (f.temb_rows > 0 || f.own[1][1] > 0 || f.keep[0][1] > 0) ? 1 : 0;
+        if (f.use_last) {
+            StepScratch sc;
+            rc = step_scratch(s, (f.own[0][1] - f.own[0][0]) + (f.own[1][1] - f.own[1][0]), &sc);
+            if (rc) return rc;
+            f.ticket = sc.ticket; f.gran = sc.gran;
+            if (++*sc.tag == 0) ++*sc.tag;   // 0 is the buffer's initial tag
+            f.gtag = *sc.tag;
+        }
+        DPPO_CHECK(n_metrics >= 0 && n_metrics <= 256 && (n_metrics == 0 || (metrics && mout)),
+                   "dppo_optimizer_step: bad metrics copy");
+        DPPO_CHECK(metrics_tag == 0 || (mout && metrics_tag < ((uint64_t)1 << 53)),
+                   "dppo_optimizer_step: a tag needs metrics_out and < 2^53");
+        DPPO_CHECK(step >= 1 && (mode == DPPO_ADAMW_KERAS || mode == DPPO_ADAMW_TORCH), "dppo_adamw: bad step or mode");
+        DPPO_CHECK(params && grads && m && v, "dppo_adamw: null pointer");
+        const double bc1 = 1.0 - pow((double)beta1, (double)step);
+        const double bc2 = 1.0 - pow((double)beta2, (double)step);
+        const AdamHP h = {lr, weight_decay, beta1, beta2, eps, (float)((double)lr * sqrt(bc2) / bc1), (float)bc1,
+                          (float)bc2, mode};
+        const int64_t blocks64 = (n + 255) / 256;
+        const unsigned blocks = (unsigned)(blocks64 < FUSE_BLOCKS ? blocks64 : FUSE_BLOCKS);
+        const size_t lds = f.use_last ? sizeof(float) * ((size_t)(f.own[0][1] - f.own[0][0]) +
+                                                         (size_t)(f.own[1][1] - f.own[1][0]) +
+                                                         (f.temb_rows > 0 ? (size_t)3 * R * D.TD : 0)) : 0;
+        DPPO_CHECK(lds <= 64 * 1024, "dppo_optimizer_step: fused step LDS %zu B", lds);
+        DppoKtScope kt(KT_ADAMW, s);
+        if (precision == DPPO_BF16)
+            hipLaunchKernelGGL((adamw_fused_kernel<__bf16, 32, 8>), dim3(blocks), dim3(256), lds, s, params, grads, m, v,
+                               n, h, metrics, mout, n_metrics, metrics_tag, vt, f);
+        else if (precision == DPPO_F16)
+            hipLaunchKernelGGL((adamw_fused_kernel<_Float16, 32, 8>), dim3(blocks), dim3(256), lds, s, params, grads, m,
+                               v, n, h, metrics, mout, n_metrics, metrics_tag, vt, f);
+        else
+            hipLaunchKernelGGL((adamw_fused_kernel<float, 16, 4>), dim3(blocks), dim3(256), lds, s, params, grads, m, v,
+                               n, h, metrics, mout, n_metrics, metrics_tag, vt, f);
+        DPPO_HIP(hipGetLastError());
+        if (!fuse) return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s, defer);
+        return one_actor && two ? dppo_mark_tables_stale(D, precision, actor_params, packed_actor) : DPPO_OK;
+    }
+    // the launch-per-stage form (any ranges and images): AdamW, the pack, then the clears
     rc = launch_adamw(params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode, metrics, mout,
                       n_metrics, metrics_tag, s, vt);
     if (rc) return rc;
-    return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s, defer);
+    rc = dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s, defer);
+    if (rc || (!clear_g && n_clear == 0)) return rc;
+    ZeroArgs z = {};
+    int nz = 0;
+    if (clear_g && n > 0) { z.p[0] = grads; z.n[0] = (size_t)n * sizeof(float); nz = 1; }
+    for (int r = 0; r < n_clear; ++r) {
+        if (nz == 4) {
+            hipLaunchKernelGGL(zero_kernel, dim3(16), dim3(256), 0, s, z);
+            DPPO_HIP(hipGetLastError());
+            z = ZeroArgs{};
+            nz = 0;
+        }
+        z.p[nz] = clear_ptrs[r]; z.n[nz] = clear_bytes[r]; ++nz;
+    }
+    if (nz) {
+        DppoKtScope kt(KT_ZERO, s);
+        hipLaunchKernelGGL(zero_kernel, dim3(16), dim3(256), 0, s, z);
+        DPPO_HIP(hipGetLastError());
+    }
+    return DPPO_OK;
+}
+
+extern "C" int dppo_optimizer_step(const dppo_dims* d, int precision, float* params, const float* grads, float* m,
+                                   float* v, int64_t n, int64_t step, float lr, float weight_decay, float beta1,
+                                   float beta2, float eps, int mode, const float* actor_params, void* packed_actor,
+                                   const float* critic_params, void* packed_critic, const double* metrics,
+                                   double* metrics_out, int n_metrics, uint64_t metrics_tag, void* stream) {
+    DPPO_CHECK((mode & DPPO_STEP_CLEAR_GRADS) == 0, "dppo_optimizer_step: DPPO_STEP_CLEAR_GRADS needs dppo_optimizer_step_ex");
+    return optimizer_step_impl(d, precision, params, const_cast<float*>(grads), m, v, n, step, lr, weight_decay, beta1,
+                               beta2, eps, mode, actor_params, packed_actor, critic_params, packed_critic, metrics,
+                               metrics_out, n_metrics, metrics_tag, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int dppo_optimizer_step_ex(const dppo_dims* d, int precision, float* params, float* grads, float* m,
+                                      float* v, int64_t n, int64_t step, float lr, float weight_decay, float beta1,
+                                      float beta2, float eps, int mode, const float* actor_params, void* packed_actor,
+                                      const float* critic_params, void* packed_critic, const double* metrics,
+                                      double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
+                                      const size_t* clear_bytes, int n_clear, void* stream) {
+    return optimizer_step_impl(d, precision, params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode,
+                               actor_params, packed_actor, critic_params, packed_critic, metrics, metrics_out,
+                               n_metrics, metrics_tag, clear_ptrs, clear_bytes, n_clear, stream);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -992,6 +1315,50 @@ static int launch_critic_l2_back(const Dims& D, int precision, const float* cpl2
     return DPPO_OK;
 }
 
+// the atomically accumulated outputs a minibatch half (or the whole) zeroes first: gradients (entry
+// 0), metrics (actor: 0, 2..15; critic: 1), pl2 | bucket sums, cpl2 | stats | crow_cnt. Entries 1..3
+// are what dppo_ppo_clear_ranges reports (the gradients are cleared by the optimizer step's AdamW)
+static ZeroArgs minibatch_zero_args(const Dims& D, const PpoWorkspace& ws, float* grads, double* metrics, int parts) {
+    const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
+    const FlatOffsets FC = make_flat_offsets(D.SD, D.HC, 1, 0);
+    ZeroArgs z = {};
+    const size_t actor_acc = (size_t)((const uint8_t*)(ws.gseg + 16 * D.H) - (const uint8_t*)ws.pl2);
+    const size_t critic_acc = (size_t)((const uint8_t*)(ws.crow_cnt + 1) - (const uint8_t*)ws.cpl2);
+    if (parts == 3) {
+        z.p[0] = grads; z.n[0] = (FA.count + FC.count) * sizeof(float);
+        z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
+        z.p[2] = ws.pl2; z.n[2] = actor_acc;
+        z.p[3] = ws.cpl2; z.n[3] = critic_acc;
+    } else if (parts == 1 || parts == 4) {
+        z.p[0] = grads; z.n[0] = FA.count * sizeof(float);
+        z.p[1] = metrics; z.n[1] = sizeof(double);
+        z.p[2] = metrics + 2; z.n[2] = 14 * sizeof(double);
+        z.p[3] = ws.pl2; z.n[3] = actor_acc;
+    } else if (parts == 2) {
+        z.p[0] = grads ? grads + FA.count : nullptr; z.n[0] = FC.count * sizeof(float);
+        z.p[1] = metrics + 1; z.n[1] = sizeof(double);
+        z.p[2] = ws.cpl2; z.n[2] = critic_acc;
+    }
+    return z;
+}
+
+extern "C" int dppo_ppo_clear_ranges(const dppo_dims* d, int precision, int batch_rows, void* workspace,
+                                     double* metrics, int part, void** ptrs, size_t* bytes, int* count) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
+    DPPO_CHECK(workspace && metrics && ptrs && bytes && count && batch_rows > 0, "dppo_ppo_clear_ranges: bad arguments");
+    DPPO_CHECK(part == 1 || part == 2 || part == 3 || part == 4, "dppo_ppo_clear_ranges: part must be 1, 2, 3 or 4");
+    const PpoWorkspace ws = make_ppo_workspace(D, precision, batch_rows, (uint8_t*)workspace);
+    const ZeroArgs z = minibatch_zero_args(D, ws, nullptr, metrics, part);
+    int n = 0;
+    for (int r = 1; r < 4; ++r)
+        if (z.p[r]) { ptrs[n] = z.p[r]; bytes[n] = z.n[r]; ++n; }
+    *count = n;
+    return DPPO_OK;
+}
+
 // parts: 3 = the whole minibatch (critic on the internal side stream); 1 = the actor's half only,
 // 2 = the critic's half only, each on the caller's stream (the caller overlaps them; see
 // dppo_ppo_minibatch_part in include/dppo.h)
@@ -1021,30 +1388,16 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     DPPO_CHECK(parts >= 1 && parts <= 5, "dppo_ppo_minibatch: bad part %d", parts);
     DPPO_CHECK(parts == 3 || adv_stats || parts == 2 || parts == 5,
                "dppo_ppo_minibatch_part: the actor half needs adv_stats");
-    // one launch zeroes the atomically accumulated outputs of the half (or whole) being run:
-    // gradients, metrics (actor: 0, 2..15; critic: 1), pl2 | bucket sums, cpl2 | stats
-    ZeroArgs z = {};
-    const size_t actor_acc = (size_t)((const uint8_t*)(ws.gseg + 16 * D.H) - (const uint8_t*)ws.pl2);
-    const size_t critic_acc = (size_t)((const uint8_t*)(ws.crow_cnt + 1) - (const uint8_t*)ws.cpl2);   // cpl2 | stats | crow_cnt
-    if (parts == 3) {
-        z.p[0] = grads; z.n[0] = (FA.count + FC.count) * sizeof(float);
-        z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
-        z.p[2] = ws.pl2; z.n[2] = actor_acc;
-        z.p[3] = ws.cpl2; z.n[3] = critic_acc;
-    } else if (parts == 1 || parts == 4) {
-        z.p[0] = grads; z.n[0] = FA.count * sizeof(float);
-        z.p[1] = metrics; z.n[1] = sizeof(double);
-        z.p[2] = metrics + 2; z.n[2] = 14 * sizeof(double);
-        z.p[3] = ws.pl2; z.n[3] = actor_acc;
-    } else if (parts == 2) {
-        z.p[0] = grads + FA.count; z.n[0] = FC.count * sizeof(float);
-        z.p[1] = metrics + 1; z.n[1] = sizeof(double);
-        z.p[2] = ws.cpl2; z.n[2] = critic_acc;
-    }
+    DPPO_CHECK((hp->flags & ~(DPPO_PPO_L2_DEFERRED | DPPO_PPO_LEARN_ETA | DPPO_PPO_PRECLEARED)) == 0,
+               "dppo_ppo_minibatch: unknown flags 0x%x", hp->flags);
+    // one launch zeroes the atomically accumulated outputs of the half (or whole) being run
+    // (minibatch_zero_args) unless the caller's optimizer step already did (DPPO_PPO_PRECLEARED)
+    const ZeroArgs z = minibatch_zero_args(D, ws, grads, metrics, parts);
     // few workgroups: the split update runs this while the other stream's row tiles hold most CUs,
     // and a 256-block grid waited ~25 us for slots (DPPO_ZERO_BLOCKS: measurement knob)
     static const int zero_blocks = [] { const char* e = getenv("DPPO_ZERO_BLOCKS"); return e ? atoi(e) : 16; }();
-    if (parts != 5) {      // part 5 continues the actor half whose part 4 zeroed its outputs
+    // part 5 continues the actor half whose part 4 zeroed its outputs
+    if (parts != 5 && !(hp->flags & DPPO_PPO_PRECLEARED)) {
         DppoKtScope kt(KT_ZERO, s);
         hipLaunchKernelGGL(zero_kernel, dim3(zero_blocks > 0 ? zero_blocks : 16), dim3(256), 0, s, z);
         DPPO_HIP(hipGetLastError());
@@ -1068,8 +1421,6 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     // fp16: the backward images carry GRAD_SCALE x the gradient (fp16 range); dW divides it out
     const float gscale = dppo_grad_scale_rows(precision, hp->global_rows);
     lh.grad_scale = hp->loss_scale / (float)hp->global_rows * gscale;
-    DPPO_CHECK((hp->flags & ~(DPPO_PPO_L2_DEFERRED | DPPO_PPO_LEARN_ETA)) == 0, "dppo_ppo_minibatch: unknown flags 0x%x",
-               hp->flags);
     lh.eta_unscale = (hp->flags & DPPO_PPO_LEARN_ETA) ? 1.f / gscale : 0.f;
     // the actor's l2 gradient left factored in its own grads region (include/dppo.h)
     const bool l2_def = (hp->flags & DPPO_PPO_L2_DEFERRED) != 0;

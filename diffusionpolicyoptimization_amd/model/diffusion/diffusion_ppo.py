@@ -7,7 +7,7 @@ fused HIP pass (dppo_ppo_minibatch), left in `self.grads` for the optimiser. The
 import numpy as np
 import torch
 
-from ... import ops
+from ... import _lib, ops
 from .diffusion_vpg import VPGDiffusion, _as_state
 
 # metrics slots written by the kernels (sums over rows; see update.hip)
@@ -70,11 +70,16 @@ class PPODiffusion(VPGDiffusion):
                                    self.workspace(max_rows), self.grads, max_rows)
         hps = {}
 
-        def run(epoch, start, rows, global_rows=None, adv_stats=None, part=None, metrics=None, stream=None):
+        def run(epoch, start, rows, global_rows=None, adv_stats=None, part=None, metrics=None, stream=None,
+                precleared=False):
+            # precleared (ABI 11, DPPO_PPO_PRECLEARED): the optimizer step before this call already
+            # zeroed what the part would zero first (its gradients and ops.ClearRanges for these rows)
             g = int(global_rows or rows)
-            hp = hps.get(g)
+            hp = hps.get((g, precleared))
             if hp is None:
-                hp = hps[g] = self.hparams(g, reward_horizon, loss_scale, l2_deferred=l2_deferred)
+                hp = hps[(g, precleared)] = self.hparams(g, reward_horizon, loss_scale, l2_deferred=l2_deferred)
+                if precleared:
+                    hp.flags |= _lib.DPPO_PPO_PRECLEARED
             bound(hp, epoch, start, rows, self.metrics if metrics is None else metrics, adv_stats=adv_stats, part=part,
                   stream=stream)
         return run

@@ -828,7 +828,10 @@ class BoundOptimizerStep:
 
     def __init__(self, d: ModelDims, precision, params, grads, m, v, weight_decay, beta1, beta2, eps, mode,
                  actor_params=None, packed_actor=None, critic_params=None, packed_critic=None,
-                 defer_sampler_tables=False, l2_from_pl2=False):
+                 defer_sampler_tables=False, l2_from_pl2=False, fused_pack=False, clear_grads=False):
+        """fused_pack (ABI 11, DPPO_STEP_FUSED_PACK): AdamW and the image in one launch where the
+        library can (one network whose parameters are the range); clear_grads (DPPO_STEP_CLEAR_GRADS):
+        the step zeroes the range's gradients and the `clear` ranges of each call after reading them."""
         n = params.numel()
         for t, nm in ((grads, "grads"), (m, "m"), (v, "v")):
             if t.numel() != n:
@@ -837,24 +840,52 @@ class BoundOptimizerStep:
         self._dims = _dims_c(d)
         mode_i = ((_lib.DPPO_ADAMW_KERAS if mode == "keras" else _lib.DPPO_ADAMW_TORCH) |
                   (_lib.DPPO_STEP_DEFER_SAMPLER_TABLES if defer_sampler_tables else 0) |
-                  (_lib.DPPO_STEP_L2_FROM_PL2 if l2_from_pl2 else 0))
+                  (_lib.DPPO_STEP_L2_FROM_PL2 if l2_from_pl2 else 0) |
+                  (_lib.DPPO_STEP_FUSED_PACK if fused_pack else 0) |
+                  (_lib.DPPO_STEP_CLEAR_GRADS if clear_grads else 0))
         self._head = (ctypes.byref(self._dims), _prec(precision), ptr(params), ptr(grads), ptr(m), ptr(v), int(n))
         self._hp = (float(weight_decay), float(beta1), float(beta2), float(eps), mode_i, ptr(actor_params),
                     ptr(packed_actor), ptr(critic_params), ptr(packed_critic))
         self._dev = params.device
         self._keep = (params, grads, m, v, actor_params, packed_actor, critic_params, packed_critic)
 
-    def __call__(self, step, lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0, stream=None):
+    def __call__(self, step, lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0, stream=None, clear=None):
         """metrics_out: a device tensor or a dppo_host_alloc address (as optimizer_step); metrics: a
-        device tensor or address; stream: a raw stream handle (default: the current stream)."""
+        device tensor or address; stream: a raw stream handle (default: the current stream); clear: a
+        ClearRanges (byte ranges zeroed after the step's last read, dppo_optimizer_step_ex)."""
         mo = metrics_out if isinstance(metrics_out, int) else (metrics_out.data_ptr() if metrics_out is not None else None)
         mi = metrics if isinstance(metrics, int) else ptr(metrics)
-        rc = self._lib.dppo_optimizer_step(*self._head, int(step), float(lr), *self._hp, mi,
-                                           ctypes.c_void_p(mo) if mo else None, int(n_metrics),
-                                           ctypes.c_uint64(int(metrics_tag)),
-                                           stream_handle(self._dev) if stream is None else stream)
+        cp, cb, cn = (None, None, 0) if clear is None else clear.args
+        rc = self._lib.dppo_optimizer_step_ex(*self._head, int(step), float(lr), *self._hp, mi,
+                                              ctypes.c_void_p(mo) if mo else None, int(n_metrics),
+                                              ctypes.c_uint64(int(metrics_tag)), cp, cb, cn,
+                                              stream_handle(self._dev) if stream is None else stream)
         if rc != 0:
             raise _lib.DppoError(f"dppo_optimizer_step failed ({rc}): {self._lib.dppo_last_error().decode()}")
+
+
+class ClearRanges:
+    """The non-gradient byte ranges a minibatch part zeroes first (dppo_ppo_clear_ranges: metric slots
+    of `metrics`, the workspace's accumulators for `rows`), marshalled for dppo_optimizer_step_ex, so
+    the optimizer step before that minibatch clears them and the minibatch runs with
+    DPPO_PPO_PRECLEARED. metrics: a device address or fp64[16] tensor; workspace: the uint8 tensor."""
+
+    def __init__(self, d: ModelDims, precision, rows, workspace, metrics, part):
+        lib = _lib.load()
+        self._ptrs = (ctypes.c_void_p * 4)()
+        self._bytes = (ctypes.c_size_t * 4)()
+        cnt = ctypes.c_int(0)
+        mptr = metrics if isinstance(metrics, int) else metrics.data_ptr()
+        rc = lib.dppo_ppo_clear_ranges(ctypes.byref(_dims_c(d)), _prec(precision), int(rows), ptr(workspace),
+                                       ctypes.c_void_p(mptr), int(part), self._ptrs, self._bytes, ctypes.byref(cnt))
+        if rc != 0:
+            raise _lib.DppoError(f"dppo_ppo_clear_ranges failed ({rc}): {lib.dppo_last_error().decode()}")
+        self.count = cnt.value
+        self.args = (self._ptrs, self._bytes, self.count)
+        self._keep = (workspace, metrics)
+
+    def ranges(self):
+        return [(int(self._ptrs[i]), int(self._bytes[i])) for i in range(self.count)]
 
 
 def q_sched_table(schedule):

@@ -52,19 +52,22 @@ class AdamW:
                            ap, pa, cp, pc, metrics, metrics_out, n_metrics, metrics_tag,
                            defer_sampler_tables=defer_sampler_tables)
 
-    def bind_range(self, grads, lo, hi, dims, precision, packs=(), defer_sampler_tables=False, l2_from_pl2=False):
+    def bind_range(self, grads, lo, hi, dims, precision, packs=(), defer_sampler_tables=False, l2_from_pl2=False,
+                   fused_pack=False, clear_grads=False):
         """apply_range over a fixed range and fixed images, validated and marshalled once
         (ops.BoundOptimizerStep): returns f(lr, metrics=None, metrics_out=None, n_metrics=0,
-        metrics_tag=0) for the step begin_step() opened."""
+        metrics_tag=0, stream=None, clear=None) for the step begin_step() opened. fused_pack /
+        clear_grads: ABI 11 (one launch; the gradients and the `clear` ranges zeroed after use)."""
         pk = dict(packs)
         ap, pa = pk.get("actor", (None, None))
         cp, pc = pk.get("critic", (None, None))
         b = ops.BoundOptimizerStep(dims, precision, self.params[lo:hi], grads[lo:hi], self.m[lo:hi], self.v[lo:hi],
                                    self.weight_decay, self.beta_1, self.beta_2, self.epsilon, self.mode, ap, pa, cp,
-                                   pc, defer_sampler_tables=defer_sampler_tables, l2_from_pl2=l2_from_pl2)
+                                   pc, defer_sampler_tables=defer_sampler_tables, l2_from_pl2=l2_from_pl2,
+                                   fused_pack=fused_pack, clear_grads=clear_grads)
 
-        def step(lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0, stream=None):
-            b(self.iterations, lr, metrics, metrics_out, n_metrics, metrics_tag, stream=stream)
+        def step(lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0, stream=None, clear=None):
+            b(self.iterations, lr, metrics, metrics_out, n_metrics, metrics_tag, stream=stream, clear=clear)
         return step
 
     def apply_gradients_split(self, grads, ranges):

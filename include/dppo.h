@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 10
+#define DPPO_ABI_VERSION 11
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -54,6 +54,16 @@ enum { DPPO_STEP_DEFER_SAMPLER_TABLES = 0x100 };
  * form of DPPO_PPO_L2_DEFERRED; AdamW forms it from pl2, db_out and the actor image's rnd(W_out)
  * (needs actor_params == params and packed_actor). */
 enum { DPPO_STEP_L2_FROM_PL2 = 0x200 };
+/* ABI 11, OR'd into dppo_optimizer_step's mode. DPPO_STEP_FUSED_PACK: AdamW and the pack in ONE
+ * launch when the step packs a single network whose flat parameters are exactly the range (the actor
+ * with 2-byte operands also needs DPPO_STEP_DEFER_SAMPLER_TABLES): each element's thread stores its
+ * updated value into its slots of the images (the values the pack writes), and the launch's last
+ * workgroup derives the actor's TEMB table. The image must have been fully packed once before (its
+ * zero padding is not rewritten). Any other combination runs the two launches.
+ * DPPO_STEP_CLEAR_GRADS (dppo_optimizer_step_ex only): the step zeroes the range's gradients after
+ * reading them, and the byte ranges given to dppo_optimizer_step_ex after every read, so the next
+ * minibatch of this range may skip its zeroing launch (DPPO_PPO_PRECLEARED). */
+enum { DPPO_STEP_FUSED_PACK = 0x400, DPPO_STEP_CLEAR_GRADS = 0x800 };
 
 /* Model / schedule dimensions (cfg keys of cfg/gym/finetune/hopper-v2/ft_ppo_diffusion_mlp.yaml:18-25,78-110). */
 typedef struct dppo_dims {
@@ -280,6 +290,11 @@ enum { DPPO_PPO_L2_DEFERRED = 1 };
  * d loss / d eta into metrics[8] (fp64), through sigma = eta s and d = sqrt(clip(1 - abar_prev -
  * sigma^2, 0, 1e6)) of each row (schedule column 7 = s). dppo_eta_step applies it. */
 enum { DPPO_PPO_LEARN_ETA = 2 };
+/* ABI 11, dppo_ppo_hparams.flags. DPPO_PPO_PRECLEARED: the outputs this part would zero first (its
+ * gradient range and the ranges dppo_ppo_clear_ranges reports for the same workspace, rows and
+ * metrics) are already zero — the previous optimizer step of the range cleared them
+ * (DPPO_STEP_CLEAR_GRADS) — so the part skips its zeroing launch. */
+enum { DPPO_PPO_PRECLEARED = 4 };
 
 /* ABI 9: the learnable DDIM eta's optimizer step (the original DPPO's EtaFixed trained by its own
  * AdamW every eta_update_interval minibatches, train_ppo_diffusion_agent.py:28-45, 358-359 — the
@@ -335,6 +350,12 @@ DPPO_API int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const vo
  * the actor's dW + time-MLP backward, so a data-parallel caller can all-reduce the metrics with the
  * critic's gradients while the actor's dW runs. Same arguments and results as dppo_ppo_minibatch,
  * which runs both halves (the critic on an internal side stream). */
+/* ABI 11: the non-gradient byte ranges part (1/4 = actor, 2 = critic, 3 = whole) of a minibatch of
+ * batch_rows rows zeroes before it runs (metric slots of `metrics`, workspace accumulators): up to 3,
+ * their count in *count. A caller passes them to the preceding dppo_optimizer_step_ex to run that
+ * minibatch with DPPO_PPO_PRECLEARED. */
+DPPO_API int dppo_ppo_clear_ranges(const dppo_dims* d, int precision, int batch_rows, void* workspace, double* metrics,
+                                   int part, void** ptrs, size_t* bytes, int* count);
 DPPO_API int dppo_ppo_minibatch_part(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
                             const void* packed_ft, const void* packed_critic, const float* actor_params,
                             const float* sched, const float* obs, const float* chains, const float* lp_old_mean,
@@ -380,6 +401,14 @@ DPPO_API int dppo_optimizer_step(const dppo_dims* d, int precision, float* param
                         float beta2, float eps, int mode, const float* actor_params, void* packed_actor,
                         const float* critic_params, void* packed_critic, const double* metrics,
                         double* metrics_out, int n_metrics, uint64_t metrics_tag, void* stream);
+/* ABI 11: dppo_optimizer_step that also zeroes n_clear (<= 4) byte ranges (4-B aligned, sizes multiples
+ * of 4) after the launch's last read, and with DPPO_STEP_CLEAR_GRADS the gradients of the range. */
+DPPO_API int dppo_optimizer_step_ex(const dppo_dims* d, int precision, float* params, float* grads, float* m,
+                           float* v, int64_t n, int64_t step, float lr, float weight_decay, float beta1,
+                           float beta2, float eps, int mode, const float* actor_params, void* packed_actor,
+                           const float* critic_params, void* packed_critic, const double* metrics,
+                           double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
+                           const size_t* clear_bytes, int n_clear, void* stream);
 
 #ifdef __cplusplus
 }

@@ -3,6 +3,7 @@
 Tolerances: fp32 (f32-input MFMA) mode is checked tightly; bf16 mode (bf16 operands, fp32
 accumulate/epilogue) against a stated looser bound. Integer work (Feistel permutation) is bit-exact.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -523,6 +524,67 @@ def test_l2_deferred_minibatch_and_step(cuda, precision):
         out[virt] = (P, M, V, img)
     for a, b in zip(out[True], out[False]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("net", ["actor", "actor_l2v", "critic"])
+def test_fused_optimizer_step_matches_two_launches(cuda, precision, net):
+    """ABI 11: an optimizer step with DPPO_STEP_FUSED_PACK | DPPO_STEP_CLEAR_GRADS (one launch: AdamW,
+    each element's image slots, then the last workgroup's W_OUT / T_OUT slots, TEMB rows and clears)
+    gives bit-identical parameters, moments and image bytes to AdamW + the pack (two launches), zeroes
+    the range's gradients and the given byte ranges, and leaves its ticket counter reusable (three
+    steps in a row on one stream)."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp_64env",
+                      [f"model.precision={precision}"])
+    m = instantiate(cfg.model, device=cuda, seed=0)
+    d = m.dims
+    actor = net != "critic"
+    P0 = (m.actor_ft_params if actor else m.critic_params).clone()
+    img0 = (m.packed_ft if actor else m.packed_critic).clone()
+    n = P0.numel()
+    gen = torch.Generator(device=cuda).manual_seed(7)
+    G0 = torch.randn(n, device=cuda, generator=gen) * 0.05
+    if net == "actor_l2v":   # the factored l2 gradient: pl2 [H][XD] at the l2 region's start, the rest zero
+        offs, o = {}, 0
+        for name, shape in ops.actor_param_spec(d):
+            offs[name] = (o, int(np.prod(shape)))
+            o += offs[name][1]
+        l2w, nl2 = offs["l2_w"]
+        G0[l2w + d.actor_hidden * d.xd:l2w + nl2] = 0
+        G0[offs["l2_b"][0]:offs["l2_b"][0] + offs["l2_b"][1]] = 0
+    M0 = torch.rand(n, device=cuda, generator=gen) * 1e-4
+    V0 = torch.rand(n, device=cuda, generator=gen) * 1e-7
+    scratch = torch.full((3, 300), 7.0, dtype=torch.float64, device=cuda)
+    out = {}
+    for fused in (False, True):
+        P, M, V, img, G = P0.clone(), M0.clone(), V0.clone(), img0.clone(), G0.clone()
+        packs = (P, img, None, None) if actor else (None, None, P, img)
+        step = ops.BoundOptimizerStep(d, m.precision, P, G, M, V, 0.004, 0.9, 0.999, 1e-7, "keras", *packs,
+                                      defer_sampler_tables=actor, l2_from_pl2=net == "actor_l2v",
+                                      fused_pack=fused, clear_grads=fused)
+        clear = None
+        if fused:   # three byte ranges of a scratch buffer, as dppo_ppo_clear_ranges would give
+            clear = type("C", (), {})()
+            base = scratch.data_ptr()
+            ptrs = (ctypes.c_void_p * 4)(base, base + 2400, base + 4800 + 16)
+            nb = (ctypes.c_size_t * 4)(8, 2400, 1000)
+            clear.args = (ptrs, nb, 3)
+        for it in range(3):
+            if fused and it:
+                G.copy_(G0)
+            step(it + 2, 1e-3 * (it + 1), clear=clear)
+        torch.cuda.synchronize()
+        out[fused] = (P, M, V, img, G)
+    for name, a, b in zip(("params", "m", "v", "image"), out[True][:4], out[False][:4]):
+        assert torch.equal(a, b), name
+    assert int(torch.count_nonzero(out[True][4])) == 0
+    flat = scratch.view(torch.uint8).view(-1)
+    assert int(torch.count_nonzero(flat[:8])) == 0 and int(torch.count_nonzero(flat[2400:4800])) == 0
+    assert int(torch.count_nonzero(flat[4816:5816])) == 0
+    assert bool((flat[8:2400] != 0).any()) and bool((flat[5816:] != 0).any())   # nothing outside the ranges
 
 
 def test_value_moments(cuda):
