@@ -478,6 +478,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             fuse_mode = os.environ.get("DPPO_FUSED_STEP", "critic")   # "0" | "critic" | "all" (A/B knob)
             fuse = split and self.minibatch_hook is None and fuse_mode != "0"
             fuse_actor = fuse and fuse_mode == "all"
+            # the actor's step (AdamW + pack) clears the actor's accumulators in its pack launch
+            clear_actor = fuse and os.environ.get("DPPO_ACTOR_CLEAR", "1") != "0"
             opt = self.actor_optimizer
             ng_all = m.grads.numel()
             # the bound calls are reused across updates while every buffer they captured is the same
@@ -486,7 +488,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             bkey = (ptrs(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, m.grads, m.train_params,
                          m.packed_ft, m.packed_critic, m.sched, m.workspace(rows_local_full), opt.m, opt.v),
                     self.perm_seed, rows_local_full, self.reward_horizon, l2_def, split, defer,
-                    self.max_grad_norm is None, m.dims.ft_denoising_steps, m.precision, fuse, fuse_actor)
+                    self.max_grad_norm is None, m.dims.ft_denoising_steps, m.precision, fuse, fuse_actor, clear_actor)
             if getattr(self, "_bound_key", None) != bkey:
                 bound = {"run_mb": m.bind_minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat,
                                                     self.perm_seed, rows_local_full, reward_horizon=self.reward_horizon,
@@ -495,7 +497,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     bound["actor"] = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
                                                     packs={"actor": (m.actor_ft_params, m.packed_ft)},
                                                     defer_sampler_tables=defer, l2_from_pl2=l2_def,
-                                                    fused_pack=fuse_actor, clear_grads=fuse_actor)
+                                                    fused_pack=fuse_actor, clear_grads=clear_actor or fuse_actor)
                     bound["critic"] = opt.bind_range(m.grads, na, ng_all, m.dims, m.precision,
                                                      packs={"critic": (m.critic_params, m.packed_critic)},
                                                      fused_pack=fuse, clear_grads=fuse)
@@ -552,7 +554,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         if dp:
                             ng = m.grads.numel()
                             run_mb(*mb_args, **mb_kw, part=4, metrics=met,   # actor row tiles
-                                   precleared=pre and fuse_actor)
+                                   precleared=pre and (clear_actor or fuse_actor))
                             self._ev_rows.record(stream)
                             with torch.cuda.stream(side):          # bucket 1: critic gradients + metrics
                                 side.wait_event(self._ev_rows)
@@ -567,7 +569,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             stream.wait_event(self._ev_met)
                         else:
                             run_mb(*mb_args, **mb_kw, part=1, metrics=met_p, stream=st_main,
-                                   precleared=pre and fuse_actor)
+                                   precleared=pre and (clear_actor or fuse_actor))
                             if not tagged:
                                 stream.wait_event(ev_c)
                     else:
@@ -613,7 +615,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         if split:
                             ctag = tag
                             ca, cc = clear_next[(k + 1) % 2] if fuse else (None, None)
-                            ca = ca if fuse_actor else None
+                            ca = ca if (clear_actor or fuse_actor) else None
                             step_actor(lr, metrics=met_p, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
                                        stream=st_main, clear=ca)
                             step_critic(lr, metrics=met_p + 8, metrics_out=self._cmet_map[slot].address,   # met[1]

@@ -19,8 +19,10 @@ int dppo_check_dims(const dppo_dims* d, Dims* out);
 // the images of the given networks (either may be null) and the actor's time tables, one launch;
 // defer_sampler_tables: the actor's split-sampler tables are left stale and re-derived by the
 // sampler before its next launch on that image (dppo_refresh_sampler_tables, pack.hip)
+// zero_ptrs / zero_bytes: up to a few byte ranges (4-B aligned, sizes multiples of 4) the launch also zeroes
 int dppo_pack_models(const Dims& D, int precision, const float* actor_params, void* packed_actor,
-                     const float* critic_params, void* packed_critic, hipStream_t s, bool defer_sampler_tables = false);
+                     const float* critic_params, void* packed_critic, hipStream_t s, bool defer_sampler_tables = false,
+                     void* const* zero_ptrs = nullptr, const size_t* zero_bytes = nullptr, int n_zero = 0);
 
 // The pack of one network as per-element stores (DPPO_STEP_FUSED_PACK, update.hip): each job maps
 // the elements [lo, hi) of the network's flat parameters to one image segment

@@ -11,7 +11,7 @@
 // zero-padded fp32 copy; the time-table blocks follow the job blocks.
 #define PACK_MAXJ 24
 struct PackJob {
-    int kind;            // 0 = packed matrix, 1 = fp32 copy with zero padding
+    int kind;            // 0 = packed matrix, 1 = fp32 copy with zero padding, 2 = zero n 4-byte words
     int K, N, transposed;
     int k_split, k_skip; // source row of packed row k: k < k_split ? k : k + k_skip (row subsets)
     int n, npad;         // copy: valid / padded element counts
@@ -224,6 +224,13 @@ __global__ __launch_bounds__(PACK_THREADS) void pack_all_kernel(PackArgs a) {
         reinterpret_cast<float*>(J.dst)[t] = t < J.n ? W[t] : 0.f;
         return;
     }
+    if (J.kind == 2) {   // words [4t, 4t + 4) of the range
+        uint32_t* q = reinterpret_cast<uint32_t*>(J.dst);
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (4 * t + w < J.n) q[4 * t + w] = 0u;
+        return;
+    }
     const int KS = packed_ksteps(J.K, KG);
     const int lane = t & 63;
     const int ks = (t >> 6) % KS;
@@ -430,9 +437,16 @@ extern "C" int dppo_refresh_sampler_tables(const void* packed, void* stream) {
 }
 
 int dppo_pack_models(const Dims& D, int precision, const float* actor_params, void* packed_actor,
-                     const float* critic_params, void* packed_critic, hipStream_t s, bool defer_sampler_tables) {
+                     const float* critic_params, void* packed_critic, hipStream_t s, bool defer_sampler_tables,
+                     void* const* zero_ptrs, const size_t* zero_bytes, int n_zero) {
     PackArgs a = {};
     int rc;
+    // byte ranges zeroed by the same launch (4-byte words, < 2^33 bytes each): jobs of their own
+    for (int r = 0; r < n_zero; ++r) {
+        if (a.njobs == PACK_MAXJ) return dppo_set_error(DPPO_EINVAL, "pack: too many jobs in one launch");
+        PackJob& J = a.j[a.njobs++];
+        J.kind = 2; J.dst = (uint8_t*)zero_ptrs[r]; J.n = (int)(zero_bytes[r] / 4); J.threads = (J.n + 3) / 4;
+    }
     if (actor_params && packed_actor) {
         const bool defer = defer_sampler_tables && D.TD > 0 && dppo_prec_2b(precision);
         rc = add_mlp_jobs(a, D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS,

@@ -397,16 +397,34 @@ __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __res
     float* da1 = a1 + KF * 2 * TD;      // [KF][2TD]
     float* gs = stage_g ? da1 + KF * 2 * TD : nullptr;   // [KF][H] copy of G when it fits
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (gs) {
-#pragma unroll 8
-        for (int i = tid; i < KF * H; i += TB_THREADS) gs[i] = gseg[i];
+    // Staging: every global load of a chunk is issued before its first LDS store, so the phase pays
+    // one load latency per chunk (one chunk at hopper's sizes) instead of one per array (separate
+    // load-then-store loops waited out four round trips in a row)
+    {
+        constexpr int U = 8;
+        const int ng = gs ? KF * H : 0, nw = TD * H, nt = TD * 2 * TD;
+        const float* wsrc = prm + F.in_w + (size_t)XD * H;
+        for (int base = 0; base < ng || base < nw || base < nt; base += U * TB_THREADS) {
+            float rg[U], rw[U], r1[U], r2[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = base + u * TB_THREADS + tid;
+                rg[u] = i < ng ? gseg[i] : 0.f;
+                rw[u] = i < nw ? wsrc[i] : 0.f;
+                r1[u] = i < nt ? prm[F.time_w1 + i] : 0.f;
+                r2[u] = i < nt ? prm[F.time_w2 + i] : 0.f;
+            }
+            const float rb = base == 0 && tid < 2 * TD ? prm[F.time_b1 + tid] : 0.f;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = base + u * TB_THREADS + tid;
+                if (i < ng) gs[i] = rg[u];
+                if (i < nw) win[i] = rw[u];
+                if (i < nt) { w1[i] = r1[u]; w2[i] = r2[u]; }
+            }
+            if (base == 0 && tid < 2 * TD) b1[tid] = rb;
+        }
     }
-    // (loops with global loads are unrolled so their loads issue together: a runtime-bound loop
-    // otherwise waits out one load latency per iteration)
-#pragma unroll 8
-    for (int i = tid; i < TD * H; i += TB_THREADS) win[i] = prm[F.in_w + (size_t)XD * H + i];
-    for (int i = tid; i < TD * 2 * TD; i += TB_THREADS) { w1[i] = prm[F.time_w1 + i]; w2[i] = prm[F.time_w2 + i]; }
-    for (int i = tid; i < 2 * TD; i += TB_THREADS) b1[i] = prm[F.time_b1 + i];
     const int half = TD / 2;
     const float lnf = logf(10000.f) / (float)(half - 1);
     for (int i = tid; i < KF * TD; i += TB_THREADS) {
@@ -983,7 +1001,7 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
     const bool one_critic = packed_critic && !packed_actor && critic_params == params && n == (int64_t)FC.count;
     const int R = D.K;
     const size_t lds_max = sizeof(float) * ((size_t)3 * R * D.TD + (FA.in_w - FA.time_w1) + (size_t)D.H * D.XD);
-    if ((fuse || clear_g) && (one_actor || one_critic) && (!one_actor || lds_max <= 64 * 1024) && n > 0) {
+    if (fuse && (one_actor || one_critic) && (!one_actor || lds_max <= 64 * 1024) && n > 0) {
         const bool two = dppo_prec_2b(precision);
         StepFuse f = {};
         for (int r = 0; r < 2; ++r) f.own[r][0] = f.own[r][1] = f.keep[r][0] = f.keep[r][1] = -1;
@@ -1043,28 +1061,32 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
             hipLaunchKernelGGL((adamw_fused_kernel<float, 16, 4>), dim3(blocks), dim3(256), lds, s, params, grads, m, v,
                                n, h, metrics, mout, n_metrics, metrics_tag, vt, f);
         DPPO_HIP(hipGetLastError());
-        if (!fuse) return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s, defer);
         return one_actor && two ? dppo_mark_tables_stale(D, precision, actor_params, packed_actor) : DPPO_OK;
     }
-    // the launch-per-stage form (any ranges and images): AdamW, the pack, then the clears
+    // the launch-per-stage form (any ranges and images): AdamW, then the pack, which also zeroes the
+    // gradients AdamW has read (DPPO_STEP_CLEAR_GRADS) and the caller's ranges
     rc = launch_adamw(params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode, metrics, mout,
                       n_metrics, metrics_tag, s, vt);
     if (rc) return rc;
-    rc = dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s, defer);
-    if (rc || (!clear_g && n_clear == 0)) return rc;
-    ZeroArgs z = {};
+    void* zp[5];
+    size_t zb[5];
     int nz = 0;
-    if (clear_g && n > 0) { z.p[0] = grads; z.n[0] = (size_t)n * sizeof(float); nz = 1; }
-    for (int r = 0; r < n_clear; ++r) {
-        if (nz == 4) {
-            hipLaunchKernelGGL(zero_kernel, dim3(16), dim3(256), 0, s, z);
-            DPPO_HIP(hipGetLastError());
-            z = ZeroArgs{};
-            nz = 0;
+    if (clear_g && n > 0) { zp[nz] = grads; zb[nz] = (size_t)n * sizeof(float); ++nz; }
+    for (int r = 0; r < n_clear; ++r) { zp[nz] = clear_ptrs[r]; zb[nz] = clear_bytes[r]; ++nz; }
+    for (int r = 0; r < nz; ++r)
+        DPPO_CHECK(zb[r] / 4 < ((size_t)1 << 31), "dppo_optimizer_step_ex: clear range %d too large", r);
+    if (packed_actor || packed_critic)
+        return dppo_pack_models(D, precision, actor_params, packed_actor, critic_params, packed_critic, s, defer, zp, zb, nz);
+    if (nz) {   // no image to pack: the clears alone
+        ZeroArgs z = {};
+        for (int r = 0; r < nz; ++r) {
+            if (r == 4) {
+                hipLaunchKernelGGL(zero_kernel, dim3(16), dim3(256), 0, s, z);
+                DPPO_HIP(hipGetLastError());
+                z = ZeroArgs{};
+            }
+            z.p[r % 4] = zp[r]; z.n[r % 4] = zb[r];
         }
-        z.p[nz] = clear_ptrs[r]; z.n[nz] = clear_bytes[r]; ++nz;
-    }
-    if (nz) {
         DppoKtScope kt(KT_ZERO, s);
         hipLaunchKernelGGL(zero_kernel, dim3(16), dim3(256), 0, s, z);
         DPPO_HIP(hipGetLastError());

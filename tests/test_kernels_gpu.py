@@ -528,12 +528,14 @@ def test_l2_deferred_minibatch_and_step(cuda, precision):
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("net", ["actor", "actor_l2v", "critic"])
-def test_fused_optimizer_step_matches_two_launches(cuda, precision, net):
+@pytest.mark.parametrize("variant", ["fused", "clear"])
+def test_fused_optimizer_step_matches_two_launches(cuda, precision, net, variant):
     """ABI 11: an optimizer step with DPPO_STEP_FUSED_PACK | DPPO_STEP_CLEAR_GRADS (one launch: AdamW,
     each element's image slots, then the last workgroup's W_OUT / T_OUT slots, TEMB rows and clears)
-    gives bit-identical parameters, moments and image bytes to AdamW + the pack (two launches), zeroes
-    the range's gradients and the given byte ranges, and leaves its ticket counter reusable (three
-    steps in a row on one stream)."""
+    — or DPPO_STEP_CLEAR_GRADS alone (the clears ride on the pack launch) — gives bit-identical
+    parameters, moments and image bytes to AdamW + the pack (two launches), zeroes the range's
+    gradients and the given byte ranges, and leaves its ticket counter reusable (three steps in a
+    row on one stream)."""
     import torch
     from diffusionpolicyoptimization_amd import ops
     from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
@@ -564,7 +566,7 @@ def test_fused_optimizer_step_matches_two_launches(cuda, precision, net):
         packs = (P, img, None, None) if actor else (None, None, P, img)
         step = ops.BoundOptimizerStep(d, m.precision, P, G, M, V, 0.004, 0.9, 0.999, 1e-7, "keras", *packs,
                                       defer_sampler_tables=actor, l2_from_pl2=net == "actor_l2v",
-                                      fused_pack=fused, clear_grads=fused)
+                                      fused_pack=fused and variant == "fused", clear_grads=fused)
         clear = None
         if fused:   # three byte ranges of a scratch buffer, as dppo_ppo_clear_ranges would give
             clear = type("C", (), {})()
