@@ -466,8 +466,11 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # AdamW launch forms it (DPPO_PPO_L2_DEFERRED + DPPO_STEP_L2_FROM_PL2): one launch fewer
             # per minibatch. The factored form is linear, so the data-parallel all-reduce is unchanged.
             # Not with per-tensor gradient clipping (it needs the tensor) or a test hook reading grads.
+            fuse_mode = os.environ.get("DPPO_FUSED_STEP", "critic")   # "0" | "critic" | "all" (A/B knob)
+            # the fused actor step packs W_out per element, so its l2 gradient arrives materialised
+            # (time_bwd and l2_back then share one launch after the actor's dW)
             l2_def = (self.max_grad_norm is None and self.minibatch_hook is None
-                      and os.environ.get("DPPO_L2_DEFER", "1") != "0")
+                      and os.environ.get("DPPO_L2_DEFER", "1") != "0" and not (split and fuse_mode == "all"))
             # ABI 11: the critic's optimizer step is one launch (AdamW storing the image slots;
             # DPPO_STEP_FUSED_PACK) that also zeroes what the critic's next half would zero first
             # (its gradients, metric slot and workspace accumulators: DPPO_STEP_CLEAR_GRADS +
@@ -475,7 +478,6 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # minibatch on the side stream. The actor's half the same way ("all") measured slower:
             # with the virtual l2 gradient its last workgroup's W_out work is serial.
             # Not with a test hook reading the gradients (they are zero after the step).
-            fuse_mode = os.environ.get("DPPO_FUSED_STEP", "critic")   # "0" | "critic" | "all" (A/B knob)
             fuse = split and self.minibatch_hook is None and fuse_mode != "0"
             fuse_actor = fuse and fuse_mode == "all"
             # the actor's step (AdamW + pack) clears the actor's accumulators in its pack launch

@@ -330,7 +330,7 @@ __device__ inline float packed_elem(const uint8_t* img, int K, int k, int n, int
 constexpr int L2B_ROWS = 4;   // rows h of dW_l2 per workgroup
 constexpr int L2B_MAXN = 32;
 template <int NJ, int NQ>
-__device__ inline void l2_back_cols(const L2Back& a, int b) {
+__device__ inline void l2_back_cols(const L2Back& a, int b, int t, int nt) {
     const int H = a.H;
     const int h0 = L2B_ROWS * b;
     float pv[L2B_ROWS + 1][NQ];   // the workgroup's pl2 rows, then (workgroup 0) db_out
@@ -342,7 +342,7 @@ __device__ inline void l2_back_cols(const L2Back& a, int b) {
     for (int q = 0; q < NQ; ++q) pv[L2B_ROWS][q] = (b == 0 && q < a.N) ? a.gob[q] : 0.f;
 #pragma unroll
     for (int c = 0; c < NJ; ++c) {
-        const int j = threadIdx.x + c * (int)blockDim.x;
+        const int j = t + c * nt;
         if (j >= H) continue;
         float w[NQ];
 #pragma unroll
@@ -361,18 +361,20 @@ __device__ inline void l2_back_cols(const L2Back& a, int b) {
     }
 }
 template <int NQ>
-__device__ inline void l2_back_n(const L2Back& a, int b) {
-    if (a.H <= 256) l2_back_cols<1, NQ>(a, b);
-    else l2_back_cols<2, NQ>(a, b);
+__device__ inline void l2_back_n(const L2Back& a, int b, int t) {   // 256 threads per row group b
+    if (a.H <= 256) l2_back_cols<1, NQ>(a, b, t, 256);
+    else l2_back_cols<2, NQ>(a, b, t, 256);
+}
+__device__ inline void l2_back_rows(const L2Back& a, int b, int t) {
+    switch (a.N) {     // the action-chunk widths of the cfgs (hopper 12; walker2d / halfcheetah 24), the critic's 1
+        case 1: l2_back_n<1>(a, b, t); break;
+        case 12: l2_back_n<12>(a, b, t); break;
+        case 24: l2_back_n<24>(a, b, t); break;
+        default: l2_back_n<L2B_MAXN>(a, b, t); break;   // any N <= 32, zero-padded
+    }
 }
 __global__ __launch_bounds__(256) void l2_back_kernel(L2Back a) {
-    const int b = (int)blockIdx.x;
-    switch (a.N) {     // the action-chunk widths of the cfgs (hopper 12; walker2d / halfcheetah 24), the critic's 1
-        case 1: l2_back_n<1>(a, b); break;
-        case 12: l2_back_n<12>(a, b); break;
-        case 24: l2_back_n<24>(a, b); break;
-        default: l2_back_n<L2B_MAXN>(a, b); break;   // any N <= 32, zero-padded
-    }
+    l2_back_rows(a, (int)blockIdx.x, (int)threadIdx.x);
     if (a.zcnt) {   // the critic's row tiles and dW (earlier on this stream) were the counts' last readers
         const int nz = *a.zn;
         for (int r = (int)(blockIdx.x * blockDim.x + threadIdx.x); r < nz; r += (int)(gridDim.x * blockDim.x))
@@ -383,10 +385,9 @@ __global__ __launch_bounds__(256) void l2_back_kernel(L2Back a) {
 // One workgroup; every parameter it reads (the TD temb rows of W_in and the time MLP) is staged into
 // LDS in one batch of coalesced loads at the start, so the dependent phases below run from LDS and
 // the kernel pays global-load latency about twice (staging, then G) instead of once per phase.
-__global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __restrict__ gseg, const float* __restrict__ prm,
-                                                       float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF,
-                                                       int TS, int stage_g) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
+__device__ inline void time_bwd_body(const float* __restrict__ gseg, const float* __restrict__ prm,
+                                     float* __restrict__ grad, const FlatOffsets& F, int XD, int TD, int H, int KF, int TS,
+                                     int stage_g, float* sm) {
     float* win = sm;                    // [TD][H]   W_in rows XD .. XD+TD-1
     float* w1 = win + TD * H;           // [TD][2TD]
     float* b1 = w1 + TD * 2 * TD;       // [2TD]
@@ -496,6 +497,28 @@ __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __res
         for (int q = 0; q < KF; ++q) s += da1[q * 2 * TD + h];
         grad[F.time_b1 + h] = s;
     }
+}
+
+__global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __restrict__ gseg, const float* __restrict__ prm,
+                                                       float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF,
+                                                       int TS, int stage_g) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    time_bwd_body(gseg, prm, grad, F, XD, TD, H, KF, TS, stage_g, sm);
+}
+// time_bwd and the actor's l2_back in one launch (both follow the actor's dW and are independent of
+// each other): workgroup 0 runs the time-MLP backward, the others l2_back's row groups, TB_THREADS /
+// 256 per workgroup
+__global__ __launch_bounds__(TB_THREADS) void time_l2_bwd_kernel(const float* __restrict__ gseg,
+                                                          const float* __restrict__ prm, float* __restrict__ grad,
+                                                          FlatOffsets F, int XD, int TD, int H, int KF, int TS,
+                                                          int stage_g, L2Back l2b, int l2_groups) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    if (blockIdx.x == 0) {
+        time_bwd_body(gseg, prm, grad, F, XD, TD, H, KF, TS, stage_g, sm);
+        return;
+    }
+    const int grp = ((int)blockIdx.x - 1) * (TB_THREADS / 256) + (int)threadIdx.x / 256;
+    if (grp < l2_groups) l2_back_rows(l2b, grp, (int)threadIdx.x % 256);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1299,24 +1322,22 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
                   D.XD, precision, nullptr, nullptr, nullptr};
     DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
     // (time_bwd forked onto a side stream beside l2_back measured slower: 0.428 vs 0.406 ms per
-    // minibatch, same box, tools/r03_ab2.sh)
-    if (l2_back) {
-        DppoKtScope kt(KT_L2_BACK, s);
-        hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
-        DPPO_HIP(hipGetLastError());
-    }
+    // minibatch, same box, tools/r03_ab2.sh; since r04 the two share one launch instead)
     size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
                                   (size_t)nb * (2 * D.TD + 2 * 2 * D.TD));
     DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
     const int stage_g = tsm + sizeof(float) * (size_t)nb * D.H <= 160 * 1024;
     if (stage_g) tsm += sizeof(float) * (size_t)nb * D.H;
-    if (tsm > 64 * 1024) {
-        static bool attr = false;   // opt in to more than 64 KB of dynamic LDS once
-        if (!attr) {
-            DPPO_HIP(hipFuncSetAttribute((const void*)time_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            attr = true;
-        }
+    if (l2_back) {
+        const int groups = dppo_cdiv(D.H, L2B_ROWS), per = TB_THREADS / 256;
+        { const int rc_ = dppo_func_lds((const void*)time_l2_bwd_kernel, tsm); if (rc_) return rc_; }
+        DppoKtScope kt(KT_TIME_BWD, s);
+        hipLaunchKernelGGL(time_l2_bwd_kernel, dim3(1 + dppo_cdiv(groups, per)), dim3(TB_THREADS), tsm, s, gseg,
+                           actor_params, ga, FA, D.XD, D.TD, D.H, nb, TS, stage_g, l2b, groups);
+        DPPO_HIP(hipGetLastError());
+        return DPPO_OK;
     }
+    { const int rc_ = dppo_func_lds((const void*)time_bwd_kernel, tsm); if (rc_) return rc_; }
     DppoKtScope kt(KT_TIME_BWD, s);
     hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD, D.TD, D.H,
                        nb, TS, stage_g);
