@@ -467,10 +467,14 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # per minibatch. The factored form is linear, so the data-parallel all-reduce is unchanged.
             # Not with per-tensor gradient clipping (it needs the tensor) or a test hook reading grads.
             fuse_mode = os.environ.get("DPPO_FUSED_STEP", "critic")   # "0" | "critic" | "all" (A/B knob)
-            # the fused actor step packs W_out per element, so its l2 gradient arrives materialised
-            # (time_bwd and l2_back then share one launch after the actor's dW)
-            l2_def = (self.max_grad_norm is None and self.minibatch_hook is None
-                      and os.environ.get("DPPO_L2_DEFER", "1") != "0" and not (split and fuse_mode == "all"))
+            # DPPO_L2_DEFER = "auto" (default) | "1" | "0". Materialised (time_bwd and l2_back share one
+            # launch after the actor's dW), the actor's AdamW reads plain gradients; deferred, it saves
+            # that l2_back work but forms dW_l2 per element. Same-box A/Bs (profiles/r04l_tail_ab.txt):
+            # deferred 0.5 % faster at 50,000-row minibatches, materialised 4 % faster at an 8-GPU
+            # rank's 6,250 rows. The fused actor step (fuse_mode "all") needs it materialised.
+            l2_mode = os.environ.get("DPPO_L2_DEFER", "auto")
+            l2_def = (self.max_grad_norm is None and self.minibatch_hook is None and l2_mode != "0"
+                      and not (split and fuse_mode == "all") and (l2_mode == "1" or rows_local_full >= 16384))
             # ABI 11: the critic's optimizer step is one launch (AdamW storing the image slots;
             # DPPO_STEP_FUSED_PACK) that also zeroes what the critic's next half would zero first
             # (its gradients, metric slot and workspace accumulators: DPPO_STEP_CLEAR_GRADS +

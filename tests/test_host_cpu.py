@@ -75,6 +75,34 @@ def test_host_queries_match_python_layout(lib):
     assert lib.dppo_reward_scale_workspace_doubles(500, 64) > 0
 
 
+def test_ppo_clear_ranges_are_what_each_part_zeroes(lib):
+    """ABI 11: dppo_ppo_clear_ranges (host-side address arithmetic, no device work) reports the
+    non-gradient ranges a minibatch part zeroes: the actor (part 1 / 4) metrics 0 and 2..15 and its
+    workspace accumulators, the critic (part 2) metric 1 and its own; all inside the workspace or the
+    metrics buffer, 4-B aligned, disjoint between the halves."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    d = ops.ModelDims()
+    rows = 6250
+    ws = torch.empty(ops._workspace_bytes(d, 1, rows), dtype=torch.uint8)
+    met = torch.zeros(16, dtype=torch.float64)
+    w0, w1, m0 = ws.data_ptr(), ws.data_ptr() + ws.numel(), met.data_ptr()
+    got = {p: ops.ClearRanges(d, "bf16", rows, ws, met, p).ranges() for p in (1, 2, 3, 4)}
+    assert got[1] == got[4] and len(got[1]) == 3 and len(got[2]) == 2 and len(got[3]) == 3
+    assert got[1][:2] == [(m0, 8), (m0 + 16, 112)] and got[2][0] == (m0 + 8, 8)
+    assert got[3][0] == (m0, 128)
+    spans = []
+    for p in (1, 2):
+        for a, n in got[p]:
+            assert a % 4 == 0 and n % 4 == 0 and n > 0
+            assert (m0 <= a and a + n <= m0 + 128) or (w0 <= a and a + n <= w1)
+            spans.append((a, a + n))
+    spans.sort()
+    assert all(e <= s for (_, e), (s, _) in zip(spans, spans[1:]))   # actor and critic ranges disjoint
+    with pytest.raises(Exception):
+        ops.ClearRanges(d, "bf16", rows, ws, met, 5)
+
+
 @pytest.mark.parametrize("field,value,msg", [("actor_hidden", 100, "actor_hidden"), ("time_dim", 3, "time_dim"),
                                              ("ft_denoising_steps", 30, "ft_denoising_steps"),
                                              ("action_dim", 9, "horizon_steps*action_dim")])
