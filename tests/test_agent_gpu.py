@@ -241,7 +241,11 @@ def test_pipelined_rollout_matches_model_call_lowdim(cuda, protocol, threads, mo
         np.testing.assert_array_equal(obs_traj[i].cpu().numpy(), o.reshape(E, -1))
         ref = model(torch.tensor(o.reshape(E, -1), device=cuda), return_chain=True)
         a = ref.trajectories.reshape(E, 4, d.action_dim).cpu().numpy()
-        np.testing.assert_array_equal(got_a[i], a)
+        # (go protocol: the launch writes its actions into the float buffer itself, and launch i + 1,
+        # released by the step's publish, may overwrite it before the test's copy; the observations
+        # and rewards below are the actions' downstream check there)
+        if protocol == "tagged":
+            np.testing.assert_array_equal(got_a[i], a)
         ob, r, _, _, _ = ref_env.step(a)
         o = ob["state"].copy()
         np.testing.assert_array_equal(got_o[i], o)
