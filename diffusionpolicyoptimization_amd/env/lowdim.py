@@ -225,7 +225,8 @@ class GymSimulator(CallbackSimulator):
     """The reference's simulator: gym.make(id) per env with d4rl's locomotion registrations
     (env/gym_utils/__init__.py:125-174), stepped through the callback table. Needs gym, d4rl and
     mujoco_py; raises ImportError when they are missing (they are absent on the MI355X hosts, so
-    this class is written against their documented API and has not run). mujoco_py's step holds the
+    it has not run against MuJoCo: its callback and per-env RNG logic runs in
+    tests/test_envstack_cpu.py over stand-in gym / d4rl modules). mujoco_py's step holds the
     GIL, so these envs step serially on one thread; a MuJoCo C-API simulator filling the same
     callback table (one mjData per env) is the intended multi-threaded filler.
 

@@ -135,6 +135,77 @@ def test_multistep_timelimit_branch_through_python_callbacks():
     assert n_trunc > 0 and n_term > 0
 
 
+class _GlobalRngEnv:
+    """A gym-API env (seed / reset / step -> (obs, reward, done, info)) that draws its noise from the
+    process-global NumPy RNG, as the reference's wrapper seeds it (one process per env:
+    wrapper/mujoco_locomotion_lowdim.py:39-43); rs: its own RandomState instead (the oracle's
+    one-process-per-env stream)."""
+
+    def __init__(self, rs=None, limit=6):
+        self.rs, self.limit, self.t, self.s = rs, limit, 0, np.zeros(5)
+
+    def _r(self):
+        return self.rs if self.rs is not None else np.random
+
+    def seed(self, s):
+        self.seeded = s
+
+    def reset(self):
+        self.t = 0
+        self.s = 0.5 * self._r().normal(size=5)
+        return self.s.copy()
+
+    def step(self, a):
+        a = np.asarray(a, np.float64)
+        self.t += 1
+        self.s = 0.9 * self.s + 0.1 * np.concatenate([a, a])[:5] + 0.05 * self._r().normal(size=5)
+        done = bool(abs(self.s[0]) > 1.0)
+        info = {}
+        if self.t >= self.limit:
+            info["TimeLimit.truncated"] = not done
+            done = True
+        return self.s.copy(), float(self.s.sum()), done, info
+
+
+def test_gym_simulator_keeps_one_global_rng_stream_per_env(monkeypatch):
+    """GymSimulator (env/lowdim.py) over stand-in gym / d4rl modules (the real ones need MuJoCo):
+    envs that draw from the global NumPy RNG step through the callback table and the batched
+    wrapper stack exactly like one process per env seeded with np.random.seed(seed_i) — each env's
+    global-RNG state is swapped in around its calls — and the caller's own global RNG state is left
+    untouched."""
+    import sys
+    import types
+
+    from diffusionpolicyoptimization_amd.env.lowdim import GymSimulator, LowdimVecEnv
+    made = []
+    gym = types.ModuleType("gym")
+    gym.make = lambda env_id: made.append(env_id) or _GlobalRngEnv()
+    d4rl = types.ModuleType("d4rl")
+    d4rl.gym_mujoco = types.ModuleType("d4rl.gym_mujoco")
+    monkeypatch.setitem(sys.modules, "gym", gym)
+    monkeypatch.setitem(sys.modules, "d4rl", d4rl)
+    monkeypatch.setitem(sys.modules, "d4rl.gym_mujoco", d4rl.gym_mujoco)
+    E, Ta = 4, 4
+    seeds = [7 + 3 * i for i in range(E)]
+    sim = GymSimulator("hopper-medium-v2", E, 5, 3)
+    assert made == ["hopper-medium-v2"] * E
+    sim.seed(seeds)
+    assert [e.seeded for e in sim.envs] == seeds
+    norm = {"obs_min": -2 * np.ones(5, np.float32), "obs_max": 2 * np.ones(5, np.float32),
+            "action_min": -np.ones(3, np.float32), "action_max": np.ones(3, np.float32)}
+    venv = LowdimVecEnv(sim, E, 5, 3, act_steps=Ta, n_obs_steps=1, max_episode_steps=1000,
+                        reset_within_step=True, normalization=norm)
+    oracle_envs = [MultiStepOracle(LowdimWrapperOracle(_GlobalRngEnv(np.random.RandomState(s)), norm), n_obs_steps=1,
+                                   n_action_steps=Ta, max_episode_steps=1000, reset_within_step=True)
+                   for s in seeds]
+    np.random.seed(12345)
+    outer = np.random.get_state()
+    n_term, n_trunc, _ = _compare(venv, oracle_envs, E, Ta, 12, np.random.default_rng(3))
+    after = np.random.get_state()
+    assert after[0] == outer[0] and np.array_equal(after[1], outer[1]) and after[2:] == outer[2:]
+    assert n_term + n_trunc > 0
+
+
 def test_callback_errors_surface():
     from diffusionpolicyoptimization_amd.env.lowdim import CallbackSimulator, LowdimVecEnv
 
