@@ -275,6 +275,26 @@ def test_data_parallel_agent_two_ranks_share_one_gpu(tmp_path, overrides):
     assert "replicas_identical=True" in out.stdout
 
 
+def test_rccl_runs_the_update_bucket_pattern(cuda):
+    """RCCL ("nccl") on the one-GPU box: a world-size-1 process group all-reduces the agent's two
+    gradient buckets from the two streams the split update issues them on (tools/rccl_probe.py);
+    the results are the inputs (a sum over one rank). Multi-rank RCCL needs more than one GPU."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(ROOT, "tools", "rccl_probe.py")],
+                         env=dict(os.environ), capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    res = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["backend"] == "nccl" and res["world"] == 1 and res["result_ok"], res
+
+
 def test_data_parallel_update_equals_single_rank_on_the_union(cuda, tmp_path):
     """SURVEY §8(e) on the HIP path: 2 ranks (gloo, both on cuda:0), reference batch semantics
     (dp_scale_batch = false: the GLOBAL minibatch is batch_size rows, batch_size / 2 drawn by each
