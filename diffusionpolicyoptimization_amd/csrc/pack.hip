@@ -21,7 +21,7 @@ struct PackJob {
 };
 // the actor's time tables: blocks [0, R) TEMB rows; with 2-byte operands also blocks [R, 2R) TIN
 // rows and block 2R B_OUT2 (tables = 2R + 1, else R); and nfold blocks of FOLD / ROUT fragments (one
-// 16-feature tile each), which the launch runs first
+// 16-feature tile each). Launch order: fold blocks, table blocks, then the element jobs
 struct TembArgs {
     const float* params;
     FlatOffsets F;
@@ -34,7 +34,7 @@ struct PackArgs {
     PackJob j[PACK_MAXJ];
     int start[PACK_MAXJ + 1];
     int njobs;
-    int pack_blocks;     // blocks of the job part (256 threads each); time-table blocks follow
+    int pack_blocks;     // blocks of the job part (256 threads each), after the time-table blocks
     TembArgs tb;
 };
 
@@ -209,10 +209,13 @@ __global__ __launch_bounds__(PACK_THREADS) void pack_all_kernel(PackArgs a) {
         return;
     }
     blk -= a.tb.nfold;
-    if (blk >= a.pack_blocks) {
-        time_table_block<ET>(a.tb, a.tb.first_table + blk - a.pack_blocks);
+    // the time-table blocks next (each a chain of dependent global round trips: the launch's long
+    // pole), then the element jobs, which are one round trip each
+    if (blk < a.tb.tables) {
+        time_table_block<ET>(a.tb, a.tb.first_table + blk);
         return;
     }
+    blk -= a.tb.tables;
     const int gid = blk * blockDim.x + threadIdx.x;
     if (gid >= a.start[a.njobs]) return;
     int ji = 0;
