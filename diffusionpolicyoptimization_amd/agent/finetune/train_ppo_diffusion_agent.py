@@ -453,7 +453,9 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             defer = os.environ.get("DPPO_DEFER_TABLES", "1") != "0"   # A/B knob (measurement)
             if split:
                 if getattr(self, "_side", None) is None:
-                    self._side = torch.cuda.Stream(device=self.device)
+                    # DPPO_SIDE_PRIORITY (measurement knob): the side stream's priority (negative = higher)
+                    self._side = torch.cuda.Stream(device=self.device,
+                                                   priority=int(os.environ.get("DPPO_SIDE_PRIORITY", "0")))
                     self._met_dev = [torch.zeros(16, dtype=torch.float64, device=self.device) for _ in range(2)]
                     self._ev_rows = torch.cuda.Event()
                     self._ev_met = torch.cuda.Event()
