@@ -869,9 +869,12 @@ static int dispatch_critic(const CriticArgs& a, hipStream_t s) {
     return dppo_set_error(DPPO_EUNSUPPORTED, "critic: hidden %d not instantiated", a.HC);
 }
 
+#ifndef DPPO_CRITIC_MT
+#define DPPO_CRITIC_MT 2   // 16-row MFMA tiles per critic row tile (measurement knob of tuning builds)
+#endif
 int launch_critic_rowtile(const CriticArgs& a, int precision, hipStream_t s) {
-    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, 2, 8, true>(a, s)
-         : precision == DPPO_F16  ? dispatch_critic<PolicyF16, 2, 8, true>(a, s)
+    return precision == DPPO_BF16 ? dispatch_critic<PolicyBF16, DPPO_CRITIC_MT, 8, true>(a, s)
+         : precision == DPPO_F16  ? dispatch_critic<PolicyF16, DPPO_CRITIC_MT, 8, true>(a, s)
                                   : dispatch_critic<PolicyF32, 2, 8, true>(a, s);
 }
 
