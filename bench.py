@@ -153,7 +153,7 @@ def kernel_stats_csv(path=KERNEL_STATS_CSV):
                 base = "critic_rowtile_train" if "true" in k else "critic_rowtile_forward"
             elif base == "adv_stats_all_kernel":
                 base = "adv_stats_kernel"
-            elif base == "adamw_fused_kernel":
+            elif "adamw_fused_kernel" in base:   # (rocprof leaves this template's name mangled)
                 base = "adamw_kernel"
             tot, calls = float(r["TotalDurationNs"]) / 1e6, int(r["Calls"])
             t0, c0 = out.get(base, (0.0, 0))
