@@ -165,7 +165,7 @@ __device__ inline int xcc_id() {
 __device__ inline int slot_feature(int j, int e) { return e < 4 ? 4 * j + e : 16 + 4 * j + (e - 4); }
 
 
-// tuning knobs of the P = 4 kernel (tools/split_variant.sh + tools/ab_variants.sh)
+// tuning knobs of the split kernel (tools/variant_build.sh <tag> "-D..." + tools/ab_variants.sh)
 #ifndef DPPO_S4_L1D
 #define DPPO_S4_L1D 4        // l1: u1 fragment reads kept in flight ahead of the MFMA chain
 #endif
