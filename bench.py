@@ -21,7 +21,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec + PPO-updates/sec, hopper-v2 64 envs 20 DDPM steps, 1/2/4/8 GPU"
-PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md chip table
+PEAK = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md chip table
 HBM_PEAK_GBS = 8000.0
 
 
@@ -63,7 +63,7 @@ def sampler_stream_bytes_per_tile(d, precision):
 
     from diffusionpolicyoptimization_amd import _lib
     out, waves = ctypes.c_int64(), ctypes.c_int()
-    _lib.call("dppo_sampler_stream_bytes", ctypes.byref(d.c()), 1 if precision == "bf16" else 0,
+    _lib.call("dppo_sampler_stream_bytes", ctypes.byref(d.c()), _lib.PRECISION[precision],
               ctypes.byref(out), ctypes.byref(waves))
     return out.value
 
@@ -79,6 +79,7 @@ def cpu_baseline(cfg, n_envs, S, bs):
 
     from oracle import cpu_reference as C
     threads = torch.get_num_threads()
+    omp = os.environ.get("OMP_NUM_THREADS")
     kw = dict(obs_dim=cfg.obs_dim, action_dim=cfg.action_dim)
     upd = int(cfg.train.update_epochs)
     t_full, br = C.time_iteration(n_envs, S, bs, upd, **kw)
@@ -95,6 +96,10 @@ def cpu_baseline(cfg, n_envs, S, bs):
             "value_1thread": env_steps / t1_iter,
             "ppo_updates_per_sec": n_mb / br["update_s"] if br["update_s"] > 0 else None,
             "seconds_per_iter": t_full, "breakdown_s": {k: br[k] for k in ("rollout_s", "passes_s", "update_s")},
+            "cores_note": (f"{threads} threads = torch's pool, which follows OMP_NUM_THREADS={omp}: the CPU share the GPU "
+                           "box gives one GPU's job (the harness sets it to 16 per GPU and its process guard limits "
+                           "the job's CPU use; nproc / os.cpu_count() show the whole host, "
+                           f"{C.physical_cores()} physical cores, shared with the other GPUs' jobs)"),
             "sample": (f"oracle/cpu_reference.py (fp32 torch-CPU, autograd) timed on ONE full iteration: {n_envs} "
                        f"envs x {S} chunks, K={cfg.denoising_steps}, {n_mb} minibatches of {bs} rows, "
                        f"{threads} threads, {t_full:.1f} s; value_1thread from {s1} chunks + 1 full minibatch "
@@ -420,8 +425,8 @@ def main():
         "rollout_s_per_iter": t_roll / args.steps, "update_s_per_iter": t_upd / args.steps,
         "sampler_bound": bound,
         "roofline": {"bound": "mfma", "kernel": kname + " (K-step DDPM sampler, all layers fused)",
-                     "achieved": achieved, "peak": PEAK["bf16" if prec == "bf16" else "fp32"], "unit": "TFLOP/s",
-                     "frac": achieved / PEAK["bf16" if prec == "bf16" else "fp32"], "traffic": traffic,
+                     "achieved": achieved, "peak": PEAK[prec], "unit": "TFLOP/s",
+                     "frac": achieved / PEAK[prec], "traffic": traffic,
                      "avg_launch_ms": samp_ms, "flops_per_launch": flops, "burst_launches": n_burst,
                      "in_loop_event_ms": loop_samp_ms if agent.sampler_events else None,
                      "note": ("M = envs/GPU rows per GEMM: at 64 envs the sampler is a dependent chain of "

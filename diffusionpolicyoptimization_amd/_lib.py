@@ -22,6 +22,7 @@ DPPO_PPO_LEARN_ETA = 2                   # (ABI 9) d loss / d eta into metrics[8
 DPPO_STEP_FUSED_PACK = 0x400             # (ABI 11) AdamW + the image in one launch
 DPPO_STEP_CLEAR_GRADS = 0x800            # (ABI 11) the step zeroes the range's gradients after reading
 DPPO_PPO_PRECLEARED = 4                  # (ABI 11) the part's accumulators are already zero
+DPPO_PPO_TIME_BWD_IN_STEP = 8            # (ABI 12) the actor's time-MLP backward runs in dppo_actor_step
 SCHED_COLS = 8
 PRECISION = {"fp32": DPPO_F32, "f32": DPPO_F32, "bf16": DPPO_BF16, "fp16": DPPO_F16, "f16": DPPO_F16}
 
@@ -81,6 +82,9 @@ _SIGNATURES = {
     "dppo_reward_scale": (_I, [_P, _P, _P, _P, _P, _I, _I, _D, _D, _D, _P]),
     "dppo_reward_scale_moments": (_I, [_P, _P, _P, _P, _P, _I, _I, _D, _P]),
     "dppo_reward_scale_apply": (_I, [_P, _P, _I, _I, _D, _D, _P]),
+    "dppo_reward_scale_per_env": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _D, _D, _D, _P, _P]),
+    "dppo_reward_scale_per_env_moments": (_I, [_P, _P, _P, _P, _P, _I, _I, _D, _P]),
+    "dppo_reward_scale_per_env_apply": (_I, [_P, _P, _I, _I, _I, _D, _D, _P, _P]),
     "dppo_gae": (_I, [_P, _P, _P, _P, _I, _I, _D, _D, _D, _P, _P, _P]),
     "dppo_ppo_workspace_bytes": (_SZ, [_DIMS, _I, _I]),
     "dppo_ppo_adv_stats": (_I, [_P, _I64, _I, _U64, _I, _I64, _I, _P, _P, _P]),
@@ -99,6 +103,8 @@ _SIGNATURES = {
                                  _P, _I, _U64, _P]),
     "dppo_optimizer_step_ex": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P,
                                     _P, _P, _I, _U64, _P, _P, _I, _P]),
+    "dppo_actor_step": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _I, _P, _P, _I, _U64,
+                             _P, _P, _I, _P]),
     "dppo_ppo_clear_ranges": (_I, [_DIMS, _I, _I, _P, _P, _I, _P, _P, ctypes.POINTER(ctypes.c_int)]),
     "dppo_value_moments": (_I, [_P, _P, _I64, _P, _P]),
     "dppo_refresh_sampler_tables": (_I, [_P, _P]),
@@ -110,7 +116,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class DppoError(RuntimeError):

@@ -468,24 +468,28 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # AdamW launch forms it (DPPO_PPO_L2_DEFERRED + DPPO_STEP_L2_FROM_PL2): one launch fewer
             # per minibatch. The factored form is linear, so the data-parallel all-reduce is unchanged.
             # Not with per-tensor gradient clipping (it needs the tensor) or a test hook reading grads.
-            fuse_mode = os.environ.get("DPPO_FUSED_STEP", "critic")   # "0" | "critic" | "all" (A/B knob)
-            # DPPO_L2_DEFER = "auto" (default) | "1" | "0". Materialised (time_bwd and l2_back share one
-            # launch after the actor's dW), the actor's AdamW reads plain gradients; deferred, it saves
-            # that l2_back work but forms dW_l2 per element. Same-box A/Bs (profiles/r04l_tail_ab.txt):
-            # deferred 0.5 % faster at 50,000-row minibatches, materialised 4 % faster at an 8-GPU
-            # rank's 6,250 rows. The fused actor step (fuse_mode "all") needs it materialised.
-            l2_mode = os.environ.get("DPPO_L2_DEFER", "auto")
-            l2_def = (self.max_grad_norm is None and self.minibatch_hook is None and l2_mode != "0"
-                      and not (split and fuse_mode == "all") and (l2_mode == "1" or rows_local_full >= 16384))
-            # ABI 11: the critic's optimizer step is one launch (AdamW storing the image slots;
-            # DPPO_STEP_FUSED_PACK) that also zeroes what the critic's next half would zero first
-            # (its gradients, metric slot and workspace accumulators: DPPO_STEP_CLEAR_GRADS +
-            # ops.ClearRanges), which then runs with DPPO_PPO_PRECLEARED: two launches fewer per
-            # minibatch on the side stream. The actor's half the same way ("all") measured slower:
-            # with the virtual l2 gradient its last workgroup's W_out work is serial.
-            # Not with a test hook reading the gradients (they are zero after the step).
+            # DPPO_FUSED_STEP = "all" (default) | "critic" | "0" (A/B knob). "all": each half's optimizer
+            # step is ONE launch. The actor's (dppo_actor_step, ABI 12) also runs the actor's time-MLP
+            # backward (the minibatch stops after its dW: DPPO_PPO_TIME_BWD_IN_STEP) and forms the l2
+            # gradient from its factored form (DPPO_PPO_L2_DEFERRED), so after the actor's dW the
+            # minibatch chain is that one launch instead of time_bwd -> AdamW -> pack; the TEMB table is
+            # derived by its consumers. The critic's (ABI 11) zeroes what its next half would zero first
+            # (DPPO_STEP_CLEAR_GRADS + ops.ClearRanges; the next half runs DPPO_PPO_PRECLEARED).
+            # "critic": the r04 form (actor: time_bwd in the minibatch, AdamW + pack launches).
+            # Under data parallelism the time-MLP backward stays in the minibatch (its gradients are part
+            # of the all-reduced actor bucket). Not with a test hook reading the gradients (zero after
+            # the step).
+            fuse_mode = os.environ.get("DPPO_FUSED_STEP", "all")
             fuse = split and self.minibatch_hook is None and fuse_mode != "0"
             fuse_actor = fuse and fuse_mode == "all"
+            tb_in_step = fuse_actor and not dp
+            # DPPO_L2_DEFER = "auto" (default) | "1" | "0". Deferred, the actor's step forms dW_l2 per
+            # element from pl2; materialised, an l2_back launch follows the actor's dW. With the one-launch
+            # actor step "auto" always defers; with the r04 step it materialises below 16,384 rows per rank
+            # (profiles/r04l_tail_ab.txt).
+            l2_mode = os.environ.get("DPPO_L2_DEFER", "auto")
+            l2_def = (self.max_grad_norm is None and self.minibatch_hook is None and l2_mode != "0"
+                      and (l2_mode == "1" or fuse_actor or rows_local_full >= 16384))
             # the actor's step (AdamW + pack) clears the actor's accumulators in its pack launch
             clear_actor = fuse and os.environ.get("DPPO_ACTOR_CLEAR", "1") != "0"
             opt = self.actor_optimizer
@@ -496,16 +500,22 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             bkey = (ptrs(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, m.grads, m.train_params,
                          m.packed_ft, m.packed_critic, m.sched, m.workspace(rows_local_full), opt.m, opt.v),
                     self.perm_seed, rows_local_full, self.reward_horizon, l2_def, split, defer,
-                    self.max_grad_norm is None, m.dims.ft_denoising_steps, m.precision, fuse, fuse_actor, clear_actor)
+                    self.max_grad_norm is None, m.dims.ft_denoising_steps, m.precision, fuse, fuse_actor, clear_actor,
+                    tb_in_step)
             if getattr(self, "_bound_key", None) != bkey:
                 bound = {"run_mb": m.bind_minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat,
                                                     self.perm_seed, rows_local_full, reward_horizon=self.reward_horizon,
-                                                    l2_deferred=l2_def)}
+                                                    l2_deferred=l2_def, time_bwd_in_step=tb_in_step)}
                 if split:
-                    bound["actor"] = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
-                                                    packs={"actor": (m.actor_ft_params, m.packed_ft)},
-                                                    defer_sampler_tables=defer, l2_from_pl2=l2_def,
-                                                    fused_pack=fuse_actor, clear_grads=clear_actor or fuse_actor)
+                    if fuse_actor:
+                        bound["actor"] = opt.bind_actor(m.grads, na, m.dims, m.precision, m.packed_ft,
+                                                        workspace=m.workspace(rows_local_full) if tb_in_step else None,
+                                                        batch_rows=rows_local_full, l2_from_pl2=l2_def, clear_grads=True)
+                    else:
+                        bound["actor"] = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
+                                                        packs={"actor": (m.actor_ft_params, m.packed_ft)},
+                                                        defer_sampler_tables=defer, l2_from_pl2=l2_def,
+                                                        clear_grads=clear_actor)
                     bound["critic"] = opt.bind_range(m.grads, na, ng_all, m.dims, m.precision,
                                                      packs={"critic": (m.critic_params, m.packed_critic)},
                                                      fused_pack=fuse, clear_grads=fuse)
@@ -624,8 +634,12 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             ctag = tag
                             ca, cc = clear_next[(k + 1) % 2] if fuse else (None, None)
                             ca = ca if (clear_actor or fuse_actor) else None
-                            step_actor(lr, metrics=met_p, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
-                                       stream=st_main, clear=ca)
+                            if fuse_actor:   # a partial minibatch's workspace layout follows its rows
+                                step_actor(lr, metrics=met_p, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
+                                           stream=st_main, clear=ca, rows=rows)
+                            else:
+                                step_actor(lr, metrics=met_p, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
+                                           stream=st_main, clear=ca)
                             step_critic(lr, metrics=met_p + 8, metrics_out=self._cmet_map[slot].address,   # met[1]
                                         n_metrics=1, metrics_tag=ctag, stream=st_side, clear=cc)
                             cleared = fuse

@@ -38,7 +38,8 @@ constexpr int FUSE_MAXJ = 12;
 // parameters start at element 0 of the step's range; returns the job count (<= FUSE_MAXJ) or -1
 int dppo_fuse_jobs(int in_dim, int hidden, int out_dim, int time_dim, int precision, void* packed, int temb_steps,
                    FuseJob* jobs);
-int dppo_mark_tables_stale(const Dims& D, int precision, const float* actor_params, const void* packed_actor);
+// temb: the TEMB table is stale too (the fused actor step), not only the split-sampler tables
+int dppo_mark_tables_stale(const Dims& D, int precision, const float* actor_params, const void* packed_actor, bool temb);
 
 
 // precision enum values the library implements; the two 2-byte operand policies share layouts

@@ -80,6 +80,7 @@ struct ActorArgs {
     const float* obs;      // [nsamp][SD]
     const float* chains;   // [nsamp][KF+1][XD]
     int XD, SD, TD, IN, H, KF, Da, mode;
+    int TS;                // time stride: row r of the time embeddings is t_emb(r TS)
     int64_t nrows;         // logprob: nsamp*KF; train: rows
     // logprob outputs
     float* lp_elem;

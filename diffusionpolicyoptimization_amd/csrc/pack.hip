@@ -269,15 +269,17 @@ static inline uint8_t* P_out(void* p) { return (uint8_t*)p; }
 
 // the jobs of one MLP image (and, for an actor, its time tables) appended to a
 // PackArgs; returns DPPO_OK or an error code. what: PACK_ALL, PACK_UPDATE (everything but the
-// split sampler's tables: W_XS, FOLD / ROUT, TIN, B_OUT2) or PACK_SAMPLER (those tables only)
-enum { PACK_ALL = 0, PACK_UPDATE = 1, PACK_SAMPLER = 2 };
+// split sampler's tables: W_XS, FOLD / ROUT, TIN, B_OUT2), PACK_SAMPLER (those tables only) or
+// PACK_SAMPLER_TEMB (those tables and the TEMB table: after a fused actor step, any precision)
+enum { PACK_ALL = 0, PACK_UPDATE = 1, PACK_SAMPLER = 2, PACK_SAMPLER_TEMB = 3 };
 static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int time_dim, int precision,
                         const float* params, void* packed, int temb_steps, int time_stride, int what = PACK_ALL) {
     const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision, temb_steps);
     const FlatOffsets F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
     const int KG = dppo_prec_2b(precision) ? 32 : 16;
     const bool split_tables = time_dim > 0 && L.temb_steps > 0 && dppo_prec_2b(precision);
-    const bool main_jobs = what != PACK_SAMPLER, sampler_tables = split_tables && what != PACK_UPDATE;
+    const bool main_jobs = what != PACK_SAMPLER && what != PACK_SAMPLER_TEMB;
+    const bool sampler_tables = split_tables && what != PACK_UPDATE;
     const int jobs = (main_jobs ? 11 + (time_dim > 0 ? 1 : 0) : 0) + (sampler_tables ? 1 : 0);
     if (a.njobs + jobs > PACK_MAXJ) return dppo_set_error(DPPO_EINVAL, "pack: too many images in one launch");
     auto mat = [&](size_t src, int K, int N, bool tr, int seg) {
@@ -324,7 +326,7 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
         b.rout = P_out(packed) + L.off[SEG_ROUT];
         // blocks: [0, R) TEMB rows, [R, 2R) TIN rows, 2R B_OUT2 (time_table_block)
         b.nfold = sampler_tables ? L.nt_h : 0;
-        b.first_table = what == PACK_SAMPLER ? L.temb_steps : 0;
+        b.first_table = what == PACK_SAMPLER ? L.temb_steps : 0;   // PACK_SAMPLER_TEMB: the TEMB rows too
         b.tables = sampler_tables ? 2 * L.temb_steps + 1 - b.first_table : L.temb_steps;
     }
     return DPPO_OK;
@@ -384,7 +386,7 @@ static int launch_pack(PackArgs& a, int precision, hipStream_t s) {
 // a run of minibatches packs each actor image without them and the rollout after the update pays
 // for them once. Keyed by the image's address; stream order is the caller's, as for every launch.
 namespace {
-struct StaleTables { const void* packed; const float* params; Dims D; int precision; };
+struct StaleTables { const void* packed; const float* params; Dims D; int precision; bool temb; };
 constexpr int MAX_STALE = 32;
 std::mutex g_stale_mu;
 StaleTables g_stale[MAX_STALE];
@@ -396,19 +398,21 @@ void clear_stale(const void* packed) {
         if (g_stale[i].packed == packed) { g_stale[i] = g_stale[--g_nstale]; return; }
 }
 
-int mark_stale(const Dims& D, int precision, const float* params, const void* packed) {
+// the latest update of an image decides what is stale: a PACK_UPDATE pack rewrites TEMB (temb =
+// false), a fused actor step does not (temb = true)
+int mark_stale(const Dims& D, int precision, const float* params, const void* packed, bool temb) {
     std::lock_guard<std::mutex> lk(g_stale_mu);
     for (int i = 0; i < g_nstale; ++i)
-        if (g_stale[i].packed == packed) { g_stale[i] = {packed, params, D, precision}; return DPPO_OK; }
+        if (g_stale[i].packed == packed) { g_stale[i] = {packed, params, D, precision, temb}; return DPPO_OK; }
     if (g_nstale == MAX_STALE) return dppo_set_error(DPPO_EINVAL, "deferred sampler tables: more than %d stale images", MAX_STALE);
-    g_stale[g_nstale++] = {packed, params, D, precision};
+    g_stale[g_nstale++] = {packed, params, D, precision, temb};
     return DPPO_OK;
 }
 }  // namespace
 
 // the fused step leaves the actor image's split-sampler tables stale like a PACK_UPDATE pack
-int dppo_mark_tables_stale(const Dims& D, int precision, const float* actor_params, const void* packed_actor) {
-    return mark_stale(D, precision, actor_params, packed_actor);
+int dppo_mark_tables_stale(const Dims& D, int precision, const float* actor_params, const void* packed_actor, bool temb) {
+    return mark_stale(D, precision, actor_params, packed_actor, temb);
 }
 
 int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* params,
@@ -434,7 +438,7 @@ extern "C" int dppo_refresh_sampler_tables(const void* packed, void* stream) {
     }
     PackArgs a = {};
     int rc = add_mlp_jobs(a, e.D.IN, e.D.H, e.D.XD, e.D.TD, e.precision, e.params, (void*)e.packed, e.D.K, e.D.TS,
-                          PACK_SAMPLER);
+                          e.temb ? PACK_SAMPLER_TEMB : PACK_SAMPLER);
     if (rc) return rc;
     return launch_pack(a, e.precision, s);
 }
@@ -455,7 +459,7 @@ int dppo_pack_models(const Dims& D, int precision, const float* actor_params, vo
         rc = add_mlp_jobs(a, D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS,
                           defer ? PACK_UPDATE : PACK_ALL);
         if (rc) return rc;
-        if (defer) rc = mark_stale(D, precision, actor_params, packed_actor);
+        if (defer) rc = mark_stale(D, precision, actor_params, packed_actor, false);
         else clear_stale(packed_actor);   // a full pack makes a pending refresh moot
         if (rc) return rc;
     }

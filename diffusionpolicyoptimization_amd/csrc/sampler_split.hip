@@ -1812,8 +1812,16 @@ int xchg_for(hipStream_t s, uint64_t** buf, uint32_t* seq, uint32_t** fail_dev) 
         // rebind the slot of a stream with no work pending; only when every such stream is busy,
         // wait for ONE of them (never the whole device: another stream may hold a pipelined launch
         // that waits for an observation the host publishes only after this call returns)
-        for (int i = 0; i < 16 && slot < 0; ++i)
-            if (g_xb[i].device == dev && hipStreamQuery(g_xb[i].stream) == hipSuccess) slot = i;
+        // (a query that is neither done nor not-ready means the stream no longer exists — its owner
+        // destroyed it without dppo_sampler_release_stream: its slot is free, nothing to wait for)
+        for (int i = 0; i < 16 && slot < 0; ++i) {
+            if (g_xb[i].device != dev) continue;
+            const hipError_t q = hipStreamQuery(g_xb[i].stream);
+            if (q != hipErrorNotReady) {
+                (void)hipGetLastError();
+                slot = i;
+            }
+        }
         if (slot < 0) {
             static int next_evict = 0;
             for (int k = 0; k < 16 && slot < 0; ++k) {

@@ -237,7 +237,124 @@ extern "C" int dppo_reward_scale_apply(double* reward, const double* rms_state, 
 }
 
 extern "C" size_t dppo_reward_scale_workspace_doubles(int S, int E) {
-    return (size_t)S * E + (size_t)3 * E + 3;
+    // the shared scan (rets [S,E] + per-env moments + 3) and, for per_env, the column moments [S][2]
+    return (size_t)S * E + (size_t)3 * E + 3 + (size_t)2 * S;
+}
+
+// ---------------------------------------------------------------------------------------------
+// per_env = True (util/reward_scaling.py:51-66): the RunningMeanStd has shape (num_envs,) and is
+// updated with ret_rms.update(rets) on rets [E, S] (env-major), i.e. with np.mean / np.var over
+// axis 0 — the ENVS — so each time column t contributes one (mean_t, var_t) pair with batch count E,
+// and the state broadcasts against the S columns by NumPy's rules (shape (E,) needs S == E, or one
+// side of length 1). transform() then divides reward [E, S] by sqrt(var + eps) along the last axis.
+// The sums run over e in order 0..E-1, as NumPy's add.reduce does over a non-contiguous axis.
+// rms layout: fp64 [1 + 2 L] = {count, mean[L], var[L]}.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void col_moments_kernel(const double* __restrict__ rets, int S, int E,
+                                                          double* __restrict__ colm) {
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < S; t += gridDim.x * 256) {
+        double s = 0.0;
+        for (int e = 0; e < E; ++e) s += rets[(size_t)t * E + e];
+        const double mean = s / (double)E;
+        double q = 0.0;
+        for (int e = 0; e < E; ++e) {
+            const double d = rets[(size_t)t * E + e] - mean;
+            q += d * d;
+        }
+        colm[2 * t] = mean;
+        colm[2 * t + 1] = q / (double)E;
+    }
+}
+
+// RunningMeanStd.update_from_moments (reward_scaling.py:29-39) per output column j < Lo with
+// NumPy broadcasting: batch column j (S == 1 -> 0), state entry j (Li == 1 -> 0)
+__global__ __launch_bounds__(256) void rms_cols_update_kernel(const double* __restrict__ colm, int S, int E,
+                                                              const double* __restrict__ rin, int Li,
+                                                              double* __restrict__ rout, int Lo) {
+    const double count = rin[0], bc = (double)E;
+    const double tot = count + bc;
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < Lo; j += gridDim.x * 256) {
+        const int t = S == 1 ? 0 : j, l = Li == 1 ? 0 : j;
+        const double bm = colm[2 * t], bv = colm[2 * t + 1];
+        const double mean = rin[1 + l], var = rin[1 + Li + l];
+        const double delta = bm - mean;
+        const double m_a = var * count;
+        const double m_b = bv * bc;
+        const double M2 = m_a + m_b + delta * delta * count * bc / tot;
+        rout[1 + j] = mean + delta * bc / tot;
+        rout[1 + Lo + j] = M2 / (tot - 1.0);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) rout[0] = tot;
+}
+
+// out [C, E] time-major, C = S (Lo == S or Lo == 1) or Lo (S == 1): out[c][e] = clip(reward[s][e] /
+// sqrt(var[v] + eps)), s = (S == 1 ? 0 : c), v = (Lo == 1 ? 0 : c)
+__global__ __launch_bounds__(256) void scale_cols_kernel(const double* __restrict__ rew, const double* __restrict__ rms,
+                                                         int S, int E, int Lo, int C, double cliprew, double eps,
+                                                         double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)C * E) return;
+    const int c = (int)(i / E), e = (int)(i - (int64_t)c * E);
+    const int s = S == 1 ? 0 : c, v = Lo == 1 ? 0 : c;
+    double r = rew[(size_t)s * E + e] / sqrt(rms[1 + Lo + v] + eps);
+    r = r < -cliprew ? -cliprew : (r > cliprew ? cliprew : r);
+    out[i] = r;
+}
+
+static int bcast_len(int S, int L) { return S == L ? L : (S == 1 ? L : (L == 1 ? S : -1)); }
+
+extern "C" int dppo_reward_scale_per_env_moments(const double* reward, const uint8_t* first, double* ret_state,
+                                                 double* workspace, double* col_moments, int S, int E, double gamma,
+                                                 void* stream) {
+    DPPO_CHECK(S > 0 && E > 0, "dppo_reward_scale_per_env_moments: empty");
+    DPPO_CHECK(reward && first && ret_state && workspace && col_moments, "dppo_reward_scale_per_env_moments: null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    double* rets = workspace;
+    double* env_mom = rets + (size_t)S * E;
+    { DppoKtScope kt(KT_RETS, s);
+        hipLaunchKernelGGL(rets_kernel, dim3(dppo_cdiv(E, SCAN_WAVES)), dim3(64 * SCAN_WAVES), 0, s,
+                           reward, first, ret_state, rets, env_mom, S, E, gamma);
+    }
+    DPPO_HIP(hipGetLastError());
+    { DppoKtScope kt(KT_MOMENTS, s);
+        hipLaunchKernelGGL(col_moments_kernel, dim3(dppo_cdiv(S, 256)), dim3(256), 0, s, rets, S, E, col_moments);
+    }
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+extern "C" int dppo_reward_scale_per_env_apply(const double* reward, const double* rms_state, int S, int E, int L,
+                                               double cliprew, double epsilon, double* out, void* stream) {
+    DPPO_CHECK(S > 0 && E > 0 && L > 0, "dppo_reward_scale_per_env_apply: empty");
+    DPPO_CHECK(reward && rms_state && out, "dppo_reward_scale_per_env_apply: null pointer");
+    const int C = bcast_len(S, L);
+    DPPO_CHECK(C > 0, "operands could not be broadcast together with shapes (%d,) (%d,)", S, L);
+    DPPO_CHECK(out != reward || C == S, "dppo_reward_scale_per_env_apply: S == 1 < L needs a separate [L, E] out");
+    hipStream_t s = (hipStream_t)stream;
+    { DppoKtScope kt(KT_SCALE_APPLY, s);
+        hipLaunchKernelGGL(scale_cols_kernel, dim3(dppo_cdiv(C * E, 256)), dim3(256), 0, s, reward, rms_state, S, E, L,
+                           C, cliprew, epsilon, out);
+    }
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
+}
+
+extern "C" int dppo_reward_scale_per_env(const double* reward, const uint8_t* first, double* ret_state,
+                                         const double* rms_in, int L_in, double* rms_out, double* workspace, int S,
+                                         int E, double gamma, double cliprew, double epsilon, double* out,
+                                         void* stream) {
+    DPPO_CHECK(S > 0 && E > 0 && L_in > 0, "dppo_reward_scale_per_env: empty");
+    DPPO_CHECK(rms_in && rms_out && rms_in != rms_out, "dppo_reward_scale_per_env: rms_in and rms_out must differ");
+    const int Lo = bcast_len(S, L_in);
+    DPPO_CHECK(Lo > 0, "operands could not be broadcast together with shapes (%d,) (%d,)", S, L_in);
+    double* colm = workspace + (size_t)S * E + (size_t)3 * E + 3;
+    int rc = dppo_reward_scale_per_env_moments(reward, first, ret_state, workspace, colm, S, E, gamma, stream);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(rms_cols_update_kernel, dim3(dppo_cdiv(Lo, 256)), dim3(256), 0, s, colm, S, E, rms_in, L_in,
+                       rms_out, Lo);
+    DPPO_HIP(hipGetLastError());
+    return dppo_reward_scale_per_env_apply(reward, rms_out, S, E, Lo, cliprew, epsilon, out, stream);
 }
 
 extern "C" int dppo_reward_scale(double* reward, const uint8_t* first, double* ret_state, double* rms_state,

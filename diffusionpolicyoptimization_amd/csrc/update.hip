@@ -1,6 +1,7 @@
 // update.hip — weight gradients, time-MLP backward, minibatch statistics, optimiser, and the
 // dppo_ppo_minibatch orchestration (agent/finetune/train_ppo_diffusion_agent.py:287-356).
 #include <stdlib.h>
+#include <mutex>
 #include "dppo_ppo.h"
 
 // ---------------------------------------------------------------------------------------------
@@ -324,9 +325,13 @@ __device__ inline float packed_elem(const uint8_t* img, int K, int k, int n, int
 // Workgroup b forms rows [L2B_ROWS b, +L2B_ROWS) of dW_l2 (workgroup 0 also db_l2): thread t owns
 // columns j = t, t + 256, ... with rnd(W_out[j][:]) in registers; the workgroup's pl2 rows are
 // loaded up front (uniform addresses: one round trip for all of them, not one per row). No LDS and
-// a few hundred FMAs per thread, so the launch fits beside the other stream's row tiles. (Inside
-// time_bwd's single workgroup the H x H x N products took 210 us; as extra workgroups of that launch
-// they inherited its dynamic LDS and waited for CUs, 48 us; one row's loads at a time, 33 us.)
+// a few hundred FMAs per thread, so the launch fits beside the other stream's row tiles. (r03: inside
+// time_bwd's single workgroup the H x H x N products took 210 us; as extra workgroups of that launch,
+// inheriting its dynamic LDS, they waited for CUs, 48 us; one row's loads at a time, 33 us. r04's
+// time_l2_bwd_kernel nevertheless runs them as extra workgroups of time_bwd's launch — one launch
+// fewer on the chain measured faster at 6,250 rows, profiles/r04l_tail_ab.txt — and is used only by
+// the r04 step path (DPPO_FUSED_STEP=critic below 16,384 rows). Since ABI 12 the default actor step
+// runs the time-MLP backward itself and l2_back, when materialised, is this LDS-free launch alone.)
 constexpr int L2B_ROWS = 4;   // rows h of dW_l2 per workgroup
 constexpr int L2B_MAXN = 32;
 template <int NJ, int NQ>
@@ -519,6 +524,15 @@ __global__ __launch_bounds__(TB_THREADS) void time_l2_bwd_kernel(const float* __
     }
     const int grp = ((int)blockIdx.x - 1) * (TB_THREADS / 256) + (int)threadIdx.x / 256;
     if (grp < l2_groups) l2_back_rows(l2b, grp, (int)threadIdx.x % 256);
+}
+
+// dynamic LDS of time_bwd_body over nb buckets; *stage_g = whether the bucket sums are staged too
+static size_t time_bwd_lds(const Dims& D, int nb, int* stage_g) {
+    size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
+                                  (size_t)nb * (2 * D.TD + 2 * 2 * D.TD));
+    *stage_g = tsm + sizeof(float) * (size_t)nb * D.H <= 160 * 1024;
+    if (*stage_g) tsm += sizeof(float) * (size_t)nb * D.H;
+    return tsm;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -734,7 +748,7 @@ __device__ inline void adamw_elem(float& pi, float& mi, float& vi, float gi, con
 // minibatch's critical path than a separate copy. With a tag, met_out[nmet] receives it after
 // the sums (system-scope release), so the host polls host-mapped memory instead of recording
 // and waiting on an event (a marker packet on the minibatch chain). Workgroup 0.
-__device__ inline void copy_metrics(const double* __restrict__ met, double* __restrict__ met_out, int nmet, uint64_t tag) {
+__device__ inline void copy_metrics(const double* met, double* met_out, int nmet, uint64_t tag) {
     if ((int)threadIdx.x < nmet) met_out[threadIdx.x] = met[threadIdx.x];
     if (tag) {
         __syncthreads();
@@ -769,31 +783,20 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 //  * each element's thread stores its updated parameter into its slots of the images (the pack's
 //    per-element values: the same RNE conversion, FuseJob in dppo_internal.h), and zeroes its
 //    gradient after the read (CLEAR_GRADS);
-//  * the launch's last workgroup (ticket counter) then writes what other threads read during the
-//    launch or what needs every element final: the actor's W_OUT / T_OUT images (the virtual l2
-//    gradient reads rnd(W_out)), the pl2 and db_out gradients (read by every l2 element), the TEMB
-//    table (temb_* in dppo_common.cuh, the pack's arithmetic) and the caller's byte ranges (the
-//    next minibatch's metrics and workspace accumulators, dppo_ppo_clear_ranges).
+//  * the caller's byte ranges (the next minibatch's metrics and workspace accumulators,
+//    dppo_ppo_clear_ranges) are zeroed by the launch's LAST workgroup (per-XCD ticket counters), so
+//    no range is cleared before every workgroup has read what it reads — the metric sums copied out
+//    included, whichever ranges the caller passes.
+// The actor's step (ABI 12, actor_step_kernel below) adds its time-MLP backward and the W_out
+// elements the virtual l2 gradient reads; a critic's step is this kernel.
 // ---------------------------------------------------------------------------------------------
 struct StepFuse {
     int njobs;
     FuseJob j[FUSE_MAXJ];
-    // elements whose new values the last workgroup needs: [0] the actor's time MLP (it derives TEMB
-    // from them), [1] W_out (its image slots are written by the last workgroup: the virtual l2
-    // gradient reads the old image during the launch). Their threads also publish the new value as
-    // a tagged granule {tag, fp32 bits} with an agent-scope store (the split sampler's exchange form)
-    int64_t own[2][2];
-    uint64_t* gran;                 // [own[0] count + own[1] count] granules
-    uint32_t gtag;                  // this launch's tag (nonzero, new per launch on the stream)
-    int temb_rows, TD, TS;          // the actor's TEMB rows (0: none) and its time stride
-    int64_t b1, w2, b2;             // time-MLP offsets relative to own[0][0] (= time_w1)
-    float* temb;
     int clear_grads;
-    int64_t keep[2][2];             // gradients other elements read: cleared by the last workgroup
     void* clr[4];
     uint32_t clr_words[4];
-    int use_last;                   // 0: no last-workgroup phase (block 0 clears, no ticket)
-    unsigned* ticket;               // zero between launches (the last workgroup resets it)
+    unsigned* ticket;               // zero between launches (the last workgroup resets it); null: no clears
 };
 
 template <class ET, int KG, int EPL>
@@ -809,141 +812,181 @@ __device__ inline void fuse_store(const FuseJob& J, int64_t e, float x) {
     const size_t slot = ((size_t)(nn >> 4) * J.KS + k / KG) * 64 + (nn & 15) + 16 * ((k % KG) / EPL);
     reinterpret_cast<ET*>(J.dst + slot * 16)[k % EPL] = (ET)x;
 }
+template <class ET, int KG, int EPL>
+__device__ inline void fuse_all(const FuseJob* jobs, int njobs, int64_t i, float x) {
+#pragma unroll 1
+    for (int q = 0; q < njobs; ++q) {
+        const FuseJob& J = jobs[q];
+        if (i >= J.lo && i < J.hi) fuse_store<ET, KG, EPL>(J, i - J.lo, x);
+    }
+}
 
 __device__ inline bool in_range(int64_t i, const int64_t* r) { return i >= r[0] && i < r[1]; }
 
-// No device-scope fences (a release fence per workgroup is an L2 write-back on gfx950: ~2,000 of
-// them per launch). What the last workgroup reads from other workgroups comes as tagged granules it
-// polls; what it overwrites — the W_OUT / T_OUT slots and the pl2 / db_out gradients the virtual l2
-// gradient reads — every other workgroup has finished reading when it takes its ticket. Tickets are
-// counted per XCD first (blockIdx % 8), so no single address takes more than ~1/8 of the atomics.
+// true in exactly one workgroup, the last to arrive (thread 0's view broadcast through LDS); the
+// counters are per XCD first (blockIdx % 8), so no single address takes more than ~1/8 of the
+// atomics, and the last workgroup resets them for the next launch on the stream
+__device__ inline bool last_workgroup(unsigned* ticket) {
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned xcd = blockIdx.x & 7, per = (gridDim.x - xcd + 7) / 8;   // blocks counted on this XCD's ticket
+        int l = 0;
+        if (atomicAdd(ticket + 16 * xcd, 1u) == per - 1) {
+            ticket[16 * xcd] = 0u;
+            const unsigned nx = gridDim.x < 8 ? gridDim.x : 8;
+            l = atomicAdd(ticket + 128, 1u) == nx - 1;
+            if (l) ticket[128] = 0u;
+        }
+        last = l;
+    }
+    __syncthreads();
+    return last != 0;
+}
+__device__ inline void clear_words(void* const* clr, const uint32_t* words) {
+    for (int r = 0; r < 4; ++r)
+        for (uint32_t i = threadIdx.x; i < words[r]; i += blockDim.x) reinterpret_cast<uint32_t*>(clr[r])[i] = 0u;
+}
+
 // The job loops stay rolled: unrolled they made the kernel ~20k instructions long.
 constexpr int FUSE_BLOCKS = 1024;
 template <class ET, int KG, int EPL>
 __global__ __launch_bounds__(256) void adamw_fused_kernel(float* __restrict__ p, float* g, float* __restrict__ m,
                                                           float* __restrict__ v, int64_t n, AdamHP h,
-                                                          const double* __restrict__ met, double* __restrict__ met_out,
-                                                          int nmet, uint64_t tag, L2Virt vt, StepFuse f) {
-    extern __shared__ __attribute__((aligned(16))) float fsm[];
-    const int tid = threadIdx.x;
-    const int64_t n0 = f.own[0][1] - f.own[0][0], n1 = f.own[1][1] - f.own[1][0];
+                                                          const double* met, double* met_out, int nmet, uint64_t tag,
+                                                          StepFuse f) {
     if (blockIdx.x == 0) copy_metrics(met, met_out, nmet, tag);
-    auto clears = [&]() {
-        for (int r = 0; r < 4; ++r)
-            for (uint32_t i = tid; i < f.clr_words[r]; i += 256) reinterpret_cast<uint32_t*>(f.clr[r])[i] = 0u;
-    };
-    if (!f.use_last && blockIdx.x == 0) clears();
-    for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < n; i += (int64_t)gridDim.x * 256) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         float pi = p[i], mi = m[i], vi = v[i];
-        const bool virt = vt.on && i >= vt.w_off && i < vt.b_off + vt.H;
-        const float gi = virt ? l2_virtual_grad(g, vt, i) : g[i];
+        const float gi = g[i];
         adamw_elem(pi, mi, vi, gi, h);
         p[i] = pi; m[i] = mi; v[i] = vi;
-        if (f.clear_grads && !in_range(i, f.keep[0]) && !in_range(i, f.keep[1])) g[i] = 0.f;
-        const bool o0 = in_range(i, f.own[0]), o1 = in_range(i, f.own[1]);
-        if (o0 || o1)
-            __hip_atomic_store(f.gran + (o0 ? i - f.own[0][0] : n0 + i - f.own[1][0]),
-                               ((uint64_t)f.gtag << 32) | __float_as_uint(pi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (o1) continue;   // W_OUT / T_OUT: the last workgroup's
-#pragma unroll 1
-        for (int q = 0; q < f.njobs; ++q) {
-            const FuseJob& J = f.j[q];
-            if (i >= J.lo && i < J.hi) fuse_store<ET, KG, EPL>(J, i - J.lo, pi);
-        }
+        if (f.clear_grads) g[i] = 0.f;
+        fuse_all<ET, KG, EPL>(f.j, f.njobs, i, pi);
     }
-    if (!f.use_last) return;
-    __syncthreads();
-    __shared__ int last;
-    if (tid == 0) {
-        const unsigned xcd = blockIdx.x & 7, per = (gridDim.x - xcd + 7) / 8;   // blocks counted on this XCD's ticket
-        int l = 0;
-        if (atomicAdd(f.ticket + 16 * xcd, 1u) == per - 1) {
-            f.ticket[16 * xcd] = 0u;
-            const unsigned nx = gridDim.x < 8 ? gridDim.x : 8;
-            l = atomicAdd(f.ticket + 128, 1u) == nx - 1;
-        }
-        last = l;
-    }
-    __syncthreads();
-    if (!last) return;
-    if (tid == 0) f.ticket[128] = 0u;
-    float* ov = fsm;   // [n0 + n1] the owned elements' new values, then TEMB scratch
-    const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 100000000ull;   // 1 s (100 MHz)
-    constexpr int GB = 8;   // granule loads in flight per thread
-    for (int64_t base = 0; base < n0 + n1; base += 256 * GB) {
-        uint64_t w[GB];
-#pragma unroll
-        for (int u = 0; u < GB; ++u) {
-            const int64_t q = base + u * 256 + tid;
-            w[u] = q < n0 + n1 ? __hip_atomic_load(f.gran + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < GB; ++u) {
-            const int64_t q = base + u * 256 + tid;
-            if (q >= n0 + n1) continue;
-            uint64_t x = w[u];
-            while ((uint32_t)(x >> 32) != f.gtag) {   // published before its workgroup's ticket; bounded
-                if (__builtin_amdgcn_s_memrealtime() > t_end) { x = ((uint64_t)f.gtag << 32) | 0x7fc00000u; break; }
-                __builtin_amdgcn_s_sleep(1);
-                x = __hip_atomic_load(f.gran + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            ov[q] = __uint_as_float((uint32_t)x);
-        }
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int jq = 0; jq < f.njobs; ++jq) {   // job-major: each job's fields are loaded once
-        const FuseJob& J = f.j[jq];
-        const int64_t lo = J.lo > f.own[1][0] ? J.lo : f.own[1][0], hi = J.hi < f.own[1][1] ? J.hi : f.own[1][1];
-        for (int64_t i = lo + tid; i < hi; i += 256) fuse_store<ET, KG, EPL>(J, i - J.lo, ov[n0 + i - f.own[1][0]]);
-    }
-    if (f.temb_rows > 0) temb_rows_block(ov, 0, f.b1, f.w2, f.b2, f.TD, f.TS, f.temb_rows, f.temb, ov + n0 + n1);
-    if (f.clear_grads)
-        for (int r = 0; r < 2; ++r)
-            for (int64_t i = f.keep[r][0] + tid; i < f.keep[r][1]; i += 256) g[i] = 0.f;
-    clears();
+    if (f.ticket && last_workgroup(f.ticket)) clear_words(f.clr, f.clr_words);
 }
 
-// per (device, stream): a zeroed ticket counter, the granule buffer of the fused step and its launch
-// tag, created on first use and grown on demand (launches on one stream are ordered, so they share
-// them; the critic's step on the side stream has its own)
-struct StepScratch { unsigned* ticket; uint64_t* gran; int64_t cap; uint32_t* tag; };
-static int step_scratch(hipStream_t s, int64_t ngran, StepScratch* out) {
-    struct Ent { int dev; hipStream_t s; unsigned* ticket; uint64_t* gran; int64_t cap; uint32_t tag; };
-    thread_local Ent ents[16] = {};
-    thread_local int next = 0;
+// ---------------------------------------------------------------------------------------------
+// The actor's optimizer step in ONE launch (ABI 12, dppo_actor_step): everything after the actor's
+// weight-gradient GEMM of a minibatch — the time-MLP backward (time_bwd_body, from the per-t bucket
+// sums of dh1), the virtual l2 gradient (DPPO_STEP_L2_FROM_PL2), Keras AdamW, the image slots, the
+// gradient and accumulator clears — which took three launches (time_bwd, adamw, pack) before. The
+// elements are split so that nothing waits on another workgroup's result:
+//  * workgroup 0 runs the time-MLP backward (it reads the OLD W_in time-embedding rows and time MLP
+//    and writes the gradients of the time MLP and b_in), then steps exactly those elements;
+//  * workgroups 1.. step every other element except W_out; the l2 elements' virtual gradient reads
+//    pl2 / db_out and the OLD rnd(W_out) of the image's W_OUT segment;
+//  * the last workgroup to arrive (tickets) steps W_out — so its W_OUT / T_OUT slots change only
+//    after every l2 element has read them — then zeroes pl2 / db_out and the caller's ranges.
+// The TEMB table is NOT rewritten: the row tiles derive the time embeddings they use from the fp32
+// time MLP in the image (rowtile.hip), and the sampler re-derives TEMB with its deferred tables.
+// ---------------------------------------------------------------------------------------------
+struct ActorStep {
+    int njobs;
+    FuseJob j[FUSE_MAXJ];
+    int64_t own0[3][2];     // workgroup 0's elements: the time MLP, W_in's time-embedding rows, b_in
+    int64_t wout[2];        // the last workgroup's: W_out
+    int64_t keep[2][2];     // read by every l2 element (pl2 region, db_out): zeroed by the last workgroup
+    const float* gseg;      // [KF][H] bucket sums of dh1, or null (the gradients are already in g)
+    FlatOffsets F;
+    int XD, TD, H, KF, TS, stage_g;
+    int clear_grads;        // zero each gradient after its read (DPPO_STEP_CLEAR_GRADS)
+    void* clr[4];
+    uint32_t clr_words[4];
+    unsigned* ticket;
+};
+constexpr int ACTOR_STEP_THREADS = TB_THREADS;
+template <class ET, int KG, int EPL>
+__global__ __launch_bounds__(ACTOR_STEP_THREADS) void actor_step_kernel(float* __restrict__ p, float* g,
+                                                                        float* __restrict__ m, float* __restrict__ v,
+                                                                        int64_t n, AdamHP h, const double* met,
+                                                                        double* met_out, int nmet, uint64_t tag,
+                                                                        L2Virt vt, ActorStep a) {
+    extern __shared__ __attribute__((aligned(16))) float asm_[];
+    const int tid = threadIdx.x;
+    auto step_one = [&](int64_t i, float gi) {
+        float pi = p[i], mi = m[i], vi = v[i];
+        adamw_elem(pi, mi, vi, gi, h);
+        p[i] = pi; m[i] = mi; v[i] = vi;
+        fuse_all<ET, KG, EPL>(a.j, a.njobs, i, pi);
+    };
+    if (blockIdx.x == 0) {
+        if (a.gseg) {
+            time_bwd_body(a.gseg, p, g, a.F, a.XD, a.TD, a.H, a.KF, a.TS, a.stage_g, asm_);
+            __syncthreads();   // its gradient stores, read below by other threads of this workgroup
+        }
+        for (int r = 0; r < 3; ++r)
+            for (int64_t i = a.own0[r][0] + tid; i < a.own0[r][1]; i += ACTOR_STEP_THREADS) {
+                const float gi = g[i];
+                if (a.clear_grads) g[i] = 0.f;
+                step_one(i, gi);
+            }
+    } else {
+        if (blockIdx.x == 1) copy_metrics(met, met_out, nmet, tag);
+        const int64_t stride = (int64_t)(gridDim.x - 1) * ACTOR_STEP_THREADS;
+        for (int64_t i = (int64_t)(blockIdx.x - 1) * ACTOR_STEP_THREADS + tid; i < n; i += stride) {
+            if (in_range(i, a.own0[0]) || in_range(i, a.own0[1]) || in_range(i, a.own0[2]) || in_range(i, a.wout))
+                continue;
+            const bool virt = vt.on && i >= vt.w_off && i < vt.b_off + vt.H;   // [l2_w | l2_b] are adjacent
+            const float gi = virt ? l2_virtual_grad(g, vt, i) : g[i];
+            if (a.clear_grads && !in_range(i, a.keep[0]) && !in_range(i, a.keep[1])) g[i] = 0.f;
+            step_one(i, gi);
+        }
+    }
+    if (!last_workgroup(a.ticket)) return;
+    for (int64_t i = a.wout[0] + tid; i < a.wout[1]; i += ACTOR_STEP_THREADS) {
+        const float gi = g[i];
+        if (a.clear_grads) g[i] = 0.f;
+        step_one(i, gi);
+    }
+    if (a.clear_grads)
+        for (int r = 0; r < 2; ++r)
+            for (int64_t i = a.keep[r][0] + tid; i < a.keep[r][1]; i += ACTOR_STEP_THREADS) g[i] = 0.f;
+    clear_words(a.clr, a.clr_words);
+}
+
+// per (device, stream): a zeroed ticket counter block of the fused steps, created on first use
+// (launches on one stream are ordered, so they share it; the critic's step on the side stream has its
+// own). One process-wide table under a mutex, keyed by the stream's own device.
+static int step_ticket(hipStream_t s, unsigned** out) {
+    struct Ent { int dev; hipStream_t s; unsigned* ticket; };
+    static std::mutex mu;
+    static Ent ents[64] = {};
+    static int next = 0;
     int dev = 0;
-    DPPO_HIP(hipGetDevice(&dev));
+    DPPO_HIP(hipStreamGetDevice(s, &dev));
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& x : ents)
+        if (x.ticket && x.dev == dev && x.s == s) { *out = x.ticket; return DPPO_OK; }
     Ent* e = nullptr;
     for (auto& x : ents)
-        if (x.ticket && x.dev == dev && x.s == s) { e = &x; break; }
-    if (!e) {
-        for (auto& x : ents)
-            if (!x.ticket) { e = &x; break; }
-        if (!e) {   // every slot taken (many streams): evict round robin once the device is idle
-            e = &ents[next];
-            next = (next + 1) % 16;
-            DPPO_HIP(hipDeviceSynchronize());
-            (void)hipFree(e->ticket);
-            (void)hipFree(e->gran);
-            *e = Ent{};
-        }
-        DPPO_HIP(hipMalloc((void**)&e->ticket, 1024));   // 8 per-XCD counters 64 B apart, the total at 512 B
-        e->dev = dev; e->s = s;
-        DPPO_HIP(hipMemsetAsync(e->ticket, 0, 1024, s));
+        if (!x.ticket) { e = &x; break; }
+    if (!e) {   // every slot taken (many streams): evict round robin once that device is idle
+        e = &ents[next];
+        next = (next + 1) % 64;
+        int cur = 0;
+        DPPO_HIP(hipGetDevice(&cur));
+        DPPO_HIP(hipSetDevice(e->dev));
+        DPPO_HIP(hipDeviceSynchronize());
+        (void)hipFree(e->ticket);
+        DPPO_HIP(hipSetDevice(cur));
+        *e = Ent{};
     }
-    if (ngran > e->cap) {   // stale granules never match: the tag is new per launch
-        if (e->gran) {
-            DPPO_HIP(hipStreamSynchronize(s));
-            (void)hipFree(e->gran);
-            e->gran = nullptr; e->cap = 0;
-        }
-        const int64_t cap = ngran > 32768 ? ngran : 32768;
-        DPPO_HIP(hipMalloc((void**)&e->gran, (size_t)cap * 8));
-        DPPO_HIP(hipMemsetAsync(e->gran, 0, (size_t)cap * 8, s));
-        e->cap = cap;
+    int cur = 0;
+    DPPO_HIP(hipGetDevice(&cur));
+    if (cur != dev) DPPO_HIP(hipSetDevice(dev));
+    const hipError_t ea = hipMalloc((void**)&e->ticket, 1024);   // 8 per-XCD counters 64 B apart, the total at 512 B
+    const hipError_t ez = ea == hipSuccess ? hipMemsetAsync(e->ticket, 0, 1024, s) : ea;
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (ea != hipSuccess || ez != hipSuccess) {
+        if (ea == hipSuccess) (void)hipFree(e->ticket);
+        e->ticket = nullptr;
+        (void)hipGetLastError();
+        return dppo_set_error(DPPO_EHIP, "fused step: ticket allocation failed");
     }
-    out->ticket = e->ticket; out->gran = e->gran; out->cap = e->cap; out->tag = &e->tag;
+    e->dev = dev; e->s = s;
+    *out = e->ticket;
     return DPPO_OK;
 }
 
@@ -979,7 +1022,7 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
                                float eps, int mode, const float* actor_params, void* packed_actor,
                                const float* critic_params, void* packed_critic, const double* metrics,
                                double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
-                               const size_t* clear_bytes, int n_clear, void* stream) {
+                               const size_t* clear_bytes, int n_clear, void* stream, const float* gseg = nullptr) {
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
@@ -1017,46 +1060,13 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
         vt = L2Virt{1, (int64_t)FA.l2_w, (int64_t)FA.l2_b, (int64_t)FA.out_b, D.H, D.XD, precision,
                     (const uint8_t*)packed_actor + L.off[SEG_W_OUT]};
     }
-    // the one-launch form: a single network whose parameters are exactly the range, and (actor,
-    // 2-byte operands) its split-sampler tables deferred, as the pack would leave them
-    const bool one_actor = packed_actor && !packed_critic && actor_params == params && n == (int64_t)FA.count &&
-                           (!dppo_prec_2b(precision) || defer);
+    // the one-launch form: a single network whose parameters are exactly the range. The actor's
+    // (actor_step_kernel) leaves its TEMB table and split-sampler tables to their consumers (the row
+    // tiles derive the time embeddings, the sampler re-derives the tables before its next launch)
+    const bool one_actor = packed_actor && !packed_critic && actor_params == params && n == (int64_t)FA.count;
     const bool one_critic = packed_critic && !packed_actor && critic_params == params && n == (int64_t)FC.count;
-    const int R = D.K;
-    const size_t lds_max = sizeof(float) * ((size_t)3 * R * D.TD + (FA.in_w - FA.time_w1) + (size_t)D.H * D.XD);
-    if (fuse && (one_actor || one_critic) && (!one_actor || lds_max <= 64 * 1024) && n > 0) {
-        const bool two = dppo_prec_2b(precision);
-        StepFuse f = {};
-        for (int r = 0; r < 2; ++r) f.own[r][0] = f.own[r][1] = f.keep[r][0] = f.keep[r][1] = -1;
-        if (fuse) {
-            f.njobs = one_actor ? dppo_fuse_jobs(D.IN, D.H, D.XD, D.TD, precision, packed_actor, D.K, f.j)
-                                : dppo_fuse_jobs(D.SD, D.HC, 1, 0, precision, packed_critic, 0, f.j);
-            DPPO_CHECK(f.njobs >= 0, "dppo_optimizer_step: fused pack jobs");
-            if (one_actor) {
-                const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
-                f.temb_rows = R; f.TD = D.TD; f.TS = D.TS;
-                f.own[0][0] = (int64_t)FA.time_w1; f.own[0][1] = (int64_t)FA.in_w;
-                f.b1 = (int64_t)(FA.time_b1 - FA.time_w1); f.w2 = (int64_t)(FA.time_w2 - FA.time_w1);
-                f.b2 = (int64_t)(FA.time_b2 - FA.time_w1);
-                f.temb = (float*)((uint8_t*)packed_actor + L.off[SEG_TEMB]);
-                if (l2v) { f.own[1][0] = (int64_t)FA.out_w; f.own[1][1] = (int64_t)(FA.out_w + (size_t)D.H * D.XD); }
-            }
-        }
-        f.clear_grads = clear_g ? 1 : 0;
-        if (l2v && clear_g) {   // read by every l2 element's virtual gradient
-            f.keep[0][0] = (int64_t)FA.l2_w; f.keep[0][1] = (int64_t)(FA.l2_w + (size_t)D.H * D.XD);
-            f.keep[1][0] = (int64_t)FA.out_b; f.keep[1][1] = (int64_t)(FA.out_b + D.XD);
-        }
-        for (int r = 0; r < n_clear; ++r) { f.clr[r] = clear_ptrs[r]; f.clr_words[r] = (uint32_t)(clear_bytes[r] / 4); }
-        f.use_last = (f.temb_rows > 0 || f.own[1][1] > 0 || f.keep[0][1] > 0) ? 1 : 0;
-        if (f.use_last) {
-            StepScratch sc;
-            rc = step_scratch(s, (f.own[0][1] - f.own[0][0]) + (f.own[1][1] - f.own[1][0]), &sc);
-            if (rc) return rc;
-            f.ticket = sc.ticket; f.gran = sc.gran;
-            if (++*sc.tag == 0) ++*sc.tag;   // 0 is the buffer's initial tag
-            f.gtag = *sc.tag;
-        }
+    DPPO_CHECK(!gseg || (fuse && one_actor), "dppo_actor_step: the time-MLP backward needs the fused actor step");
+    if (fuse && (one_actor || one_critic) && n > 0) {
         DPPO_CHECK(n_metrics >= 0 && n_metrics <= 256 && (n_metrics == 0 || (metrics && mout)),
                    "dppo_optimizer_step: bad metrics copy");
         DPPO_CHECK(metrics_tag == 0 || (mout && metrics_tag < ((uint64_t)1 << 53)),
@@ -1067,24 +1077,80 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
         const double bc2 = 1.0 - pow((double)beta2, (double)step);
         const AdamHP h = {lr, weight_decay, beta1, beta2, eps, (float)((double)lr * sqrt(bc2) / bc1), (float)bc1,
                           (float)bc2, mode};
-        const int64_t blocks64 = (n + 255) / 256;
-        const unsigned blocks = (unsigned)(blocks64 < FUSE_BLOCKS ? blocks64 : FUSE_BLOCKS);
-        const size_t lds = f.use_last ? sizeof(float) * ((size_t)(f.own[0][1] - f.own[0][0]) +
-                                                         (size_t)(f.own[1][1] - f.own[1][0]) +
-                                                         (f.temb_rows > 0 ? (size_t)3 * R * D.TD : 0)) : 0;
-        DPPO_CHECK(lds <= 64 * 1024, "dppo_optimizer_step: fused step LDS %zu B", lds);
-        DppoKtScope kt(KT_ADAMW, s);
-        if (precision == DPPO_BF16)
-            hipLaunchKernelGGL((adamw_fused_kernel<__bf16, 32, 8>), dim3(blocks), dim3(256), lds, s, params, grads, m, v,
-                               n, h, metrics, mout, n_metrics, metrics_tag, vt, f);
-        else if (precision == DPPO_F16)
-            hipLaunchKernelGGL((adamw_fused_kernel<_Float16, 32, 8>), dim3(blocks), dim3(256), lds, s, params, grads, m,
-                               v, n, h, metrics, mout, n_metrics, metrics_tag, vt, f);
-        else
-            hipLaunchKernelGGL((adamw_fused_kernel<float, 16, 4>), dim3(blocks), dim3(256), lds, s, params, grads, m, v,
-                               n, h, metrics, mout, n_metrics, metrics_tag, vt, f);
+        if (one_critic) {
+            StepFuse f = {};
+            f.njobs = dppo_fuse_jobs(D.SD, D.HC, 1, 0, precision, packed_critic, 0, f.j);
+            DPPO_CHECK(f.njobs >= 0, "dppo_optimizer_step: fused pack jobs");
+            f.clear_grads = clear_g ? 1 : 0;
+            for (int r = 0; r < n_clear; ++r) { f.clr[r] = clear_ptrs[r]; f.clr_words[r] = (uint32_t)(clear_bytes[r] / 4); }
+            if (n_clear > 0) {
+                rc = step_ticket(s, &f.ticket);
+                if (rc) return rc;
+            }
+            const int64_t blocks64 = (n + 255) / 256;
+            const unsigned blocks = (unsigned)(blocks64 < FUSE_BLOCKS ? blocks64 : FUSE_BLOCKS);
+            DppoKtScope kt(KT_ADAMW, s);
+            if (precision == DPPO_BF16)
+                hipLaunchKernelGGL((adamw_fused_kernel<__bf16, 32, 8>), dim3(blocks), dim3(256), 0, s, params, grads, m, v,
+                                   n, h, metrics, mout, n_metrics, metrics_tag, f);
+            else if (precision == DPPO_F16)
+                hipLaunchKernelGGL((adamw_fused_kernel<_Float16, 32, 8>), dim3(blocks), dim3(256), 0, s, params, grads, m,
+                                   v, n, h, metrics, mout, n_metrics, metrics_tag, f);
+            else
+                hipLaunchKernelGGL((adamw_fused_kernel<float, 16, 4>), dim3(blocks), dim3(256), 0, s, params, grads, m, v,
+                                   n, h, metrics, mout, n_metrics, metrics_tag, f);
+            DPPO_HIP(hipGetLastError());
+            return DPPO_OK;
+        }
+        ActorStep a = {};
+        a.njobs = dppo_fuse_jobs(D.IN, D.H, D.XD, D.TD, precision, packed_actor, D.K, a.j);
+        DPPO_CHECK(a.njobs >= 0, "dppo_optimizer_step: fused pack jobs");
+        a.own0[0][0] = (int64_t)FA.time_w1; a.own0[0][1] = (int64_t)FA.in_w;
+        a.own0[1][0] = (int64_t)(FA.in_w + (size_t)D.XD * D.H); a.own0[1][1] = (int64_t)(FA.in_w + (size_t)(D.XD + D.TD) * D.H);
+        a.own0[2][0] = (int64_t)FA.in_b; a.own0[2][1] = (int64_t)(FA.in_b + D.H);
+        a.wout[0] = (int64_t)FA.out_w; a.wout[1] = (int64_t)(FA.out_w + (size_t)D.H * D.XD);
+        for (int r = 0; r < 2; ++r) a.keep[r][0] = a.keep[r][1] = -1;
+        if (l2v) {   // read by every l2 element's virtual gradient: zeroed by the last workgroup
+            a.keep[0][0] = (int64_t)FA.l2_w; a.keep[0][1] = (int64_t)(FA.l2_w + (size_t)D.H * D.XD);
+            a.keep[1][0] = (int64_t)FA.out_b; a.keep[1][1] = (int64_t)(FA.out_b + D.XD);
+        }
+        a.clear_grads = clear_g ? 1 : 0;
+        a.gseg = gseg;
+        a.F = FA; a.XD = D.XD; a.TD = D.TD; a.H = D.H; a.KF = D.KF; a.TS = D.TS;
+        size_t lds = 0;
+        if (gseg) {
+            lds = time_bwd_lds(D, D.KF, &a.stage_g);
+            DPPO_CHECK(lds <= 160 * 1024, "dppo_actor_step: time-MLP backward LDS %zu B exceeds 160 KB", lds);
+        }
+        for (int r = 0; r < n_clear; ++r) { a.clr[r] = clear_ptrs[r]; a.clr_words[r] = (uint32_t)(clear_bytes[r] / 4); }
+        rc = step_ticket(s, &a.ticket);
+        if (rc) return rc;
+        // one workgroup per CU: workgroup 0's time-MLP backward (~10 us of dependent phases) runs
+        // beside the other workgroups' AdamW, so the launch ends about when it does
+        const int cus = dw_device_cus();
+        const unsigned blocks = (unsigned)(cus > 2 ? cus : 2);
+        if (lds > 64 * 1024) {
+            const void* fn = precision == DPPO_BF16 ? (const void*)actor_step_kernel<__bf16, 32, 8>
+                           : precision == DPPO_F16 ? (const void*)actor_step_kernel<_Float16, 32, 8>
+                                                    : (const void*)actor_step_kernel<float, 16, 4>;
+            rc = dppo_func_lds(fn, lds);
+            if (rc) return rc;
+        }
+        {
+            DppoKtScope kt(KT_ADAMW, s);
+            if (precision == DPPO_BF16)
+                hipLaunchKernelGGL((actor_step_kernel<__bf16, 32, 8>), dim3(blocks), dim3(ACTOR_STEP_THREADS), lds, s,
+                                   params, grads, m, v, n, h, metrics, mout, n_metrics, metrics_tag, vt, a);
+            else if (precision == DPPO_F16)
+                hipLaunchKernelGGL((actor_step_kernel<_Float16, 32, 8>), dim3(blocks), dim3(ACTOR_STEP_THREADS), lds, s,
+                                   params, grads, m, v, n, h, metrics, mout, n_metrics, metrics_tag, vt, a);
+            else
+                hipLaunchKernelGGL((actor_step_kernel<float, 16, 4>), dim3(blocks), dim3(ACTOR_STEP_THREADS), lds, s,
+                                   params, grads, m, v, n, h, metrics, mout, n_metrics, metrics_tag, vt, a);
+        }
         DPPO_HIP(hipGetLastError());
-        return one_actor && two ? dppo_mark_tables_stale(D, precision, actor_params, packed_actor) : DPPO_OK;
+        // TEMB (every precision) and the split sampler's tables (2-byte) wait for the next sampler launch
+        return dppo_mark_tables_stale(D, precision, actor_params, packed_actor, true);
     }
     // the launch-per-stage form (any ranges and images): AdamW, then the pack, which also zeroes the
     // gradients AdamW has read (DPPO_STEP_CLEAR_GRADS) and the caller's ranges
@@ -1137,6 +1203,30 @@ extern "C" int dppo_optimizer_step_ex(const dppo_dims* d, int precision, float* 
     return optimizer_step_impl(d, precision, params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode,
                                actor_params, packed_actor, critic_params, packed_critic, metrics, metrics_out,
                                n_metrics, metrics_tag, clear_ptrs, clear_bytes, n_clear, stream);
+}
+
+// ABI 12: the actor's optimizer step in one launch (actor_step_kernel); with a workspace it also
+// runs the time-MLP backward from that minibatch's bucket sums (DPPO_PPO_TIME_BWD_IN_STEP)
+extern "C" int dppo_actor_step(const dppo_dims* d, int precision, float* params, float* grads, float* m, float* v,
+                               int64_t step, float lr, float weight_decay, float beta1, float beta2, float eps, int mode,
+                               void* packed_actor, const void* workspace, int batch_rows, const double* metrics,
+                               double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
+                               const size_t* clear_bytes, int n_clear, void* stream) {
+    Dims D;
+    int rc = dppo_check_dims(d, &D);
+    if (rc) return rc;
+    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
+    DPPO_CHECK((mode & ~(DPPO_STEP_L2_FROM_PL2 | DPPO_STEP_CLEAR_GRADS | DPPO_STEP_DEFER_SAMPLER_TABLES |
+                         DPPO_STEP_FUSED_PACK | 1)) == 0, "dppo_actor_step: unknown mode bits 0x%x", mode);
+    DPPO_CHECK(packed_actor && params, "dppo_actor_step: null image or parameters");
+    DPPO_CHECK(!workspace || batch_rows > 0, "dppo_actor_step: a workspace needs its batch_rows");
+    DPPO_CHECK(D.KF <= 16, "dppo_actor_step: ft_denoising_steps > 16 unsupported (bucket sums)");
+    const float* gseg = nullptr;
+    if (workspace) gseg = make_ppo_workspace(D, precision, batch_rows, (uint8_t*)const_cast<void*>(workspace)).gseg;
+    const int64_t n = (int64_t)make_flat_offsets(D.IN, D.H, D.XD, D.TD).count;
+    return optimizer_step_impl(d, precision, params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps,
+                               mode | DPPO_STEP_FUSED_PACK, params, packed_actor, nullptr, nullptr, metrics, metrics_out,
+                               n_metrics, metrics_tag, clear_ptrs, clear_bytes, n_clear, stream, gseg);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1323,11 +1413,9 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
     DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
     // (time_bwd forked onto a side stream beside l2_back measured slower: 0.428 vs 0.406 ms per
     // minibatch, same box, tools/r03_ab2.sh; since r04 the two share one launch instead)
-    size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
-                                  (size_t)nb * (2 * D.TD + 2 * 2 * D.TD));
+    int stage_g = 0;
+    const size_t tsm = time_bwd_lds(D, nb, &stage_g);
     DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
-    const int stage_g = tsm + sizeof(float) * (size_t)nb * D.H <= 160 * 1024;
-    if (stage_g) tsm += sizeof(float) * (size_t)nb * D.H;
     if (l2_back) {
         const int groups = dppo_cdiv(D.H, L2B_ROWS), per = TB_THREADS / 256;
         { const int rc_ = dppo_func_lds((const void*)time_l2_bwd_kernel, tsm); if (rc_) return rc_; }
@@ -1431,7 +1519,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     DPPO_CHECK(parts >= 1 && parts <= 5, "dppo_ppo_minibatch: bad part %d", parts);
     DPPO_CHECK(parts == 3 || adv_stats || parts == 2 || parts == 5,
                "dppo_ppo_minibatch_part: the actor half needs adv_stats");
-    DPPO_CHECK((hp->flags & ~(DPPO_PPO_L2_DEFERRED | DPPO_PPO_LEARN_ETA | DPPO_PPO_PRECLEARED)) == 0,
+    DPPO_CHECK((hp->flags & ~(DPPO_PPO_L2_DEFERRED | DPPO_PPO_LEARN_ETA | DPPO_PPO_PRECLEARED |
+                              DPPO_PPO_TIME_BWD_IN_STEP)) == 0,
                "dppo_ppo_minibatch: unknown flags 0x%x", hp->flags);
     // one launch zeroes the atomically accumulated outputs of the half (or whole) being run
     // (minibatch_zero_args) unless the caller's optimizer step already did (DPPO_PPO_PRECLEARED)
@@ -1472,7 +1561,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     aa.packed = (const uint8_t*)packed_ft;
     aa.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     aa.sched = sched; aa.obs = obs; aa.chains = chains;
-    aa.XD = D.XD; aa.SD = D.SD; aa.TD = D.TD; aa.IN = D.IN; aa.H = D.H; aa.KF = D.KF; aa.Da = D.Da;
+    aa.XD = D.XD; aa.SD = D.SD; aa.TD = D.TD; aa.IN = D.IN; aa.H = D.H; aa.KF = D.KF; aa.Da = D.Da; aa.TS = D.TS;
     aa.mode = ROWS_TRAIN; aa.nrows = rows; aa.fk = fk; aa.start = start; aa.row_index = row_index;
     aa.lp_old = lp_old_mean; aa.adv = advantages; aa.adv_stats = stats; aa.hp = lh; aa.ws = ws; aa.metrics = metrics;
 
@@ -1549,6 +1638,22 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         return launch_critic_l2_back(D, precision, ws.cpl2, packed_critic, gc, crit_cnt, ws.crow_n, ws.crow_cnt, st);
     };
 
+    // after the actor's dW: the time-MLP backward (+ l2_back when l2 is materialised), unless the
+    // caller's actor step (dppo_actor_step) runs the time-MLP backward itself
+    auto actor_tail = [&]() -> int {
+        if (!(hp->flags & DPPO_PPO_TIME_BWD_IN_STEP))
+            return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def);
+        if (l2_def) return DPPO_OK;
+        const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+        L2Back l2b = {ws.pl2, ga + FA.out_b, (const uint8_t*)packed_ft + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b,
+                      D.H, D.XD, precision, nullptr, nullptr, nullptr};
+        DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
+        DppoKtScope kt(KT_L2_BACK, s);
+        hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
+        DPPO_HIP(hipGetLastError());
+        return DPPO_OK;
+    };
+
     // The critic is independent of the actor: its row tiles and then its weight gradients run on a
     // side stream, filling the CUs the actor's row tiles leave idle (the actor's last partial round)
     // and overlapping the critic's HBM-bound dW with the actor's tiles. Joined before the
@@ -1570,7 +1675,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (parts == 4) return DPPO_OK;
         rc = launch_grads(true, s);
         if (rc) return rc;
-        return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def);
+        return actor_tail();
     }
     SideStream* side = side_stream();
     if (side) {
@@ -1606,8 +1711,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
     }
-
-    return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def);
+    return actor_tail();
 }
 
 extern "C" int dppo_ppo_minibatch(const dppo_dims* d, int precision, const dppo_ppo_hparams* hp,
@@ -1707,7 +1811,7 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     aa.packed = (const uint8_t*)packed_actor;
     aa.L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     aa.sched = sched; aa.obs = cond; aa.chains = x_start;
-    aa.XD = D.XD; aa.SD = D.SD; aa.TD = D.TD; aa.IN = D.IN; aa.H = D.H; aa.KF = D.K; aa.Da = D.Da;
+    aa.XD = D.XD; aa.SD = D.SD; aa.TD = D.TD; aa.IN = D.IN; aa.H = D.H; aa.KF = D.K; aa.Da = D.Da; aa.TS = 1;
     aa.mode = ROWS_PRETRAIN; aa.nrows = rows; aa.ws = ws; aa.metrics = metrics;
     aa.tsteps = t; aa.noise = noise; aa.qsched = qsched;
     // loss = mean over global_rows * XD elements of (eps - noise)^2 (diffusion.py:192)

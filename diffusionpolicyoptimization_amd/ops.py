@@ -668,6 +668,48 @@ def reward_scale_apply(reward, rms_state, cliprew=10.0, epsilon=1e-8):
     return reward
 
 
+def _bcast_len(S, L):
+    if S == L or S == 1:
+        return L
+    if L == 1:
+        return S
+    raise ValueError(f"operands could not be broadcast together with shapes ({S},) ({L},)")
+
+
+def reward_scale_per_env(reward, first, ret_state, rms_in, L_in, rms_out, workspace, out, gamma=0.99, cliprew=10.0,
+                         epsilon=1e-8):
+    """RunningRewardScaler(per_env=True).__call__ (reference util/reward_scaling.py:51-66), time-major:
+    reward / first [S,E], rms_in / rms_out fp64 [1 + 2 L] = {count, mean[L], var[L]} (distinct buffers),
+    out [C, E] (C = S, or the new state length when S == 1). Returns the new state length."""
+    S, E = reward.shape
+    _check(reward, (S, E), torch.float64, "reward")
+    _check(first, (S, E), torch.uint8, "first")
+    _check(ret_state, (E,), torch.float64, "ret_state")
+    Lo = _bcast_len(S, L_in)
+    C = S if (S > 1 or Lo == 1) else Lo
+    _check(out, (C, E), torch.float64, "out")
+    if rms_in.numel() < 1 + 2 * L_in or rms_out.numel() < 1 + 2 * Lo:
+        raise ValueError("rms state buffers too small")
+    _lib.call("dppo_reward_scale_per_env", ptr(reward), ptr(first), ptr(ret_state), ptr(rms_in), int(L_in), ptr(rms_out),
+              ptr(workspace), S, E, float(gamma), float(cliprew), float(epsilon), ptr(out), stream_handle(reward.device))
+    return Lo
+
+
+def reward_scale_per_env_moments(reward, first, ret_state, workspace, col_moments, gamma=0.99):
+    S, E = reward.shape
+    _check(col_moments, (S, 2), torch.float64, "col_moments")
+    _lib.call("dppo_reward_scale_per_env_moments", ptr(reward), ptr(first), ptr(ret_state), ptr(workspace),
+              ptr(col_moments), S, E, float(gamma), stream_handle(reward.device))
+    return col_moments
+
+
+def reward_scale_per_env_apply(reward, rms_state, L, out, cliprew=10.0, epsilon=1e-8):
+    S, E = reward.shape
+    _lib.call("dppo_reward_scale_per_env_apply", ptr(reward), ptr(rms_state), S, E, int(L), float(cliprew),
+              float(epsilon), ptr(out), stream_handle(reward.device))
+    return out
+
+
 # ------------------------------------------------------------------------------------------------
 # update
 # ------------------------------------------------------------------------------------------------
@@ -862,6 +904,49 @@ class BoundOptimizerStep:
                                               stream_handle(self._dev) if stream is None else stream)
         if rc != 0:
             raise _lib.DppoError(f"dppo_optimizer_step failed ({rc}): {self._lib.dppo_last_error().decode()}")
+
+
+class BoundActorStep:
+    """dppo_actor_step (ABI 12) over the actor's flat range, marshalled once: the actor's AdamW, its
+    image, the gradient / accumulator clears and (workspace given: the minibatch ran with
+    DPPO_PPO_TIME_BWD_IN_STEP) the time-MLP backward in ONE launch."""
+
+    def __init__(self, d: ModelDims, precision, params, grads, m, v, weight_decay, beta1, beta2, eps, mode,
+                 packed_actor, workspace=None, batch_rows=0, l2_from_pl2=False, clear_grads=True):
+        na, _ = _n_params(d)
+        for t, nm in ((params, "params"), (grads, "grads"), (m, "m"), (v, "v")):
+            if t.numel() != na:
+                raise ValueError(f"{nm}: expected the actor's {na} elements")
+        if workspace is not None and _workspace_bytes(d, _prec(precision), int(batch_rows)) > workspace.numel():
+            raise ValueError("workspace too small for batch_rows")
+        self._lib = _lib.load()
+        self._dims = _dims_c(d)
+        mode_i = ((_lib.DPPO_ADAMW_KERAS if mode == "keras" else _lib.DPPO_ADAMW_TORCH) |
+                  (_lib.DPPO_STEP_L2_FROM_PL2 if l2_from_pl2 else 0) |
+                  (_lib.DPPO_STEP_CLEAR_GRADS if clear_grads else 0))
+        self._head = (ctypes.byref(self._dims), _prec(precision), ptr(params), ptr(grads), ptr(m), ptr(v))
+        self._mid = (float(weight_decay), float(beta1), float(beta2), float(eps), mode_i, ptr(packed_actor),
+                     ptr(workspace))
+        self._rows = int(batch_rows) if workspace is not None else 0
+        self._dev = params.device
+        self._keep = (params, grads, m, v, packed_actor, workspace)
+
+    def __call__(self, step, lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0, stream=None, clear=None,
+                 rows=None):
+        """rows: the minibatch's row count when it differs from batch_rows (a partial minibatch: the
+        workspace layout, and so its bucket sums, depend on it)."""
+        mo = metrics_out if isinstance(metrics_out, int) else (metrics_out.data_ptr() if metrics_out is not None else None)
+        mi = metrics if isinstance(metrics, int) else ptr(metrics)
+        cp, cb, cn = (None, None, 0) if clear is None else clear.args
+        r = self._rows if (rows is None or not self._rows) else int(rows)
+        if self._rows and not 0 < r <= self._rows:
+            raise ValueError(f"rows {r} outside (0, {self._rows}]")
+        rc = self._lib.dppo_actor_step(*self._head, int(step), float(lr), *self._mid, r, mi,
+                                       ctypes.c_void_p(mo) if mo else None, int(n_metrics),
+                                       ctypes.c_uint64(int(metrics_tag)), cp, cb, cn,
+                                       stream_handle(self._dev) if stream is None else stream)
+        if rc != 0:
+            raise _lib.DppoError(f"dppo_actor_step failed ({rc}): {self._lib.dppo_last_error().decode()}")
 
 
 class ClearRanges:

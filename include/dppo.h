@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 11
+#define DPPO_ABI_VERSION 12
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -55,14 +55,17 @@ enum { DPPO_STEP_DEFER_SAMPLER_TABLES = 0x100 };
  * (needs actor_params == params and packed_actor). */
 enum { DPPO_STEP_L2_FROM_PL2 = 0x200 };
 /* ABI 11, OR'd into dppo_optimizer_step's mode. DPPO_STEP_FUSED_PACK: AdamW and the pack in ONE
- * launch when the step packs a single network whose flat parameters are exactly the range (the actor
- * with 2-byte operands also needs DPPO_STEP_DEFER_SAMPLER_TABLES): each element's thread stores its
- * updated value into its slots of the images (the values the pack writes), and the launch's last
- * workgroup derives the actor's TEMB table. The image must have been fully packed once before (its
- * zero padding is not rewritten). Any other combination runs the two launches.
+ * launch when the step packs a single network whose flat parameters are exactly the range: each
+ * element's thread stores its updated value into its slots of the images (the values the pack writes).
+ * For an actor (since ABI 12) the launch leaves the TEMB table and the split sampler's tables to their
+ * consumers: the PPO / log-prob row tiles derive the time embeddings from the image's fp32 time MLP,
+ * and the next sampler launch (or dppo_refresh_sampler_tables) re-derives TEMB and the tables, as
+ * after DPPO_STEP_DEFER_SAMPLER_TABLES. The image must have been fully packed once before (its zero
+ * padding is not rewritten). Any other combination runs the two launches.
  * DPPO_STEP_CLEAR_GRADS (dppo_optimizer_step_ex only): the step zeroes the range's gradients after
- * reading them, and the byte ranges given to dppo_optimizer_step_ex after every read, so the next
- * minibatch of this range may skip its zeroing launch (DPPO_PPO_PRECLEARED). */
+ * reading them, and the byte ranges given to dppo_optimizer_step_ex after every read of the launch
+ * (by its last workgroup), so the next minibatch of this range may skip its zeroing launch
+ * (DPPO_PPO_PRECLEARED). */
 enum { DPPO_STEP_FUSED_PACK = 0x400, DPPO_STEP_CLEAR_GRADS = 0x800 };
 
 /* Model / schedule dimensions (cfg keys of cfg/gym/finetune/hopper-v2/ft_ppo_diffusion_mlp.yaml:18-25,78-110). */
@@ -151,6 +154,8 @@ DPPO_API int dppo_sampler_max_in_flight(const dppo_dims* d, int precision, int n
  * reuses that buffer instead of a new allocation. Slots are also rebound, without a device-wide
  * synchronisation, when more than 16 streams sample. (No reference counterpart: the reference's
  * sampler is a TF call, diffusion_vpg.py:250-339.) */
+/* A stream that sampled must be released before its owner destroys it (ops.RolloutPipe.close does);
+ * a slot whose stream no longer answers hipStreamQuery is treated as released. */
 DPPO_API int dppo_sampler_release_stream(void* stream);
 
 /* Kernel timer (ABI 10, measurement): while enabled, the library brackets the launches of its
@@ -241,6 +246,26 @@ DPPO_API int dppo_reward_scale_moments(const double* reward, const uint8_t* firs
 /* ... caller all-reduces/merges moments into rms_state, then pass 2 */
 DPPO_API int dppo_reward_scale_apply(double* reward, const double* rms_state, int S, int E, double cliprew,
                             double epsilon, void* stream);
+/* ABI 12: RunningRewardScaler(per_env=True) (util/reward_scaling.py:51-66). The reference's
+ * RunningMeanStd then has shape (num_envs,) and is updated by ret_rms.update(rets) with rets [E, S]:
+ * the moments are taken over axis 0, the ENVS, one (mean, var) pair per time column with batch count
+ * E, and NumPy broadcasting joins them to the state (so S must equal the state's length L, or one of
+ * the two be 1); transform() divides reward [E, S] by sqrt(var + eps) along its last axis. Kept as
+ * written, broadcasting errors included (DPPO_EINVAL "operands could not be broadcast together").
+ *   rms_in / rms_out fp64 [1 + 2 L] = {count, mean[L], var[L]} (init {1e-4, 0..., 1...}, L = E);
+ *   rms_out has L_out = broadcast(S, L_in) entries and must not alias rms_in;
+ *   out [C, E] time-major (C = S, or L_out when S == 1 < L_out: the reference returns [E, L_out]); out
+ *   may alias reward when C == S. reward / first / ret_state / workspace as dppo_reward_scale. */
+DPPO_API int dppo_reward_scale_per_env(const double* reward, const uint8_t* first, double* ret_state,
+                                       const double* rms_in, int L_in, double* rms_out, double* workspace, int S, int E,
+                                       double gamma, double cliprew, double epsilon, double* out, void* stream);
+/* ... the same split for multi-GPU: the scan and the per-column moments col_moments fp64 [S][2] =
+ * {mean_t, var_t} over this rank's envs (the caller merges ranks and updates the state), then the scale */
+DPPO_API int dppo_reward_scale_per_env_moments(const double* reward, const uint8_t* first, double* ret_state,
+                                               double* workspace, double* col_moments, int S, int E, double gamma,
+                                               void* stream);
+DPPO_API int dppo_reward_scale_per_env_apply(const double* reward, const double* rms_state, int S, int E, int L,
+                                             double cliprew, double epsilon, double* out, void* stream);
 
 /* ---- a19: GAE (train_ppo_diffusion_agent.py:239-263). reward fp64 [S,E], values fp32 [S,E],
  * last_values fp32 [E], terminated u8 [S,E] -> advantages, returns fp32 [S,E] */
@@ -295,6 +320,11 @@ enum { DPPO_PPO_LEARN_ETA = 2 };
  * metrics) are already zero — the previous optimizer step of the range cleared them
  * (DPPO_STEP_CLEAR_GRADS) — so the part skips its zeroing launch. */
 enum { DPPO_PPO_PRECLEARED = 4 };
+/* ABI 12, dppo_ppo_hparams.flags. DPPO_PPO_TIME_BWD_IN_STEP: the actor's part (1, 3 or 5) stops after
+ * its weight-gradient GEMM (plus l2_back when the l2 gradient is materialised): the time-MLP backward
+ * is left to the following dppo_actor_step, which reads this minibatch's bucket sums from the same
+ * workspace. The time-MLP and b_in gradients in grads are then NOT formed by the minibatch. */
+enum { DPPO_PPO_TIME_BWD_IN_STEP = 8 };
 
 /* ABI 9: the learnable DDIM eta's optimizer step (the original DPPO's EtaFixed trained by its own
  * AdamW every eta_update_interval minibatches, train_ppo_diffusion_agent.py:28-45, 358-359 — the
@@ -409,6 +439,21 @@ DPPO_API int dppo_optimizer_step_ex(const dppo_dims* d, int precision, float* pa
                            const float* critic_params, void* packed_critic, const double* metrics,
                            double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
                            const size_t* clear_bytes, int n_clear, void* stream);
+
+/* ABI 12: the actor's whole optimizer step after a PPO minibatch in ONE launch (train_ppo_diffusion_agent.py:
+ * 346-356 apply_gradients over actor_ft, plus the weight image every kernel reads): replaces the
+ * time-MLP backward, dppo_adamw and the pack (three launches on every minibatch's critical path).
+ * params / grads / m / v: the actor's flat range (dppo_actor_param_count elements). mode: DPPO_ADAMW_*,
+ * optionally | DPPO_STEP_L2_FROM_PL2 (the l2 gradient in its factored form) | DPPO_STEP_CLEAR_GRADS.
+ * workspace / batch_rows: the minibatch's PPO workspace when it ran with DPPO_PPO_TIME_BWD_IN_STEP
+ * (the time-MLP backward then runs in this launch from its bucket sums), or NULL / 0 when grads
+ * already hold every gradient. metrics / clear ranges as dppo_optimizer_step_ex. The TEMB table and
+ * the split sampler's tables are left stale (see DPPO_STEP_FUSED_PACK). */
+DPPO_API int dppo_actor_step(const dppo_dims* d, int precision, float* params, float* grads, float* m, float* v,
+                             int64_t step, float lr, float weight_decay, float beta1, float beta2, float eps, int mode,
+                             void* packed_actor, const void* workspace, int batch_rows, const double* metrics,
+                             double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
+                             const size_t* clear_bytes, int n_clear, void* stream);
 
 #ifdef __cplusplus
 }

@@ -568,8 +568,16 @@ def torch_adamw_step(param, grad, m, v, step, lr=1e-4, wd=0.0, beta1=0.9, beta2=
 # a18: RunningRewardScaler (util/reward_scaling.py:13-87)
 # ----------------------------------------------------------------------------------------------
 class RunningRewardScalerOracle:
-    def __init__(self, num_envs, cliprew=10.0, gamma=0.99, epsilon=1e-8):
-        self.mean, self.var, self.count = 0.0, 1.0, 1e-4        # :19-21
+    """util/reward_scaling.py:13-87. per_env=True keeps the reference's shapes: RunningMeanStd of
+    shape (num_envs,) updated with rets [E, S] reduced over axis 0 (the envs, :23-27, :65), joined by
+    NumPy broadcasting (so S == num_envs, or a length-1 side)."""
+
+    def __init__(self, num_envs, cliprew=10.0, gamma=0.99, epsilon=1e-8, per_env=False):
+        shape = (num_envs,) if per_env else ()
+        self.mean, self.var, self.count = np.zeros(shape), np.ones(shape), 1e-4   # :19-21
+        if not per_env:
+            self.mean, self.var = 0.0, 1.0
+        self.per_env = per_env
         self.ret = np.zeros(num_envs)
         self.cliprew, self.gamma, self.epsilon = cliprew, gamma, epsilon
 
@@ -580,8 +588,8 @@ class RunningRewardScalerOracle:
         for t in range(reward.shape[1]):                          # :84-87
             prev = rets[:, t] = reward[:, t] + (1 - first[:, t]) * self.gamma * prev
         self.ret = rets[:, -1]
-        x = rets.reshape(-1)
-        bm, bv, bc = x.mean(), x.var(), x.shape[0]                # :23-27
+        x = rets if self.per_env else rets.reshape(-1)            # :65
+        bm, bv, bc = x.mean(axis=0), x.var(axis=0), x.shape[0]    # :23-27
         delta = bm - self.mean                                    # :29-39
         tot = self.count + bc
         self.mean = self.mean + delta * bc / tot

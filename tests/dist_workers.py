@@ -1,4 +1,4 @@
-"""Rank bodies for tests/test_dist_cpu.py (world_size-2 gloo). Kept in their own module so the
+"""Rank bodies for tests/test_dist_cpu.py (gloo, world_size 2 / 4 / 8). Kept in their own module so the
 spawned processes import them without re-running the test module. Each body asserts against the
 single-process oracle on the full (un-sharded) data; mp.spawn re-raises a failure in the parent."""
 import os
@@ -25,7 +25,7 @@ def reward_rms(rank, world, port):
     from diffusionpolicyoptimization_amd.util import dist as D
     _init(rank, world, port)
     rng = np.random.default_rng(7)
-    S, E = 37, 8
+    S, E = 37, 16
     n_loc, off = D.shard_envs(E, world, rank)
     ref = O.RunningRewardScalerOracle(E)
     rms = (0.0, 1.0, 1e-4)
@@ -100,7 +100,7 @@ def episodes_and_ev(rank, world, port):
     from diffusionpolicyoptimization_amd.util import dist as D
     _init(rank, world, port)
     rng = np.random.default_rng(3)
-    S, E, act_steps = 60, 6, 4
+    S, E, act_steps = 60, 16, 4
     firsts = (rng.random((S + 1, E)) < 0.08).astype(np.float64)
     firsts[0] = 1
     rew = rng.normal(1.0, 2.0, (S, E))

@@ -1,4 +1,4 @@
-"""Data-parallel decomposition on world_size 2 with gloo on the CPU: every
+"""Data-parallel decomposition on world_size 2, 4 and 8 with gloo on the CPU: every
 cross-rank reduction the agent performs gives the single-process oracle's answer on the whole
 batch. The same util/dist.py functions run over RCCL on GPUs."""
 import socket
@@ -37,13 +37,18 @@ def test_chan_merge_matches_concatenation():
     np.testing.assert_allclose([mean, m2], [x.mean(), ((x - x.mean()) ** 2).sum()], rtol=1e-12)
 
 
-def test_reward_rms_world2():
-    _spawn(W.reward_rms)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_reward_rms(world):
+    """The rank-order Chan merge of the reward-RMS moments at 2 / 4 / 8 ranks."""
+    _spawn(W.reward_rms, world)
 
 
-def test_dp_gradient_world2():
-    _spawn(W.dp_gradient)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_dp_gradient(world):
+    """The advantage-moment table and the summed 1/B-scaled gradients at 2 / 4 / 8 ranks."""
+    _spawn(W.dp_gradient, world)
 
 
-def test_episode_stats_and_explained_variance_world2():
-    _spawn(W.episodes_and_ev)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_episode_stats_and_explained_variance(world):
+    _spawn(W.episodes_and_ev, world)

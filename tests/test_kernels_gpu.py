@@ -377,6 +377,55 @@ def test_reward_scale_matches_reference_goldens(cuda, entry):
     assert ci == 4
 
 
+@pytest.mark.parametrize("entry", ["RunningRewardScaler.__call__", "RunningRewardScaler.scale_"])
+def test_reward_scale_per_env_matches_reference_goldens(cuda, entry):
+    """a18's per_env=True branch (util/reward_scaling.py:51-66) against outputs of the reference's own
+    RunningRewardScaler(per_env=True) (tests/golden/reward_scaling_per_env.npz, make_golden.py):
+    the state of shape (num_envs,) updated with moments over the ENVS of each time column, NumPy
+    broadcasting included — S == E, E == 1 (the state takes S's shape), S == 1 (the output
+    broadcasts to [E, L]) — and the shape the reference rejects (E = 4, S = 50) raising ValueError.
+    scale_ (in place, time-major) skips the S == 1 < L calls, which cannot be in place."""
+    import torch
+    from diffusionpolicyoptimization_amd.util.reward_scaling import RunningRewardScaler
+    g = np.load(os.path.join(ROOT, "tests", "golden", "reward_scaling_per_env.npz"))
+    ci = 0
+    checked = 0
+    while f"c{ci}_meta" in g:
+        E, n_calls = (int(x) for x in g[f"c{ci}_meta"])
+        sc = RunningRewardScaler(E, per_env=True, device=cuda)
+        for k in range(n_calls):
+            p = f"c{ci}_k{k}_"
+            r, first = g[p + "reward"], g[p + "first"]
+            if p + "raises" in g:
+                with pytest.raises(ValueError):
+                    sc(reward=r, first=first)
+                checked += 1
+                break
+            if entry == "RunningRewardScaler.scale_" and r.shape[1] == 1 and np.asarray(g[p + "var"]).size > 1:
+                with pytest.raises(ValueError):
+                    sc.scale_(torch.tensor(np.ascontiguousarray(r.T), device=cuda),
+                              torch.tensor(np.ascontiguousarray(first.T).astype(np.uint8), device=cuda))
+                break
+            if entry == "RunningRewardScaler.__call__":
+                out = sc(reward=r, first=first)
+            else:
+                rt = torch.tensor(np.ascontiguousarray(r.T), device=cuda)
+                sc.scale_(rt, torch.tensor(np.ascontiguousarray(first.T).astype(np.uint8), device=cuda))
+                out = rt.cpu().numpy().T
+            torch.cuda.synchronize()
+            assert out.shape == g[p + "out"].shape
+            np.testing.assert_allclose(out, g[p + "out"], rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(sc.ret.cpu().numpy(), g[p + "ret"], rtol=1e-12, atol=1e-12)
+            st = sc.ret_rms
+            np.testing.assert_allclose(st.mean, np.broadcast_to(g[p + "mean"], st.mean.shape), rtol=1e-12, atol=1e-15)
+            assert st.mean.shape == np.asarray(g[p + "mean"]).reshape(-1).shape
+            np.testing.assert_allclose(st.var, g[p + "var"], rtol=1e-12)
+            np.testing.assert_allclose(st.count, g[p + "count"], rtol=1e-12)
+            checked += 1
+        ci += 1
+    assert ci == 6 and checked >= 8
+
+
 def test_feistel_bit_exact(cuda):
     from diffusionpolicyoptimization_amd import ops
     for n, seed, ep in [(320000, 42, 0), (1000, 7, 3), (13, 1, 1), (1, 5, 0)]:
@@ -531,11 +580,12 @@ def test_l2_deferred_minibatch_and_step(cuda, precision):
 @pytest.mark.parametrize("variant", ["fused", "clear"])
 def test_fused_optimizer_step_matches_two_launches(cuda, precision, net, variant):
     """ABI 11: an optimizer step with DPPO_STEP_FUSED_PACK | DPPO_STEP_CLEAR_GRADS (one launch: AdamW,
-    each element's image slots, then the last workgroup's W_OUT / T_OUT slots, TEMB rows and clears)
+    each element's image slots, the actor's W_OUT / T_OUT slots and the clears by the last workgroup)
     — or DPPO_STEP_CLEAR_GRADS alone (the clears ride on the pack launch) — gives bit-identical
-    parameters, moments and image bytes to AdamW + the pack (two launches), zeroes the range's
-    gradients and the given byte ranges, and leaves its ticket counter reusable (three steps in a
-    row on one stream)."""
+    parameters, moments and image bytes to AdamW + the pack (two launches) once the tables each path
+    leaves stale are re-derived (the fused actor step leaves TEMB to its consumers since ABI 12),
+    zeroes the range's gradients and the given byte ranges, and leaves its ticket counter reusable
+    (three steps in a row on one stream)."""
     import torch
     from diffusionpolicyoptimization_amd import ops
     from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
@@ -578,6 +628,8 @@ def test_fused_optimizer_step_matches_two_launches(cuda, precision, net, variant
             if fused and it:
                 G.copy_(G0)
             step(it + 2, 1e-3 * (it + 1), clear=clear)
+        if actor:   # the tables each path left stale (ABI 12: the fused actor step leaves TEMB stale too)
+            ops.refresh_sampler_tables(img)
         torch.cuda.synchronize()
         out[fused] = (P, M, V, img, G)
     for name, a, b in zip(("params", "m", "v", "image"), out[True][:4], out[False][:4]):
@@ -587,6 +639,111 @@ def test_fused_optimizer_step_matches_two_launches(cuda, precision, net, variant
     assert int(torch.count_nonzero(flat[:8])) == 0 and int(torch.count_nonzero(flat[2400:4800])) == 0
     assert int(torch.count_nonzero(flat[4816:5816])) == 0
     assert bool((flat[8:2400] != 0).any()) and bool((flat[5816:] != 0).any())   # nothing outside the ranges
+
+
+@pytest.mark.parametrize("net", ["actor", "critic"])
+def test_fused_step_clears_after_the_metrics_copy(cuda, net):
+    """the fused step's clear ranges are zeroed by its LAST workgroup, after every read of
+    the launch, so a range that overlaps the metric sums the step copies out (or its own gradients)
+    never zeroes them before they are read: metrics_out holds the sums, the range is zero after."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp_64env", [])
+    m = instantiate(cfg.model, device=cuda, seed=0)
+    d = m.dims
+    actor = net == "actor"
+    P = (m.actor_ft_params if actor else m.critic_params).clone()
+    img = (m.packed_ft if actor else m.packed_critic).clone()
+    n = P.numel()
+    G = torch.randn(n, device=cuda, generator=torch.Generator(device=cuda).manual_seed(2)) * 0.05
+    M, V = torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    met = torch.arange(1, 17, dtype=torch.float64, device=cuda)
+    out = ops.MappedDoubles(9)
+    packs = (P, img, None, None) if actor else (None, None, P, img)
+    step = ops.BoundOptimizerStep(d, m.precision, P, G, M, V, 0.004, 0.9, 0.999, 1e-7, "keras", *packs,
+                                  defer_sampler_tables=actor, fused_pack=True, clear_grads=True)
+    clear = type("C", (), {})()
+    ptrs = (ctypes.c_void_p * 4)(met.data_ptr())
+    nb = (ctypes.c_size_t * 4)(16 * 8)
+    clear.args = (ptrs, nb, 1)
+    step(1, 1e-3, metrics=met, metrics_out=out.address, n_metrics=8, metrics_tag=5, clear=clear)
+    out.wait_tag(8, 5)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.array[:8], np.arange(1, 9, dtype=np.float64))
+    assert int(torch.count_nonzero(met)) == 0 and int(torch.count_nonzero(G)) == 0
+    if actor:
+        ops.refresh_sampler_tables(img)
+        torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32", "fp16"])
+def test_actor_step_runs_the_time_mlp_backward(cuda, precision):
+    """ABI 12: dppo_actor_step with the minibatch's workspace (DPPO_PPO_TIME_BWD_IN_STEP) forms the
+    time-MLP and b_in gradients in its workgroup 0 — equal to the ones the minibatch's own
+    time_bwd forms (1e-5 of the tensor's max: the two minibatch runs differ by float-atomic order) —
+    and steps exactly as AdamW + a full pack of the gradients it formed (params, moments and image
+    bytes equal once the TEMB / sampler tables it leaves stale are re-derived). With clear_grads the
+    whole actor gradient range is zero afterwards."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp_64env",
+                      [f"model.precision={precision}"])
+    m = instantiate(cfg.model, device=cuda, seed=0)
+    d = m.dims
+    N, kf, rows = 64 * 40, d.ft_denoising_steps, 3000
+    gen = torch.Generator(device=cuda).manual_seed(0)
+    obs = torch.rand(N, d.sd, device=cuda, generator=gen) * 2 - 1
+    chains = torch.randn(N, kf + 1, d.xd, device=cuda, generator=gen) * 0.5
+    adv = torch.randn(N, device=cuda, generator=gen)
+    ret = torch.randn(N, device=cuda, generator=gen)
+    lp_old = torch.empty(N, kf, device=cuda)
+    ops.logprob(d, m.precision, m.packed_ft, m.sched, obs, chains, want_elem=False, lp_mean=lp_old)
+    lp_old += 0.01 * torch.randn(N, kf, device=cuda, generator=gen)
+    na = m.n_actor
+    f = m.bind_minibatch(obs, chains, lp_old, adv, ret, 11, rows)
+    f(3, 0, rows)
+    torch.cuda.synchronize()
+    g_ref = m.grads[:na].clone()                       # time_bwd in the minibatch (the r04 path)
+    f = m.bind_minibatch(obs, chains, lp_old, adv, ret, 11, rows, time_bwd_in_step=True)
+    f(3, 0, rows)
+    torch.cuda.synchronize()
+    offs, o = {}, 0
+    for name, shape in ops.actor_param_spec(d):
+        offs[name] = (o, o + int(np.prod(shape)))
+        o += offs[name][1] - offs[name][0]
+    time_rng = [offs[k] for k in ("time_w1", "time_b1", "time_w2", "time_b2", "in_b")]
+    g_in = m.grads[:na].clone()
+    P0, img0 = m.actor_ft_params.clone(), m.packed_ft.clone()
+    gen2 = torch.Generator(device=cuda).manual_seed(1)
+    M0 = torch.rand(na, device=cuda, generator=gen2) * 1e-4
+    V0 = torch.rand(na, device=cuda, generator=gen2) * 1e-7
+    ws = m.workspace(rows)
+    for clear in (False, True):
+        P, M, V, img, G = P0.clone(), M0.clone(), V0.clone(), img0.clone(), g_in.clone()
+        step = ops.BoundActorStep(d, m.precision, P, G, M, V, 0.004, 0.9, 0.999, 1e-7, "keras", img,
+                                  workspace=ws, batch_rows=rows, clear_grads=clear)
+        step(2, 1e-3)
+        ops.refresh_sampler_tables(img)
+        torch.cuda.synchronize()
+        if not clear:
+            g_formed = G.clone()
+            for lo, hi in time_rng:
+                a, b = g_formed[lo:hi], g_ref[lo:hi]
+                assert (a - b).abs().max() <= 1e-5 * b.abs().max() + 1e-12, (lo, float((a - b).abs().max()))
+            Pb, Mb, Vb = P0.clone(), M0.clone(), V0.clone()
+            ops.adamw(Pb, g_formed, Mb, Vb, 2, 1e-3, 0.004, 0.9, 0.999, 1e-7, "keras")
+            full = img0.clone()
+            ops.pack_actor(d, Pb, m.precision, out=full)
+            torch.cuda.synchronize()
+            assert torch.equal(P, Pb) and torch.equal(M, Mb) and torch.equal(V, Vb)
+            assert torch.equal(img, full)
+            ref = (P, M, V, img)
+        else:
+            assert int(torch.count_nonzero(G)) == 0
+            for a, b in zip((P, M, V, img), ref):
+                assert torch.equal(a, b)
 
 
 def test_value_moments(cuda):

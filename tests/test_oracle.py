@@ -46,6 +46,31 @@ def test_reward_scaler_matches_reference_goldens():
     assert ci == 4
 
 
+def test_reward_scaler_per_env_matches_reference_goldens():
+    """per_env=True (reward_scaling.py:51-66): the restatement against the reference's own outputs
+    (tests/golden/reward_scaling_per_env.npz), broadcasting cases and the rejected shape included."""
+    g = np.load(os.path.join(GOLD, "reward_scaling_per_env.npz"))
+    ci = 0
+    while f"c{ci}_meta" in g:
+        E, n_calls = (int(x) for x in g[f"c{ci}_meta"])
+        orc = O.RunningRewardScalerOracle(E, per_env=True)
+        for k in range(n_calls):
+            p = f"c{ci}_k{k}_"
+            if p + "raises" in g:
+                with pytest.raises(ValueError):
+                    orc(g[p + "reward"], g[p + "first"])
+                break
+            out = orc(g[p + "reward"], g[p + "first"])
+            assert out.shape == g[p + "out"].shape
+            np.testing.assert_allclose(out, g[p + "out"], rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(orc.mean, g[p + "mean"], rtol=1e-12, atol=1e-15)
+            np.testing.assert_allclose(orc.var, g[p + "var"], rtol=1e-12)
+            np.testing.assert_allclose(orc.count, g[p + "count"], rtol=1e-12)
+            np.testing.assert_allclose(orc.ret, g[p + "ret"], rtol=1e-12)
+        ci += 1
+    assert ci == 6
+
+
 def test_philox_known_answers():
     """Random123 kat_vectors for philox4x32_10."""
     kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),

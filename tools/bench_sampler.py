@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--envs", type=int, default=64)
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--config-dir", default=os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"))
+    ap.add_argument("--config-name", default="ft_ppo_diffusion_mlp_64env")
     ap.add_argument("--tag", default=os.environ.get("DPPO_SAMPLER_QD", "default"))
     args = ap.parse_args()
     import numpy as np
@@ -28,8 +30,7 @@ def main():
 
     from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
     dev = torch.device("cuda:0")
-    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp_64env",
-                      [f"model.precision={args.precision}"])
+    cfg = load_config(args.config_dir, args.config_name, [f"model.precision={args.precision}"])
     m = instantiate(cfg.model, device=dev, seed=0)
     cond = torch.rand(args.envs, m.dims.sd, device=dev, generator=torch.Generator(device=dev).manual_seed(1)) * 2 - 1
     m._call_id = 0
