@@ -105,6 +105,12 @@ _SIGNATURES = {
                                     _P, _P, _I, _U64, _P, _P, _I, _P]),
     "dppo_actor_step": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _I, _P, _P, _I, _U64,
                              _P, _P, _I, _P]),
+    "dppo_ipc_region_bytes": (_SZ, [_I64]),
+    "dppo_ipc_alloc": (_I, [_SZ, ctypes.POINTER(ctypes.c_void_p), _P]),
+    "dppo_ipc_open": (_I, [_P, ctypes.POINTER(ctypes.c_void_p)]),
+    "dppo_ipc_close": (_I, [_P]),
+    "dppo_ipc_free": (_I, [_P]),
+    "dppo_ipc_allreduce": (_I, [_P, _I, _I, _I64, _P, _I64, _U64, _P, _P]),
     "dppo_ppo_clear_ranges": (_I, [_DIMS, _I, _I, _P, _P, _I, _P, _P, ctypes.POINTER(ctypes.c_int)]),
     "dppo_value_moments": (_I, [_P, _P, _I64, _P, _P]),
     "dppo_refresh_sampler_tables": (_I, [_P, _P]),

@@ -187,6 +187,28 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
     def _allreduce(self, t):
         return allreduce_sum_(t)
 
+    def _bucket_allreduce(self, name, t):
+        """The per-minibatch gradient buckets (fp32, grads_ext slices): torch.distributed (RCCL,
+        the default) or, with train.allreduce = ipc (env DPPO_ALLREDUCE), dppo_ipc_allreduce over
+        IPC-mapped peer regions (util/ipc.py; one group per bucket, since the two buckets run on two
+        streams), on the current stream."""
+        groups = getattr(self, "_ipc_groups", None)
+        if groups is None:
+            return self._allreduce(t)
+        return groups[name](t)
+
+    def _ipc_setup(self):
+        """Collective (every rank, same point of the update): the IPC groups of the gradient buckets."""
+        mode = os.environ.get("DPPO_ALLREDUCE") or str(self.cfg.train.get("allreduce", "rccl"))
+        if mode != "ipc" or self.world_size == 1 or getattr(self, "_ipc_groups", None) is not None:
+            return
+        from ...util.ipc import IpcAllReduce
+        m = self.model
+        na, ne = m.n_actor, m.grads_ext.numel()
+        self._ipc_groups = {"actor": IpcAllReduce(na, device=self.device),
+                            "critic": IpcAllReduce(ne - na, device=self.device),
+                            "all": IpcAllReduce(ne, device=self.device)}
+
     # ------------------------------------------------------------------ rollout (agent :58-141)
     def rollout(self, eval_mode, defer_stats=False):
         """One rollout of S chunks; returns the episode statistics, or None with defer_stats (the
@@ -431,6 +453,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 return inf, self.target_kl is not None and inf["approx_kl"] > self.target_kl
 
             dp = self.world_size > 1
+            if dp:
+                self._ipc_setup()
             # every minibatch's advantage moments (norm_adv, diffusion_ppo.py:74-75) in one launch, and
             # on several GPUs one all-reduce of the whole table instead of one per minibatch
             n_mb = self.update_epochs * num_batch
@@ -578,12 +602,12 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                                 side.wait_event(self._ev_rows)
                                 m.grads_ext[ng:ng + 5].copy_(met[:5])
                                 m.grads_ext[ng + 5:ng + 6].copy_(met[8:9])   # learn_eta: d loss / d eta
-                                self._allreduce(m.grads_ext[na:])
+                                self._bucket_allreduce("critic", m.grads_ext[na:])
                                 met[:5].copy_(m.grads_ext[ng:ng + 5])
                                 met[8:9].copy_(m.grads_ext[ng + 5:ng + 6])
                                 self._ev_met.record(side)
                             run_mb(*mb_args, **mb_kw, part=5, metrics=met)   # actor dW + time MLP
-                            self._allreduce(m.grads_ext[:na])      # bucket 2: actor gradients
+                            self._bucket_allreduce("actor", m.grads_ext[:na])      # bucket 2: actor gradients
                             stream.wait_event(self._ev_met)
                         else:
                             run_mb(*mb_args, **mb_kw, part=1, metrics=met_p, stream=st_main,
@@ -596,7 +620,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             ng = m.grads.numel()
                             m.grads_ext[ng:ng + 5].copy_(m.metrics[:5])
                             m.grads_ext[ng + 5:ng + 6].copy_(m.metrics[8:9])
-                            self._allreduce(m.grads_ext)
+                            self._bucket_allreduce("all", m.grads_ext)
                             m.metrics[:5].copy_(m.grads_ext[ng:ng + 5])
                             m.metrics[8:9].copy_(m.grads_ext[ng + 5:ng + 6])
                     if self.minibatch_hook is not None:

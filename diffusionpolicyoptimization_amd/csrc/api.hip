@@ -88,7 +88,7 @@ const char* const kKtNames[KT_COUNT] = {
     "sampler", "actor_rowtile_train", "actor_rowtile_logprob", "critic_rowtile_train",
     "critic_rowtile_forward", "dw_kernel_actor", "dw_kernel_critic", "l2_back_kernel", "time_bwd_kernel",
     "adamw_kernel", "pack_all_kernel", "gae_kernel", "rets_kernel", "moments_kernel", "scale_apply_kernel",
-    "zero_kernel", "crit_rows_kernel", "adv_stats_kernel"};
+    "zero_kernel", "crit_rows_kernel", "adv_stats_kernel", "ipc_allreduce_kernel"};
 struct KtRec { int id; hipEvent_t e0, e1; };
 std::mutex g_kt_mu;
 std::vector<KtRec> g_kt;     // event pool; [0, g_kt_used) hold this window's launches

@@ -68,7 +68,7 @@ inline float dppo_grad_scale_rows(int p, int64_t global_rows) {
 enum DppoKt {
     KT_SAMPLER, KT_ACTOR_TRAIN, KT_ACTOR_LOGPROB, KT_CRITIC_TRAIN, KT_CRITIC_FWD, KT_DW_ACTOR, KT_DW_CRITIC,
     KT_L2_BACK, KT_TIME_BWD, KT_ADAMW, KT_PACK_ALL, KT_GAE, KT_RETS, KT_MOMENTS, KT_SCALE_APPLY, KT_ZERO,
-    KT_CRIT_ROWS, KT_ADV_STATS, KT_COUNT
+    KT_CRIT_ROWS, KT_ADV_STATS, KT_ALLREDUCE, KT_COUNT
 };
 extern volatile int g_dppo_kt_on;
 int dppo_kt_begin(int id, hipStream_t s);   // -1 when disabled

@@ -168,41 +168,55 @@ DPPO_ENV_API void dppo_env_publish_tagged(int64_t count, const float* obs, uint6
     }
 }
 
-/* dppo_env_step_gated with the tagged protocol both ways: spin until every action granule of
- * act_tagged carries act_tag (the device's stores are the ready flag: no wait for the done counter,
- * whose bit 31 still reports a device-side timeout), decode them into `actions` (the float buffer the
- * caller keeps), step, and when no episode ended publish the observation as granules with `tag`. */
+/* dppo_env_step_gated with the tagged protocol both ways: the envs go in blocks of EB = 16 (the
+ * split sampler's env group: each group of a pre-enqueued launch polls only its own 16 envs'
+ * observation granules), and for each block in turn: spin until its action granules in act_tagged
+ * carry act_tag (the device's stores are the ready flag: no wait for the done counter, whose bit 31
+ * still reports a device-side timeout), decode them into `actions` (the float buffer the caller
+ * keeps), step the block and, when no episode of the block ended, publish its observation as
+ * granules with `tag` at once — so the next launch's first groups run while the host still steps
+ * the later blocks. Returns n_done, with DPPO_ENV_PUBLISHED when every block was published (an
+ * ended episode leaves its block to the caller, which resets and publishes the whole observation:
+ * the early blocks' granules are rewritten with the same tag and values). */
 DPPO_ENV_API int dppo_env_step_gated_tagged(int E, int Do, int Da, int act_steps, int Ta, int max_steps, int n_obs_steps,
                                             const double* AT, const double* B, const double* c, const double* goal,
                                             double* state, int64_t* cnt, float* actions, double* reward,
                                             uint8_t* terminated, uint8_t* truncated, float* obs_out,
                                             const volatile uint32_t* done, const uint64_t* act_tagged,
                                             uint32_t act_tag, uint64_t* obs_tagged, uint32_t tag, double timeout_s) {
-    const int64_t na = (int64_t)E * Ta * Da;
+    const int64_t per = (int64_t)Ta * Da, per_obs = (int64_t)n_obs_steps * Do;
     double t_end = -1.0;
-    int64_t i = 0;   /* granules before i are known to carry act_tag */
-    for (uint32_t spins = 0;; ++spins) {
-        while (i < na) {
-            const uint64_t x = __atomic_load_n(act_tagged + i, __ATOMIC_ACQUIRE);
-            if ((uint32_t)(x >> 32) != act_tag) break;
-            const uint32_t bits = (uint32_t)x;
-            memcpy(actions + i, &bits, 4);
-            ++i;
+    int n_done = 0, all_published = 1;
+    for (int e0 = 0; e0 < E; e0 += EB) {
+        const int nb = E - e0 < EB ? E - e0 : EB;
+        int64_t i = e0 * per;   /* granules before i are known to carry act_tag */
+        const int64_t end = (e0 + nb) * per;
+        for (uint32_t spins = 0;; ++spins) {
+            while (i < end) {
+                const uint64_t x = __atomic_load_n(act_tagged + i, __ATOMIC_ACQUIRE);
+                if ((uint32_t)(x >> 32) != act_tag) break;
+                const uint32_t bits = (uint32_t)x;
+                memcpy(actions + i, &bits, 4);
+                ++i;
+            }
+            if (i == end) break;
+            if (__atomic_load_n(done, __ATOMIC_ACQUIRE) & 0x80000000u) return -2;
+            _mm_pause();
+            if ((spins & 1023u) == 1023u) {
+                const double now = env_now_s();
+                if (t_end < 0.0) t_end = now + timeout_s;
+                else if (now > t_end) return -1;
+            }
         }
-        if (i == na) break;
-        if (__atomic_load_n(done, __ATOMIC_ACQUIRE) & 0x80000000u) return -2;
-        _mm_pause();
-        if ((spins & 1023u) == 1023u) {
-            const double now = env_now_s();
-            if (t_end < 0.0) t_end = now + timeout_s;
-            else if (now > t_end) return -1;
-        }
+        const int nd = dppo_env_step(nb, Do, Da, act_steps, Ta, max_steps, n_obs_steps, AT, B, c, goal,
+                                     state + (size_t)e0 * Do, cnt + e0, actions + (size_t)e0 * per, reward + e0,
+                                     terminated + e0, truncated + e0, obs_out + (size_t)e0 * per_obs);
+        n_done += nd;
+        if (nd == 0 && obs_tagged)
+            dppo_env_publish_tagged((int64_t)nb * per_obs, obs_out + (size_t)e0 * per_obs, obs_tagged + (size_t)e0 * per_obs, tag);
+        else
+            all_published = 0;
     }
-    const int n_done = dppo_env_step(E, Do, Da, act_steps, Ta, max_steps, n_obs_steps, AT, B, c, goal, state, cnt,
-                                     actions, reward, terminated, truncated, obs_out);
-    if (n_done == 0 && obs_tagged) {
-        dppo_env_publish_tagged((int64_t)E * n_obs_steps * Do, obs_out, obs_tagged, tag);
-        return DPPO_ENV_PUBLISHED;
-    }
+    if (all_published && obs_tagged) return n_done | DPPO_ENV_PUBLISHED;
     return n_done;
 }

@@ -20,9 +20,9 @@
  *
  * The gated entries (dppo_lowdim_step_gated_tagged / _gated) are the pipelined rollout's host
  * step (ops.RolloutPipe): each slice thread polls ITS envs' action granules in mapped
- * memory, steps them, and publishes ITS envs' observation granules as soon as they are final, so
- * the sampler launch for the next chunk (already enqueued, polling per granule) starts on the
- * observation the moment the last slice publishes.
+ * memory, steps them, and publishes ITS envs' observation granules as soon as they are final, 16
+ * envs (one sampler env group) at a time, so the sampler launch for the next chunk (already
+ * enqueued, each group polling its own granules) starts group by group while the host still steps.
  *
  * Arithmetic follows NumPy's on the reference's dtypes, bit for bit (compiled with
  * -ffp-contract=off): the action map is float32 ((a + 1) / 2 * (max - min) + min, every operand
@@ -76,20 +76,33 @@ typedef struct {
     pthread_cond_t cv;
 } Pool;
 
+/* per-env MultiStep flags, one cache line per env: the slice threads write their own envs' flags
+ * every sub-step, and packed bytes would put neighbouring slices on one line (false sharing) */
+typedef struct {
+    uint8_t term, trunc, alive, last_done;
+    uint8_t pad[60];
+} EnvFlags;
+
+/* one thread's sub-step scratch (the rows of its slice), in allocations of its own */
+typedef struct {
+    int32_t* idx;
+    double *act, *obs, *rew;
+    uint8_t* done;
+    int8_t* tl;
+} Scratch;
+
 typedef struct LowdimEnv {
     int E, Do, Da, To, act_steps, max_episode_steps, reset_within_step;
     dppo_sim_step_fn step;
     dppo_sim_reset_fn reset;
     void* ctx;
     float *obs_min, *obs_max, *act_min, *act_max;   /* NULL: identity maps (no normalisation file) */
+    float *obs_rng, *act_rng;   /* (float)(max - min) + 1e-6f and max - min, the maps' float32 ranges */
     int64_t* cnt;        /* MultiStep.cnt per env */
     double* hist;        /* [E][To][Do]: the last To normalised observations (MultiStep.obs deque) */
-    /* scratch, [E]-sized; slice [lo, hi) uses rows [lo, hi) */
-    int32_t* idx;
-    double *act, *obs, *rew;
-    uint8_t* done;
-    int8_t* tl;
-    uint8_t *term, *trunc, *alive, *last_done;
+    EnvFlags* fl;        /* [E] */
+    Scratch* scr;        /* [nscr] per pool thread (scr[0]: the caller's, E rows) */
+    int nscr;
     Pool* pool;          /* NULL: one thread */
     Chunk chunk;         /* the chunk in flight */
 } LowdimEnv;
@@ -102,40 +115,82 @@ static double mono_s(void) {
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
-/* mujoco_locomotion_lowdim.py:57-58, n rows of Do: out = 2 * ((raw - min) / (max - min + 1e-6) - 0.5) */
-DPPO_ENV_API void dppo_lowdim_normalize_obs(int64_t n, int Do, const double* raw, const float* mn, const float* mx,
-                                            double* out) {
-    for (int64_t r = 0; r < n; ++r)
-        for (int j = 0; j < Do; ++j) {
-            const float rng = (float)(mx[j] - mn[j]) + 1e-6f;      /* float32 array + weak python float */
-            const double v = (raw[r * Do + j] - (double)mn[j]) / (double)rng;
-            out[r * Do + j] = 2.0 * (v - 0.5);
-        }
+/* mujoco_locomotion_lowdim.py:57-58, one row of Do: out = 2 * ((raw - min) / (max - min + 1e-6) - 0.5),
+ * rng[j] = (float)(max - min) + 1e-6f (float32 array + weak python float) */
+static inline void norm_obs_row(int Do, const double* raw, const float* mn, const float* rng, double* out) {
+    for (int j = 0; j < Do; ++j) {
+        const double v = (raw[j] - (double)mn[j]) / (double)rng[j];
+        out[j] = 2.0 * (v - 0.5);
+    }
 }
+static inline float obs_rng_of(float mn, float mx) { return (float)(mx - mn) + 1e-6f; }
 
 /* mujoco_locomotion_lowdim.py:60-62, float32: a01 = (a + 1) / 2; raw = a01 * (max - min) + min */
+static inline void unnorm_act_row(int Da, const float* a, const float* mn, const float* rng, float* out) {
+    for (int i = 0; i < Da; ++i) {
+        const float a01 = (a[i] + 1.0f) / 2.0f;
+        const float m = a01 * rng[i];
+        out[i] = m + mn[i];
+    }
+}
+
+DPPO_ENV_API void dppo_lowdim_normalize_obs(int64_t n, int Do, const double* raw, const float* mn, const float* mx,
+                                            double* out) {
+    float rng[256];
+    if (Do > 256) return;
+    for (int j = 0; j < Do; ++j) rng[j] = obs_rng_of(mn[j], mx[j]);
+    for (int64_t r = 0; r < n; ++r) norm_obs_row(Do, raw + r * Do, mn, rng, out + r * Do);
+}
+
 DPPO_ENV_API void dppo_lowdim_unnormalize_action(int64_t n, int Da, const float* a, const float* mn, const float* mx,
                                                  float* out) {
-    for (int64_t r = 0; r < n; ++r)
-        for (int i = 0; i < Da; ++i) {
-            const float a01 = (a[r * Da + i] + 1.0f) / 2.0f;
-            const float rng = mx[i] - mn[i];
-            const float m = a01 * rng;
-            out[r * Da + i] = m + mn[i];
-        }
+    float rng[64];
+    if (Da > 64) return;
+    for (int i = 0; i < Da; ++i) rng[i] = mx[i] - mn[i];
+    for (int64_t r = 0; r < n; ++r) unnorm_act_row(Da, a + r * Da, mn, rng, out + r * Da);
 }
 
 static void* xcalloc(size_t n, size_t s) { return calloc(n ? n : 1, s); }
 
 static void pool_destroy(Pool* p);
 
+static void scratch_free(LowdimEnv* e) {
+    for (int t = 0; t < e->nscr; ++t) {
+        Scratch* c = &e->scr[t];
+        free(c->idx); free(c->act); free(c->obs); free(c->rew); free(c->done); free(c->tl);
+    }
+    free(e->scr);
+    e->scr = NULL;
+    e->nscr = 0;
+}
+
+/* n scratch sets of `rows` rows each (64-B aligned allocations: no two threads' scratch shares a line) */
+static int scratch_alloc(LowdimEnv* e, int n, int rows) {
+    scratch_free(e);
+    e->scr = (Scratch*)xcalloc(n, sizeof(Scratch));
+    if (!e->scr) return -1;
+    e->nscr = n;
+    const size_t r64 = ((size_t)rows + 63) & ~(size_t)63;
+    for (int t = 0; t < n; ++t) {
+        Scratch* c = &e->scr[t];
+        c->idx = (int32_t*)aligned_alloc(64, 4 * r64);
+        c->act = (double*)aligned_alloc(64, 8 * r64 * e->Da);
+        c->obs = (double*)aligned_alloc(64, 8 * r64 * e->Do);
+        c->rew = (double*)aligned_alloc(64, 8 * r64);
+        c->done = (uint8_t*)aligned_alloc(64, r64);
+        c->tl = (int8_t*)aligned_alloc(64, r64);
+        if (!c->idx || !c->act || !c->obs || !c->rew || !c->done || !c->tl) return -1;
+    }
+    return 0;
+}
+
 DPPO_ENV_API void dppo_lowdim_destroy(void* h) {
     LowdimEnv* e = (LowdimEnv*)h;
     if (!e) return;
     pool_destroy(e->pool);
-    free(e->obs_min); free(e->obs_max); free(e->act_min); free(e->act_max);
-    free(e->cnt); free(e->hist); free(e->idx); free(e->act); free(e->obs); free(e->rew);
-    free(e->done); free(e->tl); free(e->term); free(e->trunc); free(e->alive); free(e->last_done);
+    free(e->obs_min); free(e->obs_max); free(e->act_min); free(e->act_max); free(e->obs_rng); free(e->act_rng);
+    free(e->cnt); free(e->hist); free(e->fl);
+    scratch_free(e);
     free(e);
 }
 
@@ -154,30 +209,23 @@ DPPO_ENV_API void* dppo_lowdim_create(int E, int Do, int Da, int To, int act_ste
     e->max_episode_steps = max_episode_steps; e->reset_within_step = reset_within_step;
     e->step = step; e->reset = reset; e->ctx = ctx;
     if (obs_min) {
-        e->obs_min = (float*)xcalloc(Do, 4); e->obs_max = (float*)xcalloc(Do, 4);
+        e->obs_min = (float*)xcalloc(Do, 4); e->obs_max = (float*)xcalloc(Do, 4); e->obs_rng = (float*)xcalloc(Do, 4);
         memcpy(e->obs_min, obs_min, 4 * (size_t)Do); memcpy(e->obs_max, obs_max, 4 * (size_t)Do);
+        for (int j = 0; j < Do; ++j) e->obs_rng[j] = obs_rng_of(obs_min[j], obs_max[j]);
     }
     if (act_min) {
-        e->act_min = (float*)xcalloc(Da, 4); e->act_max = (float*)xcalloc(Da, 4);
+        e->act_min = (float*)xcalloc(Da, 4); e->act_max = (float*)xcalloc(Da, 4); e->act_rng = (float*)xcalloc(Da, 4);
         memcpy(e->act_min, act_min, 4 * (size_t)Da); memcpy(e->act_max, act_max, 4 * (size_t)Da);
+        for (int i = 0; i < Da; ++i) e->act_rng[i] = act_max[i] - act_min[i];
     }
     e->cnt = (int64_t*)xcalloc(E, 8);
     e->hist = (double*)xcalloc((size_t)E * To * Do, 8);
-    e->idx = (int32_t*)xcalloc(E, 4);
-    e->act = (double*)xcalloc((size_t)E * Da, 8);
-    e->obs = (double*)xcalloc((size_t)E * Do, 8);
-    e->rew = (double*)xcalloc(E, 8);
-    e->done = (uint8_t*)xcalloc(E, 1);
-    e->tl = (int8_t*)xcalloc(E, 1);
-    e->term = (uint8_t*)xcalloc(E, 1);
-    e->trunc = (uint8_t*)xcalloc(E, 1);
-    e->alive = (uint8_t*)xcalloc(E, 1);
-    e->last_done = (uint8_t*)xcalloc(E, 1);
-    if (!e->cnt || !e->hist || !e->idx || !e->act || !e->obs || !e->rew || !e->done || !e->tl || !e->term ||
-        !e->trunc || !e->alive || !e->last_done) {
+    e->fl = (EnvFlags*)aligned_alloc(64, sizeof(EnvFlags) * (size_t)E);
+    if (!e->cnt || !e->hist || !e->fl || scratch_alloc(e, 1, E)) {
         dppo_lowdim_destroy(e);
         return NULL;
     }
+    memset(e->fl, 0, sizeof(EnvFlags) * (size_t)E);
     return e;
 }
 
@@ -187,7 +235,7 @@ static void hist_put(LowdimEnv* e, int i, const double* raw, int fill) {
     double* h = e->hist + (size_t)i * e->To * e->Do;
     double v[256];
     double* nv = e->Do <= 256 ? v : (double*)malloc(8 * (size_t)e->Do);
-    if (e->obs_min) dppo_lowdim_normalize_obs(1, e->Do, raw, e->obs_min, e->obs_max, nv);
+    if (e->obs_min) norm_obs_row(e->Do, raw, e->obs_min, e->obs_rng, nv);
     else memcpy(nv, raw, 8 * (size_t)e->Do);
     if (fill) {
         for (int o = 0; o < e->To; ++o) memcpy(h + (size_t)o * e->Do, nv, 8 * (size_t)e->Do);
@@ -219,7 +267,7 @@ static int reset_envs(LowdimEnv* e, int n, const int32_t* idx, double* obs) {
 /* ---- the pool: persistent threads, slice t of a chunk = envs [E t / n, E (t + 1) / n) ---- */
 static int slice_lo(const LowdimEnv* e, int n, int t) { return (int)((int64_t)e->E * t / n); }
 
-static int run_slice(LowdimEnv* e, int lo, int hi);
+static int run_slice(LowdimEnv* e, int t, int lo, int hi);
 
 typedef struct { Pool* p; int t; } WorkerArg;
 
@@ -251,7 +299,7 @@ static void* worker(void* a) {
         if (p->stop) break;
         seen = __atomic_load_n(&p->gen, __ATOMIC_ACQUIRE);
         LowdimEnv* e = p->env;
-        p->rc[t] = run_slice(e, slice_lo(e, p->n, t), slice_lo(e, p->n, t + 1));
+        p->rc[t] = run_slice(e, t, slice_lo(e, p->n, t), slice_lo(e, p->n, t + 1));
         __atomic_fetch_sub(&p->pending, 1, __ATOMIC_ACQ_REL);
     }
     return NULL;
@@ -283,6 +331,7 @@ DPPO_ENV_API int dppo_lowdim_set_threads(void* h, int n, double spin_us) {
     }
     pool_destroy(e->pool);
     e->pool = NULL;
+    if (scratch_alloc(e, n, e->E)) return -1;   /* one scratch set per thread (set 0 also serves resets) */
     if (n == 1) return 1;
     Pool* p = (Pool*)xcalloc(1, sizeof(Pool));
     if (!p) return -1;
@@ -315,13 +364,13 @@ DPPO_ENV_API int dppo_lowdim_threads(void* h) {
  * results, or the most negative one. */
 static int run_chunk(LowdimEnv* e) {
     Pool* p = e->pool;
-    if (!p) return run_slice(e, 0, e->E);
+    if (!p) return run_slice(e, 0, 0, e->E);
     __atomic_store_n(&p->pending, p->n - 1, __ATOMIC_RELEASE);
     pthread_mutex_lock(&p->mu);
     __atomic_fetch_add(&p->gen, 1, __ATOMIC_ACQ_REL);
     if (p->sleepers) pthread_cond_broadcast(&p->cv);
     pthread_mutex_unlock(&p->mu);
-    p->rc[0] = run_slice(e, 0, slice_lo(e, p->n, 1));
+    p->rc[0] = run_slice(e, 0, 0, slice_lo(e, p->n, 1));
     /* yield now and then: a worker the scheduler placed on this CPU must get to run */
     for (uint32_t spins = 1; __atomic_load_n(&p->pending, __ATOMIC_ACQUIRE) > 0; ++spins) {
         _mm_pause();
@@ -361,7 +410,7 @@ static int slice_wait_actions(LowdimEnv* e, int lo, int hi) {
 }
 
 /* One chunk for envs [lo, hi) (multi_step.py:135-192); see dppo_lowdim_step. */
-static int run_slice(LowdimEnv* e, int lo, int hi) {
+static int run_block(LowdimEnv* e, int t, int lo, int hi) {
     const Chunk* c = &e->chunk;
     const int Do = e->Do, Da = e->Da, To = e->To, Ta = c->Ta;
     if (lo >= hi) return 0;
@@ -369,17 +418,19 @@ static int run_slice(LowdimEnv* e, int lo, int hi) {
         const int w = slice_wait_actions(e, lo, hi);
         if (w) return w;
     }
-    int32_t* idx = e->idx + lo;
-    double* act = e->act + (size_t)lo * Da;
-    double* obs = e->obs + (size_t)lo * Do;
-    double* rew = e->rew + lo;
-    uint8_t* done = e->done + lo;
-    int8_t* tl = e->tl + lo;
+    const Scratch* sc = &e->scr[t];
+    int32_t* idx = sc->idx;
+    double* act = sc->act;
+    double* obs = sc->obs;
+    double* rew = sc->rew;
+    uint8_t* done = sc->done;
+    int8_t* tl = sc->tl;
+    EnvFlags* fl = e->fl;
     const int nsub = e->act_steps < Ta ? e->act_steps : Ta;
     for (int i = lo; i < hi; ++i) {
-        e->term[i] = e->trunc[i] = 0;
-        e->alive[i] = 1;
-        e->last_done[i] = 0;
+        fl[i].term = fl[i].trunc = 0;
+        fl[i].alive = 1;
+        fl[i].last_done = 0;
         c->reward[i] = 0.0;
         if (c->has_final) c->has_final[i] = 0;
     }
@@ -387,16 +438,16 @@ static int run_slice(LowdimEnv* e, int lo, int hi) {
         /* for act_step, act in enumerate(action): self.cnt += 1; if terminated or truncated: break */
         int n = 0;
         for (int i = lo; i < hi; ++i) {
-            if (!e->alive[i]) continue;
+            if (!fl[i].alive) continue;
             e->cnt[i] += 1;
-            if (e->term[i] || e->trunc[i]) {
-                e->alive[i] = 0;
+            if (fl[i].term || fl[i].trunc) {
+                fl[i].alive = 0;
                 continue;
             }
             idx[n] = i;
             const float* a = c->actions + ((size_t)i * Ta + k) * Da;
             float raw[64];
-            if (e->act_min) dppo_lowdim_unnormalize_action(1, Da, a, e->act_min, e->act_max, raw);
+            if (e->act_min) unnorm_act_row(Da, a, e->act_min, e->act_rng, raw);
             else memcpy(raw, a, 4 * (size_t)Da);
             for (int j = 0; j < Da; ++j) act[(size_t)n * Da + j] = (double)raw[j];
             ++n;
@@ -408,25 +459,25 @@ static int run_slice(LowdimEnv* e, int lo, int hi) {
             hist_put(e, i, obs + (size_t)r * Do, 0);
             c->reward[i] += rew[r];                                /* reward_agg_method = "sum" */
             if (tl[r] < 0) {                                       /* no "TimeLimit.truncated" in info */
-                if (done[r]) e->term[i] = 1;
-                else if (e->max_episode_steps > 0 && e->cnt[i] >= e->max_episode_steps) e->trunc[i] = 1;
+                if (done[r]) fl[i].term = 1;
+                else if (e->max_episode_steps > 0 && e->cnt[i] >= e->max_episode_steps) fl[i].trunc = 1;
             } else {
-                e->trunc[i] = (uint8_t)(tl[r] != 0);
-                e->term[i] = done[r] ? 1 : 0;
+                fl[i].trunc = (uint8_t)(tl[r] != 0);
+                fl[i].term = done[r] ? 1 : 0;
             }
-            e->last_done[i] = e->term[i] || e->trunc[i];          /* self.done[-1] */
+            fl[i].last_done = fl[i].term || fl[i].trunc;          /* self.done[-1] */
         }
     }
     /* the returned observation, then reset within the step where the chunk ended (:172-187) */
     int n_done = 0, nr = 0;
     for (int i = lo; i < hi; ++i) {
-        c->terminated[i] = e->term[i];
-        c->truncated[i] = e->trunc[i];
+        c->terminated[i] = fl[i].term;
+        c->truncated[i] = fl[i].trunc;
         hist_out(e, i, c->obs_out);
-        if (e->last_done[i]) {
+        if (fl[i].last_done) {
             ++n_done;
             if (e->reset_within_step) {
-                if (e->trunc[i] && c->final_obs) {
+                if (fl[i].trunc && c->final_obs) {
                     memcpy(c->final_obs + (size_t)i * To * Do, c->obs_out + (size_t)i * To * Do, 4 * (size_t)To * Do);
                     c->has_final[i] = 1;
                 }
@@ -450,11 +501,27 @@ static int run_slice(LowdimEnv* e, int lo, int hi) {
     return n_done;
 }
 
+/* A slice goes in blocks of ENV_GROUP envs, the split sampler's env group (each group of a
+ * pre-enqueued launch polls only its own envs' observation granules): block by block the slice
+ * waits for the block's actions, steps it and publishes it, so the device's first groups start
+ * while the host still steps later blocks. Envs are independent (per-env seeded resets), so the
+ * blocking changes no value. */
+#define ENV_GROUP 16
+static int run_slice(LowdimEnv* e, int t, int lo, int hi) {
+    int n_done = 0;
+    for (int b = lo; b < hi; b += ENV_GROUP) {
+        const int rc = run_block(e, t, b, b + ENV_GROUP < hi ? b + ENV_GROUP : hi);
+        if (rc < 0) return rc;
+        n_done += rc;
+    }
+    return n_done;
+}
+
 /* AsyncVectorEnv.reset_arg -> MultiStep.reset for every env; obs_out [E][To][Do] float32 */
 DPPO_ENV_API int dppo_lowdim_reset_all(void* h, float* obs_out) {
     LowdimEnv* e = (LowdimEnv*)h;
-    for (int i = 0; i < e->E; ++i) e->idx[i] = i;
-    if (reset_envs(e, e->E, e->idx, e->obs)) return -1;
+    for (int i = 0; i < e->E; ++i) e->scr[0].idx[i] = i;
+    if (reset_envs(e, e->E, e->scr[0].idx, e->scr[0].obs)) return -1;
     for (int i = 0; i < e->E; ++i) hist_out(e, i, obs_out);
     return 0;
 }
@@ -463,7 +530,7 @@ DPPO_ENV_API int dppo_lowdim_reset_one(void* h, int env, float* obs_out) {
     LowdimEnv* e = (LowdimEnv*)h;
     if (env < 0 || env >= e->E) return -1;
     int32_t one = env;
-    if (reset_envs(e, 1, &one, e->obs)) return -1;
+    if (reset_envs(e, 1, &one, e->scr[0].obs)) return -1;
     hist_out(e, env, obs_out);
     return 0;
 }
@@ -603,48 +670,66 @@ DPPO_ENV_API void dppo_sim_linear_destroy(void* p) {
     free(m->seed); free(m->episode); free(m);
 }
 
+/* Blocks of up to SIM_RB rows are stepped structure-of-arrays (coordinate-major scratch on the stack,
+ * so concurrent slices share nothing), with every row's sum still taken term by term in the oracle's
+ * order: sn[j] = c[j] + sum_q A[j][q] s[q] + sum_q B[q][j] a[q] (q ascending), err and |a|^2 likewise.
+ * The loops over the block's rows are innermost, so they vectorise across envs without reassociating
+ * any row's arithmetic (the results are bit-identical to one row at a time). */
+#define SIM_RB 32
 DPPO_ENV_API int dppo_sim_linear_step(void* ctx, int n, const int32_t* idx, const double* act, double* obs,
                                       double* reward, uint8_t* done, int8_t* time_limit) {
     LinearSim* m = (LinearSim*)ctx;
     const int Do = m->Do, Da = m->Da;
-    double sn[256];
-    if (Do > 256) return 1;
-    for (int r = 0; r < n; ++r) {
-        double* s = m->s + (size_t)idx[r] * Do;
-        const double* a = act + (size_t)r * Da;
-        double err = 0.0, asq = 0.0;
-        int out = 0;
-        /* sn[j] = c[j] + sum_q A[j][q] s[q] + sum_q B[q][j] a[q], each row's terms added in that
-         * order (the oracle's): the loops run over j innermost so they vectorise without
-         * reassociating any row's sum */
-        for (int j = 0; j < Do; ++j) sn[j] = m->c[j];
-        for (int q = 0; q < Do; ++q) {
-            const double sq = s[q];
-            const double* at = m->AT + (size_t)q * Do;
-            for (int j = 0; j < Do; ++j) sn[j] += at[j] * sq;
-        }
-        for (int q = 0; q < Da; ++q) {
-            const double aq = a[q];
-            const double* b = m->B + (size_t)q * Do;
-            for (int j = 0; j < Do; ++j) sn[j] += b[j] * aq;
+    if (Do > 64 || Da > 64) return 1;
+    double xs[64 * SIM_RB], xn[64 * SIM_RB], xa[64 * SIM_RB], err[SIM_RB], asq[SIM_RB];
+    int out[SIM_RB];
+    for (int r0 = 0; r0 < n; r0 += SIM_RB) {
+        const int nb = n - r0 < SIM_RB ? n - r0 : SIM_RB;
+        for (int r = 0; r < nb; ++r) {
+            const double* s = m->s + (size_t)idx[r0 + r] * Do;
+            for (int q = 0; q < Do; ++q) xs[q * SIM_RB + r] = s[q];
+            for (int q = 0; q < Da; ++q) xa[q * SIM_RB + r] = act[(size_t)(r0 + r) * Da + q];
+            err[r] = 0.0; asq[r] = 0.0; out[r] = 0;
         }
         for (int j = 0; j < Do; ++j) {
-            const double v = sn[j];
-            const double d = v - m->goal[j];
-            err += d * d;
-            const double dc = v - m->center[j];
-            out |= dc > m->bound[j] || dc < -m->bound[j];
+            double* o = xn + j * SIM_RB;
+            const double cj = m->c[j];
+            for (int r = 0; r < nb; ++r) o[r] = cj;
+            for (int q = 0; q < Do; ++q) {
+                const double aj = m->A[(size_t)j * Do + q];
+                const double* x = xs + q * SIM_RB;
+                for (int r = 0; r < nb; ++r) o[r] += aj * x[r];
+            }
+            for (int q = 0; q < Da; ++q) {
+                const double bj = m->B[(size_t)q * Do + j];
+                const double* x = xa + q * SIM_RB;
+                for (int r = 0; r < nb; ++r) o[r] += bj * x[r];
+            }
+            const double gj = m->goal[j], cen = m->center[j], bd = m->bound[j];
+            for (int r = 0; r < nb; ++r) {
+                const double d = o[r] - gj;
+                err[r] += d * d;
+                const double dc = o[r] - cen;
+                out[r] |= dc > bd || dc < -bd;
+            }
         }
-        for (int q = 0; q < Da; ++q) asq += a[q] * a[q];
-        memcpy(s, sn, 8 * (size_t)Do);
-        memcpy(obs + (size_t)r * Do, sn, 8 * (size_t)Do);
-        reward[r] = 1.0 - err / Do - 1e-3 * asq;
-        done[r] = (uint8_t)out;
-        time_limit[r] = -1;
-        if (m->cost_s > 0) {
-            const double t_end = mono_s() + m->cost_s;
-            while (mono_s() < t_end) _mm_pause();
+        for (int q = 0; q < Da; ++q) {
+            const double* x = xa + q * SIM_RB;
+            for (int r = 0; r < nb; ++r) asq[r] += x[r] * x[r];
         }
+        for (int r = 0; r < nb; ++r) {
+            double* s = m->s + (size_t)idx[r0 + r] * Do;
+            double* ob = obs + (size_t)(r0 + r) * Do;
+            for (int j = 0; j < Do; ++j) s[j] = ob[j] = xn[j * SIM_RB + r];
+            reward[r0 + r] = 1.0 - err[r] / Do - 1e-3 * asq[r];
+            done[r0 + r] = (uint8_t)out[r];
+            time_limit[r0 + r] = -1;
+        }
+        if (m->cost_s > 0)
+            for (int r = 0; r < nb; ++r) {
+                const double t_end = mono_s() + m->cost_s;
+                while (mono_s() < t_end) _mm_pause();
+            }
     }
     return 0;
 }

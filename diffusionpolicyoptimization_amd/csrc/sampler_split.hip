@@ -1906,13 +1906,22 @@ int launch_split_k(const SplitArgs& sa, hipStream_t s) {
 // waves per member of the P = 4 kernel. The kernel also builds with 4 (one wave per SIMD, 512
 // registers: the l1 / l2 fragments partly in AGPRs, each wave two l1 n-tiles and eight in-Dense /
 // l2 n-tiles): measured 63.7 vs 59.3 us per launch at 8 (no second wave to hide its latencies), so
-// only 8 is instantiated
-constexpr int SPLIT4_WAVES = 8;
+// 8 is the default (-DDPPO_S4_WAVES=4 builds the one-wave-per-SIMD form as an A/B variant)
+#ifndef DPPO_S4_WAVES
+#define DPPO_S4_WAVES 8
+#endif
+constexpr int SPLIT4_WAVES = DPPO_S4_WAVES;
 int split_waves() { return SPLIT4_WAVES; }
 
 template <class Pol, int XQ, int KX, bool INJ, int SWV, int PM>
 int launch_split4_kw(const SplitArgs& sa, hipStream_t s) {
     constexpr int NO = (4 * XQ + 15) / 16;
+    // the finishing lanes are the members' lanes: a wave's 16 x XD / SWV coordinates in (64 / PM)
+    // slots at most PM deep (the one-wave-per-SIMD form covers XD <= 16 at PM = 2)
+    constexpr int NVW = 16 * 4 * XQ / SWV, KW = (NVW + 64 / PM - 1) / (64 / PM);
+    if constexpr (KW > PM) {
+        return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler: %d waves per member do not cover XD = %d", SWV, 4 * XQ);
+    } else {
     auto k = sample_split4_kernel<Pol, XQ, KX, INJ, SWV, PM>;
     const SampleArgs& a = sa.a;
     const size_t lds = split4_lds_bytes(a.XD, a.SD, a.K, KX, NO, SWV);
@@ -1923,6 +1932,7 @@ int launch_split4_kw(const SplitArgs& sa, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(blocks), dim3(SWV * 64), lds, s, sa);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
+    }
 }
 
 // the pair kernel's instantiated shapes: hopper dims (XD = 12, XD + SD <= 32)

@@ -455,6 +455,26 @@ DPPO_API int dppo_actor_step(const dppo_dims* d, int precision, float* params, f
                              double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
                              const size_t* clear_bytes, int n_clear, void* stream);
 
+/* ---- ABI 12, §8(e): the data-parallel gradient all-reduce as one kernel over IPC-mapped peer
+ * buffers (the reference has no collective: it applies gradients on one device,
+ * train_ppo_diffusion_agent.py:345-356, script/run.py:82; RCCL's all_reduce is the default here).
+ * Every rank allocates one region of dppo_ipc_region_bytes(capacity) with dppo_ipc_alloc (device
+ * memory, zeroed; handle = 64 bytes for hipIpcOpenMemHandle), exchanges the handles out of band
+ * (torch.distributed) and opens every peer's with dppo_ipc_open. dppo_ipc_allreduce then sums
+ * data[0, n) (fp32, n <= capacity) over the ranks IN PLACE on every rank, in rank order 0..W-1 (so
+ * every rank gets the same bits: a sequential fp32 sum): regions[x] = rank x's region as mapped in
+ * this process (regions[rank] = the own one), world <= 8, generation = 1, 2, ... the same on every
+ * rank for the same call; every rank must make the same calls in the same order, one launch each on
+ * its stream. A barrier that waits more than ~2 s sets *fail_host (dppo_host_alloc memory) and the
+ * next call returns DPPO_EHIP. */
+DPPO_API size_t dppo_ipc_region_bytes(int64_t capacity);
+DPPO_API int dppo_ipc_alloc(size_t bytes, void** ptr, void* handle);
+DPPO_API int dppo_ipc_open(const void* handle, void** ptr);
+DPPO_API int dppo_ipc_close(void* ptr);
+DPPO_API int dppo_ipc_free(void* ptr);
+DPPO_API int dppo_ipc_allreduce(void* const* regions, int world, int rank, int64_t capacity, float* data, int64_t n,
+                                uint64_t generation, uint32_t* fail_host, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -41,6 +41,8 @@ def main():
                  world=np.int64(a.world_size), params=m.train_params.cpu().numpy())
     a.minibatch_hook = hook
     a.iteration(force_train=True)
+    torch.cuda.synchronize()
+    np.save(os.path.join(out_dir, f"rank{rank}_params_end.npy"), a.model.train_params.cpu().numpy())
     dist.barrier()
     if rank == 0:
         print("dp_equiv done", flush=True)

@@ -33,3 +33,5 @@ print(sys.argv[2], "emu8", round(d["value"]), "ms/it", round(d["ms_per_step"], 2
 PY
   done
 done
+[ -n "$VARIANTS" ] && bash tools/ab_variants.sh $VARIANTS
+exit 0
