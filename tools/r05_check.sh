@@ -2,7 +2,7 @@
 # Round 5 check: GPU tests, then the bench (N = 1 and one emulated W = 8 rank) with the one-launch
 # actor step (default) and the r04 step (DPPO_FUSED_STEP=critic) alternating, each step time-limited.
 # usage: tools/r05_check.sh <tag>   TESTS=<pytest -k expr> narrows the tests; NOTESTS=1 skips them;
-# PAIRS=<n> A/B rounds (default 1)
+# PAIRS=<n> A/B rounds (default 1); NOBENCH=1 skips the bench A/B
 set -o pipefail
 tag=${1:-chk}
 cd $GRAFT_REPO_ROOT
@@ -13,6 +13,14 @@ if [ -z "$NOTESTS" ]; then
     > gpurun_out/gpu_tests_$tag.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/gpu_tests_$tag.log; exit 1; }
   tail -3 gpurun_out/gpu_tests_$tag.log
 fi
+# VARTESTS="<tag>..." runs the sampler parity tests against lib/variants/libdppo_hip_<tag>.so
+for v in $VARTESTS; do
+  DPPO_LIB=diffusionpolicyoptimization_amd/lib/variants/libdppo_hip_$v.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -v \
+    --timeout 120 --timeout-method thread -k "sampler or pipelined" > gpurun_out/gpu_tests_${tag}_$v.log 2>&1 \
+    || { echo "variant $v tests failed"; tail -40 gpurun_out/gpu_tests_${tag}_$v.log; exit 1; }
+  echo "variant $v: $(tail -1 gpurun_out/gpu_tests_${tag}_$v.log)"
+done
+[ -n "$NOBENCH" ] && { [ -n "$VARIANTS" ] && bash tools/ab_variants.sh $VARIANTS; exit 0; }
 for r in $(seq 1 ${PAIRS:-1}); do
   for mode in all critic; do
     DPPO_FUSED_STEP=$mode timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/bench_${tag}_${mode}_$r.log 2>&1 \
