@@ -31,6 +31,18 @@ __device__ inline unsigned int dppo_pack_f16x2(float lo, float hi) {
     return __builtin_bit_cast(unsigned int, __builtin_convertvector((f32x2_t){lo, hi}, f16x2_t));
 }
 
+// One DDPM posterior step of the samplers (diffusion.py:198-201 x0 reconstruction + clip at 1,
+// :239-242 posterior mean, diffusion_vpg.py:301-320 mean + std z) with every product and sum rounded
+// on its own, as NumPy / TF evaluate it: no FMA contraction, so every sampler path (split, XR, pair,
+// P = 8, streaming) gives the same bits whatever the compiler does around it.
+__device__ inline float ddpm_post(float c0, float c1, float c2, float c3, float sd, float x, float ep, float z) {
+#pragma clang fp contract(off)
+    float x0 = c0 * x - c1 * ep;
+    x0 = fminf(fmaxf(x0, -1.f), 1.f);
+    const float mu = c2 * x0 + c3 * x;
+    return mu + sd * z;
+}
+
 #define DPPO_WAVES 8
 #define DPPO_THREADS (DPPO_WAVES * 64)
 

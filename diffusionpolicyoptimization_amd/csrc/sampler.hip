@@ -399,16 +399,13 @@ __global__ __launch_bounds__(SW * 64) void sample_kernel(SampleArgs a) {
             for (int w = 0; w < SW; ++w) eps += part[(w * 16 + r) * NOC + q];
             const float* sc = sch + t * DPPO_SCHED_COLS;
             const float x = xs[tid];
-            float xr = sc[0] * x - sc[1] * eps;
-            xr = fminf(fmaxf(xr, -1.f), 1.f);                    // denoised_clip_value = 1 (diffusion.py:28)
-            const float mu = sc[2] * xr + sc[3] * x;
             float sd = expf(0.5f * sc[4]);
             // eval noise rule of the table row (include/dppo.h: DDPM t = 0 or any DDIM row -> 0;
             // other DDPM rows clip at 1e-3; diffusion_vpg.py:303-315)
             if (a.deterministic && sc[6] != 0.f) sd = 0.f;
             else if (a.deterministic) sd = fminf(fmaxf(sd, sc[5]), 1e6f);
             else sd = fminf(fmaxf(sd, a.min_std), 1e6f);
-            float xn = mu + sd * zt[i * 16 * XD + tid];
+            float xn = ddpm_post(sc[0], sc[1], sc[2], sc[3], sd, x, eps, zt[i * 16 * XD + tid]);   // (:198-242, :301-320)
             if (a.final_clip > 0.f && i == K - 1) xn = fminf(fmaxf(xn, -a.final_clip), a.final_clip);
             xs[tid] = xn;
             a0[r * lda0 + q] = P::cvt(xn);                      // next step's input

@@ -700,10 +700,7 @@ __global__ __launch_bounds__(SW * 64) void sample_split_kernel(SplitArgs sa) {
                 const int v = ve, r = re, q = qe, row = row0 + r;
                 ep += be;
                 const float x = xe;
-                float xr = c0 * x - c1 * ep;                         // x0 reconstruction (:198-201)
-                xr = fminf(fmaxf(xr, -1.f), 1.f);                    // denoised_clip_value = 1 (diffusion.py:28)
-                const float mu = c2 * xr + c3 * x;                   // posterior mean (:239-242)
-                float y = mu + sd * ze;                              // (:301-320)
+                float y = ddpm_post(c0, c1, c2, c3, sd, x, ep, ze);   // (:198-242, :301-320)
                 if (a.final_clip > 0.f && i == K - 1) y = fminf(fmaxf(y, -a.final_clip), a.final_clip);
                 if (failed) y = __builtin_nanf("");
                 xs[v] = y;
@@ -1223,10 +1220,7 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
                             ep += __uint_as_float((uint32_t)ga[2][ks][e]) + __uint_as_float((uint32_t)ga[3][ks][e]);
                         ep += bb[H + q];
                         const float x = xr[ks][e];
-                        float xq = c0 * x - c1 * ep;                         // x0 reconstruction (:198-201)
-                        xq = fminf(fmaxf(xq, -1.f), 1.f);                    // denoised_clip_value = 1
-                        const float mu = c2 * xq + c3 * x;                   // posterior mean (:239-242)
-                        float y = mu + sd * zt[i * 16 * XD + env * XD + q];  // (:301-320)
+                        float y = ddpm_post(c0, c1, c2, c3, sd, x, ep, zt[i * 16 * XD + env * XD + q]);   // (:198-242, :301-320)
                         if (a.final_clip > 0.f && i == K - 1) y = fminf(fmaxf(y, -a.final_clip), a.final_clip);
                         if (failed) y = __builtin_nanf("");
                         xr[ks][e] = y;
@@ -1291,10 +1285,7 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
                 const int v = ve, r = re, q = qe, row = row0 + r;
                 ep += be;
                 const float x = xe;
-                float xr = c0 * x - c1 * ep;                         // x0 reconstruction (:198-201)
-                xr = fminf(fmaxf(xr, -1.f), 1.f);                    // denoised_clip_value = 1 (diffusion.py:28)
-                const float mu = c2 * xr + c3 * x;                   // posterior mean (:239-242)
-                float y = mu + sd * ze;                              // (:301-320)
+                float y = ddpm_post(c0, c1, c2, c3, sd, x, ep, ze);   // (:198-242, :301-320)
                 if (a.final_clip > 0.f && i == K - 1) y = fminf(fmaxf(y, -a.final_clip), a.final_clip);
                 if (failed) y = __builtin_nanf("");
                 xs[v] = y;
@@ -1745,10 +1736,7 @@ __global__ __launch_bounds__(512) void sample_pair_kernel(SplitArgs sa) {
 #pragma unroll
             for (int k = 1; k < KW; ++k) ep = xm == k ? val[k] : ep;
             ep += be;
-            float xr = ec[0] * x - ec[1] * ep;                   // x0 reconstruction (:198-201)
-            xr = fminf(fmaxf(xr, -1.f), 1.f);                    // denoised_clip_value = 1 (diffusion.py:28)
-            const float mu = ec[2] * xr + ec[3] * x;             // posterior mean (:239-242)
-            float y = mu + sd * ze;                              // (:301-320)
+            float y = ddpm_post(ec[0], ec[1], ec[2], ec[3], sd, x, ep, ze);   // (:198-242, :301-320)
             if (a.final_clip > 0.f && i == K - 1) y = fminf(fmaxf(y, -a.final_clip), a.final_clip);
             if (failed) y = __builtin_nanf("");
             XS[ve] = y;
