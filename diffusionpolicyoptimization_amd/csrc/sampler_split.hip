@@ -120,20 +120,6 @@ extern "C" DPPO_API int dppo_debug_split_cycles(unsigned long long* out, int res
 namespace {
 
 // a store of a kernel output that leaves no dirty line in L2 (write-through; see DPPO_SPLIT_SIGNAL)
-// one lane's A-fragment of a k-step from its EPL fp32 column values (the rounding of Pol::cvt)
-template <class Pol, int EPL>
-__device__ inline u32x4 frag_of(const float (&v)[EPL]) {
-    u32x4 f;
-    if constexpr (EPL == 8) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) f[j] = Pol::pack2(v[2 * j], v[2 * j + 1]);
-    } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) f[j] = __float_as_uint(v[j]);
-    }
-    return f;
-}
-
 __device__ inline void store_out(float* p, float v) {
 #if DPPO_SPLIT_SIGNAL >= 2
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -182,9 +168,6 @@ __device__ inline int slot_feature(int j, int e) { return e < 4 ? 4 * j + e : 16
 // tuning knobs of the split kernel (tools/variant_build.sh <tag> "-D..." + tools/ab_variants.sh)
 #ifndef DPPO_S4_L1D
 #define DPPO_S4_L1D 4        // l1: u1 fragment reads kept in flight ahead of the MFMA chain
-#endif
-#ifndef DPPO_S4_XREG
-#define DPPO_S4_XREG 0       // x in registers across steps (every wave reads the whole exchange block)
 #endif
 #ifndef DPPO_S4_INREADY
 #define DPPO_S4_INREADY 1    // in-Dense: all LDS operands in one round trip
@@ -996,22 +979,6 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     }
     const int env = lane & 15, jq = lane >> 4;
     const int xmode = __builtin_amdgcn_readfirstlane(xfail[1]);
-    // XR (DPPO_S4_XREG): x stays in registers in the in-Dense A-fragment layout: lane (env, jq)
-    // holds columns c = ks*KG + jq*EPL + e of [x | state | 0] for its env as fp32 (x exact; the
-    // state and padding as their rounded operand values), and every wave finishes the whole
-    // exchange block for its own columns itself: no x / a0 LDS round trip and no step-end barrier
-    constexpr bool XR = DPPO_S4_XREG != 0 && NO == 1 && KX == 1;   // larger shapes spill with it
-    constexpr int KG = Pol::KG, EPL = Pol::EPL;
-    float xr[KX][EPL];
-    if constexpr (XR) {
-#pragma unroll
-        for (int ks = 0; ks < KX; ++ks)
-#pragma unroll
-            for (int e = 0; e < EPL; ++e) {
-                const int cc = ks * KG + jq * EPL + e;
-                xr[ks][e] = cc < XD ? xs[env * XD + cc] : Pol::tof(a0[env * lda0 + cc]);
-            }
-    }
     uint64_t* const xregion = sa.xbuf + (size_t)xmode * XREGION;
     // this lane's exchange/epilogue coordinate (launch-constant): lane (slot sl, member m) finishes
     // coordinate sl + SL m of its wave's slice
@@ -1034,16 +1001,13 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
         // this step's epilogue inputs, read with the in-Dense operands (none depends on this step)
         const f32x4 ec = *(const f32x4*)(sch + i * DPPO_SCHED_COLS);      // c0 c1 c2 c3
         const float esd = sch[i * DPPO_SCHED_COLS + 4];
-        const float xe = XR ? 0.f : xs[ve], ze = XR ? 0.f : zt[i * 16 * XD + ve], be = XR ? 0.f : bb[H + qe];
+        const float xe = xs[ve], ze = zt[i * 16 * XD + ve], be = bb[H + qe];
         // ---- in-Dense (transposed): h1 = TIN[t] + W_xs^T [x; state]; no activation (mlp.py:144)
         f32x4 h1[NTI];
         {
             u32x4 af[KX], wf[KX][NTI];
 #pragma unroll
-            for (int ks = 0; ks < KX; ++ks) {
-                if constexpr (XR) af[ks] = frag_of<Pol>(xr[ks]);
-                else af[ks] = lds_afrag<Pol>(a0, lda0, 0, ks, lane);
-            }
+            for (int ks = 0; ks < KX; ++ks) af[ks] = lds_afrag<Pol>(a0, lda0, 0, ks, lane);
 #pragma unroll
             for (int n = 0; n < NTI; ++n) h1[n] = *(const f32x4*)(tin + t * H + 16 * (NTI * wave + n) + 4 * jq);
 #pragma unroll
@@ -1175,71 +1139,6 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
             }
             XPHASE(15);
             const float c0 = ec[0], c1 = ec[1], c2 = ec[2], c3 = ec[3], sd = esd;
-            if constexpr (XR) {
-                // this lane's columns of every member's block
-                const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
-                uint64_t ga[P][KX][EPL];
-                bool failed = false;
-                for (;;) {
-                    bool ok = true;
-#pragma unroll
-                    for (int ks = 0; ks < KX; ++ks)
-#pragma unroll
-                        for (int e = 0; e < EPL; ++e) {
-                            if (ks * KG + e >= XD) continue;
-                            const int cc = ks * KG + jq * EPL + e, q = cc < XD ? cc : 0;   // others re-read column 0
-#pragma unroll
-                            for (int m = 0; m < P; ++m) {
-                                ga[m][ks][e] = __hip_atomic_load(xb + (size_t)m * NV + env * XD + q, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT);
-                                ok &= (uint32_t)(ga[m][ks][e] >> 32) == tag;
-                            }
-                        }
-                    if (__all(ok)) break;
-                    if (__builtin_amdgcn_s_memrealtime() > t_end) {
-                        failed = true;
-                        if (lane == 0) {
-                            *xfail = 1;
-                            __hip_atomic_store(sa.xfail_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        }
-                        break;
-                    }
-                }
-                XPHASE(5);
-                const int row = row0 + env;
-#pragma unroll
-                for (int ks = 0; ks < KX; ++ks)
-#pragma unroll
-                    for (int e = 0; e < EPL; ++e) {
-                        if (ks * KG + e >= XD) continue;
-                        const int q = ks * KG + jq * EPL + e;
-                        if (q >= XD) continue;
-                        // the member sum in the P = 2 / 4 DPP order: (v0 + v1) [+ (v2 + v3)]
-                        float ep = __uint_as_float((uint32_t)ga[0][ks][e]) + __uint_as_float((uint32_t)ga[1][ks][e]);
-                        if constexpr (P == 4)
-                            ep += __uint_as_float((uint32_t)ga[2][ks][e]) + __uint_as_float((uint32_t)ga[3][ks][e]);
-                        ep += bb[H + q];
-                        const float x = xr[ks][e];
-                        float y = ddpm_post(c0, c1, c2, c3, sd, x, ep, zt[i * 16 * XD + env * XD + q]);   // (:198-242, :301-320)
-                        if (a.final_clip > 0.f && i == K - 1) y = fminf(fmaxf(y, -a.final_clip), a.final_clip);
-                        if (failed) y = __builtin_nanf("");
-                        xr[ks][e] = y;
-                        // outputs: member 0, one wave per column
-                        if (c == 0 && wave == (ks * EPL + e) % SW && row < a.E) {
-                            if (a.chains && t <= KF) store_out(a.chains + ((size_t)row * (KF + 1) + (KF - t)) * XD + q, y);
-                            if (i == K - 1) {
-                                store_out(a.actions + (size_t)row * XD + q, y);
-                                if (a.actions_tagged)
-                                    __hip_atomic_store(a.actions_tagged + (size_t)row * XD + q,
-                                                       ((uint64_t)a.cond_tag << 32) | __float_as_uint(y), __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_SYSTEM);
-                                else if (a.actions_host) a.actions_host[(size_t)row * XD + q] = y;
-                            }
-                        }
-                    }
-                XPHASE(6);
-                continue;   // no step-end barrier: see the XR note above
-            }
             const int m = xm, sl = xsl;
             const uint64_t* src = xb + (size_t)m * NV + vw;
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 10000000ull;   // 100 ms
@@ -1311,20 +1210,7 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     XPHASE(9);
     if (sa.dual && set == 0) {
         // hand x to the fine-tuned set (member 0 of the group: every member holds the same bits)
-        if constexpr (XR) {
-            if (c == 0 && wave == 0) {
-#pragma unroll
-                for (int ks = 0; ks < KX; ++ks)
-#pragma unroll
-                    for (int e = 0; e < EPL; ++e) {
-                        const int q = ks * KG + jq * EPL + e;
-                        if (ks * KG + e < XD && q < XD)
-                            __hip_atomic_store(xh + env * XD + q, ((uint64_t)htag << 32) | __float_as_uint(xr[ks][e]),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-            }
-            __syncthreads();   // every wave's failure flag before the report below
-        } else if (c == 0 && tid < NV)
+        if (c == 0 && tid < NV)
             __hip_atomic_store(xh + tid, ((uint64_t)htag << 32) | __float_as_uint(xs[tid]), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         if (c == 0 && tid == 0 && a.done && *xfail)

@@ -390,9 +390,11 @@ __global__ __launch_bounds__(256) void l2_back_kernel(L2Back a) {
 // One workgroup; every parameter it reads (the TD temb rows of W_in and the time MLP) is staged into
 // LDS in one batch of coalesced loads at the start, so the dependent phases below run from LDS and
 // the kernel pays global-load latency about twice (staging, then G) instead of once per phase.
-__device__ inline void time_bwd_body(const float* __restrict__ gseg, const float* __restrict__ prm,
-                                     float* __restrict__ grad, const FlatOffsets& F, int XD, int TD, int H, int KF, int TS,
-                                     int stage_g, float* sm) {
+// after_stage() runs once every staged parameter is in LDS (the one-launch actor step steps W_in's
+// time-embedding rows there: their old values are read, their gradient is the dW's)
+template <class AfterStage>
+__device__ inline void time_bwd_body(const float* __restrict__ gseg, const float* prm, float* grad, const FlatOffsets& F,
+                                     int XD, int TD, int H, int KF, int TS, int stage_g, float* sm, AfterStage&& after_stage) {
     float* win = sm;                    // [TD][H]   W_in rows XD .. XD+TD-1
     float* w1 = win + TD * H;           // [TD][2TD]
     float* b1 = w1 + TD * 2 * TD;       // [2TD]
@@ -447,6 +449,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
         }
     }
     __syncthreads();
+    after_stage();
     if (gs) {   // from the staged copy: no second global round trip
         for (int n = tid; n < H; n += TB_THREADS) {
             float s = 0.f;
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __res
                                                        float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF,
                                                        int TS, int stage_g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    time_bwd_body(gseg, prm, grad, F, XD, TD, H, KF, TS, stage_g, sm);
+    time_bwd_body(gseg, prm, grad, F, XD, TD, H, KF, TS, stage_g, sm, [] {});
 }
 // time_bwd and the actor's l2_back in one launch (both follow the actor's dW and are independent of
 // each other): workgroup 0 runs the time-MLP backward, the others l2_back's row groups, TB_THREADS /
@@ -519,7 +522,7 @@ __global__ __launch_bounds__(TB_THREADS) void time_l2_bwd_kernel(const float* __
                                                           int stage_g, L2Back l2b, int l2_groups) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     if (blockIdx.x == 0) {
-        time_bwd_body(gseg, prm, grad, F, XD, TD, H, KF, TS, stage_g, sm);
+        time_bwd_body(gseg, prm, grad, F, XD, TD, H, KF, TS, stage_g, sm, [] {});
         return;
     }
     const int grp = ((int)blockIdx.x - 1) * (TB_THREADS / 256) + (int)threadIdx.x / 256;
@@ -911,17 +914,24 @@ __global__ __launch_bounds__(ACTOR_STEP_THREADS) void actor_step_kernel(float* _
         p[i] = pi; m[i] = mi; v[i] = vi;
         fuse_all<ET, KG, EPL>(a.j, a.njobs, i, pi);
     };
+    auto step_own = [&](int r) {   // independent elements, 4 in flight per thread
+#pragma unroll 4
+        for (int64_t i = a.own0[r][0] + tid; i < a.own0[r][1]; i += ACTOR_STEP_THREADS) {
+            const float gi = g[i];
+            if (a.clear_grads) g[i] = 0.f;
+            step_one(i, gi);
+        }
+    };
     if (blockIdx.x == 0) {
         if (a.gseg) {
-            time_bwd_body(a.gseg, p, g, a.F, a.XD, a.TD, a.H, a.KF, a.TS, a.stage_g, asm_);
+            // W_in's time-embedding rows are stepped as soon as the backward has staged their old values
+            time_bwd_body(a.gseg, p, g, a.F, a.XD, a.TD, a.H, a.KF, a.TS, a.stage_g, asm_, [&] { step_own(1); });
             __syncthreads();   // its gradient stores, read below by other threads of this workgroup
+            step_own(0);
+            step_own(2);
+        } else {
+            for (int r = 0; r < 3; ++r) step_own(r);
         }
-        for (int r = 0; r < 3; ++r)
-            for (int64_t i = a.own0[r][0] + tid; i < a.own0[r][1]; i += ACTOR_STEP_THREADS) {
-                const float gi = g[i];
-                if (a.clear_grads) g[i] = 0.f;
-                step_one(i, gi);
-            }
     } else {
         if (blockIdx.x == 1) copy_metrics(met, met_out, nmet, tag);
         const int64_t stride = (int64_t)(gridDim.x - 1) * ACTOR_STEP_THREADS;
@@ -1108,7 +1118,9 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
         a.own0[0][0] = (int64_t)FA.time_w1; a.own0[0][1] = (int64_t)FA.in_w;
         a.own0[1][0] = (int64_t)(FA.in_w + (size_t)D.XD * D.H); a.own0[1][1] = (int64_t)(FA.in_w + (size_t)(D.XD + D.TD) * D.H);
         a.own0[2][0] = (int64_t)FA.in_b; a.own0[2][1] = (int64_t)(FA.in_b + D.H);
-        a.wout[0] = (int64_t)FA.out_w; a.wout[1] = (int64_t)(FA.out_w + (size_t)D.H * D.XD);
+        // W_out last only when the l2 elements' virtual gradient reads its image slots
+        a.wout[0] = a.wout[1] = -1;
+        if (l2v) { a.wout[0] = (int64_t)FA.out_w; a.wout[1] = (int64_t)(FA.out_w + (size_t)D.H * D.XD); }
         for (int r = 0; r < 2; ++r) a.keep[r][0] = a.keep[r][1] = -1;
         if (l2v) {   // read by every l2 element's virtual gradient: zeroed by the last workgroup
             a.keep[0][0] = (int64_t)FA.l2_w; a.keep[0][1] = (int64_t)(FA.l2_w + (size_t)D.H * D.XD);
@@ -1125,10 +1137,13 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
         for (int r = 0; r < n_clear; ++r) { a.clr[r] = clear_ptrs[r]; a.clr_words[r] = (uint32_t)(clear_bytes[r] / 4); }
         rc = step_ticket(s, &a.ticket);
         if (rc) return rc;
-        // one workgroup per CU: workgroup 0's time-MLP backward (~10 us of dependent phases) runs
-        // beside the other workgroups' AdamW, so the launch ends about when it does
+        // about one element per thread (two workgroups per CU at most: every workgroup gets the time-MLP
+        // backward's LDS): workgroup 0's backward (~10 us of dependent phases) runs beside the other
+        // workgroups' AdamW. (r05: one workgroup per CU, two elements per thread, took 32 us alone
+        // against 16 us for AdamW + pack; tools/bench_step.py)
         const int cus = dw_device_cus();
-        const unsigned blocks = (unsigned)(cus > 2 ? cus : 2);
+        const int64_t want = 1 + (n + ACTOR_STEP_THREADS - 1) / ACTOR_STEP_THREADS;
+        const unsigned blocks = (unsigned)(want < 2 * (int64_t)cus ? (want > 2 ? want : 2) : 2 * (int64_t)cus);
         if (lds > 64 * 1024) {
             const void* fn = precision == DPPO_BF16 ? (const void*)actor_step_kernel<__bf16, 32, 8>
                            : precision == DPPO_F16 ? (const void*)actor_step_kernel<_Float16, 32, 8>
