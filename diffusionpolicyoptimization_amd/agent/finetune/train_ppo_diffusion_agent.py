@@ -492,28 +492,30 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # AdamW launch forms it (DPPO_PPO_L2_DEFERRED + DPPO_STEP_L2_FROM_PL2): one launch fewer
             # per minibatch. The factored form is linear, so the data-parallel all-reduce is unchanged.
             # Not with per-tensor gradient clipping (it needs the tensor) or a test hook reading grads.
-            # DPPO_FUSED_STEP = "all" (default) | "critic" | "0" (A/B knob). "all": each half's optimizer
-            # step is ONE launch. The actor's (dppo_actor_step, ABI 12) also runs the actor's time-MLP
+            # DPPO_FUSED_STEP = "critic" (default) | "all" | "0" (A/B knob). "critic": the critic's
+            # optimizer step is ONE launch (ABI 11) that zeroes what its next half would zero first
+            # (DPPO_STEP_CLEAR_GRADS + ops.ClearRanges; the next half runs DPPO_PPO_PRECLEARED); the
+            # actor's is time_bwd (+ l2_back) in the minibatch, then AdamW and the pack launch. "all": the
+            # actor's step is ONE launch too (dppo_actor_step, ABI 12), which also runs the time-MLP
             # backward (the minibatch stops after its dW: DPPO_PPO_TIME_BWD_IN_STEP) and forms the l2
-            # gradient from its factored form (DPPO_PPO_L2_DEFERRED), so after the actor's dW the
-            # minibatch chain is that one launch instead of time_bwd -> AdamW -> pack; the TEMB table is
-            # derived by its consumers. The critic's (ABI 11) zeroes what its next half would zero first
-            # (DPPO_STEP_CLEAR_GRADS + ops.ClearRanges; the next half runs DPPO_PPO_PRECLEARED).
-            # "critic": the r04 form (actor: time_bwd in the minibatch, AdamW + pack launches).
+            # gradient from its factored form (DPPO_PPO_L2_DEFERRED). Measured slower on one box
+            # (profiles/r05g_step_ab.txt: update 13.1 vs 12.4 ms at N = 1, 31.5 vs 27.5 ms on the
+            # emulated W = 8 rank): its per-element image stores and its workgroup-0 backward cost more
+            # than the launches they replace.
             # Under data parallelism the time-MLP backward stays in the minibatch (its gradients are part
             # of the all-reduced actor bucket). Not with a test hook reading the gradients (zero after
             # the step).
-            fuse_mode = os.environ.get("DPPO_FUSED_STEP", "all")
+            fuse_mode = os.environ.get("DPPO_FUSED_STEP", "critic")
             fuse = split and self.minibatch_hook is None and fuse_mode != "0"
             fuse_actor = fuse and fuse_mode == "all"
             tb_in_step = fuse_actor and not dp
             # DPPO_L2_DEFER = "auto" (default) | "1" | "0". Deferred, the actor's step forms dW_l2 per
-            # element from pl2; materialised, an l2_back launch follows the actor's dW. With the one-launch
-            # actor step "auto" always defers; with the r04 step it materialises below 16,384 rows per rank
-            # (profiles/r04l_tail_ab.txt).
+            # element from pl2; materialised, an l2_back launch follows the actor's dW. "auto" materialises
+            # below 16,384 rows per rank (profiles/r04l_tail_ab.txt; the one-launch actor step with the
+            # virtual l2 takes 32 vs 19 us alone, profiles/r05g_bench_step.txt).
             l2_mode = os.environ.get("DPPO_L2_DEFER", "auto")
             l2_def = (self.max_grad_norm is None and self.minibatch_hook is None and l2_mode != "0"
-                      and (l2_mode == "1" or fuse_actor or rows_local_full >= 16384))
+                      and (l2_mode == "1" or rows_local_full >= 16384))
             # the actor's step (AdamW + pack) clears the actor's accumulators in its pack launch
             clear_actor = fuse and os.environ.get("DPPO_ACTOR_CLEAR", "1") != "0"
             opt = self.actor_optimizer

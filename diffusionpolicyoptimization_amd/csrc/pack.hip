@@ -272,6 +272,9 @@ static inline uint8_t* P_out(void* p) { return (uint8_t*)p; }
 // split sampler's tables: W_XS, FOLD / ROUT, TIN, B_OUT2), PACK_SAMPLER (those tables only) or
 // PACK_SAMPLER_TEMB (those tables and the TEMB table: after a fused actor step, any precision)
 enum { PACK_ALL = 0, PACK_UPDATE = 1, PACK_SAMPLER = 2, PACK_SAMPLER_TEMB = 3 };
+#ifndef DPPO_PACK_UPDATE_TEMB
+#define DPPO_PACK_UPDATE_TEMB 0   // 1: PACK_UPDATE still writes the TEMB rows (the r04 pack; A/B builds)
+#endif
 static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int time_dim, int precision,
                         const float* params, void* packed, int temb_steps, int time_stride, int what = PACK_ALL) {
     const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision, temb_steps);
@@ -312,7 +315,10 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
         a.j[a.njobs - 1].k_split = out_dim;
         a.j[a.njobs - 1].k_skip = time_dim;
     }
-    if (L.temb_steps > 0) {
+    // PACK_UPDATE leaves TEMB to its consumers too: the row tiles derive their time embeddings from the
+    // fp32 time MLP (rowtile.hip), the sampler's table refresh re-derives the table (r05: the TEMB
+    // blocks were the pack launch's long pole on every minibatch)
+    if (L.temb_steps > 0 && (what != PACK_UPDATE || DPPO_PACK_UPDATE_TEMB)) {
         if (time_dim > 64 || out_dim > 32)
             return dppo_set_error(DPPO_EUNSUPPORTED, "time table: time_dim <= 64 and out_dim <= 32");
         if (a.tb.tables) return dppo_set_error(DPPO_EINVAL, "pack: one actor per launch");
@@ -398,8 +404,8 @@ void clear_stale(const void* packed) {
         if (g_stale[i].packed == packed) { g_stale[i] = g_stale[--g_nstale]; return; }
 }
 
-// the latest update of an image decides what is stale: a PACK_UPDATE pack rewrites TEMB (temb =
-// false), a fused actor step does not (temb = true)
+// the latest update of an image decides what is stale: since r05 neither a PACK_UPDATE pack nor a
+// fused actor step rewrites TEMB (temb = true); the flag stays for callers that do
 int mark_stale(const Dims& D, int precision, const float* params, const void* packed, bool temb) {
     std::lock_guard<std::mutex> lk(g_stale_mu);
     for (int i = 0; i < g_nstale; ++i)
@@ -459,7 +465,7 @@ int dppo_pack_models(const Dims& D, int precision, const float* actor_params, vo
         rc = add_mlp_jobs(a, D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS,
                           defer ? PACK_UPDATE : PACK_ALL);
         if (rc) return rc;
-        if (defer) rc = mark_stale(D, precision, actor_params, packed_actor, false);
+        if (defer) rc = mark_stale(D, precision, actor_params, packed_actor, !DPPO_PACK_UPDATE_TEMB);
         else clear_stale(packed_actor);   // a full pack makes a pending refresh moot
         if (rc) return rc;
     }

@@ -330,7 +330,7 @@ __device__ inline float packed_elem(const uint8_t* img, int K, int k, int n, int
 // inheriting its dynamic LDS, they waited for CUs, 48 us; one row's loads at a time, 33 us. r04's
 // time_l2_bwd_kernel nevertheless runs them as extra workgroups of time_bwd's launch — one launch
 // fewer on the chain measured faster at 6,250 rows, profiles/r04l_tail_ab.txt — and is used only by
-// the r04 step path (DPPO_FUSED_STEP=critic below 16,384 rows). Since ABI 12 the default actor step
+// the default step path (DPPO_FUSED_STEP=critic) below 16,384 rows. Since ABI 12 the one-launch actor step
 // runs the time-MLP backward itself and l2_back, when materialised, is this LDS-free launch alone.)
 constexpr int L2B_ROWS = 4;   // rows h of dW_l2 per workgroup
 constexpr int L2B_MAXN = 32;

@@ -181,6 +181,19 @@ def test_iterations_match_oracle(cuda, seed, tmp_path):
     assert [e["eval"] for e in errs] == [True, False, False]
 
 
+@pytest.mark.parametrize("l2_defer", ["1", "0"])
+def test_iterations_match_oracle_one_launch_actor_step(cuda, tmp_path, monkeypatch, l2_defer):
+    """The opt-in one-launch actor step (DPPO_FUSED_STEP=all: dppo_actor_step with the time-MLP
+    backward in its workgroup 0, the virtual or the materialised l2 gradient) over the same three
+    iterations, against the oracle at the default path's tolerances."""
+    monkeypatch.setenv("DPPO_FUSED_STEP", "all")
+    monkeypatch.setenv("DPPO_L2_DEFER", l2_defer)
+    a, orc = _agent_and_oracle(42, tmp_path)
+    errs = _run_and_compare(a, orc)
+    _record(f"one_launch_actor_step_l2defer{l2_defer}", errs)
+    assert [e["eval"] for e in errs] == [True, False, False]
+
+
 @pytest.mark.parametrize("seed", [42, 43, 44])
 def test_iterations_bf16_returns_match_oracle(cuda, seed, tmp_path):
     """The BASELINE config-2 operand policy (bf16 denoiser) over the same three iterations:
