@@ -518,6 +518,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                       and (l2_mode == "1" or rows_local_full >= 16384))
             # the actor's step (AdamW + pack) clears the actor's accumulators in its pack launch
             clear_actor = fuse and os.environ.get("DPPO_ACTOR_CLEAR", "1") != "0"
+            actor_fused = os.environ.get("DPPO_ACTOR_FUSED", "1") != "0"
             opt = self.actor_optimizer
             ng_all = m.grads.numel()
             # the bound calls are reused across updates while every buffer they captured is the same
@@ -527,7 +528,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                          m.packed_ft, m.packed_critic, m.sched, m.workspace(rows_local_full), opt.m, opt.v),
                     self.perm_seed, rows_local_full, self.reward_horizon, l2_def, split, defer,
                     self.max_grad_norm is None, m.dims.ft_denoising_steps, m.precision, fuse, fuse_actor, clear_actor,
-                    tb_in_step)
+                    tb_in_step, actor_fused)
             if getattr(self, "_bound_key", None) != bkey:
                 bound = {"run_mb": m.bind_minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat,
                                                     self.perm_seed, rows_local_full, reward_horizon=self.reward_horizon,
@@ -538,10 +539,12 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                                                         workspace=m.workspace(rows_local_full) if tb_in_step else None,
                                                         batch_rows=rows_local_full, l2_from_pl2=l2_def, clear_grads=True)
                     else:
+                        # the actor's AdamW and image in ONE coalesced launch (actor_tile_step_kernel, r05);
+                        # DPPO_ACTOR_FUSED=0: the AdamW + pack launches (A/B knob)
                         bound["actor"] = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
                                                         packs={"actor": (m.actor_ft_params, m.packed_ft)},
                                                         defer_sampler_tables=defer, l2_from_pl2=l2_def,
-                                                        clear_grads=clear_actor)
+                                                        fused_pack=fuse and actor_fused, clear_grads=clear_actor)
                     bound["critic"] = opt.bind_range(m.grads, na, ng_all, m.dims, m.precision,
                                                      packs={"critic": (m.critic_params, m.packed_critic)},
                                                      fused_pack=fuse, clear_grads=fuse)

@@ -403,7 +403,8 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
     float* e = dtemb + KF * TD;         // [KF][TD]
     float* a1 = e + KF * TD;            // [KF][2TD]
     float* da1 = a1 + KF * 2 * TD;      // [KF][2TD]
-    float* gs = stage_g ? da1 + KF * 2 * TD : nullptr;   // [KF][H] copy of G when it fits
+    float* ma1 = da1 + KF * 2 * TD;     // [KF][2TD] mish(a1), once per element (time_w2's gradient reads it TD times)
+    float* gs = stage_g ? ma1 + KF * 2 * TD : nullptr;   // [KF][H] copy of G when it fits
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // Staging: every global load of a chunk is issued before its first LDS store, so the phase pays
     // one load latency per chunk (one chunk at hopper's sizes) instead of one per array (separate
@@ -474,6 +475,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
         float s = b1[h];
         for (int k = 0; k < TD; ++k) s += e[q * TD + k] * w1[k * 2 * TD + h];
         a1[i] = s;
+        ma1[i] = mishf(s);
     }
     __syncthreads();
     for (int i = tid; i < KF * 2 * TD; i += TB_THREADS) {
@@ -485,7 +487,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
     for (int i = tid; i < 2 * TD * TD; i += TB_THREADS) {            // time_w2 [2TD][TD]
         const int h = i / TD, j = i % TD;
         float s = 0.f;
-        for (int q = 0; q < KF; ++q) s += mishf(a1[q * 2 * TD + h]) * dtemb[q * TD + j];
+        for (int q = 0; q < KF; ++q) s += ma1[q * 2 * TD + h] * dtemb[q * TD + j];
         grad[F.time_w2 + i] = s;
     }
     for (int j = tid; j < TD; j += TB_THREADS) {
@@ -532,7 +534,7 @@ __global__ __launch_bounds__(TB_THREADS) void time_l2_bwd_kernel(const float* __
 // dynamic LDS of time_bwd_body over nb buckets; *stage_g = whether the bucket sums are staged too
 static size_t time_bwd_lds(const Dims& D, int nb, int* stage_g) {
     size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
-                                  (size_t)nb * (2 * D.TD + 2 * 2 * D.TD));
+                                  (size_t)nb * (2 * D.TD + 3 * 2 * D.TD));
     *stage_g = tsm + sizeof(float) * (size_t)nb * D.H <= 160 * 1024;
     if (*stage_g) tsm += sizeof(float) * (size_t)nb * D.H;
     return tsm;
@@ -956,6 +958,126 @@ __global__ __launch_bounds__(ACTOR_STEP_THREADS) void actor_step_kernel(float* _
     clear_words(a.clr, a.clr_words);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The actor's optimizer step as ONE coalesced launch (r05; the step without the time-MLP backward).
+// actor_step_kernel stores each element into its image slots one 2-byte value at a time (fuse_all):
+// two scattered stores per weight, slower than AdamW + the coalesced pack launch. Here every wave owns
+// the elements of ONE 16-byte slot per lane of a weight tensor's packed image — a block of 16 outputs
+// x KG inputs — steps them with AdamW, stores the slot (one coalesced 1 KiB wave store) and, through a
+// wave-private LDS tile, the 64 slots the block covers in the transposed image; the remaining waves
+// step the fp32 tensors (biases, time MLP) one element per lane and copy them into their fp32
+// segments. The image bytes are the pack's (same (ET) conversion, zero padding). Under the virtual l2
+// gradient (DPPO_STEP_L2_FROM_PL2) the W_out blocks and the zeroing of what the l2 elements read wait
+// for the last workgroup, as in actor_step_kernel; the caller's clear ranges too.
+// ---------------------------------------------------------------------------------------------
+struct TileMat {
+    int64_t off;            // first element in the step's range
+    int K, N, KS, KST;      // rows (inputs), columns (outputs), k-steps of the image and of the transposed one
+    uint8_t* img;           // packed [K][N] image
+    uint8_t* timg;          // packed image of the transpose ([N][K]), or null
+    int nb;                 // 16-column blocks
+};
+struct TileCpy { int64_t lo, n; float* dst; };
+constexpr int TILE_MAXM = 4, TILE_MAXC = 8, TILE_THREADS = 256;
+struct TileStep {
+    int nmat;
+    TileMat mat[TILE_MAXM];
+    int mstart[TILE_MAXM + 1];      // wave prefix over the mats the main grid steps
+    int ncpy;
+    TileCpy cpy[TILE_MAXC];
+    int64_t cstart[TILE_MAXC + 1];  // element prefix over the copies
+    int last_mat;                   // the mat the last workgroup steps (W_out under the virtual l2), or -1
+    int64_t keep[2][2];             // read by every l2 element: zeroed by the last workgroup
+    int clear_grads;
+    void* clr[4];
+    uint32_t clr_words[4];
+    unsigned* ticket;
+};
+template <class ET, int KG, int EPL>
+__device__ inline void tile_block(float* p, float* g, float* m, float* v, const AdamHP& h, const L2Virt& vt,
+                                  const TileStep& a, const TileMat& M, int b, ET* tile, int lane) {
+    static_assert(EPL * (int)sizeof(ET) == 16 && 4 * EPL == KG, "one 16-B slot per lane");
+    const int nb = b % M.nb, kb = b / M.nb;
+    const int n = 16 * nb + (lane & 15), jq = lane >> 4;
+    ET val[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+        const int k = KG * kb + EPL * jq + e;
+        float x = 0.f;
+        if (k < M.K && n < M.N) {
+            const int64_t i = M.off + (int64_t)k * M.N + n;
+            float pi = p[i], mi = m[i], vi = v[i];
+            const bool virt = vt.on && i >= vt.w_off && i < vt.b_off + vt.H;
+            const float gi = virt ? l2_virtual_grad(g, vt, i) : g[i];
+            if (a.clear_grads && !in_range(i, a.keep[0]) && !in_range(i, a.keep[1])) g[i] = 0.f;
+            adamw_elem(pi, mi, vi, gi, h);
+            p[i] = pi; m[i] = mi; v[i] = vi;
+            x = pi;
+        }
+        val[e] = (ET)x;
+    }
+    u32x4 w;
+    __builtin_memcpy(&w, val, 16);
+    *reinterpret_cast<u32x4*>(M.img + ((((size_t)nb * M.KS + kb) << 6) + lane) * 16) = w;
+    if (!M.timg) return;
+    // the transposed image: tile[kl][nl] (KG x 16, wave-private) -> lane (kk, grp) reads row
+    // kl = 16 (grp / NGRP) + kk, columns EPL ng .. EPL ng + EPL - 1, one T slot
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) tile[(EPL * jq + e) * 16 + (lane & 15)] = val[e];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int NGRP = 16 / EPL;
+    const int kk = lane & 15, grp = lane >> 4;
+    const int kl = 16 * (grp / NGRP) + kk, ng = grp % NGRP;
+    const int k = KG * kb + kl, n0 = 16 * nb + EPL * ng;
+    const u32x4 tv = *reinterpret_cast<const u32x4*>(tile + kl * 16 + EPL * ng);
+    if (k < 16 * ((M.K + 15) / 16)) {
+        const int ntp = k >> 4, ksp = n0 / KG, lanep = kk + 16 * ((n0 % KG) / EPL);
+        *reinterpret_cast<u32x4*>(M.timg + ((((size_t)ntp * M.KST + ksp) << 6) + lanep) * 16) = tv;
+    }
+    __builtin_amdgcn_wave_barrier();   // the tile is rewritten by this wave's next block
+}
+template <class ET, int KG, int EPL>
+__global__ __launch_bounds__(TILE_THREADS) void actor_tile_step_kernel(float* p, float* g, float* m, float* v, AdamHP h,
+                                                                      const double* met, double* met_out, int nmet,
+                                                                      uint64_t tag, L2Virt vt, TileStep a) {
+    __shared__ __attribute__((aligned(16))) ET tiles[TILE_THREADS / 64][KG * 16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (blockIdx.x == 0) copy_metrics(met, met_out, nmet, tag);
+    const int gw = (int)blockIdx.x * (TILE_THREADS / 64) + wave;
+    if (gw < a.mstart[a.nmat]) {
+        int mi = 0;
+        while (gw >= a.mstart[mi + 1]) ++mi;
+        tile_block<ET, KG, EPL>(p, g, m, v, h, vt, a, a.mat[mi], gw - a.mstart[mi], tiles[wave], lane);
+    } else {
+        const int64_t e = (int64_t)(gw - a.mstart[a.nmat]) * 64 + lane;
+        if (e < a.cstart[a.ncpy]) {
+            int c = 0;
+            while (e >= a.cstart[c + 1]) ++c;
+            const int64_t local = e - a.cstart[c], i = a.cpy[c].lo + local;
+            float pi = p[i], mi = m[i], vi = v[i];
+            const bool virt = vt.on && i >= vt.w_off && i < vt.b_off + vt.H;
+            const float gi = virt ? l2_virtual_grad(g, vt, i) : g[i];
+            if (a.clear_grads && !in_range(i, a.keep[0]) && !in_range(i, a.keep[1])) g[i] = 0.f;
+            adamw_elem(pi, mi, vi, gi, h);
+            p[i] = pi; m[i] = mi; v[i] = vi;
+            a.cpy[c].dst[local] = pi;
+        }
+    }
+    if (!a.ticket || !last_workgroup(a.ticket)) return;
+    if (a.last_mat >= 0) {
+        const TileMat& M = a.mat[a.last_mat];
+        const int nblk = M.nb * M.KS;
+        for (int b = wave; b < nblk; b += TILE_THREADS / 64) tile_block<ET, KG, EPL>(p, g, m, v, h, vt, a, M, b, tiles[wave], lane);
+        __syncthreads();   // every W_out slot read by an l2 element was read before the ticket
+    }
+    if (a.clear_grads)
+        for (int r = 0; r < 2; ++r)
+            for (int64_t i = a.keep[r][0] + threadIdx.x; i < a.keep[r][1]; i += TILE_THREADS) g[i] = 0.f;
+    clear_words(a.clr, a.clr_words);
+}
+
 // per (device, stream): a zeroed ticket counter block of the fused steps, created on first use
 // (launches on one stream are ordered, so they share it; the critic's step on the side stream has its
 // own). One process-wide table under a mutex, keyed by the stream's own device.
@@ -1111,6 +1233,69 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
                                    n, h, metrics, mout, n_metrics, metrics_tag, f);
             DPPO_HIP(hipGetLastError());
             return DPPO_OK;
+        }
+        static const bool tile_on = [] { const char* e = getenv("DPPO_ACTOR_TILE_STEP"); return !e || atoi(e) != 0; }();
+        if (!gseg && tile_on) {
+            FuseJob jobs[FUSE_MAXJ];
+            const int nj = dppo_fuse_jobs(D.IN, D.H, D.XD, D.TD, precision, packed_actor, D.K, jobs);
+            DPPO_CHECK(nj >= 0, "dppo_optimizer_step: fused pack jobs");
+            TileStep t = {};
+            t.last_mat = -1;
+            for (int q = 0; q < nj; ++q) {
+                const FuseJob& J = jobs[q];
+                if (J.kind == 0) {
+                    DPPO_CHECK(t.nmat < TILE_MAXM, "actor tile step: too many weight tensors");
+                    TileMat& M = t.mat[t.nmat++];
+                    M.off = J.lo; M.K = J.IK; M.N = J.IN; M.KS = J.KS; M.img = J.dst; M.timg = nullptr; M.KST = 0;
+                    M.nb = dppo_cdiv(M.N, 16);
+                } else if (J.kind == 2) {
+                    DPPO_CHECK(t.ncpy < TILE_MAXC, "actor tile step: too many fp32 tensors");
+                    t.cpy[t.ncpy++] = TileCpy{J.lo, J.hi - J.lo, (float*)J.dst};
+                }
+            }
+            for (int q = 0; q < nj; ++q) {   // the transposed images, matched to their tensor
+                const FuseJob& J = jobs[q];
+                if (J.kind != 1) continue;
+                int mi = 0;
+                while (mi < t.nmat && t.mat[mi].off != J.lo) ++mi;
+                DPPO_CHECK(mi < t.nmat && J.IK == t.mat[mi].N && J.IN == t.mat[mi].K, "actor tile step: transposed image");
+                t.mat[mi].timg = J.dst; t.mat[mi].KST = J.KS;
+            }
+            for (int r = 0; r < 2; ++r) t.keep[r][0] = t.keep[r][1] = -1;
+            if (l2v) {
+                for (int mi = 0; mi < t.nmat; ++mi)
+                    if (t.mat[mi].off == (int64_t)FA.out_w) t.last_mat = mi;
+                DPPO_CHECK(t.last_mat >= 0, "actor tile step: W_out");
+                t.keep[0][0] = (int64_t)FA.l2_w; t.keep[0][1] = (int64_t)(FA.l2_w + (size_t)D.H * D.XD);
+                t.keep[1][0] = (int64_t)FA.out_b; t.keep[1][1] = (int64_t)(FA.out_b + D.XD);
+            }
+            t.mstart[0] = 0;
+            for (int mi = 0; mi < t.nmat; ++mi)
+                t.mstart[mi + 1] = t.mstart[mi] + (mi == t.last_mat ? 0 : t.mat[mi].nb * t.mat[mi].KS);
+            t.cstart[0] = 0;
+            for (int c = 0; c < t.ncpy; ++c) t.cstart[c + 1] = t.cstart[c] + t.cpy[c].n;
+            t.clear_grads = clear_g ? 1 : 0;
+            for (int r = 0; r < n_clear; ++r) { t.clr[r] = clear_ptrs[r]; t.clr_words[r] = (uint32_t)(clear_bytes[r] / 4); }
+            if (l2v || n_clear > 0 || clear_g) {
+                rc = step_ticket(s, &t.ticket);
+                if (rc) return rc;
+            }
+            const int64_t waves = t.mstart[t.nmat] + (t.cstart[t.ncpy] + 63) / 64;
+            const unsigned blocks = (unsigned)((waves + TILE_THREADS / 64 - 1) / (TILE_THREADS / 64));
+            {
+                DppoKtScope kt(KT_ADAMW, s);
+                if (precision == DPPO_BF16)
+                    hipLaunchKernelGGL((actor_tile_step_kernel<__bf16, 32, 8>), dim3(blocks), dim3(TILE_THREADS), 0, s,
+                                       params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
+                else if (precision == DPPO_F16)
+                    hipLaunchKernelGGL((actor_tile_step_kernel<_Float16, 32, 8>), dim3(blocks), dim3(TILE_THREADS), 0, s,
+                                       params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
+                else
+                    hipLaunchKernelGGL((actor_tile_step_kernel<float, 16, 4>), dim3(blocks), dim3(TILE_THREADS), 0, s,
+                                       params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
+            }
+            DPPO_HIP(hipGetLastError());
+            return dppo_mark_tables_stale(D, precision, actor_params, packed_actor, true);
         }
         ActorStep a = {};
         a.njobs = dppo_fuse_jobs(D.IN, D.H, D.XD, D.TD, precision, packed_actor, D.K, a.j);
