@@ -33,5 +33,5 @@ run lowdim_t4_c0 --env lowdim --env-threads 4
 run lowdim_t1_c20 --env lowdim --env-threads 1 --sim-cost-us 20
 run lowdim_t8_c20 --env lowdim --env-threads 8 --sim-cost-us 20
 [ -n "$NOPROF" ] && exit 0
-SARGS="--envs 256 --config-dir $F/walker2d-v2 --config-name ft_ppo_diffusion_mlp" bash tools/profile_sampler.sh ${tag}_walker256 && echo prof walker
-SARGS="--envs 512 --precision fp16 --config-dir $F/hopper-v2 --config-name ft_ppo_diffusion_mlp_ddim" bash tools/profile_sampler.sh ${tag}_ddim512 && echo prof ddim
+SARGS="--envs 256 --config-dir $GRAFT_REPO_ROOT/$F/walker2d-v2 --config-name ft_ppo_diffusion_mlp" bash tools/profile_sampler.sh ${tag}_walker256 && echo prof walker
+SARGS="--envs 512 --precision fp16 --config-dir $GRAFT_REPO_ROOT/$F/hopper-v2 --config-name ft_ppo_diffusion_mlp_ddim" bash tools/profile_sampler.sh ${tag}_ddim512 && echo prof ddim
