@@ -38,6 +38,9 @@ constexpr int FUSE_MAXJ = 12;
 // parameters start at element 0 of the step's range; returns the job count (<= FUSE_MAXJ) or -1
 int dppo_fuse_jobs(int in_dim, int hidden, int out_dim, int time_dim, int precision, void* packed, int temb_steps,
                    FuseJob* jobs);
+// the row tiles' fold segments (RT_*) of an actor image, alone: after a fused actor step (pack.hip)
+int dppo_pack_rt_fold(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* actor_params,
+                      void* packed_actor, int temb_steps, hipStream_t s);
 // temb: the TEMB table is stale too (the fused actor step), not only the split-sampler tables
 int dppo_mark_tables_stale(const Dims& D, int precision, const float* actor_params, const void* packed_actor, bool temb);
 

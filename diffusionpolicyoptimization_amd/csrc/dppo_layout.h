@@ -27,6 +27,16 @@
 //          value to ~16 bits), for a B operand that repeats the 4 activations in both halves
 //   ROUT   the same geometry with both halves = rnd(W_out[f][o]) (the residual h1 term, whose B
 //          operand is h1's hi/lo pair)
+// and, for an actor, the same fold for the row tiles (rowtile.hip), whose forward then runs no l2
+// GEMM (eps = relu(h2) M + a0 M0 + RT_BOUT) and whose backward forms d relu(h2) = dy M^T (no dh3 W_l2^T
+// GEMM). NHL = 2 hi/lo copies for 2-byte operands (the fp32 product to ~16 bits), 1 for fp32:
+//   RT_FOLD    NHL packed fwd [K=H][N=out] matrices: M = rnd(W_l2) rnd(W_out) (hi, then lo)
+//   RT_FOLD0   NHL packed fwd [K=in_dim][N=out]: M0 = rnd(W_in) rnd(W_out) (the residual h1 through the
+//              out-Dense, from the in-Dense's input)
+//   RT_TFOLD   packed bwd [K=ks_out_t*KG][N=H]: element (k, f) = hi(M[f][k]) for k < out, and (2-byte)
+//              lo(M[f][k - LOK]) for LOK <= k < LOK + out, LOK = ks_out_t*KG/2, against a dy tile whose
+//              columns [LOK, LOK + out) repeat dy: one GEMM of the dy tile's width gives both halves
+//   RT_BOUT    fp32 [16*ceil(out/16)] b_out + sum_h (b_in[h] + b_l2[h]) rnd(W_out[h][o])
 // A packed matrix [K][N] is ceil(N/16) n-tiles x KS k-steps x 64 lanes x 16 B, with
 // KS = ceil(K / KG) rounded up to EVEN (the weight stream runs in k-step pairs), KG = 32 (bf16)
 // or 16 (fp32). Lane l of (ntile, ks) holds, for e < EPL,
@@ -43,7 +53,7 @@
 
 enum MlpSeg { SEG_TIME = 0, SEG_W_IN, SEG_B_IN, SEG_W_L1, SEG_B_L1, SEG_W_L2, SEG_B_L2, SEG_W_OUT, SEG_B_OUT,
               SEG_T_OUT, SEG_T_L2, SEG_T_L1, SEG_TEMB, SEG_W_XS, SEG_TIN, SEG_B_OUT2,
-              SEG_FOLD, SEG_ROUT, SEG_COUNT };
+              SEG_FOLD, SEG_ROUT, SEG_RT_FOLD, SEG_RT_FOLD0, SEG_RT_TFOLD, SEG_RT_BOUT, SEG_COUNT };
 
 struct MlpLayout {
     int in_dim, hidden, out_dim, time_dim, precision, temb_steps;
@@ -61,6 +71,11 @@ DPPO_HD inline int packed_ksteps(int K, int KG) { return (dppo_cdiv(K, KG) + 1) 
 DPPO_HD inline size_t packed_matrix_bytes(int K, int N, int KG) {
     return (size_t)dppo_cdiv(N, 16) * (size_t)packed_ksteps(K, KG) * 64 * 16;
 }
+
+// hi/lo copies of the row tiles' fold fragments (dppo_layout.h RT_*), and the k offset of the lo half
+// of RT_TFOLD (2-byte operands: half the transposed out-layer's k extent)
+DPPO_HD inline int rt_fold_copies(int precision) { return (precision == 1 || precision == 2) ? 2 : 1; }
+DPPO_HD inline int rt_tfold_lok(int ks_out_t, int KG) { return ks_out_t * KG / 2; }
 
 DPPO_HD inline MlpLayout make_mlp_layout(int in_dim, int hidden, int out_dim, int time_dim, int precision,
                                          int temb_steps = 0) {
@@ -95,6 +110,13 @@ DPPO_HD inline MlpLayout make_mlp_layout(int in_dim, int hidden, int out_dim, in
     const size_t fold_bytes = time_dim > 0 ? (size_t)L.nt_h * L.nt_out * 1024 : 0;
     L.off[SEG_FOLD] = o; o = dppo_align256(o + fold_bytes);
     L.off[SEG_ROUT] = o; o = dppo_align256(o + fold_bytes);
+    const bool rt = time_dim > 0;           // actor: the row tiles' fold
+    const int nhl = rt_fold_copies(precision);
+    L.off[SEG_RT_FOLD] = o; o = dppo_align256(o + (rt ? nhl * packed_matrix_bytes(hidden, out_dim, L.KG) : 0));
+    L.off[SEG_RT_FOLD0] = o; o = dppo_align256(o + (rt ? nhl * packed_matrix_bytes(in_dim, out_dim, L.KG) : 0));
+    L.off[SEG_RT_TFOLD] = o;
+    o = dppo_align256(o + (rt ? packed_matrix_bytes(L.ks_out_t * L.KG, hidden, L.KG) : 0));
+    L.off[SEG_RT_BOUT] = o; o = dppo_align256(o + (rt ? (size_t)4 * 16 * L.nt_out : 0));
     L.total = o;
     return L;
 }

@@ -8,8 +8,9 @@
 struct PpoWorkspace {
     uint8_t* base;    // start of the workspace (buffer-resource base of the image stores)
     size_t ldm;
-    // actor (no dh3 image: l2's weight gradient is formed through the out layer, see pl2)
-    void *a0T, *u1T, *u2T, *h3T, *dyT, *dh2T, *dh1T;
+    // actor (no dh3 image: l2's weight gradient is formed through the out layer, see pl2; no h3 image:
+    // the folded row tile never forms h3, see pa0)
+    void *a0T, *u1T, *u2T, *dyT, *dh2T, *dh1T;
     // critic
     void *csT, *cu1T, *cu2T, *ch3T, *cdvT, *cdh2T, *cdh1T;
     int8_t* seg;      // [ldm] t of each row (bucket id for the one-hot bias/temb sums), -1 invalid
@@ -19,6 +20,10 @@ struct PpoWorkspace {
     // the H x H products from l2_back_kernel. Each is followed by the buffer zeroed with it: pl2 |
     // gseg, cpl2 | stats
     float* pl2;
+    // W_out's weight gradient through the folded forward (h3 = u2 W_l2 + a0 W_in + b_l2 + b_in):
+    //   dW_out = W_l2^T pl2 + W_in^T pa0 + (b_l2 + b_in) db_out,  pa0 = a0^T dy [IN][XD] (dW GEMM),
+    // formed by the out_back groups after the dW (update.hip); zeroed with pl2 | pa0 | gseg
+    float* pa0;
     float* gseg;      // [64][H] per-t sums of dh1 (actor in-layer; 16 buckets in PPO, K in pretraining)
     float* cpl2;
     double* stats;    // [4] adv {count, sum, sumsq}
@@ -41,12 +46,13 @@ inline PpoWorkspace make_ppo_workspace(const Dims& D, int precision, int rows, u
         o = dppo_align256(o + feats * w.ldm * es);
         return p;
     };
-    w.a0T = take(D.IN); w.u1T = take(D.H); w.u2T = take(D.H); w.h3T = take(D.H);
+    w.a0T = take(D.IN); w.u1T = take(D.H); w.u2T = take(D.H);
     w.dyT = take(D.XD); w.dh2T = take(D.H); w.dh1T = take(D.H);
     w.csT = take(D.SD); w.cu1T = take(D.HC); w.cu2T = take(D.HC); w.ch3T = take(D.HC);
     w.cdvT = take(1); w.cdh2T = take(D.HC); w.cdh1T = take(D.HC);
     w.seg = base ? (int8_t*)(base + o) : nullptr; o = dppo_align256(o + w.ldm);
     w.pl2 = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * (size_t)D.H * D.XD);
+    w.pa0 = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * (size_t)D.IN * D.XD);
     w.gseg = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * 64 * (size_t)D.H);
     w.cpl2 = base ? (float*)(base + o) : nullptr; o = dppo_align256(o + 4 * (size_t)D.HC);
     w.stats = base ? (double*)(base + o) : nullptr; o += 8 * 4;

@@ -105,8 +105,7 @@ __device__ void time_table_block(const TembArgs& b, int blk) {
 // values (exact) in one round trip at hopper's out_dim <= 16 (chunks of 256 rows above);
 // thread (g, f, oq) sums j-quarter g of each chunk for feature f and outs 4 oq.. (+16), so one
 // broadcast read of W_l2 and one 8-B read of W_out feed 4 FMAs; the quarters are added in a fixed
-// order at the end. These blocks come first in the launch: the pack is on every minibatch's
-// critical path.
+// order at the end. These blocks come first in the launch (the split sampler's table refresh).
 template <class ET>
 __device__ void fold_block(const TembArgs& b, int T) {
     if constexpr (sizeof(ET) == 2) {
@@ -201,6 +200,192 @@ __device__ void fold_block(const TembArgs& b, int T) {
     }
 }
 
+// The row tiles' fold (dppo_layout.h RT_*), one wave per tile, on the matrix cores from the image
+// the same stream has just written (the pack launch, or a fused optimizer step): the cross-element
+// products a per-element step cannot form.
+//   M tile T (16 l2 inputs i): M[i][o] = sum_j rnd(W_l2[i][j]) rnd(W_out[j][o]) as 16x16 MFMA tiles whose
+//     A operand is the T_L2 image's n-tile T (lane: W_l2[i][8 consecutive j]) and B the W_OUT image's
+//     (lane: W_out[8 consecutive j][o]): KS_h k-steps, exact products summed in fp32 (the 2-byte
+//     policies; fp32 images: the fp32 values);
+//   M0 tile (16 in-Dense inputs i): the same with W_in's rows read from the fp32 parameters (i < in_dim;
+//     rows up to RT_FOLD0's padded k range are zero);
+//   the last block: RT_BOUT = b_out + sum_h (b_in + b_l2)[h] rnd(W_out[h][o]) (fixed-order reduction).
+// The tile's M values go through LDS ([o][i]) into the RT_FOLD / RT_FOLD0 slots (hi, then lo) and the
+// RT_TFOLD slots of n-tile T (hi at k = o, lo at k = LOK + o).
+struct RtFoldArgs {
+    uint8_t* img;
+    const float* params;
+    FlatOffsets F;
+    size_t off_wout, off_tl2, off_fold, off_fold0, off_tfold, off_bout;
+    int H, XD, IN, nt_out, ks_h, ks_in, ks_out_t, nm, nm0;
+};
+// one M (M0) tile: NO out tiles, the k-steps in batches of KB whose loads are all issued before the
+// batch's MFMAs, with no branch inside a batch (a conditional load made hipcc wait vmcnt(0) per k-step:
+// a chain of KS_h global latencies, 17 us for the launch)
+template <class P, int NO, int KB, bool M0>
+__device__ inline void rt_fold_tile(const RtFoldArgs& a, const __amdgpu_buffer_rsrc_t& rs, int T, int lane,
+                                    float (*sm)[17]) {
+    using AT = typename P::AT;
+    constexpr int KG = P::KG, EPL = P::EPL;
+    const WSrc wo = wsrc(rs, a.off_wout), tl2 = wsrc(rs, a.off_tl2);
+    const int H = a.H, i = 16 * T + (lane & 15);
+    const bool irow = i < a.IN;
+    const float* wrow = a.params + a.F.in_w + (size_t)(irow ? i : 0) * H + (lane >> 4) * EPL;   // 16-B aligned
+    f32x4 acc[NO];
+#pragma unroll
+    for (int n = 0; n < NO; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < a.ks_h; kb += KB) {
+        u32x4 av[KB], bv[NO][KB];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            if constexpr (!M0) {
+                av[u] = load_bfrag_c(tl2, a.ks_h, T, kb + u, lane);
+            } else {   // W_in[i][8 (4) consecutive j] from the fp32 parameters, rounded as the pack rounds
+                const f32x4* src = (const f32x4*)(wrow + (kb + u) * KG);
+                AT e[EPL];
+#pragma unroll
+                for (int q = 0; q < EPL / 4; ++q) {
+                    const f32x4 x = src[q];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) e[4 * q + c] = (AT)(irow ? x[c] : 0.f);
+                }
+                __builtin_memcpy(&av[u], e, 16);
+            }
+#pragma unroll
+            for (int n = 0; n < NO; ++n) bv[n][u] = load_bfrag_c(wo, a.ks_h, n, kb + u, lane);
+        }
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+#pragma unroll
+            for (int n = 0; n < NO; ++n) acc[n] = P::mma(av[u], bv[n][u], acc[n]);
+    }
+    // C[m = i][n = o]: lane holds i = 4 (lane >> 4) + r, o = 16 n + (lane & 15)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm[16 * n + (lane & 15)][4 * (lane >> 4) + r] = n < NO ? acc[n < NO ? n : 0][r] : 0.f;
+}
+
+// RT_BOUT = b_out + sum_j (b_in + b_l2)[j] rnd(W_out[j][o]): lane (o = lane & 15, group jg = lane >> 4)
+// takes rnd(W_out) from the W_OUT image's fragments (its EPL consecutive j per k-step, zero past out_dim)
+// and the bias sums of those j, 4 k-steps per batch of loads; the 4 groups add through two lane swaps
+template <class P, int NO>
+__device__ inline void rt_fold_bias(const RtFoldArgs& a, const __amdgpu_buffer_rsrc_t& rs, int lane) {
+    using AT = typename P::AT;
+    constexpr int KG = P::KG, EPL = P::EPL, KB = 4;
+    const WSrc wo = wsrc(rs, a.off_wout);
+    const int jg = lane >> 4;
+    const float* bi = a.params + a.F.in_b + jg * EPL;   // 16-B aligned (host-checked offsets)
+    const float* bl = a.params + a.F.l2_b + jg * EPL;
+    float acc[NO];
+#pragma unroll
+    for (int n = 0; n < NO; ++n) acc[n] = 0.f;
+    for (int kb = 0; kb < a.ks_h; kb += KB) {
+        u32x4 w[NO][KB];
+        f32x4 vb[KB][EPL / 4], vl[KB][EPL / 4];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+#pragma unroll
+            for (int n = 0; n < NO; ++n) w[n][u] = load_bfrag_c(wo, a.ks_h, n, kb + u, lane);
+#pragma unroll
+            for (int q = 0; q < EPL / 4; ++q) {
+                vb[u][q] = *(const f32x4*)(bi + (kb + u) * KG + 4 * q);
+                vl[u][q] = *(const f32x4*)(bl + (kb + u) * KG + 4 * q);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+#pragma unroll
+            for (int n = 0; n < NO; ++n) {
+                AT e[EPL];
+                __builtin_memcpy(e, &w[n][u], 16);
+#pragma unroll
+                for (int q = 0; q < EPL; ++q) acc[n] = fmaf(vb[u][q / 4][q % 4] + vl[u][q / 4][q % 4], (float)e[q], acc[n]);
+            }
+    }
+    float* bout = (float*)(a.img + a.off_bout);
+#pragma unroll
+    for (int n = 0; n < NO; ++n) {
+        float v = acc[n];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        const int o = 16 * n + (lane & 15);
+        if (lane < 16) bout[o] = o < a.XD ? a.params[a.F.out_b + o] + v : 0.f;
+    }
+}
+
+template <class P>
+__global__ __launch_bounds__(64) void rt_fold_kernel(RtFoldArgs a) {
+    using AT = typename P::AT;
+    constexpr int KG = P::KG, EPL = P::EPL;
+    constexpr bool TWO = sizeof(AT) == 2;
+    constexpr int NHL = TWO ? 2 : 1, NLG = 16 / EPL;
+    __shared__ float sm[32][17];   // [o][i] of the tile
+    const int lane = threadIdx.x, b = (int)blockIdx.x;
+    const int XD = a.XD, H = a.H;
+    const float* prm = a.params;
+    const __amdgpu_buffer_rsrc_t rs = packed_rsrc(a.img);
+    if (b == a.nm + a.nm0) {   // RT_BOUT
+        if (a.nt_out > 1) rt_fold_bias<P, 2>(a, rs, lane);
+        else rt_fold_bias<P, 1>(a, rs, lane);
+        return;
+    }
+    const bool m0 = b >= a.nm;
+    const int T = m0 ? b - a.nm : b;
+    const int kb4 = a.ks_h % 8 ? 4 : 8;   // k-steps per batch (H = 128 / 384 with 2-byte operands: 4)
+    if (m0) {
+        if (a.nt_out > 1) { if (kb4 == 8) rt_fold_tile<P, 2, 8, true>(a, rs, T, lane, sm); else rt_fold_tile<P, 2, 4, true>(a, rs, T, lane, sm); }
+        else { if (kb4 == 8) rt_fold_tile<P, 1, 8, true>(a, rs, T, lane, sm); else rt_fold_tile<P, 1, 4, true>(a, rs, T, lane, sm); }
+    } else {
+        if (a.nt_out > 1) { if (kb4 == 8) rt_fold_tile<P, 2, 8, false>(a, rs, T, lane, sm); else rt_fold_tile<P, 2, 4, false>(a, rs, T, lane, sm); }
+        else { if (kb4 == 8) rt_fold_tile<P, 1, 8, false>(a, rs, T, lane, sm); else rt_fold_tile<P, 1, 4, false>(a, rs, T, lane, sm); }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // RT_FOLD / RT_FOLD0 slots of the tile: copy h, lane group lg of its k range, column c
+    {
+        const int KS = m0 ? a.ks_in : a.ks_h;
+        uint8_t* dst = a.img + (m0 ? a.off_fold0 : a.off_fold);
+        const size_t mat = (size_t)a.nt_out * KS * 64 * 16;
+        const int h = lane / (NLG * 16), lgl = (lane / 16) % NLG, c = lane & 15;
+        if (h < NHL) {
+            const int f0 = 16 * T + lgl * EPL, ks = f0 / KG, sl = c + 16 * ((f0 % KG) / EPL);
+            for (int n = 0; n < a.nt_out; ++n) {
+                AT e[EPL];
+#pragma unroll
+                for (int q = 0; q < EPL; ++q) {
+                    const float m = sm[16 * n + c][lgl * EPL + q];
+                    const AT hi = (AT)m;
+                    e[q] = h == 0 ? hi : (AT)(m - (float)hi);
+                }
+                u32x4 w;
+                __builtin_memcpy(&w, e, 16);
+                *reinterpret_cast<u32x4*>(dst + h * mat + (((size_t)n * KS + ks) * 64 + sl) * 16) = w;
+            }
+        }
+    }
+    if (!m0) {   // RT_TFOLD n-tile T
+        const int LOK = rt_tfold_lok(a.ks_out_t, KG);
+        for (int ks = 0; ks < a.ks_out_t; ++ks) {
+            const int k0 = ks * KG + (lane >> 4) * EPL;
+            AT e[EPL];
+#pragma unroll
+            for (int q = 0; q < EPL; ++q) {
+                const int k = k0 + q;
+                const bool lo = TWO && k >= LOK;
+                const int o = lo ? k - LOK : k;
+                const float m = o < XD ? sm[o][lane & 15] : 0.f;
+                const AT hi = (AT)m;
+                e[q] = lo ? (AT)(m - (float)hi) : hi;
+            }
+            u32x4 w;
+            __builtin_memcpy(&w, e, 16);
+            *reinterpret_cast<u32x4*>(a.img + a.off_tfold + (((size_t)T * a.ks_out_t + ks) * 64 + lane) * 16) = w;
+        }
+    }
+}
+
 template <int KG, int EPL, class ET = __bf16>
 __global__ __launch_bounds__(PACK_THREADS) void pack_all_kernel(PackArgs a) {
     int blk = (int)blockIdx.x;                       // whole blocks take a branch: no barrier is skipped
@@ -269,8 +454,9 @@ static inline uint8_t* P_out(void* p) { return (uint8_t*)p; }
 
 // the jobs of one MLP image (and, for an actor, its time tables) appended to a
 // PackArgs; returns DPPO_OK or an error code. what: PACK_ALL, PACK_UPDATE (everything but the
-// split sampler's tables: W_XS, FOLD / ROUT, TIN, B_OUT2), PACK_SAMPLER (those tables only) or
-// PACK_SAMPLER_TEMB (those tables and the TEMB table: after a fused actor step, any precision)
+// split sampler's tables: W_XS, FOLD / ROUT, TIN, B_OUT2), PACK_SAMPLER (those tables only),
+// PACK_SAMPLER_TEMB (those tables and the TEMB table: after a fused actor step, any precision). Every
+// pack with the main jobs of an actor is followed by the row tiles' fold (launch_rt_fold).
 enum { PACK_ALL = 0, PACK_UPDATE = 1, PACK_SAMPLER = 2, PACK_SAMPLER_TEMB = 3 };
 #ifndef DPPO_PACK_UPDATE_TEMB
 #define DPPO_PACK_UPDATE_TEMB 0   // 1: PACK_UPDATE still writes the TEMB rows (the r04 pack; A/B builds)
@@ -280,10 +466,12 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
     const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision, temb_steps);
     const FlatOffsets F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
     const int KG = dppo_prec_2b(precision) ? 32 : 16;
-    const bool split_tables = time_dim > 0 && L.temb_steps > 0 && dppo_prec_2b(precision);
-    const bool main_jobs = what != PACK_SAMPLER && what != PACK_SAMPLER_TEMB;
-    const bool sampler_tables = split_tables && what != PACK_UPDATE;
-    const int jobs = (main_jobs ? 11 + (time_dim > 0 ? 1 : 0) : 0) + (sampler_tables ? 1 : 0);
+    const bool actor = time_dim > 0;
+    const bool split_tables = actor && L.temb_steps > 0 && dppo_prec_2b(precision);
+    const bool main_jobs = what == PACK_ALL || what == PACK_UPDATE;
+    const bool sampler_tables = split_tables && (what == PACK_ALL || what == PACK_SAMPLER || what == PACK_SAMPLER_TEMB);
+    const bool temb_rows = L.temb_steps > 0 && (what != PACK_UPDATE || DPPO_PACK_UPDATE_TEMB);
+    const int jobs = (main_jobs ? 11 + (actor ? 1 : 0) : 0) + (sampler_tables ? 1 : 0);
     if (a.njobs + jobs > PACK_MAXJ) return dppo_set_error(DPPO_EINVAL, "pack: too many images in one launch");
     auto mat = [&](size_t src, int K, int N, bool tr, int seg) {
         PackJob& J = a.j[a.njobs++];
@@ -296,7 +484,7 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
         J.kind = 1; J.n = n; J.npad = npad; J.src = params + src; J.dst = P_out(packed) + L.off[seg]; J.threads = npad;
     };
     if (main_jobs) {
-        if (time_dim > 0) cpy(F.time_w1, (int)(F.in_w - F.time_w1), (int)(F.in_w - F.time_w1), SEG_TIME);
+        if (actor) cpy(F.time_w1, (int)(F.in_w - F.time_w1), (int)(F.in_w - F.time_w1), SEG_TIME);
         mat(F.in_w, in_dim, hidden, false, SEG_W_IN);
         cpy(F.in_b, hidden, hidden, SEG_B_IN);
         mat(F.l1_w, hidden, hidden, false, SEG_W_L1);
@@ -307,7 +495,7 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
         cpy(F.out_b, out_dim, 16 * L.nt_out, SEG_B_OUT);
         // transposed images: W^T viewed as a [K'=out][N'=in] weight, i.e. element (k', n') = W[n'][k']
         mat(F.out_w, out_dim, hidden, true, SEG_T_OUT);
-        mat(F.l2_w, hidden, hidden, true, SEG_T_L2);
+        mat(F.l2_w, hidden, hidden, true, SEG_T_L2);   // the actor's: the A operand of its fold (rt_fold_kernel)
         mat(F.l1_w, hidden, hidden, true, SEG_T_L1);
     }
     if (sampler_tables) {   // split sampler: W_in rows [x ; state] (skipping the TD time-embedding rows)
@@ -318,22 +506,22 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
     // PACK_UPDATE leaves TEMB to its consumers too: the row tiles derive their time embeddings from the
     // fp32 time MLP (rowtile.hip), the sampler's table refresh re-derives the table (r05: the TEMB
     // blocks were the pack launch's long pole on every minibatch)
-    if (L.temb_steps > 0 && (what != PACK_UPDATE || DPPO_PACK_UPDATE_TEMB)) {
+    if (actor && (temb_rows || sampler_tables)) {
         if (time_dim > 64 || out_dim > 32)
             return dppo_set_error(DPPO_EUNSUPPORTED, "time table: time_dim <= 64 and out_dim <= 32");
-        if (a.tb.tables) return dppo_set_error(DPPO_EINVAL, "pack: one actor per launch");
+        if (a.tb.params) return dppo_set_error(DPPO_EINVAL, "pack: one actor per launch");
         TembArgs& b = a.tb;
         b.params = params; b.F = F; b.TD = time_dim; b.stride = time_stride; b.R = L.temb_steps; b.XD = out_dim;
         b.H = hidden; b.nout = 16 * L.nt_out;
         b.temb = (float*)(P_out(packed) + L.off[SEG_TEMB]);
         b.tin = (float*)(P_out(packed) + L.off[SEG_TIN]);
         b.bout2 = (float*)(P_out(packed) + L.off[SEG_B_OUT2]);
-        b.fold = P_out(packed) + L.off[SEG_FOLD];
-        b.rout = P_out(packed) + L.off[SEG_ROUT];
-        // blocks: [0, R) TEMB rows, [R, 2R) TIN rows, 2R B_OUT2 (time_table_block)
+        b.fold = sampler_tables ? P_out(packed) + L.off[SEG_FOLD] : nullptr;
+        b.rout = sampler_tables ? P_out(packed) + L.off[SEG_ROUT] : nullptr;
         b.nfold = sampler_tables ? L.nt_h : 0;
+        // table blocks: [0, R) TEMB rows, [R, 2R) TIN rows, 2R B_OUT2 (time_table_block)
         b.first_table = what == PACK_SAMPLER ? L.temb_steps : 0;   // PACK_SAMPLER_TEMB: the TEMB rows too
-        b.tables = sampler_tables ? 2 * L.temb_steps + 1 - b.first_table : L.temb_steps;
+        b.tables = sampler_tables ? 2 * L.temb_steps + 1 - b.first_table : (temb_rows ? L.temb_steps : 0);
     }
     return DPPO_OK;
 }
@@ -427,7 +615,37 @@ int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precisi
     int rc = add_mlp_jobs(a, in_dim, hidden, out_dim, time_dim, precision, params, packed, temb_steps, time_stride);
     if (rc) return rc;
     if (temb_steps > 0) clear_stale(packed);
-    return launch_pack(a, precision, s);
+    rc = launch_pack(a, precision, s);
+    if (rc) return rc;
+    return dppo_pack_rt_fold(in_dim, hidden, out_dim, time_dim, precision, params, packed, temb_steps, s);
+}
+
+// the row tiles' fold segments of an actor image whose W_OUT / T_L2 slots are final on stream s (after
+// its pack launch or a fused optimizer step): rt_fold_kernel, one wave per tile
+int dppo_pack_rt_fold(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* actor_params,
+                      void* packed_actor, int temb_steps, hipStream_t s) {
+    const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision, temb_steps);
+    if (time_dim <= 0) return DPPO_OK;
+    if (out_dim > 32 || (dppo_prec_2b(precision) && out_dim > rt_tfold_lok(L.ks_out_t, L.KG)))
+        return dppo_set_error(DPPO_EUNSUPPORTED, "row-tile fold: out_dim %d > 32", out_dim);
+    const FlatOffsets F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
+    if (F.in_w % 4 || F.in_b % 4 || F.l2_b % 4 || hidden % 8)
+        return dppo_set_error(DPPO_EUNSUPPORTED, "row-tile fold: W_in / biases not 16-B aligned (time_dim %d)", time_dim);
+    RtFoldArgs a = {};
+    a.img = (uint8_t*)packed_actor; a.params = actor_params;
+    a.F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
+    a.off_wout = L.off[SEG_W_OUT]; a.off_tl2 = L.off[SEG_T_L2]; a.off_fold = L.off[SEG_RT_FOLD];
+    a.off_fold0 = L.off[SEG_RT_FOLD0]; a.off_tfold = L.off[SEG_RT_TFOLD]; a.off_bout = L.off[SEG_RT_BOUT];
+    a.H = hidden; a.XD = out_dim; a.IN = in_dim; a.nt_out = L.nt_out; a.ks_h = L.ks_h; a.ks_in = L.ks_in;
+    a.ks_out_t = L.ks_out_t;
+    a.nm = L.nt_h;
+    a.nm0 = L.ks_in * L.KG / 16;   // RT_FOLD0's padded k range, 16 rows per tile
+    DppoKtScope kt(KT_PACK_ALL, s);
+    if (precision == DPPO_BF16) hipLaunchKernelGGL(rt_fold_kernel<PolicyBF16>, dim3(a.nm + a.nm0 + 1), dim3(64), 0, s, a);
+    else if (precision == DPPO_F16) hipLaunchKernelGGL(rt_fold_kernel<PolicyF16>, dim3(a.nm + a.nm0 + 1), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(rt_fold_kernel<PolicyF32>, dim3(a.nm + a.nm0 + 1), dim3(64), 0, s, a);
+    DPPO_HIP(hipGetLastError());
+    return DPPO_OK;
 }
 
 extern "C" int dppo_refresh_sampler_tables(const void* packed, void* stream) {
@@ -473,5 +691,7 @@ int dppo_pack_models(const Dims& D, int precision, const float* actor_params, vo
         rc = add_mlp_jobs(a, D.SD, D.HC, 1, 0, precision, critic_params, packed_critic, 0, 1);
         if (rc) return rc;
     }
-    return launch_pack(a, precision, s);
+    rc = launch_pack(a, precision, s);
+    if (rc || !(actor_params && packed_actor)) return rc;
+    return dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, s);
 }

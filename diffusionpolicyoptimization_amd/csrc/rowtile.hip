@@ -115,7 +115,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     float* radv = (float*)(smem + S.radv);   // per row: the row's advantage (train)
     float* rlpo = (float*)(smem + S.rlpo);   // per row: its old log-prob (train)
     float* nrm = (float*)(smem + S.nrm);     // advantage normalisation: mean, std + 1e-8
-    float* part = (float*)(smem + S.tB);   // out-layer partials alias tB (u2 is dead by then)
+    float* part = (float*)(smem + S.tA);   // out-layer partials alias tA (relu(h1) is dead after L2)
     const size_t grow0 = (size_t)a.row0 + (size_t)blockIdx.x * ROWS;
     const __amdgpu_buffer_rsrc_t wsr = packed_rsrc(a.ws.base);
     const uint32_t ldm32 = (uint32_t)a.ws.ldm, grow32 = (uint32_t)grow0;
@@ -133,7 +133,10 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     auto W = [&](int seg) { return wsrc(rs, L.off[seg]); };
     constexpr int QD = DPPO_ROWTILE_QD;   // weight k-steps in flight per wave
     WQueue<QD, NT> R;
-    queue_prime(R, W(SEG_W_IN), KSI, NextLayers{W(SEG_W_L1), KSH, W(SEG_W_L2), KSH}, ntile0, lane);
+    // the stream after L1: l1 (L2), then (train) the backward's W_out^T, M^T and l1^T
+    const NextLayers after_l1 = train ? NextLayers{W(SEG_W_L1), KSH, W(SEG_T_OUT), KSO}
+                                      : NextLayers{W(SEG_W_L1), KSH, W(SEG_W_L1), KSH};
+    queue_prime(R, W(SEG_W_IN), KSI, after_l1, ntile0, lane);
     // Phase 1 computes only the row map, so its barrier waits on no global load: the per-row
     // advantage / old log-prob and the minibatch moments are loaded into registers here and
     // reach LDS after L1 (first read in the epilogue); parameters and gathers share phase 2.
@@ -182,7 +185,8 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     for (int i = tid; i < KF * 2 * TD; i += THREADS)
         a1_s[i] = temb_hidden(tp, TF.time_w1, TF.time_b1, te_s + (i / (2 * TD)) * TD, TD, i % (2 * TD));
     for (int i = tid; i < 3 * H + 16 * NO; i += THREADS) {
-        const int seg = i < H ? SEG_B_IN : (i < 2 * H ? SEG_B_L1 : (i < 3 * H ? SEG_B_L2 : SEG_B_OUT));
+        // the out-Dense bias with b_in and b_l2 folded through it (RT_BOUT: the forward runs no l2 GEMM)
+        const int seg = i < H ? SEG_B_IN : (i < 2 * H ? SEG_B_L1 : (i < 3 * H ? SEG_B_L2 : SEG_RT_BOUT));
         const int j = i < 3 * H ? i % H : i - 3 * H;
         bias[i] = ((const float*)(a.packed + L.off[seg]))[j];
     }
@@ -238,12 +242,18 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     static_assert(MT * NT * 4 <= 64, "relu masks are at most 64-bit");
     MaskT mask1 = 0, mask2 = 0;
     // The weight stream is one QD-deep queue per wave through every layer of the kernel:
-    //   in -> l1 -> l2 -> in (again: the residual h1 is recomputed as a0 W_in, 2 more k-steps,
-    //   instead of holding 8*MT*NT fp32 registers from L1 to L3) -> [train] out^T -> l2^T -> l1^T.
-    ORing<NOK, NO> ob;
+    //   in -> l1 -> [train] out^T -> M^T -> l1^T. The l2 layer never runs as a GEMM: the residual block
+    //   is linear from the l2 product to the out-Dense (mlp.py:186-206), so
+    //     eps  = relu(h2) M + a0 M0 + RT_BOUT,    M = W_l2 W_out, M0 = W_in W_out  (dppo_layout.h RT_*)
+    //     d relu(h2) = dy M^T,                    dh3 = dy W_out^T (the residual's share of dh1)
+    //   with M, M0 as 2-byte hi/lo pairs (fp32 products of the rounded weights): h3 is never formed,
+    //   so it is never rounded (the oracle's round_h3=False rounding points).
+    constexpr bool TWO = sizeof(AT) == 2;
+    const size_t fold_mat = packed_matrix_bytes(H, XD, P::KG), fold0_mat = packed_matrix_bytes(IN, XD, P::KG);
+    ORing<NOK, NO> obh, obl;              // RT_FOLD hi / lo fragments of this wave's k-steps
+    u32x4 o0[2][NO];                      // RT_FOLD0 hi / lo of k-step `wave` (waves < KSI)
     // ---- L1: h1 = a0 W_in + b (no activation on the input layer) ----
-    gemm_queue<P, MT, NT, KSI, QD>(a0, lda0, W(SEG_W_IN), ntile0, acc, lane, R,
-                                   NextLayers{W(SEG_W_L1), KSH, W(SEG_W_L2), KSH});
+    gemm_queue<P, MT, NT, KSI, QD>(a0, lda0, W(SEG_W_IN), ntile0, acc, lane, R, after_l1);
     add_bias(acc, bias, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -265,8 +275,21 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         else if (tid == ROWS) { nrm[0] = pre_m; nrm[1] = pre_s; }
     }
     // ---- L2: h2 = relu(h1) W_l1 + b ----
-    gemm_queue<P, MT, NT, KSH, QD>(tA, ldh, W(SEG_W_L1), ntile0, acc, lane, R,
-                                   NextLayers{W(SEG_W_L2), KSH, W(SEG_W_IN), KSI});
+    if constexpr (train)
+        gemm_queue<P, MT, NT, KSH, QD>(tA, ldh, W(SEG_W_L1), ntile0, acc, lane, R,
+                                       NextLayers{W(SEG_T_OUT), KSO, W(SEG_RT_TFOLD), KSO});
+    else
+        gemm_queue<P, MT, NT, KSH, QD, true, true>(tA, ldh, W(SEG_W_L1), ntile0, acc, lane, R, after_l1);
+    // the folded out-Dense's fragments: fetched here so they land during the relu / stores / barrier
+    out_prefetch<NOK, NO, WAVES>(obh, W(SEG_RT_FOLD), KSH, wave, lane);
+    if constexpr (TWO) out_prefetch<NOK, NO, WAVES>(obl, wsrc(rs, L.off[SEG_RT_FOLD] + fold_mat), KSH, wave, lane);
+    if (wave < KSI) {
+#pragma unroll
+        for (int n = 0; n < NO; ++n) {
+            o0[0][n] = load_bfrag_c(W(SEG_RT_FOLD0), KSI, n, wave, lane);
+            if constexpr (TWO) o0[1][n] = load_bfrag_c(wsrc(rs, L.off[SEG_RT_FOLD0] + fold0_mat), KSI, n, wave, lane);
+        }
+    }
     add_bias(acc, bias + H, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -282,35 +305,36 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.u2T), ldm32, ntile0, grow32, lane, acc);
     lds_sync();
     PHASE(2);
-    // out-layer fragments: fetched here so they land during L3 (not held through L1/L2: VGPRs)
-    out_prefetch<NOK, NO, WAVES>(ob, W(SEG_W_OUT), KSH, wave, lane);
-    // ---- L3: h3 = relu(h2) W_l2 + b_l2 + h1 = [relu(h2) | a0] [W_l2 ; W_in] + b_l2 + b_in ----
-    gemm_queue<P, MT, NT, KSH, QD>(tB, ldh, W(SEG_W_L2), ntile0, acc, lane, R,
-                                   train ? NextLayers{W(SEG_W_IN), KSI, W(SEG_T_OUT), KSO}
-                                         : NextLayers{W(SEG_W_IN), KSI, W(SEG_W_IN), KSI});
-    if constexpr (train)
-        gemm_queue<P, MT, NT, KSI, QD, false>(a0, lda0, W(SEG_W_IN), ntile0, acc, lane, R,
-                                              NextLayers{W(SEG_T_OUT), KSO, W(SEG_T_L2), KSH});
-    else
-        gemm_queue<P, MT, NT, KSI, QD, false, true>(a0, lda0, W(SEG_W_IN), ntile0, acc, lane, R,
-                                                    NextLayers{W(SEG_W_IN), KSI, W(SEG_W_IN), KSI});
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-        const int col = (ntile0 + n) * 16 + ccol(lane);
-        const float bv = bias[2 * H + col] + bias[col];
+    // ---- L4 (folded): eps = relu(h2) M + a0 M0 + RT_BOUT; the relu(h2) k-steps dealt over the waves
+    //      (NOK each), a0's KSI k-steps to waves 0..KSI-1; partials reduce through LDS ----
+    {
+        f32x4 po[MT][NO];
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[m][n][r] += bv;
-    }
-    store_acc_lds<P, MT, NT>(tA, ldh, ntile0, lane, acc);
-    if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.h3T), ldm32, ntile0, grow32, lane, acc);
-    lds_sync();
-    PHASE(3);
-    // ---- L4: eps = h3 W_out + b (k split over the waves, fragments prefetched before L1) ----
-    {
-        f32x4 po[MT][NO];
-        gemm_narrow_pre<P, MT, NOK, NO, WAVES>(tA, ldh, ob, po, wave, lane);
+            for (int n = 0; n < NO; ++n) zero_acc(po[m][n]);
+#pragma unroll
+        for (int i = 0; i < NOK; ++i)
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const u32x4 av = lds_afrag<P>(tB, ldh, m, wave + WAVES * i, lane);
+#pragma unroll
+                for (int n = 0; n < NO; ++n) {
+                    po[m][n] = P::mma(av, obh.b[i][n], po[m][n]);
+                    if constexpr (TWO) po[m][n] = P::mma(av, obl.b[i][n], po[m][n]);
+                }
+            }
+        if (wave < KSI) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const u32x4 av = lds_afrag<P>(a0, lda0, m, wave, lane);
+#pragma unroll
+                for (int n = 0; n < NO; ++n) {
+                    po[m][n] = P::mma(av, o0[0][n], po[m][n]);
+                    if constexpr (TWO) po[m][n] = P::mma(av, o0[1][n], po[m][n]);
+                }
+            }
+        }
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -327,9 +351,9 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     // clip flags into scratch in tA (h3 is dead once the out layer has run); (B) one row per lane
     // of wave 0 -> the row's mean log-prob and loss terms; (C) one (row, q) element per thread ->
     // d loss / d eps into the dy tile (A operand of the backward) and the dyT image.
-    const float* bo = bias + 3 * H;
+    const float* bo = bias + 3 * H;            // RT_BOUT
     const int nh = min(a.hp.reward_horizon, XD / a.Da) * a.Da;                      // [:, :reward_horizon]
-    float* e_lp = (float*)tA;                  // [ROWS][XD]
+    float* e_lp = (float*)tB;                  // [ROWS][XD] (relu(h2) is dead once the out layer has run)
     float* e_mu = e_lp + ROWS * XD;            // [ROWS][XD]
     float* e_uc = e_mu + ROWS * XD;            // [ROWS][XD] 1 = x_recon not clipped
     float* e_dn = e_uc + ROWS * XD;            // [ROWS] d loss / d newlogprob
@@ -414,8 +438,13 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     float sq = 0.f;                      // pretrain: this thread's sum of (eps - noise)^2
     float geta = 0.f;                    // learnable DDIM eta: this thread's share of d loss / d eta
     const bool leta = a.hp.eta_unscale != 0.f;
+    // 2-byte operands: columns [LOK, LOK + XD) of the dy tile repeat dy, the A operand of M^T's lo half
+    // (RT_TFOLD); the dyT image and the metric sums take the first copy only
+    const int LOK = rt_tfold_lok(KSO, P::KG);
     for (int idx = tid; idx < ROWS * ktw; idx += THREADS) {
-        const int q = idx / ROWS, r = idx % ROWS;
+        const int qa = idx / ROWS, r = idx % ROWS;
+        const bool dup = TWO && qa >= LOK;
+        const int q = dup ? qa - LOK : qa;
         float d = 0.f;
         if (pre) {
             // p_losses, predict_epsilon (diffusion.py:186-194): mean((eps - noise)^2)
@@ -424,7 +453,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
 #pragma unroll
                 for (int w = 0; w < WAVES; ++w) eps += part[(w * ROWS + r) * (16 * NO) + q];
                 const float e = eps - xn[r * XD + q];
-                sq += e * e;
+                if (!dup) sq += e * e;
                 d = a.pre_scale * e;
             }
         } else if (q < XD && q < nh && rn[r] >= 0) {
@@ -436,7 +465,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
             const float res = xn[r * XD + q] - e_mu[e];
             const float dmu = dlp * res / (sd * sd);
             d = e_uc[e] != 0.f ? -sc[1] * sc[2] * dmu : 0.f;
-            if (leta) {
+            if (leta && !dup) {
                 // DDIM row (include/dppo.h): mu = sqrt(abar_prev) x0 + dd eps', sigma = max(eta s, 1e-10),
                 // dd = sqrt(clip(1 - abar_prev - sigma^2, 0, 1e6)); d mu / d eta = (d dd / d eta) eps' with
                 // eps' = (x - sqrt(abar) x0) / sqrt(1 - abar) = (x - x0 / c0) c0 / c1, dd = c3 c1 / c0;
@@ -456,7 +485,7 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
                 geta += dlp * (res / (sd * sd) * ddd * ep2 + (res * res / (sd * sd * sd) - 1.f / sd) * dstd);
             }
         }
-        dyt[r * lda0 + q] = P::cvt(d);
+        dyt[r * lda0 + qa] = P::cvt(d);
     }
     if (pre) {
         sq = wave_sum(sq);
@@ -477,12 +506,12 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     // B4: dh3 = dy W_out^T (kept only in tB: B2 re-reads it from there, which frees 8*MT*NT VGPRs;
     // no image: l2's weight gradient is (u2^T dy) W_out^T, dppo_ppo.h pl2)
     gemm_queue<P, MT, NT, KSO, QD>(a0, lda0, W(SEG_T_OUT), ntile0, acc, lane, R,
-                                   NextLayers{W(SEG_T_L2), KSH, W(SEG_T_L1), KSH});
+                                   NextLayers{W(SEG_RT_TFOLD), KSO, W(SEG_T_L1), KSH});
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
-    lds_sync();
     PHASE(8);
-    // B3: dh2 = (dh3 W_l2^T) * relu'(h2)
-    gemm_queue<P, MT, NT, KSH, QD>(tB, ldh, W(SEG_T_L2), ntile0, acc, lane, R,
+    // B3 (folded): dh2 = (dy M^T) * relu'(h2) = (dh3 W_l2^T) * relu'(h2), from the same dy tile (its
+    // repeated columns against M^T's lo half)
+    gemm_queue<P, MT, NT, KSO, QD>(a0, lda0, W(SEG_RT_TFOLD), ntile0, acc, lane, R,
                                    NextLayers{W(SEG_T_L1), KSH, W(SEG_T_L1), KSH});
 #pragma unroll
     for (int m = 0; m < MT; ++m)

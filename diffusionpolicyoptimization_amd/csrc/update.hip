@@ -322,6 +322,19 @@ __device__ inline float packed_elem(const uint8_t* img, int K, int k, int n, int
     if (prec == DPPO_F16) return (float)*(const _Float16*)e;
     return *(const float*)e;
 }
+// the same with the precision a compile-time constant: no branch between the loads (a per-element
+// precision switch made hipcc wait vmcnt(0) after every 2-byte load)
+template <int PREC>
+__device__ inline float packed_elem_t(const uint8_t* img, int K, int k, int n) {
+    constexpr bool two = PREC == DPPO_BF16 || PREC == DPPO_F16;
+    constexpr int KG = two ? 32 : 16, EPL = two ? 8 : 4;
+    const int lane = (n & 15) + 16 * ((k % KG) / EPL);
+    const size_t slot = ((size_t)(n >> 4) * packed_ksteps(K, KG) + k / KG) * 64 + lane;
+    const uint8_t* e = img + slot * 16 + (size_t)(k % EPL) * (two ? 2 : 4);
+    if constexpr (PREC == DPPO_BF16) return (float)*(const __bf16*)e;
+    else if constexpr (PREC == DPPO_F16) return (float)*(const _Float16*)e;
+    else return *(const float*)e;
+}
 // Workgroup b forms rows [L2B_ROWS b, +L2B_ROWS) of dW_l2 (workgroup 0 also db_l2): thread t owns
 // columns j = t, t + 256, ... with rnd(W_out[j][:]) in registers; the workgroup's pl2 rows are
 // loaded up front (uniform addresses: one round trip for all of them, not one per row). No LDS and
@@ -334,52 +347,152 @@ __device__ inline float packed_elem(const uint8_t* img, int K, int k, int n, int
 // runs the time-MLP backward itself and l2_back, when materialised, is this LDS-free launch alone.)
 constexpr int L2B_ROWS = 4;   // rows h of dW_l2 per workgroup
 constexpr int L2B_MAXN = 32;
-template <int NJ, int NQ>
+template <int PREC, int NJ, int NQ>
 __device__ inline void l2_back_cols(const L2Back& a, int b, int t, int nt) {
-    const int H = a.H;
+    // branch-free loads (a conditional load made hipcc wait for it alone): N is the instantiation's
+    // width for the cfgs' widths (l2_back_rows_p), the workgroup's rows exist (b < H / L2B_ROWS), column
+    // indices past H are clamped and their stores masked
+    const int H = a.H, N = NQ < L2B_MAXN ? NQ : a.N;
     const int h0 = L2B_ROWS * b;
-    float pv[L2B_ROWS + 1][NQ];   // the workgroup's pl2 rows, then (workgroup 0) db_out
+    float pv[L2B_ROWS + 1][NQ];   // the workgroup's pl2 rows, then db_out (stored by workgroup 0)
 #pragma unroll
     for (int r = 0; r < L2B_ROWS; ++r)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) pv[r][q] = (h0 + r < H && q < a.N) ? a.pl2[(size_t)(h0 + r) * a.N + q] : 0.f;
+        for (int q = 0; q < NQ; ++q) pv[r][q] = q < N ? a.pl2[(size_t)(h0 + r) * N + q] : 0.f;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) pv[L2B_ROWS][q] = (b == 0 && q < a.N) ? a.gob[q] : 0.f;
+    for (int q = 0; q < NQ; ++q) pv[L2B_ROWS][q] = q < N ? a.gob[q] : 0.f;
+    float w[NJ][NQ];
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) {
+        const int j = min(t + c * nt, H - 1);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) w[c][q] = q < N ? packed_elem_t<PREC>(a.wimg, H, j, q) : 0.f;
+    }
 #pragma unroll
     for (int c = 0; c < NJ; ++c) {
         const int j = t + c * nt;
         if (j >= H) continue;
-        float w[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) w[q] = q < a.N ? packed_elem(a.wimg, H, j, q, a.prec) : 0.f;
 #pragma unroll
         for (int r = 0; r <= L2B_ROWS; ++r) {
             float sum = 0.f;
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) sum = fmaf(pv[r][q], w[q], sum);
-            if (r < L2B_ROWS) {
-                if (h0 + r < H) a.gw[(size_t)(h0 + r) * H + j] = sum;
-            } else if (b == 0) {
-                a.gb[j] = sum;
-            }
+            for (int q = 0; q < NQ; ++q) sum = fmaf(pv[r][q], w[c][q], sum);
+            if (r < L2B_ROWS) a.gw[(size_t)(h0 + r) * H + j] = sum;
+            else if (b == 0) a.gb[j] = sum;
         }
     }
 }
-template <int NQ>
+template <int PREC, int NQ>
 __device__ inline void l2_back_n(const L2Back& a, int b, int t) {   // 256 threads per row group b
-    if (a.H <= 256) l2_back_cols<1, NQ>(a, b, t, 256);
-    else l2_back_cols<2, NQ>(a, b, t, 256);
+    if (a.H <= 256) l2_back_cols<PREC, 1, NQ>(a, b, t, 256);
+    else l2_back_cols<PREC, 2, NQ>(a, b, t, 256);
 }
-__device__ inline void l2_back_rows(const L2Back& a, int b, int t) {
+template <int PREC>
+__device__ __forceinline__ void l2_back_rows_p(const L2Back& a, int b, int t) {
     switch (a.N) {     // the action-chunk widths of the cfgs (hopper 12; walker2d / halfcheetah 24), the critic's 1
-        case 1: l2_back_n<1>(a, b, t); break;
-        case 12: l2_back_n<12>(a, b, t); break;
-        case 24: l2_back_n<24>(a, b, t); break;
-        default: l2_back_n<L2B_MAXN>(a, b, t); break;   // any N <= 32, zero-padded
+        case 1: l2_back_n<PREC, 1>(a, b, t); break;
+        case 12: l2_back_n<PREC, 12>(a, b, t); break;
+        case 24: l2_back_n<PREC, 24>(a, b, t); break;
+        default: l2_back_n<PREC, L2B_MAXN>(a, b, t); break;   // any N <= 32, zero-padded
     }
 }
-__global__ __launch_bounds__(256) void l2_back_kernel(L2Back a) {
-    l2_back_rows(a, (int)blockIdx.x, (int)threadIdx.x);
+// the kernels below are instantiated per precision (a runtime switch here made hipcc outline these
+// bodies as calls)
+// W_out's weight gradient through the folded forward (rowtile.hip: the row tiles never form h3,
+// dppo_ppo.h pa0): dW_out[f][q] = sum_g rnd(W_l2[g][f]) pl2[g][q] + sum_i rnd(W_in[i][f]) pa0[i][q] +
+// (b_l2[f] + b_in[f]) db_out[q], the oracle's h3^T dy with h3 = u2 rnd(W_l2) + b_l2 + a0 rnd(W_in) + b_in.
+// A group of 256 threads forms OB_ROWS rows f: thread t takes rows g = t, t + 256, ... of W_l2 (4 features
+// in one 16-B load) and pl2, and row i = t of W_in / pa0, so each thread pays one round trip; the
+// OB_ROWS x N partial sums reduce over the lanes (DPP) and then the 4 waves through LDS in a fixed order.
+struct OutBack {
+    const float* prm;     // the actor's flat fp32 parameters
+    FlatOffsets F;
+    const float* pl2;     // [H][N] (the factored l2 region of the gradients when l2 is deferred)
+    const float* pa0;     // [IN][N]
+    const float* gob;     // [N] db_out (final: the dW launch before this one produced it)
+    float* gw;            // [H][N] dW_out
+    int H, IN, N, prec;
+};
+constexpr int OB_ROWS = 4;
+template <int PREC>
+__device__ inline float round_prec(float x) {
+    if constexpr (PREC == DPPO_BF16) return (float)(__bf16)x;
+    else if constexpr (PREC == DPPO_F16) return (float)(_Float16)x;
+    else return x;
+}
+template <int PREC, int NQ>
+__device__ inline void out_back_n(const OutBack& a, int b, bool valid, int t, float* red) {
+    const int H = a.H, N = a.N, f0 = OB_ROWS * b, lane = t & 63, w = t >> 6;
+    const int NE = NQ < L2B_MAXN ? NQ : N;   // the instantiation's width (out_back_group)
+    float acc[OB_ROWS][NQ];
+#pragma unroll
+    for (int r = 0; r < OB_ROWS; ++r)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[r][q] = 0.f;
+    if (valid) {
+        // every load of the thread first (rows t, t + 256, t + 512 of W_l2 / pl2 and row t of W_in / pa0),
+        // then the FMAs: one round trip (a rolled loop waited for each row's loads in turn)
+        constexpr int NG = 3;   // H <= 768 (host-checked)
+        float wv[NG + 1][OB_ROWS], pv[NG + 1][NQ];
+#pragma unroll
+        for (int u = 0; u <= NG; ++u) {
+            const bool l2 = u < NG;
+            const int g = l2 ? t + 256 * u : t;
+            const bool ok = l2 ? g < H : g < a.IN;
+            const float* W = l2 ? a.prm + a.F.l2_w : a.prm + a.F.in_w;
+            const float* P = l2 ? a.pl2 : a.pa0;
+            const f32x4 w4 = ok ? *(const f32x4*)(W + (size_t)g * H + f0) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < OB_ROWS; ++r) wv[u][r] = round_prec<PREC>(w4[r]);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) pv[u][q] = (ok && q < NE) ? P[(size_t)(ok ? g : 0) * NE + q] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u <= NG; ++u)
+#pragma unroll
+            for (int r = 0; r < OB_ROWS; ++r)
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) acc[r][q] = fmaf(wv[u][r], pv[u][q], acc[r][q]);
+    }
+#pragma unroll
+    for (int r = 0; r < OB_ROWS; ++r)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const float v = wave_sum(acc[r][q]);
+            if (lane == 0) red[w * OB_ROWS * NQ + r * NQ + q] = v;
+        }
+    __syncthreads();
+    if (valid && t < OB_ROWS * N) {
+        const int r = t / N, q = t % N, f = f0 + r;
+        constexpr int S = OB_ROWS * NQ;
+        if (f < H) {
+            const float s = (red[r * NQ + q] + red[S + r * NQ + q]) + (red[2 * S + r * NQ + q] + red[3 * S + r * NQ + q]);
+            const float bb = a.prm[a.F.l2_b + f] + a.prm[a.F.in_b + f];
+            a.gw[(size_t)f * N + q] = fmaf(bb, a.gob[q], s);
+        }
+    }
+}
+// every thread of the workgroup calls this (it holds a barrier); valid = the group has rows to form.
+// red: 4 x OB_ROWS x L2B_MAXN floats of LDS for this 256-thread group
+template <int PREC>
+__device__ __forceinline__ void out_back_group(const OutBack& a, int b, bool valid, int t, float* red) {
+    switch (a.N) {
+        case 12: out_back_n<PREC, 12>(a, b, valid, t, red); break;
+        case 24: out_back_n<PREC, 24>(a, b, valid, t, red); break;
+        default: out_back_n<PREC, L2B_MAXN>(a, b, valid, t, red); break;   // any N <= 32
+    }
+}
+
+constexpr int OB_RED = 4 * OB_ROWS * L2B_MAXN;   // floats of LDS per 256-thread group
+
+// block b: l2_back's row group b (b < l2_blocks), then the actor's out_back group b (b < ob_groups)
+template <int PREC>
+__global__ __launch_bounds__(256) void l2_back_kernel(L2Back a, int l2_blocks, OutBack ob, int ob_groups) {
+    if ((int)blockIdx.x < l2_blocks) l2_back_rows_p<PREC>(a, (int)blockIdx.x, (int)threadIdx.x);
+    if (ob_groups > 0) {
+        __shared__ float red[OB_RED];
+        out_back_group<PREC>(ob, (int)blockIdx.x, (int)blockIdx.x < ob_groups, (int)threadIdx.x, red);
+    }
     if (a.zcnt) {   // the critic's row tiles and dW (earlier on this stream) were the counts' last readers
         const int nz = *a.zn;
         for (int r = (int)(blockIdx.x * blockDim.x + threadIdx.x); r < nz; r += (int)(gridDim.x * blockDim.x))
@@ -509,26 +622,36 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
     }
 }
 
-__global__ __launch_bounds__(TB_THREADS) void time_bwd_kernel(const float* __restrict__ gseg, const float* __restrict__ prm,
-                                                       float* __restrict__ grad, FlatOffsets F, int XD, int TD, int H, int KF,
-                                                       int TS, int stage_g) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    time_bwd_body(gseg, prm, grad, F, XD, TD, H, KF, TS, stage_g, sm, [] {});
-}
-// time_bwd and the actor's l2_back in one launch (both follow the actor's dW and are independent of
-// each other): workgroup 0 runs the time-MLP backward, the others l2_back's row groups, TB_THREADS /
-// 256 per workgroup
+// time_bwd, the actor's l2_back and its out_back in one launch (all follow the actor's dW and are
+// independent of each other): workgroup 0 runs the time-MLP backward, the others TB_THREADS / 256 groups
+// each, group g l2_back's row group g and then out_back's group g (as many workgroups as the larger
+// count needs: extra workgroups waited for CUs beside the other stream's kernels)
+template <int PREC>
 __global__ __launch_bounds__(TB_THREADS) void time_l2_bwd_kernel(const float* __restrict__ gseg,
                                                           const float* __restrict__ prm, float* __restrict__ grad,
                                                           FlatOffsets F, int XD, int TD, int H, int KF, int TS,
-                                                          int stage_g, L2Back l2b, int l2_groups) {
+                                                          int stage_g, L2Back l2b, int l2_groups, OutBack ob,
+                                                          int ob_groups) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     if (blockIdx.x == 0) {
         time_bwd_body(gseg, prm, grad, F, XD, TD, H, KF, TS, stage_g, sm, [] {});
         return;
     }
-    const int grp = ((int)blockIdx.x - 1) * (TB_THREADS / 256) + (int)threadIdx.x / 256;
-    if (grp < l2_groups) l2_back_rows(l2b, grp, (int)threadIdx.x % 256);
+    constexpr int per = TB_THREADS / 256;
+    const int grp = ((int)blockIdx.x - 1) * per + (int)threadIdx.x / 256;
+    if (grp < l2_groups) l2_back_rows_p<PREC>(l2b, grp, (int)threadIdx.x % 256);
+    if (ob_groups > 0) out_back_group<PREC>(ob, grp, grp < ob_groups, (int)threadIdx.x % 256, sm + ((int)threadIdx.x / 256) * OB_RED);
+}
+
+// the precision instantiation of the l2_back / time_l2_bwd kernels
+static void launch_l2_back(int prec, unsigned blocks, hipStream_t s, const L2Back& l2b, int l2g, const OutBack& ob, int obg) {
+    if (prec == DPPO_BF16) hipLaunchKernelGGL(l2_back_kernel<DPPO_BF16>, dim3(blocks), dim3(256), 0, s, l2b, l2g, ob, obg);
+    else if (prec == DPPO_F16) hipLaunchKernelGGL(l2_back_kernel<DPPO_F16>, dim3(blocks), dim3(256), 0, s, l2b, l2g, ob, obg);
+    else hipLaunchKernelGGL(l2_back_kernel<DPPO_F32>, dim3(blocks), dim3(256), 0, s, l2b, l2g, ob, obg);
+}
+static const void* time_l2_bwd_fn(int prec) {
+    return prec == DPPO_BF16 ? (const void*)time_l2_bwd_kernel<DPPO_BF16>
+         : prec == DPPO_F16 ? (const void*)time_l2_bwd_kernel<DPPO_F16> : (const void*)time_l2_bwd_kernel<DPPO_F32>;
 }
 
 // dynamic LDS of time_bwd_body over nb buckets; *stage_g = whether the bucket sums are staged too
@@ -1295,6 +1418,8 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
                                        params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
             }
             DPPO_HIP(hipGetLastError());
+            rc = dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, s);   // cross-element: not per element
+            if (rc) return rc;
             return dppo_mark_tables_stale(D, precision, actor_params, packed_actor, true);
         }
         ActorStep a = {};
@@ -1349,6 +1474,9 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
                                    params, grads, m, v, n, h, metrics, mout, n_metrics, metrics_tag, vt, a);
         }
         DPPO_HIP(hipGetLastError());
+        // the row tiles' fold needs every element final: its own small launch (pack.hip PACK_RT_FOLD)
+        rc = dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, s);
+        if (rc) return rc;
         // TEMB (every precision) and the split sampler's tables (2-byte) wait for the next sampler launch
         return dppo_mark_tables_stale(D, precision, actor_params, packed_actor, true);
     }
@@ -1604,31 +1732,45 @@ static SideStream* side_stream() {
 
 // the actor's l2 weight gradient from pl2 (l2_back_kernel: no LDS, so it starts on any CU with a
 // free wave slot), then the time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg)
-static int launch_time_bwd(const Dims& D, int precision, const float* gseg, const float* pl2, const void* packed_actor,
-                           const float* actor_params, float* ga, int nb, int TS, hipStream_t s, bool l2_back = true) {
+// the actor's out_back (dW_out through the folded forward) over the pl2 / pa0 sums of the dW launch
+static OutBack make_out_back(const Dims& D, int precision, const float* actor_params, const float* pl2, const float* pa0,
+                             float* ga) {
+    const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
+    return OutBack{actor_params, FA, pl2, pa0, ga + FA.out_b, ga + FA.out_w, D.H, D.IN, D.XD, precision};
+}
+
+// after the actor's dW: the time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg),
+// W_out's gradient (out_back) and, unless the l2 gradient stays factored, l2's from pl2, in one launch
+static int launch_time_bwd(const Dims& D, int precision, const float* gseg, const float* pl2, const float* pa0,
+                           const void* packed_actor, const float* actor_params, float* ga, int nb, int TS, hipStream_t s,
+                           bool l2_back = true) {
     const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
     const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     L2Back l2b = {pl2, ga + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b, D.H,
                   D.XD, precision, nullptr, nullptr, nullptr};
     DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
+    DPPO_CHECK(D.H <= 768 && D.IN <= 256 && D.H % OB_ROWS == 0, "out_back: hidden %d > 768 or in_dim %d > 256", D.H, D.IN);
     // (time_bwd forked onto a side stream beside l2_back measured slower: 0.428 vs 0.406 ms per
     // minibatch, same box, tools/r03_ab2.sh; since r04 the two share one launch instead)
     int stage_g = 0;
-    const size_t tsm = time_bwd_lds(D, nb, &stage_g);
+    const size_t tsm0 = time_bwd_lds(D, nb, &stage_g);
+    const size_t tsm = tsm0 > sizeof(float) * OB_RED * (TB_THREADS / 256) ? tsm0 : sizeof(float) * OB_RED * (TB_THREADS / 256);
     DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
-    if (l2_back) {
-        const int groups = dppo_cdiv(D.H, L2B_ROWS), per = TB_THREADS / 256;
-        { const int rc_ = dppo_func_lds((const void*)time_l2_bwd_kernel, tsm); if (rc_) return rc_; }
-        DppoKtScope kt(KT_TIME_BWD, s);
-        hipLaunchKernelGGL(time_l2_bwd_kernel, dim3(1 + dppo_cdiv(groups, per)), dim3(TB_THREADS), tsm, s, gseg,
-                           actor_params, ga, FA, D.XD, D.TD, D.H, nb, TS, stage_g, l2b, groups);
-        DPPO_HIP(hipGetLastError());
-        return DPPO_OK;
-    }
-    { const int rc_ = dppo_func_lds((const void*)time_bwd_kernel, tsm); if (rc_) return rc_; }
+    const int per = TB_THREADS / 256;
+    const int l2g = l2_back ? dppo_cdiv(D.H, L2B_ROWS) : 0, obg = dppo_cdiv(D.H, OB_ROWS);
+    { const int rc_ = dppo_func_lds(time_l2_bwd_fn(precision), tsm); if (rc_) return rc_; }
     DppoKtScope kt(KT_TIME_BWD, s);
-    hipLaunchKernelGGL(time_bwd_kernel, dim3(1), dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD, D.TD, D.H,
-                       nb, TS, stage_g);
+    const OutBack ob = make_out_back(D, precision, actor_params, pl2, pa0, ga);
+    const dim3 grid(1 + dppo_cdiv(l2g > obg ? l2g : obg, per));
+    if (precision == DPPO_BF16)
+        hipLaunchKernelGGL(time_l2_bwd_kernel<DPPO_BF16>, grid, dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD,
+                           D.TD, D.H, nb, TS, stage_g, l2b, l2g, ob, obg);
+    else if (precision == DPPO_F16)
+        hipLaunchKernelGGL(time_l2_bwd_kernel<DPPO_F16>, grid, dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD,
+                           D.TD, D.H, nb, TS, stage_g, l2b, l2g, ob, obg);
+    else
+        hipLaunchKernelGGL(time_l2_bwd_kernel<DPPO_F32>, grid, dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD,
+                           D.TD, D.H, nb, TS, stage_g, l2b, l2g, ob, obg);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -1641,7 +1783,7 @@ static int launch_critic_l2_back(const Dims& D, int precision, const float* cpl2
     L2Back l2b = {cpl2, gc + FC.out_b, (const uint8_t*)packed_critic + L.off[SEG_W_OUT], gc + FC.l2_w, gc + FC.l2_b, D.HC, 1,
                   precision, zcnt, zlist, zn};
     DppoKtScope kt(KT_L2_BACK, s);
-    hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.HC, L2B_ROWS)), dim3(256), 0, s, l2b);
+    launch_l2_back(precision, (unsigned)dppo_cdiv(D.HC, L2B_ROWS), s, l2b, dppo_cdiv(D.HC, L2B_ROWS), OutBack{}, 0);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -1653,7 +1795,7 @@ static ZeroArgs minibatch_zero_args(const Dims& D, const PpoWorkspace& ws, float
     const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
     const FlatOffsets FC = make_flat_offsets(D.SD, D.HC, 1, 0);
     ZeroArgs z = {};
-    const size_t actor_acc = (size_t)((const uint8_t*)(ws.gseg + 16 * D.H) - (const uint8_t*)ws.pl2);
+    const size_t actor_acc = (size_t)((const uint8_t*)(ws.gseg + 16 * D.H) - (const uint8_t*)ws.pl2);   // pl2 | pa0 | gseg
     const size_t critic_acc = (size_t)((const uint8_t*)(ws.crow_cnt + 1) - (const uint8_t*)ws.cpl2);
     if (parts == 3) {
         z.p[0] = grads; z.n[0] = (FA.count + FC.count) * sizeof(float);
@@ -1791,7 +1933,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
             add(ws.a0T, D.IN, ws.dh1T, D.H, ga + FA.in_w, EXTRA_ONEHOT, ws.gseg);
             add(ws.u1T, D.H, ws.dh2T, D.H, ga + FA.l1_w, EXTRA_ONES, ga + FA.l1_b);
             add(ws.u2T, D.H, ws.dyT, D.XD, l2_def ? ga + FA.l2_w : ws.pl2, EXTRA_NONE, nullptr);   // l2 through the out layer
-            add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
+            add(ws.a0T, D.IN, ws.dyT, D.XD, ws.pa0, EXTRA_ONES, ga + FA.out_b);   // out through the fold (out_back)
         } else {
             add(ws.csT, D.SD, ws.cdh1T, D.HC, gc + FC.in_w, EXTRA_ONES, gc + FC.in_b);
             add(ws.cu1T, D.HC, ws.cdh2T, D.HC, gc + FC.l1_w, EXTRA_ONES, gc + FC.l1_b);
@@ -1840,16 +1982,21 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
 
     // after the actor's dW: the time-MLP backward (+ l2_back when l2 is materialised), unless the
     // caller's actor step (dppo_actor_step) runs the time-MLP backward itself
+    const float* pl2_src = l2_def ? ga + FA.l2_w : ws.pl2;
     auto actor_tail = [&]() -> int {
         if (!(hp->flags & DPPO_PPO_TIME_BWD_IN_STEP))
-            return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_ft, actor_params, ga, D.KF, D.TS, s, !l2_def);
-        if (l2_def) return DPPO_OK;
+            return launch_time_bwd(D, precision, ws.gseg, pl2_src, ws.pa0, packed_ft, actor_params, ga, D.KF, D.TS, s,
+                                   !l2_def);
+        // the caller's actor step runs the time-MLP backward: W_out's gradient (and l2's unless it
+        // stays factored) here, before that step reads them
         const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
         L2Back l2b = {ws.pl2, ga + FA.out_b, (const uint8_t*)packed_ft + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b,
                       D.H, D.XD, precision, nullptr, nullptr, nullptr};
         DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
+        const int l2g = l2_def ? 0 : dppo_cdiv(D.H, L2B_ROWS), obg = dppo_cdiv(D.H, OB_ROWS);
         DppoKtScope kt(KT_L2_BACK, s);
-        hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
+        launch_l2_back(precision, (unsigned)(l2g > obg ? l2g : obg), s, l2b, l2g,
+                       make_out_back(D, precision, actor_params, pl2_src, ws.pa0, ga), obg);
         DPPO_HIP(hipGetLastError());
         return DPPO_OK;
     };
@@ -1954,7 +2101,7 @@ extern "C" int dppo_materialize_l2(const dppo_dims* d, int precision, const void
     L2Back l2b = {ws.pl2, grads + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], grads + FA.l2_w,
                   grads + FA.l2_b, D.H, D.XD, precision, nullptr, nullptr, nullptr};
     DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
-    hipLaunchKernelGGL(l2_back_kernel, dim3(dppo_cdiv(D.H, L2B_ROWS)), dim3(256), 0, s, l2b);
+    launch_l2_back(precision, (unsigned)dppo_cdiv(D.H, L2B_ROWS), s, l2b, dppo_cdiv(D.H, L2B_ROWS), OutBack{}, 0);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -2003,7 +2150,7 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     ZeroArgs z = {};
     z.p[0] = grads; z.n[0] = FA.count * sizeof(float);
     z.p[1] = metrics; z.n[1] = 16 * sizeof(double);
-    z.p[2] = ws.pl2; z.n[2] = (size_t)D.H * D.XD * sizeof(float);
+    z.p[2] = ws.pl2; z.n[2] = (size_t)((const uint8_t*)ws.gseg - (const uint8_t*)ws.pl2);   // pl2 | pa0
     hipLaunchKernelGGL(zero_kernel, dim3(256), dim3(256), 0, s, z);
     DPPO_HIP(hipGetLastError());
 
@@ -2033,7 +2180,7 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     add(ws.a0T, D.IN, ws.dh1T, D.H, ga + FA.in_w, EXTRA_NONE, nullptr);
     add(ws.u1T, D.H, ws.dh2T, D.H, ga + FA.l1_w, EXTRA_ONES, ga + FA.l1_b);
     add(ws.u2T, D.H, ws.dyT, D.XD, ws.pl2, EXTRA_NONE, nullptr);   // l2 through the out layer
-    add(ws.h3T, D.H, ws.dyT, D.XD, ga + FA.out_w, EXTRA_ONES, ga + FA.out_b);
+    add(ws.a0T, D.IN, ws.dyT, D.XD, ws.pa0, EXTRA_ONES, ga + FA.out_b);   // out through the fold (out_back)
     w.ldm = ws.ldm;
     w.seg = ws.seg;
     w.out_scale = 1.f / gscale;
@@ -2058,5 +2205,5 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
         hipLaunchKernelGGL(seg_reduce_kernel<float>, dim3(D.H), dim3(256), 0, s, (const float*)ws.dh1T, ws.seg, ws.ldm,
                            D.K, ws.gseg, D.H, inv);
     DPPO_HIP(hipGetLastError());
-    return launch_time_bwd(D, precision, ws.gseg, ws.pl2, packed_actor, actor_params, ga, D.K, 1, s);
+    return launch_time_bwd(D, precision, ws.gseg, ws.pl2, ws.pa0, packed_actor, actor_params, ga, D.K, 1, s);
 }

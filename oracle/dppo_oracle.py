@@ -225,7 +225,10 @@ def residual_mlp_forward(p, x, act, prefix, rnd=None, round_h3=True):
     """rnd: optional operand-rounding function applied exactly where the bf16 kernels round
     (GEMM A/B operands; accumulators, residual h1 and epilogues stay fp32). None = exact f64.
     round_h3=False: the out-Dense input is not rounded (the split sampler feeds it as a hi/lo
-    bf16 pair, sampler_split.hip), only its weights are."""
+    bf16 pair, sampler_split.hip), only its weights are. It is also the folded form of the actor's
+    row tiles (csrc/rowtile.hip, dppo_layout.h RT_*: eps = relu(h2) M + a0 M0 + b with M = rnd(W_l2)
+    rnd(W_out), M0 = rnd(W_in) rnd(W_out) to fp32), whose backward forms d relu(h2) = dy M^T without
+    rounding dh3 (residual_mlp_backward reads cache["fold"])."""
     a, _ = ACT[act]
     R = rnd or _ident
     xr = R(x)
@@ -236,7 +239,7 @@ def residual_mlp_forward(p, x, act, prefix, rnd=None, round_h3=True):
     h3 = u2 @ R(p[prefix + "l2_w"]) + np.asarray(p[prefix + "l2_b"], np.float64) + h1
     h3r = R(h3) if round_h3 else np.asarray(h3, np.float64)
     y = h3r @ R(p[prefix + "out_w"]) + np.asarray(p[prefix + "out_b"], np.float64)
-    return y, dict(x=xr, h1=h1, u1=u1, h2=h2, u2=u2, h3=h3r, R=R)
+    return y, dict(x=xr, h1=h1, u1=u1, h2=h2, u2=u2, h3=h3r, R=R, fold=not round_h3)
 
 
 def residual_mlp_backward(p, cache, dy, act, prefix):
@@ -256,7 +259,10 @@ def residual_mlp_backward(p, cache, dy, act, prefix):
     # csrc/update.hip l2_back_rows): u2^T (dy W_out^T) = (u2^T dy) W_out^T, unrounded dh3
     g[prefix + "l2_w"] = (cache["u2"].T @ dyr) @ wo.T
     g[prefix + "l2_b"] = g[prefix + "out_b"] @ wo.T
-    du2 = dh3r @ R(p[prefix + "l2_w"]).T
+    if cache.get("fold"):   # the folded row tile: dy (R(W_l2) R(W_out))^T, dh3 unrounded on this path
+        du2 = dyr @ (R(p[prefix + "l2_w"]) @ wo).T
+    else:
+        du2 = dh3r @ R(p[prefix + "l2_w"]).T
     dh2 = Rg(du2 * ag(cache["h2"]))
     g[prefix + "l1_w"] = cache["u1"].T @ dh2
     g[prefix + "l1_b"] = dh2.sum(0)
@@ -378,14 +384,15 @@ def gaussian_logprob(x, mu, std):
 # ----------------------------------------------------------------------------------------------
 # a10: get_logprobs (diffusion_vpg.py:343-425)
 # ----------------------------------------------------------------------------------------------
-def get_logprobs(p_ft, sched, state, chains, ft_steps, min_logprob_std=0.1, rnd=None):
-    """state [n,To,Do], chains [n,K'+1,Ta,Da] -> logprob [n*K', Ta, Da]; row = n*K' + j, t = K'-1-j."""
+def get_logprobs(p_ft, sched, state, chains, ft_steps, min_logprob_std=0.1, rnd=None, round_h3=False):
+    """state [n,To,Do], chains [n,K'+1,Ta,Da] -> logprob [n*K', Ta, Da]; row = n*K' + j, t = K'-1-j.
+    round_h3=False: the folded row tile's rounding points (residual_mlp_forward)."""
     n = chains.shape[0]
     cond = np.repeat(state, ft_steps, axis=0)                    # :374-379 (sample-major tile)
     t_all = np.tile(np.arange(ft_steps - 1, -1, -1), n)          # :385-390
     prev = chains[:, :-1].reshape(-1, *chains.shape[2:])          # :402-407
     nxt = chains[:, 1:].reshape(-1, *chains.shape[2:])
-    eps, _ = diffusion_mlp_forward(p_ft, prev, t_all * _tstride(sched), cond, rnd=rnd)
+    eps, _ = diffusion_mlp_forward(p_ft, prev, t_all * _tstride(sched), cond, rnd=rnd, round_h3=round_h3)
     mu, logvar, _ = p_mean_var(sched, eps, prev, t_all)
     std = np.clip(np.exp(0.5 * logvar), min_logprob_std, 1e6)    # :417-418
     return gaussian_logprob(nxt, mu, std)
@@ -399,12 +406,13 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
            advantages, oldlogprobs, ft_steps, gamma_denoising=0.99, clip_ploss_coef=0.01,
            clip_ploss_coef_base=0.01, clip_ploss_coef_rate=3.0, clip_vloss_coef=None,
            norm_adv=True, min_logprob_std=0.1, vf_coef=0.5, with_grad=True, reward_horizon=4, rnd=None,
-           adv_mean_std=None, denom=None, critic_dedup=None, eta_grad=False):
+           adv_mean_std=None, denom=None, critic_dedup=None, eta_grad=False, round_h3=False):
     """Returns (metrics dict, grads_actor dict, grads_critic dict).
 
     Data-parallel restatement hooks: adv_mean_std overrides the minibatch
     advantage mean/std (the global ones), denom overrides the row count the means divide by
     (the global minibatch size) — summing such per-shard gradients gives the full-batch one.
+    round_h3=False: the folded actor row tile's rounding points (residual_mlp_forward).
 
     oldlogprobs may be per element [b,Ta,Da] (clipped & averaged here, :50-59) or already the
     clipped per-row mean [b]."""
@@ -413,7 +421,7 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
     if rnd is round_fp16:                    # the fp16 gradient images use the row-tied scale
         rnd = round_fp16_rows(b if denom is None else denom)
     t = ft_steps - 1 - j                                          # :456-458
-    eps, acache = diffusion_mlp_forward(p_ft, chains_prev, t * _tstride(sched), obs, rnd=rnd)
+    eps, acache = diffusion_mlp_forward(p_ft, chains_prev, t * _tstride(sched), obs, rnd=rnd, round_h3=round_h3)
     mu, logvar, pm = p_mean_var(sched, eps, chains_prev, t)
     std = np.clip(np.exp(0.5 * logvar), min_logprob_std, 1e6)
     lp_el = gaussian_logprob(chains_next, mu, std)
@@ -520,7 +528,7 @@ def q_sample(sched, x_start, t, noise):
     return sa.reshape(shape).astype(np.float64) * x_start + s1.reshape(shape).astype(np.float64) * noise
 
 
-def p_losses(p, sched, x_start, state, t, noise, with_grad=True, rnd=None, denom=None):
+def p_losses(p, sched, x_start, state, t, noise, with_grad=True, rnd=None, denom=None, round_h3=False):
     """diffusion.py:186-194: loss = mean((network(q_sample(x_0, t, noise), t, cond) - noise)^2) and
     its parameter gradient. x_start, noise [B,Ta,Da]; state [B,To,Do]; t [B] int (the draws of
     :182 and :187 are inputs here). denom overrides the element count of the mean (data-parallel
@@ -529,7 +537,7 @@ def p_losses(p, sched, x_start, state, t, noise, with_grad=True, rnd=None, denom
     if rnd is round_fp16:                    # the fp16 gradient images use the row-tied scale
         xd = x_start.shape[1] * x_start.shape[2]
         rnd = round_fp16_rows(x_start.shape[0] if denom is None else denom // xd)
-    eps, cache = diffusion_mlp_forward(p, xn, np.asarray(t), state, rnd=rnd)
+    eps, cache = diffusion_mlp_forward(p, xn, np.asarray(t), state, rnd=rnd, round_h3=round_h3)
     e = eps - noise
     n = e.size if denom is None else denom
     loss = float((e ** 2).sum() / n)
