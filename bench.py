@@ -112,7 +112,7 @@ def cpu_baseline(cfg, n_envs, S, bs):
 # run: the library's kernel timer (dppo_kernel_timing, HIP events around each launch on its own
 # stream) over one instrumented iteration. The committed rocprofv3 whole-iteration trace of the
 # same workload is reported beside them as a cross-check.
-KERNEL_STATS_CSV = os.path.join(ROOT, "profiles", "r04n_iteration_kernel_stats.csv")
+KERNEL_STATS_CSV = os.path.join(ROOT, "profiles", "r05p_iteration_kernel_stats.csv")
 
 
 def kernel_times_live(agent):
@@ -150,8 +150,12 @@ def kernel_stats_csv(path=KERNEL_STATS_CSV):
             k = r["Name"]
             k = k[5:] if k.startswith("void ") else k
             base = k.split("<")[0].split("(")[0].split("::")[-1]
-            if "pack_all_kernel" in base:
+            if "pack_all_kernel" in base or base == "rt_fold_kernel":   # the live timer's KT_PACK_ALL scope
                 base = "pack_all_kernel"
+            elif base == "time_l2_bwd_kernel":
+                base = "time_bwd_kernel"
+            elif "actor_tile_step_kernel" in k or "actor_step_kernel" in k:
+                base = "adamw_kernel"
             elif base.startswith("actor_rowtile_kernel"):
                 base = "actor_rowtile_train" if "true" in k else "actor_rowtile_logprob"
             elif base.startswith("critic_rowtile_kernel"):
@@ -207,7 +211,10 @@ def kernel_figures(d, S, E, batch, n_mb, precision, times, source, iters=1):
         fl = 2 * 2 * na * batch            # forward + backward-dX of the actor, per minibatch
         ns = tot * 1e6 / n_mb
         out["actor_rowtile_train"] = {"flops_per_minibatch": fl, "launches": calls, "us_per_minibatch": ns / 1e3,
-                                      "achieved_TFLOPs": fl / ns / 1e3, "frac": fl / ns / 1e3 / peak}
+                                      "achieved_TFLOPs": fl / ns / 1e3, "frac": fl / ns / 1e3 / peak,
+                                      "note": "algorithmic FLOPs of the reference network (its l2 layer included); "
+                                              "since r05 the kernel folds l2 into the out-Dense (DESIGN §3) and "
+                                              "computes about half of them"}
     dw = [times[k] for k in ("dw_kernel_actor", "dw_kernel_critic", "dw_kernel") if k in times]
     if dw:
         tot = sum(t for t, _ in dw)

@@ -483,6 +483,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     self._met_dev = [torch.zeros(16, dtype=torch.float64, device=self.device) for _ in range(2)]
                     self._ev_rows = torch.cuda.Event()
                     self._ev_met = torch.cuda.Event()
+                    self._ev_astep = torch.cuda.Event()
                 side = self._side
                 side.wait_stream(stream)
                 na = m.n_actor
@@ -571,6 +572,11 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             st_main = stream.cuda_stream
             st_side = side.cuda_stream if split else None
             met_ptrs = [t.data_ptr() for t in self._met_dev] if split else None
+            # DPPO_CRITIC_AFTER_STEP (A/B knob): the critic's half of minibatch k waits for the actor's
+            # optimizer step of k - 1 (its AdamW and fold launches are short and latency-bound; the
+            # critic's row tiles started beside them took the CUs they wait for), so it overlaps the
+            # actor's row tiles and dW of k instead
+            critic_after = split and not dp and os.environ.get("DPPO_CRITIC_AFTER_STEP", "0") != "0"
             k = 0
             for update_epoch in range(self.update_epochs):
                 for batch in range(num_batch):
@@ -594,6 +600,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     if split:
                         met = self._met_dev[k % 2]
                         met_p = met_ptrs[k % 2]
+                        if critic_after and k > 0:
+                            side.wait_event(self._ev_astep)
                         run_mb(*mb_args, **mb_kw, part=2, metrics=met_p, stream=st_side, precleared=pre)
                         if not tagged and not dp:
                             ev_c = torch.cuda.Event()
@@ -669,6 +677,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             else:
                                 step_actor(lr, metrics=met_p, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
                                            stream=st_main, clear=ca)
+                            if critic_after:
+                                self._ev_astep.record(stream)
                             step_critic(lr, metrics=met_p + 8, metrics_out=self._cmet_map[slot].address,   # met[1]
                                         n_metrics=1, metrics_tag=ctag, stream=st_side, clear=cc)
                             cleared = fuse

@@ -280,16 +280,6 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
                                        NextLayers{W(SEG_T_OUT), KSO, W(SEG_RT_TFOLD), KSO});
     else
         gemm_queue<P, MT, NT, KSH, QD, true, true>(tA, ldh, W(SEG_W_L1), ntile0, acc, lane, R, after_l1);
-    // the folded out-Dense's fragments: fetched here so they land during the relu / stores / barrier
-    out_prefetch<NOK, NO, WAVES>(obh, W(SEG_RT_FOLD), KSH, wave, lane);
-    if constexpr (TWO) out_prefetch<NOK, NO, WAVES>(obl, wsrc(rs, L.off[SEG_RT_FOLD] + fold_mat), KSH, wave, lane);
-    if (wave < KSI) {
-#pragma unroll
-        for (int n = 0; n < NO; ++n) {
-            o0[0][n] = load_bfrag_c(W(SEG_RT_FOLD0), KSI, n, wave, lane);
-            if constexpr (TWO) o0[1][n] = load_bfrag_c(wsrc(rs, L.off[SEG_RT_FOLD0] + fold0_mat), KSI, n, wave, lane);
-        }
-    }
     add_bias(acc, bias + H, ntile0, lane);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -303,6 +293,17 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
     asm volatile("" : "+v"(mask2));
     store_acc_lds<P, MT, NT>(tB, ldh, ntile0, lane, acc);
     if constexpr (train) store_accT<P, MT, NT>(wsr, ws_off(a.ws, a.ws.u2T), ldm32, ntile0, grow32, lane, acc);
+    // the folded out-Dense's fragments: fetched after the l1 result's stores (held
+    // through them they pushed the 16-wave tile into spills), landing during the barrier
+    out_prefetch<NOK, NO, WAVES>(obh, W(SEG_RT_FOLD), KSH, wave, lane);
+    if constexpr (TWO) out_prefetch<NOK, NO, WAVES>(obl, wsrc(rs, L.off[SEG_RT_FOLD] + fold_mat), KSH, wave, lane);
+    if (wave < KSI) {
+#pragma unroll
+        for (int n = 0; n < NO; ++n) {
+            o0[0][n] = load_bfrag_c(W(SEG_RT_FOLD0), KSI, n, wave, lane);
+            if constexpr (TWO) o0[1][n] = load_bfrag_c(wsrc(rs, L.off[SEG_RT_FOLD0] + fold0_mat), KSI, n, wave, lane);
+        }
+    }
     lds_sync();
     PHASE(2);
     // ---- L4 (folded): eps = relu(h2) M + a0 M0 + RT_BOUT; the relu(h2) k-steps dealt over the waves

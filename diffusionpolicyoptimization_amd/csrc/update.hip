@@ -454,19 +454,35 @@ __device__ inline void out_back_n(const OutBack& a, int b, bool valid, int t, fl
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) acc[r][q] = fmaf(wv[u][r], pv[u][q], acc[r][q]);
     }
+    // the wave's OB_ROWS x NQP partial sums (q padded to a power of two) reduced over its 64 lanes by
+    // recursive halving: each xor step a lane keeps half of its vector and adds the partner's copy of
+    // that half, so 6 steps leave lane l with the sums of V / 64 values (63 lane swaps for V = 64,
+    // against 11 dependent DPP / readlane ops per value for a whole-wave sum each)
+    constexpr int NQP = NQ <= 16 ? 16 : 32, V = OB_ROWS * NQP, PER = V / 64;
+    float x[V];
 #pragma unroll
     for (int r = 0; r < OB_ROWS; ++r)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const float v = wave_sum(acc[r][q]);
-            if (lane == 0) red[w * OB_ROWS * NQ + r * NQ + q] = v;
+        for (int q = 0; q < NQP; ++q) x[r * NQP + q] = q < NQ ? acc[r][q] : 0.f;
+#pragma unroll
+    for (int st = 0; st < 6; ++st) {
+        const int m = 32 >> st, half = V >> (st + 1);
+        const bool up = (lane & m) != 0;
+#pragma unroll
+        for (int i = 0; i < half; ++i) {
+            const float send = up ? x[i] : x[i + half];
+            const float keep = up ? x[i + half] : x[i];
+            x[i] = keep + __shfl_xor(send, m, 64);
         }
+    }
+    // lane l holds values PER l .. PER l + PER - 1 (the kept halves' offsets sum to PER l)
+#pragma unroll
+    for (int i = 0; i < PER; ++i) red[w * V + PER * lane + i] = x[i];
     __syncthreads();
     if (valid && t < OB_ROWS * N) {
-        const int r = t / N, q = t % N, f = f0 + r;
-        constexpr int S = OB_ROWS * NQ;
+        const int r = t / N, q = t % N, f = f0 + r, v = r * NQP + q;
         if (f < H) {
-            const float s = (red[r * NQ + q] + red[S + r * NQ + q]) + (red[2 * S + r * NQ + q] + red[3 * S + r * NQ + q]);
+            const float s = (red[v] + red[V + v]) + (red[2 * V + v] + red[3 * V + v]);
             const float bb = a.prm[a.F.l2_b + f] + a.prm[a.F.in_b + f];
             a.gw[(size_t)f * N + q] = fmaf(bb, a.gob[q], s);
         }
