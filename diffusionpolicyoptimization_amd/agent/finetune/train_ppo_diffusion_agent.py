@@ -510,13 +510,13 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             fuse = split and self.minibatch_hook is None and fuse_mode != "0"
             fuse_actor = fuse and fuse_mode == "all"
             tb_in_step = fuse_actor and not dp
-            # DPPO_L2_DEFER = "auto" (default) | "1" | "0". Deferred, the actor's step forms dW_l2 per
-            # element from pl2; materialised, an l2_back launch follows the actor's dW. "auto" materialises
-            # below 16,384 rows per rank (profiles/r04l_tail_ab.txt; the one-launch actor step with the
-            # virtual l2 takes 32 vs 19 us alone, profiles/r05g_bench_step.txt).
-            l2_mode = os.environ.get("DPPO_L2_DEFER", "auto")
-            l2_def = (self.max_grad_norm is None and self.minibatch_hook is None and l2_mode != "0"
-                      and (l2_mode == "1" or rows_local_full >= 16384))
+            # DPPO_L2_DEFER = "0" (default, also "auto") | "1". Deferred, the actor's step forms dW_l2 per
+            # element from pl2 (its virtual gradient); materialised, l2_back's groups in the launch after the
+            # actor's dW do. r04 materialised only below 16,384 rows per rank; since the row-tile fold (r05)
+            # the coalesced actor step with the virtual l2 is the slower form at every size (N = 1 update
+            # 10.3-10.4 vs 11.2-11.4 ms per iteration, profiles/r05r_l2_defer_ab.txt)
+            l2_mode = os.environ.get("DPPO_L2_DEFER", "0")
+            l2_def = (self.max_grad_norm is None and self.minibatch_hook is None and l2_mode == "1")
             # the actor's step (AdamW + pack) clears the actor's accumulators in its pack launch
             clear_actor = fuse and os.environ.get("DPPO_ACTOR_CLEAR", "1") != "0"
             actor_fused = os.environ.get("DPPO_ACTOR_FUSED", "1") != "0"

@@ -43,11 +43,14 @@ static_assert(DW_LINE == 64 || DW_LINE == 128, "DPPO_DW_LINE must be 64 or 128")
 // bound by the latency of its staged loads (Little's law over the LDS ring: about 96 KiB in flight
 // per CU either way), so the 256-row tile's 1.33x MFMAs per staged byte is what it buys; the
 // k-tile edge is chosen per launch (DPPO_DW_TK: measurement knob).
-template <int WK> struct DWGeom {
+// RC caps the ring (the critic's dW runs beside the actor's time-MLP backward, whose workgroup needs
+// LDS on the same CU: a 3-slot WK = 128 ring, 101 KiB, leaves it room)
+template <int WK, int RC = 8> struct DWGeom {
     static constexpr int W = WK / 32;                    // waves: 4 or 8
     static constexpr int AOPB = WK * DW_LINE;            // A (activation) operand's stage image
     static constexpr int SLOT = AOPB + DW_BOPB + 1024;   // A | B | the stage's seg bytes (padded)
-    static constexpr int RING = 160 * 1024 / SLOT < 8 ? 160 * 1024 / SLOT : 8;   // ring slots (RING - 1 in flight)
+    static constexpr int RING0 = 160 * 1024 / SLOT < 8 ? 160 * 1024 / SLOT : 8;
+    static constexpr int RING = RING0 < RC ? RING0 : RC;   // ring slots (RING - 1 in flight)
     static constexpr int AI = WK / DW_FPI / W;           // A wave-instructions per wave per stage
     static constexpr int BI = DW_TN / DW_FPI / W;        // B wave-instructions per wave per stage
     static_assert(RING * SLOT <= 160 * 1024, "dW ring exceeds the CU's LDS");
@@ -113,12 +116,12 @@ __device__ inline void vm_wait() {
 // register allocator sees one uniform accumulator set per loop (a data-dependent MFMA inside
 // one loop made hipcc shuttle the accumulators between AGPRs and VGPRs every k-step).
 // SEGLD: this wave also copies the stage's seg bytes (ONEHOT extra rows).
-template <class P, int WK, bool EXTRA, bool SEGLD>
+template <class P, int WK, int RC, bool EXTRA, bool SEGLD>
 __device__ __forceinline__ void dw_loop(uint8_t* smem, const DWArgs& a, const DWProb& pr, int nst, size_t m_begin,
-                                        int wave, int lane, const typename P::AT* const (&srcA)[DWGeom<WK>::AI],
-                                        const typename P::AT* const (&srcB)[DWGeom<WK>::BI],
+                                        int wave, int lane, const typename P::AT* const (&srcA)[DWGeom<WK, RC>::AI],
+                                        const typename P::AT* const (&srcB)[DWGeom<WK, RC>::BI],
                                         f32x4 (&acc)[4][4], f32x4 (&acce)[4]) {
-    using G = DWGeom<WK>;
+    using G = DWGeom<WK, RC>;
     constexpr int BK = DW_LINE / (int)sizeof(typename P::AT);
     constexpr int OPS = G::AI + G::BI + (SEGLD ? 1 : 0);      // vector-memory ops per stage per wave
     const int wr = wave >> 1, wc = wave & 1;
@@ -187,10 +190,10 @@ static int dw_device_cus() {
     return n;
 }
 
-template <class P, int WK>
-__global__ __launch_bounds__(DWGeom<WK>::W * 64) void dw_kernel(DWArgs a) {
+template <class P, int WK, int RC>
+__global__ __launch_bounds__(WK / 32 * 64) void dw_kernel(DWArgs a) {   // DWGeom::W waves
     using AT = typename P::AT;
-    using G = DWGeom<WK>;
+    using G = DWGeom<WK, RC>;
     constexpr int BK = DW_LINE / (int)sizeof(AT);     // rows per stage: 32 bf16 / 16 fp32 (64-B lines)
     constexpr int EPC = 16 / (int)sizeof(AT);         // elements per 16-B chunk
     // one LDS object (a second __shared__ array can make hipcc drain the glds queue at every
@@ -255,9 +258,9 @@ __global__ __launch_bounds__(DWGeom<WK>::W * 64) void dw_kernel(DWArgs a) {
         for (int j = 0; j < 4; ++j) zero_acc(acc[i][j]);
     }
     // the other waves of an extra tile run the plain loop; the barrier count per stage is identical
-    if (seg_ld) dw_loop<P, WK, true, true>(smem, a, pr, nst, m_begin, wave, lane, srcA, srcB, acc, acce);
-    else if (do_extra) dw_loop<P, WK, true, false>(smem, a, pr, nst, m_begin, wave, lane, srcA, srcB, acc, acce);
-    else dw_loop<P, WK, false, false>(smem, a, pr, nst, m_begin, wave, lane, srcA, srcB, acc, acce);
+    if (seg_ld) dw_loop<P, WK, RC, true, true>(smem, a, pr, nst, m_begin, wave, lane, srcA, srcB, acc, acce);
+    else if (do_extra) dw_loop<P, WK, RC, true, false>(smem, a, pr, nst, m_begin, wave, lane, srcA, srcB, acc, acce);
+    else dw_loop<P, WK, RC, false, false>(smem, a, pr, nst, m_begin, wave, lane, srcA, srcB, acc, acce);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -361,22 +364,30 @@ __device__ inline void l2_back_cols(const L2Back& a, int b, int t, int nt) {
         for (int q = 0; q < NQ; ++q) pv[r][q] = q < N ? a.pl2[(size_t)(h0 + r) * N + q] : 0.f;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) pv[L2B_ROWS][q] = q < N ? a.gob[q] : 0.f;
-    float w[NJ][NQ];
-#pragma unroll
-    for (int c = 0; c < NJ; ++c) {
+    // both columns' W_out values up front when they fit the registers (NQ <= 16), else one column at a
+    // time (the 1024-thread time_l2_bwd workgroups have 128 VGPRs)
+    constexpr int NW = NQ <= 16 ? NJ : 1;
+    float w[NW][NQ];
+    auto load_w = [&](int c, float* dst) {
         const int j = min(t + c * nt, H - 1);
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) w[c][q] = q < N ? packed_elem_t<PREC>(a.wimg, H, j, q) : 0.f;
+        for (int q = 0; q < NQ; ++q) dst[q] = q < N ? packed_elem_t<PREC>(a.wimg, H, j, q) : 0.f;
+    };
+    if constexpr (NW == NJ) {
+#pragma unroll
+        for (int c = 0; c < NJ; ++c) load_w(c, w[c]);
     }
 #pragma unroll
     for (int c = 0; c < NJ; ++c) {
         const int j = t + c * nt;
+        if constexpr (NW != NJ) load_w(c, w[0]);
+        const float* wc = w[NW == NJ ? c : 0];
         if (j >= H) continue;
 #pragma unroll
         for (int r = 0; r <= L2B_ROWS; ++r) {
             float sum = 0.f;
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) sum = fmaf(pv[r][q], w[c][q], sum);
+            for (int q = 0; q < NQ; ++q) sum = fmaf(pv[r][q], wc[q], sum);
             if (r < L2B_ROWS) a.gw[(size_t)(h0 + r) * H + j] = sum;
             else if (b == 0) a.gb[j] = sum;
         }
@@ -387,23 +398,20 @@ __device__ inline void l2_back_n(const L2Back& a, int b, int t) {   // 256 threa
     if (a.H <= 256) l2_back_cols<PREC, 1, NQ>(a, b, t, 256);
     else l2_back_cols<PREC, 2, NQ>(a, b, t, 256);
 }
-template <int PREC>
-__device__ __forceinline__ void l2_back_rows_p(const L2Back& a, int b, int t) {
-    switch (a.N) {     // the action-chunk widths of the cfgs (hopper 12; walker2d / halfcheetah 24), the critic's 1
-        case 1: l2_back_n<PREC, 1>(a, b, t); break;
-        case 12: l2_back_n<PREC, 12>(a, b, t); break;
-        case 24: l2_back_n<PREC, 24>(a, b, t); break;
-        default: l2_back_n<PREC, L2B_MAXN>(a, b, t); break;   // any N <= 32, zero-padded
-    }
-}
-// the kernels below are instantiated per precision (a runtime switch here made hipcc outline these
-// bodies as calls)
+// the kernels below are instantiated per precision and width NQ (the action-chunk widths of the cfgs:
+// hopper 12, walker2d / halfcheetah 24, the critic's 1, any other N <= 32 zero-padded to 32): a runtime
+// switch made hipcc outline the bodies as calls, and the unused widths' registers spilled in the
+// 1024-thread time_l2_bwd workgroups
+__host__ __device__ constexpr int l2_nq(int N) { return N == 1 ? 1 : (N == 12 ? 12 : (N == 24 ? 24 : L2B_MAXN)); }
 // W_out's weight gradient through the folded forward (rowtile.hip: the row tiles never form h3,
 // dppo_ppo.h pa0): dW_out[f][q] = sum_g rnd(W_l2[g][f]) pl2[g][q] + sum_i rnd(W_in[i][f]) pa0[i][q] +
 // (b_l2[f] + b_in[f]) db_out[q], the oracle's h3^T dy with h3 = u2 rnd(W_l2) + b_l2 + a0 rnd(W_in) + b_in.
-// A group of 256 threads forms OB_ROWS rows f: thread t takes rows g = t, t + 256, ... of W_l2 (4 features
-// in one 16-B load) and pl2, and row i = t of W_in / pa0, so each thread pays one round trip; the
-// OB_ROWS x N partial sums reduce over the lanes (DPP) and then the 4 waves through LDS in a fixed order.
+// A group of 256 threads forms OBR rows f (4 for N <= 16, else 2: 64 partial sums per thread either
+// way): thread t takes rows g = t, t + 256 of W_l2 / pl2 (OBR features in one load) and row i = t of
+// W_in / pa0, all loads issued before the FMAs (one round trip; a rolled loop waited for each row in
+// turn); the 64 partial sums reduce over the lanes by recursive halving and then over the 4 waves
+// through LDS in a fixed order. Sized for 128 VGPRs (time_l2_bwd's 1024-thread workgroups: the first
+// form, 4 rows x 32 widths, spilled 1 KB per lane there).
 struct OutBack {
     const float* prm;     // the actor's flat fp32 parameters
     FlatOffsets F;
@@ -413,7 +421,7 @@ struct OutBack {
     float* gw;            // [H][N] dW_out
     int H, IN, N, prec;
 };
-constexpr int OB_ROWS = 4;
+__host__ __device__ constexpr int ob_rows(int N) { return N <= 16 ? 4 : 2; }
 template <int PREC>
 __device__ inline float round_prec(float x) {
     if constexpr (PREC == DPPO_BF16) return (float)(__bf16)x;
@@ -422,48 +430,49 @@ __device__ inline float round_prec(float x) {
 }
 template <int PREC, int NQ>
 __device__ inline void out_back_n(const OutBack& a, int b, bool valid, int t, float* red) {
-    const int H = a.H, N = a.N, f0 = OB_ROWS * b, lane = t & 63, w = t >> 6;
-    const int NE = NQ < L2B_MAXN ? NQ : N;   // the instantiation's width (out_back_group)
-    float acc[OB_ROWS][NQ];
-#pragma unroll
-    for (int r = 0; r < OB_ROWS; ++r)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[r][q] = 0.f;
-    if (valid) {
-        // every load of the thread first (rows t, t + 256, t + 512 of W_l2 / pl2 and row t of W_in / pa0),
-        // then the FMAs: one round trip (a rolled loop waited for each row's loads in turn)
-        constexpr int NG = 3;   // H <= 768 (host-checked)
-        float wv[NG + 1][OB_ROWS], pv[NG + 1][NQ];
-#pragma unroll
-        for (int u = 0; u <= NG; ++u) {
-            const bool l2 = u < NG;
-            const int g = l2 ? t + 256 * u : t;
-            const bool ok = l2 ? g < H : g < a.IN;
-            const float* W = l2 ? a.prm + a.F.l2_w : a.prm + a.F.in_w;
-            const float* P = l2 ? a.pl2 : a.pa0;
-            const f32x4 w4 = ok ? *(const f32x4*)(W + (size_t)g * H + f0) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int r = 0; r < OB_ROWS; ++r) wv[u][r] = round_prec<PREC>(w4[r]);
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) pv[u][q] = (ok && q < NE) ? P[(size_t)(ok ? g : 0) * NE + q] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u <= NG; ++u)
-#pragma unroll
-            for (int r = 0; r < OB_ROWS; ++r)
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) acc[r][q] = fmaf(wv[u][r], pv[u][q], acc[r][q]);
-    }
-    // the wave's OB_ROWS x NQP partial sums (q padded to a power of two) reduced over its 64 lanes by
-    // recursive halving: each xor step a lane keeps half of its vector and adds the partner's copy of
-    // that half, so 6 steps leave lane l with the sums of V / 64 values (63 lane swaps for V = 64,
-    // against 11 dependent DPP / readlane ops per value for a whole-wave sum each)
-    constexpr int NQP = NQ <= 16 ? 16 : 32, V = OB_ROWS * NQP, PER = V / 64;
+    constexpr int OBR = ob_rows(NQ), NQP = NQ <= 16 ? 16 : 32, V = OBR * NQP;   // V = 64
+    static_assert(V == 64, "one value per lane after the halving");
+    const int H = a.H, f0 = OBR * b, lane = t & 63, w = t >> 6;
+    const int NE = NQ < L2B_MAXN ? NQ : a.N;   // the instantiation's width (out_back_group)
     float x[V];
 #pragma unroll
-    for (int r = 0; r < OB_ROWS; ++r)
+    for (int v = 0; v < V; ++v) x[v] = 0.f;
+    if (valid) {
+        // batches of rows g = t + 512 c, t + 512 c + 256 of W_l2 / pl2, then row t of W_in / pa0
+        const int nb = (H + 511) / 512;
+        for (int c = 0; c <= nb; ++c) {
+            constexpr int NU = 2;
+            float wv[NU][OBR], pv[NU][NQ];
 #pragma unroll
-        for (int q = 0; q < NQP; ++q) x[r * NQP + q] = q < NQ ? acc[r][q] : 0.f;
+            for (int u = 0; u < NU; ++u) {
+                const bool l2 = c < nb;
+                const int g = l2 ? t + 512 * c + 256 * u : t;
+                const bool ok = l2 ? g < H : (u == 0 && g < a.IN);
+                const float* W = (l2 ? a.prm + a.F.l2_w : a.prm + a.F.in_w) + (size_t)(ok ? g : 0) * H + f0;
+                const float* P = (l2 ? a.pl2 : a.pa0) + (size_t)(ok ? g : 0) * NE;
+                if constexpr (OBR == 4) {
+                    const f32x4 w4 = *(const f32x4*)W;
+#pragma unroll
+                    for (int r = 0; r < OBR; ++r) wv[u][r] = ok ? round_prec<PREC>(w4[r]) : 0.f;
+                } else {
+                    const f32x2_t w2 = *(const f32x2_t*)W;
+#pragma unroll
+                    for (int r = 0; r < OBR; ++r) wv[u][r] = ok ? round_prec<PREC>(w2[r]) : 0.f;
+                }
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) pv[u][q] = (ok && q < NE) ? P[q] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < NU; ++u)
+#pragma unroll
+                for (int r = 0; r < OBR; ++r)
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) x[r * NQP + q] = fmaf(wv[u][r], pv[u][q], x[r * NQP + q]);
+        }
+    }
+    // recursive halving over the 64 lanes: each xor step a lane keeps half of its vector and adds the
+    // partner's copy of that half, so 6 steps leave lane l with the sum of value l (63 lane swaps,
+    // against 11 dependent DPP / readlane ops per value for a whole-wave sum each)
 #pragma unroll
     for (int st = 0; st < 6; ++st) {
         const int m = 32 >> st, half = V >> (st + 1);
@@ -475,39 +484,31 @@ __device__ inline void out_back_n(const OutBack& a, int b, bool valid, int t, fl
             x[i] = keep + __shfl_xor(send, m, 64);
         }
     }
-    // lane l holds values PER l .. PER l + PER - 1 (the kept halves' offsets sum to PER l)
-#pragma unroll
-    for (int i = 0; i < PER; ++i) red[w * V + PER * lane + i] = x[i];
+    red[w * V + lane] = x[0];   // lane l: value l (the kept halves' offsets sum to l)
     __syncthreads();
-    if (valid && t < OB_ROWS * N) {
-        const int r = t / N, q = t % N, f = f0 + r, v = r * NQP + q;
+    if (valid && t < OBR * NE) {
+        const int r = t / NE, q = t % NE, f = f0 + r, v = r * NQP + q;
         if (f < H) {
             const float s = (red[v] + red[V + v]) + (red[2 * V + v] + red[3 * V + v]);
             const float bb = a.prm[a.F.l2_b + f] + a.prm[a.F.in_b + f];
-            a.gw[(size_t)f * N + q] = fmaf(bb, a.gob[q], s);
+            a.gw[(size_t)f * NE + q] = fmaf(bb, a.gob[q], s);
         }
     }
 }
-// every thread of the workgroup calls this (it holds a barrier); valid = the group has rows to form.
-// red: 4 x OB_ROWS x L2B_MAXN floats of LDS for this 256-thread group
-template <int PREC>
-__device__ __forceinline__ void out_back_group(const OutBack& a, int b, bool valid, int t, float* red) {
-    switch (a.N) {
-        case 12: out_back_n<PREC, 12>(a, b, valid, t, red); break;
-        case 24: out_back_n<PREC, 24>(a, b, valid, t, red); break;
-        default: out_back_n<PREC, L2B_MAXN>(a, b, valid, t, red); break;   // any N <= 32
-    }
-}
+// out_back_n: every thread of the workgroup calls it (it holds a barrier); valid = the group has rows to
+// form; red: OB_RED floats of LDS for this 256-thread group
 
-constexpr int OB_RED = 4 * OB_ROWS * L2B_MAXN;   // floats of LDS per 256-thread group
+constexpr int OB_RED = 4 * 64;   // floats of LDS per 256-thread group (4 waves x 64 values)
 
 // block b: l2_back's row group b (b < l2_blocks), then the actor's out_back group b (b < ob_groups)
-template <int PREC>
+template <int PREC, int NQ>
 __global__ __launch_bounds__(256) void l2_back_kernel(L2Back a, int l2_blocks, OutBack ob, int ob_groups) {
-    if ((int)blockIdx.x < l2_blocks) l2_back_rows_p<PREC>(a, (int)blockIdx.x, (int)threadIdx.x);
-    if (ob_groups > 0) {
-        __shared__ float red[OB_RED];
-        out_back_group<PREC>(ob, (int)blockIdx.x, (int)blockIdx.x < ob_groups, (int)threadIdx.x, red);
+    if ((int)blockIdx.x < l2_blocks) l2_back_n<PREC, NQ>(a, (int)blockIdx.x, (int)threadIdx.x);
+    if constexpr (NQ > 1) {   // (the critic's N = 1 has no out_back)
+        if (ob_groups > 0) {
+            __shared__ float red[OB_RED];
+            out_back_n<PREC, NQ>(ob, (int)blockIdx.x, (int)blockIdx.x < ob_groups, (int)threadIdx.x, red);
+        }
     }
     if (a.zcnt) {   // the critic's row tiles and dW (earlier on this stream) were the counts' last readers
         const int nz = *a.zn;
@@ -642,7 +643,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
 // independent of each other): workgroup 0 runs the time-MLP backward, the others TB_THREADS / 256 groups
 // each, group g l2_back's row group g and then out_back's group g (as many workgroups as the larger
 // count needs: extra workgroups waited for CUs beside the other stream's kernels)
-template <int PREC>
+template <int PREC, int NQ>
 __global__ __launch_bounds__(TB_THREADS) void time_l2_bwd_kernel(const float* __restrict__ gseg,
                                                           const float* __restrict__ prm, float* __restrict__ grad,
                                                           FlatOffsets F, int XD, int TD, int H, int KF, int TS,
@@ -655,26 +656,46 @@ __global__ __launch_bounds__(TB_THREADS) void time_l2_bwd_kernel(const float* __
     }
     constexpr int per = TB_THREADS / 256;
     const int grp = ((int)blockIdx.x - 1) * per + (int)threadIdx.x / 256;
-    if (grp < l2_groups) l2_back_rows_p<PREC>(l2b, grp, (int)threadIdx.x % 256);
-    if (ob_groups > 0) out_back_group<PREC>(ob, grp, grp < ob_groups, (int)threadIdx.x % 256, sm + ((int)threadIdx.x / 256) * OB_RED);
+    if (grp < l2_groups) l2_back_n<PREC, NQ>(l2b, grp, (int)threadIdx.x % 256);
+    if (ob_groups > 0) out_back_n<PREC, NQ>(ob, grp, grp < ob_groups, (int)threadIdx.x % 256, sm + ((int)threadIdx.x / 256) * OB_RED);
 }
 
-// the precision instantiation of the l2_back / time_l2_bwd kernels
-static void launch_l2_back(int prec, unsigned blocks, hipStream_t s, const L2Back& l2b, int l2g, const OutBack& ob, int obg) {
-    if (prec == DPPO_BF16) hipLaunchKernelGGL(l2_back_kernel<DPPO_BF16>, dim3(blocks), dim3(256), 0, s, l2b, l2g, ob, obg);
-    else if (prec == DPPO_F16) hipLaunchKernelGGL(l2_back_kernel<DPPO_F16>, dim3(blocks), dim3(256), 0, s, l2b, l2g, ob, obg);
-    else hipLaunchKernelGGL(l2_back_kernel<DPPO_F32>, dim3(blocks), dim3(256), 0, s, l2b, l2g, ob, obg);
+// the (precision, width) instantiations of the l2_back / time_l2_bwd kernels
+template <int PREC>
+static void launch_l2_back_p(int nq, unsigned blocks, hipStream_t s, const L2Back& l2b, int l2g, const OutBack& ob, int obg) {
+    switch (nq) {
+        case 1: hipLaunchKernelGGL((l2_back_kernel<PREC, 1>), dim3(blocks), dim3(256), 0, s, l2b, l2g, ob, obg); break;
+        case 12: hipLaunchKernelGGL((l2_back_kernel<PREC, 12>), dim3(blocks), dim3(256), 0, s, l2b, l2g, ob, obg); break;
+        case 24: hipLaunchKernelGGL((l2_back_kernel<PREC, 24>), dim3(blocks), dim3(256), 0, s, l2b, l2g, ob, obg); break;
+        default: hipLaunchKernelGGL((l2_back_kernel<PREC, L2B_MAXN>), dim3(blocks), dim3(256), 0, s, l2b, l2g, ob, obg); break;
+    }
 }
-static const void* time_l2_bwd_fn(int prec) {
-    return prec == DPPO_BF16 ? (const void*)time_l2_bwd_kernel<DPPO_BF16>
-         : prec == DPPO_F16 ? (const void*)time_l2_bwd_kernel<DPPO_F16> : (const void*)time_l2_bwd_kernel<DPPO_F32>;
+static void launch_l2_back(int prec, unsigned blocks, hipStream_t s, const L2Back& l2b, int l2g, const OutBack& ob, int obg) {
+    const int nq = l2_nq(l2b.N);
+    if (prec == DPPO_BF16) launch_l2_back_p<DPPO_BF16>(nq, blocks, s, l2b, l2g, ob, obg);
+    else if (prec == DPPO_F16) launch_l2_back_p<DPPO_F16>(nq, blocks, s, l2b, l2g, ob, obg);
+    else launch_l2_back_p<DPPO_F32>(nq, blocks, s, l2b, l2g, ob, obg);
+}
+template <int PREC>
+static const void* time_l2_bwd_fn_p(int nq) {
+    return nq == 12 ? (const void*)time_l2_bwd_kernel<PREC, 12> : nq == 24 ? (const void*)time_l2_bwd_kernel<PREC, 24>
+         : (const void*)time_l2_bwd_kernel<PREC, L2B_MAXN>;
+}
+static const void* time_l2_bwd_fn(int prec, int nq) {
+    return prec == DPPO_BF16 ? time_l2_bwd_fn_p<DPPO_BF16>(nq) : prec == DPPO_F16 ? time_l2_bwd_fn_p<DPPO_F16>(nq)
+                                                                                : time_l2_bwd_fn_p<DPPO_F32>(nq);
 }
 
 // dynamic LDS of time_bwd_body over nb buckets; *stage_g = whether the bucket sums are staged too
 static size_t time_bwd_lds(const Dims& D, int nb, int* stage_g) {
     size_t tsm = sizeof(float) * ((size_t)D.TD * D.H + 4 * (size_t)D.TD * D.TD + 2 * D.TD +
                                   (size_t)nb * (2 * D.TD + 3 * 2 * D.TD));
-    *stage_g = tsm + sizeof(float) * (size_t)nb * D.H <= 160 * 1024;
+    // the bucket sums are staged only when the workgroup stays small enough to share a CU with the
+    // critic's dW (its 101 KiB ring): waiting for a CU cost more than the extra global round trip
+    // (DPPO_TB_STAGE_G=1: stage whenever it fits, the r04 form; A/B knob)
+    static const bool always = [] { const char* e = getenv("DPPO_TB_STAGE_G"); return e && atoi(e) != 0; }();
+    const size_t cap = always ? 160 * 1024 : 56 * 1024;
+    *stage_g = tsm + sizeof(float) * (size_t)nb * D.H <= cap;
     if (*stage_g) tsm += sizeof(float) * (size_t)nb * D.H;
     return tsm;
 }
@@ -1707,14 +1728,17 @@ extern "C" size_t dppo_ppo_workspace_bytes(const dppo_dims* d, int precision, in
     return make_ppo_workspace(D, precision, batch_rows, nullptr).total;
 }
 
+// wk = 256 / 128, or 0: WK = 128 with the 3-slot ring (the critic's dW beside the actor's tail)
 template <class P>
 static int launch_dw(const DWArgs& a, int wk, hipStream_t s) {
     const int tiles = a.tile_start[a.nprob];
     const int64_t blocks = 8 * (((int64_t)tiles * a.nchunks + 7) / 8);   // whole XCD rounds
     if (wk == 256)
-        hipLaunchKernelGGL((dw_kernel<P, 256>), dim3((unsigned)blocks), dim3(DWGeom<256>::W * 64), 0, s, a);
+        hipLaunchKernelGGL((dw_kernel<P, 256, 8>), dim3((unsigned)blocks), dim3(DWGeom<256>::W * 64), 0, s, a);
+    else if (wk == 128)
+        hipLaunchKernelGGL((dw_kernel<P, 128, 8>), dim3((unsigned)blocks), dim3(DWGeom<128>::W * 64), 0, s, a);
     else
-        hipLaunchKernelGGL((dw_kernel<P, 128>), dim3((unsigned)blocks), dim3(DWGeom<128>::W * 64), 0, s, a);
+        hipLaunchKernelGGL((dw_kernel<P, 128, 3>), dim3((unsigned)blocks), dim3(128 / 32 * 64), 0, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -1765,7 +1789,7 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
     L2Back l2b = {pl2, ga + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b, D.H,
                   D.XD, precision, nullptr, nullptr, nullptr};
     DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
-    DPPO_CHECK(D.H <= 768 && D.IN <= 256 && D.H % OB_ROWS == 0, "out_back: hidden %d > 768 or in_dim %d > 256", D.H, D.IN);
+    DPPO_CHECK(D.IN <= 256 && D.H % 4 == 0, "out_back: in_dim %d > 256", D.IN);
     // (time_bwd forked onto a side stream beside l2_back measured slower: 0.428 vs 0.406 ms per
     // minibatch, same box, tools/r03_ab2.sh; since r04 the two share one launch instead)
     int stage_g = 0;
@@ -1773,20 +1797,19 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
     const size_t tsm = tsm0 > sizeof(float) * OB_RED * (TB_THREADS / 256) ? tsm0 : sizeof(float) * OB_RED * (TB_THREADS / 256);
     DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
     const int per = TB_THREADS / 256;
-    const int l2g = l2_back ? dppo_cdiv(D.H, L2B_ROWS) : 0, obg = dppo_cdiv(D.H, OB_ROWS);
-    { const int rc_ = dppo_func_lds(time_l2_bwd_fn(precision), tsm); if (rc_) return rc_; }
+    const int l2g = l2_back ? dppo_cdiv(D.H, L2B_ROWS) : 0, obg = dppo_cdiv(D.H, ob_rows(D.XD));
+    const int nq = l2_nq(D.XD);
+    const void* fn = time_l2_bwd_fn(precision, nq);
+    { const int rc_ = dppo_func_lds(fn, tsm); if (rc_) return rc_; }
     DppoKtScope kt(KT_TIME_BWD, s);
     const OutBack ob = make_out_back(D, precision, actor_params, pl2, pa0, ga);
     const dim3 grid(1 + dppo_cdiv(l2g > obg ? l2g : obg, per));
-    if (precision == DPPO_BF16)
-        hipLaunchKernelGGL(time_l2_bwd_kernel<DPPO_BF16>, grid, dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD,
-                           D.TD, D.H, nb, TS, stage_g, l2b, l2g, ob, obg);
-    else if (precision == DPPO_F16)
-        hipLaunchKernelGGL(time_l2_bwd_kernel<DPPO_F16>, grid, dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD,
-                           D.TD, D.H, nb, TS, stage_g, l2b, l2g, ob, obg);
-    else
-        hipLaunchKernelGGL(time_l2_bwd_kernel<DPPO_F32>, grid, dim3(TB_THREADS), tsm, s, gseg, actor_params, ga, FA, D.XD,
-                           D.TD, D.H, nb, TS, stage_g, l2b, l2g, ob, obg);
+    int XD = D.XD, TD = D.TD, H = D.H;
+    FlatOffsets fa = FA;
+    const float* prm = actor_params;
+    void* args[] = {(void*)&gseg, (void*)&prm, (void*)&ga, (void*)&fa, (void*)&XD, (void*)&TD, (void*)&H, (void*)&nb,
+                    (void*)&TS, (void*)&stage_g, (void*)&l2b, (void*)&l2g, (void*)&ob, (void*)&obg};
+    DPPO_HIP(hipLaunchKernel(fn, grid, dim3(TB_THREADS), args, tsm, s));
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -1938,10 +1961,14 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         DWArgs w = {};
         if (!actor) w.rows_dev = crit_rows_dev;
         const size_t span = ws.ldm;
+        // the critic's dW runs beside the actor's dW tail: its smaller ring (WK = 128, 3 slots) leaves the
+        // CU room for the time-MLP backward's workgroup (DPPO_CDW_RING=0: the actor's geometry, A/B knob)
+        static const bool cring = [] { const char* e = getenv("DPPO_CDW_RING"); return !e || atoi(e) != 0; }();
+        const int wk = (!actor && cring) ? 0 : tk, tke = wk ? wk : 128;
         auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
             DWProb& p = w.p[w.nprob];
             p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
-            p.ktiles = dppo_cdiv(Kx, tk); p.ntiles = dppo_cdiv(N, DW_TN);
+            p.ktiles = dppo_cdiv(Kx, tke); p.ntiles = dppo_cdiv(N, DW_TN);
             w.tile_start[w.nprob + 1] = w.tile_start[w.nprob] + p.ktiles * p.ntiles;
             w.nprob++;
         };
@@ -1971,8 +1998,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         w.mchunk = (int)(dppo_cdiv((int)span, nch * 64) * 64);
         w.nchunks = dppo_cdiv((int)span, w.mchunk);
         DppoKtScope kt(actor ? KT_DW_ACTOR : KT_DW_CRITIC, st);
-        return precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, tk, st)
-             : precision == DPPO_F16  ? launch_dw<PolicyF16>(w, tk, st) : launch_dw<PolicyF32>(w, tk, st);
+        return precision == DPPO_BF16 ? launch_dw<PolicyBF16>(w, wk, st)
+             : precision == DPPO_F16  ? launch_dw<PolicyF16>(w, wk, st) : launch_dw<PolicyF32>(w, wk, st);
     };
 
     // the critic's distinct samples (sample-weighted value loss, crit_rows_kernel), on the stream
@@ -2009,7 +2036,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         L2Back l2b = {ws.pl2, ga + FA.out_b, (const uint8_t*)packed_ft + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b,
                       D.H, D.XD, precision, nullptr, nullptr, nullptr};
         DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
-        const int l2g = l2_def ? 0 : dppo_cdiv(D.H, L2B_ROWS), obg = dppo_cdiv(D.H, OB_ROWS);
+        const int l2g = l2_def ? 0 : dppo_cdiv(D.H, L2B_ROWS), obg = dppo_cdiv(D.H, ob_rows(D.XD));
         DppoKtScope kt(KT_L2_BACK, s);
         launch_l2_back(precision, (unsigned)(l2g > obg ? l2g : obg), s, l2b, l2g,
                        make_out_back(D, precision, actor_params, pl2_src, ws.pa0, ga), obg);

@@ -181,16 +181,17 @@ def test_iterations_match_oracle(cuda, seed, tmp_path):
     assert [e["eval"] for e in errs] == [True, False, False]
 
 
-@pytest.mark.parametrize("l2_defer", ["1", "0"])
-def test_iterations_match_oracle_one_launch_actor_step(cuda, tmp_path, monkeypatch, l2_defer):
-    """The opt-in one-launch actor step (DPPO_FUSED_STEP=all: dppo_actor_step with the time-MLP
-    backward in its workgroup 0, the virtual or the materialised l2 gradient) over the same three
-    iterations, against the oracle at the default path's tolerances."""
-    monkeypatch.setenv("DPPO_FUSED_STEP", "all")
+@pytest.mark.parametrize("fused,l2_defer", [("all", "1"), ("all", "0"), ("critic", "1")])
+def test_iterations_match_oracle_one_launch_actor_step(cuda, tmp_path, monkeypatch, fused, l2_defer):
+    """The opt-in step forms over the same three iterations, against the oracle at the default path's
+    tolerances: the one-launch actor step (DPPO_FUSED_STEP=all: dppo_actor_step with the time-MLP
+    backward in its workgroup 0) with the virtual or the materialised l2 gradient, and the default
+    coalesced actor step with the virtual l2 gradient (DPPO_L2_DEFER=1; materialised is the default)."""
+    monkeypatch.setenv("DPPO_FUSED_STEP", fused)
     monkeypatch.setenv("DPPO_L2_DEFER", l2_defer)
     a, orc = _agent_and_oracle(42, tmp_path)
     errs = _run_and_compare(a, orc)
-    _record(f"one_launch_actor_step_l2defer{l2_defer}", errs)
+    _record(f"step_{fused}_l2defer{l2_defer}", errs)
     assert [e["eval"] for e in errs] == [True, False, False]
 
 
