@@ -40,7 +40,7 @@ int dppo_fuse_jobs(int in_dim, int hidden, int out_dim, int time_dim, int precis
                    FuseJob* jobs);
 // the row tiles' fold segments (RT_*) of an actor image, alone: after a fused actor step (pack.hip)
 int dppo_pack_rt_fold(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* actor_params,
-                      void* packed_actor, int temb_steps, hipStream_t s);
+                      void* packed_actor, int temb_steps, int time_stride, hipStream_t s);
 // temb: the TEMB table is stale too (the fused actor step), not only the split-sampler tables
 int dppo_mark_tables_stale(const Dims& D, int precision, const float* actor_params, const void* packed_actor, bool temb);
 

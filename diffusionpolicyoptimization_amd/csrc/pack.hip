@@ -216,8 +216,9 @@ struct RtFoldArgs {
     uint8_t* img;
     const float* params;
     FlatOffsets F;
-    size_t off_wout, off_tl2, off_fold, off_fold0, off_tfold, off_bout;
+    size_t off_wout, off_tl2, off_fold, off_fold0, off_tfold, off_bout, off_temb;
     int H, XD, IN, nt_out, ks_h, ks_in, ks_out_t, nm, nm0;
+    int TD, TS, R;        // the TEMB table's rows (row r = t_emb(r TS), r < R)
 };
 // one M (M0) tile: NO out tiles, the k-steps in batches of KB whose loads are all issued before the
 // batch's MFMAs, with no branch inside a batch (a conditional load made hipcc wait vmcnt(0) per k-step:
@@ -324,6 +325,17 @@ __global__ __launch_bounds__(64) void rt_fold_kernel(RtFoldArgs a) {
     const int lane = threadIdx.x, b = (int)blockIdx.x;
     const int XD = a.XD, H = a.H;
     const float* prm = a.params;
+    if (b > a.nm + a.nm0) {   // TEMB row r (the row tiles read their time embeddings from the table)
+        const int r = b - a.nm - a.nm0 - 1, TD = a.TD;
+        float* te = &sm[0][0];          // [TD]
+        float* a1 = te + 64;            // [2 TD]
+        if (lane < TD) te[lane] = temb_sinusoid(lane, r * a.TS, TD);
+        __syncthreads();
+        if (lane < 2 * TD) a1[lane] = temb_hidden(prm, a.F.time_w1, a.F.time_b1, te, TD, lane);
+        __syncthreads();
+        if (lane < TD) ((float*)(a.img + a.off_temb))[(size_t)r * TD + lane] = temb_output(prm, a.F.time_w2, a.F.time_b2, a1, TD, lane);
+        return;
+    }
     const __amdgpu_buffer_rsrc_t rs = packed_rsrc(a.img);
     if (b == a.nm + a.nm0) {   // RT_BOUT
         if (a.nt_out > 1) rt_fold_bias<P, 2>(a, rs, lane);
@@ -617,13 +629,13 @@ int dppo_pack_mlp(int in_dim, int hidden, int out_dim, int time_dim, int precisi
     if (temb_steps > 0) clear_stale(packed);
     rc = launch_pack(a, precision, s);
     if (rc) return rc;
-    return dppo_pack_rt_fold(in_dim, hidden, out_dim, time_dim, precision, params, packed, temb_steps, s);
+    return dppo_pack_rt_fold(in_dim, hidden, out_dim, time_dim, precision, params, packed, temb_steps, time_stride, s);
 }
 
 // the row tiles' fold segments of an actor image whose W_OUT / T_L2 slots are final on stream s (after
 // its pack launch or a fused optimizer step): rt_fold_kernel, one wave per tile
 int dppo_pack_rt_fold(int in_dim, int hidden, int out_dim, int time_dim, int precision, const float* actor_params,
-                      void* packed_actor, int temb_steps, hipStream_t s) {
+                      void* packed_actor, int temb_steps, int time_stride, hipStream_t s) {
     const MlpLayout L = make_mlp_layout(in_dim, hidden, out_dim, time_dim, precision, temb_steps);
     if (time_dim <= 0) return DPPO_OK;
     if (out_dim > 32 || (dppo_prec_2b(precision) && out_dim > rt_tfold_lok(L.ks_out_t, L.KG)))
@@ -640,10 +652,14 @@ int dppo_pack_rt_fold(int in_dim, int hidden, int out_dim, int time_dim, int pre
     a.ks_out_t = L.ks_out_t;
     a.nm = L.nt_h;
     a.nm0 = L.ks_in * L.KG / 16;   // RT_FOLD0's padded k range, 16 rows per tile
+    // and the TEMB table (one block per row): the row tiles read their time embeddings from it
+    a.off_temb = L.off[SEG_TEMB]; a.TD = time_dim; a.TS = time_stride; a.R = L.temb_steps;
+    if (time_dim > 32) return dppo_set_error(DPPO_EUNSUPPORTED, "row-tile fold: time_dim %d > 32", time_dim);
+    const dim3 grid(a.nm + a.nm0 + 1 + a.R);
     DppoKtScope kt(KT_PACK_ALL, s);
-    if (precision == DPPO_BF16) hipLaunchKernelGGL(rt_fold_kernel<PolicyBF16>, dim3(a.nm + a.nm0 + 1), dim3(64), 0, s, a);
-    else if (precision == DPPO_F16) hipLaunchKernelGGL(rt_fold_kernel<PolicyF16>, dim3(a.nm + a.nm0 + 1), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(rt_fold_kernel<PolicyF32>, dim3(a.nm + a.nm0 + 1), dim3(64), 0, s, a);
+    if (precision == DPPO_BF16) hipLaunchKernelGGL(rt_fold_kernel<PolicyBF16>, grid, dim3(64), 0, s, a);
+    else if (precision == DPPO_F16) hipLaunchKernelGGL(rt_fold_kernel<PolicyF16>, grid, dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(rt_fold_kernel<PolicyF32>, grid, dim3(64), 0, s, a);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
 }
@@ -693,5 +709,5 @@ int dppo_pack_models(const Dims& D, int precision, const float* actor_params, vo
     }
     rc = launch_pack(a, precision, s);
     if (rc || !(actor_params && packed_actor)) return rc;
-    return dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, s);
+    return dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS, s);
 }

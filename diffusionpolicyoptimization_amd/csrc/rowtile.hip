@@ -171,19 +171,13 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         pre_m = (float)mean;
         pre_s = (float)(sqrt(var) + 1e-8);
     }
-    // time embeddings t_emb(r TS), r < K' (mlp_diffusion.py:40-45), derived here from the image's fp32
-    // time MLP (SEG_TIME) with the pack's own fmaf chains (dppo_common.cuh temb_*), so no optimizer
-    // step has to rewrite a TEMB table before this launch: sinusoid now, hidden layer in the next
-    // phase, output layer after it. Scratch in tA (first written by L1).
-    float* te_s = (float*)tA;                 // [KF][TD]
-    float* a1_s = te_s + KF * TD;             // [KF][2TD]
-    const float* tp = (const float*)(a.packed + L.off[SEG_TIME]);
-    const FlatOffsets TF = make_flat_offsets(0, 0, 0, TD);
-    for (int i = tid; i < KF * TD; i += THREADS) te_s[i] = temb_sinusoid(i % TD, (i / TD) * a.TS, TD);
     lds_sync();
+    // time embeddings t_emb(r TS), r < K' (mlp_diffusion.py:40-45): rows of the image's TEMB table,
+    // which the fold launch after every write of the image re-derives (pack.hip rt_fold_kernel; r05's
+    // in-tile derivation, three dependent phases of global reads, took 11k of a tile's cycles)
+    const float* temb_img = (const float*)(a.packed + L.off[SEG_TEMB]);
+    for (int i = tid; i < KF * TD; i += THREADS) temb[i] = temb_img[i];
     for (int i = tid; i < KF * DPPO_SCHED_COLS; i += THREADS) sch[i] = a.sched[i];
-    for (int i = tid; i < KF * 2 * TD; i += THREADS)
-        a1_s[i] = temb_hidden(tp, TF.time_w1, TF.time_b1, te_s + (i / (2 * TD)) * TD, TD, i % (2 * TD));
     for (int i = tid; i < 3 * H + 16 * NO; i += THREADS) {
         // the out-Dense bias with b_in and b_l2 folded through it (RT_BOUT: the forward runs no l2 GEMM)
         const int seg = i < H ? SEG_B_IN : (i < 2 * H ? SEG_B_L1 : (i < 3 * H ? SEG_B_L2 : SEG_RT_BOUT));
@@ -209,9 +203,6 @@ __device__ __forceinline__ void actor_rowtile_body(const ActorArgs& a) {
         const int r = i / SD, c = i % SD, n = rn[r];
         st[i] = n >= 0 ? a.obs[(size_t)n * SD + c] : 0.f;
     }
-    lds_sync();
-    for (int i = tid; i < KF * TD; i += THREADS)
-        temb[i] = temb_output(tp, TF.time_w2, TF.time_b2, a1_s + (i / TD) * 2 * TD, TD, i % TD);
     lds_sync();
     // a0 = [x_prev, temb(t), state] (mlp_diffusion.py:86), t = K'-1-j (diffusion_vpg.py:456-458)
     for (int i = tid; i < ROWS * k1w; i += THREADS) {

@@ -1455,7 +1455,7 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
                                        params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
             }
             DPPO_HIP(hipGetLastError());
-            rc = dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, s);   // cross-element: not per element
+            rc = dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS, s);   // cross-element: not per element
             if (rc) return rc;
             return dppo_mark_tables_stale(D, precision, actor_params, packed_actor, true);
         }
@@ -1512,7 +1512,7 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
         }
         DPPO_HIP(hipGetLastError());
         // the row tiles' fold needs every element final: its own small launch (pack.hip PACK_RT_FOLD)
-        rc = dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, s);
+        rc = dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS, s);
         if (rc) return rc;
         // TEMB (every precision) and the split sampler's tables (2-byte) wait for the next sampler launch
         return dppo_mark_tables_stale(D, precision, actor_params, packed_actor, true);
