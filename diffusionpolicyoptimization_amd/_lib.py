@@ -122,7 +122,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 class DppoError(RuntimeError):

@@ -33,7 +33,9 @@
 extern "C" {
 #endif
 
-#define DPPO_ABI_VERSION 12
+/* ABI 13: the actor image (dppo_actor_packed_bytes) holds the row tiles' l2 fold segments; a pack or
+ * fused step of an actor image is followed by the fold launch (DPPO_STEP_FUSED_PACK above) */
+#define DPPO_ABI_VERSION 13
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -57,11 +59,12 @@ enum { DPPO_STEP_L2_FROM_PL2 = 0x200 };
 /* ABI 11, OR'd into dppo_optimizer_step's mode. DPPO_STEP_FUSED_PACK: AdamW and the pack in ONE
  * launch when the step packs a single network whose flat parameters are exactly the range: each
  * element's thread stores its updated value into its slots of the images (the values the pack writes).
- * For an actor (since ABI 12) the launch leaves the TEMB table and the split sampler's tables to their
- * consumers: the PPO / log-prob row tiles derive the time embeddings from the image's fp32 time MLP,
- * and the next sampler launch (or dppo_refresh_sampler_tables) re-derives TEMB and the tables, as
- * after DPPO_STEP_DEFER_SAMPLER_TABLES. The image must have been fully packed once before (its zero
- * padding is not rewritten). Any other combination runs the two launches.
+ * For an actor the launch leaves the split sampler's tables to the next sampler launch (or
+ * dppo_refresh_sampler_tables), as after DPPO_STEP_DEFER_SAMPLER_TABLES; a second, small launch on the
+ * same stream re-derives the cross-element segments the row tiles read (the l2 fold M = W_l2 W_out,
+ * M0 = W_in W_out, the folded out bias and the TEMB table), as it does after every pack of an actor
+ * image. The image must have been fully packed once before (its zero padding is not rewritten). Any
+ * other combination runs the two launches.
  * DPPO_STEP_CLEAR_GRADS (dppo_optimizer_step_ex only): the step zeroes the range's gradients after
  * reading them, and the byte ranges given to dppo_optimizer_step_ex after every read of the launch
  * (by its last workgroup), so the next minibatch of this range may skip its zeroing launch
