@@ -40,6 +40,10 @@
 
 #define DPPO_ENV_API __attribute__((visibility("default")))
 
+/* default solo floor (dppo_lowdim_set_solo_floor): a pool hand-off measured 11-15 us per chunk on
+ * the GPU box's host (profiles/r04r_bench_lowdim_t{1,4}_c0.json) */
+#define DPPO_SOLO_FLOOR_US 25.0
+
 /* the simulator callback table (dppo_sim_step_fn / dppo_sim_reset_fn) and every entry point are
  * declared in include/dppo_env.h */
 
@@ -105,6 +109,13 @@ typedef struct LowdimEnv {
     int nscr;
     Pool* pool;          /* NULL: one thread */
     Chunk chunk;         /* the chunk in flight */
+    /* the solo floor (dppo_lowdim_set_solo_floor): a pool steps a chunk on the caller's thread alone
+     * while the chunk's estimated stepping work is below the hand-off it would save */
+    double solo_floor_s; /* 0: always use the pool */
+    double work_est_s;   /* running estimate of one chunk's stepping work, all envs (< 0: none yet) */
+    double work0_s;      /* this chunk's stepping work on the caller's thread (waits excluded) */
+    int solo;            /* the current mode (hysteresis: enter below the floor, leave above twice it) */
+    int64_t solo_chunks;
 } LowdimEnv;
 
 DPPO_ENV_API int dppo_lowdim_abi(void) { return 2; }
@@ -208,6 +219,8 @@ DPPO_ENV_API void* dppo_lowdim_create(int E, int Do, int Da, int To, int act_ste
     e->E = E; e->Do = Do; e->Da = Da; e->To = To; e->act_steps = act_steps;
     e->max_episode_steps = max_episode_steps; e->reset_within_step = reset_within_step;
     e->step = step; e->reset = reset; e->ctx = ctx;
+    e->solo_floor_s = DPPO_SOLO_FLOOR_US * 1e-6;
+    e->work_est_s = -1.0;
     if (obs_min) {
         e->obs_min = (float*)xcalloc(Do, 4); e->obs_max = (float*)xcalloc(Do, 4); e->obs_rng = (float*)xcalloc(Do, 4);
         memcpy(e->obs_min, obs_min, 4 * (size_t)Do); memcpy(e->obs_max, obs_max, 4 * (size_t)Do);
@@ -355,6 +368,22 @@ DPPO_ENV_API int dppo_lowdim_set_threads(void* h, int n, double spin_us) {
     return n;
 }
 
+/* The solo floor: with a pool, a chunk whose estimated stepping work (a running average of the
+ * measured simulator + wrapper time, waits for actions excluded, scaled to all envs) is below
+ * floor_us runs on the caller's thread alone; the pool is used again once the estimate exceeds twice
+ * the floor. 0 disables (always the pool). Results do not depend on it. */
+DPPO_ENV_API int dppo_lowdim_set_solo_floor(void* h, double floor_us) {
+    LowdimEnv* e = (LowdimEnv*)h;
+    if (!e || floor_us < 0.0) return -1;
+    e->solo_floor_s = floor_us * 1e-6;
+    e->work_est_s = -1.0;
+    e->solo = 0;
+    return 0;
+}
+
+/* chunks stepped on the caller's thread alone under the solo floor */
+DPPO_ENV_API int64_t dppo_lowdim_solo_chunks(void* h) { return ((LowdimEnv*)h)->solo_chunks; }
+
 DPPO_ENV_API int dppo_lowdim_threads(void* h) {
     LowdimEnv* e = (LowdimEnv*)h;
     return e->pool ? e->pool->n : 1;
@@ -362,9 +391,24 @@ DPPO_ENV_API int dppo_lowdim_threads(void* h) {
 
 /* run e->chunk on every slice; the caller's thread takes slice 0. Returns the sum of the slices'
  * results, or the most negative one. */
+static void note_work(LowdimEnv* e, double chunk_work_s) {
+    e->work_est_s = e->work_est_s < 0.0 ? chunk_work_s : e->work_est_s + 0.5 * (chunk_work_s - e->work_est_s);
+    if (e->solo) e->solo = e->work_est_s <= 2.0 * e->solo_floor_s;
+    else e->solo = e->work_est_s < e->solo_floor_s;
+}
+
 static int run_chunk(LowdimEnv* e) {
     Pool* p = e->pool;
     if (!p) return run_slice(e, 0, 0, e->E);
+    e->work0_s = 0.0;
+    if (e->solo && e->solo_floor_s > 0.0) {
+        /* below the floor a pool hand-off (wake, per-slice spins, the join) costs more than the
+         * slices it would run in parallel: step every env here, in slice order (bit-identical) */
+        const int rc = run_slice(e, 0, 0, e->E);
+        e->solo_chunks++;
+        note_work(e, e->work0_s);
+        return rc;
+    }
     __atomic_store_n(&p->pending, p->n - 1, __ATOMIC_RELEASE);
     pthread_mutex_lock(&p->mu);
     __atomic_fetch_add(&p->gen, 1, __ATOMIC_ACQ_REL);
@@ -376,6 +420,8 @@ static int run_chunk(LowdimEnv* e) {
         _mm_pause();
         if ((spins & 63u) == 0) sched_yield();
     }
+    const int n0 = slice_lo(e, p->n, 1);
+    if (e->solo_floor_s > 0.0 && n0 > 0) note_work(e, e->work0_s * e->E / n0);
     int sum = 0, worst = 0;
     for (int t = 0; t < p->n; ++t) {
         if (p->rc[t] < worst) worst = p->rc[t];
@@ -418,6 +464,7 @@ static int run_block(LowdimEnv* e, int t, int lo, int hi) {
         const int w = slice_wait_actions(e, lo, hi);
         if (w) return w;
     }
+    const double w0 = t == 0 ? mono_s() : 0.0;
     const Scratch* sc = &e->scr[t];
     int32_t* idx = sc->idx;
     double* act = sc->act;
@@ -498,6 +545,7 @@ static int run_block(LowdimEnv* e, int t, int lo, int hi) {
             __atomic_store_n(c->obs_tagged + q, hi_tag | bits, __ATOMIC_RELEASE);
         }
     }
+    if (t == 0) e->work0_s += mono_s() - w0;
     return n_done;
 }
 

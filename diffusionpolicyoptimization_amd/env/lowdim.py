@@ -29,6 +29,9 @@ envs are split into contiguous slices over a pool of host threads inside the C l
 env count). A C simulator with per-env state (LinearSimulator, a MuJoCo C-API stepper with one
 mjData per env) steps its slices concurrently; a Python simulator holds the GIL in every callback,
 so it gets one thread unless it says otherwise. Outputs are bit-identical for any thread count.
+Below a per-chunk work floor (measured, 25 us by default: `solo_floor_us`, DPPO_ENV_SOLO_FLOOR_US)
+a pool steps the chunk on the caller's thread alone, where the hand-off would cost more than the
+parallel slices save (a trivial C simulator).
 
 Pipelined rollout: step(..., gate=("tagged", ...)) is the gated host step of ops.RolloutPipe over
 this stack (dppo_lowdim_step_gated_tagged): each slice thread polls its envs' action granules,
@@ -66,6 +69,9 @@ def lib():
                                                                                ctypes.c_uint32, ctypes.c_double]
         L.dppo_lowdim_set_threads.argtypes = [_P, ctypes.c_int, ctypes.c_double]
         L.dppo_lowdim_threads.argtypes = [_P]
+        L.dppo_lowdim_set_solo_floor.argtypes = [_P, ctypes.c_double]
+        L.dppo_lowdim_solo_chunks.restype = ctypes.c_int64
+        L.dppo_lowdim_solo_chunks.argtypes = [_P]
         L.dppo_lowdim_normalize_obs.argtypes = [ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P]
         L.dppo_lowdim_normalize_obs.restype = None
         L.dppo_lowdim_unnormalize_action.argtypes = [ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P]
@@ -299,6 +305,9 @@ class LowdimVecEnv:
             else:
                 num_threads = sim.suggested_threads(num_envs) if hasattr(sim, "suggested_threads") else 1
         self.set_threads(num_threads)
+        floor = os.environ.get("DPPO_ENV_SOLO_FLOOR_US")
+        if floor is not None:
+            self.set_solo_floor(float(floor))
         E, To, Do = num_envs, n_obs_steps, obs_dim
         self._reward = np.empty(E)
         self._term = np.empty(E, np.uint8)
@@ -318,6 +327,17 @@ class LowdimVecEnv:
             raise RuntimeError("dppo_lowdim_set_threads failed")
         self.num_threads = got
         return got
+
+    def set_solo_floor(self, floor_us):
+        """Chunks whose measured stepping work is below floor_us run on the caller's thread alone
+        (0: always the pool); see include/dppo_env.h."""
+        if lib().dppo_lowdim_set_solo_floor(self._h, float(floor_us)) != 0:
+            raise ValueError(f"solo floor {floor_us} us")
+
+    @property
+    def solo_chunks(self):
+        """Chunks stepped on the caller's thread alone under the solo floor."""
+        return int(lib().dppo_lowdim_solo_chunks(self._h))
 
     def _make(self, reset_within_step):
         L = lib()

@@ -60,6 +60,14 @@ void dppo_lowdim_destroy(void* h);
 int dppo_lowdim_set_threads(void* h, int n, double spin_us);
 int dppo_lowdim_threads(void* h);
 
+/* The solo floor: with n > 1 threads, a chunk whose estimated stepping work (a running average of
+ * the measured simulator + wrapper time, waits for actions excluded, scaled to all envs) is below
+ * floor_us runs on the caller's thread alone, since the pool's hand-off would cost more than it
+ * saves; the pool is used again once the estimate exceeds twice the floor. 0 disables; the default
+ * is 25 us. Outputs do not depend on it. 0 or -1. _solo_chunks: chunks stepped alone so far. */
+int dppo_lowdim_set_solo_floor(void* h, double floor_us);
+int64_t dppo_lowdim_solo_chunks(void* h);
+
 /* AsyncVectorEnv.reset_arg / reset_one_arg: obs_out [E][To][Do] float32. 0 or -1 (simulator error) */
 int dppo_lowdim_reset_all(void* h, float* obs_out);
 int dppo_lowdim_reset_one(void* h, int env, float* obs_out);

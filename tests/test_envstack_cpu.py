@@ -253,6 +253,7 @@ def _lowdim(E, threads, To=2, cost_us=0.0, max_steps=10):
 def test_thread_pool_is_bit_identical_to_one_thread(threads):
     E = 37                                  # ragged slices
     one, many = _lowdim(E, 1), _lowdim(E, threads)
+    many.set_solo_floor(0.0)                # every chunk through the pool
     assert one.num_threads == 1 and many.num_threads == min(threads, E)
     np.testing.assert_array_equal(one.reset_arg()["state"], many.reset_arg()["state"])
     rng = np.random.default_rng(7)
@@ -285,6 +286,29 @@ def test_thread_pool_survives_resize_and_idle_sleep():
     assert v.set_threads(2) == 2 and v.set_threads(1) == 1 and v.set_threads(5) == 5
     v.step(a)
     v.close()
+
+
+@pytest.mark.parametrize("cost_us,solo", [(0.0, True), (30.0, False)])
+def test_solo_floor_steps_cheap_chunks_on_the_caller(cost_us, solo):
+    """A trivial simulator's chunk (a few us of work for 16 envs) is below the default 25 us floor
+    and runs on the caller's thread alone; at 30 us per env sub-step the pool is used. Outputs match
+    a pool that never goes solo, bit for bit."""
+    E = 16
+    auto, pool = _lowdim(E, 4, cost_us=cost_us), _lowdim(E, 4, cost_us=cost_us)
+    pool.set_solo_floor(0.0)
+    np.testing.assert_array_equal(auto.reset_arg()["state"], pool.reset_arg()["state"])
+    rng = np.random.default_rng(3)
+    for _ in range(30):
+        a = rng.uniform(-1.2, 1.2, (E, 4, 3)).astype(np.float32)
+        o1, r1, t1, u1, _ = auto.step(a)
+        o2, r2, t2, u2, _ = pool.step(a)
+        np.testing.assert_array_equal(o1["state"], o2["state"])
+        np.testing.assert_array_equal(r1, r2)
+        np.testing.assert_array_equal(t1 | u1, t2 | u2)
+    assert pool.solo_chunks == 0
+    assert (auto.solo_chunks >= 20) if solo else (auto.solo_chunks == 0)
+    with pytest.raises(ValueError):
+        auto.set_solo_floor(-1.0)
 
 
 def test_python_simulator_refuses_threads():
