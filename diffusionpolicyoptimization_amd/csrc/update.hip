@@ -1751,23 +1751,25 @@ static int dw_tk() {
 
 // one non-blocking side stream (+ fork/join events) per device and host thread, created on first use;
 // null if creation fails (the caller then runs everything on its own stream)
+// (which = 0: the critic's half of a whole minibatch; 1: the actor's time-MLP backward fork)
 struct SideStream { hipStream_t stream; hipEvent_t fork, join; };
-static SideStream* side_stream() {
+static SideStream* side_stream(int which = 0) {
     constexpr int MAXDEV = 16;
-    thread_local SideStream ss[MAXDEV] = {};
-    thread_local bool tried[MAXDEV] = {};
+    thread_local SideStream ss[2][MAXDEV] = {};
+    thread_local bool tried[2][MAXDEV] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
-    if (!tried[dev]) {
-        tried[dev] = true;
-        if (hipStreamCreateWithFlags(&ss[dev].stream, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&ss[dev].fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ss[dev].join, hipEventDisableTiming) != hipSuccess) {
+    SideStream& e = ss[which][dev];
+    if (!tried[which][dev]) {
+        tried[which][dev] = true;
+        if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.join, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
-            ss[dev].stream = nullptr;
+            e.stream = nullptr;
         }
     }
-    return ss[dev].stream ? &ss[dev] : nullptr;
+    return e.stream ? &e : nullptr;
 }
 
 // the actor's l2 weight gradient from pl2 (l2_back_kernel: no LDS, so it starts on any CU with a
@@ -1783,7 +1785,7 @@ static OutBack make_out_back(const Dims& D, int precision, const float* actor_pa
 // W_out's gradient (out_back) and, unless the l2 gradient stays factored, l2's from pl2, in one launch
 static int launch_time_bwd(const Dims& D, int precision, const float* gseg, const float* pl2, const float* pa0,
                            const void* packed_actor, const float* actor_params, float* ga, int nb, int TS, hipStream_t s,
-                           bool l2_back = true) {
+                           bool l2_back = true, bool groups = true) {
     const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
     const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     L2Back l2b = {pl2, ga + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b, D.H,
@@ -1797,7 +1799,7 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
     const size_t tsm = tsm0 > sizeof(float) * OB_RED * (TB_THREADS / 256) ? tsm0 : sizeof(float) * OB_RED * (TB_THREADS / 256);
     DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
     const int per = TB_THREADS / 256;
-    const int l2g = l2_back ? dppo_cdiv(D.H, L2B_ROWS) : 0, obg = dppo_cdiv(D.H, ob_rows(D.XD));
+    const int l2g = l2_back && groups ? dppo_cdiv(D.H, L2B_ROWS) : 0, obg = groups ? dppo_cdiv(D.H, ob_rows(D.XD)) : 0;
     const int nq = l2_nq(D.XD);
     const void* fn = time_l2_bwd_fn(precision, nq);
     { const int rc_ = dppo_func_lds(fn, tsm); if (rc_) return rc_; }
@@ -1957,15 +1959,20 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     static const int env_ch = [] { const char* e = getenv("DPPO_DW_CHUNKS"); return e ? atoi(e) : 0; }();
     const int tk = dw_tk();
     const int* crit_rows_dev = nullptr;
-    auto launch_grads = [&](bool actor, hipStream_t st) -> int {
+    auto launch_grads = [&](bool actor, hipStream_t st, unsigned pmask = 0xFu) -> int {
         DWArgs w = {};
+        int all_tiles = 0;
         if (!actor) w.rows_dev = crit_rows_dev;
         const size_t span = ws.ldm;
         // the critic's dW runs beside the actor's dW tail: its smaller ring (WK = 128, 3 slots) leaves the
         // CU room for the time-MLP backward's workgroup (DPPO_CDW_RING=0: the actor's geometry, A/B knob)
         static const bool cring = [] { const char* e = getenv("DPPO_CDW_RING"); return !e || atoi(e) != 0; }();
         const int wk = (!actor && cring) ? 0 : tk, tke = wk ? wk : 128;
+        int pi = 0;
         auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
+            const bool on = (pmask >> pi++) & 1u;
+            all_tiles += dppo_cdiv(Kx, tke) * dppo_cdiv(N, DW_TN);
+            if (!on) return;
             DWProb& p = w.p[w.nprob];
             p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
             p.ktiles = dppo_cdiv(Kx, tke); p.ntiles = dppo_cdiv(N, DW_TN);
@@ -1986,7 +1993,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         w.ldm = ws.ldm;
         w.seg = ws.seg;
         w.out_scale = 1.f / gscale;
-        const int tiles = w.tile_start[w.nprob];
+        // the chunking of a subset (pmask) is the whole set's: the subsets run concurrently
+        const int tiles = all_tiles;
         // about one workgroup per CU, but no chunk under 768 rows: at small minibatches (6,250 rows,
         // an 8-GPU rank's share) thinner chunks cost more in partial-tile atomics than they gain
         // in parallelism (0.177 -> 0.154 ms per minibatch, tools/ab_small_mb2.sh)
@@ -2026,8 +2034,26 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     // after the actor's dW: the time-MLP backward (+ l2_back when l2 is materialised), unless the
     // caller's actor step (dppo_actor_step) runs the time-MLP backward itself
     const float* pl2_src = l2_def ? ga + FA.l2_w : ws.pl2;
+    // The time-MLP backward needs only the bucket sums gseg, which the in_w problem of the actor's dW
+    // forms (its one-hot extra rows): that problem and then the backward run on a forked stream beside
+    // the rest of the dW and the l2_back / out_back launch, joined before the part returns
+    // (DPPO_TB_FORK=0: one dW launch, then the time_l2_bwd launch; A/B knob)
+    static const bool tb_fork_env = [] { const char* e = getenv("DPPO_TB_FORK"); return !e || atoi(e) != 0; }();
+    SideStream* tbf = (tb_fork_env && !(hp->flags & DPPO_PPO_TIME_BWD_IN_STEP)) ? side_stream(1) : nullptr;
+    auto actor_grads = [&]() -> int {
+        if (!tbf) return launch_grads(true, s);
+        DPPO_HIP(hipEventRecord(tbf->fork, s));
+        DPPO_HIP(hipStreamWaitEvent(tbf->stream, tbf->fork, 0));
+        int rc_ = launch_grads(true, tbf->stream, 0x1u);
+        if (rc_) return rc_;
+        rc_ = launch_time_bwd(D, precision, ws.gseg, pl2_src, ws.pa0, packed_ft, actor_params, ga, D.KF, D.TS,
+                              tbf->stream, false, false);
+        if (rc_) return rc_;
+        DPPO_HIP(hipEventRecord(tbf->join, tbf->stream));
+        return launch_grads(true, s, 0xEu);
+    };
     auto actor_tail = [&]() -> int {
-        if (!(hp->flags & DPPO_PPO_TIME_BWD_IN_STEP))
+        if (!(hp->flags & DPPO_PPO_TIME_BWD_IN_STEP) && !tbf)
             return launch_time_bwd(D, precision, ws.gseg, pl2_src, ws.pa0, packed_ft, actor_params, ga, D.KF, D.TS, s,
                                    !l2_def);
         // the caller's actor step runs the time-MLP backward: W_out's gradient (and l2's unless it
@@ -2041,6 +2067,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         launch_l2_back(precision, (unsigned)(l2g > obg ? l2g : obg), s, l2b, l2g,
                        make_out_back(D, precision, actor_params, pl2_src, ws.pa0, ga), obg);
         DPPO_HIP(hipGetLastError());
+        if (tbf) DPPO_HIP(hipStreamWaitEvent(s, tbf->join, 0));
         return DPPO_OK;
     };
 
@@ -2063,7 +2090,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
             if (rc) return rc;
         }
         if (parts == 4) return DPPO_OK;
-        rc = launch_grads(true, s);
+        rc = actor_grads();
         if (rc) return rc;
         return actor_tail();
     }
@@ -2092,12 +2119,12 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (rc) return rc;
         rc = critic_tail(s);
         if (rc) return rc;
-        rc = launch_grads(true, s);
+        rc = actor_grads();
         if (rc) return rc;
     } else {
         rc = launch_actor_rowtile(aa, precision, s);
         if (rc) return rc;
-        rc = launch_grads(true, s);
+        rc = actor_grads();
         if (rc) return rc;
         DPPO_HIP(hipStreamWaitEvent(s, side->join, 0));
     }
