@@ -2,7 +2,8 @@
 # Round 5 check: GPU tests, then the bench (N = 1 and one emulated W = 8 rank) with the one-launch
 # actor step (default) and the r04 step (DPPO_FUSED_STEP=critic) alternating, each step time-limited.
 # usage: tools/r05_check.sh <tag>   TESTS=<pytest -k expr> narrows the tests; NOTESTS=1 skips them;
-# PAIRS=<n> A/B rounds (default 1); NOBENCH=1 skips the bench A/B
+# PAIRS=<n> A/B rounds (default 1); NOBENCH=1 skips the bench A/B; AB_VAR / AB_VALS: the knob and its
+# values (default DPPO_FUSED_STEP, "all critic")
 set -o pipefail
 tag=${1:-chk}
 cd $GRAFT_REPO_ROOT
@@ -22,8 +23,8 @@ for v in $VARTESTS; do
 done
 [ -n "$NOBENCH" ] && { [ -n "$VARIANTS" ] && bash tools/ab_variants.sh $VARIANTS; exit 0; }
 for r in $(seq 1 ${PAIRS:-1}); do
-  for mode in all critic; do
-    DPPO_FUSED_STEP=$mode timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/bench_${tag}_${mode}_$r.log 2>&1 \
+  for mode in ${AB_VALS:-all critic}; do
+    env ${AB_VAR:-DPPO_FUSED_STEP}=$mode timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/bench_${tag}_${mode}_$r.log 2>&1 \
       || { echo "bench failed"; tail -30 gpurun_out/bench_${tag}_${mode}_$r.log; exit 1; }
     python - gpurun_out/bench_${tag}_${mode}_$r.log $mode <<'PY'
 import json, sys
@@ -31,7 +32,7 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print(sys.argv[2], "N=1", round(d["value"]), "ms/it", round(d["ms_per_step"], 2), "mb_ms", round(d["ppo_minibatch_avg_ms"], 4),
       "roll_ms", round(1e3 * d["rollout_s_per_iter"], 2), "upd_ms", round(1e3 * d["update_s_per_iter"], 2))
 PY
-    DPPO_FUSED_STEP=$mode timeout -k 10 300 python -u bench.py --no-cpu-baseline --emulate-ranks 8 > gpurun_out/bench_${tag}_emu8_${mode}_$r.log 2>&1 \
+    env ${AB_VAR:-DPPO_FUSED_STEP}=$mode timeout -k 10 300 python -u bench.py --no-cpu-baseline --emulate-ranks 8 > gpurun_out/bench_${tag}_emu8_${mode}_$r.log 2>&1 \
       || { echo "emu bench failed"; tail -30 gpurun_out/bench_${tag}_emu8_${mode}_$r.log; exit 1; }
     python - gpurun_out/bench_${tag}_emu8_${mode}_$r.log $mode <<'PY'
 import json, sys
