@@ -2034,11 +2034,14 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     // after the actor's dW: the time-MLP backward (+ l2_back when l2 is materialised), unless the
     // caller's actor step (dppo_actor_step) runs the time-MLP backward itself
     const float* pl2_src = l2_def ? ga + FA.l2_w : ws.pl2;
-    // The time-MLP backward needs only the bucket sums gseg, which the in_w problem of the actor's dW
-    // forms (its one-hot extra rows): that problem and then the backward run on a forked stream beside
-    // the rest of the dW and the l2_back / out_back launch, joined before the part returns
-    // (DPPO_TB_FORK=0: one dW launch, then the time_l2_bwd launch; A/B knob)
-    static const bool tb_fork_env = [] { const char* e = getenv("DPPO_TB_FORK"); return !e || atoi(e) != 0; }();
+    // DPPO_TB_FORK=1 (A/B knob, off): the time-MLP backward needs only the bucket sums gseg, which the
+    // in_w problem of the actor's dW forms (its one-hot extra rows), so that problem and then the
+    // backward can run on a forked stream beside the rest of the dW and the l2_back / out_back launch,
+    // joined before the part returns. Measured slower (profiles/r05y_tb_fork_ab.txt: N = 1 update 11.9
+    // vs 10.1 ms, emulated W = 8 rank 30.4 vs 25.2 ms): a dW launch's latency is its chunk's rows, not
+    // its problem count, so the in_w problem alone takes as long as the whole dW (21 vs 22 us), and the
+    // forked stream shares a hardware queue with the critic's half (GPU_MAX_HW_QUEUES = 4)
+    static const bool tb_fork_env = [] { const char* e = getenv("DPPO_TB_FORK"); return e && atoi(e) != 0; }();
     SideStream* tbf = (tb_fork_env && !(hp->flags & DPPO_PPO_TIME_BWD_IN_STEP)) ? side_stream(1) : nullptr;
     auto actor_grads = [&]() -> int {
         if (!tbf) return launch_grads(true, s);
