@@ -522,6 +522,69 @@ __global__ __launch_bounds__(256) void l2_back_kernel(L2Back a, int l2_blocks, O
 // the kernel pays global-load latency about twice (staging, then G) instead of once per phase.
 // after_stage() runs once every staged parameter is in LDS (the one-launch actor step steps W_in's
 // time-embedding rows there: their old values are read, their gradient is the dW's)
+// dtemb[q][0..16) = G[q] . W_in[XD + j] for TD = 16, H = 64 NU: one wave per bucket q, its G row
+// loaded in one batch, 16 partial dot products per lane, reduced over the lanes by recursive halving
+// (lane bits 5..2 pick the value's j, bits 1..0 are summed last)
+template <int NU>
+__device__ inline void dtemb_rows(const float* g0, const float* win, float* dtemb, int KF, int wave, int lane) {
+    constexpr int H = 64 * NU;
+    for (int q = wave; q < KF; q += TB_THREADS / 64) {
+        const float* g = g0 + q * H + lane;
+        float gv[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) gv[u] = g[64 * u];
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            float s = 0.f;
+#pragma unroll
+            for (int u = 0; u < NU; ++u) s += gv[u] * win[j * H + 64 * u + lane];
+            v[j] = s;
+        }
+#pragma unroll
+        for (int lvl = 0; lvl < 4; ++lvl) {
+            const int half = 8 >> lvl, o = 32 >> lvl;
+            const bool up = (lane & o) != 0;
+#pragma unroll
+            for (int k = 0; k < half; ++k) {
+                const float keep = up ? v[k + half] : v[k], send = up ? v[k] : v[k + half];
+                v[k] = keep + __shfl_xor(send, o);
+            }
+        }
+        float t = v[0];
+        t += __shfl_xor(t, 2);
+        t += __shfl_xor(t, 1);
+        const int j = ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
+        if ((lane & 3) == 0) dtemb[q * 16 + j] = t;
+    }
+}
+
+// timing build (-DDPPO_TB_TIMING): shader-clock cycles of each phase of the time-MLP backward as
+// thread 0 sees them (barrier waits included), summed over launches (tools/bench_update.py reads them)
+#ifdef DPPO_TB_TIMING
+__device__ unsigned long long dppo_tb_cycles[8];
+#define TBPH_START unsigned long long tb_t_ = __builtin_readcyclecounter()
+#define TBPH(k)                                                                   \
+    do {                                                                          \
+        if (threadIdx.x == 0) {                                                   \
+            const unsigned long long now_ = __builtin_readcyclecounter();         \
+            atomicAdd(&dppo_tb_cycles[(k)], now_ - tb_t_);                         \
+            tb_t_ = now_;                                                         \
+        }                                                                         \
+    } while (0)
+extern "C" DPPO_API int dppo_debug_tb_cycles(unsigned long long* out, int reset) {
+    DPPO_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dppo_tb_cycles), sizeof(unsigned long long) * 8));
+    if (reset) {
+        unsigned long long z[8] = {};
+        DPPO_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dppo_tb_cycles), z, sizeof(z)));
+    }
+    return DPPO_OK;
+}
+#else
+#define TBPH_START
+#define TBPH(k) do {} while (0)
+#endif
+
 template <class AfterStage>
 __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float* prm, float* grad, const FlatOffsets& F,
                                      int XD, int TD, int H, int KF, int TS, int stage_g, float* sm, AfterStage&& after_stage) {
@@ -536,6 +599,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
     float* ma1 = da1 + KF * 2 * TD;     // [KF][2TD] mish(a1), once per element (time_w2's gradient reads it TD times)
     float* gs = stage_g ? ma1 + KF * 2 * TD : nullptr;   // [KF][H] copy of G when it fits
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    TBPH_START;
     // Staging: every global load of a chunk is issued before its first LDS store, so the phase pays
     // one load latency per chunk (one chunk at hopper's sizes) instead of one per array (separate
     // load-then-store loops waited out four round trips in a row)
@@ -564,6 +628,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
             if (base == 0 && tid < 2 * TD) b1[tid] = rb;
         }
     }
+    TBPH(0);
     const int half = TD / 2;
     const float lnf = logf(10000.f) / (float)(half - 1);
     for (int i = tid; i < KF * TD; i += TB_THREADS) {
@@ -581,6 +646,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
     }
     __syncthreads();
     after_stage();
+    TBPH(1);
     if (gs) {   // from the staged copy: no second global round trip
         for (int n = tid; n < H; n += TB_THREADS) {
             float s = 0.f;
@@ -589,8 +655,15 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
             grad[F.in_b + n] = s;
         }
     }
-    // dtemb[q][j] = G[q] . W_in[XD + j]: one wave per (q, j), lanes over the hidden units, G from
-    // LDS when it was staged (gs != nullptr), W_in rows from LDS
+    // dtemb[q][j] = G[q] . W_in[XD + j], G from LDS when it was staged (gs != nullptr), W_in rows from
+    // LDS: for TD = 16 one wave per bucket (dtemb_rows); otherwise (and with -DDPPO_TB_DTEMB_PAIRS, the
+    // A/B form) one wave per (q, j) — a G load and a whole-wave sum per pair, KF * TD / 16 rounds of
+    // both per wave
+#ifndef DPPO_TB_DTEMB_PAIRS
+    if (TD == 16 && H == 512) {
+        dtemb_rows<8>(gs ? gs : gseg, win, dtemb, KF, wave, lane);
+    } else
+#endif
     for (int i = wave; i < KF * TD; i += TB_THREADS / 64) {
         const int q = i / TD, j = i % TD;
         const float* g = (gs ? gs : gseg) + q * H;
@@ -600,6 +673,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
         s = wave_sum(s);
         if (lane == 0) dtemb[i] = s;
     }
+    TBPH(2);
     for (int i = tid; i < KF * 2 * TD; i += TB_THREADS) {
         const int q = i / (2 * TD), h = i % (2 * TD);
         float s = b1[h];
@@ -608,6 +682,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
         ma1[i] = mishf(s);
     }
     __syncthreads();
+    TBPH(3);
     for (int i = tid; i < KF * 2 * TD; i += TB_THREADS) {
         const int q = i / (2 * TD), h = i % (2 * TD);
         float dm = 0.f;
@@ -626,6 +701,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
         grad[F.time_b2 + j] = s;
     }
     __syncthreads();
+    TBPH(4);
     for (int i = tid; i < TD * 2 * TD; i += TB_THREADS) {            // time_w1 [TD][2TD]
         const int k = i / (2 * TD), h = i % (2 * TD);
         float s = 0.f;
@@ -637,6 +713,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
         for (int q = 0; q < KF; ++q) s += da1[q * 2 * TD + h];
         grad[F.time_b1 + h] = s;
     }
+    TBPH(5);
 }
 
 // time_bwd, the actor's l2_back and its out_back in one launch (all follow the actor's dW and are

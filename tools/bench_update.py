@@ -60,7 +60,16 @@ def main():
         lib.dppo_debug_phase_cycles(buf, 1)
         tiles = (args.rows + 63) // 64
         phases = {f"p{i}": round(buf[i] / tiles) for i in range(11)}
-    print(json.dumps({"rowtile": "default", "lib": os.path.basename(_lib.LIB_PATH),
+    tb = None
+    if hasattr(lib, "dppo_debug_tb_cycles"):   # timing build: the time-MLP backward's phases, one minibatch
+        import ctypes
+        buf = (ctypes.c_ulonglong * 8)()
+        lib.dppo_debug_tb_cycles(buf, 1)
+        m.minibatch(obs, chains, lp_old, adv, ret, 7, 0, 0, args.rows, global_rows=args.rows)
+        torch.cuda.synchronize()
+        lib.dppo_debug_tb_cycles(buf, 1)
+        tb = {f"t{i}": int(buf[i]) for i in range(6)}
+    print(json.dumps({"rowtile": "default", "lib": os.path.basename(_lib.LIB_PATH), "time_bwd_cycles": tb,
                       "phase_cycles_per_tile": phases,
                       "minibatch_ms": mb,
                       "logprob_pass_ms": lp, "value_pass_ms": cv,
