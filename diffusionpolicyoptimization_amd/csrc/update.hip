@@ -591,7 +591,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
     float* win = sm;                    // [TD][H]   W_in rows XD .. XD+TD-1
     float* w1 = win + TD * H;           // [TD][2TD]
     float* b1 = w1 + TD * 2 * TD;       // [2TD]
-    float* w2 = b1 + 2 * TD;            // [2TD][TD]
+    float* w2 = b1 + 2 * TD;            // [TD][2TD]: time_w2 transposed (da1's reads run along h, conflict-free)
     float* dtemb = w2 + 2 * TD * TD;    // [KF][TD]
     float* e = dtemb + KF * TD;         // [KF][TD]
     float* a1 = e + KF * TD;            // [KF][2TD]
@@ -603,9 +603,19 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
     // Staging: every global load of a chunk is issued before its first LDS store, so the phase pays
     // one load latency per chunk (one chunk at hopper's sizes) instead of one per array (separate
     // load-then-store loops waited out four round trips in a row)
+    // in_b' = sum_q G[q] (G unstaged): thread n's KF bucket values ride in the staging batch, so the
+    // sum pays no round trip of its own (clamped addresses: no branch between the loads)
+    constexpr int GQ = 16;
+    const bool pre_in = !gs && KF <= GQ && H <= TB_THREADS;
+    float gin[GQ];
     {
         constexpr int U = 8;
         const int ng = gs ? KF * H : 0, nw = TD * H, nt = TD * 2 * TD;
+        if (pre_in) {
+            const int nn = tid < H ? tid : 0;
+#pragma unroll
+            for (int q = 0; q < GQ; ++q) gin[q] = gseg[(q < KF ? q : 0) * H + nn];
+        }
         const float* wsrc = prm + F.in_w + (size_t)XD * H;
         for (int base = 0; base < ng || base < nw || base < nt; base += U * TB_THREADS) {
             float rg[U], rw[U], r1[U], r2[U];
@@ -623,7 +633,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
                 const int i = base + u * TB_THREADS + tid;
                 if (i < ng) gs[i] = rg[u];
                 if (i < nw) win[i] = rw[u];
-                if (i < nt) { w1[i] = r1[u]; w2[i] = r2[u]; }
+                if (i < nt) { w1[i] = r1[u]; w2[(i % TD) * 2 * TD + i / TD] = r2[u]; }
             }
             if (base == 0 && tid < 2 * TD) b1[tid] = rb;
         }
@@ -636,7 +646,15 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
         const float f = expf(-(float)(j % half) * lnf) * (float)(q * TS);   // bucket q = row q: t = q * TS
         e[i] = j < half ? sinf(f) : cosf(f);
     }
-    if (!gs) {
+    if (pre_in) {
+        if (tid < H) {
+            float s = 0.f;
+#pragma unroll
+            for (int q = 0; q < GQ; ++q)
+                if (q < KF) s += gin[q];
+            grad[F.in_b + tid] = s;
+        }
+    } else if (!gs) {
         for (int n = tid; n < H; n += TB_THREADS) {   // in_b' = sum_q G[q]
             float s = 0.f;
 #pragma unroll 8
@@ -686,7 +704,7 @@ __device__ inline void time_bwd_body(const float* __restrict__ gseg, const float
     for (int i = tid; i < KF * 2 * TD; i += TB_THREADS) {
         const int q = i / (2 * TD), h = i % (2 * TD);
         float dm = 0.f;
-        for (int j = 0; j < TD; ++j) dm += dtemb[q * TD + j] * w2[h * TD + j];
+        for (int j = 0; j < TD; ++j) dm += dtemb[q * TD + j] * w2[j * 2 * TD + h];
         da1[i] = dm * mish_gradf(a1[i]);
     }
     for (int i = tid; i < 2 * TD * TD; i += TB_THREADS) {            // time_w2 [2TD][TD]
