@@ -762,6 +762,10 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     constexpr int KW = (NVW + SL - 1) / SL;  // sweep loads per lane
     static_assert(KW <= P, "the finishing lanes are the members' lanes");
     constexpr int NB = H + NOC;            // per-actor bias floats: b_l1 | B_OUT2
+    // TIN rows in LDS: all K (hopper's KX = 1), or a 2-row ring refilled one step ahead by LDS-DMA
+    // (KX = 2, walker2d / halfcheetah: the K rows' 40 KB on top of the 2-k-step in-Dense fragments
+    // would exceed the CU's 160 KB, split4_lds_bytes)
+    constexpr bool TRING = KX == 2;
 
     const SampleArgs& a = sa.a;
     // dual: set 0 runs the base actor's steps (t >= K'), set 1 the fine-tuned actor's (t < K'), each
@@ -790,11 +794,19 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     int* xfail = (int*)(smem + o); o += 16;                // [0] exchange failure, [1] exchange mode
     float* xs = (float*)(smem + o); o += dppo_align16(4 * 16 * XD);
     float* st = (float*)(smem + o); o += dppo_align16(4 * 16 * SD);
-    float* tin = (float*)(smem + o); o += dppo_align16(4 * K * H);
+    float* tin = (float*)(smem + o); o += dppo_align16(4 * (TRING ? 2 : K) * H);
     float* sch = (float*)(smem + o); o += dppo_align16(4 * K * DPPO_SCHED_COLS);
     float* bias = (float*)(smem + o); o += dppo_align16(4 * 2 * NB);
     float* zt = (float*)(smem + o); o += dppo_align16(4 * K * 16 * XD);
     u32x4* wxs = (u32x4*)(smem + o); o += (size_t)SW * NTI * KX * 1024;   // [wave][n][ks] in-Dense fragments
+    // TRING: row t of the actor that runs it (fine-tuned below K'), as 2 KB of LDS-DMA by waves 0 and 1
+    // (lane l's 16 B at slot + 16 l); waited for by the issuing wave's vmcnt(0) and published by a barrier
+    auto tin_dma = [&](int tr, int slot) {
+        if (wave < H / 256) {
+            const uint8_t* src = (tr < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIN] + (size_t)tr * H * 4 + 1024 * wave + 16 * lane;
+            __builtin_amdgcn_global_load_lds((void*)src, (__attribute__((address_space(3))) void*)(tin + slot * H + 256 * wave), 16, 0, 0);
+        }
+    };
 
     // ---- resident weight fragments (one actor at a time): l1 and the folded out-Dense in
     //      registers; the in-Dense fragments in this wave's own LDS ----
@@ -848,9 +860,13 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
                                     : *((const float4*)(PK + L.off[SEG_B_OUT2]) + (j - H) / 4);
     }
     // TIN row t of the actor that runs step t (base for t >= K', fine-tuned below)
-    for (int i4 = tid; i4 < K * H / 4; i4 += ST) {
-        const int t = 4 * i4 / H;
-        ((float4*)tin)[i4] = ((const float4*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIN]))[i4];
+    if constexpr (TRING) {
+        tin_dma(K - 1 - i0, i0 & 1);   // the set's first step; later rows one step ahead
+    } else {
+        for (int i4 = tid; i4 < K * H / 4; i4 += ST) {
+            const int t = 4 * i4 / H;
+            ((float4*)tin)[i4] = ((const float4*)((t < KF ? a.packed_ft : a.packed_base) + L.off[SEG_TIN]))[i4];
+        }
     }
     // per-step epilogue constants [i][c0 c1 c2 c3 sd]: schedule row t = K-1-i and the noise rule
     // (include/dppo.h: eval DDPM t = 0 or any DDIM row -> 0; other DDPM rows clip at 1e-3; train:
@@ -1009,32 +1025,38 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
 #pragma unroll
             for (int ks = 0; ks < KX; ++ks) af[ks] = lds_afrag<Pol>(a0, lda0, 0, ks, lane);
 #pragma unroll
-            for (int n = 0; n < NTI; ++n) h1[n] = *(const f32x4*)(tin + t * H + 16 * (NTI * wave + n) + 4 * jq);
+            for (int n = 0; n < NTI; ++n) h1[n] = *(const f32x4*)(tin + (TRING ? (i & 1) : t) * H + 16 * (NTI * wave + n) + 4 * jq);
 #pragma unroll
-            for (int ks = 0; ks < KX; ++ks)
-#pragma unroll
-                for (int n = 0; n < NTI; ++n) wf[ks][n] = wxs[((wave * NTI + n) * KX + ks) * 64 + lane];
-            // one LDS round trip for all of them
+            for (int n = 0; n < NTI; ++n) wf[0][n] = wxs[((wave * NTI + n) * KX + 0) * 64 + lane];
+            // one LDS round trip for all of them (KX = 2: the second k-step's operands in a second
+            // round trip after the first k-step's MFMAs, which keeps the walker2d form within 256 VGPRs
+            // — all at once it spilled the epilogue's output addresses to scratch)
 #if DPPO_S4_INREADY
             asm volatile("" ::"v"(af[0]), "v"(h1[0]), "v"(h1[1]), "v"(h1[2]), "v"(h1[3]), "v"(wf[0][0]), "v"(wf[0][1]),
                          "v"(wf[0][2]), "v"(wf[0][3]));
             if constexpr (NTI == 8)
                 asm volatile("" ::"v"(h1[NTI - 4]), "v"(h1[NTI - 3]), "v"(h1[NTI - 2]), "v"(h1[NTI - 1]), "v"(wf[0][NTI - 4]),
                              "v"(wf[0][NTI - 3]), "v"(wf[0][NTI - 2]), "v"(wf[0][NTI - 1]));
-            if constexpr (KX == 2)
-                asm volatile("" ::"v"(af[KX - 1]), "v"(wf[KX - 1][0]), "v"(wf[KX - 1][1]), "v"(wf[KX - 1][2]), "v"(wf[KX - 1][3]));
-            if constexpr (KX == 2 && NTI == 8)
-                asm volatile("" ::"v"(wf[KX - 1][NTI - 4]), "v"(wf[KX - 1][NTI - 3]), "v"(wf[KX - 1][NTI - 2]),
-                             "v"(wf[KX - 1][NTI - 1]));
 #endif
 #if DPPO_S4_EPIEARLY
             asm volatile("" ::"v"(ec), "v"(esd), "v"(xe), "v"(ze), "v"(be));
 #endif
 #pragma unroll
-            for (int ks = 0; ks < KX; ++ks)
+            for (int n = 0; n < NTI; ++n) h1[n] = Pol::mma(wf[0][n], af[0], h1[n]);
+            if constexpr (KX == 2) {
 #pragma unroll
-                for (int n = 0; n < NTI; ++n) h1[n] = Pol::mma(wf[ks][n], af[ks], h1[n]);
+                for (int n = 0; n < NTI; ++n) wf[1][n] = wxs[((wave * NTI + n) * KX + 1) * 64 + lane];
+#if DPPO_S4_INREADY
+                asm volatile("" ::"v"(af[1]), "v"(wf[1][0]), "v"(wf[1][1]), "v"(wf[1][2]), "v"(wf[1][3]));
+                if constexpr (NTI == 8)
+                    asm volatile("" ::"v"(wf[1][NTI - 4]), "v"(wf[1][NTI - 3]), "v"(wf[1][NTI - 2]), "v"(wf[1][NTI - 1]));
+#endif
+#pragma unroll
+                for (int n = 0; n < NTI; ++n) h1[n] = Pol::mma(wf[1][n], af[1], h1[n]);
+            }
             if (pre) load_in(PKn);
+            if constexpr (TRING)   // the next step's row into the other slot (last read in step i - 1)
+                if (i + 1 < i1) tin_dma(t - 1, (i + 1) & 1);
 #pragma unroll
             for (int n = 0; n < NTI; ++n) {
                 const int f = 16 * (NTI * wave + n) + 4 * jq;
@@ -1169,6 +1191,10 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
             }
 #pragma unroll
             for (int k = 0; k < KW; ++k) val[k] = __uint_as_float((uint32_t)xa[k]);
+            // TRING: the next TIN row (issued before the poll's loads, so their vmcnt(0) already covered
+            // it) has landed before this wave reaches the step-end barrier
+            if constexpr (TRING)
+                if (wave < H / 256) __builtin_amdgcn_s_waitcnt(0x0F70);
             XPHASE(5);
             // member sum: xor 1 (then xor 2) inside the quad; every lane adds the same two partial
             // sums, so all P hold the same bits
@@ -1724,7 +1750,7 @@ size_t split4_lds_bytes(int XD, int SD, int K, int KX, int NO, int sw) {
     o += 16;
     o += dppo_align16(4 * 16 * XD);
     o += dppo_align16(4 * 16 * SD);
-    o += dppo_align16(4 * K * SPLIT_H);
+    o += dppo_align16(4 * (KX == 2 ? 2 : K) * SPLIT_H);   // TIN: all K rows, or the KX = 2 kernel's 2-row ring
     o += dppo_align16(4 * K * DPPO_SCHED_COLS);
     o += dppo_align16(4 * 2 * (SPLIT_H + 16 * NO));
     o += dppo_align16(4 * K * 16 * XD);

@@ -421,6 +421,7 @@ struct OutBack {
     float* gw;            // [H][N] dW_out
     int H, IN, N, prec;
 };
+// (of the INSTANTIATED width l2_nq(N): the host's group count must use the same width as the kernel)
 __host__ __device__ constexpr int ob_rows(int N) { return N <= 16 ? 4 : 2; }
 template <int PREC>
 __device__ inline float round_prec(float x) {
@@ -1894,7 +1895,7 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
     const size_t tsm = tsm0 > sizeof(float) * OB_RED * (TB_THREADS / 256) ? tsm0 : sizeof(float) * OB_RED * (TB_THREADS / 256);
     DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
     const int per = TB_THREADS / 256;
-    const int l2g = l2_back && groups ? dppo_cdiv(D.H, L2B_ROWS) : 0, obg = groups ? dppo_cdiv(D.H, ob_rows(D.XD)) : 0;
+    const int l2g = l2_back && groups ? dppo_cdiv(D.H, L2B_ROWS) : 0, obg = groups ? dppo_cdiv(D.H, ob_rows(l2_nq(D.XD))) : 0;
     const int nq = l2_nq(D.XD);
     const void* fn = time_l2_bwd_fn(precision, nq);
     { const int rc_ = dppo_func_lds(fn, tsm); if (rc_) return rc_; }
@@ -2160,7 +2161,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         L2Back l2b = {ws.pl2, ga + FA.out_b, (const uint8_t*)packed_ft + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b,
                       D.H, D.XD, precision, nullptr, nullptr, nullptr};
         DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
-        const int l2g = l2_def ? 0 : dppo_cdiv(D.H, L2B_ROWS), obg = dppo_cdiv(D.H, ob_rows(D.XD));
+        const int l2g = l2_def ? 0 : dppo_cdiv(D.H, L2B_ROWS), obg = dppo_cdiv(D.H, ob_rows(l2_nq(D.XD)));
         DppoKtScope kt(KT_L2_BACK, s);
         launch_l2_back(precision, (unsigned)(l2g > obg ? l2g : obg), s, l2b, l2g,
                        make_out_back(D, precision, actor_params, pl2_src, ws.pa0, ga), obg);

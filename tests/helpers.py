@@ -6,6 +6,8 @@ from oracle import dppo_oracle as O
 HOPPER = dict(obs_dim=11, action_dim=3, horizon_steps=4, cond_steps=1, time_dim=16, actor_hidden=512,
               critic_hidden=256, denoising_steps=20, ft_denoising_steps=10)
 WALKER = dict(HOPPER, obs_dim=17, action_dim=6)
+# an action width the kernels do not specialise (XD = 8: padded to the generic 32-wide instantiation)
+NARROW = dict(HOPPER, action_dim=2)
 # BASELINE config 5: DDIM, 10 sampling rows over K = 20 (time stride 2), all fine-tuned
 HOPPER_DDIM = dict(HOPPER, denoising_steps=10, ft_denoising_steps=10, time_stride=2)
 

@@ -1,8 +1,10 @@
-"""Full-size per-GPU shards of BASELINE configs 3-5 through the agent on the HIP path: one train
+"""Full-size per-GPU shards of BASELINE configs 2-5 through the agent on the HIP path: one train
 iteration at the config's own size (reference agent/finetune/train_ppo_diffusion_agent.py:58-377,
 model/diffusion/diffusion_ppo.py:32-132), checked by properties and against the oracle on sampled
 rows.
 
+  * config 2 (the benchmarked workload: hopper, 64 envs x 500 chunks, bf16 denoiser, 5 epochs x 6
+    minibatches of 50,000 rows = 30 applied);
   * config 3 / 4 (walker2d / halfcheetah dims: Do 17, Da 6, XD = 24; the per-GPU shard of the
     8-GPU halfcheetah run is the same 256 envs): 256 envs x 500 chunks, bf16 denoiser;
   * config 5 (hopper DDIM, 10 rows over K = 20, fp16; the per-GPU shard of the 4096-env run):
@@ -28,11 +30,13 @@ from tests.helpers import to_f64
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-CASES = [("walker2d-v2", "ft_ppo_diffusion_mlp", "bf16", 256, O.round_bf16),
+CASES = [("hopper-v2", "ft_ppo_diffusion_mlp_64env", "bf16", 64, O.round_bf16),
+         ("walker2d-v2", "ft_ppo_diffusion_mlp", "bf16", 256, O.round_bf16),
          ("hopper-v2", "ft_ppo_diffusion_mlp_ddim", "fp16", 512, O.round_fp16)]
 
 
-@pytest.mark.parametrize("sub,name,precision,E,rnd", CASES, ids=["walker-config3-4-256env-bf16", "ddim-config5-512env-fp16"])
+@pytest.mark.parametrize("sub,name,precision,E,rnd", CASES,
+                         ids=["hopper-config2-64env-bf16", "walker-config3-4-256env-bf16", "ddim-config5-512env-fp16"])
 def test_full_size_train_iteration(cuda, tmp_path, sub, name, precision, E, rnd):
     import torch
     from diffusionpolicyoptimization_amd import ops

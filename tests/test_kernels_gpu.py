@@ -11,7 +11,7 @@ import pytest
 
 from oracle import dppo_oracle as O
 from oracle import philox as PX
-from tests.helpers import HOPPER, HOPPER_DDIM, WALKER, make_models, to_f64
+from tests.helpers import HOPPER, HOPPER_DDIM, NARROW, WALKER, make_models, to_f64
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -110,6 +110,8 @@ def test_sampler_bf16_sizes_philox(cuda, E, dims):
     d, base, ft, critic, sched, tab, pb, pf, pc = _setup(dims, cuda)
     split = ops.sampler_layout(d, "bf16", E) > 0
     assert split == (E <= 512)
+    if split:   # every split shape runs the folded 2-member kernel (walker2d's since r06: its TIN ring)
+        assert ops.sampler_plan(d, "bf16", E)["kernel"] == 2, ops.sampler_plan(d, "bf16", E)
     seed, call = 987654321, 3
     rng = np.random.default_rng(E)
     state = rng.uniform(-1, 1, (E, 1, d.obs_dim)).astype(np.float32)
@@ -770,7 +772,8 @@ def _dedup(bi):
                                                   ("bf16", "ratio1", 1e-2), ("bf16", "perturbed", 2e-2),
                                                   ("fp32", "perturbed-ddim", 2e-3), ("fp32", "perturbed-walker", 2e-3),
                                                   ("bf16", "ratio1-walker", 1e-2), ("fp16", "ratio1", 1e-2),
-                                                  ("fp16", "ratio1-ddim", 1e-2)])
+                                                  ("fp16", "ratio1-ddim", 1e-2), ("fp32", "perturbed-narrow", 2e-3),
+                                                  ("bf16", "ratio1-narrow", 1e-2)])
 def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     """c_loss forward metrics and gradients of pg_loss + 0.5 v_loss vs the oracle.
 
@@ -782,9 +785,10 @@ def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     because these minibatch sums cancel ~12x and clip branches flip under rounding)."""
     import torch
     from diffusionpolicyoptimization_amd import ops
-    # DDIM: time-MLP gradient at t = 2j; walker: XD = 24 through the 32-row actor tile
-    dims = HOPPER_DDIM if case.endswith("-ddim") else (WALKER if case.endswith("-walker") else HOPPER)
-    case = case.replace("-ddim", "").replace("-walker", "")
+    # DDIM: time-MLP gradient at t = 2j; walker: XD = 24 through the 32-row actor tile; narrow: XD = 8,
+    # a width with no instantiation of its own (W_out's gradient through the generic out_back groups)
+    dims = {"ddim": HOPPER_DDIM, "walker": WALKER, "narrow": NARROW}.get(case.split("-")[-1], HOPPER)
+    case = case.split("-")[0]
     d, base, ft, critic, sched, tab, pb, pf, pc = _setup(dims, cuda)
     rng = np.random.default_rng(12)
     N = 40                                  # samples (steps*envs)
