@@ -113,6 +113,7 @@ _SIGNATURES = {
     "dppo_ipc_allreduce": (_I, [_P, _I, _I, _I64, _P, _I64, _U64, _P, _P]),
     "dppo_ppo_clear_ranges": (_I, [_DIMS, _I, _I, _P, _P, _I, _P, _P, ctypes.POINTER(ctypes.c_int)]),
     "dppo_value_moments": (_I, [_P, _P, _I64, _P, _P]),
+    "dppo_episode_sums": (_I, [_P, _P, _I, _I, _I, _D, _P, _P]),
     "dppo_refresh_sampler_tables": (_I, [_P, _P]),
     "dppo_materialize_l2": (_I, [_DIMS, _I, _P, _P, _P, _I, _P]),
 }
@@ -122,7 +123,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 
 class DppoError(RuntimeError):

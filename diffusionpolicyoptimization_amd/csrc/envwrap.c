@@ -147,18 +147,22 @@ static inline void unnorm_act_row(int Da, const float* a, const float* mn, const
 
 DPPO_ENV_API void dppo_lowdim_normalize_obs(int64_t n, int Do, const double* raw, const float* mn, const float* mx,
                                             double* out) {
-    float rng[256];
-    if (Do > 256) return;
+    float stack[256];   /* any Do: wider observations take the range row from the heap */
+    float* rng = Do <= 256 ? stack : (float*)malloc(sizeof(float) * (size_t)(Do > 0 ? Do : 1));
+    if (!rng) abort();  /* a void entry point: no silent uninitialised output */
     for (int j = 0; j < Do; ++j) rng[j] = obs_rng_of(mn[j], mx[j]);
     for (int64_t r = 0; r < n; ++r) norm_obs_row(Do, raw + r * Do, mn, rng, out + r * Do);
+    if (rng != stack) free(rng);
 }
 
 DPPO_ENV_API void dppo_lowdim_unnormalize_action(int64_t n, int Da, const float* a, const float* mn, const float* mx,
                                                  float* out) {
-    float rng[64];
-    if (Da > 64) return;
+    float stack[64];
+    float* rng = Da <= 64 ? stack : (float*)malloc(sizeof(float) * (size_t)(Da > 0 ? Da : 1));
+    if (!rng) abort();
     for (int i = 0; i < Da; ++i) rng[i] = mx[i] - mn[i];
     for (int64_t r = 0; r < n; ++r) unnorm_act_row(Da, a + r * Da, mn, rng, out + r * Da);
+    if (rng != stack) free(rng);
 }
 
 static void* xcalloc(size_t n, size_t s) { return calloc(n ? n : 1, s); }

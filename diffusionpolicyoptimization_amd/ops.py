@@ -172,6 +172,21 @@ def refresh_sampler_tables(packed_actor):
     _lib.call("dppo_refresh_sampler_tables", ptr(packed_actor), stream_handle(packed_actor.device))
 
 
+def episode_sums(reward, firsts, act_steps, success_threshold, out):
+    """a16 (train_ppo_diffusion_agent.py:144-167) on the device: reward fp64 [S,E] (raw), firsts u8
+    [S+1,E] -> out fp64 [E,4] rows {episodes, sum of returns, sum of best rewards, successes} per env
+    (dppo_episode_sums); sum the rows in env order."""
+    S, E = reward.shape
+    if reward.dtype != torch.float64 or firsts.dtype != torch.uint8 or tuple(firsts.shape) != (S + 1, E):
+        raise ValueError("episode_sums: reward fp64 [S,E] and firsts u8 [S+1,E] expected")
+    if out.dtype != torch.float64 or tuple(out.shape) != (E, 4) or not (reward.is_contiguous() and firsts.is_contiguous()
+                                                                          and out.is_contiguous()):
+        raise ValueError("episode_sums: out fp64 [E,4], all contiguous")
+    _lib.call("dppo_episode_sums", ptr(reward), ptr(firsts), int(S), int(E), int(act_steps), float(success_threshold),
+              ptr(out), stream_handle(reward.device))
+    return out
+
+
 def value_moments(values, returns, out_address):
     """{sum y, sum y^2, sum d, sum d^2, n} of y = returns, d = returns - values (fp64) into 5 doubles
     at out_address (host-mapped, dppo_host_alloc) or a device tensor (dppo_value_moments)."""

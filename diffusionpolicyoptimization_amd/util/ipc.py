@@ -58,6 +58,14 @@ class IpcAllReduce:
         # every rank has mapped every peer before any kernel can signal into it
         dist.barrier(group=group)
 
+    def check(self):
+        """Raise if any call of this group since the last check timed out in its barrier (a peer did not
+        arrive; the kernel's abort word made every workgroup of every rank leave): the reduced buckets
+        of that update are not valid. The agent calls it after every update's final synchronize."""
+        if self._fail is not None and ctypes.c_uint32.from_address(self._fail.value).value:
+            raise _lib.DppoError("dppo_ipc_allreduce: a barrier timed out during this update (a peer did not "
+                                 "arrive); the group's results are not valid")
+
     def __call__(self, t, stream=None):
         if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
             raise ValueError("IpcAllReduce: expected a contiguous fp32 CUDA tensor")
@@ -86,3 +94,4 @@ class IpcAllReduce:
         self.lib.dppo_ipc_free(self._own)
         self.lib.dppo_host_free(self._fail)
         self._own = None
+        self._fail = None

@@ -35,7 +35,7 @@ extern "C" {
 
 /* ABI 13: the actor image (dppo_actor_packed_bytes) holds the row tiles' l2 fold segments; a pack or
  * fused step of an actor image is followed by the fold launch (DPPO_STEP_FUSED_PACK above) */
-#define DPPO_ABI_VERSION 13
+#define DPPO_ABI_VERSION 14
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -275,6 +275,14 @@ DPPO_API int dppo_reward_scale_per_env_apply(const double* reward, const double*
 DPPO_API int dppo_gae(const double* reward, const float* values, const float* last_values, const uint8_t* terminated,
              int S, int E, double gamma, double lam, double reward_scale_const,
              float* advantages, float* returns, void* stream);
+
+/* ---- a16: episode accounting (train_ppo_diffusion_agent.py:144-167) on the RAW rewards fp64 [S,E]
+ * and the episode-start flags first u8 [S+1,E] (row S: the flags after the last step): per env,
+ * out fp64 [E][4] = {episodes that start and end inside the rollout (consecutive starts s < en with
+ * en - s > 1), sum of their returns, sum of their best rewards max(rew[s:en]) / act_steps, count of
+ * best >= success_threshold}; the caller sums the rows in env order. (ABI 14) */
+DPPO_API int dppo_episode_sums(const double* reward, const uint8_t* first, int S, int E, int act_steps,
+                               double success_threshold, double* out, void* stream);
 
 /* ---- a22: explained-variance moments (train_ppo_diffusion_agent.py:373-377) of y = returns and
  * d = returns - values over n rows: moments fp64[5] = {sum y, sum y^2, sum d, sum d^2, n}, one

@@ -103,6 +103,8 @@ void* dppo_sim_linear_create(int E, int Do, int Da, const double* A, const doubl
 void dppo_sim_linear_seed(void* sim, const int64_t* seeds);
 void dppo_sim_linear_set_cost(void* sim, double cost_us);   /* measurement: busy work per env sub-step */
 void dppo_sim_linear_destroy(void* sim);
+/* the C linear simulator's dimensions: obs_dim <= 64 and action_dim <= 64 (dppo_sim_linear_step returns 1
+ * past them); the wrapper stack itself takes action_dim <= 64 and any obs_dim */
 int dppo_sim_linear_step(void* ctx, int n, const int32_t* idx, const double* act, double* obs, double* reward,
                          uint8_t* done, int8_t* time_limit);
 int dppo_sim_linear_reset(void* ctx, int n, const int32_t* idx, double* obs);

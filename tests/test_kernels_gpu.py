@@ -318,6 +318,32 @@ def test_gae(cuda, S, E):
     np.testing.assert_allclose(ret.cpu().numpy(), ref_r, rtol=1e-6, atol=1e-5)
 
 
+@pytest.mark.parametrize("S,E,p", [(50, 4, 0.1), (500, 64, 0.004), (500, 512, 0.02), (7, 3, 0.0), (1, 5, 0.5)])
+def test_episode_sums(cuda, S, E, p):
+    """a16 (agent :144-167) on the device (dppo_episode_sums): the per-env rows summed in env order
+    give the oracle's episode statistics (episodes that start and end inside the rollout, their
+    returns, best rewards / act_steps and successes), incl. envs with no finished episode, starts at
+    t = 0 and t = S, and episodes of length 1 (not counted)."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    rng = np.random.default_rng(S * 1000 + E)
+    firsts = (rng.random((S + 1, E)) < p).astype(np.uint8)
+    firsts[0, ::2] = 1
+    firsts[S, ::3] = 1
+    rew = rng.normal(0, 2, (S, E))
+    act_steps, thr = 4, 0.3
+    out = torch.empty(E, 4, dtype=torch.float64, device=cuda)
+    ops.episode_sums(torch.tensor(rew, device=cuda), torch.tensor(firsts, device=cuda), act_steps, thr, out)
+    rows = out.cpu().numpy()
+    n, tot, best, succ = rows.sum(axis=0)
+    ref = O.episode_stats(firsts, rew, act_steps, thr)
+    assert int(n) == ref["num_episode_finished"]
+    if n:
+        assert abs(tot / n - ref["avg_episode_reward"]) <= 1e-12 * max(1.0, abs(ref["avg_episode_reward"]))
+        assert abs(best / n - ref["avg_best_reward"]) <= 1e-12 * max(1.0, abs(ref["avg_best_reward"]))
+        assert succ / n == ref["success_rate"]
+
+
 def test_reward_scale_multi_call(cuda):
     import torch
     from diffusionpolicyoptimization_amd import ops
