@@ -39,7 +39,7 @@ class DppoPpoHparams(ctypes.Structure):
                 ("clip_ploss_coef_base", ctypes.c_float), ("clip_ploss_coef_rate", ctypes.c_float),
                 ("min_logprob_std", ctypes.c_float), ("vf_coef", ctypes.c_float), ("norm_adv", ctypes.c_int32),
                 ("reward_horizon", ctypes.c_int32), ("loss_scale", ctypes.c_float), ("global_rows", ctypes.c_int32),
-                ("flags", ctypes.c_int32)]
+                ("flags", ctypes.c_int32), ("clip_vloss_coef", ctypes.c_float), ("old_values", ctypes.c_void_p)]
 
 
 _P = ctypes.c_void_p

@@ -582,7 +582,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             if getattr(self, "_bound_key", None) != bkey:
                 bound = {"run_mb": m.bind_minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat,
                                                     self.perm_seed, rows_local_full, reward_horizon=self.reward_horizon,
-                                                    l2_deferred=l2_def, time_bwd_in_step=tb_in_step)}
+                                                    l2_deferred=l2_def, time_bwd_in_step=tb_in_step,
+                                                    old_values=self.values)}   # the clipped v_loss's (:110-116)
                 if split:
                     if fuse_actor:
                         bound["actor"] = opt.bind_actor(m.grads, na, m.dims, m.precision, m.packed_ft,

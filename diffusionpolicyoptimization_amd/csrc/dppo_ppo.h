@@ -77,6 +77,8 @@ struct LossHP {
     int norm_adv, reward_horizon;
     float grad_scale;     // loss_scale / global_rows
     float eta_unscale;    // learnable DDIM eta (DPPO_PPO_LEARN_ETA): 1 / the fp16 seed scale, else 0
+    float clip_vloss;     // > 0: the clipped value loss against old_values (diffusion_ppo.py:110-116)
+    const float* old_values;
 };
 
 struct ActorArgs {

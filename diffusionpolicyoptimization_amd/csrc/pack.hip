@@ -453,8 +453,9 @@ __global__ __launch_bounds__(PACK_THREADS) void pack_all_kernel(PackArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int k = ks * KG + (lane >> 4) * EPL + q;
+            const int kr = k < J.k_split ? k : k + J.k_skip;   // row subsets (W_XS) as the 2-byte branch
             float x = 0.f;
-            if (k < J.K && n < J.N) x = J.transposed ? W[(size_t)n * J.K + k] : W[(size_t)k * J.N + n];
+            if (k < J.K && n < J.N) x = J.transposed ? W[(size_t)n * J.K + k] : W[(size_t)kr * J.N + n];
             e[q] = x;
         }
         v = __builtin_bit_cast(u32x4, e);
@@ -479,7 +480,9 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
     const FlatOffsets F = make_flat_offsets(in_dim, hidden, out_dim, time_dim);
     const int KG = dppo_prec_2b(precision) ? 32 : 16;
     const bool actor = time_dim > 0;
-    const bool split_tables = actor && L.temb_steps > 0 && dppo_prec_2b(precision);
+    // the split sampler's tables (every precision since r06: fp32 runs the split kernel at P = 4, its fold
+    // from RT_FOLD and its residual from W_OUT, so only the 2-byte images carry FOLD / ROUT)
+    const bool split_tables = actor && L.temb_steps > 0;
     const bool main_jobs = what == PACK_ALL || what == PACK_UPDATE;
     const bool sampler_tables = split_tables && (what == PACK_ALL || what == PACK_SAMPLER || what == PACK_SAMPLER_TEMB);
     const bool temb_rows = L.temb_steps > 0 && (what != PACK_UPDATE || DPPO_PACK_UPDATE_TEMB);
@@ -528,9 +531,10 @@ static int add_mlp_jobs(PackArgs& a, int in_dim, int hidden, int out_dim, int ti
         b.temb = (float*)(P_out(packed) + L.off[SEG_TEMB]);
         b.tin = (float*)(P_out(packed) + L.off[SEG_TIN]);
         b.bout2 = (float*)(P_out(packed) + L.off[SEG_B_OUT2]);
-        b.fold = sampler_tables ? P_out(packed) + L.off[SEG_FOLD] : nullptr;
-        b.rout = sampler_tables ? P_out(packed) + L.off[SEG_ROUT] : nullptr;
-        b.nfold = sampler_tables ? L.nt_h : 0;
+        const bool fold2b = sampler_tables && dppo_prec_2b(precision);
+        b.fold = fold2b ? P_out(packed) + L.off[SEG_FOLD] : nullptr;
+        b.rout = fold2b ? P_out(packed) + L.off[SEG_ROUT] : nullptr;
+        b.nfold = fold2b ? L.nt_h : 0;
         // table blocks: [0, R) TEMB rows, [R, 2R) TIN rows, 2R B_OUT2 (time_table_block)
         b.first_table = what == PACK_SAMPLER ? L.temb_steps : 0;   // PACK_SAMPLER_TEMB: the TEMB rows too
         b.tables = sampler_tables ? 2 * L.temb_steps + 1 - b.first_table : (temb_rows ? L.temb_steps : 0);
@@ -695,7 +699,7 @@ int dppo_pack_models(const Dims& D, int precision, const float* actor_params, vo
         J.kind = 2; J.dst = (uint8_t*)zero_ptrs[r]; J.n = (int)(zero_bytes[r] / 4); J.threads = (J.n + 3) / 4;
     }
     if (actor_params && packed_actor) {
-        const bool defer = defer_sampler_tables && D.TD > 0 && dppo_prec_2b(precision);
+        const bool defer = defer_sampler_tables && D.TD > 0;
         rc = add_mlp_jobs(a, D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS,
                           defer ? PACK_UPDATE : PACK_ALL);
         if (rc) return rc;

@@ -692,9 +692,21 @@ __device__ __forceinline__ void critic_rowtile_body(const CriticArgs& a) {
             float vl = 0.f, dv = 0.f;
             if (n >= 0) {
                 const float w = a.crow_mult ? (float)a.crow_mult[n] : 1.f;   // copies of the sample in the minibatch
-                const float diff = V - a.returns[n];
-                vl = 0.5f * diff * diff * w;                     // v_loss = 0.5 mean((V-R)^2), diffusion_ppo.py:118
-                dv = a.hp.vf_coef * diff * a.hp.grad_scale * w;  // loss = pg + vf_coef * v_loss (agent :340)
+                const float R = a.returns[n], diff = V - R;
+                if (a.hp.clip_vloss > 0.f) {
+                    // diffusion_ppo.py:110-116: 0.5 max((V-R)^2, (V_old + clip(V - V_old, -c, c) - R)^2); the
+                    // gradient as TF routes it: tf.maximum's to its first argument on ties, clip_by_value's
+                    // through where V - V_old lies in [-c, c] (bounds included), zero outside
+                    const float c = a.hp.clip_vloss, old = a.hp.old_values[n], d = V - old;
+                    const float vc = old + fminf(fmaxf(d, -c), c), dc = vc - R;
+                    const float lu = diff * diff, lc = dc * dc;
+                    vl = 0.5f * fmaxf(lu, lc) * w;
+                    const float g = lu >= lc ? diff : ((d >= -c && d <= c) ? dc : 0.f);
+                    dv = a.hp.vf_coef * g * a.hp.grad_scale * w;
+                } else {
+                    vl = 0.5f * diff * diff * w;                     // v_loss = 0.5 mean((V-R)^2), diffusion_ppo.py:118
+                    dv = a.hp.vf_coef * diff * a.hp.grad_scale * w;  // loss = pg + vf_coef * v_loss (agent :340)
+                }
             }
             for (int q = 0; q < ktw; ++q) a0[r * lda0 + q] = P::cvt(q == 0 ? dv : 0.f);
             ((AT*)a.ws.cdvT)[grow0 + img_pos(r)] = P::cvt(dv);

@@ -742,8 +742,16 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     static_assert(P == 2 || P == 4, "members per group");
     constexpr int NO = (4 * XQ + 15) / 16;
     using AT = typename Pol::AT;
-    auto pack_bf16x2 = [](float lo, float hi) { return Pol::pack2(lo, hi); };
-    constexpr int H = SPLIT_H, KSH = H / 32;
+    // TWO: 2-byte operands (bf16 / fp16: the fold and residual as hi/lo pairs in one 16x16x32 MFMA); else
+    // fp32 (r06, P = 4: the l1 slice is 256 KB of fp32, 128 VGPRs of fragments per lane as bf16's at P = 2;
+    // 16x16x4 MFMAs, the fold from RT_FOLD and the residual from W_OUT, exact fp32 operands)
+    constexpr bool TWO = sizeof(AT) == 2;
+    constexpr int KGP = Pol::KG;
+    auto pack_bf16x2 = [](float lo, float hi) {
+        if constexpr (TWO) return Pol::pack2(lo, hi);
+        else return 0u;
+    };
+    constexpr int H = SPLIT_H, KSH = H / KGP;
     constexpr int HS = H / P;              // features per member slice (128)
     constexpr int SW = SWV;                // waves per member: 8 (2 per SIMD) or 4 (1 per SIMD)
     constexpr int NTI = 32 / SW;           // in-Dense n-tiles per wave
@@ -754,7 +762,7 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     constexpr int ST = SW * 64;
     constexpr int pad = 16;
     constexpr int ldh = H + pad;           // u1 row stride (2-byte elements)
-    constexpr int lda0 = KX * 32 + pad;    // a0 row stride
+    constexpr int lda0 = KX * KGP + pad;   // a0 row stride
     constexpr int XD = 4 * XQ;
     constexpr int NV = 16 * XD;            // coordinates of a 16-env eps block
     constexpr int NVW = NV / SW;           // per wave: 2 XD
@@ -765,7 +773,7 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     // TIN rows in LDS: all K (hopper's KX = 1), or a 2-row ring refilled one step ahead by LDS-DMA
     // (KX = 2, walker2d / halfcheetah: the K rows' 40 KB on top of the 2-k-step in-Dense fragments
     // would exceed the CU's 160 KB, split4_lds_bytes)
-    constexpr bool TRING = KX == 2;
+    constexpr bool TRING = KX == 2 || !TWO;
 
     const SampleArgs& a = sa.a;
     // dual: set 0 runs the base actor's steps (t >= K'), set 1 the fine-tuned actor's (t < K'), each
@@ -782,14 +790,14 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     const int row0 = g * 16;
     const MlpLayout& L = a.L;
     const int SD = a.SD, K = a.K, KF = a.KF;
-    const int KSX = packed_ksteps(XD + SD, 32);   // k-step stride of the W_XS image
+    const int KSX = packed_ksteps(XD + SD, KGP);  // k-step stride of the W_XS image
     const int i0 = sa.dual && set == 1 ? K - KF : 0, i1 = sa.dual && set == 0 ? K - KF : K;   // steps of this set
 
     // ---- LDS carve (all offsets multiples of 16 B) ----
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     size_t o = 0;
-    AT* a0 = (AT*)(smem + o); o += dppo_align16(2 * 16 * lda0);
-    AT* u1 = (AT*)(smem + o); o += dppo_align16(2 * 16 * ldh);
+    AT* a0 = (AT*)(smem + o); o += dppo_align16(sizeof(AT) * 16 * lda0);
+    AT* u1 = (AT*)(smem + o); o += dppo_align16(sizeof(AT) * 16 * ldh);
     float* part = (float*)(smem + o); o += dppo_align16(4 * SW * NV);      // [wave][16 x XD]
     int* xfail = (int*)(smem + o); o += 16;                // [0] exchange failure, [1] exchange mode
     float* xs = (float*)(smem + o); o += dppo_align16(4 * 16 * XD);
@@ -832,14 +840,26 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
             for (int j = 0; j < KSH; ++j) rl1[t][j] = load_bfrag_c(W(ft, SEG_W_L1), KSH, (HS / 16) * c + NL1 * wave + t, j, lane);
     };
     auto load_fold = [&](int ft) {
+        if constexpr (TWO) {   // FOLD / ROUT: [feature tile][out tile] hi/lo fragments
 #pragma unroll
-        for (int tt = 0; tt < NL1; ++tt)
+            for (int tt = 0; tt < NL1; ++tt)
 #pragma unroll
-            for (int n = 0; n < NO; ++n) rfold[tt][n] = load_bfrag_c(W(ft, SEG_FOLD), NO, (HS / 16) * c + NL1 * wave + tt, n, lane);
+                for (int n = 0; n < NO; ++n) rfold[tt][n] = load_bfrag_c(W(ft, SEG_FOLD), NO, (HS / 16) * c + NL1 * wave + tt, n, lane);
 #pragma unroll
-        for (int r = 0; r < NR; ++r)
+            for (int r = 0; r < NR; ++r)
 #pragma unroll
-            for (int n = 0; n < NO; ++n) rres[r][n] = load_bfrag_c(W(ft, SEG_ROUT), NO, NTI * wave + r * P + c, n, lane);
+                for (int n = 0; n < NO; ++n) rres[r][n] = load_bfrag_c(W(ft, SEG_ROUT), NO, NTI * wave + r * P + c, n, lane);
+        } else {               // fp32: M (RT_FOLD) and W_out (W_OUT) as packed [K = H][N = out]: a 16-feature
+                               // tile is one k-step
+#pragma unroll
+            for (int tt = 0; tt < NL1; ++tt)
+#pragma unroll
+                for (int n = 0; n < NO; ++n) rfold[tt][n] = load_bfrag_c(W(ft, SEG_RT_FOLD), L.ks_h, n, (HS / 16) * c + NL1 * wave + tt, lane);
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+#pragma unroll
+                for (int n = 0; n < NO; ++n) rres[r][n] = load_bfrag_c(W(ft, SEG_W_OUT), L.ks_h, n, NTI * wave + r * P + c, lane);
+        }
     };
 
     // announce this member's XCD (sc1 granule, tag = seq << 6: step tags are seq << 6 | i + 1)
@@ -927,7 +947,7 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
     }
     __syncthreads();
     // a0 = [x | state | 0]: everything but the state columns before the observation wait
-    constexpr int k1w = KX * 32;
+    constexpr int k1w = KX * KGP;
     for (int idx = tid; idx < 16 * k1w; idx += ST) {
         const int r = idx / k1w, cc = idx % k1w;
         if (cc >= XD && cc < XD + SD) continue;              // state columns: after the wait
@@ -1060,10 +1080,14 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
 #pragma unroll
             for (int n = 0; n < NTI; ++n) {
                 const int f = 16 * (NTI * wave + n) + 4 * jq;
-                u32x2 pk;
-                pk[0] = pack_bf16x2(relu_f(h1[n][0]), relu_f(h1[n][1]));
-                pk[1] = pack_bf16x2(relu_f(h1[n][2]), relu_f(h1[n][3]));
-                *(u32x2*)(u1 + env * ldh + f) = pk;
+                if constexpr (TWO) {
+                    u32x2 pk;
+                    pk[0] = pack_bf16x2(relu_f(h1[n][0]), relu_f(h1[n][1]));
+                    pk[1] = pack_bf16x2(relu_f(h1[n][2]), relu_f(h1[n][3]));
+                    *(u32x2*)(u1 + env * ldh + f) = pk;
+                } else {
+                    *(f32x4*)(u1 + env * ldh + f) = f32x4{relu_f(h1[n][0]), relu_f(h1[n][1]), relu_f(h1[n][2]), relu_f(h1[n][3])};
+                }
             }
         }
         // the residual term W_out^T h1 of this member's in-Dense tiles (h1 as a hi/lo pair against
@@ -1078,10 +1102,14 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
             for (int q = 1; q < P; ++q)
                 if (c == q) hv = h1[r * P + q];
             u32x4 bh;
-            bh[0] = pack_bf16x2(hv[0], hv[1]);
-            bh[1] = pack_bf16x2(hv[2], hv[3]);
-            bh[2] = pack_bf16x2(hv[0] - Pol::lo2f(bh[0]), hv[1] - Pol::hi2f(bh[0]));
-            bh[3] = pack_bf16x2(hv[2] - Pol::lo2f(bh[1]), hv[3] - Pol::hi2f(bh[1]));
+            if constexpr (TWO) {
+                bh[0] = pack_bf16x2(hv[0], hv[1]);
+                bh[1] = pack_bf16x2(hv[2], hv[3]);
+                bh[2] = pack_bf16x2(hv[0] - Pol::lo2f(bh[0]), hv[1] - Pol::hi2f(bh[0]));
+                bh[3] = pack_bf16x2(hv[2] - Pol::lo2f(bh[1]), hv[3] - Pol::hi2f(bh[1]));
+            } else {
+                bh = __builtin_bit_cast(u32x4, hv);   // h1's 4 features as the k-slots: exact
+            }
 #pragma unroll
             for (int n = 0; n < NO; ++n) po[n] = Pol::mma(rres[r][n], bh, po[n]);
         }
@@ -1105,24 +1133,29 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
                 for (int tt = 0; tt < NL1; ++tt) acc[tt] = Pol::mma(rl1[tt][j], fb[j], acc[tt]);
             // schedule: the bias and L1D fragment reads first, then one read per MFMA, so L1D reads
             // stay in flight ahead of the chain (left alone, hipcc issued read -> wait -> MFMA)
-            constexpr int L1D = DPPO_S4_L1D;
+            constexpr int L1D = DPPO_S4_L1D, MPC = TWO ? 1 : 4;   // hardware MFMAs per Pol::mma
             __builtin_amdgcn_sched_group_barrier(0x100, L1D + NL1, 0);
 #pragma unroll
             for (int j = 0; j < KSH - L1D; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, NL1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, NL1 * MPC, 0);
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
-            __builtin_amdgcn_sched_group_barrier(0x008, NL1 * L1D, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NL1 * MPC * L1D, 0);
             if (pre) load_l1(PKn);
             // folded l2 + out-Dense: a = relu(h2) rounded once, its 4 features per lane as k-slots
             // 0-3 and again as 4-7, against M's hi and lo halves
 #pragma unroll
             for (int tt = 0; tt < NL1; ++tt) {
                 u32x4 ba;
-                ba[0] = pack_bf16x2(relu_f(acc[tt][0]), relu_f(acc[tt][1]));
-                ba[1] = pack_bf16x2(relu_f(acc[tt][2]), relu_f(acc[tt][3]));
-                ba[2] = ba[0];
-                ba[3] = ba[1];
+                if constexpr (TWO) {
+                    ba[0] = pack_bf16x2(relu_f(acc[tt][0]), relu_f(acc[tt][1]));
+                    ba[1] = pack_bf16x2(relu_f(acc[tt][2]), relu_f(acc[tt][3]));
+                    ba[2] = ba[0];
+                    ba[3] = ba[1];
+                } else {
+                    ba = __builtin_bit_cast(u32x4, f32x4{relu_f(acc[tt][0]), relu_f(acc[tt][1]), relu_f(acc[tt][2]),
+                                                         relu_f(acc[tt][3])});
+                }
 #pragma unroll
                 for (int n = 0; n < NO; ++n) po[n] = Pol::mma(rfold[tt][n], ba, po[n]);
             }
@@ -1741,16 +1774,16 @@ size_t pair_lds_bytes(int XD, int SD, int K, int NS, int KX, int NO) {
     return o;
 }
 
-size_t split4_lds_bytes(int XD, int SD, int K, int KX, int NO, int sw) {
-    const int pad = 16, ldh = SPLIT_H + pad, lda0 = KX * 32 + pad;
+size_t split4_lds_bytes(int XD, int SD, int K, int KX, int NO, int sw, int esz = 2) {
+    const int pad = 16, ldh = SPLIT_H + pad, lda0 = KX * (esz == 2 ? 32 : 16) + pad;
     size_t o = 0;
-    o += dppo_align16(2 * 16 * lda0);
-    o += dppo_align16(2 * 16 * ldh);
+    o += dppo_align16((size_t)esz * 16 * lda0);
+    o += dppo_align16((size_t)esz * 16 * ldh);
     o += dppo_align16(4 * sw * 16 * XD);
     o += 16;
     o += dppo_align16(4 * 16 * XD);
     o += dppo_align16(4 * 16 * SD);
-    o += dppo_align16(4 * (KX == 2 ? 2 : K) * SPLIT_H);   // TIN: all K rows, or the KX = 2 kernel's 2-row ring
+    o += dppo_align16(4 * ((KX == 2 || esz == 4) ? 2 : K) * SPLIT_H);   // TIN: all K rows, or the 2-row ring (TRING)
     o += dppo_align16(4 * K * DPPO_SCHED_COLS);
     o += dppo_align16(4 * 2 * (SPLIT_H + 16 * NO));
     o += dppo_align16(4 * K * 16 * XD);
@@ -1941,7 +1974,7 @@ int launch_split4_kw(const SplitArgs& sa, hipStream_t s) {
     } else {
     auto k = sample_split4_kernel<Pol, XQ, KX, INJ, SWV, PM>;
     const SampleArgs& a = sa.a;
-    const size_t lds = split4_lds_bytes(a.XD, a.SD, a.K, KX, NO, SWV);
+    const size_t lds = split4_lds_bytes(a.XD, a.SD, a.K, KX, NO, SWV, (int)sizeof(typename Pol::AT));
     if (lds > 160 * 1024) return dppo_set_error(DPPO_EUNSUPPORTED, "split sampler needs %zu B of LDS", lds);
     { const int rc_ = dppo_func_lds((const void*)k, (size_t)lds); if (rc_) return rc_; }
     const int blocks = 8 * PM * ((sa.G + 7) / 8) * (sa.dual ? 2 : 1);
@@ -2000,15 +2033,25 @@ int split_p_choice() {
 struct SplitPlan { int P; bool dual; bool pair; int blocks; };
 
 SplitPlan split_plan(int precision, int H, int XD, int SD, int ks_in, int E, int K, int KF) {
-    if (!dppo_prec_2b(precision) || H != SPLIT_H || XD % 4 != 0 || XD > 32 || K > 62) return {0, false, false, 0};
+    // fp32 (r06): the folded kernel at P = 4 members (an fp32 l1 quarter is 128 VGPRs of fragments), for
+    // the instantiated width XD = 12 (hopper; other fp32 shapes stream the weights, sampler.hip)
+    const bool f32 = precision == DPPO_F32;
+    if ((!dppo_prec_2b(precision) && !(f32 && XD == 12)) || H != SPLIT_H || XD % 4 != 0 || XD > 32 || K > 62)
+        return {0, false, false, 0};
     const int G = dppo_cdiv(E, 16);
     if (G < 1 || G > XMAX_G) return {0, false, false, 0};
     const int cus = device_cus();
     // every workgroup of the launch co-resident (one per CU: the register budget)
     auto fits = [&](int P, int sets, int groups) { return cus == 0 || sets * 8 * P * ((groups + 7) / 8) <= cus; };
-    const int KX = dppo_cdiv(XD + SD, 32);
-    const bool p4 = KX <= 2 && split4_lds_bytes(XD, SD, K, KX, dppo_cdiv(XD, 16), split_waves()) <= 160 * 1024 &&
-                    fits(S4P, 1, G);
+    const int KX = dppo_cdiv(XD + SD, f32 ? 16 : 32);
+    const int PF = f32 ? 4 : S4P;   // members per group of the folded kernel
+    const bool p4 = KX <= 2 && split4_lds_bytes(XD, SD, K, KX, dppo_cdiv(XD, 16), split_waves(), f32 ? 4 : 2) <= 160 * 1024 &&
+                    fits(PF, 1, G);
+    if (f32) {
+        static const bool dual_f = [] { const char* e = getenv("DPPO_SPLIT_DUAL"); return !e || atoi(e) != 0; }();
+        const bool d = dual_f && KF > 0 && KF < K && (cus == 0 || 2 * 2 * 8 * PF * ((G + 7) / 8) <= cus);
+        return p4 ? SplitPlan{PF, d, false, 8 * PF * ((G + 7) / 8) * (d ? 2 : 1)} : SplitPlan{0, false, false, 0};
+    }
     const bool p8 = ks_in == 2 && fits(8, 1, G);
     static const bool dual_on = [] { const char* e = getenv("DPPO_SPLIT_DUAL"); return !e || atoi(e) != 0; }();
     // two sets only while two launches of them still fit side by side (the pipelined rollout keeps
@@ -2072,6 +2115,12 @@ int launch_sample_split(const SampleArgs& a, int precision, hipStream_t s) {
     if (rc) return rc;
     const bool inj = a.noise != nullptr;
     const bool f16 = precision == DPPO_F16;
+    if (precision == DPPO_F32) {   // split_plan took XD = 12 only
+        if (a.XD != 12 || P != 4) return DPPO_EUNSUPPORTED;
+        if (a.XD + a.SD > 16)
+            return inj ? launch_split4_kw<PolicyF32, 3, 2, true, 8, 4>(sa, s) : launch_split4_kw<PolicyF32, 3, 2, false, 8, 4>(sa, s);
+        return inj ? launch_split4_kw<PolicyF32, 3, 1, true, 8, 4>(sa, s) : launch_split4_kw<PolicyF32, 3, 1, false, 8, 4>(sa, s);
+    }
     if (plan.pair) {
         if (f16) return inj ? launch_pair_k<PolicyF16, 3, 1, true>(sa, s) : launch_pair_k<PolicyF16, 3, 1, false>(sa, s);
         return inj ? launch_pair_k<PolicyBF16, 3, 1, true>(sa, s) : launch_pair_k<PolicyBF16, 3, 1, false>(sa, s);

@@ -350,7 +350,7 @@ __device__ inline float packed_elem_t(const uint8_t* img, int K, int k, int n) {
 // runs the time-MLP backward itself and l2_back, when materialised, is this LDS-free launch alone.)
 constexpr int L2B_ROWS = 4;   // rows h of dW_l2 per workgroup
 constexpr int L2B_MAXN = 32;
-template <int PREC, int NJ, int NQ>
+template <int PREC, int NJ, int NQ, bool WT = false>
 __device__ inline void l2_back_cols(const L2Back& a, int b, int t, int nt) {
     // branch-free loads (a conditional load made hipcc wait for it alone): N is the instantiation's
     // width for the cfgs' widths (l2_back_rows_p), the workgroup's rows exist (b < H / L2B_ROWS), column
@@ -388,15 +388,21 @@ __device__ inline void l2_back_cols(const L2Back& a, int b, int t, int nt) {
             float sum = 0.f;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) sum = fmaf(pv[r][q], wc[q], sum);
-            if (r < L2B_ROWS) a.gw[(size_t)(h0 + r) * H + j] = sum;
-            else if (b == 0) a.gb[j] = sum;
+            // WT: write-through agent-scope stores (actor_tail_kernel's W_l2 blocks read them in the launch)
+            if constexpr (WT) {
+                if (r < L2B_ROWS) __hip_atomic_store(a.gw + (size_t)(h0 + r) * H + j, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if (b == 0) __hip_atomic_store(a.gb + j, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                if (r < L2B_ROWS) a.gw[(size_t)(h0 + r) * H + j] = sum;
+                else if (b == 0) a.gb[j] = sum;
+            }
         }
     }
 }
-template <int PREC, int NQ>
+template <int PREC, int NQ, bool WT = false>
 __device__ inline void l2_back_n(const L2Back& a, int b, int t) {   // 256 threads per row group b
-    if (a.H <= 256) l2_back_cols<PREC, 1, NQ>(a, b, t, 256);
-    else l2_back_cols<PREC, 2, NQ>(a, b, t, 256);
+    if (a.H <= 256) l2_back_cols<PREC, 1, NQ, WT>(a, b, t, 256);
+    else l2_back_cols<PREC, 2, NQ, WT>(a, b, t, 256);
 }
 // the kernels below are instantiated per precision and width NQ (the action-chunk widths of the cfgs:
 // hopper 12, walker2d / halfcheetah 24, the critic's 1, any other N <= 32 zero-padded to 32): a runtime
@@ -421,6 +427,11 @@ struct OutBack {
     float* gw;            // [H][N] dW_out
     int H, IN, N, prec;
 };
+static OutBack make_out_back(const Dims& D, int precision, const float* actor_params, const float* pl2, const float* pa0,
+                             float* ga) {
+    const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
+    return OutBack{actor_params, FA, pl2, pa0, ga + FA.out_b, ga + FA.out_w, D.H, D.IN, D.XD, precision};
+}
 // (of the INSTANTIATED width l2_nq(N): the host's group count must use the same width as the kernel)
 __host__ __device__ constexpr int ob_rows(int N) { return N <= 16 ? 4 : 2; }
 template <int PREC>
@@ -429,7 +440,9 @@ __device__ inline float round_prec(float x) {
     else if constexpr (PREC == DPPO_F16) return (float)(_Float16)x;
     else return x;
 }
-template <int PREC, int NQ>
+// WT: dW_out leaves as write-through agent-scope stores (actor_tail_kernel's last workgroup, on any XCD,
+// reads it in the same launch)
+template <int PREC, int NQ, bool WT = false>
 __device__ inline void out_back_n(const OutBack& a, int b, bool valid, int t, float* red) {
     constexpr int OBR = ob_rows(NQ), NQP = NQ <= 16 ? 16 : 32, V = OBR * NQP;   // V = 64
     static_assert(V == 64, "one value per lane after the halving");
@@ -492,7 +505,10 @@ __device__ inline void out_back_n(const OutBack& a, int b, bool valid, int t, fl
         if (f < H) {
             const float s = (red[v] + red[V + v]) + (red[2 * V + v] + red[3 * V + v]);
             const float bb = a.prm[a.F.l2_b + f] + a.prm[a.F.in_b + f];
-            a.gw[(size_t)f * NE + q] = fmaf(bb, a.gob[q], s);
+            if constexpr (WT)
+                __hip_atomic_store(a.gw + (size_t)f * NE + q, fmaf(bb, a.gob[q], s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                a.gw[(size_t)f * NE + q] = fmaf(bb, a.gob[q], s);
         }
     }
 }
@@ -1048,7 +1064,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 //    dppo_ppo_clear_ranges) are zeroed by the launch's LAST workgroup (per-XCD ticket counters), so
 //    no range is cleared before every workgroup has read what it reads — the metric sums copied out
 //    included, whichever ranges the caller passes.
-// The actor's step (ABI 12, actor_step_kernel below) adds its time-MLP backward and the W_out
+// The actor's step with its time-MLP backward is actor_tail_kernel below (r06); it adds the W_out
 // elements the virtual l2 gradient reads; a critic's step is this kernel.
 // ---------------------------------------------------------------------------------------------
 struct StepFuse {
@@ -1129,94 +1145,8 @@ __global__ __launch_bounds__(256) void adamw_fused_kernel(float* __restrict__ p,
 }
 
 // ---------------------------------------------------------------------------------------------
-// The actor's optimizer step in ONE launch (ABI 12, dppo_actor_step): everything after the actor's
-// weight-gradient GEMM of a minibatch — the time-MLP backward (time_bwd_body, from the per-t bucket
-// sums of dh1), the virtual l2 gradient (DPPO_STEP_L2_FROM_PL2), Keras AdamW, the image slots, the
-// gradient and accumulator clears — which took three launches (time_bwd, adamw, pack) before. The
-// elements are split so that nothing waits on another workgroup's result:
-//  * workgroup 0 runs the time-MLP backward (it reads the OLD W_in time-embedding rows and time MLP
-//    and writes the gradients of the time MLP and b_in), then steps exactly those elements;
-//  * workgroups 1.. step every other element except W_out; the l2 elements' virtual gradient reads
-//    pl2 / db_out and the OLD rnd(W_out) of the image's W_OUT segment;
-//  * the last workgroup to arrive (tickets) steps W_out — so its W_OUT / T_OUT slots change only
-//    after every l2 element has read them — then zeroes pl2 / db_out and the caller's ranges.
-// The TEMB table is NOT rewritten: the row tiles derive the time embeddings they use from the fp32
-// time MLP in the image (rowtile.hip), and the sampler re-derives TEMB with its deferred tables.
-// ---------------------------------------------------------------------------------------------
-struct ActorStep {
-    int njobs;
-    FuseJob j[FUSE_MAXJ];
-    int64_t own0[3][2];     // workgroup 0's elements: the time MLP, W_in's time-embedding rows, b_in
-    int64_t wout[2];        // the last workgroup's: W_out
-    int64_t keep[2][2];     // read by every l2 element (pl2 region, db_out): zeroed by the last workgroup
-    const float* gseg;      // [KF][H] bucket sums of dh1, or null (the gradients are already in g)
-    FlatOffsets F;
-    int XD, TD, H, KF, TS, stage_g;
-    int clear_grads;        // zero each gradient after its read (DPPO_STEP_CLEAR_GRADS)
-    void* clr[4];
-    uint32_t clr_words[4];
-    unsigned* ticket;
-};
-constexpr int ACTOR_STEP_THREADS = TB_THREADS;
-template <class ET, int KG, int EPL>
-__global__ __launch_bounds__(ACTOR_STEP_THREADS) void actor_step_kernel(float* __restrict__ p, float* g,
-                                                                        float* __restrict__ m, float* __restrict__ v,
-                                                                        int64_t n, AdamHP h, const double* met,
-                                                                        double* met_out, int nmet, uint64_t tag,
-                                                                        L2Virt vt, ActorStep a) {
-    extern __shared__ __attribute__((aligned(16))) float asm_[];
-    const int tid = threadIdx.x;
-    auto step_one = [&](int64_t i, float gi) {
-        float pi = p[i], mi = m[i], vi = v[i];
-        adamw_elem(pi, mi, vi, gi, h);
-        p[i] = pi; m[i] = mi; v[i] = vi;
-        fuse_all<ET, KG, EPL>(a.j, a.njobs, i, pi);
-    };
-    auto step_own = [&](int r) {   // independent elements, 4 in flight per thread
-#pragma unroll 4
-        for (int64_t i = a.own0[r][0] + tid; i < a.own0[r][1]; i += ACTOR_STEP_THREADS) {
-            const float gi = g[i];
-            if (a.clear_grads) g[i] = 0.f;
-            step_one(i, gi);
-        }
-    };
-    if (blockIdx.x == 0) {
-        if (a.gseg) {
-            // W_in's time-embedding rows are stepped as soon as the backward has staged their old values
-            time_bwd_body(a.gseg, p, g, a.F, a.XD, a.TD, a.H, a.KF, a.TS, a.stage_g, asm_, [&] { step_own(1); });
-            __syncthreads();   // its gradient stores, read below by other threads of this workgroup
-            step_own(0);
-            step_own(2);
-        } else {
-            for (int r = 0; r < 3; ++r) step_own(r);
-        }
-    } else {
-        if (blockIdx.x == 1) copy_metrics(met, met_out, nmet, tag);
-        const int64_t stride = (int64_t)(gridDim.x - 1) * ACTOR_STEP_THREADS;
-        for (int64_t i = (int64_t)(blockIdx.x - 1) * ACTOR_STEP_THREADS + tid; i < n; i += stride) {
-            if (in_range(i, a.own0[0]) || in_range(i, a.own0[1]) || in_range(i, a.own0[2]) || in_range(i, a.wout))
-                continue;
-            const bool virt = vt.on && i >= vt.w_off && i < vt.b_off + vt.H;   // [l2_w | l2_b] are adjacent
-            const float gi = virt ? l2_virtual_grad(g, vt, i) : g[i];
-            if (a.clear_grads && !in_range(i, a.keep[0]) && !in_range(i, a.keep[1])) g[i] = 0.f;
-            step_one(i, gi);
-        }
-    }
-    if (!last_workgroup(a.ticket)) return;
-    for (int64_t i = a.wout[0] + tid; i < a.wout[1]; i += ACTOR_STEP_THREADS) {
-        const float gi = g[i];
-        if (a.clear_grads) g[i] = 0.f;
-        step_one(i, gi);
-    }
-    if (a.clear_grads)
-        for (int r = 0; r < 2; ++r)
-            for (int64_t i = a.keep[r][0] + tid; i < a.keep[r][1]; i += ACTOR_STEP_THREADS) g[i] = 0.f;
-    clear_words(a.clr, a.clr_words);
-}
-
-// ---------------------------------------------------------------------------------------------
 // The actor's optimizer step as ONE coalesced launch (r05; the step without the time-MLP backward).
-// actor_step_kernel stores each element into its image slots one 2-byte value at a time (fuse_all):
+// r05's one-launch actor step stored each element into its image slots one 2-byte value at a time:
 // two scattered stores per weight, slower than AdamW + the coalesced pack launch. Here every wave owns
 // the elements of ONE 16-byte slot per lane of a weight tensor's packed image — a block of 16 outputs
 // x KG inputs — steps them with AdamW, stores the slot (one coalesced 1 KiB wave store) and, through a
@@ -1224,7 +1154,7 @@ __global__ __launch_bounds__(ACTOR_STEP_THREADS) void actor_step_kernel(float* _
 // step the fp32 tensors (biases, time MLP) one element per lane and copy them into their fp32
 // segments. The image bytes are the pack's (same (ET) conversion, zero padding). Under the virtual l2
 // gradient (DPPO_STEP_L2_FROM_PL2) the W_out blocks and the zeroing of what the l2 elements read wait
-// for the last workgroup, as in actor_step_kernel; the caller's clear ranges too.
+// for the last workgroup; the caller's clear ranges too.
 // ---------------------------------------------------------------------------------------------
 struct TileMat {
     int64_t off;            // first element in the step's range
@@ -1334,6 +1264,221 @@ __global__ __launch_bounds__(TILE_THREADS) void actor_tile_step_kernel(float* p,
     clear_words(a.clr, a.clr_words);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The actor's whole per-minibatch tail after its dW in ONE launch (r06; dppo_actor_step with a
+// workspace). Before: time_l2_bwd (time-MLP backward + W_out's gradient) -> the
+// coalesced AdamW step -> the fold, three dependent latency-bound launches (14.5 + 14 + 5.6 us per
+// 6,250-row minibatch, profiles/r05end_emu_timeline.txt). Here the time-MLP backward, W_out's gradient
+// (out_back), l2's gradient (the virtual form: pl2 rnd(W_out), per element) and the AdamW + image-slot
+// step of every actor parameter share one launch of TB_THREADS-thread workgroups:
+//   [0, ob_wgs)     out_back groups (TB_THREADS / 256 per workgroup): dW_out rows from the OLD W_l2, W_in,
+//                   b_l2, b_in, stored write-through; then the workgroup ARRIVES
+//   ob_wgs          the time-MLP backward (time_bwd_body) from the dW's bucket sums; it ARRIVES once it has
+//                   staged the OLD W_in time-embedding rows, steps the time MLP (its own elements), and steps
+//                   b_in after every out_back workgroup has arrived (they read the old b_in)
+//   ob_wgs + 1 ...  16 tile waves per workgroup, the coalesced step of actor_tile_step_kernel: W_in, W_l1,
+//                   W_l2 blocks and the l1_b / l2_b / out_b elements. The stores of W_in, W_l2 and b_l2 (read
+//                   OLD by out_back and the backward) wait for all arrivals
+//   the last workgroup to finish (tickets) steps W_out (its gradient from out_back's stores, its old image
+//                   read by every l2 element's virtual gradient before), zeroes pl2 / db_out and the caller's
+//                   ranges, and resets the arrival counter.
+// Every wait is on LOWER-indexed workgroups only, so the launch cannot deadlock even when not all of its
+// workgroups are co-resident (workgroups are dispatched in index order). No data crosses workgroups
+// through the cache hierarchy except dW_out (write-through stores, agent-scope loads); the waits order
+// old-value reads before new-value stores (write-after-read), which needs no fence.
+// ---------------------------------------------------------------------------------------------
+struct ActorTail {
+    TileStep ts;              // the tile step's tables; ts.last_mat = W_out (virtual l2) or -1
+    int in_mat, l2_mat;       // mats whose stores wait for the arrivals (-1: none)
+    int out_mat;              // W_out: its image is read OLD by l2_back (its stores wait too), or last_mat
+    int64_t l2bias[2];        // the l2_b elements (their stores wait too)
+    OutBack ob;
+    int ob_groups, ob_wgs;    // out_back groups and the workgroups that run them
+    L2Back l2b;               // l2's gradient materialised here (not under the virtual l2): l2_back's row
+    int l2_groups, l2_wgs;    // groups in workgroups [ob_wgs, ob_wgs + l2_wgs), stored write-through
+    const float* gseg;
+    FlatOffsets F;
+    int XD, TD, H, KF, TS, stage_g;
+    float* time_dst;          // the image's fp32 time-MLP segment (element e = F.time_w1 + e)
+    float* inb_dst;           // the image's fp32 b_in segment
+    unsigned* arrive;         // zero between launches (the last workgroup resets it)
+};
+// the arrivals every waiting store needs: the out_back workgroups + the time-MLP backward
+__device__ inline void tail_wait(const unsigned* arrive, unsigned need) {
+    if ((threadIdx.x & 63) == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 200000000ull;   // 2 s: never reached unless
+        while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need &&   // a lower-indexed
+               __builtin_amdgcn_s_memrealtime() < t_end)                                          // workgroup died
+            __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+// one 16-output x KG-input block of a packed weight (tile_block's geometry and image bytes); GA: the
+// gradient through agent-scope loads (written earlier in this launch by another workgroup); WAIT: the
+// parameter / moment / image stores after tail_wait. Virtual l2 (vt.on, the W_l2 block): the gradient of
+// element (k, n) is sum_q pl2[k][q] rnd(W_out[n][q]) (l2_back_cols' order), W_out's row n read once.
+template <class ET, int KG, int EPL, int PREC, int NQ>
+__device__ inline void tail_block(float* p, float* g, float* m, float* v, const AdamHP& h, const L2Virt& vt,
+                                  const ActorTail& a, const TileMat& M, int b, ET* tile, int lane, bool virt, bool ga,
+                                  bool wait, unsigned need) {
+    const TileStep& t = a.ts;
+    const int nb = b % M.nb, kb = b / M.nb;
+    const int n = 16 * nb + (lane & 15), jq = lane >> 4;
+    const int N = NQ < L2B_MAXN ? NQ : vt.XD;
+    float wo[NQ];
+    if (virt) {
+        const int nc = n < M.N ? n : M.N - 1;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) wo[q] = q < N ? packed_elem_t<PREC>(vt.wimg, vt.H, nc, q) : 0.f;
+    }
+    float pn[EPL], mn[EPL], vn[EPL];
+    bool ok[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+        const int k = KG * kb + EPL * jq + e;
+        ok[e] = k < M.K && n < M.N;
+        pn[e] = 0.f;
+        if (ok[e]) {
+            const int64_t i = M.off + (int64_t)k * M.N + n;
+            float pi = p[i], mi = m[i], vi = v[i], gi;
+            if (virt) {
+                const float* pv = g + vt.w_off + (int64_t)k * vt.XD;
+                float sum = 0.f;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q)
+                    if (q < N) sum = fmaf(pv[q], wo[q], sum);
+                gi = sum;
+            } else {
+                gi = ga ? __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : g[i];
+            }
+            if (t.clear_grads && !in_range(i, t.keep[0]) && !in_range(i, t.keep[1])) g[i] = 0.f;
+            adamw_elem(pi, mi, vi, gi, h);
+            pn[e] = pi; mn[e] = mi; vn[e] = vi;
+        }
+    }
+    if (wait) tail_wait(a.arrive, need);
+    ET val[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+        const int k = KG * kb + EPL * jq + e;
+        if (ok[e]) {
+            const int64_t i = M.off + (int64_t)k * M.N + n;
+            p[i] = pn[e]; m[i] = mn[e]; v[i] = vn[e];
+        }
+        val[e] = (ET)pn[e];
+    }
+    u32x4 w;
+    __builtin_memcpy(&w, val, 16);
+    *reinterpret_cast<u32x4*>(M.img + ((((size_t)nb * M.KS + kb) << 6) + lane) * 16) = w;
+    if (!M.timg) return;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) tile[(EPL * jq + e) * 16 + (lane & 15)] = val[e];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int NGRP = 16 / EPL;
+    const int kk = lane & 15, grp = lane >> 4;
+    const int kl = 16 * (grp / NGRP) + kk, ng = grp % NGRP;
+    const int k = KG * kb + kl, n0 = 16 * nb + EPL * ng;
+    const u32x4 tv = *reinterpret_cast<const u32x4*>(tile + kl * 16 + EPL * ng);
+    if (k < 16 * ((M.K + 15) / 16)) {
+        const int ntp = k >> 4, ksp = n0 / KG, lanep = kk + 16 * ((n0 % KG) / EPL);
+        *reinterpret_cast<u32x4*>(M.timg + ((((size_t)ntp * M.KST + ksp) << 6) + lanep) * 16) = tv;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <class ET, int KG, int EPL, int PREC, int NQ>
+__global__ __launch_bounds__(TB_THREADS) void actor_tail_kernel(float* p, float* g, float* m, float* v, AdamHP h,
+                                                                const double* met, double* met_out, int nmet,
+                                                                uint64_t tag, L2Virt vt, ActorTail a) {
+    extern __shared__ __attribute__((aligned(16))) float tsm[];
+    constexpr int WPB = TB_THREADS / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = (int)blockIdx.x;
+    const int tb = a.ob_wgs + a.l2_wgs;   // the time-MLP backward's workgroup
+    const unsigned need = (unsigned)tb + 1;
+    const TileStep& t = a.ts;
+    ET* tile = reinterpret_cast<ET*>(tsm) + wave * KG * 16;   // wave-private transpose tile (tile waves only)
+    if (b < tb) {
+        constexpr int per = TB_THREADS / 256;
+        if (b < a.ob_wgs) {
+            const int grp = b * per + tid / 256;
+            if constexpr (NQ > 1) out_back_n<PREC, NQ, true>(a.ob, grp, grp < a.ob_groups, tid % 256, tsm + (tid / 256) * OB_RED);
+        } else {
+            const int grp = (b - a.ob_wgs) * per + tid / 256;
+            if (grp < a.l2_groups) l2_back_n<PREC, NQ, true>(a.l2b, grp, tid % 256);
+        }
+        // every thread's loads of the old parameters have returned (their FMAs ran) and its write-through
+        // gradient stores have completed
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (b == tb) {
+        copy_metrics(met, met_out, nmet, tag);
+        time_bwd_body(a.gseg, p, g, a.F, a.XD, a.TD, a.H, a.KF, a.TS, a.stage_g, tsm, [&] {
+            if (tid == 0) __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        });
+        __syncthreads();   // the backward's gradient stores, read back below by other threads
+        auto step_fp32 = [&](int64_t i, float* dst) {
+            float pi = p[i], mi = m[i], vi = v[i];
+            const float gi = g[i];
+            if (t.clear_grads) g[i] = 0.f;
+            adamw_elem(pi, mi, vi, gi, h);
+            p[i] = pi; m[i] = mi; v[i] = vi;
+            *dst = pi;
+        };
+        for (int64_t i = (int64_t)a.F.time_w1 + tid; i < (int64_t)a.F.in_w; i += TB_THREADS)
+            step_fp32(i, a.time_dst + (i - (int64_t)a.F.time_w1));
+        tail_wait(a.arrive, need);   // b_in: read old by every out_back group
+        for (int n = tid; n < a.H; n += TB_THREADS) step_fp32((int64_t)a.F.in_b + n, a.inb_dst + n);
+    } else {
+        const int gw = (b - tb - 1) * WPB + wave;
+        if (gw < t.mstart[t.nmat]) {
+            int mi = 0;
+            while (gw >= t.mstart[mi + 1]) ++mi;
+            const bool virt = vt.on && mi == a.l2_mat;
+            const bool wait = mi == a.in_mat || mi == a.l2_mat;
+            // W_l2's materialised gradient (l2_back's write-through stores in this launch): read after
+            // every arrival, through agent-scope loads
+            const bool l2m = !vt.on && a.l2_groups > 0 && mi == a.l2_mat;
+            if (l2m) tail_wait(a.arrive, need);
+            tail_block<ET, KG, EPL, PREC, NQ>(p, g, m, v, h, vt, a, t.mat[mi], gw - t.mstart[mi], tile, lane, virt, l2m,
+                                              wait && !l2m, need);
+        } else {
+            const int64_t e = (int64_t)(gw - t.mstart[t.nmat]) * 64 + lane;
+            if (e < t.cstart[t.ncpy]) {
+                int c = 0;
+                while (e >= t.cstart[c + 1]) ++c;
+                const int64_t local = e - t.cstart[c], i = t.cpy[c].lo + local;
+                const bool l2b = in_range(i, a.l2bias);
+                const bool l2m = l2b && !vt.on && a.l2_groups > 0;   // db_l2 from l2_back's workgroup 0
+                if (l2m) tail_wait(a.arrive, need);
+                float pi = p[i], mi = m[i], vi = v[i];
+                const float gi = (vt.on && l2b) ? l2_virtual_grad(g, vt, i)
+                               : l2m ? __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : g[i];
+                if (t.clear_grads && !in_range(i, t.keep[0]) && !in_range(i, t.keep[1])) g[i] = 0.f;
+                adamw_elem(pi, mi, vi, gi, h);
+                if (l2b && !l2m) tail_wait(a.arrive, need);
+                p[i] = pi; m[i] = mi; v[i] = vi;
+                t.cpy[c].dst[local] = pi;
+            }
+        }
+    }
+    if (!last_workgroup(t.ticket)) return;
+    if (t.last_mat >= 0) {
+        const TileMat& M = t.mat[t.last_mat];
+        const int nblk = M.nb * M.KS;
+        for (int bb = wave; bb < nblk; bb += WPB)
+            tail_block<ET, KG, EPL, PREC, NQ>(p, g, m, v, h, vt, a, M, bb, tile, lane, false, true, false, need);
+        __syncthreads();
+    }
+    if (t.clear_grads)
+        for (int r = 0; r < 2; ++r)
+            for (int64_t i = t.keep[r][0] + tid; i < t.keep[r][1]; i += TB_THREADS) g[i] = 0.f;
+    clear_words(t.clr, t.clr_words);
+    if (tid == 0) __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // per (device, stream): a zeroed ticket counter block of the fused steps, created on first use
 // (launches on one stream are ordered, so they share it; the critic's step on the side stream has its
 // own). One process-wide table under a mutex, keyed by the stream's own device.
@@ -1378,6 +1523,18 @@ static int step_ticket(hipStream_t s, unsigned** out) {
     return DPPO_OK;
 }
 
+// the (precision, width) instantiations of the actor tail
+template <class ET, int KG, int EPL, int PREC>
+static const void* actor_tail_fn_p(int nq) {
+    return nq == 12 ? (const void*)actor_tail_kernel<ET, KG, EPL, PREC, 12>
+         : nq == 24 ? (const void*)actor_tail_kernel<ET, KG, EPL, PREC, 24>
+                    : (const void*)actor_tail_kernel<ET, KG, EPL, PREC, L2B_MAXN>;
+}
+static const void* actor_tail_fn(int prec, int nq) {
+    return prec == DPPO_BF16 ? actor_tail_fn_p<__bf16, 32, 8, DPPO_BF16>(nq)
+         : prec == DPPO_F16 ? actor_tail_fn_p<_Float16, 32, 8, DPPO_F16>(nq) : actor_tail_fn_p<float, 16, 4, DPPO_F32>(nq);
+}
+
 static int launch_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
                         float weight_decay, float beta1, float beta2, float eps, int mode, const double* met,
                         double* met_out, int nmet, uint64_t tag, hipStream_t s, const L2Virt& vt = L2Virt{}) {
@@ -1410,7 +1567,8 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
                                float eps, int mode, const float* actor_params, void* packed_actor,
                                const float* critic_params, void* packed_critic, const double* metrics,
                                double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
-                               const size_t* clear_bytes, int n_clear, void* stream, const float* gseg = nullptr) {
+                               const size_t* clear_bytes, int n_clear, void* stream, const float* gseg = nullptr,
+                               const float* pa0 = nullptr, const float* pl2 = nullptr) {
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
@@ -1449,7 +1607,7 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
                     (const uint8_t*)packed_actor + L.off[SEG_W_OUT]};
     }
     // the one-launch form: a single network whose parameters are exactly the range. The actor's
-    // (actor_step_kernel) leaves its TEMB table and split-sampler tables to their consumers (the row
+    // (actor_tile_step_kernel / actor_tail_kernel) leaves its TEMB table and split-sampler tables to the fold launch (the row
     // tiles derive the time embeddings, the sampler re-derives the tables before its next launch)
     const bool one_actor = packed_actor && !packed_critic && actor_params == params && n == (int64_t)FA.count;
     const bool one_critic = packed_critic && !packed_actor && critic_params == params && n == (int64_t)FC.count;
@@ -1490,8 +1648,7 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
             DPPO_HIP(hipGetLastError());
             return DPPO_OK;
         }
-        static const bool tile_on = [] { const char* e = getenv("DPPO_ACTOR_TILE_STEP"); return !e || atoi(e) != 0; }();
-        if (!gseg && tile_on) {
+        if (!gseg) {
             FuseJob jobs[FUSE_MAXJ];
             const int nj = dppo_fuse_jobs(D.IN, D.H, D.XD, D.TD, precision, packed_actor, D.K, jobs);
             DPPO_CHECK(nj >= 0, "dppo_optimizer_step: fused pack jobs");
@@ -1555,56 +1712,99 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
             if (rc) return rc;
             return dppo_mark_tables_stale(D, precision, actor_params, packed_actor, true);
         }
-        ActorStep a = {};
-        a.njobs = dppo_fuse_jobs(D.IN, D.H, D.XD, D.TD, precision, packed_actor, D.K, a.j);
-        DPPO_CHECK(a.njobs >= 0, "dppo_optimizer_step: fused pack jobs");
-        a.own0[0][0] = (int64_t)FA.time_w1; a.own0[0][1] = (int64_t)FA.in_w;
-        a.own0[1][0] = (int64_t)(FA.in_w + (size_t)D.XD * D.H); a.own0[1][1] = (int64_t)(FA.in_w + (size_t)(D.XD + D.TD) * D.H);
-        a.own0[2][0] = (int64_t)FA.in_b; a.own0[2][1] = (int64_t)(FA.in_b + D.H);
-        // W_out last only when the l2 elements' virtual gradient reads its image slots
-        a.wout[0] = a.wout[1] = -1;
-        if (l2v) { a.wout[0] = (int64_t)FA.out_w; a.wout[1] = (int64_t)(FA.out_w + (size_t)D.H * D.XD); }
-        for (int r = 0; r < 2; ++r) a.keep[r][0] = a.keep[r][1] = -1;
-        if (l2v) {   // read by every l2 element's virtual gradient: zeroed by the last workgroup
-            a.keep[0][0] = (int64_t)FA.l2_w; a.keep[0][1] = (int64_t)(FA.l2_w + (size_t)D.H * D.XD);
-            a.keep[1][0] = (int64_t)FA.out_b; a.keep[1][1] = (int64_t)(FA.out_b + D.XD);
+        // with the time-MLP backward: the actor's whole tail in one launch (actor_tail_kernel)
+        FuseJob jobs[FUSE_MAXJ];
+        const int nj = dppo_fuse_jobs(D.IN, D.H, D.XD, D.TD, precision, packed_actor, D.K, jobs);
+        DPPO_CHECK(nj >= 0, "dppo_actor_step: fused pack jobs");
+
+        ActorTail a = {};
+        TileStep& t = a.ts;
+        t.last_mat = -1;
+        a.in_mat = a.l2_mat = a.out_mat = -1;
+        for (int q = 0; q < nj; ++q) {
+            const FuseJob& J = jobs[q];
+            if (J.kind == 0) {
+                DPPO_CHECK(t.nmat < TILE_MAXM, "actor tail: too many weight tensors");
+                TileMat& M = t.mat[t.nmat];
+                M.off = J.lo; M.K = J.IK; M.N = J.IN; M.KS = J.KS; M.img = J.dst; M.timg = nullptr; M.KST = 0;
+                M.nb = dppo_cdiv(M.N, 16);
+                if (J.lo == (int64_t)FA.in_w) a.in_mat = t.nmat;
+                if (J.lo == (int64_t)FA.l2_w) a.l2_mat = t.nmat;
+                if (J.lo == (int64_t)FA.out_w) {   // the last workgroup: its gradient is out_back's, in this launch
+                    a.out_mat = t.nmat;
+                    t.last_mat = t.nmat;
+                }
+                ++t.nmat;
+            } else if (J.kind == 2) {
+                if (J.lo == (int64_t)FA.time_w1) { a.time_dst = (float*)J.dst; continue; }   // the backward's workgroup
+                if (J.lo == (int64_t)FA.in_b) { a.inb_dst = (float*)J.dst; continue; }
+                DPPO_CHECK(t.ncpy < TILE_MAXC, "actor tail: too many fp32 tensors");
+                t.cpy[t.ncpy++] = TileCpy{J.lo, J.hi - J.lo, (float*)J.dst};
+            }
         }
-        a.clear_grads = clear_g ? 1 : 0;
+        for (int q = 0; q < nj; ++q) {
+            const FuseJob& J = jobs[q];
+            if (J.kind != 1) continue;
+            int mi = 0;
+            while (mi < t.nmat && t.mat[mi].off != J.lo) ++mi;
+            DPPO_CHECK(mi < t.nmat && J.IK == t.mat[mi].N && J.IN == t.mat[mi].K, "actor tail: transposed image");
+            t.mat[mi].timg = J.dst; t.mat[mi].KST = J.KS;
+        }
+        DPPO_CHECK(a.time_dst && a.inb_dst && a.in_mat >= 0 && a.l2_mat >= 0, "actor tail: image segments");
+        for (int r = 0; r < 2; ++r) t.keep[r][0] = t.keep[r][1] = -1;
+        // db_out: read by out_back and by l2's gradient (l2_back's db_l2, or every l2 element's virtual one),
+        // zeroed by the last workgroup; under the virtual l2 also pl2 in the l2 region of the gradients
+        t.keep[1][0] = (int64_t)FA.out_b; t.keep[1][1] = (int64_t)(FA.out_b + D.XD);
+        if (l2v) { t.keep[0][0] = (int64_t)FA.l2_w; t.keep[0][1] = (int64_t)(FA.l2_w + (size_t)D.H * D.XD); }
+        a.l2bias[0] = (int64_t)FA.l2_b; a.l2bias[1] = (int64_t)(FA.l2_b + D.H);
+        t.mstart[0] = 0;
+        for (int mi = 0; mi < t.nmat; ++mi)
+            t.mstart[mi + 1] = t.mstart[mi] + (mi == t.last_mat ? 0 : t.mat[mi].nb * t.mat[mi].KS);
+        t.cstart[0] = 0;
+        for (int c = 0; c < t.ncpy; ++c) t.cstart[c + 1] = t.cstart[c] + t.cpy[c].n;
+        t.clear_grads = clear_g ? 1 : 0;
+        for (int r = 0; r < n_clear; ++r) { t.clr[r] = clear_ptrs[r]; t.clr_words[r] = (uint32_t)(clear_bytes[r] / 4); }
+        rc = step_ticket(s, &t.ticket);
+        if (rc) return rc;
+        a.arrive = t.ticket + 192;   // 768 B into the ticket block: the arrival counter
+        // W_out's gradient (out_back) from the old parameters: here under the virtual l2 (the minibatch
+        // launched nothing after its dW); otherwise the minibatch's l2_back launch materialised it
+        DPPO_CHECK(D.IN <= 256 && D.H % 4 == 0, "out_back: in_dim %d > 256", D.IN);
+        const int nq = l2_nq(D.XD);
+        DPPO_CHECK(pa0 && pl2, "dppo_actor_step: the workspace's pa0 / pl2 (W_out's and l2's gradients) are needed");
+        // W_out's gradient (out_back) from the old parameters, and l2's: virtual (pl2 in the l2 region of the
+        // gradients, formed per element) or materialised by l2_back groups from the workspace's pl2
+        a.ob = make_out_back(D, precision, actor_params, l2v ? grads + FA.l2_w : pl2, pa0, grads);
+        a.ob_groups = dppo_cdiv(D.H, ob_rows(nq));
+        a.ob_wgs = dppo_cdiv(a.ob_groups, TB_THREADS / 256);
+        if (!l2v) {
+            DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
+            const MlpLayout LA = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
+            a.l2b = L2Back{pl2, grads + FA.out_b, (const uint8_t*)packed_actor + LA.off[SEG_W_OUT], grads + FA.l2_w,
+                           grads + FA.l2_b, D.H, D.XD, precision, nullptr, nullptr, nullptr};
+            a.l2_groups = dppo_cdiv(D.H, L2B_ROWS);
+            a.l2_wgs = dppo_cdiv(a.l2_groups, TB_THREADS / 256);
+        }
         a.gseg = gseg;
         a.F = FA; a.XD = D.XD; a.TD = D.TD; a.H = D.H; a.KF = D.KF; a.TS = D.TS;
-        size_t lds = 0;
-        if (gseg) {
-            lds = time_bwd_lds(D, D.KF, &a.stage_g);
-            DPPO_CHECK(lds <= 160 * 1024, "dppo_actor_step: time-MLP backward LDS %zu B exceeds 160 KB", lds);
-        }
-        for (int r = 0; r < n_clear; ++r) { a.clr[r] = clear_ptrs[r]; a.clr_words[r] = (uint32_t)(clear_bytes[r] / 4); }
-        rc = step_ticket(s, &a.ticket);
+        size_t lds = time_bwd_lds(D, D.KF, &a.stage_g);
+        const size_t tile_lds = (size_t)(TB_THREADS / 64) * 16 * 64;   // a wave's KG x 16 transpose tile: 64 B per row
+        const size_t ob_lds = sizeof(float) * OB_RED * (TB_THREADS / 256);
+        if (lds < tile_lds) lds = tile_lds;
+        if (lds < ob_lds) lds = ob_lds;
+        DPPO_CHECK(lds <= 160 * 1024, "dppo_actor_step: tail LDS %zu B exceeds 160 KB", lds);
+        const int64_t waves = t.mstart[t.nmat] + (t.cstart[t.ncpy] + 63) / 64;
+        const unsigned blocks = (unsigned)(a.ob_wgs + a.l2_wgs + 1 + (waves + TB_THREADS / 64 - 1) / (TB_THREADS / 64));
+        const void* fn = actor_tail_fn(precision, nq);
+        rc = dppo_func_lds(fn, lds);
         if (rc) return rc;
-        // about one element per thread (two workgroups per CU at most: every workgroup gets the time-MLP
-        // backward's LDS): workgroup 0's backward (~10 us of dependent phases) runs beside the other
-        // workgroups' AdamW. (r05: one workgroup per CU, two elements per thread, took 32 us alone
-        // against 16 us for AdamW + pack; tools/bench_step.py)
-        const int cus = dw_device_cus();
-        const int64_t want = 1 + (n + ACTOR_STEP_THREADS - 1) / ACTOR_STEP_THREADS;
-        const unsigned blocks = (unsigned)(want < 2 * (int64_t)cus ? (want > 2 ? want : 2) : 2 * (int64_t)cus);
-        if (lds > 64 * 1024) {
-            const void* fn = precision == DPPO_BF16 ? (const void*)actor_step_kernel<__bf16, 32, 8>
-                           : precision == DPPO_F16 ? (const void*)actor_step_kernel<_Float16, 32, 8>
-                                                    : (const void*)actor_step_kernel<float, 16, 4>;
-            rc = dppo_func_lds(fn, lds);
-            if (rc) return rc;
-        }
         {
             DppoKtScope kt(KT_ADAMW, s);
-            if (precision == DPPO_BF16)
-                hipLaunchKernelGGL((actor_step_kernel<__bf16, 32, 8>), dim3(blocks), dim3(ACTOR_STEP_THREADS), lds, s,
-                                   params, grads, m, v, n, h, metrics, mout, n_metrics, metrics_tag, vt, a);
-            else if (precision == DPPO_F16)
-                hipLaunchKernelGGL((actor_step_kernel<_Float16, 32, 8>), dim3(blocks), dim3(ACTOR_STEP_THREADS), lds, s,
-                                   params, grads, m, v, n, h, metrics, mout, n_metrics, metrics_tag, vt, a);
-            else
-                hipLaunchKernelGGL((actor_step_kernel<float, 16, 4>), dim3(blocks), dim3(ACTOR_STEP_THREADS), lds, s,
-                                   params, grads, m, v, n, h, metrics, mout, n_metrics, metrics_tag, vt, a);
+            AdamHP hh = h;
+            L2Virt vv = vt;
+            void* args[] = {(void*)&params, (void*)&grads, (void*)&m, (void*)&v, (void*)&hh, (void*)&metrics, (void*)&mout,
+                            (void*)&n_metrics, (void*)&metrics_tag, (void*)&vv, (void*)&a};
+            DPPO_HIP(hipLaunchKernel(fn, dim3(blocks), dim3(TB_THREADS), args, lds, s));
         }
         DPPO_HIP(hipGetLastError());
         // the row tiles' fold needs every element final: its own small launch (pack.hip PACK_RT_FOLD)
@@ -1666,7 +1866,7 @@ extern "C" int dppo_optimizer_step_ex(const dppo_dims* d, int precision, float* 
                                n_metrics, metrics_tag, clear_ptrs, clear_bytes, n_clear, stream);
 }
 
-// ABI 12: the actor's optimizer step in one launch (actor_step_kernel); with a workspace it also
+// ABI 12: the actor's optimizer step (actor_tile_step_kernel); with a workspace (r06: actor_tail_kernel) it also
 // runs the time-MLP backward from that minibatch's bucket sums (DPPO_PPO_TIME_BWD_IN_STEP)
 extern "C" int dppo_actor_step(const dppo_dims* d, int precision, float* params, float* grads, float* m, float* v,
                                int64_t step, float lr, float weight_decay, float beta1, float beta2, float eps, int mode,
@@ -1683,11 +1883,18 @@ extern "C" int dppo_actor_step(const dppo_dims* d, int precision, float* params,
     DPPO_CHECK(!workspace || batch_rows > 0, "dppo_actor_step: a workspace needs its batch_rows");
     DPPO_CHECK(D.KF <= 16, "dppo_actor_step: ft_denoising_steps > 16 unsupported (bucket sums)");
     const float* gseg = nullptr;
-    if (workspace) gseg = make_ppo_workspace(D, precision, batch_rows, (uint8_t*)const_cast<void*>(workspace)).gseg;
+    const float* pa0 = nullptr;
+    const float* pl2 = nullptr;
+    if (workspace) {
+        const PpoWorkspace ws = make_ppo_workspace(D, precision, batch_rows, (uint8_t*)const_cast<void*>(workspace));
+        gseg = ws.gseg;
+        pa0 = ws.pa0;
+        pl2 = ws.pl2;
+    }
     const int64_t n = (int64_t)make_flat_offsets(D.IN, D.H, D.XD, D.TD).count;
     return optimizer_step_impl(d, precision, params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps,
                                mode | DPPO_STEP_FUSED_PACK, params, packed_actor, nullptr, nullptr, metrics, metrics_out,
-                               n_metrics, metrics_tag, clear_ptrs, clear_bytes, n_clear, stream, gseg);
+                               n_metrics, metrics_tag, clear_ptrs, clear_bytes, n_clear, stream, gseg, pa0, pl2);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1871,11 +2078,6 @@ static SideStream* side_stream(int which = 0) {
 // the actor's l2 weight gradient from pl2 (l2_back_kernel: no LDS, so it starts on any CU with a
 // free wave slot), then the time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg)
 // the actor's out_back (dW_out through the folded forward) over the pl2 / pa0 sums of the dW launch
-static OutBack make_out_back(const Dims& D, int precision, const float* actor_params, const float* pl2, const float* pa0,
-                             float* ga) {
-    const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
-    return OutBack{actor_params, FA, pl2, pa0, ga + FA.out_b, ga + FA.out_w, D.H, D.IN, D.XD, precision};
-}
 
 // after the actor's dW: the time-MLP backward over nb buckets at t = q * TS (the bucket sums in gseg),
 // W_out's gradient (out_back) and, unless the l2 gradient stays factored, l2's from pl2, in one launch
@@ -2033,6 +2235,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     const float gscale = dppo_grad_scale_rows(precision, hp->global_rows);
     lh.grad_scale = hp->loss_scale / (float)hp->global_rows * gscale;
     lh.eta_unscale = (hp->flags & DPPO_PPO_LEARN_ETA) ? 1.f / gscale : 0.f;
+    lh.clip_vloss = hp->clip_vloss_coef > 0.f && hp->old_values ? hp->clip_vloss_coef : 0.f;
+    lh.old_values = lh.clip_vloss > 0.f ? hp->old_values : nullptr;
     // the actor's l2 gradient left factored in its own grads region (include/dppo.h)
     const bool l2_def = (hp->flags & DPPO_PPO_L2_DEFERRED) != 0;
 
@@ -2155,17 +2359,8 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         if (!(hp->flags & DPPO_PPO_TIME_BWD_IN_STEP) && !tbf)
             return launch_time_bwd(D, precision, ws.gseg, pl2_src, ws.pa0, packed_ft, actor_params, ga, D.KF, D.TS, s,
                                    !l2_def);
-        // the caller's actor step runs the time-MLP backward: W_out's gradient (and l2's unless it
-        // stays factored) here, before that step reads them
-        const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
-        L2Back l2b = {ws.pl2, ga + FA.out_b, (const uint8_t*)packed_ft + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b,
-                      D.H, D.XD, precision, nullptr, nullptr, nullptr};
-        DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
-        const int l2g = l2_def ? 0 : dppo_cdiv(D.H, L2B_ROWS), obg = dppo_cdiv(D.H, ob_rows(l2_nq(D.XD)));
-        DppoKtScope kt(KT_L2_BACK, s);
-        launch_l2_back(precision, (unsigned)(l2g > obg ? l2g : obg), s, l2b, l2g,
-                       make_out_back(D, precision, actor_params, pl2_src, ws.pa0, ga), obg);
-        DPPO_HIP(hipGetLastError());
+        // the caller's actor step (dppo_actor_step: actor_tail_kernel) runs the time-MLP backward and forms
+        // W_out's and l2's gradients itself: nothing follows the dW here
         if (tbf) DPPO_HIP(hipStreamWaitEvent(s, tbf->join, 0));
         return DPPO_OK;
     };

@@ -20,8 +20,6 @@ class PPODiffusion(VPGDiffusion):
                  clip_vloss_coef=None, clip_advantage_lower_quantile=0, clip_advantage_upper_quantile=1, norm_adv=True,
                  vf_coef=0.5, **kwargs):
         super().__init__(**kwargs)
-        if clip_vloss_coef is not None:
-            raise NotImplementedError("clip_vloss_coef (None in every cfg) is not implemented in the fused loss")
         self.gamma_denoising = gamma_denoising
         self.clip_ploss_coef = clip_ploss_coef
         self.clip_ploss_coef_base = clip_ploss_coef_base
@@ -34,11 +32,14 @@ class PPODiffusion(VPGDiffusion):
         self.metrics = torch.zeros(16, dtype=torch.float64, device=self.device)
         self._ws = {}
 
-    def hparams(self, global_rows, reward_horizon=4, loss_scale=1.0, l2_deferred=False):
+    def hparams(self, global_rows, reward_horizon=4, loss_scale=1.0, l2_deferred=False, old_values=None):
+        """old_values: the rollout's value pass (fp32 [S*E] by sample), read by the clipped value loss when
+        clip_vloss_coef is set (diffusion_ppo.py:110-116)."""
         return ops.ppo_hparams(self.gamma_denoising, self.clip_ploss_coef, self.clip_ploss_coef_base,
                                self.clip_ploss_coef_rate, self.min_logprob_denoising_std, self.vf_coef, self.norm_adv,
                                reward_horizon, loss_scale, global_rows, l2_deferred=l2_deferred,
-                               learn_eta=self.learn_eta)
+                               learn_eta=self.learn_eta, clip_vloss_coef=self.clip_vloss_coef,
+                               old_values=old_values if self.clip_vloss_coef is not None else None)
 
     def workspace(self, rows):
         ws = self._ws.get(rows)
@@ -48,19 +49,19 @@ class PPODiffusion(VPGDiffusion):
 
     def minibatch(self, obs, chains, lp_old_mean, advantages, returns, perm_seed, epoch, start, rows,
                   global_rows=None, reward_horizon=4, loss_scale=1.0, adv_stats=None, row_index=None, part=None,
-                  metrics=None):
+                  metrics=None, old_values=None):
         """One fused PPO minibatch over HBM rollout buffers (obs [N,SD], chains [N,K'+1,XD],
         lp_old_mean [N,K'], advantages/returns [N]); writes self.grads and self.metrics (sums).
         part = 1 / 2 runs only the actor / critic half on the current stream (metrics: an
         alternative fp64[16] buffer)."""
-        hp = self.hparams(global_rows or rows, reward_horizon, loss_scale)
+        hp = self.hparams(global_rows or rows, reward_horizon, loss_scale, old_values=old_values)
         ops.ppo_minibatch(self.dims, self.precision, hp, self.packed_ft, self.packed_critic, self.actor_ft_params,
                           self.sched, obs, chains, lp_old_mean, advantages, returns, perm_seed, epoch, start, rows,
                           self.workspace(rows), self.grads, self.metrics if metrics is None else metrics,
                           adv_stats=adv_stats, row_index=row_index, part=part)
 
     def bind_minibatch(self, obs, chains, lp_old_mean, advantages, returns, perm_seed, max_rows, reward_horizon=4,
-                       loss_scale=1.0, l2_deferred=False, time_bwd_in_step=False):
+                       loss_scale=1.0, l2_deferred=False, time_bwd_in_step=False, old_values=None):
         """minibatch() over fixed rollout buffers for a whole update phase, its arguments validated
         and marshalled once (ops.BoundMinibatch): returns f(epoch, start, rows, global_rows=None,
         adv_stats=None, part=None, metrics=None). Every minibatch uses the max_rows workspace.
@@ -78,7 +79,8 @@ class PPODiffusion(VPGDiffusion):
             g = int(global_rows or rows)
             hp = hps.get((g, precleared))
             if hp is None:
-                hp = hps[(g, precleared)] = self.hparams(g, reward_horizon, loss_scale, l2_deferred=l2_deferred)
+                hp = hps[(g, precleared)] = self.hparams(g, reward_horizon, loss_scale, l2_deferred=l2_deferred,
+                                                         old_values=old_values)
                 if precleared:
                     hp.flags |= _lib.DPPO_PPO_PRECLEARED
                 if time_bwd_in_step:
@@ -110,7 +112,11 @@ class PPODiffusion(VPGDiffusion):
         adv = torch.as_tensor(advantages, device=dev, dtype=torch.float32).reshape(b).contiguous()
         ret = torch.as_tensor(returns, device=dev, dtype=torch.float32).reshape(b).contiguous()
         row_index = (r * kf + j).contiguous()
-        self.minibatch(state, ch, lp_old, adv, ret, 0, 0, 0, b, reward_horizon=reward_horizon, row_index=row_index)
+        oldv = None
+        if self.clip_vloss_coef is not None:   # :110-116: sample n = row r of this batch
+            oldv = torch.as_tensor(oldvalues, device=dev, dtype=torch.float32).reshape(b).contiguous()
+        self.minibatch(state, ch, lp_old, adv, ret, 0, 0, 0, b, reward_horizon=reward_horizon, row_index=row_index,
+                       old_values=oldv)
         m = (self.metrics[:5] / b).cpu().numpy()
         eta = self.current_eta()
         # entropy_loss = -mean(eta), the last element mean(eta) (diffusion_ppo.py:49, 131); with

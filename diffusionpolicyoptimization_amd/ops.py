@@ -756,14 +756,22 @@ def ppo_adv_stats_all(advantages, total, kf, perm_seed, epoch0, n_epochs, rows_f
 
 def ppo_hparams(gamma_denoising=0.99, clip_ploss_coef=0.01, clip_ploss_coef_base=0.01, clip_ploss_coef_rate=3.0,
                 min_logprob_std=0.1, vf_coef=0.5, norm_adv=True, reward_horizon=4, loss_scale=1.0, global_rows=1,
-                l2_deferred=False, learn_eta=False):
+                l2_deferred=False, learn_eta=False, clip_vloss_coef=None, old_values=None):
     """l2_deferred (ABI 8, DPPO_PPO_L2_DEFERRED): the actor's l2 gradient is left factored in grads
     for an optimizer step with l2_from_pl2 (or materialize_l2). learn_eta (ABI 9,
-    DPPO_PPO_LEARN_ETA): the row tiles add d loss / d eta of a DDIM schedule into metrics[8]."""
+    DPPO_PPO_LEARN_ETA): the row tiles add d loss / d eta of a DDIM schedule into metrics[8].
+    clip_vloss_coef (ABI 14, diffusion_ppo.py:110-116): the clipped value loss against old_values, the
+    rollout's value pass (device fp32 [S*E], indexed by sample; the caller keeps it alive)."""
     flags = (_lib.DPPO_PPO_L2_DEFERRED if l2_deferred else 0) | (_lib.DPPO_PPO_LEARN_ETA if learn_eta else 0)
+    clip = clip_vloss_coef is not None
+    if clip and (old_values is None or old_values.dtype != torch.float32 or not old_values.is_cuda):
+        raise ValueError("clip_vloss_coef needs the rollout's old values (fp32 device tensor)")
+    if clip and not float(clip_vloss_coef) > 0:
+        raise ValueError("clip_vloss_coef must be > 0")
     return _lib.DppoPpoHparams(float(gamma_denoising), float(clip_ploss_coef), float(clip_ploss_coef_base),
                                float(clip_ploss_coef_rate), float(min_logprob_std), float(vf_coef), int(bool(norm_adv)),
-                               int(reward_horizon), float(loss_scale), int(global_rows), flags)
+                               int(reward_horizon), float(loss_scale), int(global_rows), flags,
+                               float(clip_vloss_coef) if clip else 0.0, old_values.data_ptr() if clip else None)
 
 
 def ddim_eta_base(schedule):

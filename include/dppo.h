@@ -311,6 +311,12 @@ typedef struct dppo_ppo_hparams {
     float loss_scale;       /* multiplies 1/b (= 1/world_size for a DP all-reduce-sum) */
     int32_t global_rows;    /* b used in the 1/b means (rows over all ranks) */
     int32_t flags;          /* ABI 8: DPPO_PPO_* below (0: every gradient materialised) */
+    /* ABI 14: the clipped value loss (diffusion_ppo.py:110-116) when clip_vloss_coef > 0:
+     * v_loss = 0.5 mean(max((V - R)^2, (V_old + clip(V - V_old, -c, c) - R)^2)) with V_old = old_values[n],
+     * the rollout's value pass (device fp32 [S*E]); clip_vloss_coef <= 0 (or old_values NULL): the plain
+     * 0.5 mean((V - R)^2) of :118 (every shipped cfg: clip_vloss_coef null) */
+    float clip_vloss_coef;
+    const float* old_values;
 } dppo_ppo_hparams;
 
 /* ABI 8, dppo_ppo_hparams.flags. DPPO_PPO_L2_DEFERRED: the actor's l2 gradient is left in its

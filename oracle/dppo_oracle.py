@@ -461,19 +461,19 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
         first = np.asarray(first)
         cw = np.asarray(mult, np.float64)
         obs, returns = obs[first], np.asarray(returns, np.float64)[first]
+        if oldvalues is not None:
+            oldvalues = np.asarray(oldvalues, np.float64)[first]
     v, ccache = critic_forward(pc, obs, rnd=rnd)
     v = v[:, 0]                                                   # :109
-    if cw is not None:
-        if clip_vloss_coef is not None:
-            raise NotImplementedError("critic_dedup with clip_vloss_coef")
-        v_loss = 0.5 * (cw * (v - returns) ** 2).sum() / D
-    elif clip_vloss_coef is not None:                             # :110-116
+    w_rows = cw if cw is not None else np.ones_like(v)
+    if clip_vloss_coef is not None:                               # :110-116
+        oldvalues = np.asarray(oldvalues, np.float64)
         vl_un = (v - returns) ** 2
         v_cl = oldvalues + np.clip(v - oldvalues, -clip_vloss_coef, clip_vloss_coef)
         vl_cl = (v_cl - returns) ** 2
-        v_loss = 0.5 * np.maximum(vl_un, vl_cl).mean()
+        v_loss = 0.5 * (w_rows * np.maximum(vl_un, vl_cl)).sum() / D
     else:
-        v_loss = 0.5 * ((v - returns) ** 2).sum() / D             # :118
+        v_loss = 0.5 * (w_rows * (v - returns) ** 2).sum() / D   # :118
     approx_kl = ((ratio - 1) - logratio).sum() / D                # :121
     clipfrac = (np.abs(ratio - 1.0) > cc).astype(np.float64).sum() / D
     metrics = dict(pg_loss=pg_loss, entropy_loss=-1.0, v_loss=v_loss, clipfrac=clipfrac,
@@ -496,8 +496,12 @@ def c_loss(p_ft, pc, sched, obs, chains_prev, chains_next, denoising_inds, retur
     xdim = chains_prev.shape[1] * chains_prev.shape[2]
     ga = diffusion_mlp_backward(p_ft, acache, deps, xdim)
     if clip_vloss_coef is not None:
-        raise NotImplementedError("clip_vloss_coef gradient (cfg default None)")
-    dv = vf_coef * (v - returns) / D
+        # tf.maximum's gradient to its first argument on ties; tf.clip_by_value's passes inside [-c, c]
+        d_old = v - oldvalues
+        inside = (d_old >= -clip_vloss_coef) & (d_old <= clip_vloss_coef)
+        dv = vf_coef * np.where(vl_un >= vl_cl, v - returns, np.where(inside, v_cl - returns, 0.0)) / D
+    else:
+        dv = vf_coef * (v - returns) / D
     if cw is not None:
         dv = dv * cw
     gc, _ = residual_mlp_backward(pc, ccache, dv[:, None], "Mish", "")

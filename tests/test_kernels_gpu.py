@@ -55,7 +55,11 @@ def test_sampler_injected_noise(cuda, precision, tol, dims):
     xT = rng.standard_normal((E, d.horizon_steps, d.action_dim)).astype(np.float32)
     z = rng.standard_normal((d.denoising_steps, E, d.horizon_steps, d.action_dim)).astype(np.float32)
     split = ops.sampler_layout(d, precision, E) > 0
-    assert split == (precision != "fp32"), "bf16 / fp16 at 37 envs run the split sampler by default"
+    # bf16 / fp16 at 37 envs run the split sampler by default; fp32 too at hopper's width (r06: the folded
+    # kernel at P = 4, fp32 operands), walker2d's fp32 streams the weights
+    assert split == (precision != "fp32" or d.xd == 12), (precision, d.xd)
+    if split and precision == "fp32":
+        assert ops.sampler_plan(d, precision, E)["members"] == 4
     ref_a, ref_c = O.sample(to_f64(base), to_f64(ft), sched, state.astype(np.float64), xT, z, d.ft_denoising_steps,
                             rnd=_rnd(precision), round_h3=not split)
     packb, packf = ops.pack_actor(d, pb, precision), ops.pack_actor(d, pf, precision)
@@ -774,6 +778,82 @@ def test_actor_step_runs_the_time_mlp_backward(cuda, precision):
                 assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp32", "fp16"])
+def test_actor_tail_step_matches_materialised_step(cuda, precision):
+    """r06: with the l2 gradient factored (DPPO_PPO_L2_DEFERRED) and the time-MLP backward in the step
+    (DPPO_PPO_TIME_BWD_IN_STEP), the minibatch stops after its dW and ONE launch (actor_tail_kernel) forms
+    W_out's gradient (out_back), the time-MLP and b_in gradients, l2's per element, and steps every actor
+    parameter with its image slots. Against the launch-per-stage reference on the SAME minibatch run:
+    the gradients the launch left (W_out, time MLP, b_in), with l2's materialised from its factored form
+    (dppo_materialize_l2), stepped by plain AdamW and fully packed give bit-identical parameters, moments
+    and image bytes; the time-MLP gradients equal those of the plain minibatch's own time_bwd (1e-5: the
+    two minibatch runs differ by float-atomic order); with clear_grads every actor gradient is zero."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.config import instantiate, load_config
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp_64env",
+                      [f"model.precision={precision}"])
+    m = instantiate(cfg.model, device=cuda, seed=0)
+    d = m.dims
+    N, kf, rows = 64 * 40, d.ft_denoising_steps, 3000
+    gen = torch.Generator(device=cuda).manual_seed(0)
+    obs = torch.rand(N, d.sd, device=cuda, generator=gen) * 2 - 1
+    chains = torch.randn(N, kf + 1, d.xd, device=cuda, generator=gen) * 0.5
+    adv = torch.randn(N, device=cuda, generator=gen)
+    ret = torch.randn(N, device=cuda, generator=gen)
+    lp_old = torch.empty(N, kf, device=cuda)
+    ops.logprob(d, m.precision, m.packed_ft, m.sched, obs, chains, want_elem=False, lp_mean=lp_old)
+    lp_old += 0.01 * torch.randn(N, kf, device=cuda, generator=gen)
+    na = m.n_actor
+    f = m.bind_minibatch(obs, chains, lp_old, adv, ret, 11, rows)
+    f(3, 0, rows)
+    torch.cuda.synchronize()
+    g_ref = m.grads[:na].clone()                       # the plain minibatch (time_bwd + out_back in it)
+    m.grads.zero_()
+    f = m.bind_minibatch(obs, chains, lp_old, adv, ret, 11, rows, l2_deferred=True, time_bwd_in_step=True)
+    f(3, 0, rows)
+    torch.cuda.synchronize()
+    offs, o = {}, 0
+    for name, shape in ops.actor_param_spec(d):
+        offs[name] = (o, o + int(np.prod(shape)))
+        o += offs[name][1] - offs[name][0]
+    g_in = m.grads.clone()
+    P0, img0 = m.actor_ft_params.clone(), m.packed_ft.clone()
+    gen2 = torch.Generator(device=cuda).manual_seed(1)
+    M0 = torch.rand(na, device=cuda, generator=gen2) * 1e-4
+    V0 = torch.rand(na, device=cuda, generator=gen2) * 1e-7
+    ws = m.workspace(rows)
+    ref = None
+    for clear in (False, True):
+        P, M, V, img, G = P0.clone(), M0.clone(), V0.clone(), img0.clone(), g_in.clone()
+        step = ops.BoundActorStep(d, m.precision, P, G[:na], M, V, 0.004, 0.9, 0.999, 1e-7, "keras", img,
+                                  workspace=ws, batch_rows=rows, l2_from_pl2=True, clear_grads=clear)
+        step(2, 1e-3)
+        torch.cuda.synchronize()
+        if not clear:
+            for k in ("time_w1", "time_b1", "time_w2", "time_b2", "in_b", "out_w"):
+                lo, hi = offs[k]
+                a, b = G[lo:hi], g_ref[lo:hi]
+                assert (a - b).abs().max() <= 1e-5 * b.abs().max() + 1e-12, (k, float((a - b).abs().max()))
+            g_formed = G.clone()
+            ops.materialize_l2(d, m.precision, img0, g_formed, ws, rows)
+            Pb, Mb, Vb = P0.clone(), M0.clone(), V0.clone()
+            ops.adamw(Pb, g_formed[:na], Mb, Vb, 2, 1e-3, 0.004, 0.9, 0.999, 1e-7, "keras")
+            full = img0.clone()
+            ops.pack_actor(d, Pb, m.precision, out=full)
+            ops.refresh_sampler_tables(img)
+            torch.cuda.synchronize()
+            assert torch.equal(P, Pb) and torch.equal(M, Mb) and torch.equal(V, Vb)
+            assert torch.equal(img, full)
+            ref = (P, M, V, img)
+        else:
+            assert int(torch.count_nonzero(G[:na])) == 0
+            ops.refresh_sampler_tables(img)
+            torch.cuda.synchronize()
+            for a, b in zip((P, M, V, img), ref):
+                assert torch.equal(a, b)
+
+
 def test_value_moments(cuda):
     import torch
     from diffusionpolicyoptimization_amd import ops
@@ -799,7 +879,8 @@ def _dedup(bi):
                                                   ("fp32", "perturbed-ddim", 2e-3), ("fp32", "perturbed-walker", 2e-3),
                                                   ("bf16", "ratio1-walker", 1e-2), ("fp16", "ratio1", 1e-2),
                                                   ("fp16", "ratio1-ddim", 1e-2), ("fp32", "perturbed-narrow", 2e-3),
-                                                  ("bf16", "ratio1-narrow", 1e-2)])
+                                                  ("bf16", "ratio1-narrow", 1e-2), ("fp32", "perturbed-clipv", 2e-3),
+                                                  ("bf16", "ratio1-clipv", 1e-2)])
 def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     """c_loss forward metrics and gradients of pg_loss + 0.5 v_loss vs the oracle.
 
@@ -813,6 +894,9 @@ def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     from diffusionpolicyoptimization_amd import ops
     # DDIM: time-MLP gradient at t = 2j; walker: XD = 24 through the 32-row actor tile; narrow: XD = 8,
     # a width with no instantiation of its own (W_out's gradient through the generic out_back groups)
+    # clipv: the clipped value loss (diffusion_ppo.py:110-116, clip_vloss_coef = 0.2) against old values
+    # V(obs) + U(-0.4, 0.4), so both of tf.maximum's branches and both sides of the clip occur
+    clipv = case.endswith("-clipv")
     dims = {"ddim": HOPPER_DDIM, "walker": WALKER, "narrow": NARROW}.get(case.split("-")[-1], HOPPER)
     case = case.split("-")[0]
     d, base, ft, critic, sched, tab, pb, pf, pc = _setup(dims, cuda)
@@ -840,17 +924,23 @@ def test_ppo_minibatch_grads(cuda, precision, case, rtol):
     seed, epoch, start, rows = 99, 1, 37, 150
     perm = PX.feistel_permute(np.arange(start, start + rows), total, seed, epoch)
     bi, di = perm // kf, perm % kf
+    oldv, cv = None, None
+    if clipv:
+        v_now = O.critic_forward(to_f64(critic), obs.reshape(N, 1, -1).astype(np.float64), rnd=_rnd(precision))[0][:, 0]
+        oldv = (v_now + rng.uniform(-0.4, 0.4, N)).astype(np.float32)
+        cv = 0.2
     metrics_ref, ga_ref, gc_ref = O.c_loss(
         to_f64(ft), to_f64(critic), sched, obs[bi].reshape(rows, 1, -1).astype(np.float64),
         chains[bi, di].reshape(rows, d.horizon_steps, d.action_dim).astype(np.float64), chains[bi, di + 1].reshape(rows, d.horizon_steps, d.action_dim).astype(np.float64),
-        di, ret[bi].astype(np.float64), None, adv[bi].astype(np.float64), lp_old_ref[bi, di], kf,
-        rnd=_rnd(precision), critic_dedup=_dedup(bi))
+        di, ret[bi].astype(np.float64), None if oldv is None else oldv[bi].astype(np.float64), adv[bi].astype(np.float64),
+        lp_old_ref[bi, di], kf, rnd=_rnd(precision), critic_dedup=_dedup(bi), clip_vloss_coef=cv)
     na = ops.spec_count(ops.actor_param_spec(d))
     nc = ops.spec_count(ops.critic_param_spec(d))
     grads = torch.zeros(na + nc, dtype=torch.float32, device=cuda)
     metrics = torch.zeros(16, dtype=torch.float64, device=cuda)
     ws = ops.ppo_workspace(d, precision, rows, cuda)
-    hp = ops.ppo_hparams(global_rows=rows)
+    oldv_dev = T(oldv) if clipv else None
+    hp = ops.ppo_hparams(global_rows=rows, clip_vloss_coef=cv, old_values=oldv_dev)
     ops.ppo_minibatch(d, precision, hp, packf, ops.pack_critic(d, pc, precision), pf, tab,
                       T(obs), T(chains), T(lp_old_gpu), T(adv), T(ret), seed, epoch, start, rows, ws, grads, metrics)
     torch.cuda.synchronize()

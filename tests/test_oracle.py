@@ -108,7 +108,7 @@ def test_gae_against_direct_loop():
     np.testing.assert_allclose(ret, a + v)
 
 
-def _torch_closs(base, ft, critic, sched, obs, prev, nxt, j, ret, adv, oldlp, kf):
+def _torch_closs(base, ft, critic, sched, obs, prev, nxt, j, ret, adv, oldlp, kf, oldv=None, clip_v=None):
     """Independent restatement with torch float64 autograd (checker for the oracle's backward)."""
     import torch
     T = lambda x: torch.tensor(np.asarray(x, np.float64))
@@ -147,7 +147,11 @@ def _torch_closs(base, ft, critic, sched, obs, prev, nxt, j, ret, adv, oldlp, kf
     h2 = mish(h1) @ C["l1_w"] + C["l1_b"]
     h3 = mish(h2) @ C["l2_w"] + C["l2_b"] + h1
     V = (h3 @ C["out_w"] + C["out_b"])[:, 0]
-    vl = 0.5 * ((V - T(ret)) ** 2).mean()
+    if clip_v is None:
+        vl = 0.5 * ((V - T(ret)) ** 2).mean()
+    else:   # diffusion_ppo.py:110-116
+        vc = T(oldv) + torch.clamp(V - T(oldv), -clip_v, clip_v)
+        vl = 0.5 * torch.maximum((V - T(ret)) ** 2, (vc - T(ret)) ** 2).mean()
     (pg + 0.5 * vl).backward()
     return ({k: v.grad.numpy() for k, v in P.items()}, {k: v.grad.numpy() for k, v in C.items()},
             float(pg), float(vl))
@@ -171,6 +175,36 @@ def test_oracle_closs_gradient_matches_autograd():
         np.testing.assert_allclose(ga[k], ta[k], rtol=1e-8, atol=1e-12, err_msg=k)
     for k in tc:
         np.testing.assert_allclose(gc[k], tc[k], rtol=1e-8, atol=1e-12, err_msg=k)
+
+
+def test_oracle_clipped_value_loss_gradient_matches_autograd():
+    """clip_vloss_coef (diffusion_ppo.py:110-116): the oracle's v_loss and critic gradient against torch
+    float64 autograd, old values V(obs) + U(-0.4, 0.4) at c = 0.2 (both branches of the max, both sides
+    of the clip), with and without the sample-dedup weighting the kernels use (repeated samples)."""
+    base, ft, critic = make_models(0, HOPPER)
+    sched = O.ddpm_schedule(20)
+    rng = np.random.default_rng(2)
+    b, kf = 64, 10
+    obs = rng.uniform(-1, 1, (b, 1, 11))
+    obs[32:] = obs[:32]                                    # every sample twice (dedup weights 2)
+    prev = rng.normal(0, 0.5, (b, 4, 3))
+    nxt = prev + rng.normal(0, 0.1, (b, 4, 3))
+    j = rng.integers(0, kf, b)
+    ret, adv = rng.normal(size=b), rng.normal(size=b)
+    ret[32:] = ret[:32]
+    oldlp = rng.normal(0.5, 0.3, b)
+    v_now = O.critic_forward(to_f64(critic), obs)[0][:, 0]
+    oldv = v_now + rng.uniform(-0.4, 0.4, b)
+    oldv[32:] = oldv[:32]
+    ta, tc, pg, vl = _torch_closs(base, ft, critic, sched, obs, prev, nxt, j, ret, adv, oldlp, kf, oldv, 0.2)
+    d = np.abs(v_now - oldv)
+    assert (d > 0.2).any() and (d < 0.2).any()
+    for dedup in (None, (np.arange(32), np.full(32, 2))):
+        m, ga, gc = O.c_loss(to_f64(ft), to_f64(critic), sched, obs, prev, nxt, j, ret, oldv, adv, oldlp, kf,
+                             clip_vloss_coef=0.2, critic_dedup=dedup)
+        assert abs(m["v_loss"] - vl) < 1e-12
+        for k in tc:
+            np.testing.assert_allclose(gc[k], tc[k], rtol=1e-8, atol=1e-12, err_msg=k)
 
 
 def test_keras_adamw_first_step():
