@@ -43,8 +43,11 @@ CU_LOAD_PEAK_GBS = 64 * 2.4   # per-CU vector-memory (TA) path: 64 B/clk at the 
 # v_mfma_f32_16x16x32_bf16 x 16 cycles at 2.4 GHz; n per wave = in-Dense 4 + residual 4/P + l1
 # 64/P + fold 4/P: P = 2: 4 + 2 + 32 + 2 = 40, P = 4: 4 + 1 + 16 + 1 = 22; r01 8-member kernel 28).
 # Everything else in a step (LDS round trips, barriers, VALU epilogues, the DDPM update) is latency
-# this floor does not count.
+# this floor does not count. fp32 (v_mfma_f32_16x16x4_f32: 4 issues of 32 cycles per 16-wide k-step,
+# in-Dense K = XD + SD in 2 k-steps): P = 8 members of 4 waves, one wave per SIMD issuing in-Dense
+# 8 tiles x 2 k x 4 + residual 4 + l1 32 k x 4 + fold 4 = 200; P = 4 of 8 waves, 2 per SIMD x (32 + 4 + 128 + 4).
 SPLIT_DEFAULT_P = 2
+SPLIT_MFMA_US_F32 = {8: 200 * 32 / 2.4e3, 4: 2 * 168 * 32 / 2.4e3}
 SPLIT_XCHG_US = {2: 0.59, 4: 0.98, 8: 1.55}
 SPLIT_MFMA_US = {2: 2 * 40 * 16 / 2.4e3, 4: 2 * 22 * 16 / 2.4e3, 8: 2 * 28 * 16 / 2.4e3}
 
@@ -366,9 +369,7 @@ def main():
     members = sampler_layout(d, prec, agent.n_envs)
     from diffusionpolicyoptimization_amd import ops as _ops
     plan = _ops.sampler_plan(d, prec, agent.n_envs)
-    p8 = plan["kernel"] == 1
-    kname = {0: "sample_kernel", 1: "sample_split_kernel", 2: "sample_split4_kernel",
-             3: "sample_pair_kernel"}[plan["kernel"]]
+    kname = {0: "sample_kernel", 2: "sample_split4_kernel"}[plan["kernel"]]
     achieved = flops / (samp_ms * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -377,9 +378,9 @@ def main():
         if kname + "<" in tj.get("kernel", "") and tj.get("precision") == prec and tj.get("envs") == agent.n_envs:
             traffic = tj.get("hbm_bytes_per_launch")
     if members:
-        P = 8 if p8 else SPLIT_DEFAULT_P
+        P = plan["members"] or SPLIT_DEFAULT_P
         step_us = samp_ms * 1e3 / d.denoising_steps
-        floor_us = SPLIT_XCHG_US[P] + SPLIT_MFMA_US[P]
+        floor_us = SPLIT_XCHG_US[P] + (SPLIT_MFMA_US_F32 if prec == "fp32" else SPLIT_MFMA_US)[P]
         bound = {"kind": "latency", "kernel": kname, "workgroups_per_16_envs": members, "members_per_set": P,
                  "sampler_plan": plan,
                  "us_per_denoising_step": step_us, "floor_us_per_step": floor_us, "frac": floor_us / step_us,
@@ -390,17 +391,6 @@ def main():
                           "partial-sum exchange, so its floor "
                           "is that exchange (tools/xchg_probe2.hip) plus the step's MFMA issue, not bytes or "
                           "FLOPs; see DESIGN.md")}
-        if plan["kernel"] == 3:
-            # the pair kernel hides the exchange behind the other tile's l1: its own floor is the MFMA
-            # issue of BOTH tiles' steps on one SIMD (2 tiles x 2 waves x 40 MFMAs x 16 cycles)
-            pf = 2 * SPLIT_MFMA_US[2]
-            bound["pair_mfma_floor_us_per_step"] = pf
-            bound["pair_frac"] = pf / step_us
-            bound["note"] = ("the pair kernel: each member pair (P = 2 CUs, 1/2 of an actor resident each) runs TWO "
-                             "16-env tiles half a denoising step apart, so one tile's cross-CU exchange overlaps the "
-                             "other tile's l1 MFMAs; floor_us_per_step is the r02 one-tile floor (exchange + MFMA "
-                             "issue), pair_mfma_floor_us_per_step the pair kernel's own (MFMA issue of both tiles); "
-                             "see DESIGN.md")
     else:
         stream_b = sampler_stream_bytes_per_tile(d, prec)
         bound = {"kind": "load_path", "kernel": kname, "bytes_per_cu_per_launch": stream_b,

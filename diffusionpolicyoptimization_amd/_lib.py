@@ -22,7 +22,6 @@ DPPO_PPO_LEARN_ETA = 2                   # (ABI 9) d loss / d eta into metrics[8
 DPPO_STEP_FUSED_PACK = 0x400             # (ABI 11) AdamW + the image in one launch
 DPPO_STEP_CLEAR_GRADS = 0x800            # (ABI 11) the step zeroes the range's gradients after reading
 DPPO_PPO_PRECLEARED = 4                  # (ABI 11) the part's accumulators are already zero
-DPPO_PPO_TIME_BWD_IN_STEP = 8            # (ABI 12) the actor's time-MLP backward runs in dppo_actor_step
 SCHED_COLS = 8
 PRECISION = {"fp32": DPPO_F32, "f32": DPPO_F32, "bf16": DPPO_BF16, "fp16": DPPO_F16, "f16": DPPO_F16}
 
@@ -103,8 +102,6 @@ _SIGNATURES = {
                                  _P, _I, _U64, _P]),
     "dppo_optimizer_step_ex": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _P, _P,
                                     _P, _P, _I, _U64, _P, _P, _I, _P]),
-    "dppo_actor_step": (_I, [_DIMS, _I, _P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _I, _P, _P, _I, _P, _P, _I, _U64,
-                             _P, _P, _I, _P]),
     "dppo_ipc_region_bytes": (_SZ, [_I64]),
     "dppo_ipc_alloc": (_I, [_SZ, ctypes.POINTER(ctypes.c_void_p), _P]),
     "dppo_ipc_open": (_I, [_P, ctypes.POINTER(ctypes.c_void_p)]),
@@ -123,7 +120,7 @@ EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 _lib = None
 
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 
 class DppoError(RuntimeError):

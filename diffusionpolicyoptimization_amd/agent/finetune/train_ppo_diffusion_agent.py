@@ -10,7 +10,6 @@ the PPO epochs. Differences from the reference are only where data lives and wha
     the metrics are summed with torch.distributed (RCCL) so all replicas take identical steps.
 Semantics kept on purpose: eval at itr % val_freq == 0 with env reset only
 then (4), population-std advantage normalisation per minibatch (3), one optimiser (2)."""
-import contextlib
 import logging
 import os
 import pickle
@@ -195,14 +194,6 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         if getattr(self, "_pass_stream", None) is not None:
             torch.cuda.current_stream(self.device).wait_stream(self._pass_stream)
         self._passes_enqueued = True
-
-    def _update_stream(self):
-        if os.environ.get("DPPO_UPDATE_PRIO", "0") == "0":
-            return None
-        if getattr(self, "_hp_stream", None) is None:
-            _, greatest = torch.cuda.Stream.priority_range()
-            self._hp_stream = torch.cuda.Stream(device=self.device, priority=greatest)
-        return self._hp_stream
 
     def _allreduce(self, t):
         return allreduce_sum_(t)
@@ -449,13 +440,9 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         rows_local_full = eff_batch // W
         clipfracs, info = [], {}
         caller = torch.cuda.current_stream(self.device)
-        # DPPO_UPDATE_PRIO=1 runs the epochs on a high-priority stream (the actor half of a minibatch
-        # is the critical path; the critic half on the side stream has slack). Measured slower
-        # (update 15.0 vs 14.8 ms per iteration, tools/ab_env.sh), so off by default.
-        hp = self._update_stream()
-        if hp is not None:
-            hp.wait_stream(caller)
-        with (torch.cuda.stream(hp) if hp is not None else contextlib.nullcontext()):
+        # the epochs run on the caller's stream (a high-priority stream for the actor's half, r03, was
+        # measured slower: update 15.0 vs 14.8 ms per iteration, tools/ab_env.sh)
+        with torch.cuda.stream(caller):
             stream = torch.cuda.current_stream(self.device)
             # The target_kl check (:366-370) reads each minibatch's approx_kl on the host. It runs one
             # minibatch behind: minibatch i's gradients are enqueued before the host waits for i-1's
@@ -523,52 +510,30 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             # the critic's gradients + the minibatch's metric sums on the side stream once the actor's
             # row tiles have produced their loss metrics (overlapping the actor's dW), then the actor's
             # gradients on the main stream (overlapping the critic's optimiser step and repack).
-            defer = os.environ.get("DPPO_DEFER_TABLES", "1") != "0"   # A/B knob (measurement)
             if split:
                 if getattr(self, "_side", None) is None:
-                    # DPPO_SIDE_PRIORITY (measurement knob): the side stream's priority (negative = higher)
-                    self._side = torch.cuda.Stream(device=self.device,
-                                                   priority=int(os.environ.get("DPPO_SIDE_PRIORITY", "0")))
+                    self._side = torch.cuda.Stream(device=self.device)
                     self._met_dev = [torch.zeros(16, dtype=torch.float64, device=self.device) for _ in range(2)]
                     self._ev_rows = torch.cuda.Event()
                     self._ev_met = torch.cuda.Event()
-                    self._ev_astep = torch.cuda.Event()
                 side = self._side
                 side.wait_stream(stream)
                 na = m.n_actor
             # the per-update arguments of the minibatch and optimizer calls, validated and marshalled
             # once (host enqueue time per minibatch: an 8-GPU rank runs 255 small ones per iteration)
-            # The actor's l2 gradient stays factored (u2^T dy in its own grads region) and the actor's
-            # AdamW launch forms it (DPPO_PPO_L2_DEFERRED + DPPO_STEP_L2_FROM_PL2): one launch fewer
-            # per minibatch. The factored form is linear, so the data-parallel all-reduce is unchanged.
-            # Not with per-tensor gradient clipping (it needs the tensor) or a test hook reading grads.
-            # DPPO_FUSED_STEP = "critic" (default) | "all" | "0" (A/B knob). "critic": the critic's
-            # optimizer step is ONE launch (ABI 11) that zeroes what its next half would zero first
-            # (DPPO_STEP_CLEAR_GRADS + ops.ClearRanges; the next half runs DPPO_PPO_PRECLEARED); the
-            # actor's is time_bwd (+ l2_back) in the minibatch, then AdamW and the pack launch. "all": the
-            # actor's step is ONE launch too (dppo_actor_step, ABI 12), which also runs the time-MLP
-            # backward (the minibatch stops after its dW: DPPO_PPO_TIME_BWD_IN_STEP) and forms the l2
-            # gradient from its factored form (DPPO_PPO_L2_DEFERRED). Measured slower on one box
-            # (profiles/r05g_step_ab.txt: update 13.1 vs 12.4 ms at N = 1, 31.5 vs 27.5 ms on the
-            # emulated W = 8 rank): its per-element image stores and its workgroup-0 backward cost more
-            # than the launches they replace.
-            # Under data parallelism the time-MLP backward stays in the minibatch (its gradients are part
-            # of the all-reduced actor bucket). Not with a test hook reading the gradients (zero after
-            # the step).
-            fuse_mode = os.environ.get("DPPO_FUSED_STEP", "critic")
-            fuse = split and self.minibatch_hook is None and fuse_mode != "0"
-            fuse_actor = fuse and fuse_mode == "all"
-            tb_in_step = fuse_actor and not dp
-            # DPPO_L2_DEFER = "0" (default, also "auto") | "1". Deferred, the actor's step forms dW_l2 per
-            # element from pl2 (its virtual gradient); materialised, l2_back's groups in the launch after the
-            # actor's dW do. r04 materialised only below 16,384 rows per rank; since the row-tile fold (r05)
-            # the coalesced actor step with the virtual l2 is the slower form at every size (N = 1 update
-            # 10.3-10.4 vs 11.2-11.4 ms per iteration, profiles/r05r_l2_defer_ab.txt)
-            l2_mode = os.environ.get("DPPO_L2_DEFER", "0")
-            l2_def = (self.max_grad_norm is None and self.minibatch_hook is None and l2_mode == "1")
-            # the actor's step (AdamW + pack) clears the actor's accumulators in its pack launch
-            clear_actor = fuse and os.environ.get("DPPO_ACTOR_CLEAR", "1") != "0"
-            actor_fused = os.environ.get("DPPO_ACTOR_FUSED", "1") != "0"
+            # Both halves' optimizer steps are ONE launch each (ABI 11, DPPO_STEP_FUSED_PACK): AdamW, the
+            # weight image (the actor's: actor_tile_step_kernel, then its row tiles' fold launch) and the
+            # zeroing of what the next minibatch's half would zero first (DPPO_STEP_CLEAR_GRADS +
+            # ops.ClearRanges; the next half runs DPPO_PPO_PRECLEARED). The actor's time-MLP backward and
+            # W_out / l2 gradients stay one launch in the minibatch (time_l2_bwd). Measured slower and
+            # removed: the actor's whole tail in one launch (r06, profiles/r06de_actor_tail_ab.txt; r05g
+            # workgroup-0 form, profiles/r05g_step_ab.txt), the l2 gradient left factored for the step
+            # (profiles/r05r_l2_defer_ab.txt), the critic's half held behind the actor's step, and the
+            # AdamW + pack launch pair. Not with a test hook reading the gradients (zero after the step).
+            fuse = split and self.minibatch_hook is None
+            # the actor's image skips the split sampler's tables (fold, TIN, W_XS, B_OUT2), which no PPO
+            # kernel reads: the next rollout's first sampler launch re-derives them once
+            defer = True
             opt = self.actor_optimizer
             ng_all = m.grads.numel()
             # the bound calls are reused across updates while every buffer they captured is the same
@@ -576,26 +541,16 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             ptrs = lambda *ts: tuple((t.data_ptr(), tuple(t.shape)) for t in ts)
             bkey = (ptrs(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat, m.grads, m.train_params,
                          m.packed_ft, m.packed_critic, m.sched, m.workspace(rows_local_full), opt.m, opt.v),
-                    self.perm_seed, rows_local_full, self.reward_horizon, l2_def, split, defer,
-                    self.max_grad_norm is None, m.dims.ft_denoising_steps, m.precision, fuse, fuse_actor, clear_actor,
-                    tb_in_step, actor_fused)
+                    self.perm_seed, rows_local_full, self.reward_horizon, split,
+                    self.max_grad_norm is None, m.dims.ft_denoising_steps, m.precision, fuse)
             if getattr(self, "_bound_key", None) != bkey:
                 bound = {"run_mb": m.bind_minibatch(obs_flat, chains_flat, self.lp_old, adv_flat, ret_flat,
                                                     self.perm_seed, rows_local_full, reward_horizon=self.reward_horizon,
-                                                    l2_deferred=l2_def, time_bwd_in_step=tb_in_step,
                                                     old_values=self.values)}   # the clipped v_loss's (:110-116)
                 if split:
-                    if fuse_actor:
-                        bound["actor"] = opt.bind_actor(m.grads, na, m.dims, m.precision, m.packed_ft,
-                                                        workspace=m.workspace(rows_local_full) if tb_in_step else None,
-                                                        batch_rows=rows_local_full, l2_from_pl2=l2_def, clear_grads=True)
-                    else:
-                        # the actor's AdamW and image in ONE coalesced launch (actor_tile_step_kernel, r05);
-                        # DPPO_ACTOR_FUSED=0: the AdamW + pack launches (A/B knob)
-                        bound["actor"] = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
-                                                        packs={"actor": (m.actor_ft_params, m.packed_ft)},
-                                                        defer_sampler_tables=defer, l2_from_pl2=l2_def,
-                                                        fused_pack=fuse and actor_fused, clear_grads=clear_actor)
+                    bound["actor"] = opt.bind_range(m.grads, 0, na, m.dims, m.precision,
+                                                    packs={"actor": (m.actor_ft_params, m.packed_ft)},
+                                                    defer_sampler_tables=defer, fused_pack=fuse, clear_grads=fuse)
                     bound["critic"] = opt.bind_range(m.grads, na, ng_all, m.dims, m.precision,
                                                      packs={"critic": (m.critic_params, m.packed_critic)},
                                                      fused_pack=fuse, clear_grads=fuse)
@@ -608,7 +563,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     bound["all"] = opt.bind_range(m.grads, 0, ng_all, m.dims, m.precision,
                                                   packs={"actor": (m.actor_ft_params, m.packed_ft),
                                                          "critic": (m.critic_params, m.packed_critic)},
-                                                  defer_sampler_tables=defer, l2_from_pl2=l2_def)
+                                                  defer_sampler_tables=defer)
                 self._bound_key, self._bound = bkey, bound
             run_mb = self._bound["run_mb"]
             step_actor, step_critic = self._bound.get("actor"), self._bound.get("critic")
@@ -622,11 +577,6 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
             st_main = stream.cuda_stream
             st_side = side.cuda_stream if split else None
             met_ptrs = [t.data_ptr() for t in self._met_dev] if split else None
-            # DPPO_CRITIC_AFTER_STEP (A/B knob): the critic's half of minibatch k waits for the actor's
-            # optimizer step of k - 1 (its AdamW and fold launches are short and latency-bound; the
-            # critic's row tiles started beside them took the CUs they wait for), so it overlaps the
-            # actor's row tiles and dW of k instead
-            critic_after = split and not dp and os.environ.get("DPPO_CRITIC_AFTER_STEP", "0") != "0"
             k = 0
             for update_epoch in range(self.update_epochs):
                 for batch in range(num_batch):
@@ -650,8 +600,6 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                     if split:
                         met = self._met_dev[k % 2]
                         met_p = met_ptrs[k % 2]
-                        if critic_after and k > 0:
-                            side.wait_event(self._ev_astep)
                         run_mb(*mb_args, **mb_kw, part=2, metrics=met_p, stream=st_side, precleared=pre)
                         if not tagged and not dp:
                             ev_c = torch.cuda.Event()
@@ -659,7 +607,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         if dp:
                             ng = m.grads.numel()
                             run_mb(*mb_args, **mb_kw, part=4, metrics=met,   # actor row tiles
-                                   precleared=pre and (clear_actor or fuse_actor))
+                                   precleared=pre)
                             self._ev_rows.record(stream)
                             with torch.cuda.stream(side):          # bucket 1: critic gradients + metrics
                                 side.wait_event(self._ev_rows)
@@ -673,8 +621,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                             self._bucket_allreduce("actor", m.grads_ext[:na])      # bucket 2: actor gradients
                             stream.wait_event(self._ev_met)
                         else:
-                            run_mb(*mb_args, **mb_kw, part=1, metrics=met_p, stream=st_main,
-                                   precleared=pre and (clear_actor or fuse_actor))
+                            run_mb(*mb_args, **mb_kw, part=1, metrics=met_p, stream=st_main, precleared=pre)
                             if not tagged:
                                 stream.wait_event(ev_c)
                     else:
@@ -718,15 +665,8 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         if split:
                             ctag = tag
                             ca, cc = clear_next[(k + 1) % 2] if fuse else (None, None)
-                            ca = ca if (clear_actor or fuse_actor) else None
-                            if fuse_actor:   # a partial minibatch's workspace layout follows its rows
-                                step_actor(lr, metrics=met_p, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
-                                           stream=st_main, clear=ca, rows=rows)
-                            else:
-                                step_actor(lr, metrics=met_p, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
-                                           stream=st_main, clear=ca)
-                            if critic_after:
-                                self._ev_astep.record(stream)
+                            step_actor(lr, metrics=met_p, metrics_out=met_out.address, n_metrics=5, metrics_tag=tag,
+                                       stream=st_main, clear=ca)
                             step_critic(lr, metrics=met_p + 8, metrics_out=self._cmet_map[slot].address,   # met[1]
                                         n_metrics=1, metrics_tag=ctag, stream=st_side, clear=cc)
                             cleared = fuse

@@ -845,27 +845,9 @@ static int launch_actor_2b(const ActorArgs& a, hipStream_t s) {
     // out-layer partials (16 waves x 64 rows x 16*NO) only fit the aliased LDS tile for XD <= 16
     // (walker2d / halfcheetah, XD = 24, run the 32-row tile)
     if (a.H == 512 && v == 0 && a.XD <= 16) {
-        // The last round of 64-row tiles is short (minibatch 50,000 rows: 782 tiles = 3 rounds of
-        // 256 CUs + 14). DPPO_ACTOR_TAIL=1 runs those tail tiles as twice as many 32-row tiles in a
-        // launch of their own before the full rounds. Off by default: with the critic's half on the
-        // side stream filling the CUs the short last round leaves idle, the separate launch cost
-        // more than it saved (update 16.5 -> 15.5 ms per iteration without it, same box).
-        static const bool tail_on = [] { const char* e = getenv("DPPO_ACTOR_TAIL"); return e && atoi(e) != 0; }();
-        const bool tr = a.mode == ROWS_TRAIN || a.mode == ROWS_PRETRAIN;
-        if (tail_on && tr && a.row0 == 0 && a.row_end == 0) {
-            const int64_t tiles = (int64_t)a.ws.ldm / 64, cus = actor_device_cus();
-            const int64_t rem = tiles - ((tiles - 1) / cus) * cus;   // tiles of the last round
-            if (tiles > cus && rem <= cus / 4) {
-                ActorArgs t = a;
-                t.row0 = (tiles - rem) * 64;
-                t.row_end = (int64_t)a.ws.ldm;
-                int rc = dispatch_actor<P2, 2, 8>(t, s);
-                if (rc) return rc;
-                ActorArgs m = a;
-                m.row_end = (tiles - rem) * 64;
-                return dispatch_actor<P2, 4, 16>(m, s);
-            }
-        }
+        // (r05: running the short last round of 64-row tiles as twice as many 32-row tiles in a launch
+        // of their own cost more than it saved, update 16.5 vs 15.5 ms per iteration: the critic's half
+        // on the side stream fills the CUs that round leaves idle. Removed.)
         // a minibatch of less than one round of 64-row tiles (the per-rank share of an 8-GPU run
         // under the reference's global minibatch: 6,250 rows = 98 tiles) finishes in one tile's
         // latency either way, and a 32-row tile's is about 0.6 of a 64-row tile's (update 50.1 ->

@@ -7,6 +7,7 @@
 // (diffusion_vpg.py:198-243, 301-320). Activations never leave LDS; weights stream from L2.
 // The actor used at step t is actor_ft when t < K' else the frozen base actor (diffusion_vpg.py:161-180);
 // the reference's always-computed base forward (:161) does not change the result and is skipped.
+#include <mutex>
 #include <stdlib.h>
 #include <string.h>
 #include "dppo_common.cuh"
@@ -642,20 +643,28 @@ extern "C" int dppo_sample(const dppo_dims* d, int precision, const void* packed
                        stream);
 }
 
-// device address of pinned host memory (a small cache: the rollout reuses the same staging
-// buffers and counters every step); null if the memory is not mapped
+// device address of pinned host memory (a cache: the rollout reuses the same staging buffers and
+// counters every step); null if the memory is not mapped. One process-wide table under a mutex: a
+// mapped pinned allocation has one device address for every device (unified addressing), so the
+// entry does not depend on the calling thread or its current device; entries are never freed
+// (dropping one only costs a hipHostGetDevicePointer), so no eviction waits on a device.
 static void* mapped_ptr(const void* host) {
-    constexpr int N = 8;
-    thread_local const void* keys[N] = {};
-    thread_local void* vals[N] = {};
-    thread_local int next = 0;
-    for (int i = 0; i < N; ++i)
-        if (keys[i] == host && vals[i]) return vals[i];
+    constexpr int N = 32;
+    static std::mutex mu;
+    static const void* keys[N] = {};
+    static void* vals[N] = {};
+    static int next = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (int i = 0; i < N; ++i)
+            if (keys[i] == host && vals[i]) return vals[i];
+    }
     void* dev = nullptr;
     if (hipHostGetDevicePointer(&dev, const_cast<void*>(host), 0) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
+    std::lock_guard<std::mutex> lk(mu);
     keys[next] = host; vals[next] = dev;
     next = (next + 1) % N;
     return dev;

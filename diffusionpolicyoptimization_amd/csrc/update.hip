@@ -2,6 +2,7 @@
 // dppo_ppo_minibatch orchestration (agent/finetune/train_ppo_diffusion_agent.py:287-356).
 #include <stdlib.h>
 #include <mutex>
+#include <vector>
 #include "dppo_ppo.h"
 
 // ---------------------------------------------------------------------------------------------
@@ -41,8 +42,8 @@ static_assert(DW_LINE == 64 || DW_LINE == 128, "DPPO_DW_LINE must be 64 or 128")
 // Output tile = DW_TK(WK) x 128: WK = 128 (4 waves, 2x2 of 64x64; ring of 4 slots, 3 stages in
 // flight) or WK = 256 (8 waves, 4x2 of 64x64; ring of 3 slots, 2 stages in flight). The kernel is
 // bound by the latency of its staged loads (Little's law over the LDS ring: about 96 KiB in flight
-// per CU either way), so the 256-row tile's 1.33x MFMAs per staged byte is what it buys; the
-// k-tile edge is chosen per launch (DPPO_DW_TK: measurement knob).
+// per CU either way), so the 256-row tile's 1.33x MFMAs per staged byte is what it buys (the actor's
+// launches; the critic's uses the 128 ring, below).
 // RC caps the ring (the critic's dW runs beside the actor's time-MLP backward, whose workgroup needs
 // LDS on the same CU: a 3-slot WK = 128 ring, 101 KiB, leaves it room)
 template <int WK, int RC = 8> struct DWGeom {
@@ -350,7 +351,7 @@ __device__ inline float packed_elem_t(const uint8_t* img, int K, int k, int n) {
 // runs the time-MLP backward itself and l2_back, when materialised, is this LDS-free launch alone.)
 constexpr int L2B_ROWS = 4;   // rows h of dW_l2 per workgroup
 constexpr int L2B_MAXN = 32;
-template <int PREC, int NJ, int NQ, bool WT = false>
+template <int PREC, int NJ, int NQ>
 __device__ inline void l2_back_cols(const L2Back& a, int b, int t, int nt) {
     // branch-free loads (a conditional load made hipcc wait for it alone): N is the instantiation's
     // width for the cfgs' widths (l2_back_rows_p), the workgroup's rows exist (b < H / L2B_ROWS), column
@@ -388,21 +389,15 @@ __device__ inline void l2_back_cols(const L2Back& a, int b, int t, int nt) {
             float sum = 0.f;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) sum = fmaf(pv[r][q], wc[q], sum);
-            // WT: write-through agent-scope stores (actor_tail_kernel's W_l2 blocks read them in the launch)
-            if constexpr (WT) {
-                if (r < L2B_ROWS) __hip_atomic_store(a.gw + (size_t)(h0 + r) * H + j, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else if (b == 0) __hip_atomic_store(a.gb + j, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                if (r < L2B_ROWS) a.gw[(size_t)(h0 + r) * H + j] = sum;
-                else if (b == 0) a.gb[j] = sum;
-            }
+            if (r < L2B_ROWS) a.gw[(size_t)(h0 + r) * H + j] = sum;
+            else if (b == 0) a.gb[j] = sum;
         }
     }
 }
-template <int PREC, int NQ, bool WT = false>
+template <int PREC, int NQ>
 __device__ inline void l2_back_n(const L2Back& a, int b, int t) {   // 256 threads per row group b
-    if (a.H <= 256) l2_back_cols<PREC, 1, NQ, WT>(a, b, t, 256);
-    else l2_back_cols<PREC, 2, NQ, WT>(a, b, t, 256);
+    if (a.H <= 256) l2_back_cols<PREC, 1, NQ>(a, b, t, 256);
+    else l2_back_cols<PREC, 2, NQ>(a, b, t, 256);
 }
 // the kernels below are instantiated per precision and width NQ (the action-chunk widths of the cfgs:
 // hopper 12, walker2d / halfcheetah 24, the critic's 1, any other N <= 32 zero-padded to 32): a runtime
@@ -440,9 +435,7 @@ __device__ inline float round_prec(float x) {
     else if constexpr (PREC == DPPO_F16) return (float)(_Float16)x;
     else return x;
 }
-// WT: dW_out leaves as write-through agent-scope stores (actor_tail_kernel's last workgroup, on any XCD,
-// reads it in the same launch)
-template <int PREC, int NQ, bool WT = false>
+template <int PREC, int NQ>
 __device__ inline void out_back_n(const OutBack& a, int b, bool valid, int t, float* red) {
     constexpr int OBR = ob_rows(NQ), NQP = NQ <= 16 ? 16 : 32, V = OBR * NQP;   // V = 64
     static_assert(V == 64, "one value per lane after the halving");
@@ -505,10 +498,7 @@ __device__ inline void out_back_n(const OutBack& a, int b, bool valid, int t, fl
         if (f < H) {
             const float s = (red[v] + red[V + v]) + (red[2 * V + v] + red[3 * V + v]);
             const float bb = a.prm[a.F.l2_b + f] + a.prm[a.F.in_b + f];
-            if constexpr (WT)
-                __hip_atomic_store(a.gw + (size_t)f * NE + q, fmaf(bb, a.gob[q], s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-                a.gw[(size_t)f * NE + q] = fmaf(bb, a.gob[q], s);
+            a.gw[(size_t)f * NE + q] = fmaf(bb, a.gob[q], s);
         }
     }
 }
@@ -804,9 +794,8 @@ static size_t time_bwd_lds(const Dims& D, int nb, int* stage_g) {
                                   (size_t)nb * (2 * D.TD + 3 * 2 * D.TD));
     // the bucket sums are staged only when the workgroup stays small enough to share a CU with the
     // critic's dW (its 101 KiB ring): waiting for a CU cost more than the extra global round trip
-    // (DPPO_TB_STAGE_G=1: stage whenever it fits, the r04 form; A/B knob)
-    static const bool always = [] { const char* e = getenv("DPPO_TB_STAGE_G"); return e && atoi(e) != 0; }();
-    const size_t cap = always ? 160 * 1024 : 56 * 1024;
+    // (staging whenever it fits, the r04 form, measured slower in r05)
+    const size_t cap = 56 * 1024;
     *stage_g = tsm + sizeof(float) * (size_t)nb * D.H <= cap;
     if (*stage_g) tsm += sizeof(float) * (size_t)nb * D.H;
     return tsm;
@@ -927,39 +916,50 @@ __global__ __launch_bounds__(256) void crit_rows_kernel(const int64_t* __restric
     }
 }
 
-// per-(device, stream) sample-count scratch of crit_rows_kernel (zero between uses), grown on demand
-static uint32_t* crit_count_scratch(int64_t nsamp, hipStream_t s) {
-    struct Ent { int dev; hipStream_t s; uint32_t* p; int64_t cap; };
-    thread_local Ent ents[16] = {};
+// Per-(device, stream) device scratch that kernels leave zeroed between uses (the fused steps' ticket
+// counters, crit_rows_kernel's sample counts), created zeroed on first use and kept for the process:
+// one process-wide table under a mutex, keyed by the stream's OWN device (not the caller's current
+// one) and a kind. No eviction, so no device-wide wait: a pipelined sampler launch may be waiting for
+// an observation the host publishes later. Growth waits for that stream alone (the only one that
+// used the buffer).
+enum { SCRATCH_TICKET = 0, SCRATCH_CRIT_COUNT = 1 };
+static int stream_scratch(hipStream_t s, int kind, size_t bytes, void** out) {
+    struct Ent { int dev; hipStream_t s; int kind; void* p; size_t cap; };
+    static std::mutex mu;
+    static std::vector<Ent> ents;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    Ent* e = nullptr;
-    for (auto& x : ents)
-        if (x.p && x.dev == dev && x.s == s) { e = &x; break; }
-    if (!e)
-        for (auto& x : ents)
-            if (!x.p) { e = &x; break; }
-    if (!e) {
-        // every slot holds another (device, stream): a process that made many agents (one side stream
-        // each). Reuse the slots round robin; the evicted buffer is freed after the device is idle
-        thread_local int next = 0;
-        e = &ents[next];
-        next = (next + 1) % 16;
-        if (hipDeviceSynchronize() != hipSuccess) return nullptr;
-        (void)hipFree(e->p);
-        e->p = nullptr;
+    DPPO_HIP(hipStreamGetDevice(s, &dev));
+    std::lock_guard<std::mutex> lk(mu);
+    size_t i = 0;
+    while (i < ents.size() && !(ents[i].dev == dev && ents[i].s == s && ents[i].kind == kind)) ++i;
+    if (i < ents.size() && ents[i].cap >= bytes) { *out = ents[i].p; return DPPO_OK; }
+    int cur = 0;
+    DPPO_HIP(hipGetDevice(&cur));
+    if (cur != dev) DPPO_HIP(hipSetDevice(dev));
+    hipError_t err = hipSuccess;
+    if (i < ents.size()) {   // grow: the old buffer's last user is this stream
+        err = hipStreamSynchronize(s);
+        if (err == hipSuccess) (void)hipFree(ents[i].p);
+        ents.erase(ents.begin() + (ptrdiff_t)i);
     }
-    if (e->p && e->cap >= nsamp) return e->p;
-    if (e->p) {
-        if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
-        (void)hipFree(e->p);
-        e->p = nullptr;
+    void* p = nullptr;
+    if (err == hipSuccess) err = hipMalloc(&p, bytes);
+    if (err == hipSuccess) err = hipMemsetAsync(p, 0, bytes, s);
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (err != hipSuccess) {
+        if (p) (void)hipFree(p);
+        (void)hipGetLastError();
+        return dppo_set_error(DPPO_EHIP, "stream scratch (kind %d, %zu B): %s", kind, bytes, hipGetErrorString(err));
     }
+    ents.push_back(Ent{dev, s, kind, p, bytes});
+    *out = p;
+    return DPPO_OK;
+}
+
+// crit_rows_kernel's per-sample counts (zero between uses), grown on demand
+static int crit_count_scratch(int64_t nsamp, hipStream_t s, uint32_t** out) {
     const int64_t cap = nsamp > 65536 ? nsamp : 65536;
-    if (hipMalloc((void**)&e->p, (size_t)cap * 4) != hipSuccess) { (void)hipGetLastError(); e->p = nullptr; return nullptr; }
-    if (hipMemsetAsync(e->p, 0, (size_t)cap * 4, s) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
-    e->dev = dev; e->s = s; e->cap = cap;
-    return e->p;
+    return stream_scratch(s, SCRATCH_CRIT_COUNT, (size_t)cap * 4, (void**)out);
 }
 
 // DPPO_CRITIC_DEDUP=0 runs the critic per minibatch row (measurement knob)
@@ -1264,275 +1264,11 @@ __global__ __launch_bounds__(TILE_THREADS) void actor_tile_step_kernel(float* p,
     clear_words(a.clr, a.clr_words);
 }
 
-// ---------------------------------------------------------------------------------------------
-// The actor's whole per-minibatch tail after its dW in ONE launch (r06; dppo_actor_step with a
-// workspace). Before: time_l2_bwd (time-MLP backward + W_out's gradient) -> the
-// coalesced AdamW step -> the fold, three dependent latency-bound launches (14.5 + 14 + 5.6 us per
-// 6,250-row minibatch, profiles/r05end_emu_timeline.txt). Here the time-MLP backward, W_out's gradient
-// (out_back), l2's gradient (the virtual form: pl2 rnd(W_out), per element) and the AdamW + image-slot
-// step of every actor parameter share one launch of TB_THREADS-thread workgroups:
-//   [0, ob_wgs)     out_back groups (TB_THREADS / 256 per workgroup): dW_out rows from the OLD W_l2, W_in,
-//                   b_l2, b_in, stored write-through; then the workgroup ARRIVES
-//   ob_wgs          the time-MLP backward (time_bwd_body) from the dW's bucket sums; it ARRIVES once it has
-//                   staged the OLD W_in time-embedding rows, steps the time MLP (its own elements), and steps
-//                   b_in after every out_back workgroup has arrived (they read the old b_in)
-//   ob_wgs + 1 ...  16 tile waves per workgroup, the coalesced step of actor_tile_step_kernel: W_in, W_l1,
-//                   W_l2 blocks and the l1_b / l2_b / out_b elements. The stores of W_in, W_l2 and b_l2 (read
-//                   OLD by out_back and the backward) wait for all arrivals
-//   the last workgroup to finish (tickets) steps W_out (its gradient from out_back's stores, its old image
-//                   read by every l2 element's virtual gradient before), zeroes pl2 / db_out and the caller's
-//                   ranges, and resets the arrival counter.
-// Every wait is on LOWER-indexed workgroups only, so the launch cannot deadlock even when not all of its
-// workgroups are co-resident (workgroups are dispatched in index order). No data crosses workgroups
-// through the cache hierarchy except dW_out (write-through stores, agent-scope loads); the waits order
-// old-value reads before new-value stores (write-after-read), which needs no fence.
-// ---------------------------------------------------------------------------------------------
-struct ActorTail {
-    TileStep ts;              // the tile step's tables; ts.last_mat = W_out (virtual l2) or -1
-    int in_mat, l2_mat;       // mats whose stores wait for the arrivals (-1: none)
-    int out_mat;              // W_out: its image is read OLD by l2_back (its stores wait too), or last_mat
-    int64_t l2bias[2];        // the l2_b elements (their stores wait too)
-    OutBack ob;
-    int ob_groups, ob_wgs;    // out_back groups and the workgroups that run them
-    L2Back l2b;               // l2's gradient materialised here (not under the virtual l2): l2_back's row
-    int l2_groups, l2_wgs;    // groups in workgroups [ob_wgs, ob_wgs + l2_wgs), stored write-through
-    const float* gseg;
-    FlatOffsets F;
-    int XD, TD, H, KF, TS, stage_g;
-    float* time_dst;          // the image's fp32 time-MLP segment (element e = F.time_w1 + e)
-    float* inb_dst;           // the image's fp32 b_in segment
-    unsigned* arrive;         // zero between launches (the last workgroup resets it)
-};
-// the arrivals every waiting store needs: the out_back workgroups + the time-MLP backward
-__device__ inline void tail_wait(const unsigned* arrive, unsigned need) {
-    if ((threadIdx.x & 63) == 0) {
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 200000000ull;   // 2 s: never reached unless
-        while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need &&   // a lower-indexed
-               __builtin_amdgcn_s_memrealtime() < t_end)                                          // workgroup died
-            __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-// one 16-output x KG-input block of a packed weight (tile_block's geometry and image bytes); GA: the
-// gradient through agent-scope loads (written earlier in this launch by another workgroup); WAIT: the
-// parameter / moment / image stores after tail_wait. Virtual l2 (vt.on, the W_l2 block): the gradient of
-// element (k, n) is sum_q pl2[k][q] rnd(W_out[n][q]) (l2_back_cols' order), W_out's row n read once.
-template <class ET, int KG, int EPL, int PREC, int NQ>
-__device__ inline void tail_block(float* p, float* g, float* m, float* v, const AdamHP& h, const L2Virt& vt,
-                                  const ActorTail& a, const TileMat& M, int b, ET* tile, int lane, bool virt, bool ga,
-                                  bool wait, unsigned need) {
-    const TileStep& t = a.ts;
-    const int nb = b % M.nb, kb = b / M.nb;
-    const int n = 16 * nb + (lane & 15), jq = lane >> 4;
-    const int N = NQ < L2B_MAXN ? NQ : vt.XD;
-    float wo[NQ];
-    if (virt) {
-        const int nc = n < M.N ? n : M.N - 1;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) wo[q] = q < N ? packed_elem_t<PREC>(vt.wimg, vt.H, nc, q) : 0.f;
-    }
-    float pn[EPL], mn[EPL], vn[EPL];
-    bool ok[EPL];
-#pragma unroll
-    for (int e = 0; e < EPL; ++e) {
-        const int k = KG * kb + EPL * jq + e;
-        ok[e] = k < M.K && n < M.N;
-        pn[e] = 0.f;
-        if (ok[e]) {
-            const int64_t i = M.off + (int64_t)k * M.N + n;
-            float pi = p[i], mi = m[i], vi = v[i], gi;
-            if (virt) {
-                const float* pv = g + vt.w_off + (int64_t)k * vt.XD;
-                float sum = 0.f;
-#pragma unroll
-                for (int q = 0; q < NQ; ++q)
-                    if (q < N) sum = fmaf(pv[q], wo[q], sum);
-                gi = sum;
-            } else {
-                gi = ga ? __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : g[i];
-            }
-            if (t.clear_grads && !in_range(i, t.keep[0]) && !in_range(i, t.keep[1])) g[i] = 0.f;
-            adamw_elem(pi, mi, vi, gi, h);
-            pn[e] = pi; mn[e] = mi; vn[e] = vi;
-        }
-    }
-    if (wait) tail_wait(a.arrive, need);
-    ET val[EPL];
-#pragma unroll
-    for (int e = 0; e < EPL; ++e) {
-        const int k = KG * kb + EPL * jq + e;
-        if (ok[e]) {
-            const int64_t i = M.off + (int64_t)k * M.N + n;
-            p[i] = pn[e]; m[i] = mn[e]; v[i] = vn[e];
-        }
-        val[e] = (ET)pn[e];
-    }
-    u32x4 w;
-    __builtin_memcpy(&w, val, 16);
-    *reinterpret_cast<u32x4*>(M.img + ((((size_t)nb * M.KS + kb) << 6) + lane) * 16) = w;
-    if (!M.timg) return;
-#pragma unroll
-    for (int e = 0; e < EPL; ++e) tile[(EPL * jq + e) * 16 + (lane & 15)] = val[e];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    constexpr int NGRP = 16 / EPL;
-    const int kk = lane & 15, grp = lane >> 4;
-    const int kl = 16 * (grp / NGRP) + kk, ng = grp % NGRP;
-    const int k = KG * kb + kl, n0 = 16 * nb + EPL * ng;
-    const u32x4 tv = *reinterpret_cast<const u32x4*>(tile + kl * 16 + EPL * ng);
-    if (k < 16 * ((M.K + 15) / 16)) {
-        const int ntp = k >> 4, ksp = n0 / KG, lanep = kk + 16 * ((n0 % KG) / EPL);
-        *reinterpret_cast<u32x4*>(M.timg + ((((size_t)ntp * M.KST + ksp) << 6) + lanep) * 16) = tv;
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-
-template <class ET, int KG, int EPL, int PREC, int NQ>
-__global__ __launch_bounds__(TB_THREADS) void actor_tail_kernel(float* p, float* g, float* m, float* v, AdamHP h,
-                                                                const double* met, double* met_out, int nmet,
-                                                                uint64_t tag, L2Virt vt, ActorTail a) {
-    extern __shared__ __attribute__((aligned(16))) float tsm[];
-    constexpr int WPB = TB_THREADS / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = (int)blockIdx.x;
-    const int tb = a.ob_wgs + a.l2_wgs;   // the time-MLP backward's workgroup
-    const unsigned need = (unsigned)tb + 1;
-    const TileStep& t = a.ts;
-    ET* tile = reinterpret_cast<ET*>(tsm) + wave * KG * 16;   // wave-private transpose tile (tile waves only)
-    if (b < tb) {
-        constexpr int per = TB_THREADS / 256;
-        if (b < a.ob_wgs) {
-            const int grp = b * per + tid / 256;
-            if constexpr (NQ > 1) out_back_n<PREC, NQ, true>(a.ob, grp, grp < a.ob_groups, tid % 256, tsm + (tid / 256) * OB_RED);
-        } else {
-            const int grp = (b - a.ob_wgs) * per + tid / 256;
-            if (grp < a.l2_groups) l2_back_n<PREC, NQ, true>(a.l2b, grp, tid % 256);
-        }
-        // every thread's loads of the old parameters have returned (their FMAs ran) and its write-through
-        // gradient stores have completed
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-        __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (b == tb) {
-        copy_metrics(met, met_out, nmet, tag);
-        time_bwd_body(a.gseg, p, g, a.F, a.XD, a.TD, a.H, a.KF, a.TS, a.stage_g, tsm, [&] {
-            if (tid == 0) __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        });
-        __syncthreads();   // the backward's gradient stores, read back below by other threads
-        auto step_fp32 = [&](int64_t i, float* dst) {
-            float pi = p[i], mi = m[i], vi = v[i];
-            const float gi = g[i];
-            if (t.clear_grads) g[i] = 0.f;
-            adamw_elem(pi, mi, vi, gi, h);
-            p[i] = pi; m[i] = mi; v[i] = vi;
-            *dst = pi;
-        };
-        for (int64_t i = (int64_t)a.F.time_w1 + tid; i < (int64_t)a.F.in_w; i += TB_THREADS)
-            step_fp32(i, a.time_dst + (i - (int64_t)a.F.time_w1));
-        tail_wait(a.arrive, need);   // b_in: read old by every out_back group
-        for (int n = tid; n < a.H; n += TB_THREADS) step_fp32((int64_t)a.F.in_b + n, a.inb_dst + n);
-    } else {
-        const int gw = (b - tb - 1) * WPB + wave;
-        if (gw < t.mstart[t.nmat]) {
-            int mi = 0;
-            while (gw >= t.mstart[mi + 1]) ++mi;
-            const bool virt = vt.on && mi == a.l2_mat;
-            const bool wait = mi == a.in_mat || mi == a.l2_mat;
-            // W_l2's materialised gradient (l2_back's write-through stores in this launch): read after
-            // every arrival, through agent-scope loads
-            const bool l2m = !vt.on && a.l2_groups > 0 && mi == a.l2_mat;
-            if (l2m) tail_wait(a.arrive, need);
-            tail_block<ET, KG, EPL, PREC, NQ>(p, g, m, v, h, vt, a, t.mat[mi], gw - t.mstart[mi], tile, lane, virt, l2m,
-                                              wait && !l2m, need);
-        } else {
-            const int64_t e = (int64_t)(gw - t.mstart[t.nmat]) * 64 + lane;
-            if (e < t.cstart[t.ncpy]) {
-                int c = 0;
-                while (e >= t.cstart[c + 1]) ++c;
-                const int64_t local = e - t.cstart[c], i = t.cpy[c].lo + local;
-                const bool l2b = in_range(i, a.l2bias);
-                const bool l2m = l2b && !vt.on && a.l2_groups > 0;   // db_l2 from l2_back's workgroup 0
-                if (l2m) tail_wait(a.arrive, need);
-                float pi = p[i], mi = m[i], vi = v[i];
-                const float gi = (vt.on && l2b) ? l2_virtual_grad(g, vt, i)
-                               : l2m ? __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : g[i];
-                if (t.clear_grads && !in_range(i, t.keep[0]) && !in_range(i, t.keep[1])) g[i] = 0.f;
-                adamw_elem(pi, mi, vi, gi, h);
-                if (l2b && !l2m) tail_wait(a.arrive, need);
-                p[i] = pi; m[i] = mi; v[i] = vi;
-                t.cpy[c].dst[local] = pi;
-            }
-        }
-    }
-    if (!last_workgroup(t.ticket)) return;
-    if (t.last_mat >= 0) {
-        const TileMat& M = t.mat[t.last_mat];
-        const int nblk = M.nb * M.KS;
-        for (int bb = wave; bb < nblk; bb += WPB)
-            tail_block<ET, KG, EPL, PREC, NQ>(p, g, m, v, h, vt, a, M, bb, tile, lane, false, true, false, need);
-        __syncthreads();
-    }
-    if (t.clear_grads)
-        for (int r = 0; r < 2; ++r)
-            for (int64_t i = t.keep[r][0] + tid; i < t.keep[r][1]; i += TB_THREADS) g[i] = 0.f;
-    clear_words(t.clr, t.clr_words);
-    if (tid == 0) __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// per (device, stream): a zeroed ticket counter block of the fused steps, created on first use
-// (launches on one stream are ordered, so they share it; the critic's step on the side stream has its
-// own). One process-wide table under a mutex, keyed by the stream's own device.
+// per (device, stream): the fused steps' zeroed ticket counter block (launches on one stream are
+// ordered, so they share it; the critic's step on the side stream has its own)
 static int step_ticket(hipStream_t s, unsigned** out) {
-    struct Ent { int dev; hipStream_t s; unsigned* ticket; };
-    static std::mutex mu;
-    static Ent ents[64] = {};
-    static int next = 0;
-    int dev = 0;
-    DPPO_HIP(hipStreamGetDevice(s, &dev));
-    std::lock_guard<std::mutex> lk(mu);
-    for (auto& x : ents)
-        if (x.ticket && x.dev == dev && x.s == s) { *out = x.ticket; return DPPO_OK; }
-    Ent* e = nullptr;
-    for (auto& x : ents)
-        if (!x.ticket) { e = &x; break; }
-    if (!e) {   // every slot taken (many streams): evict round robin once that device is idle
-        e = &ents[next];
-        next = (next + 1) % 64;
-        int cur = 0;
-        DPPO_HIP(hipGetDevice(&cur));
-        DPPO_HIP(hipSetDevice(e->dev));
-        DPPO_HIP(hipDeviceSynchronize());
-        (void)hipFree(e->ticket);
-        DPPO_HIP(hipSetDevice(cur));
-        *e = Ent{};
-    }
-    int cur = 0;
-    DPPO_HIP(hipGetDevice(&cur));
-    if (cur != dev) DPPO_HIP(hipSetDevice(dev));
-    const hipError_t ea = hipMalloc((void**)&e->ticket, 1024);   // 8 per-XCD counters 64 B apart, the total at 512 B
-    const hipError_t ez = ea == hipSuccess ? hipMemsetAsync(e->ticket, 0, 1024, s) : ea;
-    if (cur != dev) (void)hipSetDevice(cur);
-    if (ea != hipSuccess || ez != hipSuccess) {
-        if (ea == hipSuccess) (void)hipFree(e->ticket);
-        e->ticket = nullptr;
-        (void)hipGetLastError();
-        return dppo_set_error(DPPO_EHIP, "fused step: ticket allocation failed");
-    }
-    e->dev = dev; e->s = s;
-    *out = e->ticket;
-    return DPPO_OK;
-}
-
-// the (precision, width) instantiations of the actor tail
-template <class ET, int KG, int EPL, int PREC>
-static const void* actor_tail_fn_p(int nq) {
-    return nq == 12 ? (const void*)actor_tail_kernel<ET, KG, EPL, PREC, 12>
-         : nq == 24 ? (const void*)actor_tail_kernel<ET, KG, EPL, PREC, 24>
-                    : (const void*)actor_tail_kernel<ET, KG, EPL, PREC, L2B_MAXN>;
-}
-static const void* actor_tail_fn(int prec, int nq) {
-    return prec == DPPO_BF16 ? actor_tail_fn_p<__bf16, 32, 8, DPPO_BF16>(nq)
-         : prec == DPPO_F16 ? actor_tail_fn_p<_Float16, 32, 8, DPPO_F16>(nq) : actor_tail_fn_p<float, 16, 4, DPPO_F32>(nq);
+    // 8 per-XCD counters 64 B apart, the total at 512 B
+    return stream_scratch(s, SCRATCH_TICKET, 1024, (void**)out);
 }
 
 static int launch_adamw(float* params, const float* grads, float* m, float* v, int64_t n, int64_t step, float lr,
@@ -1567,8 +1303,7 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
                                float eps, int mode, const float* actor_params, void* packed_actor,
                                const float* critic_params, void* packed_critic, const double* metrics,
                                double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
-                               const size_t* clear_bytes, int n_clear, void* stream, const float* gseg = nullptr,
-                               const float* pa0 = nullptr, const float* pl2 = nullptr) {
+                               const size_t* clear_bytes, int n_clear, void* stream) {
     Dims D;
     int rc = dppo_check_dims(d, &D);
     if (rc) return rc;
@@ -1607,11 +1342,10 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
                     (const uint8_t*)packed_actor + L.off[SEG_W_OUT]};
     }
     // the one-launch form: a single network whose parameters are exactly the range. The actor's
-    // (actor_tile_step_kernel / actor_tail_kernel) leaves its TEMB table and split-sampler tables to the fold launch (the row
+    // (actor_tile_step_kernel) leaves its TEMB table and split-sampler tables to the fold launch (the row
     // tiles derive the time embeddings, the sampler re-derives the tables before its next launch)
     const bool one_actor = packed_actor && !packed_critic && actor_params == params && n == (int64_t)FA.count;
     const bool one_critic = packed_critic && !packed_actor && critic_params == params && n == (int64_t)FC.count;
-    DPPO_CHECK(!gseg || (fuse && one_actor), "dppo_actor_step: the time-MLP backward needs the fused actor step");
     if (fuse && (one_actor || one_critic) && n > 0) {
         DPPO_CHECK(n_metrics >= 0 && n_metrics <= 256 && (n_metrics == 0 || (metrics && mout)),
                    "dppo_optimizer_step: bad metrics copy");
@@ -1648,115 +1382,39 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
             DPPO_HIP(hipGetLastError());
             return DPPO_OK;
         }
-        if (!gseg) {
-            FuseJob jobs[FUSE_MAXJ];
-            const int nj = dppo_fuse_jobs(D.IN, D.H, D.XD, D.TD, precision, packed_actor, D.K, jobs);
-            DPPO_CHECK(nj >= 0, "dppo_optimizer_step: fused pack jobs");
-            TileStep t = {};
-            t.last_mat = -1;
-            for (int q = 0; q < nj; ++q) {
-                const FuseJob& J = jobs[q];
-                if (J.kind == 0) {
-                    DPPO_CHECK(t.nmat < TILE_MAXM, "actor tile step: too many weight tensors");
-                    TileMat& M = t.mat[t.nmat++];
-                    M.off = J.lo; M.K = J.IK; M.N = J.IN; M.KS = J.KS; M.img = J.dst; M.timg = nullptr; M.KST = 0;
-                    M.nb = dppo_cdiv(M.N, 16);
-                } else if (J.kind == 2) {
-                    DPPO_CHECK(t.ncpy < TILE_MAXC, "actor tile step: too many fp32 tensors");
-                    t.cpy[t.ncpy++] = TileCpy{J.lo, J.hi - J.lo, (float*)J.dst};
-                }
-            }
-            for (int q = 0; q < nj; ++q) {   // the transposed images, matched to their tensor
-                const FuseJob& J = jobs[q];
-                if (J.kind != 1) continue;
-                int mi = 0;
-                while (mi < t.nmat && t.mat[mi].off != J.lo) ++mi;
-                DPPO_CHECK(mi < t.nmat && J.IK == t.mat[mi].N && J.IN == t.mat[mi].K, "actor tile step: transposed image");
-                t.mat[mi].timg = J.dst; t.mat[mi].KST = J.KS;
-            }
-            for (int r = 0; r < 2; ++r) t.keep[r][0] = t.keep[r][1] = -1;
-            if (l2v) {
-                for (int mi = 0; mi < t.nmat; ++mi)
-                    if (t.mat[mi].off == (int64_t)FA.out_w) t.last_mat = mi;
-                DPPO_CHECK(t.last_mat >= 0, "actor tile step: W_out");
-                t.keep[0][0] = (int64_t)FA.l2_w; t.keep[0][1] = (int64_t)(FA.l2_w + (size_t)D.H * D.XD);
-                t.keep[1][0] = (int64_t)FA.out_b; t.keep[1][1] = (int64_t)(FA.out_b + D.XD);
-            }
-            t.mstart[0] = 0;
-            for (int mi = 0; mi < t.nmat; ++mi)
-                t.mstart[mi + 1] = t.mstart[mi] + (mi == t.last_mat ? 0 : t.mat[mi].nb * t.mat[mi].KS);
-            t.cstart[0] = 0;
-            for (int c = 0; c < t.ncpy; ++c) t.cstart[c + 1] = t.cstart[c] + t.cpy[c].n;
-            t.clear_grads = clear_g ? 1 : 0;
-            for (int r = 0; r < n_clear; ++r) { t.clr[r] = clear_ptrs[r]; t.clr_words[r] = (uint32_t)(clear_bytes[r] / 4); }
-            if (l2v || n_clear > 0 || clear_g) {
-                rc = step_ticket(s, &t.ticket);
-                if (rc) return rc;
-            }
-            const int64_t waves = t.mstart[t.nmat] + (t.cstart[t.ncpy] + 63) / 64;
-            const unsigned blocks = (unsigned)((waves + TILE_THREADS / 64 - 1) / (TILE_THREADS / 64));
-            {
-                DppoKtScope kt(KT_ADAMW, s);
-                if (precision == DPPO_BF16)
-                    hipLaunchKernelGGL((actor_tile_step_kernel<__bf16, 32, 8>), dim3(blocks), dim3(TILE_THREADS), 0, s,
-                                       params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
-                else if (precision == DPPO_F16)
-                    hipLaunchKernelGGL((actor_tile_step_kernel<_Float16, 32, 8>), dim3(blocks), dim3(TILE_THREADS), 0, s,
-                                       params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
-                else
-                    hipLaunchKernelGGL((actor_tile_step_kernel<float, 16, 4>), dim3(blocks), dim3(TILE_THREADS), 0, s,
-                                       params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
-            }
-            DPPO_HIP(hipGetLastError());
-            rc = dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS, s);   // cross-element: not per element
-            if (rc) return rc;
-            return dppo_mark_tables_stale(D, precision, actor_params, packed_actor, true);
-        }
-        // with the time-MLP backward: the actor's whole tail in one launch (actor_tail_kernel)
         FuseJob jobs[FUSE_MAXJ];
         const int nj = dppo_fuse_jobs(D.IN, D.H, D.XD, D.TD, precision, packed_actor, D.K, jobs);
-        DPPO_CHECK(nj >= 0, "dppo_actor_step: fused pack jobs");
-
-        ActorTail a = {};
-        TileStep& t = a.ts;
+        DPPO_CHECK(nj >= 0, "dppo_optimizer_step: fused pack jobs");
+        TileStep t = {};
         t.last_mat = -1;
-        a.in_mat = a.l2_mat = a.out_mat = -1;
         for (int q = 0; q < nj; ++q) {
             const FuseJob& J = jobs[q];
             if (J.kind == 0) {
-                DPPO_CHECK(t.nmat < TILE_MAXM, "actor tail: too many weight tensors");
-                TileMat& M = t.mat[t.nmat];
+                DPPO_CHECK(t.nmat < TILE_MAXM, "actor tile step: too many weight tensors");
+                TileMat& M = t.mat[t.nmat++];
                 M.off = J.lo; M.K = J.IK; M.N = J.IN; M.KS = J.KS; M.img = J.dst; M.timg = nullptr; M.KST = 0;
                 M.nb = dppo_cdiv(M.N, 16);
-                if (J.lo == (int64_t)FA.in_w) a.in_mat = t.nmat;
-                if (J.lo == (int64_t)FA.l2_w) a.l2_mat = t.nmat;
-                if (J.lo == (int64_t)FA.out_w) {   // the last workgroup: its gradient is out_back's, in this launch
-                    a.out_mat = t.nmat;
-                    t.last_mat = t.nmat;
-                }
-                ++t.nmat;
             } else if (J.kind == 2) {
-                if (J.lo == (int64_t)FA.time_w1) { a.time_dst = (float*)J.dst; continue; }   // the backward's workgroup
-                if (J.lo == (int64_t)FA.in_b) { a.inb_dst = (float*)J.dst; continue; }
-                DPPO_CHECK(t.ncpy < TILE_MAXC, "actor tail: too many fp32 tensors");
+                DPPO_CHECK(t.ncpy < TILE_MAXC, "actor tile step: too many fp32 tensors");
                 t.cpy[t.ncpy++] = TileCpy{J.lo, J.hi - J.lo, (float*)J.dst};
             }
         }
-        for (int q = 0; q < nj; ++q) {
+        for (int q = 0; q < nj; ++q) {   // the transposed images, matched to their tensor
             const FuseJob& J = jobs[q];
             if (J.kind != 1) continue;
             int mi = 0;
             while (mi < t.nmat && t.mat[mi].off != J.lo) ++mi;
-            DPPO_CHECK(mi < t.nmat && J.IK == t.mat[mi].N && J.IN == t.mat[mi].K, "actor tail: transposed image");
+            DPPO_CHECK(mi < t.nmat && J.IK == t.mat[mi].N && J.IN == t.mat[mi].K, "actor tile step: transposed image");
             t.mat[mi].timg = J.dst; t.mat[mi].KST = J.KS;
         }
-        DPPO_CHECK(a.time_dst && a.inb_dst && a.in_mat >= 0 && a.l2_mat >= 0, "actor tail: image segments");
         for (int r = 0; r < 2; ++r) t.keep[r][0] = t.keep[r][1] = -1;
-        // db_out: read by out_back and by l2's gradient (l2_back's db_l2, or every l2 element's virtual one),
-        // zeroed by the last workgroup; under the virtual l2 also pl2 in the l2 region of the gradients
-        t.keep[1][0] = (int64_t)FA.out_b; t.keep[1][1] = (int64_t)(FA.out_b + D.XD);
-        if (l2v) { t.keep[0][0] = (int64_t)FA.l2_w; t.keep[0][1] = (int64_t)(FA.l2_w + (size_t)D.H * D.XD); }
-        a.l2bias[0] = (int64_t)FA.l2_b; a.l2bias[1] = (int64_t)(FA.l2_b + D.H);
+        if (l2v) {
+            for (int mi = 0; mi < t.nmat; ++mi)
+                if (t.mat[mi].off == (int64_t)FA.out_w) t.last_mat = mi;
+            DPPO_CHECK(t.last_mat >= 0, "actor tile step: W_out");
+            t.keep[0][0] = (int64_t)FA.l2_w; t.keep[0][1] = (int64_t)(FA.l2_w + (size_t)D.H * D.XD);
+            t.keep[1][0] = (int64_t)FA.out_b; t.keep[1][1] = (int64_t)(FA.out_b + D.XD);
+        }
         t.mstart[0] = 0;
         for (int mi = 0; mi < t.nmat; ++mi)
             t.mstart[mi + 1] = t.mstart[mi] + (mi == t.last_mat ? 0 : t.mat[mi].nb * t.mat[mi].KS);
@@ -1764,53 +1422,27 @@ static int optimizer_step_impl(const dppo_dims* d, int precision, float* params,
         for (int c = 0; c < t.ncpy; ++c) t.cstart[c + 1] = t.cstart[c] + t.cpy[c].n;
         t.clear_grads = clear_g ? 1 : 0;
         for (int r = 0; r < n_clear; ++r) { t.clr[r] = clear_ptrs[r]; t.clr_words[r] = (uint32_t)(clear_bytes[r] / 4); }
-        rc = step_ticket(s, &t.ticket);
-        if (rc) return rc;
-        a.arrive = t.ticket + 192;   // 768 B into the ticket block: the arrival counter
-        // W_out's gradient (out_back) from the old parameters: here under the virtual l2 (the minibatch
-        // launched nothing after its dW); otherwise the minibatch's l2_back launch materialised it
-        DPPO_CHECK(D.IN <= 256 && D.H % 4 == 0, "out_back: in_dim %d > 256", D.IN);
-        const int nq = l2_nq(D.XD);
-        DPPO_CHECK(pa0 && pl2, "dppo_actor_step: the workspace's pa0 / pl2 (W_out's and l2's gradients) are needed");
-        // W_out's gradient (out_back) from the old parameters, and l2's: virtual (pl2 in the l2 region of the
-        // gradients, formed per element) or materialised by l2_back groups from the workspace's pl2
-        a.ob = make_out_back(D, precision, actor_params, l2v ? grads + FA.l2_w : pl2, pa0, grads);
-        a.ob_groups = dppo_cdiv(D.H, ob_rows(nq));
-        a.ob_wgs = dppo_cdiv(a.ob_groups, TB_THREADS / 256);
-        if (!l2v) {
-            DPPO_CHECK(D.XD <= L2B_MAXN, "l2_back: action horizon x dim %d > %d", D.XD, L2B_MAXN);
-            const MlpLayout LA = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
-            a.l2b = L2Back{pl2, grads + FA.out_b, (const uint8_t*)packed_actor + LA.off[SEG_W_OUT], grads + FA.l2_w,
-                           grads + FA.l2_b, D.H, D.XD, precision, nullptr, nullptr, nullptr};
-            a.l2_groups = dppo_cdiv(D.H, L2B_ROWS);
-            a.l2_wgs = dppo_cdiv(a.l2_groups, TB_THREADS / 256);
+        if (l2v || n_clear > 0 || clear_g) {
+            rc = step_ticket(s, &t.ticket);
+            if (rc) return rc;
         }
-        a.gseg = gseg;
-        a.F = FA; a.XD = D.XD; a.TD = D.TD; a.H = D.H; a.KF = D.KF; a.TS = D.TS;
-        size_t lds = time_bwd_lds(D, D.KF, &a.stage_g);
-        const size_t tile_lds = (size_t)(TB_THREADS / 64) * 16 * 64;   // a wave's KG x 16 transpose tile: 64 B per row
-        const size_t ob_lds = sizeof(float) * OB_RED * (TB_THREADS / 256);
-        if (lds < tile_lds) lds = tile_lds;
-        if (lds < ob_lds) lds = ob_lds;
-        DPPO_CHECK(lds <= 160 * 1024, "dppo_actor_step: tail LDS %zu B exceeds 160 KB", lds);
         const int64_t waves = t.mstart[t.nmat] + (t.cstart[t.ncpy] + 63) / 64;
-        const unsigned blocks = (unsigned)(a.ob_wgs + a.l2_wgs + 1 + (waves + TB_THREADS / 64 - 1) / (TB_THREADS / 64));
-        const void* fn = actor_tail_fn(precision, nq);
-        rc = dppo_func_lds(fn, lds);
-        if (rc) return rc;
+        const unsigned blocks = (unsigned)((waves + TILE_THREADS / 64 - 1) / (TILE_THREADS / 64));
         {
             DppoKtScope kt(KT_ADAMW, s);
-            AdamHP hh = h;
-            L2Virt vv = vt;
-            void* args[] = {(void*)&params, (void*)&grads, (void*)&m, (void*)&v, (void*)&hh, (void*)&metrics, (void*)&mout,
-                            (void*)&n_metrics, (void*)&metrics_tag, (void*)&vv, (void*)&a};
-            DPPO_HIP(hipLaunchKernel(fn, dim3(blocks), dim3(TB_THREADS), args, lds, s));
+            if (precision == DPPO_BF16)
+                hipLaunchKernelGGL((actor_tile_step_kernel<__bf16, 32, 8>), dim3(blocks), dim3(TILE_THREADS), 0, s,
+                                   params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
+            else if (precision == DPPO_F16)
+                hipLaunchKernelGGL((actor_tile_step_kernel<_Float16, 32, 8>), dim3(blocks), dim3(TILE_THREADS), 0, s,
+                                   params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
+            else
+                hipLaunchKernelGGL((actor_tile_step_kernel<float, 16, 4>), dim3(blocks), dim3(TILE_THREADS), 0, s,
+                                   params, grads, m, v, h, metrics, mout, n_metrics, metrics_tag, vt, t);
         }
         DPPO_HIP(hipGetLastError());
-        // the row tiles' fold needs every element final: its own small launch (pack.hip PACK_RT_FOLD)
-        rc = dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS, s);
+        rc = dppo_pack_rt_fold(D.IN, D.H, D.XD, D.TD, precision, actor_params, packed_actor, D.K, D.TS, s);   // cross-element: not per element
         if (rc) return rc;
-        // TEMB (every precision) and the split sampler's tables (2-byte) wait for the next sampler launch
         return dppo_mark_tables_stale(D, precision, actor_params, packed_actor, true);
     }
     // the launch-per-stage form (any ranges and images): AdamW, then the pack, which also zeroes the
@@ -1864,37 +1496,6 @@ extern "C" int dppo_optimizer_step_ex(const dppo_dims* d, int precision, float* 
     return optimizer_step_impl(d, precision, params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps, mode,
                                actor_params, packed_actor, critic_params, packed_critic, metrics, metrics_out,
                                n_metrics, metrics_tag, clear_ptrs, clear_bytes, n_clear, stream);
-}
-
-// ABI 12: the actor's optimizer step (actor_tile_step_kernel); with a workspace (r06: actor_tail_kernel) it also
-// runs the time-MLP backward from that minibatch's bucket sums (DPPO_PPO_TIME_BWD_IN_STEP)
-extern "C" int dppo_actor_step(const dppo_dims* d, int precision, float* params, float* grads, float* m, float* v,
-                               int64_t step, float lr, float weight_decay, float beta1, float beta2, float eps, int mode,
-                               void* packed_actor, const void* workspace, int batch_rows, const double* metrics,
-                               double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
-                               const size_t* clear_bytes, int n_clear, void* stream) {
-    Dims D;
-    int rc = dppo_check_dims(d, &D);
-    if (rc) return rc;
-    DPPO_CHECK(dppo_prec_ok(precision), "bad precision %d", precision);
-    DPPO_CHECK((mode & ~(DPPO_STEP_L2_FROM_PL2 | DPPO_STEP_CLEAR_GRADS | DPPO_STEP_DEFER_SAMPLER_TABLES |
-                         DPPO_STEP_FUSED_PACK | 1)) == 0, "dppo_actor_step: unknown mode bits 0x%x", mode);
-    DPPO_CHECK(packed_actor && params, "dppo_actor_step: null image or parameters");
-    DPPO_CHECK(!workspace || batch_rows > 0, "dppo_actor_step: a workspace needs its batch_rows");
-    DPPO_CHECK(D.KF <= 16, "dppo_actor_step: ft_denoising_steps > 16 unsupported (bucket sums)");
-    const float* gseg = nullptr;
-    const float* pa0 = nullptr;
-    const float* pl2 = nullptr;
-    if (workspace) {
-        const PpoWorkspace ws = make_ppo_workspace(D, precision, batch_rows, (uint8_t*)const_cast<void*>(workspace));
-        gseg = ws.gseg;
-        pa0 = ws.pa0;
-        pl2 = ws.pl2;
-    }
-    const int64_t n = (int64_t)make_flat_offsets(D.IN, D.H, D.XD, D.TD).count;
-    return optimizer_step_impl(d, precision, params, grads, m, v, n, step, lr, weight_decay, beta1, beta2, eps,
-                               mode | DPPO_STEP_FUSED_PACK, params, packed_actor, nullptr, nullptr, metrics, metrics_out,
-                               n_metrics, metrics_tag, clear_ptrs, clear_bytes, n_clear, stream, gseg, pa0, pl2);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2046,25 +1647,22 @@ static int launch_dw(const DWArgs& a, int wk, hipStream_t s) {
     return DPPO_OK;
 }
 
-// k-tile edge of the grouped dW launches (DPPO_DW_TK = 128 / 256: measurement knob)
-static int dw_tk() {
-    static const int tk = [] { const char* e = getenv("DPPO_DW_TK"); return e && atoi(e) == 128 ? 128 : 256; }();
-    return tk;
-}
+// k-tile edge of the grouped dW launches (128 measured slower, r04)
+constexpr int DW_TK = 256;
 
 // one non-blocking side stream (+ fork/join events) per device and host thread, created on first use;
 // null if creation fails (the caller then runs everything on its own stream)
-// (which = 0: the critic's half of a whole minibatch; 1: the actor's time-MLP backward fork)
+// (the critic's half of a whole minibatch)
 struct SideStream { hipStream_t stream; hipEvent_t fork, join; };
-static SideStream* side_stream(int which = 0) {
+static SideStream* side_stream() {
     constexpr int MAXDEV = 16;
-    thread_local SideStream ss[2][MAXDEV] = {};
-    thread_local bool tried[2][MAXDEV] = {};
+    thread_local SideStream ss[MAXDEV] = {};
+    thread_local bool tried[MAXDEV] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
-    SideStream& e = ss[which][dev];
-    if (!tried[which][dev]) {
-        tried[which][dev] = true;
+    SideStream& e = ss[dev];
+    if (!tried[dev]) {
+        tried[dev] = true;
         if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&e.fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e.join, hipEventDisableTiming) != hipSuccess) {
@@ -2083,7 +1681,7 @@ static SideStream* side_stream(int which = 0) {
 // W_out's gradient (out_back) and, unless the l2 gradient stays factored, l2's from pl2, in one launch
 static int launch_time_bwd(const Dims& D, int precision, const float* gseg, const float* pl2, const float* pa0,
                            const void* packed_actor, const float* actor_params, float* ga, int nb, int TS, hipStream_t s,
-                           bool l2_back = true, bool groups = true) {
+                           bool l2_back = true) {
     const FlatOffsets FA = make_flat_offsets(D.IN, D.H, D.XD, D.TD);
     const MlpLayout L = make_mlp_layout(D.IN, D.H, D.XD, D.TD, precision, D.K);
     L2Back l2b = {pl2, ga + FA.out_b, (const uint8_t*)packed_actor + L.off[SEG_W_OUT], ga + FA.l2_w, ga + FA.l2_b, D.H,
@@ -2097,7 +1695,7 @@ static int launch_time_bwd(const Dims& D, int precision, const float* gseg, cons
     const size_t tsm = tsm0 > sizeof(float) * OB_RED * (TB_THREADS / 256) ? tsm0 : sizeof(float) * OB_RED * (TB_THREADS / 256);
     DPPO_CHECK(tsm <= 160 * 1024, "time_bwd: LDS staging %zu B exceeds 160 KB", tsm);
     const int per = TB_THREADS / 256;
-    const int l2g = l2_back && groups ? dppo_cdiv(D.H, L2B_ROWS) : 0, obg = groups ? dppo_cdiv(D.H, ob_rows(l2_nq(D.XD))) : 0;
+    const int l2g = l2_back ? dppo_cdiv(D.H, L2B_ROWS) : 0, obg = dppo_cdiv(D.H, ob_rows(l2_nq(D.XD)));
     const int nq = l2_nq(D.XD);
     const void* fn = time_l2_bwd_fn(precision, nq);
     { const int rc_ = dppo_func_lds(fn, tsm); if (rc_) return rc_; }
@@ -2200,19 +1798,17 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     DPPO_CHECK(parts >= 1 && parts <= 5, "dppo_ppo_minibatch: bad part %d", parts);
     DPPO_CHECK(parts == 3 || adv_stats || parts == 2 || parts == 5,
                "dppo_ppo_minibatch_part: the actor half needs adv_stats");
-    DPPO_CHECK((hp->flags & ~(DPPO_PPO_L2_DEFERRED | DPPO_PPO_LEARN_ETA | DPPO_PPO_PRECLEARED |
-                              DPPO_PPO_TIME_BWD_IN_STEP)) == 0,
+    DPPO_CHECK((hp->flags & ~(DPPO_PPO_L2_DEFERRED | DPPO_PPO_LEARN_ETA | DPPO_PPO_PRECLEARED)) == 0,
                "dppo_ppo_minibatch: unknown flags 0x%x", hp->flags);
     // one launch zeroes the atomically accumulated outputs of the half (or whole) being run
     // (minibatch_zero_args) unless the caller's optimizer step already did (DPPO_PPO_PRECLEARED)
     const ZeroArgs z = minibatch_zero_args(D, ws, grads, metrics, parts);
     // few workgroups: the split update runs this while the other stream's row tiles hold most CUs,
-    // and a 256-block grid waited ~25 us for slots (DPPO_ZERO_BLOCKS: measurement knob)
-    static const int zero_blocks = [] { const char* e = getenv("DPPO_ZERO_BLOCKS"); return e ? atoi(e) : 16; }();
+    // and a 256-block grid waited ~25 us for slots
     // part 5 continues the actor half whose part 4 zeroed its outputs
     if (parts != 5 && !(hp->flags & DPPO_PPO_PRECLEARED)) {
         DppoKtScope kt(KT_ZERO, s);
-        hipLaunchKernelGGL(zero_kernel, dim3(zero_blocks > 0 ? zero_blocks : 16), dim3(256), 0, s, z);
+        hipLaunchKernelGGL(zero_kernel, dim3(16), dim3(256), 0, s, z);
         DPPO_HIP(hipGetLastError());
     }
     DPPO_CHECK((uint64_t)total < ((uint64_t)1 << 32), "dppo_ppo_minibatch: %lld samples x steps exceed 2^32",
@@ -2255,24 +1851,18 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     ca.fk = fk; ca.start = start; ca.row_index = row_index; ca.returns = returns; ca.hp = lh; ca.ws = ws; ca.metrics = metrics;
     // weight-gradient problems of one network, launched as one grouped dW kernel on stream st.
     // m-chunks: about one workgroup per CU (the ring takes 132 KB of LDS) in a single round.
-    // DPPO_DW_CHUNKS overrides the chunk count (a measurement knob).
-    static const int env_ch = [] { const char* e = getenv("DPPO_DW_CHUNKS"); return e ? atoi(e) : 0; }();
-    const int tk = dw_tk();
+    const int tk = DW_TK;
     const int* crit_rows_dev = nullptr;
-    auto launch_grads = [&](bool actor, hipStream_t st, unsigned pmask = 0xFu) -> int {
+    auto launch_grads = [&](bool actor, hipStream_t st) -> int {
         DWArgs w = {};
         int all_tiles = 0;
         if (!actor) w.rows_dev = crit_rows_dev;
         const size_t span = ws.ldm;
         // the critic's dW runs beside the actor's dW tail: its smaller ring (WK = 128, 3 slots) leaves the
-        // CU room for the time-MLP backward's workgroup (DPPO_CDW_RING=0: the actor's geometry, A/B knob)
-        static const bool cring = [] { const char* e = getenv("DPPO_CDW_RING"); return !e || atoi(e) != 0; }();
-        const int wk = (!actor && cring) ? 0 : tk, tke = wk ? wk : 128;
-        int pi = 0;
+        // CU room for the time-MLP backward's workgroup
+        const int wk = actor ? tk : 0, tke = wk ? wk : 128;
         auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
-            const bool on = (pmask >> pi++) & 1u;
             all_tiles += dppo_cdiv(Kx, tke) * dppo_cdiv(N, DW_TN);
-            if (!on) return;
             DWProb& p = w.p[w.nprob];
             p.XT = XT; p.DT = DT; p.G = G; p.Gx = Gx; p.Kx = Kx; p.N = N; p.extra = extra;
             p.ktiles = dppo_cdiv(Kx, tke); p.ntiles = dppo_cdiv(N, DW_TN);
@@ -2293,13 +1883,12 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         w.ldm = ws.ldm;
         w.seg = ws.seg;
         w.out_scale = 1.f / gscale;
-        // the chunking of a subset (pmask) is the whole set's: the subsets run concurrently
         const int tiles = all_tiles;
         // about one workgroup per CU, but no chunk under 768 rows: at small minibatches (6,250 rows,
         // an 8-GPU rank's share) thinner chunks cost more in partial-tile atomics than they gain
         // in parallelism (0.177 -> 0.154 ms per minibatch, tools/ab_small_mb2.sh)
-        int nch = env_ch > 0 ? env_ch : dw_device_cus() / tiles;
-        if (env_ch <= 0 && nch > (int)(span / 768)) nch = (int)(span / 768);
+        int nch = dw_device_cus() / tiles;
+        if (nch > (int)(span / 768)) nch = (int)(span / 768);
         const int max_ch = (int)(span / 64);
         if (nch > max_ch) nch = max_ch;
         if (nch < 1) nch = 1;
@@ -2316,8 +1905,7 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
     auto critic_rows = [&](hipStream_t st) -> int {
         if (!crit_dedup()) return DPPO_OK;
         const int64_t nsamp = total / D.KF;
-        crit_cnt = crit_count_scratch(nsamp, st);
-        DPPO_CHECK(crit_cnt, "dppo_ppo_minibatch: sample-count scratch allocation failed");
+        { const int rc_ = crit_count_scratch(nsamp, st, &crit_cnt); if (rc_) return rc_; }
         const int blocks = dppo_cdiv(rows, 256) < 512 ? dppo_cdiv(rows, 256) : 512;
         DppoKtScope kt(KT_CRIT_ROWS, st);
         hipLaunchKernelGGL(crit_rows_kernel, dim3(blocks), dim3(256), 0, st, row_index, start, rows, fk, D.KF, crit_cnt,
@@ -2331,38 +1919,14 @@ static int ppo_minibatch_impl(const dppo_dims* d, int precision, const dppo_ppo_
         return launch_critic_l2_back(D, precision, ws.cpl2, packed_critic, gc, crit_cnt, ws.crow_n, ws.crow_cnt, st);
     };
 
-    // after the actor's dW: the time-MLP backward (+ l2_back when l2 is materialised), unless the
-    // caller's actor step (dppo_actor_step) runs the time-MLP backward itself
+    // after the actor's dW: the time-MLP backward, W_out's gradient and (materialised) l2's in one launch.
+    // (Forking the time-MLP backward beside the dW (r05, profiles/r05y_tb_fork_ab.txt) and running it
+    // inside a one-launch actor step (r06, profiles/r06de_actor_tail_ab.txt) were both measured slower.)
     const float* pl2_src = l2_def ? ga + FA.l2_w : ws.pl2;
-    // DPPO_TB_FORK=1 (A/B knob, off): the time-MLP backward needs only the bucket sums gseg, which the
-    // in_w problem of the actor's dW forms (its one-hot extra rows), so that problem and then the
-    // backward can run on a forked stream beside the rest of the dW and the l2_back / out_back launch,
-    // joined before the part returns. Measured slower (profiles/r05y_tb_fork_ab.txt: N = 1 update 11.9
-    // vs 10.1 ms, emulated W = 8 rank 30.4 vs 25.2 ms): a dW launch's latency is its chunk's rows, not
-    // its problem count, so the in_w problem alone takes as long as the whole dW (21 vs 22 us), and the
-    // forked stream shares a hardware queue with the critic's half (GPU_MAX_HW_QUEUES = 4)
-    static const bool tb_fork_env = [] { const char* e = getenv("DPPO_TB_FORK"); return e && atoi(e) != 0; }();
-    SideStream* tbf = (tb_fork_env && !(hp->flags & DPPO_PPO_TIME_BWD_IN_STEP)) ? side_stream(1) : nullptr;
-    auto actor_grads = [&]() -> int {
-        if (!tbf) return launch_grads(true, s);
-        DPPO_HIP(hipEventRecord(tbf->fork, s));
-        DPPO_HIP(hipStreamWaitEvent(tbf->stream, tbf->fork, 0));
-        int rc_ = launch_grads(true, tbf->stream, 0x1u);
-        if (rc_) return rc_;
-        rc_ = launch_time_bwd(D, precision, ws.gseg, pl2_src, ws.pa0, packed_ft, actor_params, ga, D.KF, D.TS,
-                              tbf->stream, false, false);
-        if (rc_) return rc_;
-        DPPO_HIP(hipEventRecord(tbf->join, tbf->stream));
-        return launch_grads(true, s, 0xEu);
-    };
+    auto actor_grads = [&]() -> int { return launch_grads(true, s); };
     auto actor_tail = [&]() -> int {
-        if (!(hp->flags & DPPO_PPO_TIME_BWD_IN_STEP) && !tbf)
-            return launch_time_bwd(D, precision, ws.gseg, pl2_src, ws.pa0, packed_ft, actor_params, ga, D.KF, D.TS, s,
-                                   !l2_def);
-        // the caller's actor step (dppo_actor_step: actor_tail_kernel) runs the time-MLP backward and forms
-        // W_out's and l2's gradients itself: nothing follows the dW here
-        if (tbf) DPPO_HIP(hipStreamWaitEvent(s, tbf->join, 0));
-        return DPPO_OK;
+        return launch_time_bwd(D, precision, ws.gseg, pl2_src, ws.pa0, packed_ft, actor_params, ga, D.KF, D.TS, s,
+                               !l2_def);
     };
 
     // The critic is independent of the actor: its row tiles and then its weight gradients run on a
@@ -2531,7 +2095,7 @@ extern "C" int dppo_pretrain_minibatch(const dppo_dims* d, int precision, const 
     rc = launch_actor_rowtile(aa, precision, s);
     if (rc) return rc;
 
-    const int tk = dw_tk();
+    const int tk = DW_TK;
     DWArgs w = {};
     auto add = [&](const void* XT, int Kx, const void* DT, int N, float* G, int extra, float* Gx) {
         DWProb& p = w.p[w.nprob];

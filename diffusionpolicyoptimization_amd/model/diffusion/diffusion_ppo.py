@@ -61,12 +61,11 @@ class PPODiffusion(VPGDiffusion):
                           adv_stats=adv_stats, row_index=row_index, part=part)
 
     def bind_minibatch(self, obs, chains, lp_old_mean, advantages, returns, perm_seed, max_rows, reward_horizon=4,
-                       loss_scale=1.0, l2_deferred=False, time_bwd_in_step=False, old_values=None):
+                       loss_scale=1.0, l2_deferred=False, old_values=None):
         """minibatch() over fixed rollout buffers for a whole update phase, its arguments validated
         and marshalled once (ops.BoundMinibatch): returns f(epoch, start, rows, global_rows=None,
         adv_stats=None, part=None, metrics=None). Every minibatch uses the max_rows workspace.
-        l2_deferred: the actor's l2 gradient stays factored for an optimizer step with l2_from_pl2.
-        time_bwd_in_step (ABI 12): the actor's time-MLP backward is left to dppo_actor_step."""
+        l2_deferred: the actor's l2 gradient stays factored for an optimizer step with l2_from_pl2."""
         bound = ops.BoundMinibatch(self.dims, self.precision, self.packed_ft, self.packed_critic, self.actor_ft_params,
                                    self.sched, obs, chains, lp_old_mean, advantages, returns, perm_seed,
                                    self.workspace(max_rows), self.grads, max_rows)
@@ -83,8 +82,6 @@ class PPODiffusion(VPGDiffusion):
                                                          old_values=old_values)
                 if precleared:
                     hp.flags |= _lib.DPPO_PPO_PRECLEARED
-                if time_bwd_in_step:
-                    hp.flags |= _lib.DPPO_PPO_TIME_BWD_IN_STEP
             bound(hp, epoch, start, rows, self.metrics if metrics is None else metrics, adv_stats=adv_stats, part=part,
                   stream=stream)
         return run

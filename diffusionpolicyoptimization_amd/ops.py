@@ -361,8 +361,8 @@ def sampler_max_in_flight(d: ModelDims, precision, n_envs):
 
 def sampler_plan(d: ModelDims, precision, n_envs):
     """The sampler the library runs for n_envs envs (dppo_sampler_plan): dict(kernel, members,
-    sets, workgroups); kernel: 0 weight streaming, 1 split P = 8, 2 folded split (one 16-env tile
-    per member set), 3 pair (two tiles per member pair)."""
+    sets, workgroups); kernel: 0 weight streaming, 2 folded split (one 16-env tile per member
+    set; kernel ids 1 and 3, the r01 P = 8 and r03 pair kernels, were measured slower and removed)."""
     out = (ctypes.c_int * 4)()
     _lib.call("dppo_sampler_plan", ctypes.byref(d.c()), _prec(precision), int(n_envs), out)
     return dict(kernel=out[0], members=out[1], sets=out[2], workgroups=out[3])
@@ -927,49 +927,6 @@ class BoundOptimizerStep:
                                               stream_handle(self._dev) if stream is None else stream)
         if rc != 0:
             raise _lib.DppoError(f"dppo_optimizer_step failed ({rc}): {self._lib.dppo_last_error().decode()}")
-
-
-class BoundActorStep:
-    """dppo_actor_step (ABI 12) over the actor's flat range, marshalled once: the actor's AdamW, its
-    image, the gradient / accumulator clears and (workspace given: the minibatch ran with
-    DPPO_PPO_TIME_BWD_IN_STEP) the time-MLP backward in ONE launch."""
-
-    def __init__(self, d: ModelDims, precision, params, grads, m, v, weight_decay, beta1, beta2, eps, mode,
-                 packed_actor, workspace=None, batch_rows=0, l2_from_pl2=False, clear_grads=True):
-        na, _ = _n_params(d)
-        for t, nm in ((params, "params"), (grads, "grads"), (m, "m"), (v, "v")):
-            if t.numel() != na:
-                raise ValueError(f"{nm}: expected the actor's {na} elements")
-        if workspace is not None and _workspace_bytes(d, _prec(precision), int(batch_rows)) > workspace.numel():
-            raise ValueError("workspace too small for batch_rows")
-        self._lib = _lib.load()
-        self._dims = _dims_c(d)
-        mode_i = ((_lib.DPPO_ADAMW_KERAS if mode == "keras" else _lib.DPPO_ADAMW_TORCH) |
-                  (_lib.DPPO_STEP_L2_FROM_PL2 if l2_from_pl2 else 0) |
-                  (_lib.DPPO_STEP_CLEAR_GRADS if clear_grads else 0))
-        self._head = (ctypes.byref(self._dims), _prec(precision), ptr(params), ptr(grads), ptr(m), ptr(v))
-        self._mid = (float(weight_decay), float(beta1), float(beta2), float(eps), mode_i, ptr(packed_actor),
-                     ptr(workspace))
-        self._rows = int(batch_rows) if workspace is not None else 0
-        self._dev = params.device
-        self._keep = (params, grads, m, v, packed_actor, workspace)
-
-    def __call__(self, step, lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0, stream=None, clear=None,
-                 rows=None):
-        """rows: the minibatch's row count when it differs from batch_rows (a partial minibatch: the
-        workspace layout, and so its bucket sums, depend on it)."""
-        mo = metrics_out if isinstance(metrics_out, int) else (metrics_out.data_ptr() if metrics_out is not None else None)
-        mi = metrics if isinstance(metrics, int) else ptr(metrics)
-        cp, cb, cn = (None, None, 0) if clear is None else clear.args
-        r = self._rows if (rows is None or not self._rows) else int(rows)
-        if self._rows and not 0 < r <= self._rows:
-            raise ValueError(f"rows {r} outside (0, {self._rows}]")
-        rc = self._lib.dppo_actor_step(*self._head, int(step), float(lr), *self._mid, r, mi,
-                                       ctypes.c_void_p(mo) if mo else None, int(n_metrics),
-                                       ctypes.c_uint64(int(metrics_tag)), cp, cb, cn,
-                                       stream_handle(self._dev) if stream is None else stream)
-        if rc != 0:
-            raise _lib.DppoError(f"dppo_actor_step failed ({rc}): {self._lib.dppo_last_error().decode()}")
 
 
 class ClearRanges:

@@ -70,19 +70,6 @@ class AdamW:
             b(self.iterations, lr, metrics, metrics_out, n_metrics, metrics_tag, stream=stream, clear=clear)
         return step
 
-    def bind_actor(self, grads, n_actor, dims, precision, packed_actor, workspace=None, batch_rows=0,
-                   l2_from_pl2=False, clear_grads=True):
-        """The actor's step over params[:n_actor] as ONE launch (ops.BoundActorStep, ABI 12): with a
-        workspace the time-MLP backward of that minibatch (DPPO_PPO_TIME_BWD_IN_STEP) runs in it."""
-        b = ops.BoundActorStep(dims, precision, self.params[:n_actor], grads[:n_actor], self.m[:n_actor],
-                               self.v[:n_actor], self.weight_decay, self.beta_1, self.beta_2, self.epsilon, self.mode,
-                               packed_actor, workspace=workspace, batch_rows=batch_rows, l2_from_pl2=l2_from_pl2,
-                               clear_grads=clear_grads)
-
-        def step(lr, metrics=None, metrics_out=None, n_metrics=0, metrics_tag=0, stream=None, clear=None, rows=None):
-            b(self.iterations, lr, metrics, metrics_out, n_metrics, metrics_tag, stream=stream, clear=clear, rows=rows)
-        return step
-
     def apply_gradients_split(self, grads, ranges):
         """One optimiser step over disjoint ranges of the flat buffer, each on its own stream:
         ranges = [(lo, hi, stream), ...]. Elementwise, so it equals apply_gradients."""

@@ -34,8 +34,11 @@ extern "C" {
 #endif
 
 /* ABI 13: the actor image (dppo_actor_packed_bytes) holds the row tiles' l2 fold segments; a pack or
- * fused step of an actor image is followed by the fold launch (DPPO_STEP_FUSED_PACK above) */
-#define DPPO_ABI_VERSION 14
+ * fused step of an actor image is followed by the fold launch (DPPO_STEP_FUSED_PACK above).
+ * ABI 15: dppo_actor_step and DPPO_PPO_TIME_BWD_IN_STEP (ABI 12) are removed: the one-launch actor
+ * tail was measured slower than the minibatch's time-MLP backward + the fused step;
+ * the actor's one-launch step is dppo_optimizer_step_ex | DPPO_STEP_FUSED_PACK over its range. */
+#define DPPO_ABI_VERSION 15
 
 #if defined(__GNUC__)
 #define DPPO_API __attribute__((visibility("default")))
@@ -337,11 +340,6 @@ enum { DPPO_PPO_LEARN_ETA = 2 };
  * metrics) are already zero — the previous optimizer step of the range cleared them
  * (DPPO_STEP_CLEAR_GRADS) — so the part skips its zeroing launch. */
 enum { DPPO_PPO_PRECLEARED = 4 };
-/* ABI 12, dppo_ppo_hparams.flags. DPPO_PPO_TIME_BWD_IN_STEP: the actor's part (1, 3 or 5) stops after
- * its weight-gradient GEMM (plus l2_back when the l2 gradient is materialised): the time-MLP backward
- * is left to the following dppo_actor_step, which reads this minibatch's bucket sums from the same
- * workspace. The time-MLP and b_in gradients in grads are then NOT formed by the minibatch. */
-enum { DPPO_PPO_TIME_BWD_IN_STEP = 8 };
 
 /* ABI 9: the learnable DDIM eta's optimizer step (the original DPPO's EtaFixed trained by its own
  * AdamW every eta_update_interval minibatches, train_ppo_diffusion_agent.py:28-45, 358-359 — the
@@ -457,20 +455,6 @@ DPPO_API int dppo_optimizer_step_ex(const dppo_dims* d, int precision, float* pa
                            double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
                            const size_t* clear_bytes, int n_clear, void* stream);
 
-/* ABI 12: the actor's whole optimizer step after a PPO minibatch in ONE launch (train_ppo_diffusion_agent.py:
- * 346-356 apply_gradients over actor_ft, plus the weight image every kernel reads): replaces the
- * time-MLP backward, dppo_adamw and the pack (three launches on every minibatch's critical path).
- * params / grads / m / v: the actor's flat range (dppo_actor_param_count elements). mode: DPPO_ADAMW_*,
- * optionally | DPPO_STEP_L2_FROM_PL2 (the l2 gradient in its factored form) | DPPO_STEP_CLEAR_GRADS.
- * workspace / batch_rows: the minibatch's PPO workspace when it ran with DPPO_PPO_TIME_BWD_IN_STEP
- * (the time-MLP backward then runs in this launch from its bucket sums), or NULL / 0 when grads
- * already hold every gradient. metrics / clear ranges as dppo_optimizer_step_ex. The TEMB table and
- * the split sampler's tables are left stale (see DPPO_STEP_FUSED_PACK). */
-DPPO_API int dppo_actor_step(const dppo_dims* d, int precision, float* params, float* grads, float* m, float* v,
-                             int64_t step, float lr, float weight_decay, float beta1, float beta2, float eps, int mode,
-                             void* packed_actor, const void* workspace, int batch_rows, const double* metrics,
-                             double* metrics_out, int n_metrics, uint64_t metrics_tag, void* const* clear_ptrs,
-                             const size_t* clear_bytes, int n_clear, void* stream);
 
 /* ---- ABI 12, §8(e): the data-parallel gradient all-reduce as one kernel over IPC-mapped peer
  * buffers (the reference has no collective: it applies gradients on one device,

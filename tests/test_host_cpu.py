@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol(lib):
     exported = set(re.findall(r"\bT (dppo_\w+)", nm))
     assert set(_declared()) <= exported
     assert exported <= set(_declared()), f"undeclared exports: {exported - set(_declared())}"
-    assert lib.dppo_abi_version() == 14
+    assert lib.dppo_abi_version() == 15
 
 
 def test_env_library_exports_exactly_its_header():

@@ -181,20 +181,6 @@ def test_iterations_match_oracle(cuda, seed, tmp_path):
     assert [e["eval"] for e in errs] == [True, False, False]
 
 
-@pytest.mark.parametrize("fused,l2_defer", [("all", "1"), ("all", "0"), ("critic", "1")])
-def test_iterations_match_oracle_one_launch_actor_step(cuda, tmp_path, monkeypatch, fused, l2_defer):
-    """The opt-in step forms over the same three iterations, against the oracle at the default path's
-    tolerances: the one-launch actor step (DPPO_FUSED_STEP=all: dppo_actor_step with the time-MLP
-    backward in its workgroup 0) with the virtual or the materialised l2 gradient, and the default
-    coalesced actor step with the virtual l2 gradient (DPPO_L2_DEFER=1; materialised is the default)."""
-    monkeypatch.setenv("DPPO_FUSED_STEP", fused)
-    monkeypatch.setenv("DPPO_L2_DEFER", l2_defer)
-    a, orc = _agent_and_oracle(42, tmp_path)
-    errs = _run_and_compare(a, orc)
-    _record(f"step_{fused}_l2defer{l2_defer}", errs)
-    assert [e["eval"] for e in errs] == [True, False, False]
-
-
 @pytest.mark.parametrize("seed", [42, 43, 44])
 def test_iterations_bf16_returns_match_oracle(cuda, seed, tmp_path):
     """The BASELINE config-2 operand policy (bf16 denoiser) over the same three iterations:

@@ -39,28 +39,6 @@ for net in ("actor", "actor_l2v", "critic"):
         torch.cuda.synchronize()
         print(f"{net:10s} {name:12s} {e0.elapsed_time(e1) / reps * 1e3:8.1f} us per step", flush=True)
 
-# ABI 12: the one-launch actor step (dppo_actor_step), without and with the time-MLP backward in its
-# workgroup 0 (a workspace whose bucket sums it reads), at an 8-GPU rank's and one GPU's minibatch
-P, img = m.actor_ft_params, m.packed_ft
-n = P.numel()
-G = torch.randn(n, device="cuda") * 1e-3
-M, V = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
-for name, rows in (("plain", 0), ("tb 6250", 6250), ("tb 50000", 50000)):
-    ws = None
-    if rows:
-        ws = torch.zeros(ops._workspace_bytes(d, ops._prec(m.precision), rows), dtype=torch.uint8, device="cuda")
-    step = ops.BoundActorStep(d, m.precision, P, G, M, V, 0.004, 0.9, 0.999, 1e-7, "keras", img, workspace=ws,
-                              batch_rows=rows)
-    for it in range(5):
-        step(it + 1, 1e-6)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 50
-    e0.record()
-    for it in range(reps):
-        step(it + 6, 1e-6)
-    e1.record()
-    torch.cuda.synchronize()
-    print(f"actor_step {name:12s} {e0.elapsed_time(e1) / reps * 1e3:8.1f} us per step", flush=True)
+img = m.packed_ft
 ops.refresh_sampler_tables(img)
 torch.cuda.synchronize()
