@@ -704,8 +704,6 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 info, _ = finish(pending)
             if split:
                 stream.wait_stream(side)
-        if hp is not None:
-            caller.wait_stream(hp)
         stream = caller
         # explained variance (:373-377) from the moments value_moments stored before the epochs
         stream.synchronize()
