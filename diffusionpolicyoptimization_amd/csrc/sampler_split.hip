@@ -463,6 +463,25 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
         for (int idx = tid; idx < NV; idx += ST) a0[(idx / XD) * lda0 + idx % XD] = Pol::cvt(xs[idx]);
         __syncthreads();
     }
+    // fp32 at KX = 2 (hopper: XD + SD = 23 > 16): the in-Dense's second k-step reads state columns only
+    // (XD <= KG), so its product is launch-constant per actor — formed once here (and again after a
+    // non-dual actor switch) and added to the TIN row: 4 of the step's 16x16x4 MFMAs per in-Dense tile
+    // and one LDS operand round trip fewer. (The 2-byte walker2d / halfcheetah form keeps its second
+    // k-step: 16 more VGPRs spill it.)
+    constexpr bool SBP = KX == 2 && !TWO;
+    static_assert(!SBP || XD <= KGP, "x within the in-Dense's first k-step");
+    f32x4 sb[SBP ? NTI : 1];
+    auto state_part = [&]() {
+        if constexpr (SBP) {
+            const u32x4 af1 = lds_afrag<Pol>(a0, lda0, 0, 1, lane);
+#pragma unroll
+            for (int n = 0; n < NTI; ++n) {
+                zero_acc(sb[n]);
+                sb[n] = Pol::mma(wxs[((wave * NTI + n) * KX + 1) * 64 + lane], af1, sb[n]);
+            }
+        }
+    };
+    state_part();
     const int env = lane & 15, jq = lane >> 4;
     const int xmode = __builtin_amdgcn_readfirstlane(xfail[1]);
     uint64_t* const xregion = sa.xbuf + (size_t)xmode * XREGION;
@@ -479,8 +498,9 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
         const int PKn = __builtin_amdgcn_readfirstlane(t >= 1 && t - 1 < KF ? 1 : 0);
         const bool pre = !sa.dual && t >= 1 && PKn != PK;   // this step is the last of its actor
         if (PK != cur) {
-            __builtin_amdgcn_s_waitcnt(0x0F70);
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // the other actor's fragments (load_in / load_l1 / load_fold)
             cur = PK;
+            state_part();
         }
         XPHASE(1);
         const float* bb = bias + PK * NB;
@@ -491,14 +511,15 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
         // ---- in-Dense (transposed): h1 = TIN[t] + W_xs^T [x; state]; no activation (mlp.py:144)
         f32x4 h1[NTI];
         {
-            u32x4 af[KX], wf[KX][NTI];
+            constexpr int KXS = SBP ? 1 : KX;   // k-steps run per step
+            u32x4 af[KXS], wf[KXS][NTI];
 #pragma unroll
-            for (int ks = 0; ks < KX; ++ks) af[ks] = lds_afrag<Pol>(a0, lda0, 0, ks, lane);
+            for (int ks = 0; ks < KXS; ++ks) af[ks] = lds_afrag<Pol>(a0, lda0, 0, ks, lane);
 #pragma unroll
             for (int n = 0; n < NTI; ++n) h1[n] = *(const f32x4*)(tin + (TRING ? (i & 1) : t) * H + 16 * (NTI * wave + n) + 4 * jq);
 #pragma unroll
             for (int n = 0; n < NTI; ++n) wf[0][n] = wxs[((wave * NTI + n) * KX + 0) * 64 + lane];
-            // one LDS round trip for all of them (KX = 2: the second k-step's operands in a second
+            // one LDS round trip for all of them (2-byte KX = 2: the second k-step's operands in a second
             // round trip after the first k-step's MFMAs, which keeps the walker2d form within 256 VGPRs
             // — all at once it spilled the epilogue's output addresses to scratch)
 #if DPPO_S4_INREADY
@@ -511,9 +532,12 @@ __global__ __launch_bounds__(SWV * 64) void sample_split4_kernel(SplitArgs sa) {
 #if DPPO_S4_EPIEARLY
             asm volatile("" ::"v"(ec), "v"(esd), "v"(xe), "v"(ze), "v"(be));
 #endif
+            if constexpr (SBP)
+#pragma unroll
+                for (int n = 0; n < NTI; ++n) h1[n] += sb[n];
 #pragma unroll
             for (int n = 0; n < NTI; ++n) h1[n] = Pol::mma(wf[0][n], af[0], h1[n]);
-            if constexpr (KX == 2) {
+            if constexpr (KXS == 2) {
 #pragma unroll
                 for (int n = 0; n < NTI; ++n) wf[1][n] = wxs[((wave * NTI + n) * KX + 1) * 64 + lane];
 #if DPPO_S4_INREADY
