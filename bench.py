@@ -43,11 +43,12 @@ CU_LOAD_PEAK_GBS = 64 * 2.4   # per-CU vector-memory (TA) path: 64 B/clk at the 
 # v_mfma_f32_16x16x32_bf16 x 16 cycles at 2.4 GHz; n per wave = in-Dense 4 + residual 4/P + l1
 # 64/P + fold 4/P: P = 2: 4 + 2 + 32 + 2 = 40, P = 4: 4 + 1 + 16 + 1 = 22; r01 8-member kernel 28).
 # Everything else in a step (LDS round trips, barriers, VALU epilogues, the DDPM update) is latency
-# this floor does not count. fp32 (v_mfma_f32_16x16x4_f32: 4 issues of 32 cycles per 16-wide k-step,
-# in-Dense K = XD + SD in 2 k-steps): P = 8 members of 4 waves, one wave per SIMD issuing in-Dense
-# 8 tiles x 2 k x 4 + residual 4 + l1 32 k x 4 + fold 4 = 200; P = 4 of 8 waves, 2 per SIMD x (32 + 4 + 128 + 4).
+# this floor does not count. fp32 (v_mfma_f32_16x16x4_f32: 4 issues of 32 cycles per 16-wide k-step;
+# the in-Dense's state k-step is formed once per launch, so one k-step per step): P = 8 members of 4
+# waves, one wave per SIMD issuing in-Dense 8 tiles x 4 + residual 4 + l1 32 k x 4 + fold 4 = 168;
+# P = 4 of 8 waves, 2 per SIMD x (16 + 4 + 128 + 4).
 SPLIT_DEFAULT_P = 2
-SPLIT_MFMA_US_F32 = {8: 200 * 32 / 2.4e3, 4: 2 * 168 * 32 / 2.4e3}
+SPLIT_MFMA_US_F32 = {8: 168 * 32 / 2.4e3, 4: 2 * 152 * 32 / 2.4e3}
 SPLIT_XCHG_US = {2: 0.59, 4: 0.98, 8: 1.55}
 SPLIT_MFMA_US = {2: 2 * 40 * 16 / 2.4e3, 4: 2 * 22 * 16 / 2.4e3, 8: 2 * 28 * 16 / 2.4e3}
 
