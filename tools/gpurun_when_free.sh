@@ -6,7 +6,7 @@ out=$1; lim=$2; cmd=$3
 for attempt in 1 2 3 4 5 6 7 8; do
   /usr/local/graft/bin/gpurun --timeout "$lim" -- "$cmd" > "$out" 2>&1
   rc=$?
-  if grep -q "no free box right now\|stopped responding while being prepared" "$out" && grep -q "run 0.0s of limit" "$out"; then
+  if grep -q "no free box right now\|stopped responding while being prepared\|are busy" "$out" && grep -q "run 0.0s of limit" "$out"; then
     echo "attempt $attempt: no box; waiting" >> "$out.retries"
     sleep 180
     continue
