@@ -467,6 +467,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                 self._ev_m = [torch.cuda.Event() for _ in range(2)]
                 self._mb_tag = 0
             pending = None
+            last_mb = None   # (epoch key, start, rows) of the last minibatch run (the bc_loss report)
             eta_now = m.current_eta()   # c_loss's eta metric (diffusion_ppo.py:131), as of the update's start
 
             def finish(p):
@@ -593,6 +594,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         ev0 = torch.cuda.Event(enable_timing=True)
                         ev0.record(stream)
                     mb_args = (update_epoch + 1000 * self.itr, start, rows)
+                    prev_mb, last_mb = last_mb, mb_args
                     pre = cleared and rows == rows_local_full
                     mb_kw = dict(global_rows=global_rows, adv_stats=stats)
                     met = m.metrics
@@ -647,6 +649,7 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
                         pending = None
                         if stop and same_epoch:                                    # :366-368
                             cleared = False   # this minibatch's sums stay; no step clears them
+                            last_mb = prev_mb   # the reference never computes this one
                             break
                     # the optimiser step (agent :346): AdamW, the metric sums to the host and the weight
                     # images re-derived, one dppo_optimizer_step per stream (two launches each). The actor
@@ -709,10 +712,30 @@ class TrainPPODiffusionAgent(TrainPPOAgent):
         stream.synchronize()
         for g in (getattr(self, "_ipc_groups", None) or {}).values():
             g.check()   # a barrier timeout in any bucket all-reduce of this update
+        if self.use_bc_loss and last_mb is not None:
+            info["bc_loss"] = self._bc_loss_report(last_mb, obs_flat, total_local, kf)
         info["explained_var"] = explained_variance_from_moments(
             self._ev_map.array.copy(), self.device, group=dist.group.WORLD if self.world_size > 1 else None)
         info["clipfrac"] = float(np.mean(clipfracs)) if clipfracs else 0.0
         return info
+
+    def _bc_loss_report(self, mb, obs_flat, total_local, kf):
+        """c_loss's bc_loss (diffusion_ppo.py:63-71) of the update's last minibatch, the value the reference
+        logs (train_ppo_diffusion_agent.py:441, 450): base-policy chains for that minibatch's observations
+        and their clipped actor_ft log-probs (PPODiffusion.bc_loss). The reference evaluates it on every
+        minibatch, but it is not in the loss (:340-342) and only the last value is observable, so only that
+        one is computed. Under data parallelism the mean is over the union of the ranks' rows."""
+        epoch_key, start, rows = mb
+        idx = ops.feistel_permute(start, rows, total_local, self.perm_seed, epoch_key, self.device)
+        idx = idx[idx >= 0]
+        m = self.model
+        n_el = float(idx.numel() * kf * m.dims.xd)
+        s = -m.bc_loss(obs_flat[idx // kf]) * n_el if idx.numel() else 0.0   # sum of the clipped log-probs
+        if self.world_size > 1:
+            t = torch.tensor([s, n_el], dtype=torch.float64, device=self.device)
+            self._allreduce(t)
+            s, n_el = float(t[0]), float(t[1])
+        return -s / max(n_el, 1.0)
 
     def _clip_by_norm_per_tensor(self):
         """Else-branch of agent :349-353: tf.clip_by_norm(grad, 1.0) per variable."""

@@ -86,12 +86,31 @@ class PPODiffusion(VPGDiffusion):
                   stream=stream)
         return run
 
+    def bc_loss(self, obs, *, x_T=None, noise=None):
+        """The behaviour-cloning term of c_loss (diffusion_ppo.py:63-71): chains of the frozen base policy
+        for these observations (every denoising step on the base actor, use_base_policy=True), their
+        log-probs under actor_ft (:343-425) clipped to [-5, 2], negated mean over every element. The agent
+        reports it but leaves it out of the loss (train_ppo_diffusion_agent.py:340-342), so it has no
+        gradient here. Its Philox draws use a call counter of their own (high call ids), so the rollout's
+        noise does not depend on use_bc_loss; x_T / noise inject the draws (tests)."""
+        state = _as_state(obs, self.device, self.dims.sd)
+        n = state.shape[0]
+        calls = getattr(self, "_bc_calls", 0)
+        _, ch = ops.sample(self.dims, self.precision, self.packed_base, self.packed_base, self.sched_for(False), state,
+                           x_T=x_T, noise=noise, seed=self.seed, call_id=(1 << 40) + calls,
+                           env_offset=self._env_offset, deterministic=False,
+                           min_sampling_std=self.get_min_sampling_denoising_std(), randn_clip=self.randn_clip_value,
+                           final_clip=self.final_action_clip_value, want_chains=True)
+        self._bc_calls = calls + 1
+        lp = self.get_logprobs(state, ch.view(n, self.ft_denoising_steps + 1, self.dims.xd))
+        return -float(lp.clamp(-5, 2).mean())
+
     def c_loss(self, obs, chains_prev, chains_next, denoising_inds, returns, oldvalues, advantages, oldlogprobs,
                use_bc_loss=False, reward_horizon=4):
         """diffusion_ppo.py:32-132 on an explicit batch. Returns (pg_loss, entropy_loss, v_loss, clipfrac,
-        approx_kl, ratio, bc_loss, eta) as floats; gradients are left in self.grads."""
-        if use_bc_loss:
-            raise NotImplementedError("use_bc_loss (False in every cfg) is not implemented")
+        approx_kl, ratio, bc_loss, eta) as floats; gradients are left in self.grads (of pg_loss +
+        vf_coef v_loss: the agent's loss, train_ppo_diffusion_agent.py:340-342; bc_loss is reported only)."""
+        bc = self.bc_loss(obs) if use_bc_loss else 0.0   # :63-71
         dev = self.device
         state = _as_state(obs, dev, self.dims.sd)
         b = state.shape[0]
@@ -119,4 +138,4 @@ class PPODiffusion(VPGDiffusion):
         # entropy_loss = -mean(eta), the last element mean(eta) (diffusion_ppo.py:49, 131); with
         # learn_eta, d loss / d eta is left in self.metrics[M_DETA]
         return (float(m[M_PG]), -eta, float(m[M_VLOSS]), float(m[M_CLIPFRAC]), float(m[M_KL]), float(m[M_RATIO]),
-                0.0, eta)
+                bc, eta)

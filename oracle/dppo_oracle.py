@@ -376,6 +376,17 @@ def sample(p_base, p_ft, sched, state, x_T, z, ft_steps, deterministic=False, mi
     return x, np.stack(chain, axis=1)
 
 
+def bc_loss(p_base, p_ft, sched, state, x_T, z, ft_steps, min_std=0.1, randn_clip=3.0, min_logprob_std=0.1,
+            rnd=None):
+    """c_loss's behaviour-cloning term (diffusion_ppo.py:63-71): chains of the base policy for every
+    denoising step (use_base_policy=True, diffusion_vpg.py:175-176), their log-probs under actor_ft,
+    clipped to [-5, 2]; -mean over every element. Reported only (agent :340-342)."""
+    _, chains = sample(p_base, p_base, sched, state, x_T, z, ft_steps, min_std=min_std, randn_clip=randn_clip,
+                       rnd=rnd, round_h3=False)
+    lp = get_logprobs(p_ft, sched, state, chains, ft_steps, min_logprob_std=min_logprob_std, rnd=rnd)
+    return -float(np.clip(lp, -5.0, 2.0).mean())
+
+
 def gaussian_logprob(x, mu, std):
     """tfp Normal(mu, std).log_prob(x) (diffusion_vpg.py:419-422)."""
     return -0.5 * ((x - mu) / std) ** 2 - np.log(std) - LOG_2PI_HALF

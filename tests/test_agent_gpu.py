@@ -575,3 +575,46 @@ def test_learn_eta_agent_iterations(cuda, tmp_path):
         assert m2.current_eta() == m.current_eta()
         np.testing.assert_array_equal(m2.sched.cpu().numpy(), m.sched.cpu().numpy())
         assert torch.equal(m2.train_params, m.train_params)
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-5), ("bf16", 2e-3)])
+def test_bc_loss_matches_oracle(cuda, precision, tol, tmp_path):
+    """c_loss's behaviour-cloning term (diffusion_ppo.py:63-71; use_bc_loss, off in every cfg): base-policy
+    chains for the batch's observations (every step on the base actor), their clipped actor_ft log-probs,
+    negated mean — PPODiffusion.bc_loss with injected draws against the oracle's composition of its
+    sampler and log-probs (bf16: the oracle rounding operands at the kernels' points). Then the agent's
+    report: use_bc_loss=True puts a finite value in the update's info; the term's Philox draws leave the
+    model's call counter (the rollout's stream) where it was."""
+    import torch
+    from diffusionpolicyoptimization_amd import ops
+    from diffusionpolicyoptimization_amd.util.config import get_class, instantiate, load_config
+    from helpers import to_f64
+    from oracle import dppo_oracle as O
+    cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
+                      [f"model.precision={precision}"])
+    m = instantiate(cfg.model, device=cuda, seed=3)
+    d = m.dims
+    E, K, kf = 37, d.denoising_steps, m.ft_denoising_steps
+    rng = np.random.default_rng(8)
+    state = rng.uniform(-1, 1, (E, d.cond_steps, d.obs_dim)).astype(np.float32)
+    xT = rng.standard_normal((E, d.horizon_steps, d.action_dim)).astype(np.float32)
+    z = rng.standard_normal((K, E, d.horizon_steps, d.action_dim)).astype(np.float32)
+    calls = m._call_id
+    bc = m.bc_loss(torch.tensor(state.reshape(E, -1), device=cuda), x_T=torch.tensor(xT.reshape(E, -1), device=cuda),
+                   noise=torch.tensor(z.reshape(K, E, -1), device=cuda))
+    assert m._call_id == calls
+    na = m.n_actor
+    base = ops.unflatten_params(m.actor_spec, m.base_params.cpu().numpy())
+    ft = ops.unflatten_params(m.actor_spec, m.train_params.cpu().numpy()[:na])
+    rnd = {"fp32": None, "bf16": O.round_bf16}[precision]
+    ref = O.bc_loss(to_f64(base), to_f64(ft), O.ddpm_schedule(K), state.astype(np.float64), xT.astype(np.float64),
+                    z.astype(np.float64), kf, min_std=m.get_min_sampling_denoising_std(), randn_clip=m.randn_clip_value,
+                    min_logprob_std=m.min_logprob_denoising_std, rnd=rnd)
+    assert abs(bc - ref) <= tol * max(1.0, abs(ref)), (bc, ref)
+    if precision == "fp32":
+        cfg = load_config(os.path.join(ROOT, "cfg/gym/finetune/hopper-v2"), "ft_ppo_diffusion_mlp",
+                          ["train.n_steps=8", "train.batch_size=160", "+train.use_bc_loss=true", f"logdir={tmp_path}",
+                           "train.save_checkpoints=false"])
+        agent = get_class(cfg._target_)(cfg)
+        info = agent.iteration(force_train=True)
+        assert math.isfinite(info["bc_loss"]) and info["bc_loss"] != 0.0, info["bc_loss"]
