@@ -328,3 +328,21 @@ def test_oracle_eta_gradient_matches_finite_differences():
     # the EtaFixed parametrisation round-trips
     lg = O.eta_logit_init(0.5, 0.1, 1.0)
     assert abs(O.eta_from_logit(lg, 0.1, 1.0) - 0.5) < 1e-12
+
+
+def test_bc_loss_samples_every_step_with_the_base_policy():
+    """c_loss's behaviour-cloning term (diffusion_ppo.py:63-71): `call(..., use_base_policy=True)` runs
+    every denoising step, the fine-tuned steps included, on the frozen base actor (diffusion_vpg.py:175-176),
+    and the log-probs of those chains are taken under actor_ft (use_base_policy=False), clipped to [-5, 2]."""
+    base, ft, _ = make_models(seed=4)
+    base, ft = to_f64(base), to_f64(ft)
+    K, kf, E = 20, 10, 6
+    rng = np.random.default_rng(2)
+    st = rng.uniform(-1, 1, (E, 1, 11))
+    xT, z = rng.standard_normal((E, 4, 3)), rng.standard_normal((K, E, 4, 3))
+    sched = O.ddpm_schedule(K)
+    v = O.bc_loss(base, ft, sched, st, xT, z, kf)
+    _, ch = O.sample(base, base, sched, st, xT, z, kf, round_h3=False)
+    assert v == -np.clip(O.get_logprobs(ft, sched, st, ch, kf), -5, 2).mean()
+    _, ch_mix = O.sample(base, ft, sched, st, xT, z, kf, round_h3=False)   # the rollout's actor mix
+    assert not np.allclose(ch, ch_mix)
