@@ -116,7 +116,7 @@ def cpu_baseline(cfg, n_envs, S, bs):
 # run: the library's kernel timer (dppo_kernel_timing, HIP events around each launch on its own
 # stream) over one instrumented iteration. The committed rocprofv3 whole-iteration trace of the
 # same workload is reported beside them as a cross-check.
-KERNEL_STATS_CSV = os.path.join(ROOT, "profiles", "r05end_iteration_kernel_stats.csv")
+KERNEL_STATS_CSV = os.path.join(ROOT, "profiles", "r06end_iteration_kernel_stats.csv")
 
 
 def kernel_times_live(agent):
