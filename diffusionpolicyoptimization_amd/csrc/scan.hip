@@ -387,41 +387,82 @@ extern "C" int dppo_reward_scale(double* reward, const uint8_t* first, double* r
 // a16 episode accounting (train_ppo_diffusion_agent.py:144-167): the episodes that start AND end
 // inside the rollout — consecutive episode starts s < en of one env with en - s > 1 — and per env
 // {count, sum of returns (sum of rew[s:en]), sum of best rewards (max of rew[s:en] / act_steps),
-// count with best >= threshold}. One thread per env walks t = 0..S in order (the reference's
-// env-major visit; per-episode sums in time order), on the RAW rewards (before the reward scaler).
+// count with best >= threshold}. One lane per env walks t = 0..S in order (the reference's env-major
+// visit; per-episode sums in time order), on the RAW rewards (before the reward scaler).
 // The caller sums the E rows in env order. (ABI 14: the host loop took ~0.4 ms at 64 envs and
 // ~13 ms at 512 inside the update loop, where the host is at most one minibatch ahead of the GPU.)
 // ---------------------------------------------------------------------------------------------
+// A workgroup owns 64 envs (one walking lane each, wave 0) and streams the [t][env] slab through LDS in
+// chunks of EP_CH steps: waves 1-3 load a chunk with coalesced rows (rewards 512 B, flags 64 B per step)
+// while wave 0 walks the previous one, so the walk never waits on a global load (one thread per
+// env reading its own column paid a load latency per step or per few steps: 208 / 155 us at S = 500,
+// against 53.5 us here; tools/r06_ep.sh).
+constexpr int EP_ENVS = 64, EP_CH = 32;
 __global__ __launch_bounds__(256) void episode_sums_kernel(const double* __restrict__ rew, const uint8_t* __restrict__ first,
                                                            int S, int E, double act_steps, double thr,
                                                            double* __restrict__ out) {
-    const int e = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (e >= E) return;
+    __shared__ double srew[2][EP_CH][EP_ENVS];
+    __shared__ uint8_t sfl[2][EP_CH][EP_ENVS];
+    const int tid = (int)threadIdx.x, e0 = (int)blockIdx.x * EP_ENVS, e = e0 + tid;
+    const int nch = (S + 1 + EP_CH - 1) / EP_CH;   // chunks over t = 0..S (flags have S + 1 rows)
+    auto load = [&](int c, int buf) {   // waves 1-3 (wave 0 walks, never waiting on a load of its own)
+        constexpr int LT = 256 - EP_ENVS, NL = (EP_CH * EP_ENVS + LT - 1) / LT;
+        double rv[NL];
+        uint8_t fv[NL];
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {   // every load of the chunk issued before the first LDS store
+            const int i = tid - EP_ENVS + LT * k, tt = i / EP_ENVS, ee = i % EP_ENVS, t = c * EP_CH + tt, eg = e0 + ee;
+            const bool ok = tid >= EP_ENVS && i < EP_CH * EP_ENVS && eg < E;
+            rv[k] = ok && t < S ? rew[(size_t)t * E + eg] : 0.0;
+            fv[k] = ok && t <= S ? first[(size_t)t * E + eg] : (uint8_t)0;
+        }
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            const int i = tid - EP_ENVS + LT * k;
+            if (tid >= EP_ENVS && i < EP_CH * EP_ENVS) {
+                srew[buf][i / EP_ENVS][i % EP_ENVS] = rv[k];
+                sfl[buf][i / EP_ENVS][i % EP_ENVS] = fv[k];
+            }
+        }
+    };
     int start = -1;
     double run = 0.0, mx = 0.0, n = 0.0, tot = 0.0, best = 0.0, succ = 0.0;
-    for (int t = 0; t <= S; ++t) {
-        if (first[(size_t)t * E + e]) {
-            if (start >= 0 && t - start > 1) {
-                const double b = mx / act_steps;
-                n += 1.0;
-                tot += run;
-                best += b;
-                succ += b >= thr ? 1.0 : 0.0;
+    load(0, 0);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        if (c + 1 < nch) load(c + 1, (c + 1) & 1);   // the next chunk in flight during this walk
+        if (tid < EP_ENVS) {
+            const int buf = c & 1;
+#pragma unroll 8
+            for (int tt = 0; tt < EP_CH; ++tt) {
+                const int t = c * EP_CH + tt;
+                if (t <= S && sfl[buf][tt][tid]) {
+                    if (start >= 0 && t - start > 1) {
+                        const double b = mx / act_steps;
+                        n += 1.0;
+                        tot += run;
+                        best += b;
+                        succ += b >= thr ? 1.0 : 0.0;
+                    }
+                    start = t;
+                    run = 0.0;
+                    mx = -__builtin_huge_val();
+                }
+                if (t < S) {
+                    const double r = srew[buf][tt][tid];
+                    run += r;
+                    mx = fmax(mx, r);
+                }
             }
-            start = t;
-            run = 0.0;
-            mx = -__builtin_huge_val();
         }
-        if (t < S) {
-            const double r = rew[(size_t)t * E + e];
-            run += r;
-            mx = fmax(mx, r);
-        }
+        __syncthreads();   // this chunk's buffer is rewritten two chunks on
     }
-    out[4 * (size_t)e + 0] = n;
-    out[4 * (size_t)e + 1] = tot;
-    out[4 * (size_t)e + 2] = best;
-    out[4 * (size_t)e + 3] = succ;
+    if (tid < EP_ENVS && e < E) {
+        out[4 * (size_t)e + 0] = n;
+        out[4 * (size_t)e + 1] = tot;
+        out[4 * (size_t)e + 2] = best;
+        out[4 * (size_t)e + 3] = succ;
+    }
 }
 
 extern "C" int dppo_episode_sums(const double* reward, const uint8_t* first, int S, int E, int act_steps,
@@ -429,7 +470,7 @@ extern "C" int dppo_episode_sums(const double* reward, const uint8_t* first, int
     DPPO_CHECK(S >= 0 && E >= 0 && act_steps > 0, "dppo_episode_sums: bad sizes");
     if (E == 0) return DPPO_OK;
     DPPO_CHECK(reward && first && out, "dppo_episode_sums: null pointer");
-    hipLaunchKernelGGL(episode_sums_kernel, dim3(dppo_cdiv(E, 256)), dim3(256), 0, (hipStream_t)stream, reward, first,
+    hipLaunchKernelGGL(episode_sums_kernel, dim3(dppo_cdiv(E, EP_ENVS)), dim3(256), 0, (hipStream_t)stream, reward, first,
                        S, E, (double)act_steps, success_threshold, out);
     DPPO_HIP(hipGetLastError());
     return DPPO_OK;
