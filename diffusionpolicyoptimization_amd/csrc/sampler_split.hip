@@ -141,7 +141,9 @@ __device__ inline int xcc_id() {
 
 // tuning knobs of the split kernel (tools/variant_build.sh <tag> "-D..." + tools/ab_variants.sh)
 #ifndef DPPO_S4_L1D
-#define DPPO_S4_L1D 4        // l1: u1 fragment reads kept in flight ahead of the MFMA chain
+#define DPPO_S4_L1D 1        // l1: u1 fragment reads kept in flight ahead of the MFMA chain (r06, same box,
+                             // 300 launches x 2: 1 46.8 / 4 47.8 / 2 47.1-47.5 / 3 47.7-47.9 / 6 47.5 / 0
+                             // 58.0 us at hopper bf16; fp32 neutral; profiles/r06l_sampler_l1d_ab.txt)
 #endif
 #ifndef DPPO_S4_INREADY
 #define DPPO_S4_INREADY 1    // in-Dense: all LDS operands in one round trip
