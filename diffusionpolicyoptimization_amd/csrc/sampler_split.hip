@@ -146,7 +146,9 @@ __device__ inline int xcc_id() {
                              // 58.0 us at hopper bf16; fp32 neutral; profiles/r06l_sampler_l1d_ab.txt)
 #endif
 #ifndef DPPO_S4_INREADY
-#define DPPO_S4_INREADY 1    // in-Dense: all LDS operands in one round trip
+#define DPPO_S4_INREADY 0    // 1: the in-Dense's LDS operands forced into one round trip (the r02-r05 form); r06 with
+                             // l1 read-ahead 1: left to the compiler measured 46.0-46.3 vs 46.8-47.0 us at hopper
+                             // bf16, -1.4 % at DDIM 512 fp16, -0.5 % walker2d 256, fp32 neutral (r06m A/B)
 #endif
 #ifndef DPPO_S4_PUBREADY
 #define DPPO_S4_PUBREADY 1   // publish: the 8 wave partials in one round trip
