@@ -765,7 +765,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4)))
 }
 
 // Row-tile shapes: actor 64 rows on 16 waves (2-byte operands, H = 512, XD <= 16, at least one
-// round of tiles), else 32 rows on 8 waves; critic 32 rows on 8 waves at occupancy 4 (the _o4
+// round of tiles), else 32 rows on 8 waves (fp32: 16); critic 32 rows on 8 waves at occupancy 4 (the _o4
 // kernel). r02 measured the alternatives (actor 32x8 at occupancy 4, 64x8; critic at occupancy 2)
 // slower or equal; r03 removed them with the binary's size in mind.
 struct RowTileCfg { int actor; int critic; };
@@ -805,7 +805,7 @@ static int launch_actor_m(const ActorArgs& a, hipStream_t s) {
 }
 
 // bf16: 64-row tiles, 16 waves (half the weight stream per row of 32-row tiles; LDS-limited);
-// fp32: 32-row tiles, 8 waves
+// fp32: 32-row tiles, 16 waves
 template <class P, int MT, int WAVES, bool O4 = false>
 static int dispatch_actor(const ActorArgs& a, hipStream_t s) {
     const int NT = a.H / (16 * WAVES), NO = dppo_cdiv(a.XD, 16), KSI = a.L.ks_in;
@@ -862,7 +862,9 @@ static int launch_actor_2b(const ActorArgs& a, hipStream_t s) {
 int launch_actor_rowtile(const ActorArgs& a, int precision, hipStream_t s) {
     if (precision == DPPO_BF16) return launch_actor_2b<PolicyBF16>(a, s);
     if (precision == DPPO_F16) return launch_actor_2b<PolicyF16>(a, s);
-    return dispatch_actor<PolicyF32, 2, 8>(a, s);
+    // fp32: 32-row tiles on 16 waves (four per SIMD behind the 16x16x4 MFMA chains): update 41.5 ->
+    // 40.5 ms per iteration against 8 waves (profiles/r06zz_f32_tile_16wave_ab.txt)
+    return dispatch_actor<PolicyF32, 2, 16>(a, s);
 }
 
 template <class P, int MT, int NT, bool TRAIN, int WAVES, bool O4>
